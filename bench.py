@@ -1,0 +1,210 @@
+"""Benchmark: images/sec of DDIM-50 sampling with the CIFAR-10 UNet on MI355X.
+
+BASELINE.json metric "images/sec at DDIM-50, CIFAR-10 UNet 32x32, bs=256;
+1/2/4/8 GPU". One bench *step* = one sampling fold of the reference harness
+(scripts/sample_uncond.py:184-190): B=256 init-noise images per GPU pushed
+through the 50 DDIM steps (model forward + fused update on each), clamped,
+and all-gathered over RCCL when N > 1. Weights are the deterministic
+synthetic CIFAR-10 UNet (35.7M params, rank-independent); noise is drawn on
+device from a per-rank seed (2022 + rank, as the reference seeds).
+
+Timing: W untimed warmup folds, then K folds bracketed by barrier +
+torch.cuda.synchronize(); the MAX over ranks is reported; `value` = images of
+all ranks / that time.
+
+Roofline: HIP events around every launch of the forward during the timed
+region (dm_unet_profile) give each kernel family's average launch duration;
+the dominant family (most GPU time) is reported against the fp32 MFMA peak
+with its algorithmic FLOPs per launch.
+
+CPU baseline: the oracle (a torch-CPU restatement of the reference path,
+bit-equal to it at equal thread count) timed on this host's cores, rank 0 /
+N=1 only, on one denoising step of the same B=256 fold, extrapolated x50.
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, 'diffusion-models-pytorch_amd')
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = 'images/sec at DDIM-50, CIFAR-10 UNet 32×32, bs=256; 1/2/4/8 GPU'
+FP32_PEAK_TFLOPS = 157.3   # MI355X dense fp32 (MFMA f32 = vector rate), MI355X_MICROARCH.md
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=3, help='timed folds')
+    ap.add_argument('--warmup', type=int, default=1, help='untimed folds')
+    ap.add_argument('--batch', type=int, default=256, help='images per GPU per fold')
+    ap.add_argument('--respace-steps', type=int, default=50)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-batch', type=int, default=256, help='batch of the timed CPU denoising step')
+    ap.add_argument('--profile-json', default=None, help='write the per-op profile here (rank 0)')
+    return ap.parse_args()
+
+
+def cpu_model_name():
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.startswith('model name'):
+                    return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or 'unknown'
+
+
+def cpu_baseline(sd, batch, n_steps):
+    """Oracle (reference op sequence on torch CPU): one DDIM step at `batch`, extrapolated."""
+    from oracle.unet import OracleUNet
+    from oracle import diffusion as od
+    model = OracleUNet(sd, dim=128)
+    ac = od.alphas_cumprod(od.beta_schedule(1000, 'linear'))
+    g = torch.Generator().manual_seed(2022)
+    x_small = torch.randn((8, 3, 32, 32), generator=g)
+    with torch.no_grad():
+        od.ddim_denoise(ac, model(x_small, torch.full((8, ), 980)), x_small, 980, 960)  # warm-up
+        x = torch.randn((batch, 3, 32, 32), generator=g)
+        t0 = time.perf_counter()
+        out = model(x, torch.full((batch, ), 980))
+        od.ddim_denoise(ac, out, x, 980, 960)
+        dt = time.perf_counter() - t0
+    return dict(value=batch / (dt * n_steps), unit='images/sec', cores=torch.get_num_threads(), kind='port',
+                sample=f'1 of {n_steps} DDIM steps (UNet forward + update) at B={batch} on torch CPU '
+                       f'({cpu_model_name()}), extrapolated x{n_steps}; {dt:.2f} s measured')
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
+    dev = torch.device('cuda', local_rank)
+
+    import dmhip
+    from diffusions import DDIM
+    from models.unet import UNet
+    from utils.synthetic import init_synthetic_
+
+    dmhip.load()
+    model = UNet().eval()
+    init_synthetic_(model)
+    sd_cpu = {k: v.clone() for k, v in model.state_dict().items()}
+    model = model.to(dev)
+    diffuser = DDIM(respace_type='uniform', respace_steps=args.respace_steps, eta=0.0, device=dev)
+    B = args.batch
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(2022 + rank)
+    gathered = torch.empty((world * B, 3, 32, 32), device=dev) if world > 1 else None
+
+    def fold():
+        noise = torch.randn((B, 3, 32, 32), device=dev, generator=gen)
+        x = diffuser.sample(model, noise, tqdm_kwargs=dict(disable=True)).clamp(-1, 1)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, x)
+            return gathered
+        return x
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        fold()
+    if args.warmup == 0:  # build the B-sized plan outside the timed region
+        model(torch.zeros((B, 3, 32, 32), device=dev), torch.zeros((B, ), dtype=torch.long, device=dev))
+    handle = model.native_handle(dev)
+    dmhip.unet_profile_enable(handle, True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = fold()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = tt.item()
+    prof = dmhip.unet_profile_read(handle)
+    dmhip.unet_profile_enable(handle, False)
+
+    # roofline of the dominant kernel family (most GPU time in the timed region)
+    fam = {}
+    for op in prof:
+        f = fam.setdefault(op['label'], dict(flops=0.0, bytes=0.0, ms=0.0, launches=0))
+        f['flops'] += op['flops'] * op['launches']
+        f['bytes'] += op['bytes'] * op['launches']
+        f['ms'] += op['ms_total']
+        f['launches'] += op['launches']
+    dom_name, dom = max(fam.items(), key=lambda kv: kv[1]['ms'])
+    avg_ms = dom['ms'] / max(1, dom['launches'])
+    flops_per_launch = dom['flops'] / max(1, dom['launches'])
+    bytes_per_launch = dom['bytes'] / max(1, dom['launches'])
+    if flops_per_launch > 0:
+        achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12
+        roof = dict(bound='mfma', achieved=round(achieved, 2), peak=FP32_PEAK_TFLOPS, unit='TFLOP/s',
+                    frac=round(achieved / FP32_PEAK_TFLOPS, 4), traffic=None)
+    else:
+        achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+        roof = dict(bound='hbm', achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit='GB/s',
+                    frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None)
+    roof.update(kernel=dom_name, avg_launch_ms=round(avg_ms, 4), launches=dom['launches'],
+                algorithmic_per_launch=flops_per_launch if flops_per_launch > 0 else bytes_per_launch)
+    total_gpu_ms = sum(f['ms'] for f in fam.values())
+    total_flops = sum(f['flops'] for f in fam.values())
+
+    if rank == 0:
+        images = world * B * args.steps
+        line = dict(
+            metric=METRIC,
+            value=round(images / elapsed, 3),
+            unit='images/sec',
+            n_gpus=world,
+            steps=args.steps,
+            warmup=args.warmup,
+            ms_per_step=round(elapsed / args.steps * 1e3, 2),
+            higher_is_better=True,
+            scaling='weak',
+            vs_baseline=None,
+            dtype='f32',
+            data='synthetic',
+            config=dict(workload=f'DDIM-{args.respace_steps} (eta=0) sampling fold, CIFAR-10 UNet '
+                                 f'(dim 128, mults 1-2-2-2, 35.7M params, synthetic weights), 3x32x32, '
+                                 f'B={B} per GPU',
+                        global_batch=world * B, parallelism=f'dp{world}', denoise_steps=args.respace_steps),
+            roofline=roof,
+            step_level=dict(model_tflops=round(total_flops / (total_gpu_ms * 1e-3) / 1e12, 2) if total_gpu_ms else None,
+                            kernel_time_frac=round(total_gpu_ms * 1e-3 / elapsed, 4)),
+        )
+        if world == 1 and not args.no_cpu_baseline:
+            line['cpu_baseline'] = cpu_baseline(sd_cpu, args.cpu_batch, args.respace_steps)
+            line['gpu_over_cpu'] = round(line['value'] / line['cpu_baseline']['value'], 1)
+        else:
+            line['cpu_baseline'] = None
+        if args.profile_json:
+            with open(args.profile_json, 'w') as f:
+                json.dump(dict(families=fam, ops=prof), f, indent=1)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,103 @@
+// C-ABI wrappers over the kernel launchers (include/dm_hip.h).
+#include <string>
+#include "dm_common.h"
+#include "dm_kernels.h"
+
+namespace dm {
+namespace {
+thread_local std::string g_last_error;
+}
+void set_error(const std::string& msg) { g_last_error = msg; }
+const char* last_error() { return g_last_error.c_str(); }
+}  // namespace dm
+
+using dm::View;
+
+extern "C" int dm_abi_version(void) { return DM_ABI_VERSION; }
+
+extern "C" const char* dm_last_error(void) { return dm::last_error(); }
+
+extern "C" int dm_sampler_step(const dm_step_desc* d, void* stream) {
+  if (!d) { dm::set_error("null step descriptor"); return DM_ERR_ARG; }
+  dm::StepArgs s{};
+  s.B = d->B; s.C = d->C; s.HW = d->HW; s.Cm = d->Cm;
+  s.xt = d->xt; s.out_c = d->model_out; s.out_u = d->model_out_uncond;
+  s.w_u = d->w_uncond; s.w_c = d->w_cond;
+  s.objective = d->objective; s.clip = d->clip_denoised;
+  s.c_recip = d->sqrt_recip_ac; s.c_recipm1 = d->sqrt_recipm1_ac;
+  s.c_sa = d->sqrt_ac; s.c_s1ma = d->sqrt_one_minus_ac;
+  s.kind = d->kind; s.m1 = d->coef1; s.m2 = d->coef2;
+  s.var_mode = d->var_mode; s.std = d->std;
+  s.min_logvar = d->min_logvar; s.max_logvar = d->max_logvar;
+  s.add_noise = d->add_noise; s.noise = d->noise;
+  s.sample = d->sample; s.mean_out = d->mean; s.x0_out = d->pred_x0; s.eps_out = d->pred_eps;
+  s.var_out = d->var;
+  if (s.objective < 0 || s.objective > 2) { dm::set_error("invalid objective"); return DM_ERR_ARG; }
+  if (s.kind < 0 || s.kind > 1) { dm::set_error("invalid sampler kind"); return DM_ERR_ARG; }
+  if (s.B < 0 || s.C <= 0 || s.HW <= 0) { dm::set_error("invalid shape"); return DM_ERR_ARG; }
+  return dm::sampler_step(s, (hipStream_t)stream);
+}
+
+extern "C" int64_t dm_groupnorm_scratch_bytes(int B, int HW, int G) {
+  return (int64_t)B * dm::gn_num_chunks(HW) * G * (int64_t)sizeof(double2);
+}
+
+extern "C" int dm_groupnorm_nhwc(const float* x, int x_pitch, float* y, int y_pitch, int B, int HW, int C, int G,
+                                 float eps, const float* gamma, const float* beta, const float* mod_scale,
+                                 const float* mod_shift, int mod_pitch, int silu, void* scratch, void* stream) {
+  if (!x || !y || !scratch) { dm::set_error("null tensor"); return DM_ERR_ARG; }
+  if (B <= 0 || HW <= 0 || C <= 0 || G <= 0) { dm::set_error("invalid shape"); return DM_ERR_ARG; }
+  View vx{const_cast<float*>(x), B, HW, 1, C, x_pitch};
+  View vy{y, B, HW, 1, C, y_pitch};
+  hipStream_t st = (hipStream_t)stream;
+  int rc = dm::gn_partial(vx, G, (double2*)scratch, st);
+  if (rc) return rc;
+  return dm::gn_apply(vx, G, (const double2*)scratch, dm::gn_num_chunks(HW), eps, gamma, beta, mod_scale,
+                      mod_shift, mod_pitch, silu ? 1 : 0, vy, st);
+}
+
+extern "C" int dm_pack_conv_weight(const float* w, int Cout, int Cin, int taps, float* out, int ldw, int col0,
+                                   void* stream) {
+  if (!w || !out) { dm::set_error("null tensor"); return DM_ERR_ARG; }
+  if (Cout <= 0 || Cin <= 0 || (taps != 1 && taps != 9) || col0 + taps * Cin > ldw) {
+    dm::set_error("invalid conv weight shape");
+    return DM_ERR_ARG;
+  }
+  return dm::repack_conv(w, Cout, Cin, taps, out, ldw, col0, (hipStream_t)stream);
+}
+
+extern "C" int dm_conv2d_nhwc(const dm_conv_desc* d, void* stream) {
+  if (!d || !d->x || !d->w || !d->y) { dm::set_error("null tensor"); return DM_ERR_ARG; }
+  dm::ConvArgs a{};
+  a.x1 = d->x; a.x1_pitch = d->x_pitch; a.Cin1 = d->Cin; a.Hin = d->Hin; a.Win = d->Win;
+  a.taps = d->taps; a.stride = d->stride; a.upsample = d->upsample;
+  a.x2 = d->x2; a.x2_pitch = d->x2_pitch; a.Cin2 = d->Cin2;
+  a.w = d->w; a.K = d->K;
+  a.y = d->y; a.y_pitch = d->y_pitch; a.Cout = d->Cout; a.B = d->B; a.Hout = d->Hout; a.Wout = d->Wout;
+  a.bias = d->bias; a.rowvec = d->rowvec; a.rowvec_pitch = d->rowvec_pitch;
+  a.res = d->res; a.res_pitch = d->res_pitch;
+  return dm::conv2d_igemm(a, (hipStream_t)stream);
+}
+
+extern "C" int dm_gemm(const dm_gemm_desc* d, void* stream) {
+  if (!d || !d->A || !d->B || !d->C) { dm::set_error("null tensor"); return DM_ERR_ARG; }
+  dm::GemmArgs g{};
+  g.M = d->M; g.N = d->N; g.K = d->K; g.Z1 = d->Z1; g.Z2 = d->Z2;
+  g.A = d->A; g.a_s1 = d->a_s1; g.a_s2 = d->a_s2; g.lda = d->lda;
+  g.Bm = d->B; g.b_s1 = d->b_s1; g.b_s2 = d->b_s2; g.ldb = d->ldb; g.b_kn = d->b_kn;
+  g.C = d->C; g.c_s1 = d->c_s1; g.c_s2 = d->c_s2; g.ldc = d->ldc;
+  g.alpha = d->alpha; g.bias = d->bias; g.res = d->res; g.ld_res = d->ld_res; g.act = d->act;
+  return dm::gemm_batched(g, (hipStream_t)stream);
+}
+
+extern "C" int dm_softmax_rows(float* x, int64_t rows, int L, int ld, void* stream) {
+  if (!x) { dm::set_error("null tensor"); return DM_ERR_ARG; }
+  return dm::softmax_rows(x, rows, L, ld, (hipStream_t)stream);
+}
+
+extern "C" int dm_timestep_embedding(const int64_t* t, int B, int dim, int kind, const float* freqs, float* out,
+                                     void* stream) {
+  if (!t || !out) { dm::set_error("null tensor"); return DM_ERR_ARG; }
+  if (B <= 0) { dm::set_error("empty batch"); return DM_ERR_ARG; }
+  return dm::timestep_embed(t, B, dim, kind, freqs, out, (hipStream_t)stream);
+}

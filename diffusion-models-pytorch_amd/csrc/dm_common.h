@@ -1,0 +1,64 @@
+// Internal helpers shared by the dm_hip kernels and the C-ABI layer.
+// Not part of the public interface (see include/dm_hip.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "dm_hip.h"
+
+namespace dm {
+
+// Thread-local last-error string, surfaced through dm_last_error().
+void set_error(const std::string& msg);
+const char* last_error();
+
+// Return codes of the C ABI (DM_OK, DM_ERR_*) come from the public header.
+
+#define DM_CHECK_HIP(expr)                                                        \
+  do {                                                                            \
+    hipError_t _e = (expr);                                                       \
+    if (_e != hipSuccess) {                                                       \
+      ::dm::set_error(std::string(#expr) + ": " + hipGetErrorString(_e));         \
+      return DM_ERR_HIP;                                                    \
+    }                                                                             \
+  } while (0)
+
+#define DM_REQUIRE(cond, msg)                                                     \
+  do {                                                                            \
+    if (!(cond)) {                                                                \
+      ::dm::set_error(std::string("argument check failed: ") + (msg));            \
+      return DM_ERR_ARG;                                                    \
+    }                                                                             \
+  } while (0)
+
+#define DM_LAUNCH_CHECK()                                                         \
+  do {                                                                            \
+    hipError_t _e = hipGetLastError();                                            \
+    if (_e != hipSuccess) {                                                       \
+      ::dm::set_error(std::string("kernel launch: ") + hipGetErrorString(_e));    \
+      return DM_ERR_HIP;                                                    \
+    }                                                                             \
+  } while (0)
+
+// NHWC activation view. Element (b, y, x, c) lives at
+//   p[((b * H + y) * W + x) * pitch + c]
+// `pitch` >= C lets a tensor be a channel slice of a wider buffer (zero-copy
+// skip concatenation: the producer of a skip writes straight into the
+// consumer's concat buffer).
+struct View {
+  float* p;
+  int B, H, W, C;
+  int pitch;
+};
+
+__host__ __device__ inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
+
+__device__ __forceinline__ float silu_f(float v) {
+  // torch CPU: x / (1 + exp(-x)), IEEE division, accurate expf.
+  return v / (1.0f + expf(-v));
+}
+
+}  // namespace dm

@@ -1,0 +1,97 @@
+// Internal kernel entry points (host-side launchers). The public C ABI in
+// include/dm_hip.h wraps these.
+#pragma once
+#include "dm_common.h"
+
+namespace dm {
+
+constexpr int kGnPixPerChunk = 64;
+
+struct ConvArgs {
+  // segment 1: NHWC input view (channel pitch x1_pitch), source resolution Hin x Win
+  const float* x1;
+  int x1_pitch, Cin1, Hin, Win;
+  int taps;      // 1 or 9
+  int stride;    // 1 or 2
+  int upsample;  // nearest 2x before a 3x3 stride-1 conv
+  // segment 2 (optional): 1x1 product of x2 at output resolution
+  const float* x2;
+  int x2_pitch, Cin2;
+  // packed weights [Cout][K], K = taps * Cin1 + Cin2
+  const float* w;
+  int K;
+  // output
+  float* y;
+  int y_pitch, Cout, B, Hout, Wout;
+  const float* bias;    // [Cout] or null
+  const float* rowvec;  // [B][rowvec_pitch] per-image additive vector or null
+  int rowvec_pitch;
+  const float* res;     // residual at output resolution or null
+  int res_pitch;
+};
+
+struct GemmArgs {
+  int M, N, K;
+  int Z1, Z2;
+  const float* A;
+  long a_s1, a_s2;
+  int lda;
+  const float* Bm;
+  long b_s1, b_s2;
+  int ldb;
+  int b_kn;  // 0: B stored [n][k]; 1: B stored [k][n]
+  float* C;
+  long c_s1, c_s2;
+  int ldc;
+  float alpha;          // multiplies A elements on load (rounded per element)
+  const float* bias;    // [N] or null
+  const float* res;     // residual [M][ld_res] (batch 0 layout only) or null
+  int ld_res;
+  int act;              // 0 none, 1 SiLU
+};
+
+struct StepArgs {
+  int B, C, HW, Cm;
+  const float* xt;
+  const float* out_c;
+  const float* out_u;   // CFG uncond branch or null
+  float w_u, w_c;       // (1 - s), s
+  int objective;        // 0 eps, 1 x0, 2 v
+  int clip;
+  float c_recip, c_recipm1, c_sa, c_s1ma;
+  int kind;             // 0 DDIM, 1 DDPM
+  float m1, m2;
+  int var_mode;         // 0 scalar std, 1 learned range
+  float std;
+  float min_logvar, max_logvar;
+  int add_noise;
+  const float* noise;
+  float* sample;
+  float* mean_out;
+  float* x0_out;
+  float* eps_out;
+  float* var_out;
+};
+
+int gn_num_chunks(int HW);
+int gn_partial(const View& x, int G, double2* part, hipStream_t st);
+int gn_apply(const View& x, int G, const double2* part, int nchunk, float eps, const float* gamma,
+             const float* beta, const float* mod_scale, const float* mod_shift, int mod_pitch, int act,
+             const View& y, hipStream_t st);
+int conv2d_igemm(const ConvArgs& a, hipStream_t st);
+int conv_pick(const ConvArgs& a);
+std::string conv_label(const ConvArgs& a);
+int gemm_batched(const GemmArgs& g, hipStream_t st);
+int gemm_pick(const GemmArgs& g);
+std::string gemm_label(const GemmArgs& g);
+int timestep_embed(const int64_t* t, int B, int dim, int kind, const float* freqs, float* out, hipStream_t st);
+int softmax_rows(float* x, long rows, int L, int ld, hipStream_t st);
+int conv3x3_small_in(const float* x, int B, int Cin, int H, int W, const float* w, const float* bias,
+                     int Cout, const View& y, hipStream_t st);
+int conv3x3_small_out(const View& x, const float* w, const float* bias, int Cout, float* y, hipStream_t st);
+int sampler_step(const StepArgs& s, hipStream_t st);
+int nchw_to_nhwc(const float* x, int B, int C, int HW, float* y, int y_pitch, hipStream_t st);
+int nhwc_to_nchw(const float* x, int B, int C, int HW, int pitch, float* y, hipStream_t st);
+int repack_conv(const float* w, int Cout, int Cin, int taps, float* out, int ldw, int col0, hipStream_t st);
+
+}  // namespace dm

@@ -1,0 +1,321 @@
+// Bandwidth-bound / small kernels of the denoising step:
+//   * timestep sinusoidal embedding   models/modules.py:45-57 (UNet, [sin, cos])
+//                                     models/adm/nn.py:103-121 (ADM, [cos, sin])
+//   * row softmax (attention)         models/modules.py:96
+//   * small-channel direct 3x3 convs  models/unet.py:72 (first_conv, Cin=1/3, NCHW in)
+//                                     models/unet.py:118 (last_conv, Cout=1/3/6, NCHW out)
+//   * NCHW <-> NHWC conversion
+//   * the per-step sampler update     diffusions/ddpm.py:174-252, diffusions/ddim.py:57-77,
+//                                     CFG combine ddim.py:185 / ddpm.py:343-345
+// The sampler update is written op-for-op in the reference's rounding order
+// and compiled with -ffp-contract=off, so with identical inputs it is
+// bit-identical to the torch CPU path (coefficients come from the host,
+// computed with the same torch 0-dim ops as the reference).
+#include "dm_common.h"
+#include "dm_kernels.h"
+
+namespace dm {
+
+namespace {
+
+__global__ void timestep_embed_kernel(const int64_t* __restrict__ t, int B, int dim, int kind,
+                                      const float* __restrict__ freqs, float* __restrict__ out) {
+  const int half = dim / 2;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= B * half) return;
+  const int b = idx / half, i = idx - (idx / half) * half;
+  const float tv = (float)t[b];
+  float f;
+  if (freqs) {
+    // host-provided table (the reference's torch CPU expression, bit-identical on that host)
+    f = freqs[i];
+  } else if (kind == 0) {
+    // UNet: exp(arange(half) * -(ln(1e4) / (half - 1)))
+    const float c = (float)(-(log(10000.0) / (double)(half - 1)));
+    f = expf((float)i * c);
+  } else {
+    // ADM: exp(-ln(1e4) * arange(half, f32) / half)
+    const float c = (float)(-log(10000.0));
+    f = expf(((float)i * c) / (float)half);
+  }
+  const float arg = tv * f;
+  float s = sinf(arg), co = cosf(arg);
+  if (kind == 0) {
+    out[(size_t)b * dim + i] = s;
+    out[(size_t)b * dim + half + i] = co;
+  } else {
+    out[(size_t)b * dim + i] = co;
+    out[(size_t)b * dim + half + i] = s;
+  }
+}
+
+// One wave per row, in place.
+__global__ void softmax_rows_kernel(float* __restrict__ x, long rows, int L, int ld) {
+  const long row = (long)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  float* r = x + row * ld;
+  float mx = -INFINITY;
+  for (int j = lane; j < L; j += 64) mx = fmaxf(mx, r[j]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  float sum = 0.f;
+  for (int j = lane; j < L; j += 64) {
+    float e = expf(r[j] - mx);
+    r[j] = e;
+    sum += e;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+  const float inv = 1.0f / sum;
+  for (int j = lane; j < L; j += 64) r[j] = r[j] * inv;
+}
+
+// first conv: NCHW input with few channels -> NHWC (pitched) output.
+// One block per (image, output row).
+__global__ void conv3x3_small_in_kernel(const float* __restrict__ x, int Cin, int H, int W,
+                                        const float* __restrict__ w, const float* __restrict__ bias,
+                                        int Cout, float* __restrict__ y, int y_pitch) {
+  extern __shared__ float rows[];  // [Cin][3][W + 2]
+  const int b = blockIdx.y, oy = blockIdx.x;
+  const int Wp = W + 2;
+  for (int i = threadIdx.x; i < Cin * 3 * Wp; i += blockDim.x) {
+    const int ci = i / (3 * Wp);
+    const int rr = (i / Wp) % 3;
+    const int xx = i % Wp - 1;
+    const int iy = oy + rr - 1;
+    float v = 0.f;
+    if (iy >= 0 && iy < H && xx >= 0 && xx < W) v = x[(((size_t)b * Cin + ci) * H + iy) * W + xx];
+    rows[i] = v;
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < W * Cout; idx += blockDim.x) {
+    const int ox = idx / Cout, co = idx - (idx / Cout) * Cout;
+    float acc = 0.f;
+    for (int ci = 0; ci < Cin; ++ci)
+      for (int ky = 0; ky < 3; ++ky)
+        for (int kx = 0; kx < 3; ++kx)
+          acc += w[((co * Cin + ci) * 3 + ky) * 3 + kx] * rows[(ci * 3 + ky) * Wp + ox + kx];
+    acc = acc + bias[co];
+    y[(((size_t)b * H + oy) * W + ox) * y_pitch + co] = acc;
+  }
+}
+
+// last conv: NHWC (pitched) input -> NCHW output with few channels.
+template <int MAXC>
+__global__ void conv3x3_small_out_kernel(const float* __restrict__ x, int B, int H, int W, int Cin,
+                                         int pitch, const float* __restrict__ w,
+                                         const float* __restrict__ bias, int Cout,
+                                         float* __restrict__ y) {
+  extern __shared__ float wl[];  // [9][Cin][Cout]
+  for (int i = threadIdx.x; i < 9 * Cin * Cout; i += blockDim.x) {
+    const int co = i % Cout;
+    const int ci = (i / Cout) % Cin;
+    const int tap = i / (Cout * Cin);
+    wl[i] = w[((size_t)co * Cin + ci) * 9 + tap];
+  }
+  __syncthreads();
+  const long pix = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long M = (long)B * H * W;
+  if (pix >= M) return;
+  const int b = pix / (H * W);
+  const int rem = pix - (long)b * H * W;
+  const int oy = rem / W, ox = rem % W;
+  float acc[MAXC];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) acc[c] = 0.f;
+  for (int tap = 0; tap < 9; ++tap) {
+    const int iy = oy + tap / 3 - 1, ix = ox + tap % 3 - 1;
+    if (iy < 0 || iy >= H || ix < 0 || ix >= W) continue;
+    const float* src = x + (((size_t)b * H + iy) * W + ix) * pitch;
+    const float* wt = wl + tap * Cin * Cout;
+    for (int ci = 0; ci < Cin; ci += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(src + ci);
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int c = 0; c < MAXC; ++c)
+          if (c < Cout) acc[c] += vv[q] * wt[(ci + q) * Cout + c];
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c)
+    if (c < Cout) y[(((size_t)b * Cout + c) * H + oy) * W + ox] = acc[c] + bias[c];
+}
+
+__global__ void sampler_step_kernel(StepArgs s) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long per = (long)s.C * s.HW;
+  const long total = per * s.B;
+  if (e >= total) return;
+  const long b = e / per, r = e - b * per;
+  const long mo = b * (long)s.Cm * s.HW + r;  // model-output index of the first C channels
+  const float xt = s.xt[e];
+
+  // predict(): model output -> (x0, eps) for one branch, reference ddpm.py:174-203
+  auto predict = [&](float out, int objective, float& x0, float& eps) {
+    if (objective == 0) {
+      x0 = s.c_recip * xt - s.c_recipm1 * out;
+    } else if (objective == 1) {
+      x0 = out;
+    } else {
+      x0 = s.c_sa * xt - s.c_s1ma * out;
+    }
+    if (s.clip) x0 = fminf(fmaxf(x0, -1.0f), 1.0f);
+    eps = (s.c_recip * xt - x0) / s.c_recipm1;
+  };
+
+  float x0, eps;
+  if (s.out_u) {
+    float x0c, epsc, x0u, epsu;
+    predict(s.out_c[mo], s.objective, x0c, epsc);
+    predict(s.out_u[mo], s.objective, x0u, epsu);
+    const float comb = s.w_u * epsu + s.w_c * epsc;
+    predict(comb, 0, x0, eps);  // hack_objective('pred_eps')
+  } else {
+    predict(s.out_c[mo], s.objective, x0, eps);
+  }
+
+  float mean, sample;
+  if (s.kind == 0) {
+    mean = s.m1 * x0 + s.m2 * eps;  // ddim.py:72-73
+  } else {
+    mean = s.m1 * x0 + s.m2 * xt;   // ddpm.py:230
+  }
+  float var = 0.f;
+  float sd = s.std;
+  if (s.var_mode == 1 && s.add_noise) {
+    // learned_range, ddpm.py:240-246; learned channel comes from the cond branch
+    const float lv = s.out_c[mo + per];
+    const float frac = (lv + 1.0f) / 2.0f;
+    const float logvar = frac * s.max_logvar + (1.0f - frac) * s.min_logvar;
+    var = expf(logvar);
+    sd = sqrtf(var);
+  }
+  if (s.add_noise) {
+    const float nz = s.noise ? s.noise[e] : 0.f;
+    sample = mean + sd * nz;
+  } else {
+    sample = mean;
+  }
+  s.sample[e] = sample;
+  if (s.mean_out) s.mean_out[e] = mean;
+  if (s.x0_out) s.x0_out[e] = x0;
+  if (s.eps_out) s.eps_out[e] = eps;
+  if (s.var_out) s.var_out[e] = var;
+}
+
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, int B, int C, int HW,
+                                    float* __restrict__ y, int y_pitch) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)B * C * HW;
+  if (e >= total) return;
+  const long b = e / ((long)C * HW);
+  const long r = e - b * C * HW;
+  const int c = r / HW, p = r % HW;
+  y[((size_t)b * HW + p) * y_pitch + c] = x[e];
+}
+
+__global__ void nhwc_to_nchw_kernel(const float* __restrict__ x, int B, int C, int HW, int pitch,
+                                    float* __restrict__ y) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)B * C * HW;
+  if (e >= total) return;
+  const long b = e / ((long)C * HW);
+  const long r = e - b * C * HW;
+  const int c = r / HW, p = r % HW;
+  y[e] = x[((size_t)b * HW + p) * pitch + c];
+}
+
+// [Cout][Cin][kh][kw] -> [Cout][kh*kw][Cin] written at row pitch ldw, column offset col0
+__global__ void repack_conv_kernel(const float* __restrict__ w, int Cout, int Cin, int taps,
+                                   float* __restrict__ out, int ldw, int col0) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)Cout * Cin * taps;
+  if (e >= total) return;
+  const int co = e / ((long)Cin * taps);
+  const int r = e - (long)co * Cin * taps;
+  const int ci = r / taps, tap = r % taps;
+  out[(size_t)co * ldw + col0 + tap * Cin + ci] = w[e];
+}
+
+}  // namespace
+
+int timestep_embed(const int64_t* t, int B, int dim, int kind, const float* freqs, float* out, hipStream_t st) {
+  DM_REQUIRE(dim % 2 == 0 && dim >= 4, "timestep embedding: dim must be even and >= 4");
+  const int n = B * (dim / 2);
+  hipLaunchKernelGGL(timestep_embed_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, st, t, B, dim, kind, freqs, out);
+  DM_LAUNCH_CHECK();
+  return DM_OK;
+}
+
+int softmax_rows(float* x, long rows, int L, int ld, hipStream_t st) {
+  DM_REQUIRE(rows > 0 && L > 0 && ld >= L, "softmax: bad shape");
+  const long blocks = (rows + 3) / 4;
+  DM_REQUIRE(blocks < (1L << 31), "softmax: too many rows");
+  hipLaunchKernelGGL(softmax_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, rows, L, ld);
+  DM_LAUNCH_CHECK();
+  return DM_OK;
+}
+
+int conv3x3_small_in(const float* x, int B, int Cin, int H, int W, const float* w, const float* bias,
+                     int Cout, const View& y, hipStream_t st) {
+  DM_REQUIRE(Cin >= 1 && Cin <= 16, "first conv: Cin out of range");
+  DM_REQUIRE(y.C == Cout && y.H == H && y.W == W && y.B == B, "first conv: output view mismatch");
+  size_t smem = (size_t)Cin * 3 * (W + 2) * sizeof(float);
+  hipLaunchKernelGGL(conv3x3_small_in_kernel, dim3(H, B), dim3(256), smem, st, x, Cin, H, W, w, bias, Cout,
+                     y.p, y.pitch);
+  DM_LAUNCH_CHECK();
+  return DM_OK;
+}
+
+int conv3x3_small_out(const View& x, const float* w, const float* bias, int Cout, float* y, hipStream_t st) {
+  DM_REQUIRE(Cout >= 1 && Cout <= 8, "last conv: Cout out of range");
+  DM_REQUIRE(x.C % 4 == 0 && x.pitch % 4 == 0, "last conv: channel alignment");
+  size_t smem = (size_t)9 * x.C * Cout * sizeof(float);
+  DM_REQUIRE(smem <= 64 * 1024, "last conv: weights exceed LDS budget");
+  const long M = (long)x.B * x.H * x.W;
+  hipLaunchKernelGGL((conv3x3_small_out_kernel<8>), dim3((unsigned)((M + 255) / 256)), dim3(256), smem, st,
+                     x.p, x.B, x.H, x.W, x.C, x.pitch, w, bias, Cout, y);
+  DM_LAUNCH_CHECK();
+  return DM_OK;
+}
+
+int sampler_step(const StepArgs& s, hipStream_t st) {
+  DM_REQUIRE(s.xt && s.out_c && s.sample, "sampler step: null tensor");
+  DM_REQUIRE(s.Cm == s.C || s.Cm == 2 * s.C, "sampler step: model output channels must be C or 2C");
+  DM_REQUIRE(s.var_mode == 0 || s.Cm == 2 * s.C, "sampler step: learned_range needs 2C model channels");
+  const long total = (long)s.B * s.C * s.HW;
+  if (total == 0) return DM_OK;
+  hipLaunchKernelGGL(sampler_step_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, s);
+  DM_LAUNCH_CHECK();
+  return DM_OK;
+}
+
+int nchw_to_nhwc(const float* x, int B, int C, int HW, float* y, int y_pitch, hipStream_t st) {
+  const long total = (long)B * C * HW;
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x, B, C, HW,
+                     y, y_pitch);
+  DM_LAUNCH_CHECK();
+  return DM_OK;
+}
+
+int nhwc_to_nchw(const float* x, int B, int C, int HW, int pitch, float* y, hipStream_t st) {
+  const long total = (long)B * C * HW;
+  hipLaunchKernelGGL(nhwc_to_nchw_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x, B, C, HW,
+                     pitch, y);
+  DM_LAUNCH_CHECK();
+  return DM_OK;
+}
+
+int repack_conv(const float* w, int Cout, int Cin, int taps, float* out, int ldw, int col0, hipStream_t st) {
+  const long total = (long)Cout * Cin * taps;
+  hipLaunchKernelGGL(repack_conv_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, w, Cout, Cin,
+                     taps, out, ldw, col0);
+  DM_LAUNCH_CHECK();
+  return DM_OK;
+}
+
+}  // namespace dm

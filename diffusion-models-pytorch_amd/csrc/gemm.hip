@@ -1,0 +1,183 @@
+// Batched fp32 MFMA GEMM: C[z][m][n] = act( sum_k (alpha * A[z][m][k]) * B[z](k, n) + bias[n] )
+//
+// Used for the small dense contractions of the denoisers:
+//   * nn.Linear layers (time MLP models/unet.py:64-69, ResBlock proj :18-21)
+//     with B = weight [N][K] ("BT" layout) and optional SiLU epilogue;
+//   * the attention contractions of SelfAttentionBlock (models/modules.py:96-97):
+//       S = (q * scale)^T k   -> A = q rows (alpha = scale), B = k rows [n][k]
+//       O = attn v^T         -> A = attn rows, B = v stored [k][n] ("BN")
+// Batch index z = z1 * Z2 + z2 with independent strides for both levels
+// (image, head).
+#include "dm_common.h"
+#include "dm_kernels.h"
+#include "mfma_tile.h"
+
+namespace dm {
+
+namespace {
+
+template <int BM, int BN, int WM, int WN, bool B_KN>
+__global__ void __launch_bounds__(256)
+gemm_kernel(GemmArgs g) {
+  using Cfg = TileCfg<BM, BN, WM, WN>;
+  __shared__ __attribute__((aligned(16))) float lds[Cfg::LDS_FLOATS];
+
+  const int z = blockIdx.z;
+  const int z1 = z / g.Z2, z2 = z - (z / g.Z2) * g.Z2;
+  const float* A = g.A + (size_t)z1 * g.a_s1 + (size_t)z2 * g.a_s2;
+  const float* Bm = g.Bm + (size_t)z1 * g.b_s1 + (size_t)z2 * g.b_s2;
+  float* C = g.C + (size_t)z1 * g.c_s1 + (size_t)z2 * g.c_s2;
+
+  const int nN = ceil_div(g.N, BN);
+  const int mt = blockIdx.x / nN, nt = blockIdx.x % nN;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int t = threadIdx.x;
+  const int lane = t & 63, wave = t >> 6;
+  const int wm = wave / Cfg::NWN, wn = wave % Cfg::NWN;
+  const int lc4 = t & 7, lrow = t >> 3;
+
+  // "BN" loader geometry: BK rows of k, BN/4 float4 per row.
+  constexpr int KN_C4 = BN / 4;
+  constexpr int KN_ROWS_PER_PASS = Cfg::NT / KN_C4;
+  constexpr int KN_ITERS = (kBK + KN_ROWS_PER_PASS - 1) / KN_ROWS_PER_PASS;
+  static_assert(!B_KN || (Cfg::NT % KN_C4 == 0), "BN loader geometry");
+
+  const int nk = ceil_div(g.K, kBK);
+  f4 ra[Cfg::A_ITERS];
+  f4 rb[B_KN ? KN_ITERS : Cfg::B_ITERS];
+  const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
+
+  auto load_tile = [&](int kt) {
+    const int k = kt * kBK + 4 * lc4;
+#pragma unroll
+    for (int i = 0; i < Cfg::A_ITERS; ++i) {
+      const int m = m0 + lrow + i * Cfg::ROWS_PER_PASS;
+      if (m < g.M && k < g.K) {
+        f4 v = *reinterpret_cast<const f4*>(A + (size_t)m * g.lda + k);
+        if (g.alpha != 1.0f) v = v * g.alpha;
+        ra[i] = v;
+      } else {
+        ra[i] = zero4;
+      }
+    }
+    if constexpr (!B_KN) {
+#pragma unroll
+      for (int j = 0; j < Cfg::B_ITERS; ++j) {
+        const int n = n0 + lrow + j * Cfg::ROWS_PER_PASS;
+        rb[j] = (n < g.N && k < g.K) ? *reinterpret_cast<const f4*>(Bm + (size_t)n * g.ldb + k) : zero4;
+      }
+    } else {
+      const int n4 = t % KN_C4, kr = t / KN_C4;
+#pragma unroll
+      for (int j = 0; j < KN_ITERS; ++j) {
+        const int kk = kt * kBK + kr + j * KN_ROWS_PER_PASS;
+        const int n = n0 + 4 * n4;
+        rb[j] = (kr + j * KN_ROWS_PER_PASS < kBK && kk < g.K && n < g.N)
+                    ? *reinterpret_cast<const f4*>(Bm + (size_t)kk * g.ldb + n)
+                    : zero4;
+      }
+    }
+  };
+
+  auto store_tile = [&](int buf) {
+    float* As = lds + buf * Cfg::STAGE;
+    float* Bs = As + Cfg::A_ELEMS;
+#pragma unroll
+    for (int i = 0; i < Cfg::A_ITERS; ++i)
+      *reinterpret_cast<f4*>(As + (lrow + i * Cfg::ROWS_PER_PASS) * kLDK + 4 * lc4) = ra[i];
+    if constexpr (!B_KN) {
+#pragma unroll
+      for (int j = 0; j < Cfg::B_ITERS; ++j)
+        *reinterpret_cast<f4*>(Bs + (lrow + j * Cfg::ROWS_PER_PASS) * kLDK + 4 * lc4) = rb[j];
+    } else {
+      const int n4 = t % KN_C4, kr = t / KN_C4;
+#pragma unroll
+      for (int j = 0; j < KN_ITERS; ++j) {
+        const int kk = kr + j * KN_ROWS_PER_PASS;
+        if (kk < kBK) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) Bs[(4 * n4 + q) * kLDK + kk] = rb[j][q];
+        }
+      }
+    }
+  };
+
+  f16v acc[Cfg::TM][Cfg::TN];
+#pragma unroll
+  for (int i = 0; i < Cfg::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < Cfg::TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) load_tile(kt + 1);
+    const float* As = lds + buf * Cfg::STAGE;
+    const float* Bs = As + Cfg::A_ELEMS;
+    mfma_slice<Cfg::TM, Cfg::TN>(As, Bs, wm * WM, wn * WN, lane, acc);
+    if (kt + 1 < nk) store_tile(buf ^ 1);
+    __syncthreads();
+  }
+
+  const int lr = lane & 31, lh = lane >> 5;
+#pragma unroll
+  for (int j = 0; j < Cfg::TN; ++j) {
+    const int n = n0 + wn * WN + j * 32 + lr;
+    if (n >= g.N) continue;
+    const float bn = g.bias ? g.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < Cfg::TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * WM + i * 32 + acc_row(r, lh);
+        if (m >= g.M) continue;
+        float v = acc[i][j][r];
+        if (g.bias) v = v + bn;
+        if (g.res) v = v + g.res[(size_t)m * g.ld_res + n];
+        if (g.act == 1) v = silu_f(v);
+        C[(size_t)m * g.ldc + n] = v;
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+int launch_gemm(const GemmArgs& g, hipStream_t st) {
+  using Cfg = TileCfg<BM, BN, WM, WN>;
+  dim3 grid(ceil_div(g.M, BM) * ceil_div(g.N, BN), 1, g.Z1 * g.Z2);
+  if (g.b_kn)
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, true>), grid, dim3(Cfg::NT), 0, st, g);
+  else
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, false>), grid, dim3(Cfg::NT), 0, st, g);
+  DM_LAUNCH_CHECK();
+  return DM_OK;
+}
+
+}  // namespace
+
+int gemm_batched(const GemmArgs& g, hipStream_t st) {
+  DM_REQUIRE(g.M > 0 && g.N > 0 && g.K > 0, "gemm: empty problem");
+  DM_REQUIRE(g.K % 4 == 0 && g.lda % 4 == 0 && g.ldb % 4 == 0, "gemm: K and leading dims must be multiples of 4");
+  DM_REQUIRE(!g.b_kn || g.N % 4 == 0, "gemm: N must be a multiple of 4 for the [k][n] B layout");
+  DM_REQUIRE((reinterpret_cast<uintptr_t>(g.A) & 15) == 0 && (reinterpret_cast<uintptr_t>(g.Bm) & 15) == 0,
+             "gemm: operands must be 16-byte aligned");
+  DM_REQUIRE(g.Z1 >= 1 && g.Z2 >= 1 && (long)g.Z1 * g.Z2 <= 65535, "gemm: batch out of range");
+  if (gemm_pick(g) == 0) return launch_gemm<128, 128, 64, 64>(g, st);
+  return launch_gemm<64, 64, 32, 32>(g, st);
+}
+
+int gemm_pick(const GemmArgs& g) {
+  const long tiles128 = (long)ceil_div(g.M, 128) * ceil_div(g.N, 128) * g.Z1 * g.Z2;
+  return (g.M >= 128 && g.N >= 128 && tiles128 >= 512) ? 0 : 1;
+}
+
+std::string gemm_label(const GemmArgs& g) {
+  std::string s = gemm_pick(g) == 0 ? "gemm_kernel<128,128,64,64" : "gemm_kernel<64,64,32,32";
+  return s + (g.b_kn ? ",true>" : ",false>");
+}
+
+}  // namespace dm

@@ -1,0 +1,826 @@
+// Native executor for the DDPM UNet denoiser (models/unet.py:46-152).
+//
+// Build time (dm_unet_create): the reference state_dict tensors are consumed
+// in registration order, checked against the expected element counts, and
+// packed into one library-owned device arena:
+//   - 3x3 / 1x1 conv weights -> implicit-GEMM layout [Cout][K] (k = tap*Cin + c);
+//     a ResBlock's 1x1 shortcut is appended to its second conv's K
+//     (W2 | Wsc, bias b2 + bsc) so the shortcut is one more K segment;
+//   - q, k, v 1x1 convs -> one [3C][C] weight (single QKV GEMM);
+//   - every ResBlock's time projection -> one [sum Cout][4*dim] weight, so the
+//     per-step projections of all blocks are a single GEMM.
+// Forward (dm_unet_forward): a flat list of launches on one stream over a
+// per-batch workspace. Activations are NHWC; skip tensors are written by
+// their producer directly into the channel slice of the up-path block that
+// concatenates them (models/unet.py:145), so torch.cat never materialises.
+#include <memory>
+#include <vector>
+#include <functional>
+#include <cmath>
+#include <map>
+
+#include "dm_common.h"
+#include "dm_kernels.h"
+
+namespace dm {
+
+namespace {
+
+struct ParamReader {
+  const float* const* params;
+  const int64_t* numels;
+  int n, pos = 0;
+  std::string err;
+  const float* take(int64_t expect, const char* what) {
+    if (pos >= n) {
+      if (err.empty()) err = std::string("too few parameters at ") + what;
+      return nullptr;
+    }
+    if (numels[pos] != expect && err.empty())
+      err = "parameter " + std::to_string(pos) + " (" + what + "): expected " + std::to_string(expect) +
+            " elements, got " + std::to_string(numels[pos]);
+    return params[pos++];
+  }
+};
+
+// A copy / repack job into the weight arena.
+struct PackJob {
+  int kind;  // 0 raw copy, 1 conv repack, 2 add (bias sum)
+  const float* src;
+  const float* src2;
+  int64_t n;
+  int Cout, Cin, taps, ldw, col0;
+  size_t dst;  // float offset in arena
+};
+
+struct Packer {
+  std::vector<PackJob> jobs;
+  size_t size = 0;
+  size_t reserve(int64_t n) {
+    size_t off = size;
+    size += ((size_t)n + 63) / 64 * 64;
+    return off;
+  }
+  size_t raw(const float* src, int64_t n) {
+    size_t off = reserve(n);
+    jobs.push_back({0, src, nullptr, n, 0, 0, 0, 0, 0, off});
+    return off;
+  }
+  void raw_at(const float* src, int64_t n, size_t off) { jobs.push_back({0, src, nullptr, n, 0, 0, 0, 0, 0, off}); }
+  void conv_at(const float* w, int Cout, int Cin, int taps, int ldw, int col0, size_t off) {
+    jobs.push_back({1, w, nullptr, (int64_t)Cout * Cin * taps, Cout, Cin, taps, ldw, col0, off});
+  }
+  void add_at(const float* a, const float* b, int64_t n, size_t off) {
+    jobs.push_back({2, a, b, n, 0, 0, 0, 0, 0, off});
+  }
+};
+
+__global__ void vec_add_kernel(const float* a, const float* b, float* out, int64_t n) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = a[i] + b[i];
+}
+
+struct GnP { size_t g, b; int C; };
+struct ConvP { size_t w, bias; int Cout, Cin, taps, K; };
+
+struct ResBlockP {
+  int cin, cout;
+  GnP gn1, gn2;
+  ConvP conv1, conv2;  // conv2 carries the shortcut segment when cin != cout
+  int proj_col;        // column offset of this block's projection in the fused proj output
+};
+
+struct AttnP {
+  int C, heads;
+  GnP gn;
+  size_t wqkv, bqkv, wproj, bproj;
+};
+
+enum NodeKind { N_RES, N_ATTN, N_DOWN, N_UP };
+
+}  // namespace
+
+struct Op {
+  std::string label;   // kernel family / tile, matches the rocprof kernel name family
+  double flops;        // algorithmic FLOPs of one launch
+  double bytes;        // algorithmic HBM bytes of one launch (read + write of logical tensors)
+  std::function<int(hipStream_t)> fn;
+};
+
+namespace {
+
+struct Node {
+  NodeKind kind;
+  int idx;        // index into res/attn/conv vectors
+  int cin, cout;  // channels in/out
+  int h_in;       // input resolution (relative to image H; H / 2^level)
+  int level_in, level_out;
+  bool skip_producer = false;
+  int skip_id = -1;       // id of the skip this node produces
+  int pops_skip = -1;     // for up-RBs: id of the skip consumed
+  int concat_cx = 0;      // for up-RBs: channels of the X part
+};
+
+}  // namespace
+
+struct UNetModel {
+  dm_unet_arch arch;
+  float* arena = nullptr;
+  size_t arena_floats = 0;
+  // packed parameters (offsets into arena)
+  size_t te_w1, te_b1, te_w2, te_b2;
+  size_t te_freqs;            // [dim/2] sinusoid frequencies
+  bool te_freqs_set = false;  // host table installed (else computed on device)
+  size_t first_w, first_b;
+  size_t proj_w, proj_b;
+  int proj_total = 0;
+  GnP last_gn;
+  size_t last_w, last_b;
+  std::vector<ResBlockP> res;
+  std::vector<AttnP> attn;
+  std::vector<ConvP> convs;  // down / up sample convs
+  std::vector<Node> nodes;
+  std::vector<int> skip_C, skip_level;  // per skip id
+  int n_levels = 0;
+
+  // workspace cache
+  struct Plan {
+    int B = 0, H = 0, W = 0;
+    std::vector<void*> allocs;
+    size_t bytes = 0;
+    std::vector<Op> ops;
+    // profiling: per-op HIP event pairs recorded on the launch stream
+    bool profiling = false;
+    std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
+    std::vector<double> prof_ms;
+    std::vector<int64_t> prof_launches;
+    const float* x = nullptr;
+    const int64_t* t = nullptr;
+    float* out = nullptr;
+  };
+  std::unique_ptr<Plan> plan;
+
+  float* P(size_t off) const { return arena + off; }
+  ~UNetModel();
+  int build_plan(int B, int H, int W);
+};
+
+static void drain_profile(UNetModel::Plan* p) {
+  for (auto& e : p->pending) {
+    float ms = 0.f;
+    if (hipEventSynchronize(e.second.second) == hipSuccess &&
+        hipEventElapsedTime(&ms, e.second.first, e.second.second) == hipSuccess) {
+      p->prof_ms[e.first] += ms;
+      p->prof_launches[e.first] += 1;
+    }
+    (void)hipEventDestroy(e.second.first);
+    (void)hipEventDestroy(e.second.second);
+  }
+  p->pending.clear();
+}
+
+static void free_plan(UNetModel::Plan* p) {
+  if (!p) return;
+  drain_profile(p);
+  for (void* a : p->allocs) (void)hipFree(a);
+  p->allocs.clear();
+}
+
+UNetModel::~UNetModel() {
+  if (plan) free_plan(plan.get());
+  if (arena) (void)hipFree(arena);
+}
+
+static int count_params(const dm_unet_arch& a) {
+  // mirrors the registration order of models/unet.py:47-119
+  int n = 4 + 2;  // time_embed (2 linears), first_conv
+  auto rb = [](int cin, int cout) { return 10 + (cin != cout ? 2 : 0); };
+  const int attn = 10;
+  int cur = a.dim;
+  std::vector<int> dims{a.dim};
+  for (int i = 0; i < a.n_stages; ++i) {
+    int out = a.dim * a.dim_mults[i];
+    for (int j = 0; j < a.num_res_blocks; ++j) {
+      n += rb(cur, out);
+      if (a.use_attn[i]) n += attn;
+      dims.push_back(out);
+      cur = out;
+    }
+    if (i < a.n_stages - 1) { n += 2; dims.push_back(out); }
+  }
+  n += rb(cur, cur) * 2 + attn;
+  for (int i = a.n_stages - 1; i >= 0; --i) {
+    int out = a.dim * a.dim_mults[i];
+    for (int j = 0; j < a.num_res_blocks + 1; ++j) {
+      int s = dims.back();
+      dims.pop_back();
+      n += rb(s + cur, out);
+      if (a.use_attn[i]) n += attn;
+      cur = out;
+    }
+    if (i > 0) n += 2;
+  }
+  n += 4;  // last_conv GN + conv
+  return n;
+}
+
+static int validate_arch(const dm_unet_arch* a) {
+  DM_REQUIRE(a != nullptr, "arch is null");
+  DM_REQUIRE(a->n_stages >= 1 && a->n_stages <= DM_MAX_STAGES, "n_stages out of range");
+  DM_REQUIRE(a->dim >= 32 && a->dim % 32 == 0, "dim must be a positive multiple of 32");
+  DM_REQUIRE(a->in_channels >= 1 && a->in_channels <= 16, "in_channels out of range (1..16)");
+  DM_REQUIRE(a->out_channels >= 1 && a->out_channels <= 8, "out_channels out of range (1..8)");
+  DM_REQUIRE(a->num_res_blocks >= 1, "num_res_blocks must be >= 1");
+  DM_REQUIRE(a->n_heads >= 1, "n_heads must be >= 1");
+  for (int i = 0; i < a->n_stages; ++i) {
+    DM_REQUIRE(a->dim_mults[i] >= 1, "dim_mults must be >= 1");
+    if (a->use_attn[i]) DM_REQUIRE((a->dim * a->dim_mults[i]) % a->n_heads == 0, "dim not divisible by heads");
+  }
+  return DM_OK;
+}
+
+// ---------------------------------------------------------------------------
+// create
+// ---------------------------------------------------------------------------
+static int unet_create(const dm_unet_arch* arch, const float* const* params, const int64_t* numels, int n_params,
+                       hipStream_t st, UNetModel** out) {
+  int rc = validate_arch(arch);
+  if (rc) return rc;
+  const dm_unet_arch a = *arch;
+  const int expect = count_params(a);
+  DM_REQUIRE(n_params == expect, "expected " + std::to_string(expect) + " parameter tensors, got " +
+                                     std::to_string(n_params));
+  auto m = std::make_unique<UNetModel>();
+  m->arch = a;
+  ParamReader rd{params, numels, n_params};
+  Packer pk;
+  const int D = a.dim, TD = 4 * a.dim;
+
+  // time embedding MLP: Linear(D, 4D) -> SiLU -> Linear(4D, 4D)
+  m->te_w1 = pk.raw(rd.take((int64_t)TD * D, "time_embed.1.weight"), (int64_t)TD * D);
+  m->te_b1 = pk.raw(rd.take(TD, "time_embed.1.bias"), TD);
+  m->te_w2 = pk.raw(rd.take((int64_t)TD * TD, "time_embed.3.weight"), (int64_t)TD * TD);
+  m->te_b2 = pk.raw(rd.take(TD, "time_embed.3.bias"), TD);
+  m->te_freqs = pk.reserve(D / 2);
+  m->first_w = pk.raw(rd.take((int64_t)D * a.in_channels * 9, "first_conv.weight"), (int64_t)D * a.in_channels * 9);
+  m->first_b = pk.raw(rd.take(D, "first_conv.bias"), D);
+
+  // Projections are collected then packed into one matrix after the walk.
+  struct ProjSrc { const float* w; const float* b; int cout; };
+  std::vector<ProjSrc> projs;
+
+  auto gn = [&](int C, const char* what) {
+    GnP g;
+    g.C = C;
+    g.g = pk.raw(rd.take(C, what), C);
+    g.b = pk.raw(rd.take(C, what), C);
+    return g;
+  };
+  auto resblock = [&](int cin, int cout) {
+    ResBlockP r;
+    r.cin = cin;
+    r.cout = cout;
+    r.gn1 = gn(cin, "ResBlock.blk1.0 (GroupNorm)");
+    const float* w1 = rd.take((int64_t)cout * cin * 9, "ResBlock.blk1.2.weight");
+    const float* b1 = rd.take(cout, "ResBlock.blk1.2.bias");
+    r.conv1 = {0, 0, cout, cin, 9, 9 * cin};
+    r.conv1.w = pk.reserve((int64_t)cout * 9 * cin);
+    pk.conv_at(w1, cout, cin, 9, 9 * cin, 0, r.conv1.w);
+    r.conv1.bias = pk.raw(b1, cout);
+    const float* pw = rd.take((int64_t)cout * TD, "ResBlock.proj.1.weight");
+    const float* pb = rd.take(cout, "ResBlock.proj.1.bias");
+    r.proj_col = m->proj_total;
+    m->proj_total += cout;
+    projs.push_back({pw, pb, cout});
+    r.gn2 = gn(cout, "ResBlock.blk2.0 (GroupNorm)");
+    const float* w2 = rd.take((int64_t)cout * cout * 9, "ResBlock.blk2.3.weight");
+    const float* b2 = rd.take(cout, "ResBlock.blk2.3.bias");
+    const int K2 = 9 * cout + (cin != cout ? cin : 0);
+    r.conv2 = {0, 0, cout, cout, 9, K2};
+    r.conv2.w = pk.reserve((int64_t)cout * K2);
+    pk.conv_at(w2, cout, cout, 9, K2, 0, r.conv2.w);
+    if (cin != cout) {
+      const float* ws = rd.take((int64_t)cout * cin, "ResBlock.shortcut.weight");
+      const float* bs = rd.take(cout, "ResBlock.shortcut.bias");
+      pk.conv_at(ws, cout, cin, 1, K2, 9 * cout, r.conv2.w);
+      r.conv2.bias = pk.reserve(cout);
+      pk.add_at(b2, bs, cout, r.conv2.bias);
+    } else {
+      r.conv2.bias = pk.raw(b2, cout);
+    }
+    m->res.push_back(r);
+    return (int)m->res.size() - 1;
+  };
+  auto attnblock = [&](int C, int heads) {
+    AttnP p;
+    p.C = C;
+    p.heads = heads;
+    p.gn = gn(C, "SelfAttentionBlock.norm");
+    p.wqkv = pk.reserve((int64_t)3 * C * C);
+    p.bqkv = pk.reserve(3 * C);
+    for (int i = 0; i < 3; ++i) {
+      const float* w = rd.take((int64_t)C * C, "SelfAttentionBlock.{q,k,v}.weight");
+      const float* b = rd.take(C, "SelfAttentionBlock.{q,k,v}.bias");
+      pk.raw_at(w, (int64_t)C * C, p.wqkv + (size_t)i * C * C);
+      pk.raw_at(b, C, p.bqkv + (size_t)i * C);
+    }
+    p.wproj = pk.raw(rd.take((int64_t)C * C, "SelfAttentionBlock.proj.weight"), (int64_t)C * C);
+    p.bproj = pk.raw(rd.take(C, "SelfAttentionBlock.proj.bias"), C);
+    m->attn.push_back(p);
+    return (int)m->attn.size() - 1;
+  };
+  auto sampleconv = [&](int C, const char* what) {
+    ConvP c{0, 0, C, C, 9, 9 * C};
+    const float* w = rd.take((int64_t)C * C * 9, what);
+    const float* b = rd.take(C, what);
+    c.w = pk.reserve((int64_t)C * 9 * C);
+    pk.conv_at(w, C, C, 9, 9 * C, 0, c.w);
+    c.bias = pk.raw(b, C);
+    m->convs.push_back(c);
+    return (int)m->convs.size() - 1;
+  };
+
+  // ---- down path (models/unet.py:77-90, forward :126-136)
+  int cur = D, level = 0, n_skips = 0;
+  std::vector<int> skip_stack;  // skip ids
+  auto push_skip = [&](int C, int lvl) {
+    m->skip_C.push_back(C);
+    m->skip_level.push_back(lvl);
+    skip_stack.push_back(n_skips);
+    return n_skips++;
+  };
+  const int s0 = push_skip(D, 0);  // first_conv output
+  (void)s0;
+  for (int i = 0; i < a.n_stages; ++i) {
+    const int out = D * a.dim_mults[i];
+    for (int j = 0; j < a.num_res_blocks; ++j) {
+      Node n{N_RES, resblock(cur, out), cur, out, 0, level, level};
+      m->nodes.push_back(n);
+      if (a.use_attn[i]) {
+        Node na{N_ATTN, attnblock(out, a.n_heads), out, out, 0, level, level};
+        m->nodes.push_back(na);
+      }
+      m->nodes.back().skip_producer = true;
+      m->nodes.back().skip_id = push_skip(out, level);
+      cur = out;
+    }
+    if (i < a.n_stages - 1) {
+      Node nd{N_DOWN, sampleconv(out, "Downsample"), out, out, 0, level, level + 1};
+      m->nodes.push_back(nd);
+      ++level;
+      m->nodes.back().skip_producer = true;
+      m->nodes.back().skip_id = push_skip(out, level);
+    }
+  }
+  m->n_levels = level + 1;
+  // ---- bottleneck (models/unet.py:93-97; attention with the default n_heads = 1)
+  m->nodes.push_back(Node{N_RES, resblock(cur, cur), cur, cur, 0, level, level});
+  m->nodes.push_back(Node{N_ATTN, attnblock(cur, 1), cur, cur, 0, level, level});
+  m->nodes.push_back(Node{N_RES, resblock(cur, cur), cur, cur, 0, level, level});
+  // ---- up path (models/unet.py:101-112, forward :142-149)
+  for (int i = a.n_stages - 1; i >= 0; --i) {
+    const int out = D * a.dim_mults[i];
+    for (int j = 0; j < a.num_res_blocks + 1; ++j) {
+      const int sid = skip_stack.back();
+      skip_stack.pop_back();
+      const int cin = cur + m->skip_C[sid];
+      Node n{N_RES, resblock(cin, out), cin, out, 0, level, level};
+      n.pops_skip = sid;
+      n.concat_cx = cur;
+      m->nodes.push_back(n);
+      if (a.use_attn[i]) m->nodes.push_back(Node{N_ATTN, attnblock(out, a.n_heads), out, out, 0, level, level});
+      cur = out;
+    }
+    if (i > 0) {
+      m->nodes.push_back(Node{N_UP, sampleconv(out, "Upsample"), out, out, 0, level, level - 1});
+      --level;
+    }
+  }
+  // ---- last conv (models/unet.py:115-119)
+  m->last_gn = gn(cur, "last_conv.0 (GroupNorm)");
+  m->last_w = pk.raw(rd.take((int64_t)a.out_channels * cur * 9, "last_conv.2.weight"), (int64_t)a.out_channels * cur * 9);
+  m->last_b = pk.raw(rd.take(a.out_channels, "last_conv.2.bias"), a.out_channels);
+  if (!rd.err.empty()) {
+    set_error(rd.err);
+    return DM_ERR_ARG;
+  }
+  DM_REQUIRE(rd.pos == n_params, "parameter count mismatch after walk");
+
+  // fused projection matrix [proj_total][TD]
+  m->proj_w = pk.reserve((int64_t)m->proj_total * TD);
+  m->proj_b = pk.reserve(m->proj_total);
+  {
+    int row = 0;
+    for (auto& p : projs) {
+      pk.raw_at(p.w, (int64_t)p.cout * TD, m->proj_w + (size_t)row * TD);
+      pk.raw_at(p.b, p.cout, m->proj_b + row);
+      row += p.cout;
+    }
+  }
+
+  // allocate + run the pack jobs
+  m->arena_floats = pk.size;
+  DM_CHECK_HIP(hipMalloc(&m->arena, pk.size * sizeof(float)));
+  for (auto& j : pk.jobs) {
+    if (!j.src) {
+      set_error("null parameter pointer");
+      return DM_ERR_ARG;
+    }
+    if (j.kind == 0) {
+      DM_CHECK_HIP(hipMemcpyAsync(m->arena + j.dst, j.src, j.n * sizeof(float), hipMemcpyDeviceToDevice, st));
+    } else if (j.kind == 1) {
+      rc = repack_conv(j.src, j.Cout, j.Cin, j.taps, m->arena + j.dst, j.ldw, j.col0, st);
+      if (rc) return rc;
+    } else {
+      hipLaunchKernelGGL(vec_add_kernel, dim3((unsigned)((j.n + 255) / 256)), dim3(256), 0, st, j.src, j.src2,
+                         m->arena + j.dst, j.n);
+      DM_LAUNCH_CHECK();
+    }
+  }
+  *out = m.release();
+  return DM_OK;
+}
+
+// ---------------------------------------------------------------------------
+// plan (per batch size / resolution)
+// ---------------------------------------------------------------------------
+int UNetModel::build_plan(int B, int H, int W) {
+  if (plan) free_plan(plan.get());
+  plan = std::make_unique<Plan>();
+  Plan& pl = *plan;
+  pl.B = B;
+  pl.H = H;
+  pl.W = W;
+  DM_REQUIRE(H % (1 << (n_levels - 1)) == 0 && W % (1 << (n_levels - 1)) == 0,
+             "image size must be divisible by 2^(n_stages-1)");
+  bool alloc_failed = false;
+  auto alloc = [&](size_t bytes) -> float* {
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes ? bytes : 16) != hipSuccess) {
+      alloc_failed = true;
+      return nullptr;
+    }
+    pl.allocs.push_back(p);
+    pl.bytes += bytes;
+    return (float*)p;
+  };
+  auto Hl = [&](int lvl) { return H >> lvl; };
+  auto Wl = [&](int lvl) { return W >> lvl; };
+  const int D = arch.dim, TD = 4 * arch.dim, G = 32;
+
+  // --- temb workspace
+  float* e0 = alloc((size_t)B * D * 4);
+  float* e1 = alloc((size_t)B * TD * 4);
+  float* se = alloc((size_t)B * TD * 4);
+  float* projs = alloc((size_t)B * proj_total * 4);
+
+  // --- scratch sizes
+  size_t max_a1 = 0, max_h = 0, max_attn = 0, max_qkv = 0, max_S = 0;
+  int max_chunks = 1;
+  for (auto& n : nodes) {
+    const size_t hw = (size_t)Hl(n.level_in) * Wl(n.level_in);
+    max_chunks = std::max(max_chunks, gn_num_chunks((int)hw));
+    if (n.kind == N_RES) {
+      max_a1 = std::max(max_a1, (size_t)B * hw * n.cin);
+      max_h = std::max(max_h, (size_t)B * hw * n.cout);
+    } else if (n.kind == N_ATTN) {
+      max_attn = std::max(max_attn, (size_t)B * hw * n.cin);
+      max_qkv = std::max(max_qkv, (size_t)B * hw * 3 * n.cin);
+      const int heads = attn[n.idx].heads;
+      max_S = std::max(max_S, (size_t)B * heads * hw * hw);
+    }
+  }
+  max_chunks = std::max(max_chunks, gn_num_chunks(H * W));
+  float* a1 = alloc(std::max(max_a1, (size_t)B * H * W * D) * 4);
+  float* hbuf = alloc(max_h * 4);
+  float* a2 = alloc(max_h * 4);
+  float* an = alloc(std::max<size_t>(max_attn, 1) * 4);
+  float* qkv = alloc(std::max<size_t>(max_qkv, 1) * 4);
+  float* Sb = alloc(std::max<size_t>(max_S, 1) * 4);
+  float* Ob = alloc(std::max<size_t>(max_attn, 1) * 4);
+  double2* part = (double2*)alloc((size_t)B * max_chunks * G * sizeof(double2));
+
+  // --- concat buffers for up-RBs and skip slot views
+  std::vector<View> skip_view(skip_C.size());
+  std::vector<View> concat_x(nodes.size());
+  for (size_t i = 0; i < nodes.size(); ++i) {
+    const Node& n = nodes[i];
+    if (n.kind == N_RES && n.pops_skip >= 0) {
+      const int lvl = n.level_in;
+      float* buf = alloc((size_t)B * Hl(lvl) * Wl(lvl) * n.cin * 4);
+      concat_x[i] = View{buf, B, Hl(lvl), Wl(lvl), n.concat_cx, n.cin};
+      skip_view[n.pops_skip] = View{buf + n.concat_cx, B, Hl(lvl), Wl(lvl), skip_C[n.pops_skip], n.cin};
+    }
+  }
+  if (alloc_failed) { set_error("workspace allocation failed"); return DM_ERR_HIP; }
+
+  auto& ops = pl.ops;
+  auto add = [&](std::string label, double flops, double bytes, std::function<int(hipStream_t)> fn) {
+    ops.push_back(Op{std::move(label), flops, bytes, std::move(fn)});
+  };
+  auto conv_cost = [](const ConvArgs& c, double& fl, double& by) {
+    const double M = (double)c.B * c.Hout * c.Wout;
+    fl = 2.0 * M * c.Cout * c.K;
+    by = 4.0 * ((double)c.B * c.Hin * c.Win * c.Cin1 + M * c.Cin2 + (double)c.Cout * c.K + M * c.Cout +
+                (c.res ? M * c.Cout : 0.0));
+  };
+  auto gemm_cost = [](const GemmArgs& g, double& fl, double& by) {
+    const double Z = (double)g.Z1 * g.Z2;
+    fl = 2.0 * Z * g.M * g.N * g.K;
+    by = 4.0 * Z * ((double)g.M * g.K + (double)g.N * g.K + (double)g.M * g.N) + (g.res ? 4.0 * g.M * g.N : 0.0);
+  };
+  auto add_conv = [&](const ConvArgs& c) {
+    double fl, by;
+    conv_cost(c, fl, by);
+    add(conv_label(c), fl, by, [=](hipStream_t st) { return conv2d_igemm(c, st); });
+  };
+  auto add_gemm = [&](const GemmArgs& g) {
+    double fl, by;
+    gemm_cost(g, fl, by);
+    add(gemm_label(g), fl, by, [=](hipStream_t st) { return gemm_batched(g, st); });
+  };
+  auto gn_bytes = [](const View& v, bool apply) {
+    const double n = (double)v.B * v.H * v.W * v.C;
+    return apply ? 8.0 * n : 4.0 * n;
+  };
+  Plan* P_ = &pl;
+  UNetModel* self = this;
+
+  // temb
+  add("timestep_embed", 0, 4.0 * B * D, [=](hipStream_t st) {
+    return timestep_embed(P_->t, B, D, 0, self->te_freqs_set ? self->P(self->te_freqs) : nullptr, e0, st);
+  });
+  {
+    GemmArgs g{};
+    g.M = B; g.N = TD; g.K = D; g.Z1 = 1; g.Z2 = 1;
+    g.A = e0; g.lda = D; g.Bm = P(te_w1); g.ldb = D; g.C = e1; g.ldc = TD; g.alpha = 1.f;
+    g.bias = P(te_b1); g.act = 1;
+    add_gemm(g);
+    GemmArgs g2 = g;
+    g2.K = TD; g2.A = e1; g2.lda = TD; g2.Bm = P(te_w2); g2.ldb = TD; g2.C = se; g2.bias = P(te_b2);
+    g2.act = 1;  // only SiLU(temb) is ever consumed (ResBlock.proj = SiLU -> Linear)
+    add_gemm(g2);
+    GemmArgs g3 = g;
+    g3.N = proj_total; g3.K = TD; g3.A = se; g3.lda = TD; g3.Bm = P(proj_w); g3.ldb = TD; g3.C = projs;
+    g3.ldc = proj_total; g3.bias = P(proj_b); g3.act = 0;
+    add_gemm(g3);
+  }
+
+  // output view of node i (and of first_conv, i = -1)
+  auto out_view_for = [&](int i, int C, int lvl) -> View {
+    if (i >= 0 && nodes[i].skip_producer) return skip_view[nodes[i].skip_id];
+    const int nx = i + 1;
+    if (nx < (int)nodes.size() && nodes[nx].kind == N_RES && nodes[nx].pops_skip >= 0) return concat_x[nx];
+    float* buf = alloc((size_t)B * Hl(lvl) * Wl(lvl) * C * 4);
+    return View{buf, B, Hl(lvl), Wl(lvl), C, C};
+  };
+
+  // first conv -> skip 0
+  View x_cur = skip_view[0];
+  {
+    View y = x_cur;
+    const float* w = P(first_w);
+    const float* bb = P(first_b);
+    const int cin = arch.in_channels;
+    add("conv3x3_small_in", 2.0 * B * H * W * D * 9 * cin, 4.0 * B * H * W * (cin + D),
+        [=](hipStream_t st) { return conv3x3_small_in(P_->x, B, cin, H, W, w, bb, D, y, st); });
+  }
+
+  for (size_t i = 0; i < nodes.size(); ++i) {
+    const Node& n = nodes[i];
+    View xin = (n.kind == N_RES && n.pops_skip >= 0)
+                   ? View{concat_x[i].p, B, concat_x[i].H, concat_x[i].W, n.cin, n.cin}
+                   : x_cur;
+    View y = out_view_for((int)i, n.cout, n.level_out);
+    if (!y.p || alloc_failed) { set_error("workspace allocation failed"); return DM_ERR_HIP; }
+    const int Hi = Hl(n.level_in), Wi = Wl(n.level_in);
+    const int hw = Hi * Wi;
+    const int nchunk = gn_num_chunks(hw);
+    if (n.kind == N_RES) {
+      const ResBlockP r = res[n.idx];
+      View va1{a1, B, Hi, Wi, r.cin, r.cin};
+      View vh{hbuf, B, Hi, Wi, r.cout, r.cout};
+      View va2{a2, B, Hi, Wi, r.cout, r.cout};
+      add("gn_partial", 0, gn_bytes(xin, false), [=](hipStream_t st) { return gn_partial(xin, G, part, st); });
+      add("gn_apply", 0, gn_bytes(xin, true), [=](hipStream_t st) {
+        return gn_apply(xin, G, part, nchunk, 1e-5f, self->P(r.gn1.g), self->P(r.gn1.b), nullptr, nullptr, 0, 1,
+                        va1, st);
+      });
+      ConvArgs c1{};
+      c1.x1 = a1; c1.x1_pitch = r.cin; c1.Cin1 = r.cin; c1.Hin = Hi; c1.Win = Wi;
+      c1.taps = 9; c1.stride = 1; c1.upsample = 0;
+      c1.w = P(r.conv1.w); c1.K = r.conv1.K;
+      c1.y = hbuf; c1.y_pitch = r.cout; c1.Cout = r.cout; c1.B = B; c1.Hout = Hi; c1.Wout = Wi;
+      c1.bias = P(r.conv1.bias); c1.rowvec = projs + r.proj_col; c1.rowvec_pitch = proj_total;
+      add_conv(c1);
+      add("gn_partial", 0, gn_bytes(vh, false), [=](hipStream_t st) { return gn_partial(vh, G, part, st); });
+      add("gn_apply", 0, gn_bytes(vh, true), [=](hipStream_t st) {
+        return gn_apply(vh, G, part, nchunk, 1e-5f, self->P(r.gn2.g), self->P(r.gn2.b), nullptr, nullptr, 0, 1,
+                        va2, st);
+      });
+      ConvArgs c2{};
+      c2.x1 = a2; c2.x1_pitch = r.cout; c2.Cin1 = r.cout; c2.Hin = Hi; c2.Win = Wi;
+      c2.taps = 9; c2.stride = 1;
+      c2.w = P(r.conv2.w); c2.K = r.conv2.K;
+      c2.y = y.p; c2.y_pitch = y.pitch; c2.Cout = r.cout; c2.B = B; c2.Hout = Hi; c2.Wout = Wi;
+      c2.bias = P(r.conv2.bias);
+      if (r.cin != r.cout) {
+        c2.x2 = xin.p; c2.x2_pitch = xin.pitch; c2.Cin2 = r.cin;
+      } else {
+        c2.res = xin.p; c2.res_pitch = xin.pitch;
+      }
+      add_conv(c2);
+    } else if (n.kind == N_ATTN) {
+      const AttnP p = attn[n.idx];
+      const int C = p.C, heads = p.heads, Dh = C / heads;
+      View van{an, B, Hi, Wi, C, C};
+      add("gn_partial", 0, gn_bytes(xin, false), [=](hipStream_t st) { return gn_partial(xin, G, part, st); });
+      add("gn_apply", 0, gn_bytes(xin, true), [=](hipStream_t st) {
+        return gn_apply(xin, G, part, nchunk, 1e-5f, self->P(p.gn.g), self->P(p.gn.b), nullptr, nullptr, 0, 0,
+                        van, st);
+      });
+      GemmArgs gq{};
+      gq.M = B * hw; gq.N = 3 * C; gq.K = C; gq.Z1 = 1; gq.Z2 = 1;
+      gq.A = an; gq.lda = C; gq.Bm = P(p.wqkv); gq.ldb = C; gq.C = qkv; gq.ldc = 3 * C;
+      gq.alpha = 1.f; gq.bias = P(p.bqkv);
+      add_gemm(gq);
+      GemmArgs gs{};
+      gs.M = hw; gs.N = hw; gs.K = Dh; gs.Z1 = B; gs.Z2 = heads;
+      gs.A = qkv; gs.a_s1 = (long)hw * 3 * C; gs.a_s2 = Dh; gs.lda = 3 * C;
+      gs.Bm = qkv + C; gs.b_s1 = (long)hw * 3 * C; gs.b_s2 = Dh; gs.ldb = 3 * C;
+      gs.C = Sb; gs.c_s1 = (long)heads * hw * hw; gs.c_s2 = (long)hw * hw; gs.ldc = hw;
+      gs.alpha = (float)std::pow((double)Dh, -0.5);
+      add_gemm(gs);
+      const long rows = (long)B * heads * hw;
+      add("softmax_rows", 0, 8.0 * rows * hw, [=](hipStream_t st) { return softmax_rows(Sb, rows, hw, hw, st); });
+      GemmArgs go{};
+      go.M = hw; go.N = Dh; go.K = hw; go.Z1 = B; go.Z2 = heads;
+      go.A = Sb; go.a_s1 = (long)heads * hw * hw; go.a_s2 = (long)hw * hw; go.lda = hw;
+      go.Bm = qkv + 2 * C; go.b_s1 = (long)hw * 3 * C; go.b_s2 = Dh; go.ldb = 3 * C; go.b_kn = 1;
+      go.C = Ob; go.c_s1 = (long)hw * C; go.c_s2 = Dh; go.ldc = C;
+      go.alpha = 1.f;
+      add_gemm(go);
+      GemmArgs gp{};
+      gp.M = B * hw; gp.N = C; gp.K = C; gp.Z1 = 1; gp.Z2 = 1;
+      gp.A = Ob; gp.lda = C; gp.Bm = P(p.wproj); gp.ldb = C; gp.C = y.p; gp.ldc = y.pitch;
+      gp.alpha = 1.f; gp.bias = P(p.bproj); gp.res = xin.p; gp.ld_res = xin.pitch;
+      add_gemm(gp);
+    } else {
+      const ConvP cv = convs[n.idx];
+      ConvArgs c{};
+      c.x1 = xin.p; c.x1_pitch = xin.pitch; c.Cin1 = n.cin; c.Hin = Hi; c.Win = Wi;
+      c.taps = 9; c.stride = n.kind == N_DOWN ? 2 : 1; c.upsample = n.kind == N_UP;
+      c.w = P(cv.w); c.K = cv.K;
+      c.y = y.p; c.y_pitch = y.pitch; c.Cout = n.cout; c.B = B;
+      c.Hout = Hl(n.level_out); c.Wout = Wl(n.level_out);
+      c.bias = P(cv.bias);
+      add_conv(c);
+    }
+    x_cur = y;
+  }
+  // last conv: GN -> SiLU -> conv(cur -> out_channels), NCHW output
+  {
+    const int C = x_cur.C;
+    View xin = x_cur;
+    View va{a1, B, H, W, C, C};
+    const int nchunk = gn_num_chunks(H * W);
+    const GnP lg = last_gn;
+    const float* lw = P(last_w);
+    const float* lb = P(last_b);
+    const int oc = arch.out_channels;
+    add("gn_partial", 0, gn_bytes(xin, false), [=](hipStream_t st) { return gn_partial(xin, G, part, st); });
+    add("gn_apply", 0, gn_bytes(xin, true), [=](hipStream_t st) {
+      return gn_apply(xin, G, part, nchunk, 1e-5f, self->P(lg.g), self->P(lg.b), nullptr, nullptr, 0, 1, va, st);
+    });
+    add("conv3x3_small_out", 2.0 * B * H * W * oc * 9 * C, 4.0 * B * H * W * (C + oc),
+        [=](hipStream_t st) { return conv3x3_small_out(va, lw, lb, oc, P_->out, st); });
+  }
+  return DM_OK;
+}
+
+}  // namespace dm
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+struct dm_unet {
+  dm::UNetModel* m;
+};
+
+extern "C" int dm_unet_param_count(const dm_unet_arch* arch, int* n_params) {
+  int rc = dm::validate_arch(arch);
+  if (rc) return rc;
+  if (!n_params) { dm::set_error("n_params is null"); return DM_ERR_ARG; }
+  *n_params = dm::count_params(*arch);
+  return DM_OK;
+}
+
+extern "C" int dm_unet_create(const dm_unet_arch* arch, const float* const* params, const int64_t* numels,
+                              int n_params, void* stream, dm_unet** out) {
+  if (!out || !params || !numels) { dm::set_error("null argument"); return DM_ERR_ARG; }
+  dm::UNetModel* m = nullptr;
+  int rc = dm::unet_create(arch, params, numels, n_params, (hipStream_t)stream, &m);
+  if (rc) return rc;
+  *out = new dm_unet{m};
+  return DM_OK;
+}
+
+extern "C" int dm_unet_forward(dm_unet* h, const float* x, const int64_t* t, int B, int H, int W, float* out,
+                               void* stream) {
+  if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
+  if (!x || !t || !out) { dm::set_error("null tensor"); return DM_ERR_ARG; }
+  if (B <= 0 || H <= 0 || W <= 0) { dm::set_error("empty batch or image"); return DM_ERR_ARG; }
+  dm::UNetModel* m = h->m;
+  if (!m->plan || m->plan->B != B || m->plan->H != H || m->plan->W != W) {
+    int rc = m->build_plan(B, H, W);
+    if (rc) {
+      m->plan.reset();
+      return rc;
+    }
+  }
+  m->plan->x = x;
+  m->plan->t = t;
+  m->plan->out = out;
+  hipStream_t st = (hipStream_t)stream;
+  auto& pl = *m->plan;
+  for (size_t i = 0; i < pl.ops.size(); ++i) {
+    if (pl.profiling) {
+      hipEvent_t a, b;
+      DM_CHECK_HIP(hipEventCreate(&a));
+      DM_CHECK_HIP(hipEventCreate(&b));
+      DM_CHECK_HIP(hipEventRecord(a, st));
+      int rc = pl.ops[i].fn(st);
+      if (rc) return rc;
+      DM_CHECK_HIP(hipEventRecord(b, st));
+      pl.pending.push_back({(int)i, {a, b}});
+    } else {
+      int rc = pl.ops[i].fn(st);
+      if (rc) return rc;
+    }
+  }
+  return DM_OK;
+}
+
+extern "C" int dm_unet_memory(const dm_unet* h, int64_t* weight_bytes, int64_t* workspace_bytes) {
+  if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
+  if (weight_bytes) *weight_bytes = (int64_t)(h->m->arena_floats * sizeof(float));
+  if (workspace_bytes) *workspace_bytes = h->m->plan ? (int64_t)h->m->plan->bytes : 0;
+  return DM_OK;
+}
+
+extern "C" int dm_unet_set_time_freqs(dm_unet* h, const float* freqs, int n, void* stream) {
+  if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
+  if (!freqs) {
+    h->m->te_freqs_set = false;
+    return DM_OK;
+  }
+  if (n != h->m->arch.dim / 2) { dm::set_error("time frequency table must have dim/2 entries"); return DM_ERR_ARG; }
+  DM_CHECK_HIP(hipMemcpyAsync(h->m->P(h->m->te_freqs), freqs, (size_t)n * sizeof(float), hipMemcpyDefault,
+                              (hipStream_t)stream));
+  h->m->te_freqs_set = true;
+  return DM_OK;
+}
+
+extern "C" int dm_unet_profile(dm_unet* h, int enable) {
+  if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
+  if (!h->m->plan) { dm::set_error("no plan yet: run dm_unet_forward once first"); return DM_ERR_STATE; }
+  auto& pl = *h->m->plan;
+  dm::drain_profile(&pl);
+  pl.profiling = enable != 0;
+  pl.prof_ms.assign(pl.ops.size(), 0.0);
+  pl.prof_launches.assign(pl.ops.size(), 0);
+  return DM_OK;
+}
+
+extern "C" int dm_unet_profile_count(dm_unet* h, int* n_ops) {
+  if (!h || !h->m || !h->m->plan || !n_ops) { dm::set_error("null model / no plan"); return DM_ERR_STATE; }
+  *n_ops = (int)h->m->plan->ops.size();
+  return DM_OK;
+}
+
+extern "C" int dm_unet_profile_get(dm_unet* h, int i, char* label, int label_len, double* flops, double* bytes,
+                                   double* ms_total, int64_t* launches) {
+  if (!h || !h->m || !h->m->plan) { dm::set_error("null model / no plan"); return DM_ERR_STATE; }
+  auto& pl = *h->m->plan;
+  if (i < 0 || i >= (int)pl.ops.size()) { dm::set_error("op index out of range"); return DM_ERR_ARG; }
+  dm::drain_profile(&pl);
+  if (pl.prof_ms.size() != pl.ops.size()) {
+    pl.prof_ms.assign(pl.ops.size(), 0.0);
+    pl.prof_launches.assign(pl.ops.size(), 0);
+  }
+  if (label && label_len > 0) {
+    std::snprintf(label, (size_t)label_len, "%s", pl.ops[i].label.c_str());
+  }
+  if (flops) *flops = pl.ops[i].flops;
+  if (bytes) *bytes = pl.ops[i].bytes;
+  if (ms_total) *ms_total = pl.prof_ms[i];
+  if (launches) *launches = pl.prof_launches[i];
+  return DM_OK;
+}
+
+extern "C" void dm_unet_destroy(dm_unet* h) {
+  if (!h) return;
+  (void)hipDeviceSynchronize();
+  delete h->m;
+  delete h;
+}

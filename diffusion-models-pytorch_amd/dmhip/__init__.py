@@ -1,0 +1,27 @@
+"""ctypes binding of the dm_hip C ABI (include/dm_hip.h).
+
+The product path has no CPU fallback: every entry point requires the native
+library and ROCm device tensors, and raises loudly otherwise.
+"""
+from dmhip._lib import (  # noqa: F401
+    DMError,
+    lib,
+    lib_path,
+    load,
+    exported_symbols,
+    require_device_tensor,
+    stream_handle,
+    StepDesc,
+    ConvDesc,
+    GemmDesc,
+    UNetArch,
+    sampler_step,
+    groupnorm_nhwc,
+    conv2d_nhwc,
+    pack_conv_weight,
+    gemm,
+    softmax_rows,
+    timestep_embedding,
+    unet_profile_enable,
+    unet_profile_read,
+)

@@ -1,0 +1,238 @@
+"""Loader and thin wrappers for libdm_hip.so.
+
+Tensors cross the boundary as raw device pointers (``tensor.data_ptr()``);
+torch-ROCm is used only for allocation and for the current HIP stream.
+"""
+import ctypes
+import os
+import re
+from typing import Optional
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+lib_path = os.path.join(_HERE, 'libdm_hip.so')
+_HEADER = os.path.join(os.path.dirname(os.path.dirname(_HERE)), 'include', 'dm_hip.h')
+
+DM_OK = 0
+DM_ERR_ARG = -1
+DM_ERR_HIP = -2
+DM_ERR_STATE = -3
+DM_ERR_UNSUPPORTED = -4
+DM_MAX_STAGES = 8
+
+
+class DMError(RuntimeError):
+    """A failure reported by the native library (HIP error, bad state)."""
+
+
+c_float_p = ctypes.POINTER(ctypes.c_float)
+vp = ctypes.c_void_p
+
+
+class UNetArch(ctypes.Structure):
+    _fields_ = [
+        ('in_channels', ctypes.c_int),
+        ('out_channels', ctypes.c_int),
+        ('dim', ctypes.c_int),
+        ('n_stages', ctypes.c_int),
+        ('dim_mults', ctypes.c_int * DM_MAX_STAGES),
+        ('use_attn', ctypes.c_int * DM_MAX_STAGES),
+        ('num_res_blocks', ctypes.c_int),
+        ('n_heads', ctypes.c_int),
+    ]
+
+
+class StepDesc(ctypes.Structure):
+    _fields_ = [
+        ('B', ctypes.c_int), ('C', ctypes.c_int), ('HW', ctypes.c_int), ('Cm', ctypes.c_int),
+        ('xt', vp), ('model_out', vp), ('model_out_uncond', vp),
+        ('w_uncond', ctypes.c_float), ('w_cond', ctypes.c_float),
+        ('objective', ctypes.c_int), ('clip_denoised', ctypes.c_int),
+        ('sqrt_recip_ac', ctypes.c_float), ('sqrt_recipm1_ac', ctypes.c_float),
+        ('sqrt_ac', ctypes.c_float), ('sqrt_one_minus_ac', ctypes.c_float),
+        ('kind', ctypes.c_int),
+        ('coef1', ctypes.c_float), ('coef2', ctypes.c_float),
+        ('var_mode', ctypes.c_int), ('std', ctypes.c_float),
+        ('min_logvar', ctypes.c_float), ('max_logvar', ctypes.c_float),
+        ('add_noise', ctypes.c_int), ('noise', vp),
+        ('sample', vp), ('mean', vp), ('pred_x0', vp), ('pred_eps', vp), ('var', vp),
+    ]
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [
+        ('x', vp), ('x_pitch', ctypes.c_int), ('Cin', ctypes.c_int), ('Hin', ctypes.c_int), ('Win', ctypes.c_int),
+        ('taps', ctypes.c_int), ('stride', ctypes.c_int), ('upsample', ctypes.c_int),
+        ('x2', vp), ('x2_pitch', ctypes.c_int), ('Cin2', ctypes.c_int),
+        ('w', vp), ('K', ctypes.c_int),
+        ('y', vp), ('y_pitch', ctypes.c_int), ('Cout', ctypes.c_int), ('B', ctypes.c_int),
+        ('Hout', ctypes.c_int), ('Wout', ctypes.c_int),
+        ('bias', vp), ('rowvec', vp), ('rowvec_pitch', ctypes.c_int),
+        ('res', vp), ('res_pitch', ctypes.c_int),
+    ]
+
+
+class GemmDesc(ctypes.Structure):
+    _fields_ = [
+        ('M', ctypes.c_int), ('N', ctypes.c_int), ('K', ctypes.c_int), ('Z1', ctypes.c_int), ('Z2', ctypes.c_int),
+        ('A', vp), ('a_s1', ctypes.c_int64), ('a_s2', ctypes.c_int64), ('lda', ctypes.c_int),
+        ('B', vp), ('b_s1', ctypes.c_int64), ('b_s2', ctypes.c_int64), ('ldb', ctypes.c_int), ('b_kn', ctypes.c_int),
+        ('C', vp), ('c_s1', ctypes.c_int64), ('c_s2', ctypes.c_int64), ('ldc', ctypes.c_int),
+        ('alpha', ctypes.c_float),
+        ('bias', vp),
+        ('res', vp), ('ld_res', ctypes.c_int),
+        ('act', ctypes.c_int),
+    ]
+
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def _declare(L: ctypes.CDLL):
+    L.dm_abi_version.restype = ctypes.c_int
+    L.dm_last_error.restype = ctypes.c_char_p
+    L.dm_unet_param_count.argtypes = [ctypes.POINTER(UNetArch), ctypes.POINTER(ctypes.c_int)]
+    L.dm_unet_create.argtypes = [ctypes.POINTER(UNetArch), ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_int64),
+                                 ctypes.c_int, vp, ctypes.POINTER(vp)]
+    L.dm_unet_forward.argtypes = [vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp]
+    L.dm_unet_profile.argtypes = [vp, ctypes.c_int]
+    L.dm_unet_profile_count.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
+    L.dm_unet_profile_get.argtypes = [vp, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
+                                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]
+    L.dm_unet_memory.argtypes = [vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
+    L.dm_unet_destroy.argtypes = [vp]
+    L.dm_unet_destroy.restype = None
+    L.dm_sampler_step.argtypes = [ctypes.POINTER(StepDesc), vp]
+    L.dm_groupnorm_scratch_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    L.dm_groupnorm_scratch_bytes.restype = ctypes.c_int64
+    L.dm_groupnorm_nhwc.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_int, ctypes.c_float, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, vp, vp]
+    L.dm_pack_conv_weight.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int,
+                                      vp]
+    L.dm_conv2d_nhwc.argtypes = [ctypes.POINTER(ConvDesc), vp]
+    L.dm_gemm.argtypes = [ctypes.POINTER(GemmDesc), vp]
+    L.dm_softmax_rows.argtypes = [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, vp]
+    L.dm_timestep_embedding.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp, vp]
+    L.dm_unet_set_time_freqs.argtypes = [vp, vp, ctypes.c_int, vp]
+
+
+def load() -> ctypes.CDLL:
+    """Load libdm_hip.so (built in-tree by __graft_entry__.build()). Raises if absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(lib_path):
+            raise DMError(
+                f'dm_hip native library not found at {lib_path}; build it with '
+                f'`python -c "import __graft_entry__ as g; g.build()"` (no CPU fallback exists)')
+        L = ctypes.CDLL(lib_path)
+        _declare(L)
+        if L.dm_abi_version() != 1:
+            raise DMError(f'dm_hip ABI mismatch: library reports {L.dm_abi_version()}, binding expects 1')
+        _lib = L
+    return _lib
+
+
+def lib() -> ctypes.CDLL:
+    return load()
+
+
+def exported_symbols():
+    """Function names declared in include/dm_hip.h."""
+    with open(_HEADER) as f:
+        text = f.read()
+    text = re.sub(r'/\*.*?\*/', '', text, flags=re.S)
+    names = re.findall(r'\b(dm_[a-z0-9_]+)\s*\(', text)
+    return sorted(set(names))
+
+
+def check(rc: int, what: str = 'dm_hip call'):
+    if rc == DM_OK:
+        return
+    msg = load().dm_last_error()
+    msg = msg.decode() if msg else ''
+    if rc == DM_ERR_ARG:
+        raise ValueError(f'{what}: {msg}')
+    raise DMError(f'{what} failed ({rc}): {msg}')
+
+
+def require_device_tensor(t: torch.Tensor, name: str, dtype=torch.float32):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f'{name} must be a torch.Tensor')
+    if t.device.type != 'cuda':
+        raise RuntimeError(
+            f'dm_hip: {name} is on {t.device}; the MI355X engine runs only on ROCm device tensors '
+            f'(there is no CPU fallback)')
+    if t.dtype != dtype:
+        raise TypeError(f'dm_hip: {name} must be {dtype}, got {t.dtype}')
+    if not t.is_contiguous():
+        raise ValueError(f'dm_hip: {name} must be contiguous')
+
+
+def stream_handle(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+# --------------------------------------------------------------------------- ops
+def sampler_step(desc: StepDesc, device=None):
+    check(load().dm_sampler_step(ctypes.byref(desc), stream_handle(device)), 'dm_sampler_step')
+
+
+def groupnorm_nhwc(x: torch.Tensor, y: torch.Tensor, B: int, HW: int, C: int, G: int, eps: float,
+                   gamma=None, beta=None, mod_scale=None, mod_shift=None, mod_pitch: int = 0, silu: bool = False,
+                   x_pitch: int = None, y_pitch: int = None):
+    L = load()
+    nbytes = L.dm_groupnorm_scratch_bytes(B, HW, G)
+    scratch = torch.empty(max(1, nbytes), dtype=torch.uint8, device=x.device)
+    check(L.dm_groupnorm_nhwc(x.data_ptr(), x_pitch or C, y.data_ptr(), y_pitch or C, B, HW, C, G, eps,
+                              _p(gamma), _p(beta), _p(mod_scale), _p(mod_shift), mod_pitch, int(silu),
+                              scratch.data_ptr(), stream_handle(x.device)), 'dm_groupnorm_nhwc')
+
+
+def pack_conv_weight(w: torch.Tensor, out: torch.Tensor, ldw: int, col0: int = 0):
+    Cout, Cin, kh, kw = w.shape
+    check(load().dm_pack_conv_weight(w.data_ptr(), Cout, Cin, kh * kw, out.data_ptr(), ldw, col0,
+                                     stream_handle(w.device)), 'dm_pack_conv_weight')
+
+
+def conv2d_nhwc(desc: ConvDesc, device=None):
+    check(load().dm_conv2d_nhwc(ctypes.byref(desc), stream_handle(device)), 'dm_conv2d_nhwc')
+
+
+def gemm(desc: GemmDesc, device=None):
+    check(load().dm_gemm(ctypes.byref(desc), stream_handle(device)), 'dm_gemm')
+
+
+def softmax_rows(x: torch.Tensor, rows: int, L: int, ld: int):
+    check(load().dm_softmax_rows(x.data_ptr(), rows, L, ld, stream_handle(x.device)), 'dm_softmax_rows')
+
+
+def timestep_embedding(t: torch.Tensor, dim: int, kind: int, out: torch.Tensor, freqs: torch.Tensor = None):
+    check(load().dm_timestep_embedding(t.data_ptr(), t.shape[0], dim, kind, _p(freqs), out.data_ptr(),
+                                       stream_handle(t.device)), 'dm_timestep_embedding')
+
+
+def unet_profile_enable(handle, enable: bool):
+    check(load().dm_unet_profile(handle, int(enable)), 'dm_unet_profile')
+
+
+def unet_profile_read(handle):
+    """List of dicts (label, flops, bytes, ms_total, launches) for every op of the cached plan."""
+    L = load()
+    n = ctypes.c_int()
+    check(L.dm_unet_profile_count(handle, ctypes.byref(n)), 'dm_unet_profile_count')
+    out = []
+    buf = ctypes.create_string_buffer(128)
+    fl, by, ms = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+    nl = ctypes.c_int64()
+    for i in range(n.value):
+        check(L.dm_unet_profile_get(handle, i, buf, 128, ctypes.byref(fl), ctypes.byref(by), ctypes.byref(ms),
+                                    ctypes.byref(nl)), 'dm_unet_profile_get')
+        out.append(dict(label=buf.value.decode(), flops=fl.value, bytes=by.value, ms_total=ms.value,
+                        launches=nl.value))
+    return out

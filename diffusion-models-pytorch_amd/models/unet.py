@@ -1,0 +1,211 @@
+"""DDPM UNet denoiser (CIFAR-10 / MNIST / CelebA configs) on the MI355X engine.
+
+Drop-in for the reference models/unet.py:46-152:
+  * same constructor (in_channels, out_channels, dim, dim_mults, use_attn,
+    num_res_blocks, n_heads, dropout) and the same parameter names/shapes, so
+    reference YAML configs and checkpoints load unchanged
+    (e.g. ``down_blocks.1.1.q.weight [256,256,1,1]``, 328 tensors for CIFAR-10);
+  * ``forward(X [B,C,H,W] f32, T [B] int64) -> [B, out_channels, H, W] f32``.
+
+The torch modules below are parameter containers only. ``forward`` hands the
+parameters to the native executor (dm_unet_create packs them once into the
+library's own layout) and runs the whole network as one C-ABI call
+(dm_unet_forward): NHWC activations, fp32 MFMA implicit-GEMM convolutions,
+fused GroupNorm+SiLU, zero-copy skip concatenation. Inference only
+(Dropout = identity, i.e. the reference in eval mode). No CPU fallback.
+"""
+import ctypes
+import math
+from typing import List, Sequence
+
+import torch
+import torch.nn as nn
+from torch import Tensor
+
+import dmhip
+from dmhip._lib import UNetArch, check, load, stream_handle
+
+
+def _gn(C: int) -> nn.GroupNorm:
+    return nn.GroupNorm(32, C)
+
+
+def _conv(cin: int, cout: int, k: int, stride: int = 1) -> nn.Conv2d:
+    return nn.Conv2d(cin, cout, k, stride=stride, padding=k // 2)
+
+
+class ResBlock(nn.Module):
+    """Parameter container of models/unet.py:10-43 (GN-SiLU-conv, temb add, GN-SiLU-conv, shortcut)."""
+
+    def __init__(self, in_channels: int, out_channels: int, embed_dim: int, dropout: float = 0.1):
+        super().__init__()
+        # Sequential indices reproduce the reference state_dict names:
+        # blk1.{0: GroupNorm, 2: Conv}, proj.1: Linear, blk2.{0: GroupNorm, 3: Conv}
+        self.blk1 = nn.Sequential(_gn(in_channels), nn.SiLU(), _conv(in_channels, out_channels, 3))
+        self.proj = nn.Sequential(nn.SiLU(), nn.Linear(embed_dim, out_channels))
+        self.blk2 = nn.Sequential(_gn(out_channels), nn.SiLU(), nn.Dropout(dropout),
+                                  _conv(out_channels, out_channels, 3))
+        self.shortcut = _conv(in_channels, out_channels, 1) if in_channels != out_channels else nn.Identity()
+
+
+class SelfAttentionBlock(nn.Module):
+    """Parameter container of models/modules.py:77-102 (GN, q/k/v/proj 1x1 convs)."""
+
+    def __init__(self, dim: int, n_heads: int = 1, groups: int = 32):
+        super().__init__()
+        assert dim % n_heads == 0
+        self.n_heads = n_heads
+        self.norm = nn.GroupNorm(groups, dim)
+        self.q = _conv(dim, dim, 1)
+        self.k = _conv(dim, dim, 1)
+        self.v = _conv(dim, dim, 1)
+        self.proj = _conv(dim, dim, 1)
+        self.scale = (dim // n_heads) ** -0.5
+
+
+class _TimeEmbedding(nn.Sequential):
+    """Index layout of the reference time MLP: 0 sinusoid (no params), 1 Linear, 2 SiLU, 3 Linear."""
+
+    def __init__(self, dim: int):
+        super().__init__(nn.Identity(), nn.Linear(dim, 4 * dim), nn.SiLU(), nn.Linear(4 * dim, 4 * dim))
+
+
+class UNet(nn.Module):
+    def __init__(
+            self,
+            in_channels: int = 3,
+            out_channels: int = 3,
+            dim: int = 128,
+            dim_mults: List[int] = (1, 2, 2, 2),
+            use_attn: List[int] = (False, True, False, False),
+            num_res_blocks: int = 2,
+            n_heads: int = 1,
+            dropout: float = 0.1,
+    ):
+        super().__init__()
+        if len(dim_mults) != len(use_attn):
+            raise ValueError('dim_mults and use_attn must have the same length')
+        self.arch = dict(in_channels=in_channels, out_channels=out_channels, dim=dim,
+                         dim_mults=list(dim_mults), use_attn=[bool(a) for a in use_attn],
+                         num_res_blocks=num_res_blocks, n_heads=n_heads)
+        temb = 4 * dim
+        self.time_embed = _TimeEmbedding(dim)
+        self.first_conv = _conv(in_channels, dim, 3)
+
+        chans = [dim]       # channels of every skip, in push order
+        cur = dim
+        self.down_blocks = nn.ModuleList()
+        for i, mult in enumerate(dim_mults):
+            out = dim * mult
+            stage = nn.ModuleList()
+            for _ in range(num_res_blocks):
+                stage.append(ResBlock(cur, out, temb, dropout))
+                if use_attn[i]:
+                    stage.append(SelfAttentionBlock(out, n_heads=n_heads))
+                chans.append(out)
+                cur = out
+            if i < len(dim_mults) - 1:
+                stage.append(_conv(out, out, 3, stride=2))   # Downsample (modules.py:70-72)
+                chans.append(out)
+            self.down_blocks.append(stage)
+
+        self.bottleneck_block = nn.ModuleList([
+            ResBlock(cur, cur, temb, dropout), SelfAttentionBlock(cur), ResBlock(cur, cur, temb, dropout),
+        ])
+
+        self.up_blocks = nn.ModuleList()
+        for i in reversed(range(len(dim_mults))):
+            out = dim * dim_mults[i]
+            stage = nn.ModuleList()
+            for _ in range(num_res_blocks + 1):
+                stage.append(ResBlock(chans.pop() + cur, out, temb, dropout))
+                if use_attn[i]:
+                    stage.append(SelfAttentionBlock(out, n_heads=n_heads))
+                cur = out
+            if i > 0:
+                # Upsample = nearest 2x then conv (modules.py:60-65); index 1 holds the conv
+                stage.append(nn.Sequential(nn.Upsample(scale_factor=2, mode='nearest'), _conv(out, out, 3)))
+            self.up_blocks.append(stage)
+
+        self.last_conv = nn.Sequential(_gn(cur), nn.SiLU(), _conv(cur, out_channels, 3))
+        self._native = None
+        self._native_key = None
+
+    # ----------------------------------------------------------- native side
+    def _arch_struct(self) -> UNetArch:
+        a = UNetArch()
+        a.in_channels = self.arch['in_channels']
+        a.out_channels = self.arch['out_channels']
+        a.dim = self.arch['dim']
+        a.n_stages = len(self.arch['dim_mults'])
+        for i, (m, at) in enumerate(zip(self.arch['dim_mults'], self.arch['use_attn'])):
+            a.dim_mults[i] = m
+            a.use_attn[i] = int(at)
+        a.num_res_blocks = self.arch['num_res_blocks']
+        a.n_heads = self.arch['n_heads']
+        return a
+
+    def _params_key(self, tensors: Sequence[Tensor]):
+        return (tuple(t.data_ptr() for t in tensors), sum(t._version for t in tensors))
+
+    def _release_native(self):
+        if self._native is not None:
+            load().dm_unet_destroy(self._native)
+            self._native = None
+            self._native_key = None
+
+    def native_handle(self, device: torch.device):
+        """Create (or reuse) the packed native model. Re-packs when parameters change."""
+        tensors = list(self.state_dict().values())
+        for i, p in enumerate(tensors):
+            if p.device != device:
+                raise RuntimeError(f'UNet parameters are on {p.device} but the input is on {device}; '
+                                   f'move the model with .to(device) first')
+            if p.dtype != torch.float32 or not p.is_contiguous():
+                raise TypeError('UNet parameters must be contiguous float32')
+        key = self._params_key(tensors)
+        if self._native is not None and self._native_key == key:
+            return self._native
+        self._release_native()
+        L = load()
+        n = len(tensors)
+        ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in tensors])
+        numels = (ctypes.c_int64 * n)(*[t.numel() for t in tensors])
+        handle = ctypes.c_void_p()
+        arch = self._arch_struct()
+        check(L.dm_unet_create(ctypes.byref(arch), ptrs, numels, n, stream_handle(device), ctypes.byref(handle)),
+              'dm_unet_create')
+        # sinusoid frequencies evaluated exactly as models/modules.py:52-54 (torch CPU exp)
+        half = self.arch['dim'] // 2
+        freqs = torch.exp(torch.arange(half) * -(math.log(10000) / (half - 1))).to(device)
+        check(L.dm_unet_set_time_freqs(handle, freqs.data_ptr(), half, stream_handle(device)),
+              'dm_unet_set_time_freqs')
+        torch.cuda.current_stream(device).synchronize()
+        self._native = handle
+        self._native_key = key
+        return handle
+
+    def _apply(self, fn, *args, **kwargs):
+        self._release_native()
+        return super()._apply(fn, *args, **kwargs)
+
+    def __del__(self):
+        try:
+            self._release_native()
+        except Exception:
+            pass
+
+    # --------------------------------------------------------------- forward
+    def forward(self, X: Tensor, T: Tensor):
+        dmhip.require_device_tensor(X, 'X')
+        dmhip.require_device_tensor(T, 'T', dtype=torch.long)
+        if X.ndim != 4 or X.shape[1] != self.arch['in_channels']:
+            raise ValueError(f'expected input [B, {self.arch["in_channels"]}, H, W], got {tuple(X.shape)}')
+        B, _, H, W = X.shape
+        if T.shape != (B, ):
+            raise ValueError(f'expected T of shape ({B},), got {tuple(T.shape)}')
+        handle = self.native_handle(X.device)
+        out = torch.empty((B, self.arch['out_channels'], H, W), device=X.device, dtype=torch.float32)
+        check(load().dm_unet_forward(handle, X.data_ptr(), T.data_ptr(), B, H, W, out.data_ptr(),
+                                     stream_handle(X.device)), 'dm_unet_forward')
+        return out

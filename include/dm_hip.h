@@ -1,0 +1,179 @@
+/*
+ * dm_hip — MI355X-native denoising-step engine (C ABI).
+ *
+ * The reference (xyfJASON/diffusion-models-pytorch) has no native code and no
+ * FFI: its hot path is two Python calls inside the sampling loop,
+ *
+ *   model_output = model(img, t_batch, **model_kwargs)   diffusions/ddpm.py:276
+ *   out = self.denoise(model_output, img, t, t_prev)     diffusions/ddpm.py:277
+ *                                                        (DDIM: diffusions/ddim.py:57-86,
+ *                                                         CFG:  ddim.py:176-188, ddpm.py:334-348)
+ *
+ * This header is the boundary that replaces both. The Python host package
+ * (`diffusions.*`, `models.unet.UNet`) binds it with ctypes; any other host
+ * (C, C++, a cgo/JNI stub) can bind the same symbols — see INTEGRATION.md.
+ *
+ * Conventions
+ *   - Every tensor argument is a raw device pointer to float32 (or int64 for
+ *     timesteps / labels) owned by the caller; shapes are explicit ints.
+ *     Images are NCHW contiguous, exactly the reference's torch layout.
+ *   - `stream` is a hipStream_t passed as void*; all calls are asynchronous on
+ *     that stream (NULL = the legacy default stream).
+ *   - Return value: DM_OK (0) or a negative DM_ERR_* code; the message of the
+ *     last failure on the calling thread is available from dm_last_error().
+ *     DM_ERR_ARG corresponds to the reference's ValueError / assertion cases.
+ *   - Objects (dm_unet) are not re-entrant: one stream at a time per object.
+ */
+#ifndef DM_HIP_H_
+#define DM_HIP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DM_ABI_VERSION 1
+
+#define DM_OK 0
+#define DM_ERR_ARG (-1)
+#define DM_ERR_HIP (-2)
+#define DM_ERR_STATE (-3)
+#define DM_ERR_UNSUPPORTED (-4)
+
+/* Library / error handling ------------------------------------------------ */
+int dm_abi_version(void);
+const char* dm_last_error(void);
+
+/* Denoiser: DDPM UNet ------------------------------------------------------
+ * Replaces models/unet.py:46-152 (UNet.__init__ / UNet.forward) with the
+ * same hyper-parameters (configs/ddpm_cifar10.yaml:16-26) and the same
+ * parameter list: `params` are the reference state_dict tensors in
+ * state_dict() order (328 tensors for the CIFAR-10 config), `numels` their
+ * element counts (validated). Weights are copied/packed into library-owned
+ * device memory at create time; the caller's tensors may be freed afterwards.
+ */
+#define DM_MAX_STAGES 8
+typedef struct dm_unet_arch {
+  int in_channels;
+  int out_channels;
+  int dim;
+  int n_stages;
+  int dim_mults[DM_MAX_STAGES];
+  int use_attn[DM_MAX_STAGES];
+  int num_res_blocks;
+  int n_heads;
+} dm_unet_arch;
+
+typedef struct dm_unet dm_unet;
+
+/* Number of parameter tensors the reference UNet with this arch registers. */
+int dm_unet_param_count(const dm_unet_arch* arch, int* n_params);
+int dm_unet_create(const dm_unet_arch* arch, const float* const* params, const int64_t* numels,
+                   int n_params, void* stream, dm_unet** out);
+/* x: [B, in_channels, H, W] f32, t: [B] int64, out: [B, out_channels, H, W] f32.
+ * Workspace for batch B at H x W is allocated on first use and cached. */
+int dm_unet_forward(dm_unet* m, const float* x, const int64_t* t, int B, int H, int W, float* out,
+                    void* stream);
+/* Install the sinusoid frequency table exp(-ln(1e4)/(dim/2-1) * i), i < dim/2
+ * (models/modules.py:52-54). The reference evaluates it with torch's CPU exp,
+ * whose last bit is host dependent; hosts pass the table they compute with
+ * the same expression so the embedding matches their reference bit for bit.
+ * `freqs` may be host or device memory; NULL reverts to the on-device expf. */
+int dm_unet_set_time_freqs(dm_unet* m, const float* freqs, int n, void* stream);
+/* Per-launch profiling of the cached plan (HIP events recorded on the launch
+ * stream around every op of dm_unet_forward while enabled). Enabling resets
+ * the accumulators; dm_unet_profile_get synchronises pending events. `label`
+ * names the kernel family/tile (matches the rocprof kernel name), `flops` /
+ * `bytes` are the op's algorithmic work per launch. */
+int dm_unet_profile(dm_unet* m, int enable);
+int dm_unet_profile_count(dm_unet* m, int* n_ops);
+int dm_unet_profile_get(dm_unet* m, int i, char* label, int label_len, double* flops, double* bytes,
+                        double* ms_total, int64_t* launches);
+/* Device bytes held by packed weights and by the cached workspace. */
+int dm_unet_memory(const dm_unet* m, int64_t* weight_bytes, int64_t* workspace_bytes);
+void dm_unet_destroy(dm_unet* m);
+
+/* Sampler update -----------------------------------------------------------
+ * One elementwise pass doing predict() (ddpm.py:174-203), the optional CFG
+ * combine (ddim.py:185 / ddpm.py:343-345, with the second predict under
+ * hack_objective('pred_eps')), and the DDIM (ddim.py:64-77) or DDPM
+ * (ddpm.py:221-252) update. All scalar coefficients are computed by the host
+ * with the reference's own torch 0-dim op sequence and passed in, so the
+ * result is bit-identical to the reference CPU path on identical inputs.
+ */
+typedef struct dm_step_desc {
+  int B, C, HW;      /* image tensor [B, C, HW] */
+  int Cm;            /* channels of the model output: C, or 2C with a learned variance */
+  const float* xt;
+  const float* model_out;        /* conditional (or only) branch, [B, Cm, HW] */
+  const float* model_out_uncond; /* CFG unconditional branch or NULL */
+  float w_uncond, w_cond;        /* (1 - s), s  (float32 of the python scalars) */
+  int objective;                 /* 0 pred_eps, 1 pred_x0, 2 pred_v */
+  int clip_denoised;
+  float sqrt_recip_ac, sqrt_recipm1_ac, sqrt_ac, sqrt_one_minus_ac;
+  int kind;                      /* 0 DDIM, 1 DDPM */
+  float coef1, coef2;            /* DDIM: sqrt(ac_prev), sqrt(1-ac_prev-var); DDPM: mean_coef1, mean_coef2 */
+  int var_mode;                  /* 0 scalar std, 1 learned_range */
+  float std;                     /* sqrt(var) for var_mode 0 */
+  float min_logvar, max_logvar;  /* learned_range */
+  int add_noise;                 /* t != 0 */
+  const float* noise;            /* [B, C, HW] or NULL (treated as zeros, e.g. DDIM eta=0) */
+  float* sample;                 /* required */
+  float* mean;                   /* optional outputs (NULL to skip) */
+  float* pred_x0;
+  float* pred_eps;
+  float* var;
+} dm_step_desc;
+
+int dm_sampler_step(const dm_step_desc* d, void* stream);
+
+/* Operator-level entry points (NHWC, channel-pitched views) ----------------
+ * Used by the parity tests and to compose other denoisers.
+ */
+/* torch.nn.GroupNorm (+ optional per-image modulation y*(1+ms)+mb, + optional SiLU).
+ * x, y: NHWC [B, H*W, C] with channel pitches; part: scratch of
+ * dm_groupnorm_scratch_bytes() bytes. */
+int64_t dm_groupnorm_scratch_bytes(int B, int HW, int G);
+int dm_groupnorm_nhwc(const float* x, int x_pitch, float* y, int y_pitch, int B, int HW, int C, int G,
+                      float eps, const float* gamma, const float* beta, const float* mod_scale,
+                      const float* mod_shift, int mod_pitch, int silu, void* scratch, void* stream);
+
+/* Pack a torch conv weight [Cout][Cin][kh][kw] into the implicit-GEMM layout
+ * [Cout][ldw] at column offset col0 (k = tap * Cin + c). */
+int dm_pack_conv_weight(const float* w, int Cout, int Cin, int taps, float* out, int ldw, int col0,
+                        void* stream);
+
+typedef struct dm_conv_desc {
+  const float* x;  int x_pitch, Cin, Hin, Win;
+  int taps, stride, upsample;
+  const float* x2; int x2_pitch, Cin2;
+  const float* w;  int K;
+  float* y;        int y_pitch, Cout, B, Hout, Wout;
+  const float* bias;
+  const float* rowvec; int rowvec_pitch;
+  const float* res; int res_pitch;
+} dm_conv_desc;
+int dm_conv2d_nhwc(const dm_conv_desc* d, void* stream);
+
+typedef struct dm_gemm_desc {
+  int M, N, K, Z1, Z2;
+  const float* A; int64_t a_s1, a_s2; int lda;
+  const float* B; int64_t b_s1, b_s2; int ldb; int b_kn;
+  float* C; int64_t c_s1, c_s2; int ldc;
+  float alpha;
+  const float* bias;
+  const float* res; int ld_res;
+  int act;
+} dm_gemm_desc;
+int dm_gemm(const dm_gemm_desc* d, void* stream);
+
+int dm_softmax_rows(float* x, int64_t rows, int L, int ld, void* stream);
+/* kind 0: models/modules.py SinusoidalPosEmb ([sin, cos]); kind 1: ADM timestep_embedding ([cos, sin]) */
+int dm_timestep_embedding(const int64_t* t, int B, int dim, int kind, const float* freqs, float* out,
+                          void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DM_HIP_H_ */

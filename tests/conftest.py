@@ -1,0 +1,45 @@
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, 'diffusion-models-pytorch_amd')
+GOLDEN = os.path.join(ROOT, 'tests', 'golden')
+for p in (ROOT, PKG):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line('markers', 'gpu: needs a ROCm GPU (MI355X) and the built libdm_hip.so')
+    config.addinivalue_line('markers', 'slow: long-running test')
+
+
+def load_golden(name):
+    with np.load(os.path.join(GOLDEN, name + '.npz'), allow_pickle=False) as z:
+        arrays = {k: z[k] for k in z.files}
+    with open(os.path.join(GOLDEN, name + '.json')) as f:
+        meta = json.load(f)
+    return arrays, meta
+
+
+@pytest.fixture(scope='session')
+def golden():
+    cache = {}
+
+    def get(name):
+        if name not in cache:
+            cache[name] = load_golden(name)
+        return cache[name]
+    return get
+
+
+@pytest.fixture(scope='session')
+def cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip('no ROCm GPU visible')
+    return torch.device('cuda:0')

@@ -1,0 +1,239 @@
+"""Generate the golden fixtures from the REFERENCE implementation.
+
+Runs only in the survey/build container, where /root/reference exists:
+    python tests/golden/make_golden.py
+It imports the reference's own modules (diffusions.schedule/ddpm/ddim,
+models.unet) through a bare package shim that skips diffusions/__init__.py
+(which would import torchvision/transformers via the CLIP guidance), drives
+them on CPU with deterministic synthetic weights and seeded CPU noise, and
+writes inputs + outputs as small .npz files next to this script. Nothing
+under tests/ or the product imports the reference at run time; the GPU box
+only reads the .npz files.
+"""
+import json
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = '/root/reference'
+
+
+def import_reference():
+    sys.path.insert(0, REF)
+    pkg = types.ModuleType('diffusions')
+    pkg.__path__ = [os.path.join(REF, 'diffusions')]
+    sys.modules['diffusions'] = pkg
+    import diffusions.schedule as schedule  # noqa: E402
+    import diffusions.ddpm as ddpm  # noqa: E402
+    import diffusions.ddim as ddim  # noqa: E402
+    import models.unet as unet  # noqa: E402
+    return schedule, ddpm, ddim, unet
+
+
+def _synthetic_module():
+    import importlib.util
+    path = os.path.join(REPO, 'diffusion-models-pytorch_amd', 'utils', 'synthetic.py')
+    spec = importlib.util.spec_from_file_location('dm_synthetic', path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def synthetic(model, seed=0):
+    syn = _synthetic_module()
+    sd = syn.synthetic_state_dict(model.state_dict(), seed)
+    model.load_state_dict(sd)
+    return syn.state_dict_sha256(sd)
+
+
+def coef_probe_sha():
+    """Fingerprint of this host's torch CPU 0-dim sqrt/pow rounding over the linear-1000 schedule."""
+    import hashlib
+    betas = torch.linspace(0.0001, 0.02, 1000, dtype=torch.float64)
+    ac = torch.cumprod(1. - betas, dim=0).to(torch.float)
+    vals = []
+    for t in range(1000):
+        a = ac[t]
+        vals += [((1. / a) ** 0.5).item(), ((1. / a - 1.) ** 0.5).item(), torch.sqrt(a).item(),
+                 torch.sqrt(1. - a).item()]
+    return hashlib.sha256(torch.tensor(vals).numpy().tobytes()).hexdigest()
+
+
+def save(name, meta, **arrays):
+    arrays = {k: (v.detach().cpu().numpy() if isinstance(v, torch.Tensor) else np.asarray(v))
+              for k, v in arrays.items()}
+    np.savez_compressed(os.path.join(HERE, name + '.npz'), **arrays)
+    with open(os.path.join(HERE, name + '.json'), 'w') as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+    print(name, {k: v.shape for k, v in arrays.items()})
+
+
+ARCHS = {
+    'cifar10': dict(in_channels=3, out_channels=3, dim=128, dim_mults=[1, 2, 2, 2],
+                    use_attn=[False, True, False, False], num_res_blocks=2, n_heads=1, dropout=0.1),
+    'mnist': dict(in_channels=1, out_channels=1, dim=64, dim_mults=[1, 2, 2, 2],
+                  use_attn=[False, True, False, False], num_res_blocks=2, n_heads=1, dropout=0.1),
+    'tiny': dict(in_channels=3, out_channels=3, dim=32, dim_mults=[1, 2],
+                 use_attn=[False, True], num_res_blocks=1, n_heads=2, dropout=0.0),
+}
+
+
+def main():
+    torch.set_num_threads(8)
+    schedule, ddpm, ddim, unet = import_reference()
+    common = dict(torch=torch.__version__, threads=torch.get_num_threads(),
+                  reference='xyfJASON/diffusion-models-pytorch @ 2024-12-20 (/root/reference)')
+
+    # 1. schedules and respaced sequences (bit-exact targets)
+    sched = {}
+    for kind, T in [('linear', 1000), ('linear', 200), ('cosine', 1000), ('quad', 1000), ('const', 1000)]:
+        d = ddpm.DDPM(total_steps=T, beta_schedule=kind, respace_type=None)
+        sched[f'ac_{kind}_{T}'] = d.alphas_cumprod
+        sched[f'betas_{kind}_{T}'] = schedule.get_beta_schedule(T, kind)
+    for rt in ['uniform', 'uniform-leading', 'uniform-linspace', 'uniform-trailing', 'quad', 'none']:
+        for S in [10, 50, 100, 250, 300, 1000]:
+            sched[f'seq_{rt}_{S}'] = schedule.get_respaced_seq(1000, rt, S)
+    save('schedule', dict(common), **sched)
+
+    # 2. sampler updates on fixed inputs, every step of several configs (bit-exact targets)
+    g = torch.Generator().manual_seed(7)
+    shape = (2, 3, 4, 4)
+    cases = [
+        ('ddim50', dict(cls='DDIM', kw=dict(respace_type='uniform', respace_steps=50, eta=0.0))),
+        ('ddim50_eta05', dict(cls='DDIM', kw=dict(respace_type='uniform', respace_steps=50, eta=0.5))),
+        ('ddim100_v', dict(cls='DDIM', kw=dict(respace_type='uniform', respace_steps=100, objective='pred_v'))),
+        ('ddpm1000_large', dict(cls='DDPM', kw=dict(var_type='fixed_large'))),
+        ('ddpm200_small10', dict(cls='DDPM', kw=dict(total_steps=200, var_type='fixed_small',
+                                                      respace_type='uniform', respace_steps=10))),
+        ('ddpm_learned50_x0', dict(cls='DDPM', kw=dict(var_type='learned_range', beta_schedule='cosine',
+                                                        respace_type='uniform', respace_steps=50,
+                                                        objective='pred_x0'))),
+    ]
+    upd = {}
+    meta = dict(common, cases={}, coef_probe_sha=coef_probe_sha())
+    for name, c in cases:
+        cls = getattr(ddim if c['cls'] == 'DDIM' else ddpm, c['cls'])
+        d = cls(**c['kw'])
+        seq = d.respaced_seq.tolist()
+        prev = [-1] + seq[:-1]
+        pairs = list(zip(reversed(seq), reversed(prev)))
+        if len(pairs) == 1000:  # DDPM-1000: a spread of steps incl. both ends
+            idx = sorted(set(list(range(0, 1000, 25)) + [1, 2, 997, 998, 999]))
+            pairs = [pairs[i] for i in idx]
+        learned = c['kw'].get('var_type') == 'learned_range'
+        cm = 6 if learned else 3
+        xs, outs, res = [], [], {k: [] for k in ('sample', 'mean', 'pred_x0', 'pred_eps', 'reverse_eps', 'var')}
+        for (t, tp) in pairs:
+            xt = torch.randn(shape, generator=g) * 1.5
+            mo = torch.randn((2, cm, 4, 4), generator=g)
+            if learned:
+                mo[:, 3:] = mo[:, 3:].clamp(-1, 1)
+            torch.manual_seed(1000 + t)
+            out = d.denoise(mo, xt, t, tp)
+            xs.append(xt)
+            outs.append(mo)
+            for k in res:
+                v = out[k]
+                res[k].append(v.expand(shape) if v.ndim == 0 else v)
+        upd[f'{name}_t'] = torch.tensor([p[0] for p in pairs])
+        upd[f'{name}_tprev'] = torch.tensor([p[1] for p in pairs])
+        upd[f'{name}_xt'] = torch.stack(xs)
+        upd[f'{name}_out'] = torch.stack(outs)
+        for k, v in res.items():
+            upd[f'{name}_{k}'] = torch.stack(v)
+        meta['cases'][name] = c
+    # CFG combine on fixed inputs (DDIMCFG.sample_loop arithmetic, ddim.py:179-187)
+    d = ddim.DDIMCFG(guidance_scale=3.0, respace_type='uniform', respace_steps=50)
+    seq = d.respaced_seq.tolist()
+    prev = [-1] + seq[:-1]
+    cf = {k: [] for k in ('xt', 'oc', 'ou', 'sample', 'pred_x0', 'pred_eps')}
+    for (t, tp) in list(zip(reversed(seq), reversed(prev)))[::7]:
+        xt = torch.randn(shape, generator=g)
+        oc = torch.randn(shape, generator=g)
+        ou = torch.randn(shape, generator=g)
+        ec = d.predict(oc, xt, t)['pred_eps']
+        eu = d.predict(ou, xt, t)['pred_eps']
+        pe = (1 - d.guidance_scale) * eu + d.guidance_scale * ec
+        with d.hack_objective('pred_eps'):
+            out = d.denoise(pe, xt, t, tp)
+        for k, v in (('xt', xt), ('oc', oc), ('ou', ou), ('sample', out['sample']), ('pred_x0', out['pred_x0']),
+                     ('pred_eps', out['pred_eps'])):
+            cf[k].append(v)
+        cf.setdefault('t', []).append(torch.tensor(t))
+        cf.setdefault('tprev', []).append(torch.tensor(tp))
+    for k, v in cf.items():
+        upd[f'cfg_{k}'] = torch.stack(v)
+    save('updates', meta, **upd)
+
+    # 3. network forwards (fp32-tolerance targets)
+    fw = {}
+    fmeta = dict(common, archs=ARCHS)
+    for name, arch in ARCHS.items():
+        model = unet.UNet(**arch).eval()
+        sha = synthetic(model)
+        fmeta[f'{name}_weights_sha256'] = sha
+        H = 16 if name == 'tiny' else 32
+        x = torch.randn((2, arch['in_channels'], H, H), generator=g)
+        t = torch.tensor([999, 0]) if name != 'tiny' else torch.tensor([10, 500])
+        with torch.no_grad():
+            y = model(x, t)
+        fw[f'{name}_x'], fw[f'{name}_t'], fw[f'{name}_y'] = x, t, y
+        fmeta[f'{name}_state_dict'] = [[k, list(v.shape)] for k, v in model.state_dict().items()]
+    save('forward', fmeta, **fw)
+
+    # 4. end-to-end trajectories (fp32-tolerance targets)
+    tr = {}
+    tmeta = dict(common)
+    # CIFAR-10 DDIM-50, B=2, init noise from torch.manual_seed(2022) as sample_uncond.py seeds
+    model = unet.UNet(**ARCHS['cifar10']).eval()
+    tmeta['cifar10_weights_sha256'] = synthetic(model)
+    d = ddim.DDIM(respace_type='uniform', respace_steps=50, eta=0.0)
+    torch.manual_seed(2022)
+    init = torch.randn((2, 3, 32, 32))
+    keep = [0, 1, 10, 25, 40, 48, 49]
+    with torch.no_grad():
+        for i, out in enumerate(d.sample_loop(model, init)):
+            if i in keep:
+                tr[f'ddim50_step{i}_sample'] = out['sample']
+                tr[f'ddim50_step{i}_pred_eps'] = out['pred_eps']
+    tr['ddim50_init'] = init
+    tmeta['ddim50_keep'] = keep
+    # MNIST DDPM T=200, fixed_small, 10 uniform steps (BASELINE config 0), per-step noise from the
+    # CPU generator after torch.manual_seed(2022): init noise first, then one randn_like per step.
+    model = unet.UNet(**ARCHS['mnist']).eval()
+    tmeta['mnist_weights_sha256'] = synthetic(model)
+    d = ddpm.DDPM(total_steps=200, var_type='fixed_small', respace_type='uniform', respace_steps=10)
+    torch.manual_seed(2022)
+    init = torch.randn((2, 1, 32, 32))
+    tr['ddpm10_init'] = init
+    with torch.no_grad():
+        for i, out in enumerate(d.sample_loop(model, init)):
+            tr[f'ddpm10_step{i}_sample'] = out['sample']
+            tr[f'ddpm10_step{i}_pred_eps'] = out['pred_eps']
+            tr[f'ddpm10_step{i}_noise'] = out['reverse_eps']
+    # tiny UNet, DDPM-5 fixed_large and DDIM-5 eta 0.5 (noise pinned per step)
+    model = unet.UNet(**ARCHS['tiny']).eval()
+    tmeta['tiny_weights_sha256'] = synthetic(model)
+    for kind in ('ddpm', 'ddim'):
+        if kind == 'ddpm':
+            d = ddpm.DDPM(var_type='fixed_large', respace_type='uniform', respace_steps=5)
+        else:
+            d = ddim.DDIM(respace_type='uniform', respace_steps=5, eta=0.5)
+        torch.manual_seed(11)
+        init = torch.randn((2, 3, 16, 16))
+        tr[f'tiny_{kind}5_init'] = init
+        with torch.no_grad():
+            for i, out in enumerate(d.sample_loop(model, init)):
+                tr[f'tiny_{kind}5_step{i}_sample'] = out['sample']
+                tr[f'tiny_{kind}5_step{i}_pred_eps'] = out['pred_eps']
+                tr[f'tiny_{kind}5_step{i}_noise'] = out['reverse_eps']
+    save('trajectory', tmeta, **tr)
+
+
+if __name__ == '__main__':
+    main()

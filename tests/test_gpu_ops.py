@@ -1,0 +1,193 @@
+"""Operator-level parity of the HIP kernels (called through the C ABI) against
+torch CPU references. Integer-valued operands make contractions exact in fp32,
+so the MFMA layout / indexing tests compare bit-for-bit."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import dmhip
+
+pytestmark = pytest.mark.gpu
+
+
+def _ints(shape, lo=-3, hi=4, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randint(lo, hi, shape, generator=g).float()
+
+
+def _gemm_desc(**kw):
+    d = dmhip.GemmDesc()
+    d.Z1 = d.Z2 = 1
+    d.alpha = 1.0
+    for k, v in kw.items():
+        setattr(d, k, v)
+    return d
+
+
+@pytest.mark.parametrize('M,N,K', [(64, 64, 32), (200, 136, 72), (256, 768, 256), (1024, 512, 128), (33, 40, 4)])
+def test_gemm_bt_exact(cuda, M, N, K):
+    A = _ints((M, K), seed=1)
+    B = _ints((N, K), seed=2)
+    bias = _ints((N, ), seed=3)
+    C = torch.empty((M, N), device=cuda)
+    Ad, Bd, bd = A.to(cuda), B.to(cuda), bias.to(cuda)
+    d = _gemm_desc(M=M, N=N, K=K, A=Ad.data_ptr(), lda=K, B=Bd.data_ptr(), ldb=K, C=C.data_ptr(), ldc=N,
+                   bias=bd.data_ptr())
+    dmhip.gemm(d, cuda)
+    ref = (A.double() @ B.double().T + bias.double()).float()
+    assert torch.equal(C.cpu(), ref)
+
+
+@pytest.mark.parametrize('M,N,K,Z1,Z2', [(256, 128, 256, 3, 2), (16, 64, 16, 4, 1), (100, 72, 100, 2, 3)])
+def test_gemm_batched_kn_alpha(cuda, M, N, K, Z1, Z2):
+    A = _ints((Z1, Z2, M, K), seed=4)
+    B = _ints((Z1, Z2, K, N), seed=5)
+    C = torch.empty((Z1, Z2, M, N), device=cuda)
+    Ad, Bd = A.to(cuda), B.to(cuda)
+    d = _gemm_desc(M=M, N=N, K=K, Z1=Z1, Z2=Z2,
+                   A=Ad.data_ptr(), a_s1=Z2 * M * K, a_s2=M * K, lda=K,
+                   B=Bd.data_ptr(), b_s1=Z2 * K * N, b_s2=K * N, ldb=N, b_kn=1,
+                   C=C.data_ptr(), c_s1=Z2 * M * N, c_s2=M * N, ldc=N, alpha=0.5)
+    dmhip.gemm(d, cuda)
+    ref = ((A.double() * 0.5) @ B.double()).float()
+    assert torch.equal(C.cpu(), ref)
+
+
+def test_gemm_silu_residual(cuda):
+    M, N, K = 130, 96, 64
+    g = torch.Generator().manual_seed(9)
+    A, B = torch.randn((M, K), generator=g), torch.randn((N, K), generator=g)
+    bias, res = torch.randn(N, generator=g), torch.randn((M, N), generator=g)
+    C = torch.empty((M, N), device=cuda)
+    Ad, Bd, bd, rd = A.to(cuda), B.to(cuda), bias.to(cuda), res.to(cuda)
+    d = _gemm_desc(M=M, N=N, K=K, A=Ad.data_ptr(), lda=K, B=Bd.data_ptr(), ldb=K, C=C.data_ptr(), ldc=N,
+                   bias=bd.data_ptr(), res=rd.data_ptr(), ld_res=N, act=1)
+    dmhip.gemm(d, cuda)
+    ref = F.silu((A.double() @ B.double().T + bias.double()) + res.double())
+    assert (C.cpu().double() - ref).abs().max().item() < 1e-5
+
+
+def _pack(w, cuda, K=None, col0=0, out=None):
+    Cout, Cin, kh, kw = w.shape
+    K = K or kh * kw * Cin
+    if out is None:
+        out = torch.zeros((Cout, K), device=cuda)
+    dmhip.pack_conv_weight(w.to(cuda).contiguous(), out, K, col0)
+    return out
+
+
+def _run_conv(cuda, x_nhwc, w_packed, Cout, Hout, Wout, taps, stride=1, upsample=0, bias=None, rowvec=None,
+              res=None, x2=None, Cin2=0, y_pitch=None, x_pitch=None):
+    B, Hin, Win, Cin = x_nhwc.shape[0], x_nhwc.shape[1], x_nhwc.shape[2], x_nhwc.shape[3]
+    x_pitch = x_pitch or Cin
+    y_pitch = y_pitch or Cout
+    y = torch.full((B, Hout, Wout, y_pitch), float('nan'), device=cuda)
+    d = dmhip.ConvDesc()
+    d.x, d.x_pitch, d.Cin, d.Hin, d.Win = x_nhwc.data_ptr(), x_pitch, Cin, Hin, Win
+    d.taps, d.stride, d.upsample = taps, stride, upsample
+    d.x2, d.x2_pitch, d.Cin2 = (x2.data_ptr() if x2 is not None else None), (x2.shape[-1] if x2 is not None else 0), Cin2
+    d.w, d.K = w_packed.data_ptr(), w_packed.shape[1]
+    d.y, d.y_pitch, d.Cout, d.B, d.Hout, d.Wout = y.data_ptr(), y_pitch, Cout, B, Hout, Wout
+    d.bias = bias.data_ptr() if bias is not None else None
+    d.rowvec = rowvec.data_ptr() if rowvec is not None else None
+    d.rowvec_pitch = rowvec.shape[1] if rowvec is not None else 0
+    d.res = res.data_ptr() if res is not None else None
+    d.res_pitch = res.shape[-1] if res is not None else 0
+    dmhip.conv2d_nhwc(d, cuda)
+    return y
+
+
+def _nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+@pytest.mark.parametrize('B,Cin,Cout,H,stride,up', [
+    (2, 32, 64, 8, 1, 0), (3, 64, 32, 16, 2, 0), (2, 32, 32, 4, 1, 1), (1, 128, 256, 16, 1, 0),
+    (5, 64, 64, 4, 1, 0), (2, 96, 160, 8, 2, 0),
+])
+def test_conv3x3_exact(cuda, B, Cin, Cout, H, stride, up):
+    x = _ints((B, Cin, H, H), -2, 3, seed=10)
+    w = _ints((Cout, Cin, 3, 3), -2, 3, seed=11)
+    b = _ints((Cout, ), seed=12)
+    xin = F.interpolate(x, scale_factor=2, mode='nearest') if up else x
+    ref = F.conv2d(xin.double(), w.double(), b.double(), stride=stride, padding=1).float()
+    Hout = ref.shape[-1]
+    y = _run_conv(cuda, _nhwc(x).to(cuda), _pack(w, cuda), Cout, Hout, Hout, 9, stride, up, b.to(cuda))
+    assert torch.equal(y.cpu(), _nhwc(ref))
+
+
+def test_conv_segments_rowvec_residual_pitch(cuda):
+    # ResBlock second conv with the shortcut folded in as a 1x1 K segment, temb rowvec, pitched output
+    B, C1, C2, Cout, H = 3, 64, 32, 64, 8
+    h = _ints((B, C1, H, H), seed=20)
+    x = _ints((B, C2, H, H), seed=21)
+    w2 = _ints((Cout, C1, 3, 3), -2, 3, seed=22)
+    ws = _ints((Cout, C2, 1, 1), seed=23)
+    b = _ints((Cout, ), seed=24)
+    rv = _ints((B, Cout), seed=25)
+    K = 9 * C1 + C2
+    wp = torch.zeros((Cout, K), device=cuda)
+    _pack(w2, cuda, K, 0, wp)
+    _pack(ws, cuda, K, 9 * C1, wp)
+    ref = (F.conv2d(h.double(), w2.double(), b.double(), padding=1) + rv.double()[:, :, None, None]
+           + F.conv2d(x.double(), ws.double())).float()
+    y = _run_conv(cuda, _nhwc(h).to(cuda), wp, Cout, H, H, 9, bias=b.to(cuda), rowvec=rv.to(cuda),
+                  x2=_nhwc(x).to(cuda), Cin2=C2, y_pitch=96)
+    assert torch.equal(y[..., :Cout].cpu(), _nhwc(ref))
+    assert torch.isnan(y[..., Cout:]).all()  # channels outside the view untouched
+
+
+def test_conv1x1_residual(cuda):
+    B, C, H = 2, 64, 8
+    x = _ints((B, C, H, H), seed=30)
+    w = _ints((C, C, 1, 1), seed=31)
+    r = _ints((B, C, H, H), seed=32)
+    ref = (F.conv2d(x.double(), w.double()) + r.double()).float()
+    y = _run_conv(cuda, _nhwc(x).to(cuda), _pack(w, cuda), C, H, H, 1, res=_nhwc(r).to(cuda))
+    assert torch.equal(y.cpu(), _nhwc(ref))
+
+
+@pytest.mark.parametrize('B,C,HW,silu,mod', [(2, 128, 1024, True, False), (3, 384, 256, True, False),
+                                              (2, 256, 16, False, False), (2, 64, 64, True, True),
+                                              (1, 192, 100, True, False)])
+def test_groupnorm(cuda, B, C, HW, silu, mod):
+    g = torch.Generator().manual_seed(40)
+    x = torch.randn((B, C, HW), generator=g) * 3 + 0.5
+    gamma, beta = torch.randn(C, generator=g), torch.randn(C, generator=g)
+    ms, mb = torch.randn((B, C), generator=g), torch.randn((B, C), generator=g)
+    ref = F.group_norm(x.double(), 32, gamma.double(), beta.double(), 1e-5)
+    if mod:
+        ref = ref * (1 + ms.double()[:, :, None]) + mb.double()[:, :, None]
+    if silu:
+        ref = F.silu(ref)
+    xn = x.permute(0, 2, 1).contiguous().to(cuda)
+    y = torch.empty_like(xn)
+    dmhip.groupnorm_nhwc(xn, y, B, HW, C, 32, 1e-5, gamma.to(cuda), beta.to(cuda),
+                         ms.to(cuda) if mod else None, mb.to(cuda) if mod else None, C if mod else 0, silu)
+    err = (y.cpu().double() - ref.permute(0, 2, 1)).abs().max().item()
+    assert err < 2e-5, err
+
+
+def test_softmax_rows(cuda):
+    g = torch.Generator().manual_seed(50)
+    for L in (16, 256, 1024, 1000):
+        x = torch.randn((37, L), generator=g) * 5
+        xd = x.to(cuda)
+        dmhip.softmax_rows(xd, 37, L, L)
+        assert (xd.cpu() - x.softmax(-1)).abs().max().item() < 1e-6
+
+
+def test_timestep_embedding(cuda):
+    import math
+    import oracle.unet as ou
+    t = torch.tensor([0, 1, 17, 500, 999])
+    ref = ou.sinusoidal(t, 128)
+    out = torch.empty((5, 128), device=cuda)
+    # host-provided frequency table (as the UNet installs it): only sin/cos ulps differ
+    freqs = torch.exp(torch.arange(64) * -(math.log(10000) / 63)).to(cuda)
+    dmhip.timestep_embedding(t.to(cuda), 128, 0, out, freqs)
+    assert (out.cpu() - ref).abs().max().item() < 1e-6
+    # on-device frequencies: expf ulps are amplified by t up to 999 (args ~1e3 rad)
+    dmhip.timestep_embedding(t.to(cuda), 128, 0, out)
+    assert (out.cpu() - ref).abs().max().item() < 1e-4
