@@ -76,6 +76,7 @@ extern "C" int dm_conv2d_nhwc(const dm_conv_desc* d, void* stream) {
   a.y = d->y; a.y_pitch = d->y_pitch; a.Cout = d->Cout; a.B = d->B; a.Hout = d->Hout; a.Wout = d->Wout;
   a.bias = d->bias; a.rowvec = d->rowvec; a.rowvec_pitch = d->rowvec_pitch;
   a.res = d->res; a.res_pitch = d->res_pitch;
+  a.tile = d->tile;
   return dm::conv2d_igemm(a, (hipStream_t)stream);
 }
 

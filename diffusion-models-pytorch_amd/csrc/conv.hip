@@ -16,6 +16,13 @@
 // Epilogue: + bias[n] + rowvec[b][n] (timestep-embedding projection,
 // models/unet.py:41) + residual[m][n] (models/unet.py:43), stored through a
 // pitched view so outputs can land inside a wider concat buffer.
+//
+// Loader: every thread owns A_ITERS output pixels for the whole K loop. Per
+// tap it derives a source row pointer and a validity bit (zero padding);
+// the loads themselves are unconditional (invalid rows read a clamped, valid
+// address and are zeroed by a select), so the compiler keeps the next
+// K-slice's global loads in flight across the MFMA work of the current one
+// instead of draining vmcnt at exec-masked branches.
 #include "dm_common.h"
 #include "dm_kernels.h"
 #include "mfma_tile.h"
@@ -24,7 +31,18 @@ namespace dm {
 
 namespace {
 
-template <int BM, int BN, int WM, int WN>
+enum ConvMode { CM_3X3_S1 = 0, CM_3X3_S2 = 1, CM_3X3_UP = 2, CM_1X1 = 3 };
+
+// Bijective XCD-aware remap of the linear block id (cdna_hip_programming.md
+// §5.5 T1): blocks dispatched round-robin over 8 XCDs; consecutive logical ids
+// land on the same XCD so the N-tiles of one M-tile share that XCD's L2.
+__device__ __forceinline__ int xcd_remap(int bid, int nblk) {
+  const int q = nblk >> 3, r = nblk & 7;
+  const int xcd = bid & 7, idx = bid >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+template <int BM, int BN, int WM, int WN, int MODE>
 __global__ void __launch_bounds__(256)
 conv_igemm_kernel(ConvArgs a) {
   using Cfg = TileCfg<BM, BN, WM, WN>;
@@ -33,85 +51,110 @@ conv_igemm_kernel(ConvArgs a) {
   const int M = a.B * a.Hout * a.Wout;
   const int N = a.Cout;
   const int nN = ceil_div(N, BN);
-  const int bid = blockIdx.x;
-  const int mt = bid / nN, nt = bid % nN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = bid / nN, nt = bid - (bid / nN) * nN;
   const int m0 = mt * BM, n0 = nt * BN;
 
   const int t = threadIdx.x;
   const int lane = t & 63, wave = t >> 6;
   const int wm = wave / Cfg::NWN, wn = wave % Cfg::NWN;
-
-  // Loader geometry: 8 threads per 32-float row slice.
   const int lc4 = t & 7;
   const int lrow = t >> 3;
+  const int HWo = a.Hout * a.Wout;
 
   // Per-thread A rows: decode the output pixel once.
-  int a_b[Cfg::A_ITERS], a_oy[Cfg::A_ITERS], a_ox[Cfg::A_ITERS];
-  bool a_ok[Cfg::A_ITERS];
-  const int HWo = a.Hout * a.Wout;
+  int r_b[Cfg::A_ITERS], r_oy[Cfg::A_ITERS], r_ox[Cfg::A_ITERS];
+  bool r_ok[Cfg::A_ITERS];
 #pragma unroll
   for (int i = 0; i < Cfg::A_ITERS; ++i) {
-    int m = m0 + lrow + i * Cfg::ROWS_PER_PASS;
-    a_ok[i] = m < M;
-    int mm = a_ok[i] ? m : 0;
-    a_b[i] = mm / HWo;
-    int rem = mm - a_b[i] * HWo;
-    a_oy[i] = rem / a.Wout;
-    a_ox[i] = rem - a_oy[i] * a.Wout;
+    const int m = m0 + lrow + i * Cfg::ROWS_PER_PASS;
+    r_ok[i] = m < M;
+    const int mm = r_ok[i] ? m : M - 1;
+    r_b[i] = mm / HWo;
+    const int rem = mm - r_b[i] * HWo;
+    r_oy[i] = rem / a.Wout;
+    r_ox[i] = rem - r_oy[i] * a.Wout;
+  }
+  // B rows (output channels), clamped + validity.
+  const float* wrow[Cfg::B_ITERS];
+  bool w_ok[Cfg::B_ITERS];
+#pragma unroll
+  for (int j = 0; j < Cfg::B_ITERS; ++j) {
+    const int n = n0 + lrow + j * Cfg::ROWS_PER_PASS;
+    w_ok[j] = n < N;
+    wrow[j] = a.w + (size_t)(w_ok[j] ? n : N - 1) * a.K + 4 * lc4;
   }
 
-  const int kt1_per_tap = a.Cin1 / kBK;
-  const int nk1 = a.taps * kt1_per_tap;
+  const int ct_per_tap = a.Cin1 / kBK;       // K-slices per tap
+  const int taps = (MODE == CM_1X1) ? 1 : 9;
+  const int nk1 = taps * ct_per_tap;
   const int nk = nk1 + a.Cin2 / kBK;
 
-  f4 ra[Cfg::A_ITERS], rb[Cfg::B_ITERS];
-
-  auto load_tile = [&](int kt) {
-    if (kt < nk1) {
-      const int tap = kt / kt1_per_tap;
-      const int c0 = (kt - tap * kt1_per_tap) * kBK + 4 * lc4;
-      int ky = 1, kx = 1;
-      if (a.taps == 9) { ky = tap / 3; kx = tap - ky * 3; }
+  // Row pointers / validity for the current tap.
+  const float* arow[Cfg::A_ITERS];
+  bool a_ok[Cfg::A_ITERS];
+  auto set_tap = [&](int tap) {
+    const int ky = (MODE == CM_1X1) ? 1 : tap / 3;
+    const int kx = (MODE == CM_1X1) ? 1 : tap - (tap / 3) * 3;
 #pragma unroll
-      for (int i = 0; i < Cfg::A_ITERS; ++i) {
-        int iy, ix;
-        bool ok = a_ok[i];
-        if (a.upsample) {
-          int uy = a_oy[i] + ky - 1, ux = a_ox[i] + kx - 1;
-          ok = ok && uy >= 0 && uy < 2 * a.Hin && ux >= 0 && ux < 2 * a.Win;
-          iy = uy >> 1; ix = ux >> 1;
-        } else {
-          iy = a_oy[i] * a.stride + ky - 1;
-          ix = a_ox[i] * a.stride + kx - 1;
-          ok = ok && iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
-        }
-        if (ok) {
-          const float* src = a.x1 + ((size_t)(a_b[i] * a.Hin + iy) * a.Win + ix) * a.x1_pitch + c0;
-          ra[i] = *reinterpret_cast<const f4*>(src);
-        } else {
-          ra[i] = f4{0.f, 0.f, 0.f, 0.f};
-        }
+    for (int i = 0; i < Cfg::A_ITERS; ++i) {
+      int iy, ix;
+      bool ok = r_ok[i];
+      if (MODE == CM_3X3_UP) {
+        const int uy = r_oy[i] + ky - 1, ux = r_ox[i] + kx - 1;
+        ok = ok && uy >= 0 && uy < 2 * a.Hin && ux >= 0 && ux < 2 * a.Win;
+        iy = uy >> 1;
+        ix = ux >> 1;
+      } else if (MODE == CM_3X3_S2) {
+        iy = 2 * r_oy[i] + ky - 1;
+        ix = 2 * r_ox[i] + kx - 1;
+        ok = ok && iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
+      } else {
+        iy = r_oy[i] + ky - 1;
+        ix = r_ox[i] + kx - 1;
+        ok = ok && iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
       }
-    } else {
-      const int c0 = (kt - nk1) * kBK + 4 * lc4;
-#pragma unroll
-      for (int i = 0; i < Cfg::A_ITERS; ++i) {
-        if (a_ok[i]) {
-          int m = m0 + lrow + i * Cfg::ROWS_PER_PASS;
-          ra[i] = *reinterpret_cast<const f4*>(a.x2 + (size_t)m * a.x2_pitch + c0);
-        } else {
-          ra[i] = f4{0.f, 0.f, 0.f, 0.f};
-        }
-      }
+      iy = min(max(iy, 0), a.Hin - 1);
+      ix = min(max(ix, 0), a.Win - 1);
+      a_ok[i] = ok;
+      arow[i] = a.x1 + ((size_t)(r_b[i] * a.Hin + iy) * a.Win + ix) * a.x1_pitch + 4 * lc4;
     }
-    const int kofs = kt * kBK + 4 * lc4;
+  };
+  auto set_seg2 = [&]() {
 #pragma unroll
-    for (int j = 0; j < Cfg::B_ITERS; ++j) {
-      int n = n0 + lrow + j * Cfg::ROWS_PER_PASS;
-      if (n < N)
-        rb[j] = *reinterpret_cast<const f4*>(a.w + (size_t)n * a.K + kofs);
-      else
-        rb[j] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < Cfg::A_ITERS; ++i) {
+      const int m = min(m0 + lrow + i * Cfg::ROWS_PER_PASS, M - 1);
+      a_ok[i] = r_ok[i];
+      arow[i] = a.x2 + (size_t)m * a.x2_pitch + 4 * lc4;
+    }
+  };
+
+  // Raw loaded registers; the zero-padding select is applied when they are
+  // written to LDS (after the MFMA work), so no wait sits between the loads
+  // and the compute that hides them.
+  f4 ra[Cfg::A_ITERS], rb[Cfg::B_ITERS];
+  bool ra_ok[Cfg::A_ITERS];
+  const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  // Loader state: the slice about to be loaded is (tap, channel offset) or segment 2.
+  int ld_tap = 0, ld_c = 0;
+  auto load_tile = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < Cfg::A_ITERS; ++i) {
+      ra[i] = *reinterpret_cast<const f4*>(arow[i] + ld_c);
+      ra_ok[i] = a_ok[i];
+    }
+#pragma unroll
+    for (int j = 0; j < Cfg::B_ITERS; ++j) rb[j] = *reinterpret_cast<const f4*>(wrow[j] + kt * kBK);
+    // advance (wave-uniform control flow only)
+    ld_c += kBK;
+    if (kt + 1 < nk1) {
+      if (ld_c == a.Cin1) {
+        ld_c = 0;
+        set_tap(++ld_tap);
+      }
+    } else if (kt + 1 == nk1) {
+      ld_c = 0;
+      set_seg2();
     }
   };
 
@@ -120,10 +163,10 @@ conv_igemm_kernel(ConvArgs a) {
     float* Bs = As + Cfg::A_ELEMS;
 #pragma unroll
     for (int i = 0; i < Cfg::A_ITERS; ++i)
-      *reinterpret_cast<f4*>(As + (lrow + i * Cfg::ROWS_PER_PASS) * kLDK + 4 * lc4) = ra[i];
+      *reinterpret_cast<f4*>(As + (lrow + i * Cfg::ROWS_PER_PASS) * kLDK + 4 * lc4) = ra_ok[i] ? ra[i] : zero4;
 #pragma unroll
     for (int j = 0; j < Cfg::B_ITERS; ++j)
-      *reinterpret_cast<f4*>(Bs + (lrow + j * Cfg::ROWS_PER_PASS) * kLDK + 4 * lc4) = rb[j];
+      *reinterpret_cast<f4*>(Bs + (lrow + j * Cfg::ROWS_PER_PASS) * kLDK + 4 * lc4) = w_ok[j] ? rb[j] : zero4;
   };
 
   f16v acc[Cfg::TM][Cfg::TN];
@@ -134,26 +177,31 @@ conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+  if (nk1 > 0) set_tap(0); else set_seg2();
   load_tile(0);
   store_tile(0);
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
-    if (kt + 1 < nk) load_tile(kt + 1);
+    const bool more = kt + 1 < nk;
+    if (more) load_tile(kt + 1);
     const float* As = lds + buf * Cfg::STAGE;
     const float* Bs = As + Cfg::A_ELEMS;
     mfma_slice<Cfg::TM, Cfg::TN>(As, Bs, wm * WM, wn * WN, lane, acc);
-    if (kt + 1 < nk) store_tile(buf ^ 1);
+    if (more) store_tile(buf ^ 1);
     __syncthreads();
   }
 
   // Epilogue.
   const int lr = lane & 31, lh = lane >> 5;
+  const bool block_one_image = (HWo % BM) == 0;
+  const int b_blk = m0 / HWo;
 #pragma unroll
   for (int j = 0; j < Cfg::TN; ++j) {
     const int n = n0 + wn * WN + j * 32 + lr;
     if (n >= N) continue;
     const float bn = a.bias ? a.bias[n] : 0.f;
+    const float rv_blk = (a.rowvec && block_one_image) ? a.rowvec[(size_t)b_blk * a.rowvec_pitch + n] : 0.f;
 #pragma unroll
     for (int i = 0; i < Cfg::TM; ++i) {
 #pragma unroll
@@ -162,7 +210,7 @@ conv_igemm_kernel(ConvArgs a) {
         if (m >= M) continue;
         float v = acc[i][j][r];
         if (a.bias) v = v + bn;
-        if (a.rowvec) v = v + a.rowvec[(size_t)(m / HWo) * a.rowvec_pitch + n];
+        if (a.rowvec) v = v + (block_one_image ? rv_blk : a.rowvec[(size_t)(m / HWo) * a.rowvec_pitch + n]);
         if (a.res) v = v + a.res[(size_t)m * a.res_pitch + n];
         a.y[(size_t)m * a.y_pitch + n] = v;
       }
@@ -171,16 +219,35 @@ conv_igemm_kernel(ConvArgs a) {
 }
 
 template <int BM, int BN, int WM, int WN>
-int launch_conv(const ConvArgs& a, hipStream_t st) {
+int launch_conv_tile(const ConvArgs& a, int mode, hipStream_t st) {
   using Cfg = TileCfg<BM, BN, WM, WN>;
   const int M = a.B * a.Hout * a.Wout;
   const int blocks = ceil_div(M, BM) * ceil_div(a.Cout, BN);
-  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN>), dim3(blocks), dim3(Cfg::NT), 0, st, a);
+  switch (mode) {
+    case CM_3X3_S1:
+      hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CM_3X3_S1>), dim3(blocks), dim3(Cfg::NT), 0, st, a);
+      break;
+    case CM_3X3_S2:
+      hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CM_3X3_S2>), dim3(blocks), dim3(Cfg::NT), 0, st, a);
+      break;
+    case CM_3X3_UP:
+      hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CM_3X3_UP>), dim3(blocks), dim3(Cfg::NT), 0, st, a);
+      break;
+    default:
+      hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, CM_1X1>), dim3(blocks), dim3(Cfg::NT), 0, st, a);
+      break;
+  }
   DM_LAUNCH_CHECK();
   return DM_OK;
 }
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+inline int conv_mode(const ConvArgs& a) {
+  if (a.taps == 1) return CM_1X1;
+  if (a.upsample) return CM_3X3_UP;
+  return a.stride == 2 ? CM_3X3_S2 : CM_3X3_S1;
+}
 
 }  // namespace
 
@@ -189,11 +256,12 @@ int conv2d_igemm(const ConvArgs& a, hipStream_t st) {
   DM_REQUIRE(a.stride == 1 || a.stride == 2, "conv: stride must be 1 or 2");
   DM_REQUIRE(!a.upsample || (a.taps == 9 && a.stride == 1), "conv: upsample needs 3x3 stride 1");
   DM_REQUIRE(a.Cin1 % kBK == 0 && a.Cin2 % kBK == 0, "conv: input channels must be multiples of 32");
+  DM_REQUIRE(a.Cin1 > 0, "conv: no input channels");
   DM_REQUIRE(a.K == a.taps * a.Cin1 + a.Cin2, "conv: K mismatch");
-  DM_REQUIRE(a.x1_pitch % 4 == 0 && a.y_pitch >= a.Cout, "conv: pitch");
+  DM_REQUIRE(a.x1_pitch % 4 == 0 && a.y_pitch >= a.Cout && a.K % 4 == 0, "conv: pitch");
   DM_REQUIRE(aligned16(a.x1) && aligned16(a.w), "conv: operands must be 16-byte aligned");
-  DM_REQUIRE(a.Cin2 == 0 || (a.x2 && aligned16(a.x2) && a.x2_pitch % 4 == 0 && a.taps >= 1),
-             "conv: segment-2 operand");
+  DM_REQUIRE(a.Cin2 == 0 || (a.x2 && aligned16(a.x2) && a.x2_pitch % 4 == 0), "conv: segment-2 operand");
+  DM_REQUIRE(a.Cout > 0 && a.B > 0 && a.Hin > 0 && a.Win > 0, "conv: empty problem");
   if (a.upsample) {
     DM_REQUIRE(a.Hout == 2 * a.Hin && a.Wout == 2 * a.Win, "conv: upsample output size");
   } else if (a.taps == 9) {
@@ -204,16 +272,19 @@ int conv2d_igemm(const ConvArgs& a, hipStream_t st) {
   }
   const long M = (long)a.B * a.Hout * a.Wout;
   DM_REQUIRE(M > 0 && M < (1L << 31), "conv: M out of range");
+  const int mode = conv_mode(a);
   switch (conv_pick(a)) {
-    case 0: return launch_conv<128, 128, 64, 64>(a, st);
-    case 1: return launch_conv<128, 64, 64, 32>(a, st);
-    default: return launch_conv<64, 64, 32, 32>(a, st);
+    case 0: return launch_conv_tile<128, 128, 64, 64>(a, mode, st);
+    case 1: return launch_conv_tile<128, 64, 64, 32>(a, mode, st);
+    default: return launch_conv_tile<64, 64, 32, 32>(a, mode, st);
   }
 }
 
 // Tile choice: prefer the 128x128 tile when it still yields >= 2 waves of
-// blocks over 256 CUs, else shrink to keep the machine busy.
+// blocks over 256 CUs, else shrink to keep the machine busy. `a.tile` (1..3)
+// forces a configuration (tests / tuning).
 int conv_pick(const ConvArgs& a) {
+  if (a.tile >= 1 && a.tile <= 3) return a.tile - 1;
   const long M = (long)a.B * a.Hout * a.Wout;
   const long b128 = ((M + 127) / 128) * ((a.Cout + 127) / 128);
   if (a.Cout >= 128 && b128 >= 512) return 0;

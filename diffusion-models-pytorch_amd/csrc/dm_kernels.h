@@ -28,6 +28,7 @@ struct ConvArgs {
   int rowvec_pitch;
   const float* res;     // residual at output resolution or null
   int res_pitch;
+  int tile;             // 0 auto, 1..3 force a tile configuration
 };
 
 struct GemmArgs {

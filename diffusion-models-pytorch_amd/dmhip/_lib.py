@@ -70,6 +70,7 @@ class ConvDesc(ctypes.Structure):
         ('Hout', ctypes.c_int), ('Wout', ctypes.c_int),
         ('bias', vp), ('rowvec', vp), ('rowvec_pitch', ctypes.c_int),
         ('res', vp), ('res_pitch', ctypes.c_int),
+        ('tile', ctypes.c_int),
     ]
 
 

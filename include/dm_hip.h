@@ -153,6 +153,7 @@ typedef struct dm_conv_desc {
   const float* bias;
   const float* rowvec; int rowvec_pitch;
   const float* res; int res_pitch;
+  int tile;  /* 0: automatic tile choice; 1..3 force 128x128 / 128x64 / 64x64 (tests, tuning) */
 } dm_conv_desc;
 int dm_conv2d_nhwc(const dm_conv_desc* d, void* stream);
 

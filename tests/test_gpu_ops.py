@@ -78,7 +78,7 @@ def _pack(w, cuda, K=None, col0=0, out=None):
 
 
 def _run_conv(cuda, x_nhwc, w_packed, Cout, Hout, Wout, taps, stride=1, upsample=0, bias=None, rowvec=None,
-              res=None, x2=None, Cin2=0, y_pitch=None, x_pitch=None):
+              res=None, x2=None, Cin2=0, y_pitch=None, x_pitch=None, tile=0):
     B, Hin, Win, Cin = x_nhwc.shape[0], x_nhwc.shape[1], x_nhwc.shape[2], x_nhwc.shape[3]
     x_pitch = x_pitch or Cin
     y_pitch = y_pitch or Cout
@@ -94,6 +94,7 @@ def _run_conv(cuda, x_nhwc, w_packed, Cout, Hout, Wout, taps, stride=1, upsample
     d.rowvec_pitch = rowvec.shape[1] if rowvec is not None else 0
     d.res = res.data_ptr() if res is not None else None
     d.res_pitch = res.shape[-1] if res is not None else 0
+    d.tile = tile
     dmhip.conv2d_nhwc(d, cuda)
     return y
 
@@ -102,22 +103,24 @@ def _nhwc(x):
     return x.permute(0, 2, 3, 1).contiguous()
 
 
+@pytest.mark.parametrize('tile', [0, 1, 2, 3])
 @pytest.mark.parametrize('B,Cin,Cout,H,stride,up', [
     (2, 32, 64, 8, 1, 0), (3, 64, 32, 16, 2, 0), (2, 32, 32, 4, 1, 1), (1, 128, 256, 16, 1, 0),
-    (5, 64, 64, 4, 1, 0), (2, 96, 160, 8, 2, 0),
+    (5, 64, 64, 4, 1, 0), (2, 96, 160, 8, 2, 0), (3, 32, 96, 5, 1, 0), (2, 64, 64, 7, 2, 0),
 ])
-def test_conv3x3_exact(cuda, B, Cin, Cout, H, stride, up):
+def test_conv3x3_exact(cuda, B, Cin, Cout, H, stride, up, tile):
     x = _ints((B, Cin, H, H), -2, 3, seed=10)
     w = _ints((Cout, Cin, 3, 3), -2, 3, seed=11)
     b = _ints((Cout, ), seed=12)
     xin = F.interpolate(x, scale_factor=2, mode='nearest') if up else x
     ref = F.conv2d(xin.double(), w.double(), b.double(), stride=stride, padding=1).float()
     Hout = ref.shape[-1]
-    y = _run_conv(cuda, _nhwc(x).to(cuda), _pack(w, cuda), Cout, Hout, Hout, 9, stride, up, b.to(cuda))
+    y = _run_conv(cuda, _nhwc(x).to(cuda), _pack(w, cuda), Cout, Hout, Hout, 9, stride, up, b.to(cuda), tile=tile)
     assert torch.equal(y.cpu(), _nhwc(ref))
 
 
-def test_conv_segments_rowvec_residual_pitch(cuda):
+@pytest.mark.parametrize('tile', [0, 1, 2, 3])
+def test_conv_segments_rowvec_residual_pitch(cuda, tile):
     # ResBlock second conv with the shortcut folded in as a 1x1 K segment, temb rowvec, pitched output
     B, C1, C2, Cout, H = 3, 64, 32, 64, 8
     h = _ints((B, C1, H, H), seed=20)
@@ -133,7 +136,7 @@ def test_conv_segments_rowvec_residual_pitch(cuda):
     ref = (F.conv2d(h.double(), w2.double(), b.double(), padding=1) + rv.double()[:, :, None, None]
            + F.conv2d(x.double(), ws.double())).float()
     y = _run_conv(cuda, _nhwc(h).to(cuda), wp, Cout, H, H, 9, bias=b.to(cuda), rowvec=rv.to(cuda),
-                  x2=_nhwc(x).to(cuda), Cin2=C2, y_pitch=96)
+                  x2=_nhwc(x).to(cuda), Cin2=C2, y_pitch=96, tile=tile)
     assert torch.equal(y[..., :Cout].cpu(), _nhwc(ref))
     assert torch.isnan(y[..., Cout:]).all()  # channels outside the view untouched
 
