@@ -85,9 +85,8 @@ conv_igemm_kernel(ConvArgs a) {
     wrow[j] = a.w + (size_t)(w_ok[j] ? n : N - 1) * a.K + 4 * lc4;
   }
 
-  const int ct_per_tap = a.Cin1 / kBK;       // K-slices per tap
   const int taps = (MODE == CM_1X1) ? 1 : 9;
-  const int nk1 = taps * ct_per_tap;
+  const int nk1 = taps * (a.Cin1 / kBK);
   const int nk = nk1 + a.Cin2 / kBK;
 
   // Row pointers / validity for the current tap.
@@ -135,8 +134,9 @@ conv_igemm_kernel(ConvArgs a) {
   f4 ra[Cfg::A_ITERS], rb[Cfg::B_ITERS];
   bool ra_ok[Cfg::A_ITERS];
   const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
-  // Loader state: the slice about to be loaded is (tap, channel offset) or segment 2.
-  int ld_tap = 0, ld_c = 0;
+  // Loader state: K slice kt = chunk * taps + tap (chunk-major, matching the
+  // packed weights), then segment 2.
+  int ld_c = 0;
   auto load_tile = [&](int kt) {
 #pragma unroll
     for (int i = 0; i < Cfg::A_ITERS; ++i) {
@@ -145,16 +145,17 @@ conv_igemm_kernel(ConvArgs a) {
     }
 #pragma unroll
     for (int j = 0; j < Cfg::B_ITERS; ++j) rb[j] = *reinterpret_cast<const f4*>(wrow[j] + kt * kBK);
-    // advance (wave-uniform control flow only)
-    ld_c += kBK;
-    if (kt + 1 < nk1) {
-      if (ld_c == a.Cin1) {
-        ld_c = 0;
-        set_tap(++ld_tap);
-      }
-    } else if (kt + 1 == nk1) {
+    // advance to slice kt + 1 (wave-uniform control flow only)
+    const int nx = kt + 1;
+    if (nx < nk1) {
+      const int chunk = (MODE == CM_1X1) ? nx : nx / 9;
+      set_tap((MODE == CM_1X1) ? 0 : nx - chunk * 9);
+      ld_c = chunk * kBK;
+    } else if (nx == nk1) {
       ld_c = 0;
       set_seg2();
+    } else {
+      ld_c += kBK;
     }
   };
 
@@ -272,19 +273,33 @@ int conv2d_igemm(const ConvArgs& a, hipStream_t st) {
   }
   const long M = (long)a.B * a.Hout * a.Wout;
   DM_REQUIRE(M > 0 && M < (1L << 31), "conv: M out of range");
+  DM_REQUIRE(a.tile >= 0 && a.tile <= 6, "conv: tile must be 0..6");
   const int mode = conv_mode(a);
-  switch (conv_pick(a)) {
+  const int pick = conv_pick(a);
+  if (pick >= 3) {
+    PatchGeom g;
+    conv_patch_pick(a, g);
+    return conv2d_patch(a, pick + 1, g, st);
+  }
+  switch (pick) {
     case 0: return launch_conv_tile<128, 128, 64, 64>(a, mode, st);
     case 1: return launch_conv_tile<128, 64, 64, 32>(a, mode, st);
     default: return launch_conv_tile<64, 64, 32, 32>(a, mode, st);
   }
 }
 
-// Tile choice: prefer the 128x128 tile when it still yields >= 2 waves of
-// blocks over 256 CUs, else shrink to keep the machine busy. `a.tile` (1..3)
-// forces a configuration (tests / tuning).
+// Kernel choice: 0..2 im2col tiles (128x128, 128x64, 64x64), 3..5 halo-patch
+// tiles (same shapes). The patch kernel handles 3x3 stride-1 / upsample
+// shapes whose tile covers whole rows; otherwise the im2col kernel, with the
+// 128x128 tile when it still yields >= 2 waves of blocks over 256 CUs.
+// `a.tile` 1..6 forces a configuration (tests / tuning); a forced patch tile
+// falls back to im2col when the shape does not tile.
 int conv_pick(const ConvArgs& a) {
   if (a.tile >= 1 && a.tile <= 3) return a.tile - 1;
+  PatchGeom g;
+  const int p = conv_patch_pick(a, g);
+  if (p) return p - 1;
+  if (a.tile >= 4) return a.tile - 4;
   const long M = (long)a.B * a.Hout * a.Wout;
   const long b128 = ((M + 127) / 128) * ((a.Cout + 127) / 128);
   if (a.Cout >= 128 && b128 >= 512) return 0;
@@ -295,7 +310,8 @@ int conv_pick(const ConvArgs& a) {
 
 std::string conv_label(const ConvArgs& a) {
   static const char* names[] = {"conv_igemm_kernel<128,128,64,64>", "conv_igemm_kernel<128,64,64,32>",
-                                "conv_igemm_kernel<64,64,32,32>"};
+                                "conv_igemm_kernel<64,64,32,32>",   "conv_patch_kernel<128,128,64,64>",
+                                "conv_patch_kernel<128,64,64,32>",  "conv_patch_kernel<64,64,32,32>"};
   return names[conv_pick(a)];
 }
 

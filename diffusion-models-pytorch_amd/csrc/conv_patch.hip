@@ -1,0 +1,310 @@
+// 3x3 convolution (stride 1, or nearest-2x upsample + stride 1) with the
+// input halo patch staged in LDS once per 32-channel chunk.
+//
+// Same GEMM view and epilogue as conv.hip (models/unet.py:16,26,41,43,
+// models/modules.py:62-65), but A is not re-gathered from global memory for
+// every tap: a block's output tile covers TB images x TH rows x the full
+// width, so its receptive field is a (TH+2) x (W+2) pixel patch per image.
+// Per channel chunk the patch is loaded once (zero padding written as zeros)
+// and the nine taps read shifted A fragments from it; only the weights
+// stream per tap. Global/L2 traffic for A drops ~9x / (halo factor) versus
+// the im2col loader, and the LDS write volume for A likewise.
+//
+// K order inside the packed weight matrix: k = (chunk * 9 + tap) * 32 + c
+// (chunk-major), followed by an optional 1x1 segment (the ResBlock shortcut)
+// of Cin2 columns, handled by a second, un-pipelined phase.
+#include "dm_common.h"
+#include "dm_kernels.h"
+#include "mfma_tile.h"
+
+namespace dm {
+
+namespace {
+
+__device__ __forceinline__ int xcd_remap_p(int bid, int nblk) {
+  const int q = nblk >> 3, r = nblk & 7;
+  const int xcd = bid & 7, idx = bid >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+template <int BM, int BN, int WM, int WN, bool UP, int MAXP>
+__global__ void __launch_bounds__(256)
+conv_patch_kernel(ConvArgs a, PatchGeom g) {
+  using Cfg = TileCfg<BM, BN, WM, WN>;
+  constexpr int PATCH_FLOATS = MAXP * kLDK;
+  constexpr int WSTAGE = BN * kLDK;
+  __shared__ __attribute__((aligned(16))) float lds[PATCH_FLOATS + 2 * WSTAGE];
+  float* patch = lds;
+  float* wbuf = lds + PATCH_FLOATS;
+
+  const int M = a.B * a.Hout * a.Wout;
+  const int N = a.Cout;
+  const int nN = ceil_div(N, BN);
+  const int bid = xcd_remap_p(blockIdx.x, gridDim.x);
+  const int mt = bid / nN, nt = bid - (bid / nN) * nN;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int HWo = a.Hout * a.Wout;
+  const int b0 = m0 / HWo;
+  const int y0 = (m0 - b0 * HWo) / a.Wout;  // first output row of the tile (even for UP)
+
+  const int t = threadIdx.x;
+  const int lane = t & 63, wave = t >> 6;
+  const int wm = wave / Cfg::NWN, wn = wave % Cfg::NWN;
+  const int lc4 = t & 7;
+  const int lrow = t >> 3;
+  const int lr = lane & 31, lh = lane >> 5;
+
+  // ---- patch loader geometry (pixel p = lrow + 32 j)
+  constexpr int PJ = (MAXP + 31) / 32;
+  const int PHW = g.PH * g.PW;
+  const float* psrc[PJ];
+  bool pok[PJ];
+  const int iy_base = UP ? (y0 >> 1) - 1 : y0 - 1;
+#pragma unroll
+  for (int j = 0; j < PJ; ++j) {
+    const int p = lrow + 32 * j;
+    const int img = p / PHW;
+    const int rem = p - img * PHW;
+    const int pr = rem / g.PW, pc = rem - (rem / g.PW) * g.PW;
+    const int b = b0 + img;
+    const int iy = iy_base + pr, ix = pc - 1;
+    const bool ok = p < g.P && b < a.B && iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
+    pok[j] = ok;
+    const int bc = min(b, a.B - 1);
+    const int iyc = min(max(iy, 0), a.Hin - 1), ixc = min(max(ix, 0), a.Win - 1);
+    psrc[j] = a.x1 + ((size_t)(bc * a.Hin + iyc) * a.Win + ixc) * a.x1_pitch + 4 * lc4;
+  }
+  // ---- weight loader
+  const float* wrow[Cfg::B_ITERS];
+  bool w_ok[Cfg::B_ITERS];
+#pragma unroll
+  for (int j = 0; j < Cfg::B_ITERS; ++j) {
+    const int n = n0 + lrow + j * Cfg::ROWS_PER_PASS;
+    w_ok[j] = n < N;
+    wrow[j] = a.w + (size_t)(w_ok[j] ? n : N - 1) * a.K + 4 * lc4;
+  }
+
+  // ---- A-fragment patch coordinates of this lane's rows
+  int fy[Cfg::TM], fx[Cfg::TM], fimg[Cfg::TM];
+  const int tile_rows = g.TH * a.Wout;
+#pragma unroll
+  for (int i = 0; i < Cfg::TM; ++i) {
+    const int ml = wm * WM + i * 32 + lr;
+    fimg[i] = ml / tile_rows;
+    const int rem = ml - fimg[i] * tile_rows;
+    fy[i] = rem / a.Wout;
+    fx[i] = rem - fy[i] * a.Wout;
+  }
+
+  const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  f4 rp[PJ], rb[Cfg::B_ITERS];
+  auto load_patch = [&](int chunk) {
+    const int co = chunk * kBK;
+#pragma unroll
+    for (int j = 0; j < PJ; ++j) rp[j] = *reinterpret_cast<const f4*>(psrc[j] + co);
+  };
+  auto store_patch = [&]() {
+#pragma unroll
+    for (int j = 0; j < PJ; ++j) {
+      const int p = lrow + 32 * j;
+      if (j * 32 < MAXP && p < MAXP)
+        *reinterpret_cast<f4*>(patch + p * kLDK + 4 * lc4) = pok[j] ? rp[j] : zero4;
+    }
+  };
+  auto load_w = [&](int kt) {
+#pragma unroll
+    for (int j = 0; j < Cfg::B_ITERS; ++j) rb[j] = *reinterpret_cast<const f4*>(wrow[j] + kt * kBK);
+  };
+  auto store_w = [&](int buf) {
+    float* Bs = wbuf + buf * WSTAGE;
+#pragma unroll
+    for (int j = 0; j < Cfg::B_ITERS; ++j)
+      *reinterpret_cast<f4*>(Bs + (lrow + j * Cfg::ROWS_PER_PASS) * kLDK + 4 * lc4) = w_ok[j] ? rb[j] : zero4;
+  };
+
+  f16v acc[Cfg::TM][Cfg::TN];
+#pragma unroll
+  for (int i = 0; i < Cfg::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < Cfg::TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // One 32-deep K slice: A rows from the patch at tap (ky, kx), B from wbuf[buf].
+  auto compute_tap = [&](int ky, int kx, int buf) {
+    int abase[Cfg::TM];
+#pragma unroll
+    for (int i = 0; i < Cfg::TM; ++i) {
+      int pr, pc;
+      if (UP) {
+        pr = ((fy[i] + ky - 1) >> 1) + 1;
+        pc = ((fx[i] + kx - 1) >> 1) + 1;
+      } else {
+        pr = fy[i] + ky;
+        pc = fx[i] + kx;
+      }
+      abase[i] = ((fimg[i] * g.PH + pr) * g.PW + pc) * kLDK + 4 * lh;
+    }
+    const float* Bs = wbuf + buf * WSTAGE;
+#pragma unroll
+    for (int kc = 0; kc < kBK; kc += 8) {
+      f4 av[Cfg::TM], bv[Cfg::TN];
+#pragma unroll
+      for (int i = 0; i < Cfg::TM; ++i) av[i] = *reinterpret_cast<const f4*>(patch + abase[i] + kc);
+#pragma unroll
+      for (int j = 0; j < Cfg::TN; ++j)
+        bv[j] = *reinterpret_cast<const f4*>(Bs + (wn * WN + j * 32 + lr) * kLDK + kc + 4 * lh);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < Cfg::TM; ++i)
+#pragma unroll
+          for (int j = 0; j < Cfg::TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i][s], bv[j][s], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  const int nchunks = a.Cin1 / kBK;
+  load_patch(0);
+  load_w(0);
+  store_patch();
+  store_w(0);
+  __syncthreads();
+  for (int c = 0; c < nchunks; ++c) {
+    const bool more_chunks = c + 1 < nchunks;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int kt = c * 9 + tap;
+      const bool more_w = (tap < 8) || more_chunks;
+      if (more_w) load_w(kt + 1);
+      if (tap == 0 && more_chunks) load_patch(c + 1);
+      compute_tap(tap / 3, tap % 3, kt & 1);
+      if (more_w) store_w((kt + 1) & 1);
+      __syncthreads();
+    }
+    if (more_chunks) {
+      store_patch();
+      __syncthreads();
+    }
+  }
+
+  // ---- segment 2: 1x1 product of x2 (ResBlock shortcut), K = Cin2, un-pipelined.
+  if (a.Cin2 > 0) {
+    const int k2base = 9 * a.Cin1;
+    float* As = patch;  // BM x kLDK fits in the patch region (P >= BM for the stride-1 geometry)
+    for (int c2 = 0; c2 < a.Cin2; c2 += kBK) {
+      f4 ra[Cfg::A_ITERS];
+      bool rok[Cfg::A_ITERS];
+#pragma unroll
+      for (int i = 0; i < Cfg::A_ITERS; ++i) {
+        const int m = m0 + lrow + i * Cfg::ROWS_PER_PASS;
+        rok[i] = m < M;
+        ra[i] = *reinterpret_cast<const f4*>(a.x2 + (size_t)min(m, M - 1) * a.x2_pitch + c2 + 4 * lc4);
+      }
+      load_w((k2base + c2) / kBK);
+#pragma unroll
+      for (int i = 0; i < Cfg::A_ITERS; ++i)
+        *reinterpret_cast<f4*>(As + (lrow + i * Cfg::ROWS_PER_PASS) * kLDK + 4 * lc4) = rok[i] ? ra[i] : zero4;
+      store_w(0);
+      __syncthreads();
+      mfma_slice<Cfg::TM, Cfg::TN>(As, wbuf, wm * WM, wn * WN, lane, acc);
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue (as conv.hip)
+  const bool block_one_image = (HWo % BM) == 0;
+#pragma unroll
+  for (int j = 0; j < Cfg::TN; ++j) {
+    const int n = n0 + wn * WN + j * 32 + lr;
+    if (n >= N) continue;
+    const float bn = a.bias ? a.bias[n] : 0.f;
+    const float rv_blk = (a.rowvec && block_one_image) ? a.rowvec[(size_t)b0 * a.rowvec_pitch + n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < Cfg::TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * WM + i * 32 + acc_row(r, lh);
+        if (m >= M) continue;
+        float v = acc[i][j][r];
+        if (a.bias) v = v + bn;
+        if (a.rowvec) v = v + (block_one_image ? rv_blk : a.rowvec[(size_t)(m / HWo) * a.rowvec_pitch + n]);
+        if (a.res) v = v + a.res[(size_t)m * a.res_pitch + n];
+        a.y[(size_t)m * a.y_pitch + n] = v;
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int MAXP>
+int launch_patch(const ConvArgs& a, const PatchGeom& g, hipStream_t st) {
+  const int M = a.B * a.Hout * a.Wout;
+  const int blocks = ceil_div(M, BM) * ceil_div(a.Cout, BN);
+  if (a.upsample)
+    hipLaunchKernelGGL((conv_patch_kernel<BM, BN, WM, WN, true, MAXP>), dim3(blocks), dim3(256), 0, st, a, g);
+  else
+    hipLaunchKernelGGL((conv_patch_kernel<BM, BN, WM, WN, false, MAXP>), dim3(blocks), dim3(256), 0, st, a, g);
+  DM_LAUNCH_CHECK();
+  return DM_OK;
+}
+
+}  // namespace
+
+// Patch geometry for a BM-row tile, or false when the shape does not tile
+// (then the im2col kernel is used).
+bool conv_patch_geom(const ConvArgs& a, int BM, PatchGeom& g) {
+  if (a.taps != 9 || a.stride != 1) return false;
+  const int Ho = a.Hout, Wo = a.Wout;
+  if (Wo > BM || BM % Wo != 0) return false;
+  const int rows = BM / Wo;  // output rows per tile (across images)
+  if (rows <= Ho) {
+    if (Ho % rows != 0) return false;
+    g.TB = 1;
+    g.TH = rows;
+  } else {
+    if (rows % Ho != 0) return false;
+    g.TB = rows / Ho;
+    g.TH = Ho;
+  }
+  if (a.upsample) {
+    if (g.TH % 2 != 0 || a.Cin2 != 0) return false;
+    g.PH = g.TH / 2 + 2;
+    g.PW = a.Win + 2;
+  } else {
+    g.PH = g.TH + 2;
+    g.PW = Wo + 2;
+  }
+  g.P = g.TB * g.PH * g.PW;
+  if (a.Cin2 > 0 && g.P < BM) return false;
+  return true;
+}
+
+constexpr int kPatchMax128 = 288;
+constexpr int kPatchMax64 = 160;
+
+int conv_patch_pick(const ConvArgs& a, PatchGeom& g) {
+  if (a.tile == 4 || a.tile == 0) {
+    const long M = (long)a.B * a.Hout * a.Wout;
+    const long b128 = ((M + 127) / 128) * ((a.Cout + 127) / 128);
+    const long b128x64 = ((M + 127) / 128) * ((a.Cout + 63) / 64);
+    if ((a.tile == 4 || (a.Cout >= 128 && b128 >= 512)) && conv_patch_geom(a, 128, g) && g.P <= kPatchMax128)
+      return 4;
+    if (a.tile == 0 && b128x64 >= 512 && conv_patch_geom(a, 128, g) && g.P <= kPatchMax128) return 5;
+    if (a.tile == 0 && conv_patch_geom(a, 64, g) && g.P <= kPatchMax64) return 6;
+  } else if (a.tile == 5) {
+    if (conv_patch_geom(a, 128, g) && g.P <= kPatchMax128) return 5;
+  } else if (a.tile == 6) {
+    if (conv_patch_geom(a, 64, g) && g.P <= kPatchMax64) return 6;
+  }
+  return 0;
+}
+
+int conv2d_patch(const ConvArgs& a, int which, const PatchGeom& g, hipStream_t st) {
+  switch (which) {
+    case 4: return launch_patch<128, 128, 64, 64, kPatchMax128>(a, g, st);
+    case 5: return launch_patch<128, 64, 64, 32, kPatchMax128>(a, g, st);
+    default: return launch_patch<64, 64, 32, 32, kPatchMax64>(a, g, st);
+  }
+}
+
+}  // namespace dm

@@ -28,7 +28,12 @@ struct ConvArgs {
   int rowvec_pitch;
   const float* res;     // residual at output resolution or null
   int res_pitch;
-  int tile;             // 0 auto, 1..3 force a tile configuration
+  int tile;             // 0 auto; 1..3 force an im2col tile, 4..6 a halo-patch tile
+};
+
+// Output tile = TB images x TH rows x full width; input patch PH x PW per image.
+struct PatchGeom {
+  int TB, TH, PH, PW, P;
 };
 
 struct GemmArgs {
@@ -81,6 +86,9 @@ int gn_apply(const View& x, int G, const double2* part, int nchunk, float eps, c
              const View& y, hipStream_t st);
 int conv2d_igemm(const ConvArgs& a, hipStream_t st);
 int conv_pick(const ConvArgs& a);
+bool conv_patch_geom(const ConvArgs& a, int BM, PatchGeom& g);
+int conv_patch_pick(const ConvArgs& a, PatchGeom& g);
+int conv2d_patch(const ConvArgs& a, int which, const PatchGeom& g, hipStream_t st);
 std::string conv_label(const ConvArgs& a);
 int gemm_batched(const GemmArgs& g, hipStream_t st);
 int gemm_pick(const GemmArgs& g);

@@ -229,7 +229,10 @@ __global__ void nhwc_to_nchw_kernel(const float* __restrict__ x, int B, int C, i
   y[e] = x[((size_t)b * HW + p) * pitch + c];
 }
 
-// [Cout][Cin][kh][kw] -> [Cout][kh*kw][Cin] written at row pitch ldw, column offset col0
+// [Cout][Cin][kh][kw] -> implicit-GEMM rows [Cout][ldw] at column offset col0.
+// 3x3: chunk-major K order k = ((ci / 32) * 9 + tap) * 32 + ci % 32, so the
+// nine taps of one 32-channel chunk are consecutive K slices (both conv
+// kernels walk K this way); 1x1: k = ci.
 __global__ void repack_conv_kernel(const float* __restrict__ w, int Cout, int Cin, int taps,
                                    float* __restrict__ out, int ldw, int col0) {
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -238,7 +241,8 @@ __global__ void repack_conv_kernel(const float* __restrict__ w, int Cout, int Ci
   const int co = e / ((long)Cin * taps);
   const int r = e - (long)co * Cin * taps;
   const int ci = r / taps, tap = r % taps;
-  out[(size_t)co * ldw + col0 + tap * Cin + ci] = w[e];
+  const int k = taps == 1 ? ci : ((ci >> 5) * taps + tap) * 32 + (ci & 31);
+  out[(size_t)co * ldw + col0 + k] = w[e];
 }
 
 }  // namespace
@@ -311,6 +315,7 @@ int nhwc_to_nchw(const float* x, int B, int C, int HW, int pitch, float* y, hipS
 }
 
 int repack_conv(const float* w, int Cout, int Cin, int taps, float* out, int ldw, int col0, hipStream_t st) {
+  DM_REQUIRE(taps == 1 || Cin % 32 == 0, "conv weight packing: 3x3 input channels must be multiples of 32");
   const long total = (long)Cout * Cin * taps;
   hipLaunchKernelGGL(repack_conv_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, w, Cout, Cin,
                      taps, out, ldw, col0);

@@ -1,0 +1,86 @@
+"""Data-parallel sampling harness (reference scripts/sample_uncond.py:179-195,
+scripts/sample_cfg.py:157-182), independent of the launcher.
+
+One process per GPU. Each rank draws its own init noise (seeded seed + rank,
+as accelerate's set_seed(device_specific=True)), samples a fold of `bspp`
+images fully independently, and the fold is gathered once over the process
+group (RCCL `all_gather_into_tensor` on ROCm, gloo on CPU) in rank order;
+only the first `bs` images of each fold are kept, exactly as
+`accelerator.gather(samples)[:bs]`.
+"""
+import math
+import os
+from typing import Callable, Iterable, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from utils.misc import amortize
+
+
+class DistEnv:
+    """Process-group view taken from torchrun / accelerate style env vars."""
+
+    def __init__(self, backend: Optional[str] = None):
+        self.world = int(os.environ.get('WORLD_SIZE', '1'))
+        self.rank = int(os.environ.get('RANK', '0'))
+        self.local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+        if torch.cuda.is_available():
+            self.device = torch.device('cuda', self.local_rank)
+            torch.cuda.set_device(self.device)
+        else:
+            self.device = torch.device('cpu')
+        if self.world > 1 and not dist.is_initialized():
+            backend = backend or ('nccl' if self.device.type == 'cuda' else 'gloo')
+            kw = dict(device_id=self.device) if backend == 'nccl' else {}
+            dist.init_process_group(backend, **kw)
+
+    @property
+    def is_main(self):
+        return self.rank == 0
+
+    def barrier(self):
+        if self.world > 1:
+            dist.barrier()
+
+    def gather(self, x: torch.Tensor) -> torch.Tensor:
+        """Concatenate every rank's tensor along dim 0 in rank order (accelerate.gather)."""
+        if self.world == 1:
+            return x
+        x = x.contiguous()
+        out = torch.empty((self.world * x.shape[0], *x.shape[1:]), dtype=x.dtype, device=x.device)
+        if x.device.type == 'cuda':
+            dist.all_gather_into_tensor(out, x)
+        else:
+            dist.all_gather(list(out.chunk(self.world)), x)
+        return out
+
+    def close(self):
+        if self.world > 1 and dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def per_process_batch(n_samples: int, batch_size: int, world: int) -> int:
+    """bspp of sample_uncond.py:182."""
+    return min(batch_size, math.ceil(n_samples / world))
+
+
+def sample_folds(sample_fn: Callable[[torch.Tensor], torch.Tensor], img_shape, n_samples: int, batch_size: int,
+                 env: DistEnv, noise_fn: Callable[[tuple], torch.Tensor],
+                 sink: Optional[Callable[[int, torch.Tensor], None]] = None) -> List[int]:
+    """Run the fold loop of sample_uncond.py:179-195.
+
+    sample_fn(init_noise) -> samples on this rank; noise_fn(shape) draws this
+    rank's init noise; sink(first_index, images) receives the gathered images
+    of a fold on rank 0. Returns the fold sizes."""
+    bspp = per_process_batch(n_samples, batch_size, env.world)
+    folds = amortize(n_samples, bspp * env.world)
+    idx = 0
+    for bs in folds:
+        init_noise = noise_fn((bspp, *img_shape))
+        samples = sample_fn(init_noise).clamp(-1, 1)
+        samples = env.gather(samples)[:bs]
+        if env.is_main and sink is not None:
+            sink(idx, samples)
+        idx += bs
+    return folds

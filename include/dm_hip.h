@@ -153,7 +153,8 @@ typedef struct dm_conv_desc {
   const float* bias;
   const float* rowvec; int rowvec_pitch;
   const float* res; int res_pitch;
-  int tile;  /* 0: automatic tile choice; 1..3 force 128x128 / 128x64 / 64x64 (tests, tuning) */
+  int tile;  /* 0: automatic; 1..3 force the im2col kernel with a 128x128 / 128x64 / 64x64 tile,
+                4..6 the halo-patch kernel with those tiles (tests, tuning) */
 } dm_conv_desc;
 int dm_conv2d_nhwc(const dm_conv_desc* d, void* stream);
 

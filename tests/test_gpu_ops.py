@@ -103,10 +103,11 @@ def _nhwc(x):
     return x.permute(0, 2, 3, 1).contiguous()
 
 
-@pytest.mark.parametrize('tile', [0, 1, 2, 3])
+@pytest.mark.parametrize('tile', [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize('B,Cin,Cout,H,stride,up', [
     (2, 32, 64, 8, 1, 0), (3, 64, 32, 16, 2, 0), (2, 32, 32, 4, 1, 1), (1, 128, 256, 16, 1, 0),
     (5, 64, 64, 4, 1, 0), (2, 96, 160, 8, 2, 0), (3, 32, 96, 5, 1, 0), (2, 64, 64, 7, 2, 0),
+    (4, 64, 128, 32, 1, 0), (3, 64, 64, 16, 1, 1), (2, 32, 64, 8, 1, 1), (3, 32, 32, 2, 1, 1),
 ])
 def test_conv3x3_exact(cuda, B, Cin, Cout, H, stride, up, tile):
     x = _ints((B, Cin, H, H), -2, 3, seed=10)
@@ -119,7 +120,7 @@ def test_conv3x3_exact(cuda, B, Cin, Cout, H, stride, up, tile):
     assert torch.equal(y.cpu(), _nhwc(ref))
 
 
-@pytest.mark.parametrize('tile', [0, 1, 2, 3])
+@pytest.mark.parametrize('tile', [0, 1, 2, 3, 4, 5, 6])
 def test_conv_segments_rowvec_residual_pitch(cuda, tile):
     # ResBlock second conv with the shortcut folded in as a 1x1 K segment, temb rowvec, pitched output
     B, C1, C2, Cout, H = 3, 64, 32, 64, 8

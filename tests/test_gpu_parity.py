@@ -97,7 +97,7 @@ def test_sampler_update_bit_exact(cuda, golden, kind):
             else:
                 assert np.array_equal(got, ref[k].numpy()), (kind, t, k, np.abs(got - ref[k].numpy()).max())
             # cross-host: 1-ulp coefficient differences, amplified where sqrt(1/ac - 1) is small
-            assert np.allclose(got, arrays[f'{kind}_{k}'][i], rtol=1e-5, atol=1e-6), (kind, t, k)
+            assert np.allclose(got, arrays[f'{kind}_{k}'][i], rtol=1e-5, atol=2e-5), (kind, t, k)
 
 
 def test_cfg_update_bit_exact(cuda, golden):
