@@ -56,6 +56,18 @@ extern "C" int dm_groupnorm_nhwc(const float* x, int x_pitch, float* y, int y_pi
                       mod_shift, mod_pitch, silu ? 1 : 0, vy, st);
 }
 
+extern "C" int dm_groupnorm_affine(const float* x, int x_pitch, int B, int HW, int C, int G, float eps,
+                                   const float* gamma, const float* beta, float* scale, float* shift, void* scratch,
+                                   void* stream) {
+  if (!x || !scale || !shift || !scratch) { dm::set_error("null tensor"); return DM_ERR_ARG; }
+  if (B <= 0 || HW <= 0 || C <= 0 || G <= 0) { dm::set_error("invalid shape"); return DM_ERR_ARG; }
+  View vx{const_cast<float*>(x), B, HW, 1, C, x_pitch};
+  hipStream_t st = (hipStream_t)stream;
+  int rc = dm::gn_partial(vx, G, (double2*)scratch, st);
+  if (rc) return rc;
+  return dm::gn_finalize(vx, G, (const double2*)scratch, eps, gamma, beta, scale, shift, st);
+}
+
 extern "C" int dm_pack_conv_weight(const float* w, int Cout, int Cin, int taps, float* out, int ldw, int col0,
                                    void* stream) {
   if (!w || !out) { dm::set_error("null tensor"); return DM_ERR_ARG; }
@@ -77,6 +89,8 @@ extern "C" int dm_conv2d_nhwc(const dm_conv_desc* d, void* stream) {
   a.bias = d->bias; a.rowvec = d->rowvec; a.rowvec_pitch = d->rowvec_pitch;
   a.res = d->res; a.res_pitch = d->res_pitch;
   a.tile = d->tile;
+  a.pro_scale = d->pro_scale;
+  a.pro_shift = d->pro_shift;
   return dm::conv2d_igemm(a, (hipStream_t)stream);
 }
 

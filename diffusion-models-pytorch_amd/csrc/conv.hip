@@ -276,6 +276,8 @@ int conv2d_igemm(const ConvArgs& a, hipStream_t st) {
   DM_REQUIRE(a.tile >= 0 && a.tile <= 6, "conv: tile must be 0..6");
   const int mode = conv_mode(a);
   const int pick = conv_pick(a);
+  DM_REQUIRE(!a.pro_scale || (pick >= 3 && a.pro_shift && aligned16(a.pro_scale) && aligned16(a.pro_shift)),
+             "conv: the GroupNorm prologue needs a halo-patch shape (3x3 stride 1 / upsample, whole-row tiles)");
   if (pick >= 3) {
     PatchGeom g;
     conv_patch_pick(a, g);

@@ -27,7 +27,7 @@ __device__ __forceinline__ int xcd_remap_p(int bid, int nblk) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
-template <int BM, int BN, int WM, int WN, bool UP, int MAXP>
+template <int BM, int BN, int WM, int WN, bool UP, int MAXP, bool PRO>
 __global__ void __launch_bounds__(256)
 conv_patch_kernel(ConvArgs a, PatchGeom g) {
   using Cfg = TileCfg<BM, BN, WM, WN>;
@@ -59,6 +59,7 @@ conv_patch_kernel(ConvArgs a, PatchGeom g) {
   const int PHW = g.PH * g.PW;
   const float* psrc[PJ];
   bool pok[PJ];
+  int pimg[PJ];
   const int iy_base = UP ? (y0 >> 1) - 1 : y0 - 1;
 #pragma unroll
   for (int j = 0; j < PJ; ++j) {
@@ -71,6 +72,7 @@ conv_patch_kernel(ConvArgs a, PatchGeom g) {
     const bool ok = p < g.P && b < a.B && iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
     pok[j] = ok;
     const int bc = min(b, a.B - 1);
+    pimg[j] = bc;
     const int iyc = min(max(iy, 0), a.Hin - 1), ixc = min(max(ix, 0), a.Win - 1);
     psrc[j] = a.x1 + ((size_t)(bc * a.Hin + iyc) * a.Win + ixc) * a.x1_pitch + 4 * lc4;
   }
@@ -103,12 +105,26 @@ conv_patch_kernel(ConvArgs a, PatchGeom g) {
 #pragma unroll
     for (int j = 0; j < PJ; ++j) rp[j] = *reinterpret_cast<const f4*>(psrc[j] + co);
   };
+  // GroupNorm + SiLU prologue on patch registers j in [j0, j1): silu(x * scale[b][c] + shift[b][c]).
+  // Spread over the taps of the previous chunk so the VALU work interleaves with MFMAs.
+  auto transform = [&](int chunk, int j0, int j1) {
+    const int cc = chunk * kBK + 4 * lc4;
+#pragma unroll
+    for (int j = 0; j < PJ; ++j) {
+      if (j >= j0 && j < j1) {
+        const f4 sc = *reinterpret_cast<const f4*>(a.pro_scale + (size_t)pimg[j] * a.Cin1 + cc);
+        const f4 sh = *reinterpret_cast<const f4*>(a.pro_shift + (size_t)pimg[j] * a.Cin1 + cc);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) rp[j][q] = silu_f(rp[j][q] * sc[q] + sh[q]);
+      }
+    }
+  };
+  // padding stays exactly 0 (applied after the transform)
   auto store_patch = [&]() {
 #pragma unroll
     for (int j = 0; j < PJ; ++j) {
       const int p = lrow + 32 * j;
-      if (j * 32 < MAXP && p < MAXP)
-        *reinterpret_cast<f4*>(patch + p * kLDK + 4 * lc4) = pok[j] ? rp[j] : zero4;
+      if (j * 32 < MAXP && p < MAXP) *reinterpret_cast<f4*>(patch + p * kLDK + 4 * lc4) = pok[j] ? rp[j] : zero4;
     }
   };
   auto load_w = [&](int kt) {
@@ -167,6 +183,7 @@ conv_patch_kernel(ConvArgs a, PatchGeom g) {
   const int nchunks = a.Cin1 / kBK;
   load_patch(0);
   load_w(0);
+  if (PRO) transform(0, 0, PJ);
   store_patch();
   store_w(0);
   __syncthreads();
@@ -178,6 +195,10 @@ conv_patch_kernel(ConvArgs a, PatchGeom g) {
       const bool more_w = (tap < 8) || more_chunks;
       if (more_w) load_w(kt + 1);
       if (tap == 0 && more_chunks) load_patch(c + 1);
+      if (PRO && tap >= 1 && more_chunks) {
+        constexpr int per = (PJ + 7) / 8;
+        transform(c + 1, (tap - 1) * per, tap == 8 ? PJ : tap * per);
+      }
       compute_tap(tap / 3, tap % 3, kt & 1);
       if (more_w) store_w((kt + 1) & 1);
       __syncthreads();
@@ -240,10 +261,18 @@ template <int BM, int BN, int WM, int WN, int MAXP>
 int launch_patch(const ConvArgs& a, const PatchGeom& g, hipStream_t st) {
   const int M = a.B * a.Hout * a.Wout;
   const int blocks = ceil_div(M, BM) * ceil_div(a.Cout, BN);
-  if (a.upsample)
-    hipLaunchKernelGGL((conv_patch_kernel<BM, BN, WM, WN, true, MAXP>), dim3(blocks), dim3(256), 0, st, a, g);
-  else
-    hipLaunchKernelGGL((conv_patch_kernel<BM, BN, WM, WN, false, MAXP>), dim3(blocks), dim3(256), 0, st, a, g);
+  const bool pro = a.pro_scale != nullptr;
+  if (a.upsample) {
+    if (pro)
+      hipLaunchKernelGGL((conv_patch_kernel<BM, BN, WM, WN, true, MAXP, true>), dim3(blocks), dim3(256), 0, st, a, g);
+    else
+      hipLaunchKernelGGL((conv_patch_kernel<BM, BN, WM, WN, true, MAXP, false>), dim3(blocks), dim3(256), 0, st, a, g);
+  } else {
+    if (pro)
+      hipLaunchKernelGGL((conv_patch_kernel<BM, BN, WM, WN, false, MAXP, true>), dim3(blocks), dim3(256), 0, st, a, g);
+    else
+      hipLaunchKernelGGL((conv_patch_kernel<BM, BN, WM, WN, false, MAXP, false>), dim3(blocks), dim3(256), 0, st, a, g);
+  }
   DM_LAUNCH_CHECK();
   return DM_OK;
 }

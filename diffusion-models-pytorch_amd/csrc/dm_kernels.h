@@ -29,6 +29,11 @@ struct ConvArgs {
   const float* res;     // residual at output resolution or null
   int res_pitch;
   int tile;             // 0 auto; 1..3 force an im2col tile, 4..6 a halo-patch tile
+  // optional operand prologue on segment 1 (halo-patch kernel only):
+  // x -> silu(x * pro_scale[b][c] + pro_shift[b][c]) before the product
+  // (GroupNorm + SiLU of the ResBlock, fused into the conv's input load)
+  const float* pro_scale;
+  const float* pro_shift;
 };
 
 // Output tile = TB images x TH rows x full width; input patch PH x PW per image.
@@ -54,6 +59,11 @@ struct GemmArgs {
   const float* res;     // residual [M][ld_res] (batch 0 layout only) or null
   int ld_res;
   int act;              // 0 none, 1 SiLU
+  // optional GroupNorm affine on A elements: a[m][k] * pro_scale[img][k] + pro_shift[img][k],
+  // img = (z1 * M + m) / pro_rows (rows per image); fused norm of the attention block's input
+  const float* pro_scale;
+  const float* pro_shift;
+  int pro_rows;
 };
 
 struct StepArgs {
@@ -81,6 +91,8 @@ struct StepArgs {
 
 int gn_num_chunks(int HW);
 int gn_partial(const View& x, int G, double2* part, hipStream_t st);
+int gn_finalize(const View& x, int G, const double2* part, float eps, const float* gamma, const float* beta,
+                float* scale, float* shift, hipStream_t st);
 int gn_apply(const View& x, int G, const double2* part, int nchunk, float eps, const float* gamma,
              const float* beta, const float* mod_scale, const float* mod_shift, int mod_pitch, int act,
              const View& y, hipStream_t st);
@@ -97,7 +109,8 @@ int timestep_embed(const int64_t* t, int B, int dim, int kind, const float* freq
 int softmax_rows(float* x, long rows, int L, int ld, hipStream_t st);
 int conv3x3_small_in(const float* x, int B, int Cin, int H, int W, const float* w, const float* bias,
                      int Cout, const View& y, hipStream_t st);
-int conv3x3_small_out(const View& x, const float* w, const float* bias, int Cout, float* y, hipStream_t st);
+int conv3x3_small_out(const View& x, const float* w, const float* bias, int Cout, float* y, hipStream_t st,
+                      const float* pro_scale = nullptr, const float* pro_shift = nullptr);
 int sampler_step(const StepArgs& s, hipStream_t st);
 int nchw_to_nhwc(const float* x, int B, int C, int HW, float* y, int y_pitch, hipStream_t st);
 int nhwc_to_nchw(const float* x, int B, int C, int HW, int pitch, float* y, hipStream_t st);

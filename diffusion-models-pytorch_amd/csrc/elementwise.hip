@@ -72,77 +72,116 @@ __global__ void softmax_rows_kernel(float* __restrict__ x, long rows, int L, int
 }
 
 // first conv: NCHW input with few channels -> NHWC (pitched) output.
-// One block per (image, output row).
-__global__ void conv3x3_small_in_kernel(const float* __restrict__ x, int Cin, int H, int W,
-                                        const float* __restrict__ w, const float* __restrict__ bias,
-                                        int Cout, float* __restrict__ y, int y_pitch) {
-  extern __shared__ float rows[];  // [Cin][3][W + 2]
+// One block per (image, output row). Thread t owns output channel co = t % Cout
+// (its 9*Cin weights live in registers) and every (256/Cout)-th pixel of the row;
+// the three input rows sit in LDS and are read as broadcasts (all lanes of a
+// wave share the pixel). Stores are coalesced over co.
+template <int CIN>
+__global__ void __launch_bounds__(256) conv3x3_small_in_kernel(const float* __restrict__ x, int H, int W,
+                                                               const float* __restrict__ w,
+                                                               const float* __restrict__ bias, int Cout,
+                                                               float* __restrict__ y, int y_pitch) {
+  extern __shared__ float rows[];  // [CIN][3][W + 2]
   const int b = blockIdx.y, oy = blockIdx.x;
   const int Wp = W + 2;
-  for (int i = threadIdx.x; i < Cin * 3 * Wp; i += blockDim.x) {
+  for (int i = threadIdx.x; i < CIN * 3 * Wp; i += blockDim.x) {
     const int ci = i / (3 * Wp);
     const int rr = (i / Wp) % 3;
     const int xx = i % Wp - 1;
     const int iy = oy + rr - 1;
     float v = 0.f;
-    if (iy >= 0 && iy < H && xx >= 0 && xx < W) v = x[(((size_t)b * Cin + ci) * H + iy) * W + xx];
+    if (iy >= 0 && iy < H && xx >= 0 && xx < W) v = x[(((size_t)b * CIN + ci) * H + iy) * W + xx];
     rows[i] = v;
   }
   __syncthreads();
-  for (int idx = threadIdx.x; idx < W * Cout; idx += blockDim.x) {
-    const int ox = idx / Cout, co = idx - (idx / Cout) * Cout;
-    float acc = 0.f;
-    for (int ci = 0; ci < Cin; ++ci)
-      for (int ky = 0; ky < 3; ++ky)
-        for (int kx = 0; kx < 3; ++kx)
-          acc += w[((co * Cin + ci) * 3 + ky) * 3 + kx] * rows[(ci * 3 + ky) * Wp + ox + kx];
-    acc = acc + bias[co];
-    y[(((size_t)b * H + oy) * W + ox) * y_pitch + co] = acc;
+  const int lanes_per_px = min(Cout, (int)blockDim.x);
+  const int px_par = blockDim.x / lanes_per_px;
+  for (int co = threadIdx.x % lanes_per_px; co < Cout; co += lanes_per_px) {
+    float wr[CIN * 9];
+#pragma unroll
+    for (int k = 0; k < CIN * 9; ++k) wr[k] = w[(size_t)co * CIN * 9 + k];
+    const float bc = bias[co];
+    for (int ox = threadIdx.x / lanes_per_px; ox < W; ox += px_par) {
+      float acc = 0.f;
+#pragma unroll
+      for (int ci = 0; ci < CIN; ++ci)
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) acc += wr[(ci * 3 + ky) * 3 + kx] * rows[(ci * 3 + ky) * Wp + ox + kx];
+      y[(((size_t)b * H + oy) * W + ox) * y_pitch + co] = acc + bc;
+    }
   }
 }
 
-// last conv: NHWC (pitched) input -> NCHW output with few channels.
-template <int MAXC>
-__global__ void conv3x3_small_out_kernel(const float* __restrict__ x, int B, int H, int W, int Cin,
-                                         int pitch, const float* __restrict__ w,
-                                         const float* __restrict__ bias, int Cout,
-                                         float* __restrict__ y) {
-  extern __shared__ float wl[];  // [9][Cin][Cout]
-  for (int i = threadIdx.x; i < 9 * Cin * Cout; i += blockDim.x) {
-    const int co = i % Cout;
-    const int ci = (i / Cout) % Cin;
-    const int tap = i / (Cout * Cin);
-    wl[i] = w[((size_t)co * Cin + ci) * 9 + tap];
-  }
-  __syncthreads();
-  const long pix = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long M = (long)B * H * W;
-  if (pix >= M) return;
-  const int b = pix / (H * W);
-  const int rem = pix - (long)b * H * W;
-  const int oy = rem / W, ox = rem % W;
-  float acc[MAXC];
+// last conv: NHWC (pitched) input -> NCHW output with few channels (Cout <= 8).
+// Block = TH x TW output pixels of one image, one pixel per thread. Per 32-channel
+// chunk the (TH+2) x (TW+2) halo patch and the chunk's weights ([tap][c][8]) are
+// staged in LDS; each thread accumulates its Cout outputs from the patch.
+constexpr int kSoTW = 32, kSoTH = 8, kSoPP = (kSoTH + 2) * (kSoTW + 2), kSoLD = 36;
+__global__ void __launch_bounds__(256) conv3x3_small_out_kernel(const float* __restrict__ x, int B, int H, int W,
+                                                                int Cin, int pitch, const float* __restrict__ w,
+                                                                const float* __restrict__ bias, int Cout,
+                                                                float* __restrict__ y,
+                                                                const float* __restrict__ pro_scale,
+                                                                const float* __restrict__ pro_shift) {
+  __shared__ __attribute__((aligned(16))) float patch[kSoPP * kSoLD];
+  __shared__ __attribute__((aligned(16))) float wl[9 * 32 * 8];
+  const int tiles_x = ceil_div(W, kSoTW), tiles_y = ceil_div(H, kSoTH);
+  const int b = blockIdx.x / (tiles_x * tiles_y);
+  const int trem = blockIdx.x - b * tiles_x * tiles_y;
+  const int ty0 = (trem / tiles_x) * kSoTH, tx0 = (trem % tiles_x) * kSoTW;
+  const int t = threadIdx.x;
+  const int py = t / kSoTW, px = t % kSoTW;
+  float acc[8];
 #pragma unroll
-  for (int c = 0; c < MAXC; ++c) acc[c] = 0.f;
-  for (int tap = 0; tap < 9; ++tap) {
-    const int iy = oy + tap / 3 - 1, ix = ox + tap % 3 - 1;
-    if (iy < 0 || iy >= H || ix < 0 || ix >= W) continue;
-    const float* src = x + (((size_t)b * H + iy) * W + ix) * pitch;
-    const float* wt = wl + tap * Cin * Cout;
-    for (int ci = 0; ci < Cin; ci += 4) {
-      const float4 v = *reinterpret_cast<const float4*>(src + ci);
-      const float vv[4] = {v.x, v.y, v.z, v.w};
+  for (int c = 0; c < 8; ++c) acc[c] = 0.f;
+  for (int c0 = 0; c0 < Cin; c0 += 32) {
+    __syncthreads();
+    for (int i = t; i < kSoPP * 8; i += blockDim.x) {
+      const int p = i >> 3, c4 = i & 7;
+      const int iy = ty0 + p / (kSoTW + 2) - 1, ix = tx0 + p % (kSoTW + 2) - 1;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (iy >= 0 && iy < H && ix >= 0 && ix < W && c0 + 4 * c4 < Cin) {
+        v = *reinterpret_cast<const float4*>(x + (((size_t)b * H + iy) * W + ix) * pitch + c0 + 4 * c4);
+        if (pro_scale) {  // GroupNorm + SiLU of last_conv (models/unet.py:115-119), padding stays 0
+          const float4 sc = *reinterpret_cast<const float4*>(pro_scale + (size_t)b * Cin + c0 + 4 * c4);
+          const float4 sh = *reinterpret_cast<const float4*>(pro_shift + (size_t)b * Cin + c0 + 4 * c4);
+          v.x = silu_f(v.x * sc.x + sh.x); v.y = silu_f(v.y * sc.y + sh.y);
+          v.z = silu_f(v.z * sc.z + sh.z); v.w = silu_f(v.w * sc.w + sh.w);
+        }
+      }
+      *reinterpret_cast<float4*>(patch + p * kSoLD + 4 * c4) = v;
+    }
+    for (int i = t; i < 9 * 32 * 8; i += blockDim.x) {
+      const int co = i & 7, c = (i >> 3) & 31, tap = i >> 8;
+      wl[i] = (co < Cout && c0 + c < Cin) ? w[((size_t)co * Cin + c0 + c) * 9 + tap] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int tap = 0; tap < 9; ++tap) {
+      const float* pr = patch + ((py + tap / 3) * (kSoTW + 2) + px + tap % 3) * kSoLD;
+      const float* wt = wl + tap * 256;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int c4 = 0; c4 < 8; ++c4) {
+        const float4 v = *reinterpret_cast<const float4*>(pr + 4 * c4);
+        const float vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int c = 0; c < MAXC; ++c)
-          if (c < Cout) acc[c] += vv[q] * wt[(ci + q) * Cout + c];
+        for (int q = 0; q < 4; ++q) {
+          const float4 wa = *reinterpret_cast<const float4*>(wt + (4 * c4 + q) * 8);
+          const float4 wb = *reinterpret_cast<const float4*>(wt + (4 * c4 + q) * 8 + 4);
+          acc[0] += vv[q] * wa.x; acc[1] += vv[q] * wa.y; acc[2] += vv[q] * wa.z; acc[3] += vv[q] * wa.w;
+          acc[4] += vv[q] * wb.x; acc[5] += vv[q] * wb.y; acc[6] += vv[q] * wb.z; acc[7] += vv[q] * wb.w;
+        }
       }
     }
   }
+  const int oy = ty0 + py, ox = tx0 + px;
+  if (oy < H && ox < W) {
 #pragma unroll
-  for (int c = 0; c < MAXC; ++c)
-    if (c < Cout) y[(((size_t)b * Cout + c) * H + oy) * W + ox] = acc[c] + bias[c];
+    for (int c = 0; c < 8; ++c)
+      if (c < Cout) y[(((size_t)b * Cout + c) * H + oy) * W + ox] = acc[c] + bias[c];
+  }
 }
 
 __global__ void sampler_step_kernel(StepArgs s) {
@@ -266,23 +305,29 @@ int softmax_rows(float* x, long rows, int L, int ld, hipStream_t st) {
 
 int conv3x3_small_in(const float* x, int B, int Cin, int H, int W, const float* w, const float* bias,
                      int Cout, const View& y, hipStream_t st) {
-  DM_REQUIRE(Cin >= 1 && Cin <= 16, "first conv: Cin out of range");
+  DM_REQUIRE(Cin >= 1 && Cin <= 4, "first conv: Cin out of range (1..4)");
   DM_REQUIRE(y.C == Cout && y.H == H && y.W == W && y.B == B, "first conv: output view mismatch");
   size_t smem = (size_t)Cin * 3 * (W + 2) * sizeof(float);
-  hipLaunchKernelGGL(conv3x3_small_in_kernel, dim3(H, B), dim3(256), smem, st, x, Cin, H, W, w, bias, Cout,
-                     y.p, y.pitch);
+  DM_REQUIRE(smem <= 64 * 1024, "first conv: image too wide");
+  dim3 grid(H, B);
+  switch (Cin) {
+    case 1: hipLaunchKernelGGL(conv3x3_small_in_kernel<1>, grid, dim3(256), smem, st, x, H, W, w, bias, Cout, y.p, y.pitch); break;
+    case 2: hipLaunchKernelGGL(conv3x3_small_in_kernel<2>, grid, dim3(256), smem, st, x, H, W, w, bias, Cout, y.p, y.pitch); break;
+    case 3: hipLaunchKernelGGL(conv3x3_small_in_kernel<3>, grid, dim3(256), smem, st, x, H, W, w, bias, Cout, y.p, y.pitch); break;
+    default: hipLaunchKernelGGL(conv3x3_small_in_kernel<4>, grid, dim3(256), smem, st, x, H, W, w, bias, Cout, y.p, y.pitch); break;
+  }
   DM_LAUNCH_CHECK();
   return DM_OK;
 }
 
-int conv3x3_small_out(const View& x, const float* w, const float* bias, int Cout, float* y, hipStream_t st) {
+int conv3x3_small_out(const View& x, const float* w, const float* bias, int Cout, float* y, hipStream_t st,
+                      const float* pro_scale, const float* pro_shift) {
   DM_REQUIRE(Cout >= 1 && Cout <= 8, "last conv: Cout out of range");
   DM_REQUIRE(x.C % 4 == 0 && x.pitch % 4 == 0, "last conv: channel alignment");
-  size_t smem = (size_t)9 * x.C * Cout * sizeof(float);
-  DM_REQUIRE(smem <= 64 * 1024, "last conv: weights exceed LDS budget");
-  const long M = (long)x.B * x.H * x.W;
-  hipLaunchKernelGGL((conv3x3_small_out_kernel<8>), dim3((unsigned)((M + 255) / 256)), dim3(256), smem, st,
-                     x.p, x.B, x.H, x.W, x.C, x.pitch, w, bias, Cout, y);
+  DM_REQUIRE((reinterpret_cast<uintptr_t>(x.p) & 15) == 0, "last conv: input must be 16-byte aligned");
+  const long tiles = (long)x.B * ceil_div(x.H, kSoTH) * ceil_div(x.W, kSoTW);
+  hipLaunchKernelGGL(conv3x3_small_out_kernel, dim3((unsigned)tiles), dim3(256), 0, st, x.p, x.B, x.H, x.W, x.C,
+                     x.pitch, w, bias, Cout, y, pro_scale, pro_shift);
   DM_LAUNCH_CHECK();
   return DM_OK;
 }

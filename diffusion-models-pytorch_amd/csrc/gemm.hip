@@ -43,38 +43,55 @@ gemm_kernel(GemmArgs g) {
   static_assert(!B_KN || (Cfg::NT % KN_C4 == 0), "BN loader geometry");
 
   const int nk = ceil_div(g.K, kBK);
+  const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  // Branch-free loaders: rows/columns outside the problem read a clamped, valid
+  // address and are zeroed when written to LDS (after the MFMA work), so the
+  // next slice's loads stay in flight across the current slice's MFMAs.
+  const float* arow[Cfg::A_ITERS];
+  bool a_ok[Cfg::A_ITERS];
+  int a_img[Cfg::A_ITERS];
+#pragma unroll
+  for (int i = 0; i < Cfg::A_ITERS; ++i) {
+    const int m = m0 + lrow + i * Cfg::ROWS_PER_PASS;
+    a_ok[i] = m < g.M;
+    const int mc = min(m, g.M - 1);
+    arow[i] = A + (size_t)mc * g.lda + 4 * lc4;
+    a_img[i] = g.pro_scale ? (z1 * g.M + mc) / g.pro_rows : 0;
+  }
+  const float* brow[B_KN ? 1 : Cfg::B_ITERS];
+  bool b_ok[B_KN ? 1 : Cfg::B_ITERS];
+  if constexpr (!B_KN) {
+#pragma unroll
+    for (int j = 0; j < Cfg::B_ITERS; ++j) {
+      const int n = n0 + lrow + j * Cfg::ROWS_PER_PASS;
+      b_ok[j] = n < g.N;
+      brow[j] = Bm + (size_t)min(n, g.N - 1) * g.ldb + 4 * lc4;
+    }
+  }
   f4 ra[Cfg::A_ITERS];
   f4 rb[B_KN ? KN_ITERS : Cfg::B_ITERS];
-  const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  bool k_ok = true;
+  bool kn_ok[B_KN ? KN_ITERS : 1];
+  int ld_k = 0;
 
   auto load_tile = [&](int kt) {
     const int k = kt * kBK + 4 * lc4;
+    k_ok = k < g.K;
+    ld_k = k_ok ? k : 0;
+    const int kofs = ld_k - 4 * lc4;
 #pragma unroll
-    for (int i = 0; i < Cfg::A_ITERS; ++i) {
-      const int m = m0 + lrow + i * Cfg::ROWS_PER_PASS;
-      if (m < g.M && k < g.K) {
-        f4 v = *reinterpret_cast<const f4*>(A + (size_t)m * g.lda + k);
-        if (g.alpha != 1.0f) v = v * g.alpha;
-        ra[i] = v;
-      } else {
-        ra[i] = zero4;
-      }
-    }
+    for (int i = 0; i < Cfg::A_ITERS; ++i) ra[i] = *reinterpret_cast<const f4*>(arow[i] + kofs);
     if constexpr (!B_KN) {
 #pragma unroll
-      for (int j = 0; j < Cfg::B_ITERS; ++j) {
-        const int n = n0 + lrow + j * Cfg::ROWS_PER_PASS;
-        rb[j] = (n < g.N && k < g.K) ? *reinterpret_cast<const f4*>(Bm + (size_t)n * g.ldb + k) : zero4;
-      }
+      for (int j = 0; j < Cfg::B_ITERS; ++j) rb[j] = *reinterpret_cast<const f4*>(brow[j] + kofs);
     } else {
       const int n4 = t % KN_C4, kr = t / KN_C4;
+      const int n = min(n0 + 4 * n4, g.N - 4);
 #pragma unroll
       for (int j = 0; j < KN_ITERS; ++j) {
         const int kk = kt * kBK + kr + j * KN_ROWS_PER_PASS;
-        const int n = n0 + 4 * n4;
-        rb[j] = (kr + j * KN_ROWS_PER_PASS < kBK && kk < g.K && n < g.N)
-                    ? *reinterpret_cast<const f4*>(Bm + (size_t)kk * g.ldb + n)
-                    : zero4;
+        kn_ok[j] = (kr + j * KN_ROWS_PER_PASS < kBK) && kk < g.K && n0 + 4 * n4 < g.N;
+        rb[j] = *reinterpret_cast<const f4*>(Bm + (size_t)min(kk, g.K - 1) * g.ldb + n);
       }
     }
   };
@@ -83,20 +100,31 @@ gemm_kernel(GemmArgs g) {
     float* As = lds + buf * Cfg::STAGE;
     float* Bs = As + Cfg::A_ELEMS;
 #pragma unroll
-    for (int i = 0; i < Cfg::A_ITERS; ++i)
-      *reinterpret_cast<f4*>(As + (lrow + i * Cfg::ROWS_PER_PASS) * kLDK + 4 * lc4) = ra[i];
+    for (int i = 0; i < Cfg::A_ITERS; ++i) {
+      f4 v = ra[i];
+      if (g.pro_scale) {  // fused GroupNorm (no activation): x * scale[img][k] + shift[img][k]
+        const f4 sc = *reinterpret_cast<const f4*>(g.pro_scale + (size_t)a_img[i] * g.K + ld_k);
+        const f4 sh = *reinterpret_cast<const f4*>(g.pro_shift + (size_t)a_img[i] * g.K + ld_k);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = v[q] * sc[q] + sh[q];
+      }
+      if (g.alpha != 1.0f) v = v * g.alpha;
+      *reinterpret_cast<f4*>(As + (lrow + i * Cfg::ROWS_PER_PASS) * kLDK + 4 * lc4) = (a_ok[i] && k_ok) ? v : zero4;
+    }
     if constexpr (!B_KN) {
 #pragma unroll
       for (int j = 0; j < Cfg::B_ITERS; ++j)
-        *reinterpret_cast<f4*>(Bs + (lrow + j * Cfg::ROWS_PER_PASS) * kLDK + 4 * lc4) = rb[j];
+        *reinterpret_cast<f4*>(Bs + (lrow + j * Cfg::ROWS_PER_PASS) * kLDK + 4 * lc4) =
+            (b_ok[j] && k_ok) ? rb[j] : zero4;
     } else {
       const int n4 = t % KN_C4, kr = t / KN_C4;
 #pragma unroll
       for (int j = 0; j < KN_ITERS; ++j) {
         const int kk = kr + j * KN_ROWS_PER_PASS;
         if (kk < kBK) {
+          const f4 v = kn_ok[j] ? rb[j] : zero4;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) Bs[(4 * n4 + q) * kLDK + kk] = rb[j][q];
+          for (int q = 0; q < 4; ++q) Bs[(4 * n4 + q) * kLDK + kk] = v[q];
         }
       }
     }
@@ -166,6 +194,7 @@ int gemm_batched(const GemmArgs& g, hipStream_t st) {
   DM_REQUIRE((reinterpret_cast<uintptr_t>(g.A) & 15) == 0 && (reinterpret_cast<uintptr_t>(g.Bm) & 15) == 0,
              "gemm: operands must be 16-byte aligned");
   DM_REQUIRE(g.Z1 >= 1 && g.Z2 >= 1 && (long)g.Z1 * g.Z2 <= 65535, "gemm: batch out of range");
+  DM_REQUIRE(!g.pro_scale || (g.pro_shift && g.pro_rows > 0 && !g.b_kn), "gemm: A prologue needs scale, shift, rows");
   if (gemm_pick(g) == 0) return launch_gemm<128, 128, 64, 64>(g, st);
   return launch_gemm<64, 64, 32, 32>(g, st);
 }

@@ -132,6 +132,32 @@ __global__ void gn_apply_kernel(const float* __restrict__ x, int HW, int C, int 
   }
 }
 
+// part [B][nchunk][G] -> per-(image, channel) affine: scale = rstd * gamma,
+// shift = -scale * mean + beta (the exact arithmetic of gn_apply_kernel), so a
+// consumer can apply the norm inside its own operand load.
+__global__ void gn_finalize_kernel(const double2* __restrict__ part, int B, int nchunk, int G, int C, double n,
+                                   float eps, const float* __restrict__ gamma, const float* __restrict__ beta,
+                                   float* __restrict__ scale, float* __restrict__ shift) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= B * C) return;
+  const int b = idx / C, c = idx - (idx / C) * C;
+  const int cpg = C / G, g = c / cpg;
+  double a = 0, q = 0;
+  for (int k = 0; k < nchunk; ++k) {
+    const double2 v = part[((size_t)b * nchunk + k) * G + g];
+    a += v.x;
+    q += v.y;
+  }
+  const double m = a / n;
+  double var = q / n - m * m;
+  if (var < 0) var = 0;
+  const float mu = (float)m;
+  const float rs = (float)(1.0 / sqrt(var + (double)eps));
+  const float sc = rs * (gamma ? gamma[c] : 1.0f);
+  scale[idx] = sc;
+  shift[idx] = -sc * mu + (beta ? beta[c] : 0.0f);
+}
+
 inline int gn_block_threads(int C) {
   int C4 = C / 4;
   int t = C4 > 256 ? C4 : 256;
@@ -158,6 +184,17 @@ int gn_partial(const View& x, int G, double2* part, hipStream_t st) {
   dim3 grid(nchunk, x.B);
   hipLaunchKernelGGL(gn_partial_kernel, grid, dim3(threads), smem, st, x.p, HW, x.C, x.pitch, G,
                      kGnPixPerChunk, nchunk, part);
+  DM_LAUNCH_CHECK();
+  return DM_OK;
+}
+
+int gn_finalize(const View& x, int G, const double2* part, float eps, const float* gamma, const float* beta,
+                float* scale, float* shift, hipStream_t st) {
+  DM_REQUIRE(x.C % G == 0, "GroupNorm finalize: C must be divisible by groups");
+  const int HW = x.H * x.W;
+  const int n = x.B * x.C;
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, st, part, x.B, gn_num_chunks(HW), G,
+                     x.C, (double)HW * (x.C / G), eps, gamma, beta, scale, shift);
   DM_LAUNCH_CHECK();
   return DM_OK;
 }

@@ -499,6 +499,11 @@ int UNetModel::build_plan(int B, int H, int W) {
   float* Sb = alloc(std::max<size_t>(max_S, 1) * 4);
   float* Ob = alloc(std::max<size_t>(max_attn, 1) * 4);
   double2* part = (double2*)alloc((size_t)B * max_chunks * G * sizeof(double2));
+  // per-(image, channel) GroupNorm affine for the fused conv prologues
+  size_t max_c = (size_t)D;
+  for (auto& n : nodes) max_c = std::max(max_c, (size_t)std::max(n.cin, n.cout));
+  float* gsc = alloc((size_t)B * max_c * 4);
+  float* gsh = alloc((size_t)B * max_c * 4);
 
   // --- concat buffers for up-RBs and skip slot views
   std::vector<View> skip_view(skip_C.size());
@@ -601,23 +606,12 @@ int UNetModel::build_plan(int B, int H, int W) {
       View va1{a1, B, Hi, Wi, r.cin, r.cin};
       View vh{hbuf, B, Hi, Wi, r.cout, r.cout};
       View va2{a2, B, Hi, Wi, r.cout, r.cout};
-      add("gn_partial", 0, gn_bytes(xin, false), [=](hipStream_t st) { return gn_partial(xin, G, part, st); });
-      add("gn_apply", 0, gn_bytes(xin, true), [=](hipStream_t st) {
-        return gn_apply(xin, G, part, nchunk, 1e-5f, self->P(r.gn1.g), self->P(r.gn1.b), nullptr, nullptr, 0, 1,
-                        va1, st);
-      });
       ConvArgs c1{};
-      c1.x1 = a1; c1.x1_pitch = r.cin; c1.Cin1 = r.cin; c1.Hin = Hi; c1.Win = Wi;
+      c1.x1_pitch = r.cin; c1.Cin1 = r.cin; c1.Hin = Hi; c1.Win = Wi;
       c1.taps = 9; c1.stride = 1; c1.upsample = 0;
       c1.w = P(r.conv1.w); c1.K = r.conv1.K;
       c1.y = hbuf; c1.y_pitch = r.cout; c1.Cout = r.cout; c1.B = B; c1.Hout = Hi; c1.Wout = Wi;
       c1.bias = P(r.conv1.bias); c1.rowvec = projs + r.proj_col; c1.rowvec_pitch = proj_total;
-      add_conv(c1);
-      add("gn_partial", 0, gn_bytes(vh, false), [=](hipStream_t st) { return gn_partial(vh, G, part, st); });
-      add("gn_apply", 0, gn_bytes(vh, true), [=](hipStream_t st) {
-        return gn_apply(vh, G, part, nchunk, 1e-5f, self->P(r.gn2.g), self->P(r.gn2.b), nullptr, nullptr, 0, 1,
-                        va2, st);
-      });
       ConvArgs c2{};
       c2.x1 = a2; c2.x1_pitch = r.cout; c2.Cin1 = r.cout; c2.Hin = Hi; c2.Win = Wi;
       c2.taps = 9; c2.stride = 1;
@@ -629,20 +623,50 @@ int UNetModel::build_plan(int B, int H, int W) {
       } else {
         c2.res = xin.p; c2.res_pitch = xin.pitch;
       }
+      const bool fuse1 = conv_pick(c1) >= 3, fuse2 = conv_pick(c2) >= 3;
+      add("gn_partial", 0, gn_bytes(xin, false), [=](hipStream_t st) { return gn_partial(xin, G, part, st); });
+      if (fuse1) {
+        // GroupNorm + SiLU folded into conv1's patch load: x read once, normalised tensor never stored
+        add("gn_finalize", 0, 8.0 * B * r.cin, [=](hipStream_t st) {
+          return gn_finalize(xin, G, part, 1e-5f, self->P(r.gn1.g), self->P(r.gn1.b), gsc, gsh, st);
+        });
+        c1.x1 = xin.p; c1.x1_pitch = xin.pitch;
+        c1.pro_scale = gsc; c1.pro_shift = gsh;
+      } else {
+        add("gn_apply", 0, gn_bytes(xin, true), [=](hipStream_t st) {
+          return gn_apply(xin, G, part, nchunk, 1e-5f, self->P(r.gn1.g), self->P(r.gn1.b), nullptr, nullptr, 0, 1,
+                          va1, st);
+        });
+        c1.x1 = a1;
+      }
+      add_conv(c1);
+      add("gn_partial", 0, gn_bytes(vh, false), [=](hipStream_t st) { return gn_partial(vh, G, part, st); });
+      if (fuse2) {
+        add("gn_finalize", 0, 8.0 * B * r.cout, [=](hipStream_t st) {
+          return gn_finalize(vh, G, part, 1e-5f, self->P(r.gn2.g), self->P(r.gn2.b), gsc, gsh, st);
+        });
+        c2.x1 = hbuf;
+        c2.pro_scale = gsc; c2.pro_shift = gsh;
+      } else {
+        add("gn_apply", 0, gn_bytes(vh, true), [=](hipStream_t st) {
+          return gn_apply(vh, G, part, nchunk, 1e-5f, self->P(r.gn2.g), self->P(r.gn2.b), nullptr, nullptr, 0, 1,
+                          va2, st);
+        });
+      }
       add_conv(c2);
     } else if (n.kind == N_ATTN) {
       const AttnP p = attn[n.idx];
       const int C = p.C, heads = p.heads, Dh = C / heads;
-      View van{an, B, Hi, Wi, C, C};
+      // GroupNorm folded into the QKV projection's A load (modules.py:91-94): one pass over x
       add("gn_partial", 0, gn_bytes(xin, false), [=](hipStream_t st) { return gn_partial(xin, G, part, st); });
-      add("gn_apply", 0, gn_bytes(xin, true), [=](hipStream_t st) {
-        return gn_apply(xin, G, part, nchunk, 1e-5f, self->P(p.gn.g), self->P(p.gn.b), nullptr, nullptr, 0, 0,
-                        van, st);
+      add("gn_finalize", 0, 8.0 * B * C, [=](hipStream_t st) {
+        return gn_finalize(xin, G, part, 1e-5f, self->P(p.gn.g), self->P(p.gn.b), gsc, gsh, st);
       });
       GemmArgs gq{};
       gq.M = B * hw; gq.N = 3 * C; gq.K = C; gq.Z1 = 1; gq.Z2 = 1;
-      gq.A = an; gq.lda = C; gq.Bm = P(p.wqkv); gq.ldb = C; gq.C = qkv; gq.ldc = 3 * C;
+      gq.A = xin.p; gq.lda = xin.pitch; gq.Bm = P(p.wqkv); gq.ldb = C; gq.C = qkv; gq.ldc = 3 * C;
       gq.alpha = 1.f; gq.bias = P(p.bqkv);
+      gq.pro_scale = gsc; gq.pro_shift = gsh; gq.pro_rows = hw;
       add_gemm(gq);
       GemmArgs gs{};
       gs.M = hw; gs.N = hw; gs.K = Dh; gs.Z1 = B; gs.Z2 = heads;
@@ -689,11 +713,13 @@ int UNetModel::build_plan(int B, int H, int W) {
     const float* lb = P(last_b);
     const int oc = arch.out_channels;
     add("gn_partial", 0, gn_bytes(xin, false), [=](hipStream_t st) { return gn_partial(xin, G, part, st); });
-    add("gn_apply", 0, gn_bytes(xin, true), [=](hipStream_t st) {
-      return gn_apply(xin, G, part, nchunk, 1e-5f, self->P(lg.g), self->P(lg.b), nullptr, nullptr, 0, 1, va, st);
+    add("gn_finalize", 0, 8.0 * B * C, [=](hipStream_t st) {
+      return gn_finalize(xin, G, part, 1e-5f, self->P(lg.g), self->P(lg.b), gsc, gsh, st);
     });
+    (void)va;
+    (void)nchunk;
     add("conv3x3_small_out", 2.0 * B * H * W * oc * 9 * C, 4.0 * B * H * W * (C + oc),
-        [=](hipStream_t st) { return conv3x3_small_out(va, lw, lb, oc, P_->out, st); });
+        [=](hipStream_t st) { return conv3x3_small_out(xin, lw, lb, oc, P_->out, st, gsc, gsh); });
   }
   return DM_OK;
 }

@@ -189,8 +189,8 @@ class DDPM:
         d.xt = xt.data_ptr()
         d.model_out = model_output.data_ptr()
         d.model_out_uncond = model_output_uncond.data_ptr() if model_output_uncond is not None else None
-        d.w_uncond = float(torch.tensor(1 - guidance_scale, dtype=torch.float32))
-        d.w_cond = float(torch.tensor(guidance_scale, dtype=torch.float32))
+        d.w_uncond = 1 - guidance_scale   # ctypes rounds to float32, as torch does for the python scalar
+        d.w_cond = guidance_scale
         d.objective = _OBJECTIVES[objective or self.objective]
         d.clip_denoised = int(bool(self.clip_denoised))
         d.sqrt_recip_ac = c['sqrt_recip_ac']
@@ -210,7 +210,13 @@ class DDPM:
         if learned:
             var = var_t
         else:
-            var = c.get('var_scalar', torch.tensor(0.0)).to(xt.device)
+            # 0-dim device copy of the scalar variance, made once per (t, t_prev) and cached:
+            # a per-step host->device copy would stall the launch stream every step.
+            key = ('var_dev', xt.device)
+            var = c.get(key)
+            if var is None:
+                var = c.get('var_scalar', torch.tensor(0.0)).to(xt.device)
+                c[key] = var
         return dict(sample=sample, mean=mean, var=var, pred_x0=x0, pred_eps=eps, reverse_eps=noise)
 
     # ----------------------------------------------------------- public API

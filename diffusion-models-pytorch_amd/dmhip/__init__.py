@@ -17,6 +17,7 @@ from dmhip._lib import (  # noqa: F401
     UNetArch,
     sampler_step,
     groupnorm_nhwc,
+    groupnorm_affine,
     conv2d_nhwc,
     pack_conv_weight,
     gemm,

@@ -71,6 +71,7 @@ class ConvDesc(ctypes.Structure):
         ('bias', vp), ('rowvec', vp), ('rowvec_pitch', ctypes.c_int),
         ('res', vp), ('res_pitch', ctypes.c_int),
         ('tile', ctypes.c_int),
+        ('pro_scale', vp), ('pro_shift', vp),
     ]
 
 
@@ -110,6 +111,8 @@ def _declare(L: ctypes.CDLL):
     L.dm_groupnorm_scratch_bytes.restype = ctypes.c_int64
     L.dm_groupnorm_nhwc.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                     ctypes.c_int, ctypes.c_float, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, vp, vp]
+    L.dm_groupnorm_affine.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_float, vp, vp, vp, vp, vp, vp]
     L.dm_pack_conv_weight.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int,
                                       vp]
     L.dm_conv2d_nhwc.argtypes = [ctypes.POINTER(ConvDesc), vp]
@@ -193,6 +196,19 @@ def groupnorm_nhwc(x: torch.Tensor, y: torch.Tensor, B: int, HW: int, C: int, G:
     check(L.dm_groupnorm_nhwc(x.data_ptr(), x_pitch or C, y.data_ptr(), y_pitch or C, B, HW, C, G, eps,
                               _p(gamma), _p(beta), _p(mod_scale), _p(mod_shift), mod_pitch, int(silu),
                               scratch.data_ptr(), stream_handle(x.device)), 'dm_groupnorm_nhwc')
+
+
+def groupnorm_affine(x: torch.Tensor, B: int, HW: int, C: int, G: int, eps: float, gamma=None, beta=None,
+                     x_pitch: int = None):
+    """-> (scale, shift) [B, C] float32 device tensors."""
+    L = load()
+    scratch = torch.empty(max(1, L.dm_groupnorm_scratch_bytes(B, HW, G)), dtype=torch.uint8, device=x.device)
+    scale = torch.empty((B, C), device=x.device)
+    shift = torch.empty((B, C), device=x.device)
+    check(L.dm_groupnorm_affine(x.data_ptr(), x_pitch or C, B, HW, C, G, eps, _p(gamma), _p(beta),
+                                scale.data_ptr(), shift.data_ptr(), scratch.data_ptr(), stream_handle(x.device)),
+          'dm_groupnorm_affine')
+    return scale, shift
 
 
 def pack_conv_weight(w: torch.Tensor, out: torch.Tensor, ldw: int, col0: int = 0):

@@ -130,6 +130,7 @@ class UNet(nn.Module):
         self.last_conv = nn.Sequential(_gn(cur), nn.SiLU(), _conv(cur, out_channels, 3))
         self._native = None
         self._native_key = None
+        self._param_list = None
 
     # ----------------------------------------------------------- native side
     def _arch_struct(self) -> UNetArch:
@@ -145,28 +146,37 @@ class UNet(nn.Module):
         a.n_heads = self.arch['n_heads']
         return a
 
-    def _params_key(self, tensors: Sequence[Tensor]):
+    @staticmethod
+    def _params_key(tensors: Sequence[Tensor]):
+        # storage identity + in-place version counters: load_state_dict / optimizer steps /
+        # manual edits all bump _version, so the packed copy is refreshed on any change
         return (tuple(t.data_ptr() for t in tensors), sum(t._version for t in tensors))
 
     def _release_native(self):
-        if self._native is not None:
+        if getattr(self, '_native', None) is not None:
             load().dm_unet_destroy(self._native)
             self._native = None
             self._native_key = None
+        self._param_list = None
 
     def native_handle(self, device: torch.device):
         """Create (or reuse) the packed native model. Re-packs when parameters change."""
-        tensors = list(self.state_dict().values())
-        for i, p in enumerate(tensors):
+        tensors = getattr(self, '_param_list', None)
+        if tensors is None:
+            # the Parameter objects themselves (their version counters see in-place updates)
+            tensors = list(self.state_dict(keep_vars=True).values())
+            self._param_list = tensors
+        if self._native is not None and self._native_key == self._params_key(tensors):
+            return self._native
+        for p in tensors:
             if p.device != device:
                 raise RuntimeError(f'UNet parameters are on {p.device} but the input is on {device}; '
                                    f'move the model with .to(device) first')
             if p.dtype != torch.float32 or not p.is_contiguous():
                 raise TypeError('UNet parameters must be contiguous float32')
         key = self._params_key(tensors)
-        if self._native is not None and self._native_key == key:
-            return self._native
         self._release_native()
+        self._param_list = tensors
         L = load()
         n = len(tensors)
         ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in tensors])

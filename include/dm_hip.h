@@ -139,6 +139,11 @@ int dm_groupnorm_nhwc(const float* x, int x_pitch, float* y, int y_pitch, int B,
                       float eps, const float* gamma, const float* beta, const float* mod_scale,
                       const float* mod_shift, int mod_pitch, int silu, void* scratch, void* stream);
 
+/* GroupNorm statistics -> per-(image, channel) affine tables scale/shift [B][C]
+ * (y = x * scale + shift equals torch.nn.GroupNorm's output), for fused consumers. */
+int dm_groupnorm_affine(const float* x, int x_pitch, int B, int HW, int C, int G, float eps, const float* gamma,
+                        const float* beta, float* scale, float* shift, void* scratch, void* stream);
+
 /* Pack a torch conv weight [Cout][Cin][kh][kw] into the implicit-GEMM layout
  * [Cout][ldw] at column offset col0 (k = tap * Cin + c). */
 int dm_pack_conv_weight(const float* w, int Cout, int Cin, int taps, float* out, int ldw, int col0,
@@ -155,6 +160,10 @@ typedef struct dm_conv_desc {
   const float* res; int res_pitch;
   int tile;  /* 0: automatic; 1..3 force the im2col kernel with a 128x128 / 128x64 / 64x64 tile,
                 4..6 the halo-patch kernel with those tiles (tests, tuning) */
+  /* optional fused GroupNorm+SiLU of the input: x -> silu(x * pro_scale[b][c] + pro_shift[b][c]),
+   * [B][Cin] tables from dm_groupnorm_affine(); halo-patch shapes only (3x3 stride 1 / upsample) */
+  const float* pro_scale;
+  const float* pro_shift;
 } dm_conv_desc;
 int dm_conv2d_nhwc(const dm_conv_desc* d, void* stream);
 

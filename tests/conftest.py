@@ -37,6 +37,25 @@ def golden():
     return get
 
 
+_REPORT = {}
+
+
+@pytest.fixture(scope='session')
+def report():
+    """record(name, value): measured parity margins, written to gpurun_out/parity_report.json."""
+    def record(name, value):
+        _REPORT[name] = float(value)
+    return record
+
+
+def pytest_sessionfinish(session, exitstatus):
+    if _REPORT:
+        out = os.path.join(ROOT, 'gpurun_out')
+        os.makedirs(out, exist_ok=True)
+        with open(os.path.join(out, 'parity_report.json'), 'w') as f:
+            json.dump(_REPORT, f, indent=1, sort_keys=True)
+
+
 @pytest.fixture(scope='session')
 def cuda():
     import torch

@@ -78,7 +78,7 @@ def _pack(w, cuda, K=None, col0=0, out=None):
 
 
 def _run_conv(cuda, x_nhwc, w_packed, Cout, Hout, Wout, taps, stride=1, upsample=0, bias=None, rowvec=None,
-              res=None, x2=None, Cin2=0, y_pitch=None, x_pitch=None, tile=0):
+              res=None, x2=None, Cin2=0, y_pitch=None, x_pitch=None, tile=0, pro=None):
     B, Hin, Win, Cin = x_nhwc.shape[0], x_nhwc.shape[1], x_nhwc.shape[2], x_nhwc.shape[3]
     x_pitch = x_pitch or Cin
     y_pitch = y_pitch or Cout
@@ -95,6 +95,8 @@ def _run_conv(cuda, x_nhwc, w_packed, Cout, Hout, Wout, taps, stride=1, upsample
     d.res = res.data_ptr() if res is not None else None
     d.res_pitch = res.shape[-1] if res is not None else 0
     d.tile = tile
+    if pro is not None:
+        d.pro_scale, d.pro_shift = pro[0].data_ptr(), pro[1].data_ptr()
     dmhip.conv2d_nhwc(d, cuda)
     return y
 
@@ -195,3 +197,25 @@ def test_timestep_embedding(cuda):
     # on-device frequencies: expf ulps are amplified by t up to 999 (args ~1e3 rad)
     dmhip.timestep_embedding(t.to(cuda), 128, 0, out)
     assert (out.cpu() - ref).abs().max().item() < 1e-4
+
+
+@pytest.mark.parametrize('tile', [0, 4, 5, 6])
+@pytest.mark.parametrize('B,Cin,Cout,H,up', [(2, 64, 64, 8, 0), (2, 96, 64, 16, 0), (3, 64, 32, 4, 0),
+                                             (2, 64, 64, 8, 1)])
+def test_conv_fused_groupnorm_silu(cuda, B, Cin, Cout, H, up, tile):
+    """GroupNorm(32) + SiLU folded into the conv's patch load == group_norm -> silu -> conv (padding after SiLU)."""
+    g = torch.Generator().manual_seed(60)
+    x = torch.randn((B, Cin, H, H), generator=g) * 2 + 0.3
+    gamma, beta = torch.randn(Cin, generator=g), torch.randn(Cin, generator=g)
+    w = torch.randn((Cout, Cin, 3, 3), generator=g) * 0.05
+    b = torch.randn(Cout, generator=g)
+    a = F.silu(F.group_norm(x.double(), 32, gamma.double(), beta.double(), 1e-5))
+    if up:
+        a = F.interpolate(a, scale_factor=2, mode='nearest')
+    ref = F.conv2d(a, w.double(), b.double(), padding=1)
+    xd = _nhwc(x).to(cuda)
+    pro = dmhip.groupnorm_affine(xd, B, H * H, Cin, 32, 1e-5, gamma.to(cuda), beta.to(cuda))
+    Ho = ref.shape[-1]
+    y = _run_conv(cuda, xd, _pack(w, cuda), Cout, Ho, Ho, 9, 1, up, b.to(cuda), tile=tile, pro=pro)
+    err = (y.cpu().double() - _nhwc(ref)).abs().max().item()
+    assert err < 1e-4, err

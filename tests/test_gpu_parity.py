@@ -29,7 +29,7 @@ def _model(meta, name, cuda):
 
 
 @pytest.mark.parametrize('name', ['tiny', 'mnist', 'cifar10'])
-def test_unet_forward_vs_reference(cuda, golden, name):
+def test_unet_forward_vs_reference(cuda, golden, report, name):
     arrays, meta = golden('forward')
     model, sha = _model(meta, name, cuda)
     assert sha == meta[f'{name}_weights_sha256']
@@ -38,6 +38,7 @@ def test_unet_forward_vs_reference(cuda, golden, name):
     y = model(x, t).cpu()
     ref = torch.from_numpy(arrays[f'{name}_y'])
     err = (y - ref).abs().max().item()
+    report(f'forward_{name}_maxabs_vs_reference', err)
     assert err <= TOL, f'{name}: max abs err {err}'
 
 
@@ -116,7 +117,7 @@ def test_cfg_update_bit_exact(cuda, golden):
             assert np.abs(out[k].cpu().numpy() - arrays[f'cfg_{k}'][i]).max() <= 1e-5
 
 
-def test_ddim50_cifar_trajectory(cuda, golden):
+def test_ddim50_cifar_trajectory(cuda, golden, report):
     """BASELINE config C3 path (DDIM-50, CIFAR-10 UNet) at B=2 against the reference."""
     arrays, meta = golden('trajectory')
     fmeta = golden('forward')[1]
@@ -131,10 +132,10 @@ def test_ddim50_cifar_trajectory(cuda, golden):
                 err = np.abs(out[k].cpu().numpy() - arrays[f'ddim50_step{i}_{k}']).max()
                 worst = max(worst, err)
                 assert err <= TOL, (i, k, err)
-    print('ddim50 worst max-abs', worst)
+    report('ddim50_cifar_B2_worst_step_maxabs_vs_reference', worst)
 
 
-def test_ddpm10_mnist_trajectory(cuda, golden):
+def test_ddpm10_mnist_trajectory(cuda, golden, report):
     """BASELINE config C1 (MNIST UNet, DDPM T=200 fixed_small, 10 steps) with the reference's CPU noise."""
     arrays, meta = golden('trajectory')
     fmeta = golden('forward')[1]
@@ -146,10 +147,13 @@ def test_ddpm10_mnist_trajectory(cuda, golden):
     d.noise_fn = lambda x: next(it)
     d.skip_unused_noise = False
     init = torch.from_numpy(arrays['ddpm10_init']).to(cuda)
+    worst = 0.0
     for i, out in enumerate(d.sample_loop(model, init, tqdm_kwargs=dict(disable=True))):
         for k in ('sample', 'pred_eps'):
             err = np.abs(out[k].cpu().numpy() - arrays[f'ddpm10_step{i}_{k}']).max()
+            worst = max(worst, err)
             assert err <= TOL, (i, k, err)
+    report('ddpm10_mnist_B2_worst_step_maxabs_vs_reference', worst)
 
 
 @pytest.mark.parametrize('kind', ['ddpm', 'ddim'])
