@@ -92,7 +92,16 @@ struct StepArgs {
 int gn_num_chunks(int HW);
 int gn_partial(const View& x, int G, double2* part, hipStream_t st);
 int gn_finalize(const View& x, int G, const double2* part, float eps, const float* gamma, const float* beta,
-                float* scale, float* shift, hipStream_t st);
+                float* scale, float* shift, hipStream_t st, const float* mod_scale = nullptr,
+                const float* mod_shift = nullptr, int mod_pitch = 0);
+// NHWC resampling (models/unet_categorial_adagn.py:24-27, models/adm/unet.py:73-160):
+// y = avg_pool2d(pro(x), 2) (down) or nearest-2x(pro(x)) (up); pro = optional silu(x * scale + shift)
+int resample2x(const View& x, const View& y, int down, const float* pro_scale, const float* pro_shift,
+               hipStream_t st);
+// out[b] = silu(temb[b] + table[y[b]]) (class embedding, unet_categorial_adagn.py:172-174);
+// rows with y == null or y[b] < 0 get silu(temb[b]) (no label / CFG unconditional branch)
+int embed_add_silu(const float* temb, const int64_t* y, const float* table, int B, int D, float* out,
+                   hipStream_t st);
 int gn_apply(const View& x, int G, const double2* part, int nchunk, float eps, const float* gamma,
              const float* beta, const float* mod_scale, const float* mod_shift, int mod_pitch, int act,
              const View& y, hipStream_t st);

@@ -246,6 +246,62 @@ __global__ void sampler_step_kernel(StepArgs s) {
   if (s.var_out) s.var_out[e] = var;
 }
 
+// avg-pool 2x2 / nearest-2x on NHWC views, float4 over channels, optional
+// GroupNorm+SiLU prologue applied to each source pixel before pooling.
+__global__ void resample2x_kernel(View x, View y, int down, const float* __restrict__ pro_scale,
+                                  const float* __restrict__ pro_shift) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int C4 = y.C >> 2;
+  const long total = (long)y.B * y.H * y.W * C4;
+  if (e >= total) return;
+  const int c4 = e % C4;
+  long p = e / C4;
+  const int ox = p % y.W;
+  p /= y.W;
+  const int oy = p % y.H;
+  const int b = p / y.H;
+  auto pro = [&](float4 v) {
+    if (pro_scale) {
+      const float4 sc = *reinterpret_cast<const float4*>(pro_scale + (size_t)b * x.C + 4 * c4);
+      const float4 sh = *reinterpret_cast<const float4*>(pro_shift + (size_t)b * x.C + 4 * c4);
+      v.x = silu_f(v.x * sc.x + sh.x); v.y = silu_f(v.y * sc.y + sh.y);
+      v.z = silu_f(v.z * sc.z + sh.z); v.w = silu_f(v.w * sc.w + sh.w);
+    }
+    return v;
+  };
+  float4 o;
+  if (down) {
+    float4 s[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int iy = 2 * oy + (q >> 1), ix = 2 * ox + (q & 1);
+      s[q] = pro(*reinterpret_cast<const float4*>(x.p + (((size_t)b * x.H + iy) * x.W + ix) * x.pitch + 4 * c4));
+    }
+    // torch avg_pool2d: row-major window sum, then / 4
+    o.x = (((s[0].x + s[1].x) + s[2].x) + s[3].x) / 4.0f;
+    o.y = (((s[0].y + s[1].y) + s[2].y) + s[3].y) / 4.0f;
+    o.z = (((s[0].z + s[1].z) + s[2].z) + s[3].z) / 4.0f;
+    o.w = (((s[0].w + s[1].w) + s[2].w) + s[3].w) / 4.0f;
+  } else {
+    o = pro(*reinterpret_cast<const float4*>(x.p + (((size_t)b * x.H + (oy >> 1)) * x.W + (ox >> 1)) * x.pitch +
+                                             4 * c4));
+  }
+  *reinterpret_cast<float4*>(y.p + (((size_t)b * y.H + oy) * y.W + ox) * y.pitch + 4 * c4) = o;
+}
+
+__global__ void embed_add_silu_kernel(const float* __restrict__ temb, const int64_t* __restrict__ y,
+                                      const float* __restrict__ table, int B, int D, float* __restrict__ out) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= B * D) return;
+  const int b = e / D, d = e - (e / D) * D;
+  float v = temb[e];
+  if (y) {
+    const int64_t cls = y[b];
+    if (cls >= 0) v = v + table[(size_t)cls * D + d];
+  }
+  out[e] = silu_f(v);
+}
+
 __global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, int B, int C, int HW,
                                     float* __restrict__ y, int y_pitch) {
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -339,6 +395,29 @@ int sampler_step(const StepArgs& s, hipStream_t st) {
   const long total = (long)s.B * s.C * s.HW;
   if (total == 0) return DM_OK;
   hipLaunchKernelGGL(sampler_step_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, s);
+  DM_LAUNCH_CHECK();
+  return DM_OK;
+}
+
+int resample2x(const View& x, const View& y, int down, const float* pro_scale, const float* pro_shift,
+               hipStream_t st) {
+  DM_REQUIRE(x.C == y.C && x.B == y.B && x.C % 4 == 0 && x.pitch % 4 == 0 && y.pitch % 4 == 0,
+             "resample: channel layout");
+  if (down)
+    DM_REQUIRE(y.H == x.H / 2 && y.W == x.W / 2 && x.H % 2 == 0 && x.W % 2 == 0, "resample: down size");
+  else
+    DM_REQUIRE(y.H == 2 * x.H && y.W == 2 * x.W, "resample: up size");
+  const long total = (long)y.B * y.H * y.W * (y.C / 4);
+  hipLaunchKernelGGL(resample2x_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x, y, down,
+                     pro_scale, pro_shift);
+  DM_LAUNCH_CHECK();
+  return DM_OK;
+}
+
+int embed_add_silu(const float* temb, const int64_t* y, const float* table, int B, int D, float* out,
+                   hipStream_t st) {
+  const int n = B * D;
+  hipLaunchKernelGGL(embed_add_silu_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, st, temb, y, table, B, D, out);
   DM_LAUNCH_CHECK();
   return DM_OK;
 }

@@ -137,7 +137,8 @@ __global__ void gn_apply_kernel(const float* __restrict__ x, int HW, int C, int 
 // consumer can apply the norm inside its own operand load.
 __global__ void gn_finalize_kernel(const double2* __restrict__ part, int B, int nchunk, int G, int C, double n,
                                    float eps, const float* __restrict__ gamma, const float* __restrict__ beta,
-                                   float* __restrict__ scale, float* __restrict__ shift) {
+                                   const float* __restrict__ mod_scale, const float* __restrict__ mod_shift,
+                                   int mod_pitch, float* __restrict__ scale, float* __restrict__ shift) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= B * C) return;
   const int b = idx / C, c = idx - (idx / C) * C;
@@ -153,9 +154,16 @@ __global__ void gn_finalize_kernel(const double2* __restrict__ part, int B, int 
   if (var < 0) var = 0;
   const float mu = (float)m;
   const float rs = (float)(1.0 / sqrt(var + (double)eps));
-  const float sc = rs * (gamma ? gamma[c] : 1.0f);
+  float sc = rs * (gamma ? gamma[c] : 1.0f);
+  float sh = -sc * mu + (beta ? beta[c] : 0.0f);
+  if (mod_scale) {
+    // AdaGN / scale-shift norm: (x * sc + sh) * (1 + ys) + yb  (modules.py:114-123)
+    const float f = 1.0f + mod_scale[(size_t)b * mod_pitch + c];
+    sc = sc * f;
+    sh = sh * f + (mod_shift ? mod_shift[(size_t)b * mod_pitch + c] : 0.0f);
+  }
   scale[idx] = sc;
-  shift[idx] = -sc * mu + (beta ? beta[c] : 0.0f);
+  shift[idx] = sh;
 }
 
 inline int gn_block_threads(int C) {
@@ -189,12 +197,13 @@ int gn_partial(const View& x, int G, double2* part, hipStream_t st) {
 }
 
 int gn_finalize(const View& x, int G, const double2* part, float eps, const float* gamma, const float* beta,
-                float* scale, float* shift, hipStream_t st) {
+                float* scale, float* shift, hipStream_t st, const float* mod_scale, const float* mod_shift,
+                int mod_pitch) {
   DM_REQUIRE(x.C % G == 0, "GroupNorm finalize: C must be divisible by groups");
   const int HW = x.H * x.W;
   const int n = x.B * x.C;
   hipLaunchKernelGGL(gn_finalize_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, st, part, x.B, gn_num_chunks(HW), G,
-                     x.C, (double)HW * (x.C / G), eps, gamma, beta, scale, shift);
+                     x.C, (double)HW * (x.C / G), eps, gamma, beta, mod_scale, mod_shift, mod_pitch, scale, shift);
   DM_LAUNCH_CHECK();
   return DM_OK;
 }

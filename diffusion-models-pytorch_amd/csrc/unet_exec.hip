@@ -88,6 +88,9 @@ struct ResBlockP {
   GnP gn1, gn2;
   ConvP conv1, conv2;  // conv2 carries the shortcut segment when cin != cout
   int proj_col;        // column offset of this block's projection in the fused proj output
+                       // (variant 0: temb add [cout]; variant 1: AdaGN [ys | yb], 2 * cout)
+  bool adagn = false;  // variant 1: AdaGN before conv2 instead of the temb add after conv1
+  int updown = 0;      // variant 1: 0 none, 1 nearest-2x up, 2 avg-pool down (unet_categorial_adagn.py:24-27)
 };
 
 struct AttnP {
@@ -131,6 +134,7 @@ struct UNetModel {
   size_t te_w1, te_b1, te_w2, te_b2;
   size_t te_freqs;            // [dim/2] sinusoid frequencies
   bool te_freqs_set = false;  // host table installed (else computed on device)
+  size_t class_embed = 0;     // variant 1: [num_classes][4 dim]
   size_t first_w, first_b;
   size_t proj_w, proj_b;
   int proj_total = 0;
@@ -156,6 +160,7 @@ struct UNetModel {
     std::vector<int64_t> prof_launches;
     const float* x = nullptr;
     const int64_t* t = nullptr;
+    const int64_t* y = nullptr;  // class labels or null
     float* out = nullptr;
   };
   std::unique_ptr<Plan> plan;
@@ -192,8 +197,10 @@ UNetModel::~UNetModel() {
 }
 
 static int count_params(const dm_unet_arch& a) {
-  // mirrors the registration order of models/unet.py:47-119
+  // mirrors the registration order of models/unet.py:47-119 (variant 1:
+  // models/unet_categorial_adagn.py:77-163, same counts per block)
   int n = 4 + 2;  // time_embed (2 linears), first_conv
+  if (a.variant == 1 && a.num_classes > 0) n += 1;  // class_embed.weight
   auto rb = [](int cin, int cout) { return 10 + (cin != cout ? 2 : 0); };
   const int attn = 10;
   int cur = a.dim;
@@ -206,7 +213,10 @@ static int count_params(const dm_unet_arch& a) {
       dims.push_back(out);
       cur = out;
     }
-    if (i < a.n_stages - 1) { n += 2; dims.push_back(out); }
+    if (i < a.n_stages - 1) {
+      n += (a.variant == 1 && a.resblock_updown) ? rb(out, out) : 2;  // ResBlockDownsample or conv
+      dims.push_back(out);
+    }
   }
   n += rb(cur, cur) * 2 + attn;
   for (int i = a.n_stages - 1; i >= 0; --i) {
@@ -218,7 +228,7 @@ static int count_params(const dm_unet_arch& a) {
       if (a.use_attn[i]) n += attn;
       cur = out;
     }
-    if (i > 0) n += 2;
+    if (i > 0) n += (a.variant == 1 && a.resblock_updown) ? rb(out, out) : 2;  // ResBlockUpsample or conv
   }
   n += 4;  // last_conv GN + conv
   return n;
@@ -231,10 +241,17 @@ static int validate_arch(const dm_unet_arch* a) {
   DM_REQUIRE(a->in_channels >= 1 && a->in_channels <= 16, "in_channels out of range (1..16)");
   DM_REQUIRE(a->out_channels >= 1 && a->out_channels <= 8, "out_channels out of range (1..8)");
   DM_REQUIRE(a->num_res_blocks >= 1, "num_res_blocks must be >= 1");
-  DM_REQUIRE(a->n_heads >= 1, "n_heads must be >= 1");
+  DM_REQUIRE(a->variant == 0 || a->variant == 1, "variant must be 0 (UNet) or 1 (UNetCategorialAdaGN)");
+  if (a->variant == 0) DM_REQUIRE(a->n_heads >= 1, "n_heads must be >= 1");
+  if (a->variant == 1) {
+    DM_REQUIRE(a->attn_head_dims >= 1, "attn_head_dims must be >= 1");
+    DM_REQUIRE(a->num_classes >= 0, "num_classes must be >= 0");
+  }
   for (int i = 0; i < a->n_stages; ++i) {
     DM_REQUIRE(a->dim_mults[i] >= 1, "dim_mults must be >= 1");
-    if (a->use_attn[i]) DM_REQUIRE((a->dim * a->dim_mults[i]) % a->n_heads == 0, "dim not divisible by heads");
+    const int c = a->dim * a->dim_mults[i];
+    if (a->use_attn[i])
+      DM_REQUIRE(c % (a->variant == 1 ? a->attn_head_dims : a->n_heads) == 0, "channels not divisible by heads");
   }
   return DM_OK;
 }
@@ -262,6 +279,8 @@ static int unet_create(const dm_unet_arch* arch, const float* const* params, con
   m->te_w2 = pk.raw(rd.take((int64_t)TD * TD, "time_embed.3.weight"), (int64_t)TD * TD);
   m->te_b2 = pk.raw(rd.take(TD, "time_embed.3.bias"), TD);
   m->te_freqs = pk.reserve(D / 2);
+  if (a.variant == 1 && a.num_classes > 0)  // unet_categorial_adagn.py:104
+    m->class_embed = pk.raw(rd.take((int64_t)a.num_classes * TD, "class_embed.weight"), (int64_t)a.num_classes * TD);
   m->first_w = pk.raw(rd.take((int64_t)D * a.in_channels * 9, "first_conv.weight"), (int64_t)D * a.in_channels * 9);
   m->first_b = pk.raw(rd.take(D, "first_conv.bias"), D);
 
@@ -276,10 +295,15 @@ static int unet_create(const dm_unet_arch* arch, const float* const* params, con
     g.b = pk.raw(rd.take(C, what), C);
     return g;
   };
-  auto resblock = [&](int cin, int cout) {
+  // variant 0 (models/unet.py:14-44): blk1 (GN, conv), proj, blk2 (GN, conv), shortcut
+  // variant 1 (models/unet_categorial_adagn.py:31-42): blk1 (GN, conv), adagn (gn, proj -> 2 cout),
+  //           blk2 conv, shortcut
+  auto resblock = [&](int cin, int cout, int updown) {
     ResBlockP r;
     r.cin = cin;
     r.cout = cout;
+    r.adagn = a.variant == 1;
+    r.updown = updown;
     r.gn1 = gn(cin, "ResBlock.blk1.0 (GroupNorm)");
     const float* w1 = rd.take((int64_t)cout * cin * 9, "ResBlock.blk1.2.weight");
     const float* b1 = rd.take(cout, "ResBlock.blk1.2.bias");
@@ -287,14 +311,16 @@ static int unet_create(const dm_unet_arch* arch, const float* const* params, con
     r.conv1.w = pk.reserve((int64_t)cout * 9 * cin);
     pk.conv_at(w1, cout, cin, 9, 9 * cin, 0, r.conv1.w);
     r.conv1.bias = pk.raw(b1, cout);
-    const float* pw = rd.take((int64_t)cout * TD, "ResBlock.proj.1.weight");
-    const float* pb = rd.take(cout, "ResBlock.proj.1.bias");
+    const int pn = r.adagn ? 2 * cout : cout;
+    if (r.adagn) r.gn2 = gn(cout, "ResBlock.adagn.gn");
+    const float* pw = rd.take((int64_t)pn * TD, r.adagn ? "ResBlock.adagn.proj.1.weight" : "ResBlock.proj.1.weight");
+    const float* pb = rd.take(pn, r.adagn ? "ResBlock.adagn.proj.1.bias" : "ResBlock.proj.1.bias");
     r.proj_col = m->proj_total;
-    m->proj_total += cout;
-    projs.push_back({pw, pb, cout});
-    r.gn2 = gn(cout, "ResBlock.blk2.0 (GroupNorm)");
-    const float* w2 = rd.take((int64_t)cout * cout * 9, "ResBlock.blk2.3.weight");
-    const float* b2 = rd.take(cout, "ResBlock.blk2.3.bias");
+    m->proj_total += pn;
+    projs.push_back({pw, pb, pn});
+    if (!r.adagn) r.gn2 = gn(cout, "ResBlock.blk2.0 (GroupNorm)");
+    const float* w2 = rd.take((int64_t)cout * cout * 9, "ResBlock.blk2 conv weight");
+    const float* b2 = rd.take(cout, "ResBlock.blk2 conv bias");
     const int K2 = 9 * cout + (cin != cout ? cin : 0);
     r.conv2 = {0, 0, cout, cout, 9, K2};
     r.conv2.w = pk.reserve((int64_t)cout * K2);
@@ -340,6 +366,9 @@ static int unet_create(const dm_unet_arch* arch, const float* const* params, con
     return (int)m->convs.size() - 1;
   };
 
+  const bool rb_updown = a.variant == 1 && a.resblock_updown;
+  // stage attention heads: variant 0 n_heads; variant 1 C / attn_head_dims (unet_categorial_adagn.py:118-121)
+  auto stage_heads = [&](int C) { return a.variant == 1 ? C / a.attn_head_dims : a.n_heads; };
   // ---- down path (models/unet.py:77-90, forward :126-136)
   int cur = D, level = 0, n_skips = 0;
   std::vector<int> skip_stack;  // skip ids
@@ -354,10 +383,10 @@ static int unet_create(const dm_unet_arch* arch, const float* const* params, con
   for (int i = 0; i < a.n_stages; ++i) {
     const int out = D * a.dim_mults[i];
     for (int j = 0; j < a.num_res_blocks; ++j) {
-      Node n{N_RES, resblock(cur, out), cur, out, 0, level, level};
+      Node n{N_RES, resblock(cur, out, 0), cur, out, 0, level, level};
       m->nodes.push_back(n);
       if (a.use_attn[i]) {
-        Node na{N_ATTN, attnblock(out, a.n_heads), out, out, 0, level, level};
+        Node na{N_ATTN, attnblock(out, stage_heads(out)), out, out, 0, level, level};
         m->nodes.push_back(na);
       }
       m->nodes.back().skip_producer = true;
@@ -365,8 +394,10 @@ static int unet_create(const dm_unet_arch* arch, const float* const* params, con
       cur = out;
     }
     if (i < a.n_stages - 1) {
-      Node nd{N_DOWN, sampleconv(out, "Downsample"), out, out, 0, level, level + 1};
-      m->nodes.push_back(nd);
+      if (rb_updown)
+        m->nodes.push_back(Node{N_RES, resblock(out, out, 2), out, out, 0, level, level + 1});
+      else
+        m->nodes.push_back(Node{N_DOWN, sampleconv(out, "Downsample"), out, out, 0, level, level + 1});
       ++level;
       m->nodes.back().skip_producer = true;
       m->nodes.back().skip_id = push_skip(out, level);
@@ -374,9 +405,9 @@ static int unet_create(const dm_unet_arch* arch, const float* const* params, con
   }
   m->n_levels = level + 1;
   // ---- bottleneck (models/unet.py:93-97; attention with the default n_heads = 1)
-  m->nodes.push_back(Node{N_RES, resblock(cur, cur), cur, cur, 0, level, level});
+  m->nodes.push_back(Node{N_RES, resblock(cur, cur, 0), cur, cur, 0, level, level});
   m->nodes.push_back(Node{N_ATTN, attnblock(cur, 1), cur, cur, 0, level, level});
-  m->nodes.push_back(Node{N_RES, resblock(cur, cur), cur, cur, 0, level, level});
+  m->nodes.push_back(Node{N_RES, resblock(cur, cur, 0), cur, cur, 0, level, level});
   // ---- up path (models/unet.py:101-112, forward :142-149)
   for (int i = a.n_stages - 1; i >= 0; --i) {
     const int out = D * a.dim_mults[i];
@@ -384,15 +415,19 @@ static int unet_create(const dm_unet_arch* arch, const float* const* params, con
       const int sid = skip_stack.back();
       skip_stack.pop_back();
       const int cin = cur + m->skip_C[sid];
-      Node n{N_RES, resblock(cin, out), cin, out, 0, level, level};
+      Node n{N_RES, resblock(cin, out, 0), cin, out, 0, level, level};
       n.pops_skip = sid;
       n.concat_cx = cur;
       m->nodes.push_back(n);
-      if (a.use_attn[i]) m->nodes.push_back(Node{N_ATTN, attnblock(out, a.n_heads), out, out, 0, level, level});
+      if (a.use_attn[i])
+        m->nodes.push_back(Node{N_ATTN, attnblock(out, stage_heads(out)), out, out, 0, level, level});
       cur = out;
     }
     if (i > 0) {
-      m->nodes.push_back(Node{N_UP, sampleconv(out, "Upsample"), out, out, 0, level, level - 1});
+      if (rb_updown)
+        m->nodes.push_back(Node{N_RES, resblock(out, out, 1), out, out, 0, level, level - 1});
+      else
+        m->nodes.push_back(Node{N_UP, sampleconv(out, "Upsample"), out, out, 0, level, level - 1});
       --level;
     }
   }
@@ -472,17 +507,22 @@ int UNetModel::build_plan(int B, int H, int W) {
   float* e0 = alloc((size_t)B * D * 4);
   float* e1 = alloc((size_t)B * TD * 4);
   float* se = alloc((size_t)B * TD * 4);
+  float* e2 = arch.variant == 1 ? alloc((size_t)B * TD * 4) : nullptr;
   float* projs = alloc((size_t)B * proj_total * 4);
 
   // --- scratch sizes
-  size_t max_a1 = 0, max_h = 0, max_attn = 0, max_qkv = 0, max_S = 0;
+  size_t max_a1 = 0, max_h = 0, max_attn = 0, max_qkv = 0, max_S = 0, max_xr = 0;
   int max_chunks = 1;
   for (auto& n : nodes) {
     const size_t hw = (size_t)Hl(n.level_in) * Wl(n.level_in);
     max_chunks = std::max(max_chunks, gn_num_chunks((int)hw));
     if (n.kind == N_RES) {
-      max_a1 = std::max(max_a1, (size_t)B * hw * n.cin);
-      max_h = std::max(max_h, (size_t)B * hw * n.cout);
+      // up/down ResBlocks convolve at the output resolution
+      const size_t hw_o = (size_t)Hl(n.level_out) * Wl(n.level_out);
+      max_chunks = std::max(max_chunks, gn_num_chunks((int)hw_o));
+      max_a1 = std::max(max_a1, (size_t)B * std::max(hw, hw_o) * n.cin);
+      max_h = std::max(max_h, (size_t)B * hw_o * n.cout);
+      if (res[n.idx].updown) max_xr = std::max(max_xr, (size_t)B * hw_o * n.cin);
     } else if (n.kind == N_ATTN) {
       max_attn = std::max(max_attn, (size_t)B * hw * n.cin);
       max_qkv = std::max(max_qkv, (size_t)B * hw * 3 * n.cin);
@@ -498,6 +538,7 @@ int UNetModel::build_plan(int B, int H, int W) {
   float* qkv = alloc(std::max<size_t>(max_qkv, 1) * 4);
   float* Sb = alloc(std::max<size_t>(max_S, 1) * 4);
   float* Ob = alloc(std::max<size_t>(max_attn, 1) * 4);
+  float* xr = alloc(std::max<size_t>(max_xr, 1) * 4);  // resampled residual of up/down ResBlocks
   double2* part = (double2*)alloc((size_t)B * max_chunks * G * sizeof(double2));
   // per-(image, channel) GroupNorm affine for the fused conv prologues
   size_t max_c = (size_t)D;
@@ -563,8 +604,19 @@ int UNetModel::build_plan(int B, int H, int W) {
     add_gemm(g);
     GemmArgs g2 = g;
     g2.K = TD; g2.A = e1; g2.lda = TD; g2.Bm = P(te_w2); g2.ldb = TD; g2.C = se; g2.bias = P(te_b2);
-    g2.act = 1;  // only SiLU(temb) is ever consumed (ResBlock.proj = SiLU -> Linear)
-    add_gemm(g2);
+    g2.act = 1;  // only SiLU(temb) is ever consumed (ResBlock.proj / AdaGN.proj = SiLU -> Linear)
+    if (arch.variant == 1) {
+      // temb + class_embed(y) before the SiLU (unet_categorial_adagn.py:172-174)
+      g2.act = 0;
+      g2.C = e2;
+      add_gemm(g2);
+      const float* table = class_embed ? P(class_embed) : nullptr;
+      add("class_embed_silu", 0, 8.0 * B * TD, [=](hipStream_t st) {
+        return embed_add_silu(e2, table ? P_->y : nullptr, table, B, TD, se, st);
+      });
+    } else {
+      add_gemm(g2);
+    }
     GemmArgs g3 = g;
     g3.N = proj_total; g3.K = TD; g3.A = se; g3.lda = TD; g3.Bm = P(proj_w); g3.ldb = TD; g3.C = projs;
     g3.ldc = proj_total; g3.bias = P(proj_b); g3.act = 0;
@@ -603,29 +655,55 @@ int UNetModel::build_plan(int B, int H, int W) {
     const int nchunk = gn_num_chunks(hw);
     if (n.kind == N_RES) {
       const ResBlockP r = res[n.idx];
-      View va1{a1, B, Hi, Wi, r.cin, r.cin};
-      View vh{hbuf, B, Hi, Wi, r.cout, r.cout};
-      View va2{a2, B, Hi, Wi, r.cout, r.cout};
+      // conv resolution: the block's output resolution (differs from the input for up/down blocks)
+      const int Ho = Hl(n.level_out), Wo = Wl(n.level_out);
+      const int nchunk_o = gn_num_chunks(Ho * Wo);
+      View va1{a1, B, Ho, Wo, r.cin, r.cin};
+      View vh{hbuf, B, Ho, Wo, r.cout, r.cout};
+      View va2{a2, B, Ho, Wo, r.cout, r.cout};
+      // residual / shortcut operand at conv resolution: X, or updown(X) (unet_categorial_adagn.py:52-57)
+      View xres = xin;
+      if (r.updown) {
+        xres = View{xr, B, Ho, Wo, r.cin, r.cin};
+        const bool down = r.updown == 2;
+        add("resample2x", 0, 4.0 * B * ((double)Hi * Wi + (double)Ho * Wo) * r.cin,
+            [=](hipStream_t st) { return resample2x(xin, xres, down, nullptr, nullptr, st); });
+      }
       ConvArgs c1{};
-      c1.x1_pitch = r.cin; c1.Cin1 = r.cin; c1.Hin = Hi; c1.Win = Wi;
+      c1.x1_pitch = r.cin; c1.Cin1 = r.cin; c1.Hin = Ho; c1.Win = Wo;
       c1.taps = 9; c1.stride = 1; c1.upsample = 0;
       c1.w = P(r.conv1.w); c1.K = r.conv1.K;
-      c1.y = hbuf; c1.y_pitch = r.cout; c1.Cout = r.cout; c1.B = B; c1.Hout = Hi; c1.Wout = Wi;
-      c1.bias = P(r.conv1.bias); c1.rowvec = projs + r.proj_col; c1.rowvec_pitch = proj_total;
+      c1.y = hbuf; c1.y_pitch = r.cout; c1.Cout = r.cout; c1.B = B; c1.Hout = Ho; c1.Wout = Wo;
+      c1.bias = P(r.conv1.bias);
+      if (!r.adagn) { c1.rowvec = projs + r.proj_col; c1.rowvec_pitch = proj_total; }
+      if (r.updown == 1) { c1.upsample = 1; c1.Hin = Hi; c1.Win = Wi; }
       ConvArgs c2{};
-      c2.x1 = a2; c2.x1_pitch = r.cout; c2.Cin1 = r.cout; c2.Hin = Hi; c2.Win = Wi;
+      c2.x1 = a2; c2.x1_pitch = r.cout; c2.Cin1 = r.cout; c2.Hin = Ho; c2.Win = Wo;
       c2.taps = 9; c2.stride = 1;
       c2.w = P(r.conv2.w); c2.K = r.conv2.K;
-      c2.y = y.p; c2.y_pitch = y.pitch; c2.Cout = r.cout; c2.B = B; c2.Hout = Hi; c2.Wout = Wi;
+      c2.y = y.p; c2.y_pitch = y.pitch; c2.Cout = r.cout; c2.B = B; c2.Hout = Ho; c2.Wout = Wo;
       c2.bias = P(r.conv2.bias);
       if (r.cin != r.cout) {
-        c2.x2 = xin.p; c2.x2_pitch = xin.pitch; c2.Cin2 = r.cin;
+        c2.x2 = xres.p; c2.x2_pitch = xres.pitch; c2.Cin2 = r.cin;
       } else {
-        c2.res = xin.p; c2.res_pitch = xin.pitch;
+        c2.res = xres.p; c2.res_pitch = xres.pitch;
       }
-      const bool fuse1 = conv_pick(c1) >= 3, fuse2 = conv_pick(c2) >= 3;
+      const bool fuse1 = r.updown != 2 && conv_pick(c1) >= 3, fuse2 = conv_pick(c2) >= 3;
+      // AdaGN modulation gn(h) * (1 + ys) + yb, [ys | yb] from the fused projection (modules.py:114-123)
+      const float* ms = r.adagn ? projs + r.proj_col : nullptr;
+      const float* mb = r.adagn ? projs + r.proj_col + r.cout : nullptr;
+      const int mp = r.adagn ? proj_total : 0;
       add("gn_partial", 0, gn_bytes(xin, false), [=](hipStream_t st) { return gn_partial(xin, G, part, st); });
-      if (fuse1) {
+      if (r.updown && !fuse1) {
+        // normalise + SiLU + resample into a1, then a plain conv at the output resolution
+        add("gn_finalize", 0, 8.0 * B * r.cin, [=](hipStream_t st) {
+          return gn_finalize(xin, G, part, 1e-5f, self->P(r.gn1.g), self->P(r.gn1.b), gsc, gsh, st);
+        });
+        const bool down = r.updown == 2;
+        add("resample2x", 0, 4.0 * B * ((double)Hi * Wi + (double)Ho * Wo) * r.cin,
+            [=](hipStream_t st) { return resample2x(xin, va1, down, gsc, gsh, st); });
+        c1.x1 = a1; c1.upsample = 0; c1.Hin = Ho; c1.Win = Wo;
+      } else if (fuse1) {
         // GroupNorm + SiLU folded into conv1's patch load: x read once, normalised tensor never stored
         add("gn_finalize", 0, 8.0 * B * r.cin, [=](hipStream_t st) {
           return gn_finalize(xin, G, part, 1e-5f, self->P(r.gn1.g), self->P(r.gn1.b), gsc, gsh, st);
@@ -643,14 +721,13 @@ int UNetModel::build_plan(int B, int H, int W) {
       add("gn_partial", 0, gn_bytes(vh, false), [=](hipStream_t st) { return gn_partial(vh, G, part, st); });
       if (fuse2) {
         add("gn_finalize", 0, 8.0 * B * r.cout, [=](hipStream_t st) {
-          return gn_finalize(vh, G, part, 1e-5f, self->P(r.gn2.g), self->P(r.gn2.b), gsc, gsh, st);
+          return gn_finalize(vh, G, part, 1e-5f, self->P(r.gn2.g), self->P(r.gn2.b), gsc, gsh, st, ms, mb, mp);
         });
         c2.x1 = hbuf;
         c2.pro_scale = gsc; c2.pro_shift = gsh;
       } else {
         add("gn_apply", 0, gn_bytes(vh, true), [=](hipStream_t st) {
-          return gn_apply(vh, G, part, nchunk, 1e-5f, self->P(r.gn2.g), self->P(r.gn2.b), nullptr, nullptr, 0, 1,
-                          va2, st);
+          return gn_apply(vh, G, part, nchunk_o, 1e-5f, self->P(r.gn2.g), self->P(r.gn2.b), ms, mb, mp, 1, va2, st);
         });
       }
       add_conv(c2);
@@ -751,8 +828,8 @@ extern "C" int dm_unet_create(const dm_unet_arch* arch, const float* const* para
   return DM_OK;
 }
 
-extern "C" int dm_unet_forward(dm_unet* h, const float* x, const int64_t* t, int B, int H, int W, float* out,
-                               void* stream) {
+extern "C" int dm_unet_forward(dm_unet* h, const float* x, const int64_t* t, const int64_t* y, int B, int H, int W,
+                               float* out, void* stream) {
   if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
   if (!x || !t || !out) { dm::set_error("null tensor"); return DM_ERR_ARG; }
   if (B <= 0 || H <= 0 || W <= 0) { dm::set_error("empty batch or image"); return DM_ERR_ARG; }
@@ -766,6 +843,7 @@ extern "C" int dm_unet_forward(dm_unet* h, const float* x, const int64_t* t, int
   }
   m->plan->x = x;
   m->plan->t = t;
+  m->plan->y = y;
   m->plan->out = out;
   hipStream_t st = (hipStream_t)stream;
   auto& pl = *m->plan;

@@ -264,14 +264,16 @@ class DDPM:
 class _CFGMixin:
     """Classifier-free guidance loop shared by DDPMCFG / DDIMCFG.
 
-    Two sequential forwards per step as upstream (ddpm.py:334-348,
-    ddim.py:176-188); predict of both branches, the (1-s)/s combine and the
-    denoise are one fused kernel.
+    Conditional and unconditional forwards per step as upstream (ddpm.py:334-348,
+    ddim.py:176-188) — batched into one 2B forward when the model accepts a
+    per-row null label (``model.supports_null_label``), else two calls; predict
+    of both branches, the (1-s)/s combine and the denoise are one fused kernel.
     """
 
     def _cfg_init(self, guidance_scale: float, cond_kwarg: str):
         self.guidance_scale = guidance_scale
         self.cond_kwarg = cond_kwarg
+        self.batch_cfg = True  # run cond + uncond as one 2B forward where the model allows it
 
     def sample_loop(
             self, model, init_noise: Tensor, uncond_conditioning: Any = None,
@@ -284,13 +286,28 @@ class _CFGMixin:
         uncond_kwargs = dict(model_kwargs)
         uncond_kwargs[self.cond_kwarg] = uncond_conditioning
         img = init_noise
+        B = img.shape[0]
+        cond = model_kwargs[self.cond_kwarg]
+        # One 2B forward instead of two B forwards when the model takes "no label" per row
+        # (y < 0, see UNetCategorialAdaGN.forward): every kernel is row-independent, so each
+        # half equals the corresponding separate call; the weights are streamed once per step.
+        batched = (self.batch_cfg and uncond_conditioning is None and len(model_kwargs) == 1
+                   and getattr(model, 'supports_null_label', False) and isinstance(cond, Tensor)
+                   and cond.shape == (B, ))
+        if batched:
+            y2 = torch.cat([cond, torch.full_like(cond, -1)])
         seq = self.respaced_seq.tolist()
         seq_prev = [-1] + seq[:-1]
         pbar = tqdm.tqdm(total=len(seq), **tqdm_kwargs)
         for t, t_prev in zip(reversed(seq), reversed(seq_prev)):
-            t_batch = torch.full((img.shape[0], ), t, device=img.device, dtype=torch.long)
-            out_c = model(img, t_batch, **model_kwargs)
-            out_u = model(img, t_batch, **uncond_kwargs)
+            if batched:
+                t2 = torch.full((2 * B, ), t, device=img.device, dtype=torch.long)
+                both = model(torch.cat([img, img]), t2, **{self.cond_kwarg: y2})
+                out_c, out_u = both[:B], both[B:]
+            else:
+                t_batch = torch.full((B, ), t, device=img.device, dtype=torch.long)
+                out_c = model(img, t_batch, **model_kwargs)
+                out_u = model(img, t_batch, **uncond_kwargs)
             out = self._step(out_c, img, t, t_prev, model_output_uncond=out_u,
                              guidance_scale=self.guidance_scale)
             img = out['sample']

@@ -40,6 +40,10 @@ class UNetArch(ctypes.Structure):
         ('use_attn', ctypes.c_int * DM_MAX_STAGES),
         ('num_res_blocks', ctypes.c_int),
         ('n_heads', ctypes.c_int),
+        ('variant', ctypes.c_int),
+        ('num_classes', ctypes.c_int),
+        ('attn_head_dims', ctypes.c_int),
+        ('resblock_updown', ctypes.c_int),
     ]
 
 
@@ -97,7 +101,7 @@ def _declare(L: ctypes.CDLL):
     L.dm_unet_param_count.argtypes = [ctypes.POINTER(UNetArch), ctypes.POINTER(ctypes.c_int)]
     L.dm_unet_create.argtypes = [ctypes.POINTER(UNetArch), ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_int64),
                                  ctypes.c_int, vp, ctypes.POINTER(vp)]
-    L.dm_unet_forward.argtypes = [vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp]
+    L.dm_unet_forward.argtypes = [vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp]
     L.dm_unet_profile.argtypes = [vp, ctypes.c_int]
     L.dm_unet_profile_count.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
     L.dm_unet_profile_get.argtypes = [vp, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,

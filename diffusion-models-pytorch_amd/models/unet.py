@@ -70,67 +70,13 @@ class _TimeEmbedding(nn.Sequential):
         super().__init__(nn.Identity(), nn.Linear(dim, 4 * dim), nn.SiLU(), nn.Linear(4 * dim, 4 * dim))
 
 
-class UNet(nn.Module):
-    def __init__(
-            self,
-            in_channels: int = 3,
-            out_channels: int = 3,
-            dim: int = 128,
-            dim_mults: List[int] = (1, 2, 2, 2),
-            use_attn: List[int] = (False, True, False, False),
-            num_res_blocks: int = 2,
-            n_heads: int = 1,
-            dropout: float = 0.1,
-    ):
-        super().__init__()
-        if len(dim_mults) != len(use_attn):
-            raise ValueError('dim_mults and use_attn must have the same length')
-        self.arch = dict(in_channels=in_channels, out_channels=out_channels, dim=dim,
-                         dim_mults=list(dim_mults), use_attn=[bool(a) for a in use_attn],
-                         num_res_blocks=num_res_blocks, n_heads=n_heads)
-        temb = 4 * dim
-        self.time_embed = _TimeEmbedding(dim)
-        self.first_conv = _conv(in_channels, dim, 3)
+class NativeDenoiser(nn.Module):
+    """Parameter-container base: packs ``state_dict()`` into the native executor and runs
+    the whole forward pass as one dm_unet_forward call. Subclasses set ``self.arch``."""
 
-        chans = [dim]       # channels of every skip, in push order
-        cur = dim
-        self.down_blocks = nn.ModuleList()
-        for i, mult in enumerate(dim_mults):
-            out = dim * mult
-            stage = nn.ModuleList()
-            for _ in range(num_res_blocks):
-                stage.append(ResBlock(cur, out, temb, dropout))
-                if use_attn[i]:
-                    stage.append(SelfAttentionBlock(out, n_heads=n_heads))
-                chans.append(out)
-                cur = out
-            if i < len(dim_mults) - 1:
-                stage.append(_conv(out, out, 3, stride=2))   # Downsample (modules.py:70-72)
-                chans.append(out)
-            self.down_blocks.append(stage)
-
-        self.bottleneck_block = nn.ModuleList([
-            ResBlock(cur, cur, temb, dropout), SelfAttentionBlock(cur), ResBlock(cur, cur, temb, dropout),
-        ])
-
-        self.up_blocks = nn.ModuleList()
-        for i in reversed(range(len(dim_mults))):
-            out = dim * dim_mults[i]
-            stage = nn.ModuleList()
-            for _ in range(num_res_blocks + 1):
-                stage.append(ResBlock(chans.pop() + cur, out, temb, dropout))
-                if use_attn[i]:
-                    stage.append(SelfAttentionBlock(out, n_heads=n_heads))
-                cur = out
-            if i > 0:
-                # Upsample = nearest 2x then conv (modules.py:60-65); index 1 holds the conv
-                stage.append(nn.Sequential(nn.Upsample(scale_factor=2, mode='nearest'), _conv(out, out, 3)))
-            self.up_blocks.append(stage)
-
-        self.last_conv = nn.Sequential(_gn(cur), nn.SiLU(), _conv(cur, out_channels, 3))
-        self._native = None
-        self._native_key = None
-        self._param_list = None
+    _native = None
+    _native_key = None
+    _param_list = None
 
     # ----------------------------------------------------------- native side
     def _arch_struct(self) -> UNetArch:
@@ -143,7 +89,11 @@ class UNet(nn.Module):
             a.dim_mults[i] = m
             a.use_attn[i] = int(at)
         a.num_res_blocks = self.arch['num_res_blocks']
-        a.n_heads = self.arch['n_heads']
+        a.n_heads = self.arch.get('n_heads', 1)
+        a.variant = self.arch.get('variant', 0)
+        a.num_classes = self.arch.get('num_classes', 0) or 0
+        a.attn_head_dims = self.arch.get('attn_head_dims', 0)
+        a.resblock_updown = int(self.arch.get('resblock_updown', False))
         return a
 
     @staticmethod
@@ -206,7 +156,7 @@ class UNet(nn.Module):
             pass
 
     # --------------------------------------------------------------- forward
-    def forward(self, X: Tensor, T: Tensor):
+    def _run(self, X: Tensor, T: Tensor, y: Tensor = None) -> Tensor:
         dmhip.require_device_tensor(X, 'X')
         dmhip.require_device_tensor(T, 'T', dtype=torch.long)
         if X.ndim != 4 or X.shape[1] != self.arch['in_channels']:
@@ -214,8 +164,90 @@ class UNet(nn.Module):
         B, _, H, W = X.shape
         if T.shape != (B, ):
             raise ValueError(f'expected T of shape ({B},), got {tuple(T.shape)}')
+        y_ptr = None
+        if y is not None:
+            dmhip.require_device_tensor(y, 'y', dtype=torch.long)
+            if y.shape != (B, ):
+                raise ValueError(f'expected y of shape ({B},), got {tuple(y.shape)}')
+            self._check_labels(y)
+            y_ptr = y.data_ptr()
         handle = self.native_handle(X.device)
         out = torch.empty((B, self.arch['out_channels'], H, W), device=X.device, dtype=torch.float32)
-        check(load().dm_unet_forward(handle, X.data_ptr(), T.data_ptr(), B, H, W, out.data_ptr(),
+        check(load().dm_unet_forward(handle, X.data_ptr(), T.data_ptr(), y_ptr, B, H, W, out.data_ptr(),
                                      stream_handle(X.device)), 'dm_unet_forward')
         return out
+
+    def _check_labels(self, y: Tensor):
+        """nn.Embedding raises IndexError on an out-of-range label; so do we (negative = no label).
+        The check syncs once per distinct label tensor (labels are fixed across a sampling loop)."""
+        key = (y.data_ptr(), y._version, y.numel())
+        if getattr(self, '_labels_ok', None) == key:
+            return
+        n = self.arch.get('num_classes', 0) or 0
+        if y.numel() and int(y.max()) >= n:
+            raise IndexError(f'class label {int(y.max())} out of range for num_classes={n}')
+        self._labels_ok = key
+
+
+class UNet(NativeDenoiser):
+    def __init__(
+            self,
+            in_channels: int = 3,
+            out_channels: int = 3,
+            dim: int = 128,
+            dim_mults: List[int] = (1, 2, 2, 2),
+            use_attn: List[int] = (False, True, False, False),
+            num_res_blocks: int = 2,
+            n_heads: int = 1,
+            dropout: float = 0.1,
+    ):
+        super().__init__()
+        if len(dim_mults) != len(use_attn):
+            raise ValueError('dim_mults and use_attn must have the same length')
+        self.arch = dict(in_channels=in_channels, out_channels=out_channels, dim=dim,
+                         dim_mults=list(dim_mults), use_attn=[bool(a) for a in use_attn],
+                         num_res_blocks=num_res_blocks, n_heads=n_heads)
+        temb = 4 * dim
+        self.time_embed = _TimeEmbedding(dim)
+        self.first_conv = _conv(in_channels, dim, 3)
+
+        chans = [dim]       # channels of every skip, in push order
+        cur = dim
+        self.down_blocks = nn.ModuleList()
+        for i, mult in enumerate(dim_mults):
+            out = dim * mult
+            stage = nn.ModuleList()
+            for _ in range(num_res_blocks):
+                stage.append(ResBlock(cur, out, temb, dropout))
+                if use_attn[i]:
+                    stage.append(SelfAttentionBlock(out, n_heads=n_heads))
+                chans.append(out)
+                cur = out
+            if i < len(dim_mults) - 1:
+                stage.append(_conv(out, out, 3, stride=2))   # Downsample (modules.py:70-72)
+                chans.append(out)
+            self.down_blocks.append(stage)
+
+        self.bottleneck_block = nn.ModuleList([
+            ResBlock(cur, cur, temb, dropout), SelfAttentionBlock(cur), ResBlock(cur, cur, temb, dropout),
+        ])
+
+        self.up_blocks = nn.ModuleList()
+        for i in reversed(range(len(dim_mults))):
+            out = dim * dim_mults[i]
+            stage = nn.ModuleList()
+            for _ in range(num_res_blocks + 1):
+                stage.append(ResBlock(chans.pop() + cur, out, temb, dropout))
+                if use_attn[i]:
+                    stage.append(SelfAttentionBlock(out, n_heads=n_heads))
+                cur = out
+            if i > 0:
+                # Upsample = nearest 2x then conv (modules.py:60-65); index 1 holds the conv
+                stage.append(nn.Sequential(nn.Upsample(scale_factor=2, mode='nearest'), _conv(out, out, 3)))
+            self.up_blocks.append(stage)
+
+        self.last_conv = nn.Sequential(_gn(cur), nn.SiLU(), _conv(cur, out_channels, 3))
+
+    def forward(self, X: Tensor, T: Tensor):
+        """models/unet.py:121-152: X [B, C, H, W] f32, T [B] int64 -> [B, out_channels, H, W]."""
+        return self._run(X, T)

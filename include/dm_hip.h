@@ -62,7 +62,14 @@ typedef struct dm_unet_arch {
   int dim_mults[DM_MAX_STAGES];
   int use_attn[DM_MAX_STAGES];
   int num_res_blocks;
-  int n_heads;
+  int n_heads;          /* variant 0: heads of the stage attention blocks */
+  /* variant 0: models/unet.py UNet (time-embedding add after conv1, conv down/upsample);
+   * variant 1: models/unet_categorial_adagn.py UNetCategorialAdaGN (AdaGN before conv2,
+   *            heads = C / attn_head_dims, ResBlock up/down when resblock_updown, class embedding) */
+  int variant;
+  int num_classes;      /* variant 1: class-embedding rows (0 = no class embedding) */
+  int attn_head_dims;   /* variant 1 */
+  int resblock_updown;  /* variant 1 */
 } dm_unet_arch;
 
 typedef struct dm_unet dm_unet;
@@ -72,9 +79,11 @@ int dm_unet_param_count(const dm_unet_arch* arch, int* n_params);
 int dm_unet_create(const dm_unet_arch* arch, const float* const* params, const int64_t* numels,
                    int n_params, void* stream, dm_unet** out);
 /* x: [B, in_channels, H, W] f32, t: [B] int64, out: [B, out_channels, H, W] f32.
+ * y: [B] int64 class labels or NULL (variant 1; y[b] < 0 = no class for that row, which lets
+ * the conditional and unconditional CFG branches run as one 2B batch).
  * Workspace for batch B at H x W is allocated on first use and cached. */
-int dm_unet_forward(dm_unet* m, const float* x, const int64_t* t, int B, int H, int W, float* out,
-                    void* stream);
+int dm_unet_forward(dm_unet* m, const float* x, const int64_t* t, const int64_t* y, int B, int H, int W,
+                    float* out, void* stream);
 /* Install the sinusoid frequency table exp(-ln(1e4)/(dim/2-1) * i), i < dim/2
  * (models/modules.py:52-54). The reference evaluates it with torch's CPU exp,
  * whose last bit is host dependent; hosts pass the table they compute with

@@ -235,5 +235,61 @@ def main():
     save('trajectory', tmeta, **tr)
 
 
+ADAGN_ARCHS = {
+    # the reference CFG-CIFAR config (configs/ddpm_cfg_cifar10.yaml:17-28)
+    'cfg_cifar10': dict(in_channels=3, out_channels=3, dim=128, dim_mults=[1, 2, 2, 2],
+                        use_attn=[False, True, True, False], num_res_blocks=2, num_classes=10,
+                        attn_head_dims=64, resblock_updown=True, dropout=0.1),
+    # reduced: ResBlock up/down, 2-head attention at 8x8
+    'tiny_updown': dict(in_channels=3, out_channels=3, dim=32, dim_mults=[1, 2], use_attn=[False, True],
+                        num_res_blocks=1, num_classes=5, attn_head_dims=32, resblock_updown=True, dropout=0.0),
+    # reduced: conv down/upsample, no class embedding (y is ignored)
+    'tiny_conv': dict(in_channels=1, out_channels=2, dim=32, dim_mults=[1, 2, 2], use_attn=[True, False, True],
+                      num_res_blocks=1, num_classes=None, attn_head_dims=32, resblock_updown=False, dropout=0.0),
+}
+
+
+def make_adagn():
+    """UNetCategorialAdaGN forwards (with and without labels) and a DDIMCFG trajectory."""
+    torch.set_num_threads(8)
+    schedule, ddpm, ddim, _ = import_reference()
+    import models.unet_categorial_adagn as ua  # noqa: E402
+    common = dict(torch=torch.__version__, threads=torch.get_num_threads(),
+                  reference='xyfJASON/diffusion-models-pytorch @ 2024-12-20 (/root/reference)',
+                  archs=ADAGN_ARCHS)
+    g = torch.Generator().manual_seed(17)
+    fx = {}
+    for name, arch in ADAGN_ARCHS.items():
+        model = ua.UNetCategorialAdaGN(**arch).eval()
+        common[f'{name}_weights_sha256'] = synthetic(model)
+        common[f'{name}_state_dict'] = [[k, list(v.shape)] for k, v in model.state_dict().items()]
+        H = 32 if name == 'cfg_cifar10' else 16
+        x = torch.randn((2, arch['in_channels'], H, H), generator=g)
+        t = torch.tensor([999, 3]) if name == 'cfg_cifar10' else torch.tensor([17, 640])
+        y = torch.tensor([3, 1])
+        with torch.no_grad():
+            fx[f'{name}_out_y'] = model(x, t, y)
+            fx[f'{name}_out_none'] = model(x, t, None)
+        fx[f'{name}_x'], fx[f'{name}_t'], fx[f'{name}_labels'] = x, t, y
+    # DDIMCFG-10 (s = 3) on the reduced up/down model, labels [1, 4], init noise seed 5
+    model = ua.UNetCategorialAdaGN(**ADAGN_ARCHS['tiny_updown']).eval()
+    synthetic(model)
+    d = ddim.DDIMCFG(guidance_scale=3.0, respace_type='uniform', respace_steps=10, eta=0.0)
+    torch.manual_seed(5)
+    init = torch.randn((2, 3, 16, 16))
+    labels = torch.tensor([1, 4])
+    fx['cfg_init'], fx['cfg_labels'] = init, labels
+    with torch.no_grad():
+        for i, out in enumerate(d.sample_loop(model, init, model_kwargs=dict(y=labels))):
+            fx[f'cfg_step{i}_sample'] = out['sample']
+            fx[f'cfg_step{i}_pred_eps'] = out['pred_eps']
+    common['cfg'] = dict(guidance_scale=3.0, respace_type='uniform', respace_steps=10, eta=0.0)
+    save('adagn', common, **fx)
+
+
 if __name__ == '__main__':
-    main()
+    if sys.argv[1:] == ['adagn']:
+        make_adagn()
+    else:
+        main()
+        make_adagn()

@@ -1,0 +1,109 @@
+"""UNetCategorialAdaGN (models/unet_categorial_adagn.py) on the MI355X path vs the reference.
+
+Golden fixtures: tests/golden/adagn.npz, made by tests/golden/make_golden.py from
+the reference module itself. Tolerance: fp32 max-abs <= 1e-4 (north_star).
+"""
+import numpy as np
+import pytest
+import torch
+
+from diffusions import DDIMCFG
+from models.unet_categorial_adagn import UNetCategorialAdaGN
+from utils.synthetic import init_synthetic_
+
+TOL = 1e-4
+NAMES = ['tiny_updown', 'tiny_conv', 'cfg_cifar10']
+
+
+def _model(meta, name):
+    m = UNetCategorialAdaGN(**meta['archs'][name]).eval()
+    sha = init_synthetic_(m)
+    return m, sha
+
+
+@pytest.mark.parametrize('name', NAMES)
+def test_adagn_state_dict_layout(golden, name):
+    _, meta = golden('adagn')
+    m = UNetCategorialAdaGN(**meta['archs'][name])
+    assert [[k, list(v.shape)] for k, v in m.state_dict().items()] == meta[f'{name}_state_dict']
+
+
+def test_adagn_param_count_matches_abi(golden):
+    """dm_unet_param_count (no GPU needed) walks the same registration order as the module."""
+    import ctypes
+    from dmhip._lib import load
+    _, meta = golden('adagn')
+    for name in NAMES:
+        m = UNetCategorialAdaGN(**meta['archs'][name])
+        n = ctypes.c_int()
+        rc = load().dm_unet_param_count(ctypes.byref(m._arch_struct()), ctypes.byref(n))
+        assert rc == 0 and n.value == len(m.state_dict()), name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', NAMES)
+def test_adagn_forward_vs_reference(cuda, golden, report, name):
+    g, meta = golden('adagn')
+    model, sha = _model(meta, name)
+    assert sha == meta[f'{name}_weights_sha256']
+    model = model.to(cuda)
+    x = torch.from_numpy(g[f'{name}_x']).to(cuda)
+    t = torch.from_numpy(g[f'{name}_t']).to(cuda)
+    y = torch.from_numpy(g[f'{name}_labels']).to(cuda)
+    out_y = model(x, t, y).cpu()
+    out_n = model(x, t, None).cpu()
+    e_y = (out_y - torch.from_numpy(g[f'{name}_out_y'])).abs().max().item()
+    e_n = (out_n - torch.from_numpy(g[f'{name}_out_none'])).abs().max().item()
+    report(f'adagn_forward_{name}_y_maxabs_vs_reference', e_y)
+    report(f'adagn_forward_{name}_none_maxabs_vs_reference', e_n)
+    assert e_y <= TOL and e_n <= TOL, (e_y, e_n)
+    # per-row null label (y = -1) equals the y=None call: the batched-CFG contract
+    mixed = model(x, t, torch.tensor([-1, int(g[f'{name}_labels'][1])], device=cuda)).cpu()
+    assert torch.equal(mixed[0], out_n[0])
+    assert torch.equal(mixed[1], out_y[1])
+
+
+@pytest.mark.gpu
+def test_adagn_label_out_of_range(cuda, golden):
+    _, meta = golden('adagn')
+    model, _ = _model(meta, 'tiny_updown')
+    model = model.to(cuda)
+    x = torch.zeros((1, 3, 16, 16), device=cuda)
+    t = torch.zeros((1, ), dtype=torch.long, device=cuda)
+    with pytest.raises(IndexError):
+        model(x, t, torch.tensor([5], device=cuda))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('batched', [True, False])
+def test_ddimcfg_trajectory_vs_reference(cuda, golden, report, batched):
+    g, meta = golden('adagn')
+    model, _ = _model(meta, 'tiny_updown')
+    model = model.to(cuda)
+    cfg = meta['cfg']
+    d = DDIMCFG(guidance_scale=cfg['guidance_scale'], respace_type=cfg['respace_type'],
+                respace_steps=cfg['respace_steps'], eta=cfg['eta'], device=cuda)
+    d.batch_cfg = batched
+    init = torch.from_numpy(g['cfg_init']).to(cuda)
+    labels = torch.from_numpy(g['cfg_labels']).to(cuda)
+    worst = 0.0
+    for i, out in enumerate(d.sample_loop(model, init, model_kwargs=dict(y=labels))):
+        err = np.abs(out['sample'].cpu().numpy() - g[f'cfg_step{i}_sample']).max()
+        worst = max(worst, float(err))
+        assert err <= TOL, (i, err)
+    report(f'ddimcfg10_adagn_{"batched" if batched else "two_calls"}_maxabs_vs_reference', worst)
+
+
+@pytest.mark.gpu
+def test_adagn_batch_invariance(cuda, golden):
+    """Row b of a B=64 batch equals the same row run at B=2 (no cross-row reduction anywhere)."""
+    g, meta = golden('adagn')
+    model, _ = _model(meta, 'cfg_cifar10')
+    model = model.to(cuda)
+    gen = torch.Generator().manual_seed(3)
+    x = torch.randn((64, 3, 32, 32), generator=gen).to(cuda)
+    t = torch.randint(0, 1000, (64, ), generator=gen).to(cuda)
+    y = torch.randint(-1, 10, (64, ), generator=gen).to(cuda)
+    big = model(x, t, y)
+    small = model(x[5:7].contiguous(), t[5:7].contiguous(), y[5:7].contiguous())
+    assert torch.equal(big[5:7], small)
