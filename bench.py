@@ -22,6 +22,7 @@ bit-equal to it at equal thread count) timed on this host's cores, rank 0 /
 N=1 only, on one denoising step of the same B=256 fold, extrapolated x50.
 """
 import argparse
+import ctypes
 import json
 import os
 import platform
@@ -53,6 +54,24 @@ def parse():
     ap.add_argument('--cpu-batch', type=int, default=256, help='batch of the timed CPU denoising step')
     ap.add_argument('--profile-json', default=None, help='write the per-op profile here (rank 0)')
     return ap.parse_args()
+
+
+def pmc_traffic(label):
+    """HBM bytes per launch of `label` from the newest committed PMC summary (profiles/rNN_vM_pmc.json,
+    FETCH_SIZE x2 + WRITE_SIZE passes of this bench, tools/gpu_profile.sh)."""
+    import glob
+    import re
+
+    def order(path):
+        m = re.search(r'r(\d+)_v(\d+)_pmc\.json$', path)
+        return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
+    files = sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*_v*_pmc.json')), key=order)
+    for path in reversed(files):
+        with open(path) as f:
+            k = json.load(f).get('kernels', {}).get(label)
+        if k and k.get('hbm_bytes_per_launch'):
+            return float(k['hbm_bytes_per_launch']), os.path.relpath(path, ROOT)
+    return None, None
 
 
 def cpu_model_name():
@@ -97,6 +116,7 @@ def main():
     dev = torch.device('cuda', local_rank)
 
     import dmhip
+    from dmhip._lib import check as _check
     from diffusions import DDIM
     from models.unet import UNet
     from utils.synthetic import init_synthetic_
@@ -143,6 +163,8 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = tt.item()
     prof = dmhip.unet_profile_read(handle)
+    wbytes, wsbytes = ctypes.c_int64(), ctypes.c_int64()
+    _check(dmhip.load().dm_unet_memory(handle, ctypes.byref(wbytes), ctypes.byref(wsbytes)), 'dm_unet_memory')
     dmhip.unet_profile_enable(handle, False)
 
     # roofline of the dominant kernel family (most GPU time in the timed region)
@@ -165,7 +187,9 @@ def main():
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
         roof = dict(bound='hbm', achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit='GB/s',
                     frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None)
-    roof.update(kernel=dom_name, avg_launch_ms=round(avg_ms, 4), launches=dom['launches'],
+    traffic, traffic_src = pmc_traffic(dom_name)
+    roof.update(traffic=traffic, traffic_source=traffic_src, algorithmic_bytes_per_launch=bytes_per_launch,
+                kernel=dom_name, avg_launch_ms=round(avg_ms, 4), launches=dom['launches'],
                 algorithmic_per_launch=flops_per_launch if flops_per_launch > 0 else bytes_per_launch)
     total_gpu_ms = sum(f['ms'] for f in fam.values())
     total_flops = sum(f['flops'] for f in fam.values())
@@ -188,7 +212,8 @@ def main():
             config=dict(workload=f'DDIM-{args.respace_steps} (eta=0) sampling fold, CIFAR-10 UNet '
                                  f'(dim 128, mults 1-2-2-2, 35.7M params, synthetic weights), 3x32x32, '
                                  f'B={B} per GPU',
-                        global_batch=world * B, parallelism=f'dp{world}', denoise_steps=args.respace_steps),
+                        global_batch=world * B, parallelism=f'dp{world}', denoise_steps=args.respace_steps,
+                        weights_gb=round(wbytes.value / 1e9, 3), workspace_gb=round(wsbytes.value / 1e9, 3)),
             roofline=roof,
             step_level=dict(model_tflops=round(total_flops / (total_gpu_ms * 1e-3) / 1e12, 2) if total_gpu_ms else None,
                             kernel_time_frac=round(total_gpu_ms * 1e-3 / elapsed, 4)),

@@ -310,11 +310,19 @@ int conv_pick(const ConvArgs& a) {
   return 2;
 }
 
+// The exact kernel instantiation (matches the rocprofv3 kernel name with spaces removed).
 std::string conv_label(const ConvArgs& a) {
   static const char* names[] = {"conv_igemm_kernel<128,128,64,64>", "conv_igemm_kernel<128,64,64,32>",
-                                "conv_igemm_kernel<64,64,32,32>",   "conv_patch_kernel<128,128,64,64>",
-                                "conv_patch_kernel<128,64,64,32>",  "conv_patch_kernel<64,64,32,32>"};
-  return names[conv_pick(a)];
+                                "conv_igemm_kernel<64,64,32,32>",   "conv_patch_kernel<128,128,64,64",
+                                "conv_patch_kernel<128,64,64,32",   "conv_patch_kernel<64,64,32,32"};
+  const int p = conv_pick(a);
+  std::string s = names[p];
+  if (p >= 3) {  // <BM,BN,WM,WN,UP,MAXP,PRO>; MAXP 288 for 128-row tiles, 160 for 64-row tiles
+    s += a.upsample ? ",true" : ",false";
+    s += p == 5 ? ",160" : ",288";
+    s += a.pro_scale ? ",true>" : ",false>";
+  }
+  return s;
 }
 
 }  // namespace dm
