@@ -102,6 +102,7 @@ extern "C" int dm_gemm(const dm_gemm_desc* d, void* stream) {
   g.Bm = d->B; g.b_s1 = d->b_s1; g.b_s2 = d->b_s2; g.ldb = d->ldb; g.b_kn = d->b_kn;
   g.C = d->C; g.c_s1 = d->c_s1; g.c_s2 = d->c_s2; g.ldc = d->ldc;
   g.alpha = d->alpha; g.bias = d->bias; g.res = d->res; g.ld_res = d->ld_res; g.act = d->act;
+  g.b_scale = d->b_scale;
   return dm::gemm_batched(g, (hipStream_t)stream);
 }
 

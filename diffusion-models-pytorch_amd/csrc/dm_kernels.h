@@ -55,6 +55,7 @@ struct GemmArgs {
   long c_s1, c_s2;
   int ldc;
   float alpha;          // multiplies A elements on load (rounded per element)
+  float b_scale;        // nonzero: multiplies B elements on load ([n][k] layout only; ADM q*s, k*s)
   const float* bias;    // [N] or null
   const float* res;     // residual [M][ld_res] (batch 0 layout only) or null
   int ld_res;

@@ -1,4 +1,4 @@
-// Batched fp32 MFMA GEMM: C[z][m][n] = act( sum_k (alpha * A[z][m][k]) * B[z](k, n) + bias[n] )
+// Batched fp32 MFMA GEMM: C[z][m][n] = act( sum_k (alpha * A[z][m][k]) * (b_scale * B[z](k, n)) + bias[n] )
 //
 // Used for the small dense contractions of the denoisers:
 //   * nn.Linear layers (time MLP models/unet.py:64-69, ResBlock proj :18-21)
@@ -115,7 +115,7 @@ gemm_kernel(GemmArgs g) {
 #pragma unroll
       for (int j = 0; j < Cfg::B_ITERS; ++j)
         *reinterpret_cast<f4*>(Bs + (lrow + j * Cfg::ROWS_PER_PASS) * kLDK + 4 * lc4) =
-            (b_ok[j] && k_ok) ? rb[j] : zero4;
+            (b_ok[j] && k_ok) ? (g.b_scale != 0.0f && g.b_scale != 1.0f ? rb[j] * g.b_scale : rb[j]) : zero4;
     } else {
       const int n4 = t % KN_C4, kr = t / KN_C4;
 #pragma unroll
@@ -195,6 +195,7 @@ int gemm_batched(const GemmArgs& g, hipStream_t st) {
              "gemm: operands must be 16-byte aligned");
   DM_REQUIRE(g.Z1 >= 1 && g.Z2 >= 1 && (long)g.Z1 * g.Z2 <= 65535, "gemm: batch out of range");
   DM_REQUIRE(!g.pro_scale || (g.pro_shift && g.pro_rows > 0 && !g.b_kn), "gemm: A prologue needs scale, shift, rows");
+  DM_REQUIRE(g.b_scale == 0.0f || !g.b_kn, "gemm: B scaling needs the [n][k] B layout");
   if (gemm_pick(g) == 0) return launch_gemm<128, 128, 64, 64>(g, st);
   return launch_gemm<64, 64, 32, 32>(g, st);
 }

@@ -95,6 +95,8 @@ struct ResBlockP {
 
 struct AttnP {
   int C, heads;
+  bool legacy = false;  // ADM QKVAttentionLegacy: head h owns qkv channels [h*3d, (h+1)*3d) = [q; k; v]
+  float sa = 1.f, sb = 0.f;  // scale applied to q (and to k when sb != 0) elements
   GnP gn;
   size_t wqkv, bqkv, wproj, bproj;
 };
@@ -134,7 +136,8 @@ struct UNetModel {
   size_t te_w1, te_b1, te_w2, te_b2;
   size_t te_freqs;            // [dim/2] sinusoid frequencies
   bool te_freqs_set = false;  // host table installed (else computed on device)
-  size_t class_embed = 0;     // variant 1: [num_classes][4 dim]
+  size_t class_embed = 0;     // variants 1, 2: [num_classes][4 dim]
+  bool has_class = false;
   size_t first_w, first_b;
   size_t proj_w, proj_b;
   int proj_total = 0;
@@ -196,15 +199,31 @@ UNetModel::~UNetModel() {
   if (arena) (void)hipFree(arena);
 }
 
+// Channels of the first conv / last conv input: dim (models/unet.py:72) or
+// channel_mult[0] * model_channels (models/adm/unet.py:499).
+static int first_channels(const dm_unet_arch& a) { return a.variant == 2 ? a.dim * a.dim_mults[0] : a.dim; }
+
+// Heads of an attention block with C channels; where: 0 down path, 1 bottleneck, 2 up path.
+static int attn_heads(const dm_unet_arch& a, int C, int where) {
+  if (a.variant == 2) {  // models/adm/unet.py:296-302, 470-471, 606
+    if (a.attn_head_dims > 0) return C / a.attn_head_dims;
+    return where == 2 ? a.n_heads_up : a.n_heads;
+  }
+  if (where == 1) return 1;  // SelfAttentionBlock(cur_dim) default n_heads (unet.py:95)
+  return a.variant == 1 ? C / a.attn_head_dims : a.n_heads;
+}
+
 static int count_params(const dm_unet_arch& a) {
   // mirrors the registration order of models/unet.py:47-119 (variant 1:
-  // models/unet_categorial_adagn.py:77-163, same counts per block)
-  int n = 4 + 2;  // time_embed (2 linears), first_conv
-  if (a.variant == 1 && a.num_classes > 0) n += 1;  // class_embed.weight
+  // models/unet_categorial_adagn.py:77-163; variant 2: models/adm/unet.py:489-635)
+  int n = 4 + 2;  // time_embed (2 linears), first conv
+  if (a.variant >= 1 && a.num_classes > 0) n += 1;  // class_embed.weight / label_emb.weight
   auto rb = [](int cin, int cout) { return 10 + (cin != cout ? 2 : 0); };
-  const int attn = 10;
-  int cur = a.dim;
-  std::vector<int> dims{a.dim};
+  const int attn = a.variant == 2 ? 6 : 10;  // norm, qkv, proj_out  |  norm, q, k, v, proj
+  const bool rb_updown = a.variant >= 1 && a.resblock_updown;
+  const int resample = (a.variant == 2 && a.pool_resample) ? 0 : 2;  // conv down/up-sample parameters
+  int cur = first_channels(a);
+  std::vector<int> dims{cur};
   for (int i = 0; i < a.n_stages; ++i) {
     int out = a.dim * a.dim_mults[i];
     for (int j = 0; j < a.num_res_blocks; ++j) {
@@ -214,7 +233,7 @@ static int count_params(const dm_unet_arch& a) {
       cur = out;
     }
     if (i < a.n_stages - 1) {
-      n += (a.variant == 1 && a.resblock_updown) ? rb(out, out) : 2;  // ResBlockDownsample or conv
+      n += rb_updown ? rb(out, out) : resample;  // ResBlock(down) or Downsample
       dims.push_back(out);
     }
   }
@@ -228,9 +247,9 @@ static int count_params(const dm_unet_arch& a) {
       if (a.use_attn[i]) n += attn;
       cur = out;
     }
-    if (i > 0) n += (a.variant == 1 && a.resblock_updown) ? rb(out, out) : 2;  // ResBlockUpsample or conv
+    if (i > 0) n += rb_updown ? rb(out, out) : resample;  // ResBlock(up) or Upsample
   }
-  n += 4;  // last_conv GN + conv
+  n += 4;  // last GN + conv
   return n;
 }
 
@@ -238,21 +257,30 @@ static int validate_arch(const dm_unet_arch* a) {
   DM_REQUIRE(a != nullptr, "arch is null");
   DM_REQUIRE(a->n_stages >= 1 && a->n_stages <= DM_MAX_STAGES, "n_stages out of range");
   DM_REQUIRE(a->dim >= 32 && a->dim % 32 == 0, "dim must be a positive multiple of 32");
-  DM_REQUIRE(a->in_channels >= 1 && a->in_channels <= 16, "in_channels out of range (1..16)");
+  DM_REQUIRE(a->in_channels >= 1 && a->in_channels <= 4, "in_channels out of range (1..4)");
   DM_REQUIRE(a->out_channels >= 1 && a->out_channels <= 8, "out_channels out of range (1..8)");
   DM_REQUIRE(a->num_res_blocks >= 1, "num_res_blocks must be >= 1");
-  DM_REQUIRE(a->variant == 0 || a->variant == 1, "variant must be 0 (UNet) or 1 (UNetCategorialAdaGN)");
+  DM_REQUIRE(a->variant >= 0 && a->variant <= 2,
+             "variant must be 0 (UNet), 1 (UNetCategorialAdaGN) or 2 (ADM UNetModel)");
   if (a->variant == 0) DM_REQUIRE(a->n_heads >= 1, "n_heads must be >= 1");
-  if (a->variant == 1) {
-    DM_REQUIRE(a->attn_head_dims >= 1, "attn_head_dims must be >= 1");
-    DM_REQUIRE(a->num_classes >= 0, "num_classes must be >= 0");
-  }
+  if (a->variant == 1) DM_REQUIRE(a->attn_head_dims >= 1, "attn_head_dims must be >= 1");
+  if (a->variant == 2 && a->attn_head_dims <= 0)
+    DM_REQUIRE(a->n_heads >= 1 && a->n_heads_up >= 1, "num_heads / num_heads_upsample must be >= 1");
+  DM_REQUIRE(a->num_classes >= 0, "num_classes must be >= 0");
   for (int i = 0; i < a->n_stages; ++i) {
     DM_REQUIRE(a->dim_mults[i] >= 1, "dim_mults must be >= 1");
     const int c = a->dim * a->dim_mults[i];
-    if (a->use_attn[i])
-      DM_REQUIRE(c % (a->variant == 1 ? a->attn_head_dims : a->n_heads) == 0, "channels not divisible by heads");
+    DM_REQUIRE(c % 32 == 0, "stage channels must be multiples of 32 (GroupNorm(32) / MFMA tiles)");
+    if (a->use_attn[i]) {
+      for (int where : {0, 2}) {
+        const int h = attn_heads(*a, c, where);
+        DM_REQUIRE(h >= 1 && c % h == 0 && (c / h) % 4 == 0, "attention channels not divisible by heads");
+      }
+    }
   }
+  const int cb = a->dim * a->dim_mults[a->n_stages - 1];
+  const int hb = attn_heads(*a, cb, 1);
+  DM_REQUIRE(hb >= 1 && cb % hb == 0 && (cb / hb) % 4 == 0, "bottleneck channels not divisible by heads");
   return DM_OK;
 }
 
@@ -271,18 +299,22 @@ static int unet_create(const dm_unet_arch* arch, const float* const* params, con
   m->arch = a;
   ParamReader rd{params, numels, n_params};
   Packer pk;
-  const int D = a.dim, TD = 4 * a.dim;
+  const int D = a.dim, TD = 4 * a.dim, C0 = first_channels(a);
+  const bool adm = a.variant == 2;
 
   // time embedding MLP: Linear(D, 4D) -> SiLU -> Linear(4D, 4D)
-  m->te_w1 = pk.raw(rd.take((int64_t)TD * D, "time_embed.1.weight"), (int64_t)TD * D);
-  m->te_b1 = pk.raw(rd.take(TD, "time_embed.1.bias"), TD);
-  m->te_w2 = pk.raw(rd.take((int64_t)TD * TD, "time_embed.3.weight"), (int64_t)TD * TD);
-  m->te_b2 = pk.raw(rd.take(TD, "time_embed.3.bias"), TD);
+  m->te_w1 = pk.raw(rd.take((int64_t)TD * D, "time_embed Linear 1 weight"), (int64_t)TD * D);
+  m->te_b1 = pk.raw(rd.take(TD, "time_embed Linear 1 bias"), TD);
+  m->te_w2 = pk.raw(rd.take((int64_t)TD * TD, "time_embed Linear 2 weight"), (int64_t)TD * TD);
+  m->te_b2 = pk.raw(rd.take(TD, "time_embed Linear 2 bias"), TD);
   m->te_freqs = pk.reserve(D / 2);
-  if (a.variant == 1 && a.num_classes > 0)  // unet_categorial_adagn.py:104
-    m->class_embed = pk.raw(rd.take((int64_t)a.num_classes * TD, "class_embed.weight"), (int64_t)a.num_classes * TD);
-  m->first_w = pk.raw(rd.take((int64_t)D * a.in_channels * 9, "first_conv.weight"), (int64_t)D * a.in_channels * 9);
-  m->first_b = pk.raw(rd.take(D, "first_conv.bias"), D);
+  if (a.variant >= 1 && a.num_classes > 0) {  // unet_categorial_adagn.py:104, adm/unet.py:496-497
+    m->class_embed = pk.raw(rd.take((int64_t)a.num_classes * TD, "class_embed / label_emb weight"),
+                            (int64_t)a.num_classes * TD);
+    m->has_class = true;
+  }
+  m->first_w = pk.raw(rd.take((int64_t)C0 * a.in_channels * 9, "first conv weight"), (int64_t)C0 * a.in_channels * 9);
+  m->first_b = pk.raw(rd.take(C0, "first conv bias"), C0);
 
   // Projections are collected then packed into one matrix after the walk.
   struct ProjSrc { const float* w; const float* b; int cout; };
@@ -298,11 +330,13 @@ static int unet_create(const dm_unet_arch* arch, const float* const* params, con
   // variant 0 (models/unet.py:14-44): blk1 (GN, conv), proj, blk2 (GN, conv), shortcut
   // variant 1 (models/unet_categorial_adagn.py:31-42): blk1 (GN, conv), adagn (gn, proj -> 2 cout),
   //           blk2 conv, shortcut
+  // variant 2 (models/adm/unet.py:201-241): in_layers (GN, conv), emb_layers (Linear -> cout or 2 cout
+  //           with use_scale_shift_norm), out_layers (GN, conv), skip_connection
   auto resblock = [&](int cin, int cout, int updown) {
     ResBlockP r;
     r.cin = cin;
     r.cout = cout;
-    r.adagn = a.variant == 1;
+    r.adagn = a.variant == 1 || (adm && a.scale_shift_norm);
     r.updown = updown;
     r.gn1 = gn(cin, "ResBlock.blk1.0 (GroupNorm)");
     const float* w1 = rd.take((int64_t)cout * cin * 9, "ResBlock.blk1.2.weight");
@@ -312,13 +346,14 @@ static int unet_create(const dm_unet_arch* arch, const float* const* params, con
     pk.conv_at(w1, cout, cin, 9, 9 * cin, 0, r.conv1.w);
     r.conv1.bias = pk.raw(b1, cout);
     const int pn = r.adagn ? 2 * cout : cout;
-    if (r.adagn) r.gn2 = gn(cout, "ResBlock.adagn.gn");
+    const bool gn2_first = a.variant == 1;  // AdaGN registers its gn before its proj
+    if (gn2_first) r.gn2 = gn(cout, "ResBlock.adagn.gn");
     const float* pw = rd.take((int64_t)pn * TD, r.adagn ? "ResBlock.adagn.proj.1.weight" : "ResBlock.proj.1.weight");
     const float* pb = rd.take(pn, r.adagn ? "ResBlock.adagn.proj.1.bias" : "ResBlock.proj.1.bias");
     r.proj_col = m->proj_total;
     m->proj_total += pn;
     projs.push_back({pw, pb, pn});
-    if (!r.adagn) r.gn2 = gn(cout, "ResBlock.blk2.0 (GroupNorm)");
+    if (!gn2_first) r.gn2 = gn(cout, "ResBlock second GroupNorm");
     const float* w2 = rd.take((int64_t)cout * cout * 9, "ResBlock.blk2 conv weight");
     const float* b2 = rd.take(cout, "ResBlock.blk2 conv bias");
     const int K2 = 9 * cout + (cin != cout ? cin : 0);
@@ -341,6 +376,23 @@ static int unet_create(const dm_unet_arch* arch, const float* const* params, con
     AttnP p;
     p.C = C;
     p.heads = heads;
+    const int Dh = C / heads;
+    if (adm) {
+      // AttentionBlock (adm/unet.py:304-313): norm, qkv Conv1d [3C][C], proj_out Conv1d [C][C];
+      // q and k each scaled by ch^-1/4 (adm/unet.py:367-370)
+      p.legacy = a.attn_legacy != 0;
+      p.sa = p.sb = (float)(1.0 / std::sqrt(std::sqrt((double)Dh)));
+      p.gn = gn(C, "AttentionBlock.norm");
+      p.wqkv = pk.raw(rd.take((int64_t)3 * C * C, "AttentionBlock.qkv.weight"), (int64_t)3 * C * C);
+      p.bqkv = pk.raw(rd.take(3 * C, "AttentionBlock.qkv.bias"), 3 * C);
+      p.wproj = pk.raw(rd.take((int64_t)C * C, "AttentionBlock.proj_out.weight"), (int64_t)C * C);
+      p.bproj = pk.raw(rd.take(C, "AttentionBlock.proj_out.bias"), C);
+      m->attn.push_back(p);
+      return (int)m->attn.size() - 1;
+    }
+    // SelfAttentionBlock (modules.py:78-87): q * (C/heads)^-1/2 (modules.py:95)
+    p.sa = (float)std::pow((double)Dh, -0.5);
+    p.sb = 0.f;
     p.gn = gn(C, "SelfAttentionBlock.norm");
     p.wqkv = pk.reserve((int64_t)3 * C * C);
     p.bqkv = pk.reserve(3 * C);
@@ -356,6 +408,7 @@ static int unet_create(const dm_unet_arch* arch, const float* const* params, con
     return (int)m->attn.size() - 1;
   };
   auto sampleconv = [&](int C, const char* what) {
+    if (adm && a.pool_resample) return -1;  // avg-pool / nearest only (adm/unet.py:126-128, 153-155)
     ConvP c{0, 0, C, C, 9, 9 * C};
     const float* w = rd.take((int64_t)C * C * 9, what);
     const float* b = rd.take(C, what);
@@ -366,11 +419,9 @@ static int unet_create(const dm_unet_arch* arch, const float* const* params, con
     return (int)m->convs.size() - 1;
   };
 
-  const bool rb_updown = a.variant == 1 && a.resblock_updown;
-  // stage attention heads: variant 0 n_heads; variant 1 C / attn_head_dims (unet_categorial_adagn.py:118-121)
-  auto stage_heads = [&](int C) { return a.variant == 1 ? C / a.attn_head_dims : a.n_heads; };
-  // ---- down path (models/unet.py:77-90, forward :126-136)
-  int cur = D, level = 0, n_skips = 0;
+  const bool rb_updown = a.variant >= 1 && a.resblock_updown;
+  // ---- down path (models/unet.py:77-90, forward :126-136; adm/unet.py:506-556, forward :674-676)
+  int cur = C0, level = 0, n_skips = 0;
   std::vector<int> skip_stack;  // skip ids
   auto push_skip = [&](int C, int lvl) {
     m->skip_C.push_back(C);
@@ -378,7 +429,7 @@ static int unet_create(const dm_unet_arch* arch, const float* const* params, con
     skip_stack.push_back(n_skips);
     return n_skips++;
   };
-  const int s0 = push_skip(D, 0);  // first_conv output
+  const int s0 = push_skip(C0, 0);  // first conv output
   (void)s0;
   for (int i = 0; i < a.n_stages; ++i) {
     const int out = D * a.dim_mults[i];
@@ -386,7 +437,7 @@ static int unet_create(const dm_unet_arch* arch, const float* const* params, con
       Node n{N_RES, resblock(cur, out, 0), cur, out, 0, level, level};
       m->nodes.push_back(n);
       if (a.use_attn[i]) {
-        Node na{N_ATTN, attnblock(out, stage_heads(out)), out, out, 0, level, level};
+        Node na{N_ATTN, attnblock(out, attn_heads(a, out, 0)), out, out, 0, level, level};
         m->nodes.push_back(na);
       }
       m->nodes.back().skip_producer = true;
@@ -404,9 +455,9 @@ static int unet_create(const dm_unet_arch* arch, const float* const* params, con
     }
   }
   m->n_levels = level + 1;
-  // ---- bottleneck (models/unet.py:93-97; attention with the default n_heads = 1)
+  // ---- bottleneck (models/unet.py:93-97; adm/unet.py:558-582)
   m->nodes.push_back(Node{N_RES, resblock(cur, cur, 0), cur, cur, 0, level, level});
-  m->nodes.push_back(Node{N_ATTN, attnblock(cur, 1), cur, cur, 0, level, level});
+  m->nodes.push_back(Node{N_ATTN, attnblock(cur, attn_heads(a, cur, 1)), cur, cur, 0, level, level});
   m->nodes.push_back(Node{N_RES, resblock(cur, cur, 0), cur, cur, 0, level, level});
   // ---- up path (models/unet.py:101-112, forward :142-149)
   for (int i = a.n_stages - 1; i >= 0; --i) {
@@ -420,7 +471,7 @@ static int unet_create(const dm_unet_arch* arch, const float* const* params, con
       n.concat_cx = cur;
       m->nodes.push_back(n);
       if (a.use_attn[i])
-        m->nodes.push_back(Node{N_ATTN, attnblock(out, stage_heads(out)), out, out, 0, level, level});
+        m->nodes.push_back(Node{N_ATTN, attnblock(out, attn_heads(a, out, 2)), out, out, 0, level, level});
       cur = out;
     }
     if (i > 0) {
@@ -431,7 +482,7 @@ static int unet_create(const dm_unet_arch* arch, const float* const* params, con
       --level;
     }
   }
-  // ---- last conv (models/unet.py:115-119)
+  // ---- last conv (models/unet.py:115-119; adm/unet.py:631-635 `out`)
   m->last_gn = gn(cur, "last_conv.0 (GroupNorm)");
   m->last_w = pk.raw(rd.take((int64_t)a.out_channels * cur * 9, "last_conv.2.weight"), (int64_t)a.out_channels * cur * 9);
   m->last_b = pk.raw(rd.take(a.out_channels, "last_conv.2.bias"), a.out_channels);
@@ -501,13 +552,13 @@ int UNetModel::build_plan(int B, int H, int W) {
   };
   auto Hl = [&](int lvl) { return H >> lvl; };
   auto Wl = [&](int lvl) { return W >> lvl; };
-  const int D = arch.dim, TD = 4 * arch.dim, G = 32;
+  const int D = arch.dim, TD = 4 * arch.dim, G = 32, C0 = skip_C[0];
 
   // --- temb workspace
   float* e0 = alloc((size_t)B * D * 4);
   float* e1 = alloc((size_t)B * TD * 4);
   float* se = alloc((size_t)B * TD * 4);
-  float* e2 = arch.variant == 1 ? alloc((size_t)B * TD * 4) : nullptr;
+  float* e2 = has_class ? alloc((size_t)B * TD * 4) : nullptr;
   float* projs = alloc((size_t)B * proj_total * 4);
 
   // --- scratch sizes
@@ -531,7 +582,7 @@ int UNetModel::build_plan(int B, int H, int W) {
     }
   }
   max_chunks = std::max(max_chunks, gn_num_chunks(H * W));
-  float* a1 = alloc(std::max(max_a1, (size_t)B * H * W * D) * 4);
+  float* a1 = alloc(std::max(max_a1, (size_t)B * H * W * C0) * 4);
   float* hbuf = alloc(max_h * 4);
   float* a2 = alloc(max_h * 4);
   float* an = alloc(std::max<size_t>(max_attn, 1) * 4);
@@ -541,7 +592,7 @@ int UNetModel::build_plan(int B, int H, int W) {
   float* xr = alloc(std::max<size_t>(max_xr, 1) * 4);  // resampled residual of up/down ResBlocks
   double2* part = (double2*)alloc((size_t)B * max_chunks * G * sizeof(double2));
   // per-(image, channel) GroupNorm affine for the fused conv prologues
-  size_t max_c = (size_t)D;
+  size_t max_c = (size_t)C0;
   for (auto& n : nodes) max_c = std::max(max_c, (size_t)std::max(n.cin, n.cout));
   float* gsc = alloc((size_t)B * max_c * 4);
   float* gsh = alloc((size_t)B * max_c * 4);
@@ -594,7 +645,9 @@ int UNetModel::build_plan(int B, int H, int W) {
 
   // temb
   add("timestep_embed", 0, 4.0 * B * D, [=](hipStream_t st) {
-    return timestep_embed(P_->t, B, D, 0, self->te_freqs_set ? self->P(self->te_freqs) : nullptr, e0, st);
+    // [sin, cos] (modules.py:56) or ADM [cos, sin] (adm/nn.py:118)
+    return timestep_embed(P_->t, B, D, self->arch.variant == 2 ? 1 : 0,
+                          self->te_freqs_set ? self->P(self->te_freqs) : nullptr, e0, st);
   });
   {
     GemmArgs g{};
@@ -605,14 +658,14 @@ int UNetModel::build_plan(int B, int H, int W) {
     GemmArgs g2 = g;
     g2.K = TD; g2.A = e1; g2.lda = TD; g2.Bm = P(te_w2); g2.ldb = TD; g2.C = se; g2.bias = P(te_b2);
     g2.act = 1;  // only SiLU(temb) is ever consumed (ResBlock.proj / AdaGN.proj = SiLU -> Linear)
-    if (arch.variant == 1) {
-      // temb + class_embed(y) before the SiLU (unet_categorial_adagn.py:172-174)
+    if (has_class) {
+      // temb + class_embed(y) before the SiLU (unet_categorial_adagn.py:172-174, adm/unet.py:669-671)
       g2.act = 0;
       g2.C = e2;
       add_gemm(g2);
-      const float* table = class_embed ? P(class_embed) : nullptr;
+      const float* table = P(class_embed);
       add("class_embed_silu", 0, 8.0 * B * TD, [=](hipStream_t st) {
-        return embed_add_silu(e2, table ? P_->y : nullptr, table, B, TD, se, st);
+        return embed_add_silu(e2, P_->y, table, B, TD, se, st);
       });
     } else {
       add_gemm(g2);
@@ -639,8 +692,8 @@ int UNetModel::build_plan(int B, int H, int W) {
     const float* w = P(first_w);
     const float* bb = P(first_b);
     const int cin = arch.in_channels;
-    add("conv3x3_small_in", 2.0 * B * H * W * D * 9 * cin, 4.0 * B * H * W * (cin + D),
-        [=](hipStream_t st) { return conv3x3_small_in(P_->x, B, cin, H, W, w, bb, D, y, st); });
+    add("conv3x3_small_in", 2.0 * B * H * W * C0 * 9 * cin, 4.0 * B * H * W * (cin + C0),
+        [=](hipStream_t st) { return conv3x3_small_in(P_->x, B, cin, H, W, w, bb, C0, y, st); });
   }
 
   for (size_t i = 0; i < nodes.size(); ++i) {
@@ -745,19 +798,24 @@ int UNetModel::build_plan(int B, int H, int W) {
       gq.alpha = 1.f; gq.bias = P(p.bqkv);
       gq.pro_scale = gsc; gq.pro_shift = gsh; gq.pro_rows = hw;
       add_gemm(gq);
+      // head h of q / k / v: columns q0 + h * hs, k0 + h * hs, v0 + h * hs of the qkv rows
+      // (q | k | v blocks: modules.py:92-94 and ADM QKVAttention; per-head [q; k; v]: QKVAttentionLegacy)
+      const int hs = p.legacy ? 3 * Dh : Dh;
+      const int k0 = p.legacy ? Dh : C, v0 = p.legacy ? 2 * Dh : 2 * C;
       GemmArgs gs{};
       gs.M = hw; gs.N = hw; gs.K = Dh; gs.Z1 = B; gs.Z2 = heads;
-      gs.A = qkv; gs.a_s1 = (long)hw * 3 * C; gs.a_s2 = Dh; gs.lda = 3 * C;
-      gs.Bm = qkv + C; gs.b_s1 = (long)hw * 3 * C; gs.b_s2 = Dh; gs.ldb = 3 * C;
+      gs.A = qkv; gs.a_s1 = (long)hw * 3 * C; gs.a_s2 = hs; gs.lda = 3 * C;
+      gs.Bm = qkv + k0; gs.b_s1 = (long)hw * 3 * C; gs.b_s2 = hs; gs.ldb = 3 * C;
       gs.C = Sb; gs.c_s1 = (long)heads * hw * hw; gs.c_s2 = (long)hw * hw; gs.ldc = hw;
-      gs.alpha = (float)std::pow((double)Dh, -0.5);
+      gs.alpha = p.sa;
+      gs.b_scale = p.sb;
       add_gemm(gs);
       const long rows = (long)B * heads * hw;
       add("softmax_rows", 0, 8.0 * rows * hw, [=](hipStream_t st) { return softmax_rows(Sb, rows, hw, hw, st); });
       GemmArgs go{};
       go.M = hw; go.N = Dh; go.K = hw; go.Z1 = B; go.Z2 = heads;
       go.A = Sb; go.a_s1 = (long)heads * hw * hw; go.a_s2 = (long)hw * hw; go.lda = hw;
-      go.Bm = qkv + 2 * C; go.b_s1 = (long)hw * 3 * C; go.b_s2 = Dh; go.ldb = 3 * C; go.b_kn = 1;
+      go.Bm = qkv + v0; go.b_s1 = (long)hw * 3 * C; go.b_s2 = hs; go.ldb = 3 * C; go.b_kn = 1;
       go.C = Ob; go.c_s1 = (long)hw * C; go.c_s2 = Dh; go.ldc = C;
       go.alpha = 1.f;
       add_gemm(go);
@@ -766,6 +824,11 @@ int UNetModel::build_plan(int B, int H, int W) {
       gp.A = Ob; gp.lda = C; gp.Bm = P(p.wproj); gp.ldb = C; gp.C = y.p; gp.ldc = y.pitch;
       gp.alpha = 1.f; gp.bias = P(p.bproj); gp.res = xin.p; gp.ld_res = xin.pitch;
       add_gemm(gp);
+    } else if (n.idx < 0) {
+      // resampling without a conv (adm/unet.py:126-128 nearest-2x, :153-155 avg-pool)
+      const bool down = n.kind == N_DOWN;
+      add("resample2x", 0, 4.0 * B * ((double)Hi * Wi + (double)y.H * y.W) * n.cin,
+          [=](hipStream_t st) { return resample2x(xin, y, down, nullptr, nullptr, st); });
     } else {
       const ConvP cv = convs[n.idx];
       ConvArgs c{};

@@ -44,6 +44,10 @@ class UNetArch(ctypes.Structure):
         ('num_classes', ctypes.c_int),
         ('attn_head_dims', ctypes.c_int),
         ('resblock_updown', ctypes.c_int),
+        ('n_heads_up', ctypes.c_int),
+        ('scale_shift_norm', ctypes.c_int),
+        ('pool_resample', ctypes.c_int),
+        ('attn_legacy', ctypes.c_int),
     ]
 
 
@@ -89,6 +93,7 @@ class GemmDesc(ctypes.Structure):
         ('bias', vp),
         ('res', vp), ('ld_res', ctypes.c_int),
         ('act', ctypes.c_int),
+        ('b_scale', ctypes.c_float),
     ]
 
 

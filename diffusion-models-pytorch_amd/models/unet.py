@@ -94,6 +94,10 @@ class NativeDenoiser(nn.Module):
         a.num_classes = self.arch.get('num_classes', 0) or 0
         a.attn_head_dims = self.arch.get('attn_head_dims', 0)
         a.resblock_updown = int(self.arch.get('resblock_updown', False))
+        a.n_heads_up = self.arch.get('n_heads_up', 0)
+        a.scale_shift_norm = int(self.arch.get('scale_shift_norm', False))
+        a.pool_resample = int(self.arch.get('pool_resample', False))
+        a.attn_legacy = int(self.arch.get('attn_legacy', False))
         return a
 
     @staticmethod
@@ -135,9 +139,15 @@ class NativeDenoiser(nn.Module):
         arch = self._arch_struct()
         check(L.dm_unet_create(ctypes.byref(arch), ptrs, numels, n, stream_handle(device), ctypes.byref(handle)),
               'dm_unet_create')
-        # sinusoid frequencies evaluated exactly as models/modules.py:52-54 (torch CPU exp)
+        # sinusoid frequencies evaluated with the reference's own torch CPU expression
         half = self.arch['dim'] // 2
-        freqs = torch.exp(torch.arange(half) * -(math.log(10000) / (half - 1))).to(device)
+        if self.arch.get('variant', 0) == 2:
+            # adm/nn.py:114-116
+            freqs = torch.exp(-math.log(10000) * torch.arange(start=0, end=half, dtype=torch.float32) / half)
+        else:
+            # models/modules.py:52-54
+            freqs = torch.exp(torch.arange(half) * -(math.log(10000) / (half - 1)))
+        freqs = freqs.to(device)
         check(L.dm_unet_set_time_freqs(handle, freqs.data_ptr(), half, stream_handle(device)),
               'dm_unet_set_time_freqs')
         torch.cuda.current_stream(device).synchronize()

@@ -67,9 +67,17 @@ typedef struct dm_unet_arch {
    * variant 1: models/unet_categorial_adagn.py UNetCategorialAdaGN (AdaGN before conv2,
    *            heads = C / attn_head_dims, ResBlock up/down when resblock_updown, class embedding) */
   int variant;
-  int num_classes;      /* variant 1: class-embedding rows (0 = no class embedding) */
-  int attn_head_dims;   /* variant 1 */
-  int resblock_updown;  /* variant 1 */
+  int num_classes;      /* variants 1, 2: class-embedding rows (0 = no class embedding) */
+  int attn_head_dims;   /* variant 1; variant 2: num_head_channels (<= 0: use n_heads / n_heads_up) */
+  int resblock_updown;  /* variants 1, 2 */
+  /* variant 2: models/adm/unet.py UNetModel (first conv to dim * dim_mults[0] channels, [cos, sin]
+   * embedding, fused qkv 1x1 conv, q and k each scaled by ch^-1/4, middle attention with the stage
+   * head rule). dim = model_channels, dim_mults = channel_mult, use_attn[l] = (2^l in
+   * attention_resolutions). */
+  int n_heads_up;       /* variant 2: num_heads_upsample (heads of up-path attention) */
+  int scale_shift_norm; /* variant 2: use_scale_shift_norm (GN(h) * (1 + scale) + shift before conv2) */
+  int pool_resample;    /* variant 2: conv_resample = False (avg-pool / nearest without a conv) */
+  int attn_legacy;      /* variant 2: QKVAttentionLegacy (per-head [q; k; v] channel interleave) */
 } dm_unet_arch;
 
 typedef struct dm_unet dm_unet;
@@ -185,6 +193,7 @@ typedef struct dm_gemm_desc {
   const float* bias;
   const float* res; int ld_res;
   int act;
+  float b_scale;  /* 0: none; else multiplies B elements on load (B stored [n][k]) */
 } dm_gemm_desc;
 int dm_gemm(const dm_gemm_desc* d, void* stream);
 

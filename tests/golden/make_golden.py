@@ -287,9 +287,110 @@ def make_adagn():
     save('adagn', common, **fx)
 
 
+ADM_ARCHS = {
+    # reduced: scale-shift norm, ResBlock up/down, legacy attention at ds 2 (2 heads), class-conditional
+    'adm_tiny': dict(image_size=16, in_channels=3, model_channels=32, out_channels=6, num_res_blocks=1,
+                     attention_resolutions=[2], dropout=0.0, channel_mult=[1, 2], num_classes=5, num_heads=2,
+                     num_head_channels=-1, use_scale_shift_norm=True, resblock_updown=True),
+    # reduced: conv resampling, additive embedding, new attention order, head channels 16, channel_mult[0] = 2
+    'adm_tiny_conv': dict(image_size=16, in_channels=3, model_channels=32, out_channels=3, num_res_blocks=1,
+                          attention_resolutions=[1, 4], dropout=0.0, channel_mult=[2, 1, 2], num_classes=None,
+                          num_head_channels=16, use_scale_shift_norm=False, resblock_updown=False,
+                          conv_resample=True, use_new_attention_order=True),
+    # reduced: pooling / nearest without conv, num_heads_upsample != num_heads
+    'adm_tiny_pool': dict(image_size=16, in_channels=1, model_channels=32, out_channels=2, num_res_blocks=2,
+                          attention_resolutions=[2], dropout=0.0, channel_mult=[1, 2], num_classes=None,
+                          num_heads=4, num_heads_upsample=2, use_scale_shift_norm=True, resblock_updown=False,
+                          conv_resample=False),
+}
+
+
+def load_yaml_model_params(path):
+    import yaml
+    with open(path) as f:
+        conf = yaml.safe_load(f)
+    return conf['model']['params']
+
+
+def make_adm(full=True):
+    """ADM UNetModel / UNetCombined forwards, a DDPM learned-range trajectory and a DDIMCFG trajectory."""
+    torch.set_num_threads(8)
+    schedule, ddpm, ddim, _ = import_reference()
+    import models.adm.unet as adm  # noqa: E402
+    import models.adm.unet_combined as admc  # noqa: E402
+    archs = dict(ADM_ARCHS)
+    meta = dict(torch=torch.__version__, threads=torch.get_num_threads(),
+                reference='xyfJASON/diffusion-models-pytorch @ 2024-12-20 (/root/reference)')
+    g = torch.Generator().manual_seed(23)
+    fx = {}
+    for name, arch in archs.items():
+        model = adm.UNetModel(**arch).eval()
+        meta[f'{name}_weights_sha256'] = synthetic(model)
+        meta[f'{name}_state_dict'] = [[k, list(v.shape)] for k, v in model.state_dict().items()]
+        x = torch.randn((2, arch['in_channels'], 16, 16), generator=g)
+        t = torch.tensor([999, 5])
+        y = torch.tensor([4, 0]) if arch.get('num_classes') else None
+        with torch.no_grad():
+            fx[f'{name}_out'] = model(x, t, y)
+        fx[f'{name}_x'], fx[f'{name}_t'] = x, t
+        if y is not None:
+            fx[f'{name}_labels'] = y
+    # DDPM-8 learned_range (the ADM diffusion config) on adm_tiny, labels [2, 3], noise pinned per step
+    model = adm.UNetModel(**archs['adm_tiny']).eval()
+    synthetic(model)
+    d = ddpm.DDPM(var_type='learned_range', respace_type='uniform', respace_steps=8)
+    torch.manual_seed(31)
+    init = torch.randn((2, 3, 16, 16))
+    labels = torch.tensor([2, 3])
+    fx['ddpm8_init'], fx['ddpm8_labels'] = init, labels
+    with torch.no_grad():
+        for i, out in enumerate(d.sample_loop(model, init, model_kwargs=dict(y=labels))):
+            fx[f'ddpm8_step{i}_sample'] = out['sample']
+            fx[f'ddpm8_step{i}_noise'] = out['reverse_eps']
+    # DDIMCFG-6 (s = 2.5) with UNetCombined built from the adm_tiny arch
+    comb = admc.UNetCombined(**archs['adm_tiny']).eval()
+    meta['combined_tiny_weights_sha256'] = synthetic(comb)
+    meta['combined_tiny_state_dict'] = [[k, list(v.shape)] for k, v in comb.state_dict().items()]
+    d = ddim.DDIMCFG(guidance_scale=2.5, respace_type='uniform', respace_steps=6, eta=0.0)
+    torch.manual_seed(37)
+    init = torch.randn((2, 3, 16, 16))
+    fx['cfg6_init'] = init
+    with torch.no_grad():
+        for i, out in enumerate(d.sample_loop(comb, init, model_kwargs=dict(y=labels))):
+            fx[f'cfg6_step{i}_sample'] = out['sample']
+    meta['cfg6'] = dict(guidance_scale=2.5, respace_type='uniform', respace_steps=6, eta=0.0)
+    if full:
+        # the reference's full-size ADM configs, B=1 at 256x256, one forward each
+        cfgs = {
+            'adm256_celebahq': os.path.join(REF, 'weights/andreas128/RePaint/celeba256_250000.yaml'),
+            'adm256_combined': os.path.join(REF, 'weights/openai/guided-diffusion/256x256_diffusion_combined.yaml'),
+        }
+        for name, path in cfgs.items():
+            params = load_yaml_model_params(path)
+            archs[name] = params
+            cls = admc.UNetCombined if name.endswith('combined') else adm.UNetModel
+            model = cls(**params).eval()
+            meta[f'{name}_weights_sha256'] = synthetic(model)
+            meta[f'{name}_n_params'] = len(model.state_dict())
+            x = torch.randn((1, 3, 256, 256), generator=g)
+            t = torch.tensor([640])
+            y = torch.tensor([207]) if name.endswith('combined') else None
+            with torch.no_grad():
+                fx[f'{name}_out'] = model(x, t, y)
+            fx[f'{name}_x'], fx[f'{name}_t'] = x, t
+            if y is not None:
+                fx[f'{name}_labels'] = y
+            del model
+    meta['archs'] = archs
+    save('adm', meta, **fx)
+
+
 if __name__ == '__main__':
     if sys.argv[1:] == ['adagn']:
         make_adagn()
+    elif sys.argv[1:] == ['adm']:
+        make_adm()
     else:
         main()
         make_adagn()
+        make_adm()
