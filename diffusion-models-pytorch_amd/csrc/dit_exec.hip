@@ -1,0 +1,392 @@
+// Native executor for the DiT denoiser (models/dit/model.py:145-252).
+//
+// Build time (dm_dit_create): the state_dict tensors are consumed in
+// registration order and copied into one library-owned arena; the adaLN
+// modulation Linear of every block and of the final layer are stacked into ONE
+// [depth * 6D + 2D][D] matrix, so all modulation vectors of a forward come from
+// a single GEMM over SiLU(t_emb + y_emb).
+//
+// Forward: tokens stay resident as one [B * T][D] fp32 matrix x, updated in
+// place by the gated-residual epilogues. Per block (dit/model.py:118-122):
+//   row_stats(x) -> QKV GEMM with the LayerNorm + modulate prologue
+//   -> S = (q * d^-1/2) k^T -> softmax -> O = P v -> proj GEMM, x += gate_msa * (.)
+//   row_stats(x) -> fc1 GEMM (LN + modulate prologue, GELU-tanh epilogue)
+//   -> fc2 GEMM, x += gate_mlp * (.)
+// so norm1/norm2/modulate/gate never materialise. All GEMMs are the fp32 MFMA
+// kernel of gemm.hip.
+#include <cmath>
+#include <memory>
+#include <vector>
+
+#include "dm_common.h"
+#include "dm_kernels.h"
+#include "plan.h"
+
+namespace dm {
+
+namespace {
+
+struct BlockP {
+  size_t qkv_w, qkv_b, proj_w, proj_b, fc1_w, fc1_b, fc2_w, fc2_b;
+};
+
+int dit_count(const dm_dit_arch& a) { return 8 + 10 * a.depth + 4; }
+
+int dit_validate(const dm_dit_arch* a) {
+  DM_REQUIRE(a != nullptr, "arch is null");
+  DM_REQUIRE(a->patch_size >= 1 && a->input_size % a->patch_size == 0, "input_size must be divisible by patch_size");
+  DM_REQUIRE(a->in_channels >= 1 && (a->in_channels * a->patch_size * a->patch_size) % 4 == 0,
+             "in_channels * patch_size^2 must be a multiple of 4");
+  DM_REQUIRE(a->hidden_size >= 32 && a->hidden_size % 4 == 0, "hidden_size must be a multiple of 4");
+  DM_REQUIRE(a->depth >= 1, "depth must be >= 1");
+  DM_REQUIRE(a->num_heads >= 1 && a->hidden_size % a->num_heads == 0 && (a->hidden_size / a->num_heads) % 4 == 0,
+             "hidden_size / num_heads must be a multiple of 4");
+  DM_REQUIRE(a->mlp_hidden >= 4 && a->mlp_hidden % 4 == 0, "mlp hidden size must be a multiple of 4");
+  DM_REQUIRE(a->num_classes >= 1, "num_classes must be >= 1");
+  return DM_OK;
+}
+
+}  // namespace
+
+struct DiTModel {
+  dm_dit_arch arch;
+  float* arena = nullptr;
+  size_t arena_floats = 0;
+  int D = 0, T = 0, OC = 0, PP = 0, ada_total = 0;
+  size_t pos, xw, xb, tw1, tb1, tw2, tb2, ytab, freqs, ada_w, ada_b, fin_w, fin_b;
+  bool freqs_set = false;
+  std::vector<BlockP> blocks;
+
+  struct Plan : PlanBase {
+    int B = 0;
+    const float* x = nullptr;
+    const int64_t* t = nullptr;
+    const int64_t* y = nullptr;
+    float* out = nullptr;
+  };
+  std::unique_ptr<Plan> plan;
+
+  float* P(size_t off) const { return arena + off; }
+  ~DiTModel() {
+    plan.reset();
+    if (arena) (void)hipFree(arena);
+  }
+  int build_plan(int B);
+};
+
+static int dit_create(const dm_dit_arch* arch, const float* const* params, const int64_t* numels, int n_params,
+                      hipStream_t st, DiTModel** out) {
+  int rc = dit_validate(arch);
+  if (rc) return rc;
+  const dm_dit_arch a = *arch;
+  DM_REQUIRE(n_params == dit_count(a), "expected " + std::to_string(dit_count(a)) + " parameter tensors, got " +
+                                           std::to_string(n_params));
+  auto m = std::make_unique<DiTModel>();
+  m->arch = a;
+  const int D = a.hidden_size, p = a.patch_size, C = a.in_channels, Hm = a.mlp_hidden;
+  const int S = a.input_size / p;
+  m->D = D;
+  m->T = S * S;
+  m->OC = a.learn_sigma ? 2 * C : C;
+  m->PP = p * p;
+  m->ada_total = a.depth * 6 * D + 2 * D;
+  const int n_cls = a.num_classes + (a.null_class ? 1 : 0);
+
+  // arena layout: everything 64-float aligned
+  size_t size = 0;
+  auto reserve = [&](int64_t n) { size_t off = size; size += ((size_t)n + 63) / 64 * 64; return off; };
+  struct Copy { size_t dst; int idx; int64_t n; };
+  std::vector<Copy> copies;
+  int idx = 0;
+  std::string err;
+  auto take = [&](int64_t n, const char* what) {
+    if (idx < n_params && numels[idx] != n && err.empty())
+      err = "parameter " + std::to_string(idx) + " (" + what + "): expected " + std::to_string(n) + " elements, got " +
+            std::to_string(numels[idx]);
+    const size_t off = reserve(n);
+    copies.push_back({off, idx++, n});
+    return off;
+  };
+  auto take_at = [&](int64_t n, size_t dst, const char* what) {
+    if (idx < n_params && numels[idx] != n && err.empty())
+      err = "parameter " + std::to_string(idx) + " (" + what + "): expected " + std::to_string(n) + " elements, got " +
+            std::to_string(numels[idx]);
+    copies.push_back({dst, idx++, n});
+  };
+
+  m->pos = take((int64_t)m->T * D, "pos_embed");
+  m->xw = take((int64_t)D * C * p * p, "x_embedder.proj.weight");
+  m->xb = take(D, "x_embedder.proj.bias");
+  m->tw1 = take((int64_t)D * 256, "t_embedder.mlp.0.weight");
+  m->tb1 = take(D, "t_embedder.mlp.0.bias");
+  m->tw2 = take((int64_t)D * D, "t_embedder.mlp.2.weight");
+  m->tb2 = take(D, "t_embedder.mlp.2.bias");
+  m->ytab = take((int64_t)n_cls * D, "y_embedder.embedding_table.weight");
+  m->freqs = reserve(128);
+  m->ada_w = reserve((int64_t)m->ada_total * D);
+  m->ada_b = reserve(m->ada_total);
+  for (int b = 0; b < a.depth; ++b) {
+    BlockP bp;
+    bp.qkv_w = take((int64_t)3 * D * D, "attn.qkv.weight");
+    bp.qkv_b = take(3 * D, "attn.qkv.bias");
+    bp.proj_w = take((int64_t)D * D, "attn.proj.weight");
+    bp.proj_b = take(D, "attn.proj.bias");
+    bp.fc1_w = take((int64_t)Hm * D, "mlp.fc1.weight");
+    bp.fc1_b = take(Hm, "mlp.fc1.bias");
+    bp.fc2_w = take((int64_t)D * Hm, "mlp.fc2.weight");
+    bp.fc2_b = take(D, "mlp.fc2.bias");
+    take_at((int64_t)6 * D * D, m->ada_w + (size_t)b * 6 * D * D, "adaLN_modulation.1.weight");
+    take_at(6 * D, m->ada_b + (size_t)b * 6 * D, "adaLN_modulation.1.bias");
+    m->blocks.push_back(bp);
+  }
+  m->fin_w = take((int64_t)m->PP * m->OC * D, "final_layer.linear.weight");
+  m->fin_b = take(m->PP * m->OC, "final_layer.linear.bias");
+  take_at((int64_t)2 * D * D, m->ada_w + (size_t)a.depth * 6 * D * D, "final_layer.adaLN_modulation.1.weight");
+  take_at(2 * D, m->ada_b + (size_t)a.depth * 6 * D, "final_layer.adaLN_modulation.1.bias");
+  if (!err.empty()) {
+    set_error(err);
+    return DM_ERR_ARG;
+  }
+  DM_REQUIRE(idx == n_params, "parameter count mismatch after walk");
+
+  m->arena_floats = size;
+  DM_CHECK_HIP(hipMalloc(&m->arena, size * sizeof(float)));
+  for (auto& c : copies) {
+    DM_REQUIRE(params[c.idx] != nullptr, "null parameter pointer");
+    DM_CHECK_HIP(hipMemcpyAsync(m->arena + c.dst, params[c.idx], c.n * sizeof(float), hipMemcpyDeviceToDevice, st));
+  }
+  *out = m.release();
+  return DM_OK;
+}
+
+int DiTModel::build_plan(int B) {
+  plan.reset();
+  plan = std::make_unique<Plan>();
+  Plan& pl = *plan;
+  pl.B = B;
+  const dm_dit_arch& a = arch;
+  const int p = a.patch_size, C = a.in_channels, S = a.input_size, Hm = a.mlp_hidden;
+  const int heads = a.num_heads, Dh = D / heads;
+  const long M = (long)B * T;
+  DM_REQUIRE((long)B * heads <= 65535, "batch * heads too large for one attention launch");
+
+  float* e0 = pl.alloc((size_t)B * 256 * 4);
+  float* e1 = pl.alloc((size_t)B * D * 4);
+  float* temb = pl.alloc((size_t)B * D * 4);
+  float* se = pl.alloc((size_t)B * D * 4);
+  float* mods = pl.alloc((size_t)B * ada_total * 4);
+  float* a0 = pl.alloc((size_t)M * C * p * p * 4);
+  float* x = pl.alloc((size_t)M * D * 4);
+  float2* stats = (float2*)pl.alloc((size_t)M * sizeof(float2));
+  float* qkv = pl.alloc((size_t)M * 3 * D * 4);
+  float* Sb = pl.alloc((size_t)B * heads * T * T * 4);
+  float* Ob = pl.alloc((size_t)M * D * 4);
+  float* hb = pl.alloc((size_t)M * Hm * 4);
+  float* lin = pl.alloc((size_t)M * PP * OC * 4);
+  if (pl.alloc_failed) { set_error("workspace allocation failed"); return DM_ERR_HIP; }
+
+  Plan* P_ = &pl;
+  DiTModel* self = this;
+  auto add_gemm = [&](const GemmArgs& g) {
+    const double Z = (double)g.Z1 * g.Z2;
+    const double fl = 2.0 * Z * g.M * g.N * g.K;
+    const double by = 4.0 * Z * ((double)g.M * g.K + (double)g.N * g.K + (double)g.M * g.N) +
+                      (g.res ? 4.0 * g.M * g.N : 0.0);
+    pl.add(gemm_label(g), fl, by, [=](hipStream_t st) { return gemm_batched(g, st); });
+  };
+  auto linear = [&](const float* A, int lda, long rows, size_t w, size_t bias, int N, int K, float* out, int ldc) {
+    GemmArgs g{};
+    g.M = (int)rows; g.N = N; g.K = K; g.Z1 = 1; g.Z2 = 1;
+    g.A = A; g.lda = lda; g.Bm = P(w); g.ldb = K; g.C = out; g.ldc = ldc; g.alpha = 1.f;
+    g.bias = bias != (size_t)-1 ? P(bias) : nullptr;
+    return g;
+  };
+
+  // --- conditioning: t_embedder (dit/model.py:40-64), y_embedder, c = t + y, SiLU for every adaLN
+  pl.add("timestep_embed", 0, 4.0 * B * 256, [=](hipStream_t st) {
+    return timestep_embed(P_->t, B, 256, 1, self->freqs_set ? self->P(self->freqs) : nullptr, e0, st);
+  });
+  {
+    GemmArgs g = linear(e0, 256, B, tw1, tb1, D, 256, e1, D);
+    g.act = 1;
+    add_gemm(g);
+    add_gemm(linear(e1, D, B, tw2, tb2, D, D, temb, D));
+  }
+  {
+    const float* table = P(ytab);
+    const int null_row = a.null_class ? a.num_classes : -1;
+    pl.add("class_embed_silu", 0, 8.0 * B * D, [=](hipStream_t st) {
+      return embed_add_silu(temb, P_->y, table, B, D, se, st, null_row);
+    });
+  }
+  // every block's (and the final layer's) adaLN modulation in one GEMM: [B][depth * 6D + 2D]
+  add_gemm(linear(se, D, B, ada_w, ada_b, ada_total, D, mods, ada_total));
+
+  // --- patch embedding + pos_embed (dit/model.py:244)
+  pl.add("patchify", 0, 8.0 * M * C * p * p,
+         [=](hipStream_t st) { return patchify(P_->x, B, C, S, S, p, a0, st); });
+  {
+    GemmArgs g = linear(a0, C * p * p, M, xw, xb, D, C * p * p, x, D);
+    g.res = P(pos); g.ld_res = D; g.res_mod = T;
+    add_gemm(g);
+  }
+
+  const float eps = 1e-6f;
+  auto stats_op = [&]() {
+    pl.add("row_stats", 0, 4.0 * M * D, [=](hipStream_t st) { return row_stats(x, M, D, eps, stats, st); });
+  };
+  for (int b = 0; b < a.depth; ++b) {
+    const BlockP bp = blocks[b];
+    const float* mb = mods + (size_t)b * 6 * D;  // shift_msa, scale_msa, gate_msa, shift_mlp, scale_mlp, gate_mlp
+    // attention branch
+    stats_op();
+    {
+      GemmArgs g = linear(x, D, M, bp.qkv_w, bp.qkv_b, 3 * D, D, qkv, 3 * D);
+      g.ln_stats = stats; g.ln_shift = mb; g.ln_scale = mb + D; g.ln_pitch = ada_total; g.ln_rows = T;
+      add_gemm(g);
+    }
+    {
+      // timm Attention: qkv.reshape(B, N, 3, heads, d): q / k / v of head h at columns h*d, D + h*d, 2D + h*d
+      GemmArgs gs{};
+      gs.M = T; gs.N = T; gs.K = Dh; gs.Z1 = B; gs.Z2 = heads;
+      gs.A = qkv; gs.a_s1 = (long)T * 3 * D; gs.a_s2 = Dh; gs.lda = 3 * D;
+      gs.Bm = qkv + D; gs.b_s1 = (long)T * 3 * D; gs.b_s2 = Dh; gs.ldb = 3 * D;
+      gs.C = Sb; gs.c_s1 = (long)heads * T * T; gs.c_s2 = (long)T * T; gs.ldc = T;
+      gs.alpha = (float)std::pow((double)Dh, -0.5);
+      add_gemm(gs);
+      const long rows = (long)B * heads * T;
+      const int L = T;
+      pl.add("softmax_rows", 0, 8.0 * rows * L, [=](hipStream_t st) { return softmax_rows(Sb, rows, L, L, st); });
+      GemmArgs go{};
+      go.M = T; go.N = Dh; go.K = T; go.Z1 = B; go.Z2 = heads;
+      go.A = Sb; go.a_s1 = (long)heads * T * T; go.a_s2 = (long)T * T; go.lda = T;
+      go.Bm = qkv + 2 * D; go.b_s1 = (long)T * 3 * D; go.b_s2 = Dh; go.ldb = 3 * D; go.b_kn = 1;
+      go.C = Ob; go.c_s1 = (long)T * D; go.c_s2 = Dh; go.ldc = D;
+      go.alpha = 1.f;
+      add_gemm(go);
+    }
+    {
+      GemmArgs g = linear(Ob, D, M, bp.proj_w, bp.proj_b, D, D, x, D);
+      g.res = x; g.ld_res = D; g.gate = mb + 2 * D; g.gate_pitch = ada_total; g.gate_rows = T;
+      add_gemm(g);
+    }
+    // MLP branch
+    stats_op();
+    {
+      GemmArgs g = linear(x, D, M, bp.fc1_w, bp.fc1_b, Hm, D, hb, Hm);
+      g.ln_stats = stats; g.ln_shift = mb + 3 * D; g.ln_scale = mb + 4 * D; g.ln_pitch = ada_total; g.ln_rows = T;
+      g.act = 2;
+      add_gemm(g);
+    }
+    {
+      GemmArgs g = linear(hb, Hm, M, bp.fc2_w, bp.fc2_b, D, Hm, x, D);
+      g.res = x; g.ld_res = D; g.gate = mb + 5 * D; g.gate_pitch = ada_total; g.gate_rows = T;
+      add_gemm(g);
+    }
+  }
+  // --- final layer (dit/model.py:138-142) + unpatchify
+  stats_op();
+  {
+    const float* mf = mods + (size_t)a.depth * 6 * D;  // shift, scale
+    GemmArgs g = linear(x, D, M, fin_w, fin_b, PP * OC, D, lin, PP * OC);
+    g.ln_stats = stats; g.ln_shift = mf; g.ln_scale = mf + D; g.ln_pitch = ada_total; g.ln_rows = T;
+    add_gemm(g);
+  }
+  const int oc = OC;
+  pl.add("unpatchify", 0, 8.0 * M * PP * OC,
+         [=](hipStream_t st) { return unpatchify(lin, B, oc, S, S, p, P_->out, st); });
+  return DM_OK;
+}
+
+}  // namespace dm
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+struct dm_dit {
+  dm::DiTModel* m;
+};
+
+extern "C" int dm_dit_param_count(const dm_dit_arch* arch, int* n_params) {
+  int rc = dm::dit_validate(arch);
+  if (rc) return rc;
+  if (!n_params) { dm::set_error("n_params is null"); return DM_ERR_ARG; }
+  *n_params = dm::dit_count(*arch);
+  return DM_OK;
+}
+
+extern "C" int dm_dit_create(const dm_dit_arch* arch, const float* const* params, const int64_t* numels,
+                             int n_params, void* stream, dm_dit** out) {
+  if (!out || !params || !numels) { dm::set_error("null argument"); return DM_ERR_ARG; }
+  dm::DiTModel* m = nullptr;
+  int rc = dm::dit_create(arch, params, numels, n_params, (hipStream_t)stream, &m);
+  if (rc) return rc;
+  *out = new dm_dit{m};
+  return DM_OK;
+}
+
+extern "C" int dm_dit_forward(dm_dit* h, const float* x, const int64_t* t, const int64_t* y, int B, float* out,
+                              void* stream) {
+  if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
+  if (!x || !t || !out) { dm::set_error("null tensor"); return DM_ERR_ARG; }
+  if (B <= 0) { dm::set_error("empty batch"); return DM_ERR_ARG; }
+  dm::DiTModel* m = h->m;
+  if (!m->plan || m->plan->B != B) {
+    int rc = m->build_plan(B);
+    if (rc) {
+      m->plan.reset();
+      return rc;
+    }
+  }
+  m->plan->x = x;
+  m->plan->t = t;
+  m->plan->y = y;
+  m->plan->out = out;
+  return m->plan->run((hipStream_t)stream);
+}
+
+extern "C" int dm_dit_set_time_freqs(dm_dit* h, const float* freqs, int n, void* stream) {
+  if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
+  if (!freqs) {
+    h->m->freqs_set = false;
+    return DM_OK;
+  }
+  if (n != 128) { dm::set_error("time frequency table must have 128 entries"); return DM_ERR_ARG; }
+  DM_CHECK_HIP(hipMemcpyAsync(h->m->P(h->m->freqs), freqs, 128 * sizeof(float), hipMemcpyDefault,
+                              (hipStream_t)stream));
+  h->m->freqs_set = true;
+  return DM_OK;
+}
+
+extern "C" int dm_dit_profile(dm_dit* h, int enable) {
+  if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
+  if (!h->m->plan) { dm::set_error("no plan yet: run dm_dit_forward once first"); return DM_ERR_STATE; }
+  h->m->plan->profile_enable(enable != 0);
+  return DM_OK;
+}
+
+extern "C" int dm_dit_profile_count(dm_dit* h, int* n_ops) {
+  if (!h || !h->m || !h->m->plan || !n_ops) { dm::set_error("null model / no plan"); return DM_ERR_STATE; }
+  *n_ops = (int)h->m->plan->ops.size();
+  return DM_OK;
+}
+
+extern "C" int dm_dit_profile_get(dm_dit* h, int i, char* label, int label_len, double* flops, double* bytes,
+                                  double* ms_total, int64_t* launches) {
+  if (!h || !h->m || !h->m->plan) { dm::set_error("null model / no plan"); return DM_ERR_STATE; }
+  return h->m->plan->profile_get(i, label, label_len, flops, bytes, ms_total, launches);
+}
+
+extern "C" int dm_dit_memory(const dm_dit* h, int64_t* weight_bytes, int64_t* workspace_bytes) {
+  if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
+  if (weight_bytes) *weight_bytes = (int64_t)(h->m->arena_floats * sizeof(float));
+  if (workspace_bytes) *workspace_bytes = h->m->plan ? (int64_t)h->m->plan->bytes : 0;
+  return DM_OK;
+}
+
+extern "C" void dm_dit_destroy(dm_dit* h) {
+  if (!h) return;
+  (void)hipDeviceSynchronize();
+  delete h->m;
+  delete h;
+}

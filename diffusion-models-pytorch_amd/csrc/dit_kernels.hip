@@ -1,0 +1,105 @@
+// Small bandwidth-bound kernels of the DiT denoiser (models/dit/model.py):
+//   * LayerNorm row statistics for the fused LN + adaLN-modulate GEMM prologue
+//     (DiTBlock norm1 / norm2, FinalLayer norm_final: eps 1e-6, no affine);
+//   * patchify (PatchEmbed's Conv2d k = s = p as a GEMM input) and unpatchify.
+#include "dm_common.h"
+#include "dm_kernels.h"
+
+namespace dm {
+
+namespace {
+
+// One 64-lane wavefront per row. fp64 accumulation of the mean, then of the
+// squared deviations (two passes over the row, the second from L1/L2).
+__global__ void __launch_bounds__(256) row_stats_kernel(const float* __restrict__ x, long rows, int D, float eps,
+                                                        float2* __restrict__ stats) {
+  const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  const float* row = x + (size_t)r * D;
+  const int D4 = D >> 2;
+  double s = 0.0;
+  for (int i = lane; i < D4; i += 64) {
+    const float4 v = reinterpret_cast<const float4*>(row)[i];
+    s += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  const double mean = s / D;
+  double q = 0.0;
+  for (int i = lane; i < D4; i += 64) {
+    const float4 v = reinterpret_cast<const float4*>(row)[i];
+    const double a = v.x - mean, b = v.y - mean, c = v.z - mean, d = v.w - mean;
+    q += a * a + b * b + c * c + d * d;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+  if (lane == 0) {
+    const float var = (float)(q / D);
+    stats[r] = make_float2((float)mean, 1.0f / sqrtf(var + eps));
+  }
+}
+
+__global__ void patchify_kernel(const float* __restrict__ x, int B, int C, int H, int W, int p,
+                                float* __restrict__ out) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)B * C * H * W;
+  if (e >= total) return;
+  // e enumerates the NCHW input; scatter into the [token][c * p * p + pr * p + qc] layout
+  const int xx = e % W;
+  long r = e / W;
+  const int yy = r % H;
+  r /= H;
+  const int c = r % C;
+  const int b = r / C;
+  const int w = W / p, h = H / p;
+  const long tok = ((long)b * h + yy / p) * w + xx / p;
+  out[tok * (C * p * p) + c * p * p + (yy % p) * p + (xx % p)] = x[e];
+}
+
+__global__ void unpatchify_kernel(const float* __restrict__ x, int B, int C, int H, int W, int p,
+                                  float* __restrict__ out) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)B * C * H * W;
+  if (e >= total) return;
+  // e enumerates the NCHW output (einsum 'nhwpqc->nchpwq', dit/model.py:229-231)
+  const int xx = e % W;
+  long r = e / W;
+  const int yy = r % H;
+  r /= H;
+  const int c = r % C;
+  const int b = r / C;
+  const int w = W / p, h = H / p;
+  const long tok = ((long)b * h + yy / p) * w + xx / p;
+  out[e] = x[tok * (p * p * C) + ((yy % p) * p + (xx % p)) * C + c];
+}
+
+}  // namespace
+
+int row_stats(const float* x, long rows, int D, float eps, float2* stats, hipStream_t st) {
+  DM_REQUIRE(D % 4 == 0 && rows > 0, "row_stats: D must be a multiple of 4");
+  const long blocks = (rows + 3) / 4;
+  hipLaunchKernelGGL(row_stats_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, rows, D, eps, stats);
+  DM_LAUNCH_CHECK();
+  return DM_OK;
+}
+
+int patchify(const float* x, int B, int C, int H, int W, int p, float* out, hipStream_t st) {
+  DM_REQUIRE(H % p == 0 && W % p == 0, "patchify: image size must be divisible by the patch size");
+  const long total = (long)B * C * H * W;
+  hipLaunchKernelGGL(patchify_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x, B, C, H, W, p,
+                     out);
+  DM_LAUNCH_CHECK();
+  return DM_OK;
+}
+
+int unpatchify(const float* x, int B, int C, int H, int W, int p, float* out, hipStream_t st) {
+  DM_REQUIRE(H % p == 0 && W % p == 0, "unpatchify: image size must be divisible by the patch size");
+  const long total = (long)B * C * H * W;
+  hipLaunchKernelGGL(unpatchify_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x, B, C, H, W, p,
+                     out);
+  DM_LAUNCH_CHECK();
+  return DM_OK;
+}
+
+}  // namespace dm

@@ -61,4 +61,11 @@ __device__ __forceinline__ float silu_f(float v) {
   return v / (1.0f + expf(-v));
 }
 
+__device__ __forceinline__ float gelu_tanh_f(float v) {
+  // torch GELU(approximate='tanh'): 0.5 x (1 + tanh(sqrt(2/pi) (x + 0.044715 x^3)))
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float inner = k0 * (v + k1 * v * v * v);
+  return 0.5f * v * (1.0f + tanhf(inner));
+}
+
 }  // namespace dm

@@ -59,12 +59,22 @@ struct GemmArgs {
   const float* bias;    // [N] or null
   const float* res;     // residual [M][ld_res] (batch 0 layout only) or null
   int ld_res;
-  int act;              // 0 none, 1 SiLU
+  int act;              // 0 none, 1 SiLU, 2 GELU(tanh)
   // optional GroupNorm affine on A elements: a[m][k] * pro_scale[img][k] + pro_shift[img][k],
   // img = (z1 * M + m) / pro_rows (rows per image); fused norm of the attention block's input
   const float* pro_scale;
   const float* pro_shift;
   int pro_rows;
+  // optional LayerNorm + adaLN modulate on A elements (DiT, models/dit/model.py:19-20, 120-121):
+  // a = ((a - mean[m]) * rstd[m]) * (1 + ln_scale[img][k]) + ln_shift[img][k], img = m / ln_rows
+  const float2* ln_stats;
+  const float* ln_scale;
+  const float* ln_shift;
+  int ln_pitch, ln_rows;
+  // optional gated residual epilogue: C = res + gate[img][n] * (acc + bias), img = m / gate_rows
+  const float* gate;
+  int gate_pitch, gate_rows;
+  int res_mod;          // > 0: residual row = m % res_mod (broadcast table, e.g. DiT pos_embed)
 };
 
 struct StepArgs {
@@ -100,9 +110,16 @@ int gn_finalize(const View& x, int G, const double2* part, float eps, const floa
 int resample2x(const View& x, const View& y, int down, const float* pro_scale, const float* pro_shift,
                hipStream_t st);
 // out[b] = silu(temb[b] + table[y[b]]) (class embedding, unet_categorial_adagn.py:172-174);
-// rows with y == null or y[b] < 0 get silu(temb[b]) (no label / CFG unconditional branch)
+// rows with y == null or y[b] < 0 use table[null_row] (DiT's CFG null class, dit/model.py:241-242),
+// or no class term when null_row < 0 (no label / CFG unconditional branch of the UNets)
 int embed_add_silu(const float* temb, const int64_t* y, const float* table, int B, int D, float* out,
-                   hipStream_t st);
+                   hipStream_t st, int null_row = -1);
+// LayerNorm statistics (no affine): stats[r] = (mean, 1 / sqrt(var + eps)) of each D-wide row
+int row_stats(const float* x, long rows, int D, float eps, float2* stats, hipStream_t st);
+// DiT patch embedding input: NCHW [B][C][H][W] -> rows [B * (H/p) * (W/p)][C * p * p] (Conv2d k = s = p order)
+int patchify(const float* x, int B, int C, int H, int W, int p, float* out, hipStream_t st);
+// DiT unpatchify (dit/model.py:219-232): rows [B * T][p * p * C] -> NCHW [B][C][H][W]
+int unpatchify(const float* x, int B, int C, int H, int W, int p, float* out, hipStream_t st);
 int gn_apply(const View& x, int G, const double2* part, int nchunk, float eps, const float* gamma,
              const float* beta, const float* mod_scale, const float* mod_shift, int mod_pitch, int act,
              const View& y, hipStream_t st);

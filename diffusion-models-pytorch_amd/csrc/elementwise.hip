@@ -290,15 +290,15 @@ __global__ void resample2x_kernel(View x, View y, int down, const float* __restr
 }
 
 __global__ void embed_add_silu_kernel(const float* __restrict__ temb, const int64_t* __restrict__ y,
-                                      const float* __restrict__ table, int B, int D, float* __restrict__ out) {
+                                      const float* __restrict__ table, int B, int D, int null_row,
+                                      float* __restrict__ out) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= B * D) return;
   const int b = e / D, d = e - (e / D) * D;
   float v = temb[e];
-  if (y) {
-    const int64_t cls = y[b];
-    if (cls >= 0) v = v + table[(size_t)cls * D + d];
-  }
+  const int64_t cls = y ? y[b] : -1;
+  const int64_t row = cls >= 0 ? cls : null_row;
+  if (row >= 0) v = v + table[(size_t)row * D + d];
   out[e] = silu_f(v);
 }
 
@@ -415,9 +415,10 @@ int resample2x(const View& x, const View& y, int down, const float* pro_scale, c
 }
 
 int embed_add_silu(const float* temb, const int64_t* y, const float* table, int B, int D, float* out,
-                   hipStream_t st) {
+                   hipStream_t st, int null_row) {
   const int n = B * D;
-  hipLaunchKernelGGL(embed_add_silu_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, st, temb, y, table, B, D, out);
+  hipLaunchKernelGGL(embed_add_silu_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, st, temb, y, table, B, D,
+                     null_row, out);
   DM_LAUNCH_CHECK();
   return DM_OK;
 }

@@ -50,13 +50,15 @@ gemm_kernel(GemmArgs g) {
   const float* arow[Cfg::A_ITERS];
   bool a_ok[Cfg::A_ITERS];
   int a_img[Cfg::A_ITERS];
+  float2 a_ln[Cfg::A_ITERS];
 #pragma unroll
   for (int i = 0; i < Cfg::A_ITERS; ++i) {
     const int m = m0 + lrow + i * Cfg::ROWS_PER_PASS;
     a_ok[i] = m < g.M;
     const int mc = min(m, g.M - 1);
     arow[i] = A + (size_t)mc * g.lda + 4 * lc4;
-    a_img[i] = g.pro_scale ? (z1 * g.M + mc) / g.pro_rows : 0;
+    a_img[i] = g.pro_scale ? (z1 * g.M + mc) / g.pro_rows : (g.ln_stats ? mc / g.ln_rows : 0);
+    a_ln[i] = g.ln_stats ? g.ln_stats[mc] : make_float2(0.f, 1.f);
   }
   const float* brow[B_KN ? 1 : Cfg::B_ITERS];
   bool b_ok[B_KN ? 1 : Cfg::B_ITERS];
@@ -107,6 +109,12 @@ gemm_kernel(GemmArgs g) {
         const f4 sh = *reinterpret_cast<const f4*>(g.pro_shift + (size_t)a_img[i] * g.K + ld_k);
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = v[q] * sc[q] + sh[q];
+      }
+      if (g.ln_stats) {  // LayerNorm (no affine) + modulate x * (1 + scale) + shift
+        const f4 sc = *reinterpret_cast<const f4*>(g.ln_scale + (size_t)a_img[i] * g.ln_pitch + ld_k);
+        const f4 sh = *reinterpret_cast<const f4*>(g.ln_shift + (size_t)a_img[i] * g.ln_pitch + ld_k);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = ((v[q] - a_ln[i].x) * a_ln[i].y) * (1.0f + sc[q]) + sh[q];
       }
       if (g.alpha != 1.0f) v = v * g.alpha;
       *reinterpret_cast<f4*>(As + (lrow + i * Cfg::ROWS_PER_PASS) * kLDK + 4 * lc4) = (a_ok[i] && k_ok) ? v : zero4;
@@ -165,8 +173,12 @@ gemm_kernel(GemmArgs g) {
         if (m >= g.M) continue;
         float v = acc[i][j][r];
         if (g.bias) v = v + bn;
-        if (g.res) v = v + g.res[(size_t)m * g.ld_res + n];
+        if (g.res) {
+          const float rv = g.res[(size_t)(g.res_mod > 0 ? m % g.res_mod : m) * g.ld_res + n];
+          v = g.gate ? rv + g.gate[(size_t)(m / g.gate_rows) * g.gate_pitch + n] * v : v + rv;
+        }
         if (g.act == 1) v = silu_f(v);
+        else if (g.act == 2) v = gelu_tanh_f(v);
         C[(size_t)m * g.ldc + n] = v;
       }
     }
@@ -196,6 +208,10 @@ int gemm_batched(const GemmArgs& g, hipStream_t st) {
   DM_REQUIRE(g.Z1 >= 1 && g.Z2 >= 1 && (long)g.Z1 * g.Z2 <= 65535, "gemm: batch out of range");
   DM_REQUIRE(!g.pro_scale || (g.pro_shift && g.pro_rows > 0 && !g.b_kn), "gemm: A prologue needs scale, shift, rows");
   DM_REQUIRE(g.b_scale == 0.0f || !g.b_kn, "gemm: B scaling needs the [n][k] B layout");
+  DM_REQUIRE(!g.ln_stats || (g.ln_scale && g.ln_shift && g.ln_rows > 0 && g.ln_pitch % 4 == 0 && !g.pro_scale &&
+                             g.Z1 == 1 && g.Z2 == 1),
+             "gemm: LayerNorm-modulate prologue needs stats, scale/shift tables and rows per image");
+  DM_REQUIRE(!g.gate || (g.res && g.gate_rows > 0), "gemm: gated residual needs the residual and rows per image");
   if (gemm_pick(g) == 0) return launch_gemm<128, 128, 64, 64>(g, st);
   return launch_gemm<64, 64, 32, 32>(g, st);
 }

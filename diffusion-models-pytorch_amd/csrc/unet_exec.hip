@@ -21,6 +21,7 @@
 
 #include "dm_common.h"
 #include "dm_kernels.h"
+#include "plan.h"
 
 namespace dm {
 
@@ -105,13 +106,6 @@ enum NodeKind { N_RES, N_ATTN, N_DOWN, N_UP };
 
 }  // namespace
 
-struct Op {
-  std::string label;   // kernel family / tile, matches the rocprof kernel name family
-  double flops;        // algorithmic FLOPs of one launch
-  double bytes;        // algorithmic HBM bytes of one launch (read + write of logical tensors)
-  std::function<int(hipStream_t)> fn;
-};
-
 namespace {
 
 struct Node {
@@ -151,16 +145,8 @@ struct UNetModel {
   int n_levels = 0;
 
   // workspace cache
-  struct Plan {
+  struct Plan : PlanBase {
     int B = 0, H = 0, W = 0;
-    std::vector<void*> allocs;
-    size_t bytes = 0;
-    std::vector<Op> ops;
-    // profiling: per-op HIP event pairs recorded on the launch stream
-    bool profiling = false;
-    std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
-    std::vector<double> prof_ms;
-    std::vector<int64_t> prof_launches;
     const float* x = nullptr;
     const int64_t* t = nullptr;
     const int64_t* y = nullptr;  // class labels or null
@@ -173,29 +159,8 @@ struct UNetModel {
   int build_plan(int B, int H, int W);
 };
 
-static void drain_profile(UNetModel::Plan* p) {
-  for (auto& e : p->pending) {
-    float ms = 0.f;
-    if (hipEventSynchronize(e.second.second) == hipSuccess &&
-        hipEventElapsedTime(&ms, e.second.first, e.second.second) == hipSuccess) {
-      p->prof_ms[e.first] += ms;
-      p->prof_launches[e.first] += 1;
-    }
-    (void)hipEventDestroy(e.second.first);
-    (void)hipEventDestroy(e.second.second);
-  }
-  p->pending.clear();
-}
-
-static void free_plan(UNetModel::Plan* p) {
-  if (!p) return;
-  drain_profile(p);
-  for (void* a : p->allocs) (void)hipFree(a);
-  p->allocs.clear();
-}
-
 UNetModel::~UNetModel() {
-  if (plan) free_plan(plan.get());
+  plan.reset();
   if (arena) (void)hipFree(arena);
 }
 
@@ -531,7 +496,7 @@ static int unet_create(const dm_unet_arch* arch, const float* const* params, con
 // plan (per batch size / resolution)
 // ---------------------------------------------------------------------------
 int UNetModel::build_plan(int B, int H, int W) {
-  if (plan) free_plan(plan.get());
+  plan.reset();
   plan = std::make_unique<Plan>();
   Plan& pl = *plan;
   pl.B = B;
@@ -539,17 +504,8 @@ int UNetModel::build_plan(int B, int H, int W) {
   pl.W = W;
   DM_REQUIRE(H % (1 << (n_levels - 1)) == 0 && W % (1 << (n_levels - 1)) == 0,
              "image size must be divisible by 2^(n_stages-1)");
-  bool alloc_failed = false;
-  auto alloc = [&](size_t bytes) -> float* {
-    void* p = nullptr;
-    if (hipMalloc(&p, bytes ? bytes : 16) != hipSuccess) {
-      alloc_failed = true;
-      return nullptr;
-    }
-    pl.allocs.push_back(p);
-    pl.bytes += bytes;
-    return (float*)p;
-  };
+  bool& alloc_failed = pl.alloc_failed;
+  auto alloc = [&](size_t bytes) -> float* { return pl.alloc(bytes); };
   auto Hl = [&](int lvl) { return H >> lvl; };
   auto Wl = [&](int lvl) { return W >> lvl; };
   const int D = arch.dim, TD = 4 * arch.dim, G = 32, C0 = skip_C[0];
@@ -611,9 +567,8 @@ int UNetModel::build_plan(int B, int H, int W) {
   }
   if (alloc_failed) { set_error("workspace allocation failed"); return DM_ERR_HIP; }
 
-  auto& ops = pl.ops;
   auto add = [&](std::string label, double flops, double bytes, std::function<int(hipStream_t)> fn) {
-    ops.push_back(Op{std::move(label), flops, bytes, std::move(fn)});
+    pl.add(std::move(label), flops, bytes, std::move(fn));
   };
   auto conv_cost = [](const ConvArgs& c, double& fl, double& by) {
     const double M = (double)c.B * c.Hout * c.Wout;
@@ -908,24 +863,7 @@ extern "C" int dm_unet_forward(dm_unet* h, const float* x, const int64_t* t, con
   m->plan->t = t;
   m->plan->y = y;
   m->plan->out = out;
-  hipStream_t st = (hipStream_t)stream;
-  auto& pl = *m->plan;
-  for (size_t i = 0; i < pl.ops.size(); ++i) {
-    if (pl.profiling) {
-      hipEvent_t a, b;
-      DM_CHECK_HIP(hipEventCreate(&a));
-      DM_CHECK_HIP(hipEventCreate(&b));
-      DM_CHECK_HIP(hipEventRecord(a, st));
-      int rc = pl.ops[i].fn(st);
-      if (rc) return rc;
-      DM_CHECK_HIP(hipEventRecord(b, st));
-      pl.pending.push_back({(int)i, {a, b}});
-    } else {
-      int rc = pl.ops[i].fn(st);
-      if (rc) return rc;
-    }
-  }
-  return DM_OK;
+  return m->plan->run((hipStream_t)stream);
 }
 
 extern "C" int dm_unet_memory(const dm_unet* h, int64_t* weight_bytes, int64_t* workspace_bytes) {
@@ -951,11 +889,7 @@ extern "C" int dm_unet_set_time_freqs(dm_unet* h, const float* freqs, int n, voi
 extern "C" int dm_unet_profile(dm_unet* h, int enable) {
   if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
   if (!h->m->plan) { dm::set_error("no plan yet: run dm_unet_forward once first"); return DM_ERR_STATE; }
-  auto& pl = *h->m->plan;
-  dm::drain_profile(&pl);
-  pl.profiling = enable != 0;
-  pl.prof_ms.assign(pl.ops.size(), 0.0);
-  pl.prof_launches.assign(pl.ops.size(), 0);
+  h->m->plan->profile_enable(enable != 0);
   return DM_OK;
 }
 
@@ -968,21 +902,7 @@ extern "C" int dm_unet_profile_count(dm_unet* h, int* n_ops) {
 extern "C" int dm_unet_profile_get(dm_unet* h, int i, char* label, int label_len, double* flops, double* bytes,
                                    double* ms_total, int64_t* launches) {
   if (!h || !h->m || !h->m->plan) { dm::set_error("null model / no plan"); return DM_ERR_STATE; }
-  auto& pl = *h->m->plan;
-  if (i < 0 || i >= (int)pl.ops.size()) { dm::set_error("op index out of range"); return DM_ERR_ARG; }
-  dm::drain_profile(&pl);
-  if (pl.prof_ms.size() != pl.ops.size()) {
-    pl.prof_ms.assign(pl.ops.size(), 0.0);
-    pl.prof_launches.assign(pl.ops.size(), 0);
-  }
-  if (label && label_len > 0) {
-    std::snprintf(label, (size_t)label_len, "%s", pl.ops[i].label.c_str());
-  }
-  if (flops) *flops = pl.ops[i].flops;
-  if (bytes) *bytes = pl.ops[i].bytes;
-  if (ms_total) *ms_total = pl.prof_ms[i];
-  if (launches) *launches = pl.prof_launches[i];
-  return DM_OK;
+  return h->m->plan->profile_get(i, label, label_len, flops, bytes, ms_total, launches);
 }
 
 extern "C" void dm_unet_destroy(dm_unet* h) {

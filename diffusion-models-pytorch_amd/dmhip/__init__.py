@@ -15,6 +15,7 @@ from dmhip._lib import (  # noqa: F401
     ConvDesc,
     GemmDesc,
     UNetArch,
+    DiTArch,
     sampler_step,
     groupnorm_nhwc,
     groupnorm_affine,

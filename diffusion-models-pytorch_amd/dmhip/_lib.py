@@ -51,6 +51,15 @@ class UNetArch(ctypes.Structure):
     ]
 
 
+class DiTArch(ctypes.Structure):
+    _fields_ = [
+        ('input_size', ctypes.c_int), ('patch_size', ctypes.c_int), ('in_channels', ctypes.c_int),
+        ('hidden_size', ctypes.c_int), ('depth', ctypes.c_int), ('num_heads', ctypes.c_int),
+        ('mlp_hidden', ctypes.c_int), ('num_classes', ctypes.c_int), ('null_class', ctypes.c_int),
+        ('learn_sigma', ctypes.c_int),
+    ]
+
+
 class StepDesc(ctypes.Structure):
     _fields_ = [
         ('B', ctypes.c_int), ('C', ctypes.c_int), ('HW', ctypes.c_int), ('Cm', ctypes.c_int),
@@ -129,6 +138,19 @@ def _declare(L: ctypes.CDLL):
     L.dm_softmax_rows.argtypes = [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, vp]
     L.dm_timestep_embedding.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp, vp]
     L.dm_unet_set_time_freqs.argtypes = [vp, vp, ctypes.c_int, vp]
+    L.dm_dit_param_count.argtypes = [ctypes.POINTER(DiTArch), ctypes.POINTER(ctypes.c_int)]
+    L.dm_dit_create.argtypes = [ctypes.POINTER(DiTArch), ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_int64),
+                                ctypes.c_int, vp, ctypes.POINTER(vp)]
+    L.dm_dit_forward.argtypes = [vp, vp, vp, vp, ctypes.c_int, vp, vp]
+    L.dm_dit_set_time_freqs.argtypes = [vp, vp, ctypes.c_int, vp]
+    L.dm_dit_profile.argtypes = [vp, ctypes.c_int]
+    L.dm_dit_profile_count.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
+    L.dm_dit_profile_get.argtypes = [vp, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
+                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]
+    L.dm_dit_memory.argtypes = [vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
+    L.dm_dit_destroy.argtypes = [vp]
+    L.dm_dit_destroy.restype = None
 
 
 def load() -> ctypes.CDLL:
@@ -243,22 +265,24 @@ def timestep_embedding(t: torch.Tensor, dim: int, kind: int, out: torch.Tensor, 
                                        stream_handle(t.device)), 'dm_timestep_embedding')
 
 
-def unet_profile_enable(handle, enable: bool):
-    check(load().dm_unet_profile(handle, int(enable)), 'dm_unet_profile')
+def unet_profile_enable(handle, enable: bool, abi: str = 'dm_unet'):
+    """Per-launch HIP-event profiling of a model's cached plan (abi: 'dm_unet' or 'dm_dit')."""
+    check(getattr(load(), abi + '_profile')(handle, int(enable)), abi + '_profile')
 
 
-def unet_profile_read(handle):
+def unet_profile_read(handle, abi: str = 'dm_unet'):
     """List of dicts (label, flops, bytes, ms_total, launches) for every op of the cached plan."""
     L = load()
     n = ctypes.c_int()
-    check(L.dm_unet_profile_count(handle, ctypes.byref(n)), 'dm_unet_profile_count')
+    check(getattr(L, abi + '_profile_count')(handle, ctypes.byref(n)), abi + '_profile_count')
     out = []
     buf = ctypes.create_string_buffer(128)
     fl, by, ms = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
     nl = ctypes.c_int64()
+    get = getattr(L, abi + '_profile_get')
     for i in range(n.value):
-        check(L.dm_unet_profile_get(handle, i, buf, 128, ctypes.byref(fl), ctypes.byref(by), ctypes.byref(ms),
-                                    ctypes.byref(nl)), 'dm_unet_profile_get')
+        check(get(handle, i, buf, 128, ctypes.byref(fl), ctypes.byref(by), ctypes.byref(ms), ctypes.byref(nl)),
+              abi + '_profile_get')
         out.append(dict(label=buf.value.decode(), flops=fl.value, bytes=by.value, ms_total=ms.value,
                         launches=nl.value))
     return out

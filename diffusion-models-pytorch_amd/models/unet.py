@@ -72,11 +72,13 @@ class _TimeEmbedding(nn.Sequential):
 
 class NativeDenoiser(nn.Module):
     """Parameter-container base: packs ``state_dict()`` into the native executor and runs
-    the whole forward pass as one dm_unet_forward call. Subclasses set ``self.arch``."""
+    the whole forward pass as one C-ABI call. Subclasses set ``self.arch``; the UNet family
+    binds the dm_unet_* entry points, other executors (DiT) override the ``_abi`` hooks."""
 
     _native = None
     _native_key = None
     _param_list = None
+    _abi = 'dm_unet'
 
     # ----------------------------------------------------------- native side
     def _arch_struct(self) -> UNetArch:
@@ -108,7 +110,7 @@ class NativeDenoiser(nn.Module):
 
     def _release_native(self):
         if getattr(self, '_native', None) is not None:
-            load().dm_unet_destroy(self._native)
+            getattr(load(), self._abi + '_destroy')(self._native)
             self._native = None
             self._native_key = None
         self._param_list = None
@@ -137,23 +139,29 @@ class NativeDenoiser(nn.Module):
         numels = (ctypes.c_int64 * n)(*[t.numel() for t in tensors])
         handle = ctypes.c_void_p()
         arch = self._arch_struct()
-        check(L.dm_unet_create(ctypes.byref(arch), ptrs, numels, n, stream_handle(device), ctypes.byref(handle)),
-              'dm_unet_create')
+        check(getattr(L, self._abi + '_create')(ctypes.byref(arch), ptrs, numels, n, stream_handle(device),
+                                                ctypes.byref(handle)), self._abi + '_create')
         # sinusoid frequencies evaluated with the reference's own torch CPU expression
-        half = self.arch['dim'] // 2
-        if self.arch.get('variant', 0) == 2:
-            # adm/nn.py:114-116
-            freqs = torch.exp(-math.log(10000) * torch.arange(start=0, end=half, dtype=torch.float32) / half)
-        else:
-            # models/modules.py:52-54
-            freqs = torch.exp(torch.arange(half) * -(math.log(10000) / (half - 1)))
-        freqs = freqs.to(device)
-        check(L.dm_unet_set_time_freqs(handle, freqs.data_ptr(), half, stream_handle(device)),
-              'dm_unet_set_time_freqs')
+        freqs = self._time_freqs().to(device)
+        check(getattr(L, self._abi + '_set_time_freqs')(handle, freqs.data_ptr(), freqs.numel(), stream_handle(device)),
+              self._abi + '_set_time_freqs')
         torch.cuda.current_stream(device).synchronize()
         self._native = handle
         self._native_key = key
         return handle
+
+    def _time_freqs(self) -> Tensor:
+        half = self.arch['dim'] // 2
+        if self.arch.get('variant', 0) == 2:
+            # adm/nn.py:114-116
+            return torch.exp(-math.log(10000) * torch.arange(start=0, end=half, dtype=torch.float32) / half)
+        # models/modules.py:52-54
+        return torch.exp(torch.arange(half) * -(math.log(10000) / (half - 1)))
+
+    def _launch(self, handle, X: Tensor, T: Tensor, y_ptr, out: Tensor):
+        B, _, H, W = X.shape
+        check(load().dm_unet_forward(handle, X.data_ptr(), T.data_ptr(), y_ptr, B, H, W, out.data_ptr(),
+                                     stream_handle(X.device)), 'dm_unet_forward')
 
     def _apply(self, fn, *args, **kwargs):
         self._release_native()
@@ -183,8 +191,7 @@ class NativeDenoiser(nn.Module):
             y_ptr = y.data_ptr()
         handle = self.native_handle(X.device)
         out = torch.empty((B, self.arch['out_channels'], H, W), device=X.device, dtype=torch.float32)
-        check(load().dm_unet_forward(handle, X.data_ptr(), T.data_ptr(), y_ptr, B, H, W, out.data_ptr(),
-                                     stream_handle(X.device)), 'dm_unet_forward')
+        self._launch(handle, X, T, y_ptr, out)
         return out
 
     def _check_labels(self, y: Tensor):
@@ -193,7 +200,7 @@ class NativeDenoiser(nn.Module):
         key = (y.data_ptr(), y._version, y.numel())
         if getattr(self, '_labels_ok', None) == key:
             return
-        n = self.arch.get('num_classes', 0) or 0
+        n = self.arch.get('label_rows', self.arch.get('num_classes', 0) or 0)
         if y.numel() and int(y.max()) >= n:
             raise IndexError(f'class label {int(y.max())} out of range for num_classes={n}')
         self._labels_ok = key

@@ -111,6 +111,44 @@ int dm_unet_profile_get(dm_unet* m, int i, char* label, int label_len, double* f
 int dm_unet_memory(const dm_unet* m, int64_t* weight_bytes, int64_t* workspace_bytes);
 void dm_unet_destroy(dm_unet* m);
 
+/* Denoiser: DiT ------------------------------------------------------------
+ * Replaces models/dit/model.py:145-252 (DiT.__init__ / forward; the timm
+ * PatchEmbed / Attention / Mlp blocks it builds on, timm~=0.9.12). `params` are
+ * the state_dict tensors in order: pos_embed, x_embedder.proj.{weight,bias},
+ * t_embedder.mlp.{0,2}.{weight,bias}, y_embedder.embedding_table.weight, then per
+ * block attn.qkv, attn.proj, mlp.fc1, mlp.fc2, adaLN_modulation.1 (weight, bias
+ * each), then final_layer.linear and final_layer.adaLN_modulation.1.
+ */
+typedef struct dm_dit_arch {
+  int input_size;    /* latent H = W */
+  int patch_size;
+  int in_channels;
+  int hidden_size;
+  int depth;
+  int num_heads;
+  int mlp_hidden;    /* int(hidden_size * mlp_ratio) */
+  int num_classes;
+  int null_class;    /* 1: the embedding table has the CFG null row num_classes (class_dropout_prob > 0) */
+  int learn_sigma;   /* out_channels = 2 * in_channels */
+} dm_dit_arch;
+
+typedef struct dm_dit dm_dit;
+
+int dm_dit_param_count(const dm_dit_arch* arch, int* n_params);
+int dm_dit_create(const dm_dit_arch* arch, const float* const* params, const int64_t* numels, int n_params,
+                  void* stream, dm_dit** out);
+/* x: [B, in_channels, S, S] f32 latents, t: [B] int64, y: [B] int64 labels or NULL (NULL / y[b] < 0 = the
+ * null class, dit/model.py:241-242), out: [B, out_channels, S, S] f32. */
+int dm_dit_forward(dm_dit* m, const float* x, const int64_t* t, const int64_t* y, int B, float* out, void* stream);
+/* 128-entry table exp(-ln(1e4) * i / 128) of the 256-wide frequency embedding (dit/model.py:51-54). */
+int dm_dit_set_time_freqs(dm_dit* m, const float* freqs, int n, void* stream);
+int dm_dit_profile(dm_dit* m, int enable);
+int dm_dit_profile_count(dm_dit* m, int* n_ops);
+int dm_dit_profile_get(dm_dit* m, int i, char* label, int label_len, double* flops, double* bytes,
+                       double* ms_total, int64_t* launches);
+int dm_dit_memory(const dm_dit* m, int64_t* weight_bytes, int64_t* workspace_bytes);
+void dm_dit_destroy(dm_dit* m);
+
 /* Sampler update -----------------------------------------------------------
  * One elementwise pass doing predict() (ddpm.py:174-203), the optional CFG
  * combine (ddim.py:185 / ddpm.py:343-345, with the second predict under

@@ -1,0 +1,99 @@
+"""DiT (models/dit/model.py) on the MI355X path.
+
+PARITY UNPINNED: the reference DiT needs timm (absent), so the expected
+outputs (tests/golden/dit.npz) come from oracle/dit.py, a restatement of
+model.py + timm 0.9.12 (tests/golden/make_dit_golden.py). Tolerance: fp32
+max-abs <= 1e-4, as for the pinned paths.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from diffusions import DDIMCFG
+from models.dit.model import DiT, DiT_models
+from utils.synthetic import init_synthetic_
+
+TOL = 1e-4
+NAMES = ['dit_tiny', 'dit_s2', 'dit_xl2']
+
+
+def _model(meta, name):
+    m = DiT(**meta['archs'][name]).eval()
+    return m, init_synthetic_(m)
+
+
+@pytest.mark.parametrize('name', NAMES)
+def test_dit_state_dict_layout(golden, name):
+    _, meta = golden('dit')
+    m = DiT(**meta['archs'][name])
+    assert [[k, list(v.shape)] for k, v in m.state_dict().items()] == meta[f'{name}_state_dict']
+    n = ctypes.c_int()
+    from dmhip._lib import load
+    assert load().dm_dit_param_count(ctypes.byref(m._arch_struct()), ctypes.byref(n)) == 0
+    assert n.value == len(m.state_dict())
+
+
+def test_dit_models_table():
+    assert set(DiT_models) == {f'DiT-{s}/{p}' for s in ('XL', 'L', 'B', 'S') for p in (2, 4, 8)}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', NAMES)
+def test_dit_forward_vs_oracle(cuda, golden, report, name):
+    g, meta = golden('dit')
+    model, sha = _model(meta, name)
+    assert sha == meta[f'{name}_weights_sha256']
+    model = model.to(cuda)
+    x = torch.from_numpy(g[f'{name}_x']).to(cuda)
+    t = torch.from_numpy(g[f'{name}_t']).to(cuda)
+    y = torch.from_numpy(g[f'{name}_labels']).to(cuda)
+    out_y = model(x, t, y).cpu()
+    out_n = model(x, t, None).cpu()
+    e_y = (out_y - torch.from_numpy(g[f'{name}_out_y'])).abs().max().item()
+    e_n = (out_n - torch.from_numpy(g[f'{name}_out_null'])).abs().max().item()
+    report(f'dit_forward_{name}_y_maxabs_vs_oracle', e_y)
+    report(f'dit_forward_{name}_null_maxabs_vs_oracle', e_n)
+    assert e_y <= TOL and e_n <= TOL, (e_y, e_n)
+    # y[b] < 0 selects the null class row, the same as y=None
+    neg = model(x, t, torch.full_like(y, -1)).cpu()
+    assert torch.equal(neg, out_n)
+    del model
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('batched', [True, False])
+def test_dit_ddimcfg_trajectory_vs_oracle(cuda, golden, report, batched):
+    g, meta = golden('dit')
+    model, _ = _model(meta, 'dit_tiny')
+    model = model.to(cuda)
+    cfg = meta['cfg5']
+    d = DDIMCFG(guidance_scale=cfg['guidance_scale'], respace_type=cfg['respace_type'],
+                respace_steps=cfg['respace_steps'], eta=cfg['eta'], device=cuda)
+    d.batch_cfg = batched
+    labels = torch.from_numpy(g['cfg5_labels']).to(cuda)
+    worst = 0.0
+    for i, out in enumerate(d.sample_loop(model, torch.from_numpy(g['cfg5_init']).to(cuda),
+                                          model_kwargs=dict(y=labels))):
+        err = float(np.abs(out['sample'].cpu().numpy() - g[f'cfg5_step{i}_sample']).max())
+        worst = max(worst, err)
+        assert err <= TOL, (i, err)
+    report(f'dit_ddimcfg5_{"batched" if batched else "two_calls"}_maxabs_vs_oracle', worst)
+
+
+@pytest.mark.gpu
+def test_dit_forward_with_cfg(cuda, golden):
+    _, meta = golden('dit')
+    model, _ = _model(meta, 'dit_tiny')
+    model = model.to(cuda)
+    gen = torch.Generator().manual_seed(5)
+    x = torch.randn((4, 4, 8, 8), generator=gen).to(cuda)
+    t = torch.full((4, ), 500, dtype=torch.long, device=cuda)
+    y = torch.tensor([1, 2, -1, -1], device=cuda)
+    out = model.forward_with_cfg(x, t, y, 1.5)
+    full = model(torch.cat([x[:2], x[:2]]), t, y)
+    ce, ue = full[:2, :3], full[2:, :3]
+    torch.testing.assert_close(out[:2, :3], ue + 1.5 * (ce - ue), rtol=0, atol=1e-6)
+    assert torch.equal(out[:, 3:], full[:, 3:])
