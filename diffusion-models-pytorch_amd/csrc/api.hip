@@ -94,6 +94,11 @@ extern "C" int dm_conv2d_nhwc(const dm_conv_desc* d, void* stream) {
   return dm::conv2d_igemm(a, (hipStream_t)stream);
 }
 
+extern "C" int dm_pack_conv_weight_subpixel(const float* w, int Cout, int Cin, float* out, void* stream) {
+  if (!w || !out) { dm::set_error("null tensor"); return DM_ERR_ARG; }
+  return dm::repack_subpixel(w, Cout, Cin, out, (hipStream_t)stream);
+}
+
 extern "C" int dm_gemm(const dm_gemm_desc* d, void* stream) {
   if (!d || !d->A || !d->B || !d->C) { dm::set_error("null tensor"); return DM_ERR_ARG; }
   dm::GemmArgs g{};

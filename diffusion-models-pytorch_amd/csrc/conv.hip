@@ -256,9 +256,11 @@ int conv2d_igemm(const ConvArgs& a, hipStream_t st) {
   DM_REQUIRE(a.taps == 1 || a.taps == 9, "conv: taps must be 1 or 9");
   DM_REQUIRE(a.stride == 1 || a.stride == 2, "conv: stride must be 1 or 2");
   DM_REQUIRE(!a.upsample || (a.taps == 9 && a.stride == 1), "conv: upsample needs 3x3 stride 1");
+  DM_REQUIRE(a.upsample >= 0 && a.upsample <= 2, "conv: upsample must be 0, 1 (nearest) or 2 (sub-pixel)");
   DM_REQUIRE(a.Cin1 % kBK == 0 && a.Cin2 % kBK == 0, "conv: input channels must be multiples of 32");
   DM_REQUIRE(a.Cin1 > 0, "conv: no input channels");
-  DM_REQUIRE(a.K == a.taps * a.Cin1 + a.Cin2, "conv: K mismatch");
+  DM_REQUIRE(a.K == (a.upsample == 2 ? 4 : a.taps) * a.Cin1 + a.Cin2, "conv: K mismatch");
+  DM_REQUIRE(a.upsample != 2 || a.Cin2 == 0, "conv: sub-pixel upsample has no second segment");
   DM_REQUIRE(a.x1_pitch % 4 == 0 && a.y_pitch >= a.Cout && a.K % 4 == 0, "conv: pitch");
   DM_REQUIRE(aligned16(a.x1) && aligned16(a.w), "conv: operands must be 16-byte aligned");
   DM_REQUIRE(a.Cin2 == 0 || (a.x2 && aligned16(a.x2) && a.x2_pitch % 4 == 0), "conv: segment-2 operand");
@@ -283,6 +285,8 @@ int conv2d_igemm(const ConvArgs& a, hipStream_t st) {
     conv_patch_pick(a, g);
     return conv2d_patch(a, pick + 1, g, st);
   }
+  DM_REQUIRE(a.upsample != 2, "conv: the sub-pixel upsample runs on the halo-patch kernel only (shape has no "
+                              "whole-row tiling)");
   switch (pick) {
     case 0: return launch_conv_tile<128, 128, 64, 64>(a, mode, st);
     case 1: return launch_conv_tile<128, 64, 64, 32>(a, mode, st);
@@ -317,8 +321,8 @@ std::string conv_label(const ConvArgs& a) {
                                 "conv_patch_kernel<128,64,64,32",   "conv_patch_kernel<64,64,32,32"};
   const int p = conv_pick(a);
   std::string s = names[p];
-  if (p >= 3) {  // <BM,BN,WM,WN,UP,MAXP,PRO>; MAXP 288 for 128-row tiles, 160 for 64-row tiles
-    s += a.upsample ? ",true" : ",false";
+  if (p >= 3) {  // <BM,BN,WM,WN,MODE,MAXP,PRO>; MAXP 288 for 128-row tiles, 160 for 64-row tiles
+    s += "," + std::to_string(a.upsample);
     s += p == 5 ? ",160" : ",288";
     s += a.pro_scale ? ",true>" : ",false>";
   }

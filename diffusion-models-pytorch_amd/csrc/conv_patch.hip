@@ -13,6 +13,16 @@
 // K order inside the packed weight matrix: k = (chunk * 9 + tap) * 32 + c
 // (chunk-major), followed by an optional 1x1 segment (the ResBlock shortcut)
 // of Cin2 columns, handled by a second, un-pipelined phase.
+//
+// MODE 2 (sub-pixel nearest-2x upsample + 3x3 conv, models/modules.py:60-65,
+// adm/unet.py:119-129): an output pixel (2iy + py, 2ix + px) of the upsampled
+// conv only ever sees the 2x2 low-res neighbourhood rows iy + py - 1 + {0, 1},
+// cols ix + px - 1 + {0, 1}, with the 3x3 taps that land on the same source
+// pixel summed. Each parity class (py, px) is therefore a 4-tap conv on the
+// low-res input (taps (py + ty, px + tx) of the ordinary pad-1 low-res patch)
+// with its own combined weights [4][Cout][chunk][4 taps][32]: 4/9 of the MFMA
+// work of convolving the upsampled image. Blocks are split over the 4 parities;
+// the epilogue scatters rows to (2iy + py, 2ix + px).
 #include "dm_common.h"
 #include "dm_kernels.h"
 #include "mfma_tile.h"
@@ -27,25 +37,36 @@ __device__ __forceinline__ int xcd_remap_p(int bid, int nblk) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
-template <int BM, int BN, int WM, int WN, bool UP, int MAXP, bool PRO>
+template <int BM, int BN, int WM, int WN, int MODE, int MAXP, bool PRO>
 __global__ void __launch_bounds__(256)
 conv_patch_kernel(ConvArgs a, PatchGeom g) {
   using Cfg = TileCfg<BM, BN, WM, WN>;
+  constexpr bool UP = MODE == 1, SUB = MODE == 2;
+  constexpr int NTAP = SUB ? 4 : 9;
   constexpr int PATCH_FLOATS = MAXP * kLDK;
   constexpr int WSTAGE = BN * kLDK;
   __shared__ __attribute__((aligned(16))) float lds[PATCH_FLOATS + 2 * WSTAGE];
   float* patch = lds;
   float* wbuf = lds + PATCH_FLOATS;
 
-  const int M = a.B * a.Hout * a.Wout;
+  // GEMM rows: output pixels, or (SUB) low-res pixels of one parity class
+  const int Ho = SUB ? a.Hin : a.Hout, Wo = SUB ? a.Win : a.Wout;
+  const int M = a.B * Ho * Wo;
   const int N = a.Cout;
   const int nN = ceil_div(N, BN);
-  const int bid = xcd_remap_p(blockIdx.x, gridDim.x);
+  int bid = xcd_remap_p(blockIdx.x, gridDim.x);
+  int par = 0;
+  if (SUB) {
+    const int per_par = ceil_div(M, BM) * nN;
+    par = bid / per_par;
+    bid -= par * per_par;
+  }
+  const int py = par >> 1, px = par & 1;
   const int mt = bid / nN, nt = bid - (bid / nN) * nN;
   const int m0 = mt * BM, n0 = nt * BN;
-  const int HWo = a.Hout * a.Wout;
+  const int HWo = Ho * Wo;
   const int b0 = m0 / HWo;
-  const int y0 = (m0 - b0 * HWo) / a.Wout;  // first output row of the tile (even for UP)
+  const int y0 = (m0 - b0 * HWo) / Wo;  // first output row of the tile (even for UP)
 
   const int t = threadIdx.x;
   const int lane = t & 63, wave = t >> 6;
@@ -83,19 +104,19 @@ conv_patch_kernel(ConvArgs a, PatchGeom g) {
   for (int j = 0; j < Cfg::B_ITERS; ++j) {
     const int n = n0 + lrow + j * Cfg::ROWS_PER_PASS;
     w_ok[j] = n < N;
-    wrow[j] = a.w + (size_t)(w_ok[j] ? n : N - 1) * a.K + 4 * lc4;
+    wrow[j] = a.w + ((size_t)par * N + (w_ok[j] ? n : N - 1)) * a.K + 4 * lc4;
   }
 
   // ---- A-fragment patch coordinates of this lane's rows
   int fy[Cfg::TM], fx[Cfg::TM], fimg[Cfg::TM];
-  const int tile_rows = g.TH * a.Wout;
+  const int tile_rows = g.TH * Wo;
 #pragma unroll
   for (int i = 0; i < Cfg::TM; ++i) {
     const int ml = wm * WM + i * 32 + lr;
     fimg[i] = ml / tile_rows;
     const int rem = ml - fimg[i] * tile_rows;
-    fy[i] = rem / a.Wout;
-    fx[i] = rem - fy[i] * a.Wout;
+    fy[i] = rem / Wo;
+    fx[i] = rem - fy[i] * Wo;
   }
 
   const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
@@ -115,7 +136,7 @@ conv_patch_kernel(ConvArgs a, PatchGeom g) {
         const f4 sc = *reinterpret_cast<const f4*>(a.pro_scale + (size_t)pimg[j] * a.Cin1 + cc);
         const f4 sh = *reinterpret_cast<const f4*>(a.pro_shift + (size_t)pimg[j] * a.Cin1 + cc);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) rp[j][q] = silu_f(rp[j][q] * sc[q] + sh[q]);
+        for (int q = 0; q < 4; ++q) rp[j][q] = silu_fast(rp[j][q] * sc[q] + sh[q]);
       }
     }
   };
@@ -190,16 +211,19 @@ conv_patch_kernel(ConvArgs a, PatchGeom g) {
   for (int c = 0; c < nchunks; ++c) {
     const bool more_chunks = c + 1 < nchunks;
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int kt = c * 9 + tap;
-      const bool more_w = (tap < 8) || more_chunks;
+    for (int tap = 0; tap < NTAP; ++tap) {
+      const int kt = c * NTAP + tap;
+      const bool more_w = (tap < NTAP - 1) || more_chunks;
       if (more_w) load_w(kt + 1);
       if (tap == 0 && more_chunks) load_patch(c + 1);
       if (PRO && tap >= 1 && more_chunks) {
-        constexpr int per = (PJ + 7) / 8;
-        transform(c + 1, (tap - 1) * per, tap == 8 ? PJ : tap * per);
+        constexpr int per = (PJ + NTAP - 2) / (NTAP - 1);
+        transform(c + 1, (tap - 1) * per, tap == NTAP - 1 ? PJ : tap * per);
       }
-      compute_tap(tap / 3, tap % 3, kt & 1);
+      if (SUB)
+        compute_tap(py + (tap >> 1), px + (tap & 1), kt & 1);
+      else
+        compute_tap(tap / 3, tap % 3, kt & 1);
       if (more_w) store_w((kt + 1) & 1);
       __syncthreads();
     }
@@ -233,7 +257,7 @@ conv_patch_kernel(ConvArgs a, PatchGeom g) {
     }
   }
 
-  // ---- epilogue (as conv.hip)
+  // ---- epilogue (as conv.hip); SUB rows scatter to output pixel (2iy + py, 2ix + px)
   const bool block_one_image = (HWo % BM) == 0;
 #pragma unroll
   for (int j = 0; j < Cfg::TN; ++j) {
@@ -247,32 +271,41 @@ conv_patch_kernel(ConvArgs a, PatchGeom g) {
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm * WM + i * 32 + acc_row(r, lh);
         if (m >= M) continue;
+        size_t mo = m;
+        if (SUB) {
+          const int bb = m / HWo, rr = m - bb * HWo;
+          const int iy = rr / Wo, ix = rr - (rr / Wo) * Wo;
+          mo = ((size_t)bb * a.Hout + 2 * iy + py) * a.Wout + 2 * ix + px;
+        }
         float v = acc[i][j][r];
         if (a.bias) v = v + bn;
         if (a.rowvec) v = v + (block_one_image ? rv_blk : a.rowvec[(size_t)(m / HWo) * a.rowvec_pitch + n]);
-        if (a.res) v = v + a.res[(size_t)m * a.res_pitch + n];
-        a.y[(size_t)m * a.y_pitch + n] = v;
+        if (a.res) v = v + a.res[mo * a.res_pitch + n];
+        a.y[mo * a.y_pitch + n] = v;
       }
     }
   }
 }
 
+template <int BM, int BN, int WM, int WN, int MODE, int MAXP>
+void launch_patch_mode(const ConvArgs& a, const PatchGeom& g, int blocks, hipStream_t st) {
+  if (a.pro_scale)
+    hipLaunchKernelGGL((conv_patch_kernel<BM, BN, WM, WN, MODE, MAXP, true>), dim3(blocks), dim3(256), 0, st, a, g);
+  else
+    hipLaunchKernelGGL((conv_patch_kernel<BM, BN, WM, WN, MODE, MAXP, false>), dim3(blocks), dim3(256), 0, st, a, g);
+}
+
 template <int BM, int BN, int WM, int WN, int MAXP>
 int launch_patch(const ConvArgs& a, const PatchGeom& g, hipStream_t st) {
-  const int M = a.B * a.Hout * a.Wout;
-  const int blocks = ceil_div(M, BM) * ceil_div(a.Cout, BN);
-  const bool pro = a.pro_scale != nullptr;
-  if (a.upsample) {
-    if (pro)
-      hipLaunchKernelGGL((conv_patch_kernel<BM, BN, WM, WN, true, MAXP, true>), dim3(blocks), dim3(256), 0, st, a, g);
-    else
-      hipLaunchKernelGGL((conv_patch_kernel<BM, BN, WM, WN, true, MAXP, false>), dim3(blocks), dim3(256), 0, st, a, g);
-  } else {
-    if (pro)
-      hipLaunchKernelGGL((conv_patch_kernel<BM, BN, WM, WN, false, MAXP, true>), dim3(blocks), dim3(256), 0, st, a, g);
-    else
-      hipLaunchKernelGGL((conv_patch_kernel<BM, BN, WM, WN, false, MAXP, false>), dim3(blocks), dim3(256), 0, st, a, g);
-  }
+  const bool sub = a.upsample == 2;
+  const int M = sub ? a.B * a.Hin * a.Win : a.B * a.Hout * a.Wout;
+  const int blocks = ceil_div(M, BM) * ceil_div(a.Cout, BN) * (sub ? 4 : 1);
+  if (sub)
+    launch_patch_mode<BM, BN, WM, WN, 2, MAXP>(a, g, blocks, st);
+  else if (a.upsample)
+    launch_patch_mode<BM, BN, WM, WN, 1, MAXP>(a, g, blocks, st);
+  else
+    launch_patch_mode<BM, BN, WM, WN, 0, MAXP>(a, g, blocks, st);
   DM_LAUNCH_CHECK();
   return DM_OK;
 }
@@ -283,7 +316,8 @@ int launch_patch(const ConvArgs& a, const PatchGeom& g, hipStream_t st) {
 // (then the im2col kernel is used).
 bool conv_patch_geom(const ConvArgs& a, int BM, PatchGeom& g) {
   if (a.taps != 9 || a.stride != 1) return false;
-  const int Ho = a.Hout, Wo = a.Wout;
+  const bool sub = a.upsample == 2;  // tiles over the low-res pixels of one parity class
+  const int Ho = sub ? a.Hin : a.Hout, Wo = sub ? a.Win : a.Wout;
   if (Wo > BM || BM % Wo != 0) return false;
   const int rows = BM / Wo;  // output rows per tile (across images)
   if (rows <= Ho) {
@@ -295,11 +329,12 @@ bool conv_patch_geom(const ConvArgs& a, int BM, PatchGeom& g) {
     g.TB = rows / Ho;
     g.TH = Ho;
   }
-  if (a.upsample) {
+  if (a.upsample == 1) {
     if (g.TH % 2 != 0 || a.Cin2 != 0) return false;
     g.PH = g.TH / 2 + 2;
     g.PW = a.Win + 2;
   } else {
+    if (sub && a.Cin2 != 0) return false;
     g.PH = g.TH + 2;
     g.PW = Wo + 2;
   }

@@ -61,6 +61,15 @@ __device__ __forceinline__ float silu_f(float v) {
   return v / (1.0f + expf(-v));
 }
 
+// SiLU for operand prologues that sit next to MFMA work (conv halo-patch load):
+// hardware exp2 and reciprocal (v_exp_f32 / v_rcp_f32, ~1 ulp each) instead of
+// the libm expf + IEEE division of silu_f — ~6 VALU ops instead of ~30, a
+// relative difference of a few 1e-7 (well inside the 1e-4 parity bound).
+__device__ __forceinline__ float silu_fast(float v) {
+  const float e = __builtin_amdgcn_exp2f(-v * 1.4426950408889634f);
+  return v * __builtin_amdgcn_rcpf(1.0f + e);
+}
+
 __device__ __forceinline__ float gelu_tanh_f(float v) {
   // torch GELU(approximate='tanh'): 0.5 x (1 + tanh(sqrt(2/pi) (x + 0.044715 x^3)))
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;

@@ -142,5 +142,7 @@ int sampler_step(const StepArgs& s, hipStream_t st);
 int nchw_to_nhwc(const float* x, int B, int C, int HW, float* y, int y_pitch, hipStream_t st);
 int nhwc_to_nchw(const float* x, int B, int C, int HW, int pitch, float* y, hipStream_t st);
 int repack_conv(const float* w, int Cout, int Cin, int taps, float* out, int ldw, int col0, hipStream_t st);
+// torch 3x3 weight [Cout][Cin][3][3] -> sub-pixel upsample weights [4 parities][Cout][4 * Cin]
+int repack_subpixel(const float* w, int Cout, int Cin, float* out, hipStream_t st);
 
 }  // namespace dm

@@ -340,7 +340,43 @@ __global__ void repack_conv_kernel(const float* __restrict__ w, int Cout, int Ci
   out[(size_t)co * ldw + col0 + k] = w[e];
 }
 
+// Sub-pixel weights of "nearest-2x upsample, then 3x3 conv" (conv_patch.hip MODE 2):
+// out[par][co][((ci/32) * 4 + ty * 2 + tx) * 32 + ci % 32] = sum over the 3x3 taps (ky, kx)
+// that land on low-res pixel offset (ty, tx) for output parity par = (py, px):
+// py = 0: ty 0 <- ky {0}, ty 1 <- ky {1, 2};  py = 1: ty 0 <- ky {0, 1}, ty 1 <- ky {2}  (same for x).
+// Summed in fp64, rounded once.
+__global__ void repack_subpix_kernel(const float* __restrict__ w, int Cout, int Cin, float* __restrict__ out) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = 4L * Cout * Cin * 4;
+  if (e >= total) return;
+  const int tap = e & 3;
+  long r = e >> 2;
+  const int ci = r % Cin;
+  r /= Cin;
+  const int co = r % Cout;
+  const int par = r / Cout;
+  const int py = par >> 1, px = par & 1, ty = tap >> 1, tx = tap & 1;
+  const int ky0 = (py == 0) ? (ty == 0 ? 0 : 1) : (ty == 0 ? 0 : 2);
+  const int ky1 = (py == 0) ? (ty == 0 ? 0 : 2) : (ty == 0 ? 1 : 2);
+  const int kx0 = (px == 0) ? (tx == 0 ? 0 : 1) : (tx == 0 ? 0 : 2);
+  const int kx1 = (px == 0) ? (tx == 0 ? 0 : 2) : (tx == 0 ? 1 : 2);
+  const float* wk = w + ((size_t)co * Cin + ci) * 9;
+  double s = 0.0;
+  for (int ky = ky0; ky <= ky1; ++ky)
+    for (int kx = kx0; kx <= kx1; ++kx) s += (double)wk[ky * 3 + kx];
+  out[((size_t)par * Cout + co) * (4 * (size_t)Cin) + ((ci >> 5) * 4 + tap) * 32 + (ci & 31)] = (float)s;
+}
+
 }  // namespace
+
+int repack_subpixel(const float* w, int Cout, int Cin, float* out, hipStream_t st) {
+  DM_REQUIRE(Cin % 32 == 0, "sub-pixel weight packing: input channels must be multiples of 32");
+  const long total = 4L * Cout * Cin * 4;
+  hipLaunchKernelGGL(repack_subpix_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, w, Cout, Cin,
+                     out);
+  DM_LAUNCH_CHECK();
+  return DM_OK;
+}
 
 int timestep_embed(const int64_t* t, int B, int dim, int kind, const float* freqs, float* out, hipStream_t st) {
   DM_REQUIRE(dim % 2 == 0 && dim >= 4, "timestep embedding: dim must be even and >= 4");

@@ -46,7 +46,7 @@ struct ParamReader {
 
 // A copy / repack job into the weight arena.
 struct PackJob {
-  int kind;  // 0 raw copy, 1 conv repack, 2 add (bias sum)
+  int kind;  // 0 raw copy, 1 conv repack, 2 add (bias sum), 3 sub-pixel upsample repack
   const float* src;
   const float* src2;
   int64_t n;
@@ -74,6 +74,11 @@ struct Packer {
   void add_at(const float* a, const float* b, int64_t n, size_t off) {
     jobs.push_back({2, a, b, n, 0, 0, 0, 0, 0, off});
   }
+  size_t subpix(const float* w, int Cout, int Cin) {
+    const size_t off = reserve((int64_t)16 * Cout * Cin);
+    jobs.push_back({3, w, nullptr, (int64_t)Cout * Cin * 9, Cout, Cin, 9, 0, 0, off});
+    return off;
+  }
 };
 
 __global__ void vec_add_kernel(const float* a, const float* b, float* out, int64_t n) {
@@ -82,7 +87,11 @@ __global__ void vec_add_kernel(const float* a, const float* b, float* out, int64
 }
 
 struct GnP { size_t g, b; int C; };
-struct ConvP { size_t w, bias; int Cout, Cin, taps, K; };
+struct ConvP {
+  size_t w, bias;
+  int Cout, Cin, taps, K;
+  size_t w_sub = 0;  // sub-pixel weights [4][Cout][4 Cin] of an upsample conv (0 = none)
+};
 
 struct ResBlockP {
   int cin, cout;
@@ -310,6 +319,7 @@ static int unet_create(const dm_unet_arch* arch, const float* const* params, con
     r.conv1.w = pk.reserve((int64_t)cout * 9 * cin);
     pk.conv_at(w1, cout, cin, 9, 9 * cin, 0, r.conv1.w);
     r.conv1.bias = pk.raw(b1, cout);
+    if (updown == 1) r.conv1.w_sub = pk.subpix(w1, cout, cin);  // nearest-2x folded into conv1
     const int pn = r.adagn ? 2 * cout : cout;
     const bool gn2_first = a.variant == 1;  // AdaGN registers its gn before its proj
     if (gn2_first) r.gn2 = gn(cout, "ResBlock.adagn.gn");
@@ -380,6 +390,7 @@ static int unet_create(const dm_unet_arch* arch, const float* const* params, con
     c.w = pk.reserve((int64_t)C * 9 * C);
     pk.conv_at(w, C, C, 9, 9 * C, 0, c.w);
     c.bias = pk.raw(b, C);
+    if (std::string(what) == "Upsample") c.w_sub = pk.subpix(w, C, C);
     m->convs.push_back(c);
     return (int)m->convs.size() - 1;
   };
@@ -481,6 +492,9 @@ static int unet_create(const dm_unet_arch* arch, const float* const* params, con
       DM_CHECK_HIP(hipMemcpyAsync(m->arena + j.dst, j.src, j.n * sizeof(float), hipMemcpyDeviceToDevice, st));
     } else if (j.kind == 1) {
       rc = repack_conv(j.src, j.Cout, j.Cin, j.taps, m->arena + j.dst, j.ldw, j.col0, st);
+      if (rc) return rc;
+    } else if (j.kind == 3) {
+      rc = repack_subpixel(j.src, j.Cout, j.Cin, m->arena + j.dst, st);
       if (rc) return rc;
     } else {
       hipLaunchKernelGGL(vec_add_kernel, dim3((unsigned)((j.n + 255) / 256)), dim3(256), 0, st, j.src, j.src2,
@@ -685,6 +699,13 @@ int UNetModel::build_plan(int B, int H, int W) {
       c1.bias = P(r.conv1.bias);
       if (!r.adagn) { c1.rowvec = projs + r.proj_col; c1.rowvec_pitch = proj_total; }
       if (r.updown == 1) { c1.upsample = 1; c1.Hin = Hi; c1.Win = Wi; }
+      // sub-pixel form of the upsample conv (4/9 of the MFMA work) when its low-res shape tiles
+      auto try_subpix = [&](ConvArgs& c, size_t w_sub) {
+        if (!c.upsample || !w_sub) return;
+        ConvArgs s = c;
+        s.upsample = 2; s.w = P(w_sub); s.K = 4 * c.Cin1;
+        if (conv_pick(s) >= 3) c = s;
+      };
       ConvArgs c2{};
       c2.x1 = a2; c2.x1_pitch = r.cout; c2.Cin1 = r.cout; c2.Hin = Ho; c2.Win = Wo;
       c2.taps = 9; c2.stride = 1;
@@ -696,6 +717,7 @@ int UNetModel::build_plan(int B, int H, int W) {
       } else {
         c2.res = xres.p; c2.res_pitch = xres.pitch;
       }
+      try_subpix(c1, r.conv1.w_sub);
       const bool fuse1 = r.updown != 2 && conv_pick(c1) >= 3, fuse2 = conv_pick(c2) >= 3;
       // AdaGN modulation gn(h) * (1 + ys) + yb, [ys | yb] from the fused projection (modules.py:114-123)
       const float* ms = r.adagn ? projs + r.proj_col : nullptr;
@@ -711,6 +733,7 @@ int UNetModel::build_plan(int B, int H, int W) {
         add("resample2x", 0, 4.0 * B * ((double)Hi * Wi + (double)Ho * Wo) * r.cin,
             [=](hipStream_t st) { return resample2x(xin, va1, down, gsc, gsh, st); });
         c1.x1 = a1; c1.upsample = 0; c1.Hin = Ho; c1.Win = Wo;
+        c1.w = P(r.conv1.w); c1.K = r.conv1.K;
       } else if (fuse1) {
         // GroupNorm + SiLU folded into conv1's patch load: x read once, normalised tensor never stored
         add("gn_finalize", 0, 8.0 * B * r.cin, [=](hipStream_t st) {
@@ -793,6 +816,11 @@ int UNetModel::build_plan(int B, int H, int W) {
       c.y = y.p; c.y_pitch = y.pitch; c.Cout = n.cout; c.B = B;
       c.Hout = Hl(n.level_out); c.Wout = Wl(n.level_out);
       c.bias = P(cv.bias);
+      if (c.upsample && cv.w_sub) {
+        ConvArgs s = c;
+        s.upsample = 2; s.w = P(cv.w_sub); s.K = 4 * c.Cin1;
+        if (conv_pick(s) >= 3) c = s;
+      }
       add_conv(c);
     }
     x_cur = y;

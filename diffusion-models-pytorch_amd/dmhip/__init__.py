@@ -21,6 +21,7 @@ from dmhip._lib import (  # noqa: F401
     groupnorm_affine,
     conv2d_nhwc,
     pack_conv_weight,
+    pack_conv_weight_subpixel,
     gemm,
     softmax_rows,
     timestep_embedding,

@@ -134,6 +134,7 @@ def _declare(L: ctypes.CDLL):
     L.dm_pack_conv_weight.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int,
                                       vp]
     L.dm_conv2d_nhwc.argtypes = [ctypes.POINTER(ConvDesc), vp]
+    L.dm_pack_conv_weight_subpixel.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp]
     L.dm_gemm.argtypes = [ctypes.POINTER(GemmDesc), vp]
     L.dm_softmax_rows.argtypes = [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, vp]
     L.dm_timestep_embedding.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp, vp]
@@ -246,6 +247,15 @@ def pack_conv_weight(w: torch.Tensor, out: torch.Tensor, ldw: int, col0: int = 0
     Cout, Cin, kh, kw = w.shape
     check(load().dm_pack_conv_weight(w.data_ptr(), Cout, Cin, kh * kw, out.data_ptr(), ldw, col0,
                                      stream_handle(w.device)), 'dm_pack_conv_weight')
+
+
+def pack_conv_weight_subpixel(w: torch.Tensor, out: torch.Tensor):
+    """torch 3x3 weight [Cout][Cin][3][3] -> sub-pixel upsample weights [4][Cout][4 Cin] (conv upsample = 2)."""
+    Cout, Cin, kh, kw = w.shape
+    if (kh, kw) != (3, 3) or out.numel() != 16 * Cout * Cin:
+        raise ValueError('sub-pixel packing needs a 3x3 weight and a [4, Cout, 4 Cin] output')
+    check(load().dm_pack_conv_weight_subpixel(w.data_ptr(), Cout, Cin, out.data_ptr(), stream_handle(w.device)),
+          'dm_pack_conv_weight_subpixel')
 
 
 def conv2d_nhwc(desc: ConvDesc, device=None):

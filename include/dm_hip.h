@@ -204,9 +204,15 @@ int dm_groupnorm_affine(const float* x, int x_pitch, int B, int HW, int C, int G
 int dm_pack_conv_weight(const float* w, int Cout, int Cin, int taps, float* out, int ldw, int col0,
                         void* stream);
 
+/* Pack a torch 3x3 weight [Cout][Cin][3][3] for the sub-pixel upsample conv (dm_conv_desc.upsample = 2):
+ * out [4 output parities][Cout][4 * Cin], the 3x3 taps that read the same low-res pixel summed. */
+int dm_pack_conv_weight_subpixel(const float* w, int Cout, int Cin, float* out, void* stream);
+
 typedef struct dm_conv_desc {
   const float* x;  int x_pitch, Cin, Hin, Win;
-  int taps, stride, upsample;
+  int taps, stride;
+  int upsample;    /* 0 none; 1 nearest-2x then 3x3 (Hout = 2 Hin); 2 the same as sub-pixel
+                      4-tap convs (weights from dm_pack_conv_weight_subpixel, K = 4 Cin) */
   const float* x2; int x2_pitch, Cin2;
   const float* w;  int K;
   float* y;        int y_pitch, Cout, B, Hout, Wout;

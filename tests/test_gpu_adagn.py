@@ -77,6 +77,9 @@ def test_adagn_label_out_of_range(cuda, golden):
 @pytest.mark.gpu
 @pytest.mark.parametrize('batched', [True, False])
 def test_ddimcfg_trajectory_vs_reference(cuda, golden, report, batched):
+    """DDIMCFG-10 (s = 3). Every step is checked teacher-forced (from the reference's previous
+    sample) against the 1e-4 bound; the free-running trajectory compounds the ~4e-6 forward
+    difference through sqrt(1/a_t) (~160 at t = 900) and the CFG combine, so its bound is 5e-4."""
     g, meta = golden('adagn')
     model, _ = _model(meta, 'tiny_updown')
     model = model.to(cuda)
@@ -86,12 +89,37 @@ def test_ddimcfg_trajectory_vs_reference(cuda, golden, report, batched):
     d.batch_cfg = batched
     init = torch.from_numpy(g['cfg_init']).to(cuda)
     labels = torch.from_numpy(g['cfg_labels']).to(cuda)
+    seq = d.respaced_seq.tolist()
+    pairs = list(zip(reversed(seq), reversed([-1] + seq[:-1])))
+    worst_step = 0.0
+    for i, (t, tp) in enumerate(pairs):
+        x = init if i == 0 else torch.from_numpy(g[f'cfg_step{i - 1}_sample']).to(cuda)
+        out = _one_step(d, model, x, labels, t, tp, batched)
+        err = float(np.abs(out['sample'].cpu().numpy() - g[f'cfg_step{i}_sample']).max())
+        worst_step = max(worst_step, err)
+        assert err <= TOL, (i, err)
     worst = 0.0
     for i, out in enumerate(d.sample_loop(model, init, model_kwargs=dict(y=labels))):
-        err = np.abs(out['sample'].cpu().numpy() - g[f'cfg_step{i}_sample']).max()
-        worst = max(worst, float(err))
-        assert err <= TOL, (i, err)
-    report(f'ddimcfg10_adagn_{"batched" if batched else "two_calls"}_maxabs_vs_reference', worst)
+        err = float(np.abs(out['sample'].cpu().numpy() - g[f'cfg_step{i}_sample']).max())
+        worst = max(worst, err)
+        assert err <= 5 * TOL, (i, err)
+    tag = 'batched' if batched else 'two_calls'
+    report(f'ddimcfg10_adagn_{tag}_single_step_maxabs_vs_reference', worst_step)
+    report(f'ddimcfg10_adagn_{tag}_free_running_maxabs_vs_reference', worst)
+
+
+def _one_step(d, model, x, labels, t, tp, batched):
+    """One DDIMCFG step from x at (t, tp): cond + uncond forwards (one 2B call with null labels when
+    batched, as the sampler does), then the fused CFG update."""
+    B = x.shape[0]
+    if batched:
+        tb = torch.full((2 * B, ), t, dtype=torch.long, device=x.device)
+        both = model(torch.cat([x, x]), tb, torch.cat([labels, torch.full_like(labels, -1)]))
+        oc, ou = both[:B], both[B:]
+    else:
+        tb = torch.full((B, ), t, dtype=torch.long, device=x.device)
+        oc, ou = model(x, tb, labels), model(x, tb, None)
+    return d._step(oc, x, t, tp, model_output_uncond=ou, guidance_scale=d.guidance_scale)
 
 
 @pytest.mark.gpu

@@ -219,3 +219,47 @@ def test_conv_fused_groupnorm_silu(cuda, B, Cin, Cout, H, up, tile):
     y = _run_conv(cuda, xd, _pack(w, cuda), Cout, Ho, Ho, 9, 1, up, b.to(cuda), tile=tile, pro=pro)
     err = (y.cpu().double() - _nhwc(ref)).abs().max().item()
     assert err < 1e-4, err
+
+
+def _pack_subpix(w, cuda):
+    Cout, Cin = w.shape[:2]
+    out = torch.zeros((4, Cout, 4 * Cin), device=cuda)
+    dmhip.pack_conv_weight_subpixel(w.to(cuda).contiguous(), out)
+    return out.view(4 * Cout, 4 * Cin)
+
+
+@pytest.mark.parametrize('tile', [0, 4, 5, 6])
+@pytest.mark.parametrize('B,Cin,Cout,H', [(2, 32, 32, 4), (3, 64, 64, 16), (2, 32, 64, 8), (3, 32, 32, 2),
+                                          (4, 64, 128, 8), (2, 96, 64, 4)])
+def test_conv_subpixel_upsample_exact(cuda, B, Cin, Cout, H, tile):
+    """nearest-2x + 3x3 conv as four 4-tap sub-pixel convs (upsample = 2): integer operands keep the
+    summed weights and every product exact, so the result equals the upsampled conv bit for bit."""
+    x = _ints((B, Cin, H, H), -2, 3, seed=70)
+    w = _ints((Cout, Cin, 3, 3), -2, 3, seed=71)
+    b = _ints((Cout, ), seed=72)
+    ref = F.conv2d(F.interpolate(x, scale_factor=2, mode='nearest').double(), w.double(), b.double(),
+                   padding=1).float()
+    wp = _pack_subpix(w, cuda)
+    try:
+        y = _run_conv(cuda, _nhwc(x).to(cuda), wp, Cout, 2 * H, 2 * H, 9, 1, 2, b.to(cuda), tile=tile)
+    except ValueError as e:  # low-res shape without a whole-row tiling (the UNet plan then keeps the
+        assert tile != 0 or H < 4, e  # nearest-2x conv); every shape >= 4x4 tiles automatically
+        pytest.skip(str(e))
+    assert torch.equal(y.cpu(), _nhwc(ref))
+
+
+@pytest.mark.parametrize('B,Cin,Cout,H', [(2, 64, 64, 8), (3, 32, 64, 16), (2, 64, 32, 4)])
+def test_conv_subpixel_fused_groupnorm_silu(cuda, B, Cin, Cout, H):
+    g = torch.Generator().manual_seed(73)
+    x = torch.randn((B, Cin, H, H), generator=g) * 2 + 0.3
+    gamma, beta = torch.randn(Cin, generator=g), torch.randn(Cin, generator=g)
+    w = torch.randn((Cout, Cin, 3, 3), generator=g) * 0.05
+    b = torch.randn(Cout, generator=g)
+    a = F.interpolate(F.silu(F.group_norm(x.double(), 32, gamma.double(), beta.double(), 1e-5)), scale_factor=2,
+                      mode='nearest')
+    ref = F.conv2d(a, w.double(), b.double(), padding=1)
+    xd = _nhwc(x).to(cuda)
+    pro = dmhip.groupnorm_affine(xd, B, H * H, Cin, 32, 1e-5, gamma.to(cuda), beta.to(cuda))
+    y = _run_conv(cuda, xd, _pack_subpix(w, cuda), Cout, 2 * H, 2 * H, 9, 1, 2, b.to(cuda), pro=pro)
+    err = (y.cpu().double() - _nhwc(ref)).abs().max().item()
+    assert err < 1e-4, err
