@@ -41,6 +41,7 @@ import torch.distributed as dist  # noqa: E402
 METRIC = 'images/sec at DDIM-50, CIFAR-10 UNet 32×32, bs=256; 1/2/4/8 GPU'
 FP32_PEAK_TFLOPS = 157.3   # MI355X dense fp32 (MFMA f32 = vector rate), MI355X_MICROARCH.md
 HBM_PEAK_GBS = 8000.0
+PROFILE_EVERY = 10   # per-launch events cost ~5 % when on every launch; 1 forward in 10 is observed
 
 
 def parse():
@@ -53,6 +54,8 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-batch', type=int, default=256, help='batch of the timed CPU denoising step')
     ap.add_argument('--profile-json', default=None, help='write the per-op profile here (rank 0)')
+    ap.add_argument('--no-profile', action='store_true',
+                    help='no per-launch HIP events in the timed region (roofline fields then null)')
     return ap.parse_args()
 
 
@@ -105,6 +108,36 @@ def cpu_baseline(sd, batch, n_steps):
                        f'({cpu_model_name()}), extrapolated x{n_steps}; {dt:.2f} s measured')
 
 
+def roofline(prof):
+    """Roofline of the dominant kernel family (most GPU time in the timed region)."""
+    fam = {}
+    for op in prof:
+        f = fam.setdefault(op['label'], dict(flops=0.0, bytes=0.0, ms=0.0, launches=0))
+        f['flops'] += op['flops'] * op['launches']
+        f['bytes'] += op['bytes'] * op['launches']
+        f['ms'] += op['ms_total']
+        f['launches'] += op['launches']
+    dom_name, dom = max(fam.items(), key=lambda kv: kv[1]['ms'])
+    avg_ms = dom['ms'] / max(1, dom['launches'])
+    flops_per_launch = dom['flops'] / max(1, dom['launches'])
+    bytes_per_launch = dom['bytes'] / max(1, dom['launches'])
+    if flops_per_launch > 0:
+        achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12
+        roof = dict(bound='mfma', achieved=round(achieved, 2), peak=FP32_PEAK_TFLOPS, unit='TFLOP/s',
+                    frac=round(achieved / FP32_PEAK_TFLOPS, 4), traffic=None)
+    else:
+        achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+        roof = dict(bound='hbm', achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit='GB/s',
+                    frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None)
+    traffic, traffic_src = pmc_traffic(dom_name)
+    roof.update(traffic=traffic, traffic_source=traffic_src, algorithmic_bytes_per_launch=bytes_per_launch,
+                kernel=dom_name, avg_launch_ms=round(avg_ms, 4), launches=dom['launches'],
+                algorithmic_per_launch=flops_per_launch if flops_per_launch > 0 else bytes_per_launch)
+    total_gpu_ms = sum(f['ms'] for f in fam.values())
+    total_flops = sum(f['flops'] for f in fam.values())
+    return roof, total_gpu_ms, total_flops, fam
+
+
 def main():
     args = parse()
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -149,7 +182,8 @@ def main():
     if args.warmup == 0:  # build the B-sized plan outside the timed region
         model(torch.zeros((B, 3, 32, 32), device=dev), torch.zeros((B, ), dtype=torch.long, device=dev))
     handle = model.native_handle(dev)
-    dmhip.unet_profile_enable(handle, True)
+    # HIP events around every launch of every PROFILE_EVERY-th forward of the timed region
+    dmhip.unet_profile_enable(handle, 0 if args.no_profile else PROFILE_EVERY)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -167,32 +201,9 @@ def main():
     _check(dmhip.load().dm_unet_memory(handle, ctypes.byref(wbytes), ctypes.byref(wsbytes)), 'dm_unet_memory')
     dmhip.unet_profile_enable(handle, False)
 
-    # roofline of the dominant kernel family (most GPU time in the timed region)
-    fam = {}
-    for op in prof:
-        f = fam.setdefault(op['label'], dict(flops=0.0, bytes=0.0, ms=0.0, launches=0))
-        f['flops'] += op['flops'] * op['launches']
-        f['bytes'] += op['bytes'] * op['launches']
-        f['ms'] += op['ms_total']
-        f['launches'] += op['launches']
-    dom_name, dom = max(fam.items(), key=lambda kv: kv[1]['ms'])
-    avg_ms = dom['ms'] / max(1, dom['launches'])
-    flops_per_launch = dom['flops'] / max(1, dom['launches'])
-    bytes_per_launch = dom['bytes'] / max(1, dom['launches'])
-    if flops_per_launch > 0:
-        achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12
-        roof = dict(bound='mfma', achieved=round(achieved, 2), peak=FP32_PEAK_TFLOPS, unit='TFLOP/s',
-                    frac=round(achieved / FP32_PEAK_TFLOPS, 4), traffic=None)
-    else:
-        achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-        roof = dict(bound='hbm', achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit='GB/s',
-                    frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None)
-    traffic, traffic_src = pmc_traffic(dom_name)
-    roof.update(traffic=traffic, traffic_source=traffic_src, algorithmic_bytes_per_launch=bytes_per_launch,
-                kernel=dom_name, avg_launch_ms=round(avg_ms, 4), launches=dom['launches'],
-                algorithmic_per_launch=flops_per_launch if flops_per_launch > 0 else bytes_per_launch)
-    total_gpu_ms = sum(f['ms'] for f in fam.values())
-    total_flops = sum(f['flops'] for f in fam.values())
+    roof, total_gpu_ms, total_flops, fam = None, 0.0, 0.0, {}
+    if not args.no_profile:
+        roof, total_gpu_ms, total_flops, fam = roofline(prof)
 
     if rank == 0:
         images = world * B * args.steps
@@ -216,7 +227,7 @@ def main():
                         weights_gb=round(wbytes.value / 1e9, 3), workspace_gb=round(wsbytes.value / 1e9, 3)),
             roofline=roof,
             step_level=dict(model_tflops=round(total_flops / (total_gpu_ms * 1e-3) / 1e12, 2) if total_gpu_ms else None,
-                            kernel_time_frac=round(total_gpu_ms * 1e-3 / elapsed, 4)),
+                            kernel_time_frac=round(total_gpu_ms * 1e-3 / elapsed, 4) if total_gpu_ms else None),
         )
         if world == 1 and not args.no_cpu_baseline:
             line['cpu_baseline'] = cpu_baseline(sd_cpu, args.cpu_batch, args.respace_steps)

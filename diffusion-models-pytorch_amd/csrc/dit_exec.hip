@@ -59,9 +59,10 @@ struct DiTModel {
 
   struct Plan : PlanBase {
     int B = 0;
-    const float* x = nullptr;
-    const int64_t* t = nullptr;
-    const int64_t* y = nullptr;
+    // plan-owned staging of the caller's tensors (graph replay reads fixed pointers)
+    float* x = nullptr;
+    int64_t* t = nullptr;
+    int64_t* y = nullptr;  // -1 rows select the null class
     float* out = nullptr;
   };
   std::unique_ptr<Plan> plan;
@@ -170,6 +171,10 @@ int DiTModel::build_plan(int B) {
   const long M = (long)B * T;
   DM_REQUIRE((long)B * heads <= 65535, "batch * heads too large for one attention launch");
 
+  pl.x = pl.alloc((size_t)B * C * S * S * 4);
+  pl.t = (int64_t*)pl.alloc((size_t)B * 8);
+  pl.y = (int64_t*)pl.alloc((size_t)B * 8);
+  pl.out = pl.alloc((size_t)B * OC * S * S * 4);
   float* e0 = pl.alloc((size_t)B * 256 * 4);
   float* e1 = pl.alloc((size_t)B * D * 4);
   float* temb = pl.alloc((size_t)B * D * 4);
@@ -338,30 +343,41 @@ extern "C" int dm_dit_forward(dm_dit* h, const float* x, const int64_t* t, const
       return rc;
     }
   }
-  m->plan->x = x;
-  m->plan->t = t;
-  m->plan->y = y;
-  m->plan->out = out;
-  return m->plan->run((hipStream_t)stream);
+  hipStream_t st = (hipStream_t)stream;
+  auto& pl = *m->plan;
+  const int S = m->arch.input_size;
+  const size_t nx = (size_t)B * m->arch.in_channels * S * S, no = (size_t)B * m->OC * S * S;
+  DM_CHECK_HIP(hipMemcpyAsync(pl.x, x, nx * sizeof(float), hipMemcpyDeviceToDevice, st));
+  DM_CHECK_HIP(hipMemcpyAsync(pl.t, t, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+  if (y)
+    DM_CHECK_HIP(hipMemcpyAsync(pl.y, y, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+  else
+    DM_CHECK_HIP(hipMemsetAsync(pl.y, 0xff, (size_t)B * sizeof(int64_t), st));  // -1: the null class
+  const int rc = pl.run(st);
+  if (rc) return rc;
+  DM_CHECK_HIP(hipMemcpyAsync(out, pl.out, no * sizeof(float), hipMemcpyDeviceToDevice, st));
+  return DM_OK;
 }
 
 extern "C" int dm_dit_set_time_freqs(dm_dit* h, const float* freqs, int n, void* stream) {
   if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
   if (!freqs) {
     h->m->freqs_set = false;
+    if (h->m->plan) h->m->plan->invalidate_graph();
     return DM_OK;
   }
   if (n != 128) { dm::set_error("time frequency table must have 128 entries"); return DM_ERR_ARG; }
   DM_CHECK_HIP(hipMemcpyAsync(h->m->P(h->m->freqs), freqs, 128 * sizeof(float), hipMemcpyDefault,
                               (hipStream_t)stream));
   h->m->freqs_set = true;
+  if (h->m->plan) h->m->plan->invalidate_graph();
   return DM_OK;
 }
 
 extern "C" int dm_dit_profile(dm_dit* h, int enable) {
   if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
   if (!h->m->plan) { dm::set_error("no plan yet: run dm_dit_forward once first"); return DM_ERR_STATE; }
-  h->m->plan->profile_enable(enable != 0);
+  h->m->plan->profile_enable(enable);
   return DM_OK;
 }
 

@@ -2,8 +2,13 @@
 //
 // A plan is the flat list of kernel launches of one forward pass for a fixed
 // batch / resolution, built once over a cached workspace and replayed on every
-// call. Profiling records a HIP event pair around each launch on the launch
-// stream; the per-op totals are read back through the dm_*_profile_* ABI.
+// call. Every pointer a launch reads is plan-owned (the caller's input and
+// output are staged through plan buffers), so the whole list is captured once
+// into a hipGraph and replayed with one hipGraphLaunch per forward. Profiling
+// records a HIP event pair around each launch on the launch stream (on the
+// observed forwards, which run launch by launch); the per-op totals are read
+// back through the dm_*_profile_* ABI.
+#include <cstdlib>
 #pragma once
 #include <functional>
 #include <string>
@@ -27,6 +32,12 @@ struct PlanBase {
   bool alloc_failed = false;
   std::vector<Op> ops;
   bool profiling = false;
+  int profile_every = 1;  // record events on every N-th run only (the others run unobserved)
+  long runs = 0;
+  // hipGraph of the op list (captured on a private stream, launched on the caller's)
+  bool graph_enabled = std::getenv("DM_NO_GRAPH") == nullptr;
+  hipGraphExec_t gexec = nullptr;
+  hipStream_t cap_stream = nullptr;
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
   std::vector<double> prof_ms;
   std::vector<int64_t> prof_launches;
@@ -65,15 +76,52 @@ struct PlanBase {
     pending.clear();
   }
 
+  void invalidate_graph() {
+    if (gexec) (void)hipGraphExecDestroy(gexec);
+    gexec = nullptr;
+  }
+
   void release() {
     drain();
+    invalidate_graph();
+    if (cap_stream) (void)hipStreamDestroy(cap_stream);
+    cap_stream = nullptr;
     for (void* a : allocs) (void)hipFree(a);
     allocs.clear();
   }
 
+  int capture() {
+    if (!cap_stream) DM_CHECK_HIP(hipStreamCreateWithFlags(&cap_stream, hipStreamNonBlocking));
+    DM_CHECK_HIP(hipStreamBeginCapture(cap_stream, hipStreamCaptureModeThreadLocal));
+    for (auto& op : ops) {
+      const int rc = op.fn(cap_stream);
+      if (rc) {
+        hipGraph_t g = nullptr;
+        (void)hipStreamEndCapture(cap_stream, &g);
+        if (g) (void)hipGraphDestroy(g);
+        return rc;
+      }
+    }
+    hipGraph_t g = nullptr;
+    DM_CHECK_HIP(hipStreamEndCapture(cap_stream, &g));
+    const hipError_t e = hipGraphInstantiate(&gexec, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    DM_CHECK_HIP(e);
+    return DM_OK;
+  }
+
   int run(hipStream_t st) {
+    const bool observe = profiling && (runs++ % profile_every) == 0;
+    if (!observe && graph_enabled) {
+      if (!gexec) {
+        const int rc = capture();
+        if (rc) return rc;
+      }
+      DM_CHECK_HIP(hipGraphLaunch(gexec, st));
+      return DM_OK;
+    }
     for (size_t i = 0; i < ops.size(); ++i) {
-      if (profiling) {
+      if (observe) {
         hipEvent_t a, b;
         DM_CHECK_HIP(hipEventCreate(&a));
         DM_CHECK_HIP(hipEventCreate(&b));
@@ -90,9 +138,11 @@ struct PlanBase {
     return DM_OK;
   }
 
-  void profile_enable(bool on) {
+  void profile_enable(int every) {
     drain();
-    profiling = on;
+    profiling = every > 0;
+    profile_every = every > 0 ? every : 1;
+    runs = 0;
     prof_ms.assign(ops.size(), 0.0);
     prof_launches.assign(ops.size(), 0);
   }

@@ -156,9 +156,10 @@ struct UNetModel {
   // workspace cache
   struct Plan : PlanBase {
     int B = 0, H = 0, W = 0;
-    const float* x = nullptr;
-    const int64_t* t = nullptr;
-    const int64_t* y = nullptr;  // class labels or null
+    // plan-owned staging of the caller's tensors (every launch reads fixed pointers: graph replay)
+    float* x = nullptr;
+    int64_t* t = nullptr;
+    int64_t* y = nullptr;  // class labels; all -1 when the caller passes none
     float* out = nullptr;
   };
   std::unique_ptr<Plan> plan;
@@ -524,6 +525,11 @@ int UNetModel::build_plan(int B, int H, int W) {
   auto Wl = [&](int lvl) { return W >> lvl; };
   const int D = arch.dim, TD = 4 * arch.dim, G = 32, C0 = skip_C[0];
 
+  // --- staging of x / t / y / out
+  pl.x = alloc((size_t)B * arch.in_channels * H * W * 4);
+  pl.t = (int64_t*)alloc((size_t)B * 8);
+  pl.y = (int64_t*)alloc((size_t)B * 8);
+  pl.out = alloc((size_t)B * arch.out_channels * H * W * 4);
   // --- temb workspace
   float* e0 = alloc((size_t)B * D * 4);
   float* e1 = alloc((size_t)B * TD * 4);
@@ -887,11 +893,19 @@ extern "C" int dm_unet_forward(dm_unet* h, const float* x, const int64_t* t, con
       return rc;
     }
   }
-  m->plan->x = x;
-  m->plan->t = t;
-  m->plan->y = y;
-  m->plan->out = out;
-  return m->plan->run((hipStream_t)stream);
+  hipStream_t st = (hipStream_t)stream;
+  auto& pl = *m->plan;
+  const size_t nx = (size_t)B * m->arch.in_channels * H * W, no = (size_t)B * m->arch.out_channels * H * W;
+  DM_CHECK_HIP(hipMemcpyAsync(pl.x, x, nx * sizeof(float), hipMemcpyDeviceToDevice, st));
+  DM_CHECK_HIP(hipMemcpyAsync(pl.t, t, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+  if (y)
+    DM_CHECK_HIP(hipMemcpyAsync(pl.y, y, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+  else
+    DM_CHECK_HIP(hipMemsetAsync(pl.y, 0xff, (size_t)B * sizeof(int64_t), st));  // -1: no label
+  const int rc = pl.run(st);
+  if (rc) return rc;
+  DM_CHECK_HIP(hipMemcpyAsync(out, pl.out, no * sizeof(float), hipMemcpyDeviceToDevice, st));
+  return DM_OK;
 }
 
 extern "C" int dm_unet_memory(const dm_unet* h, int64_t* weight_bytes, int64_t* workspace_bytes) {
@@ -905,19 +919,21 @@ extern "C" int dm_unet_set_time_freqs(dm_unet* h, const float* freqs, int n, voi
   if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
   if (!freqs) {
     h->m->te_freqs_set = false;
+    if (h->m->plan) h->m->plan->invalidate_graph();
     return DM_OK;
   }
   if (n != h->m->arch.dim / 2) { dm::set_error("time frequency table must have dim/2 entries"); return DM_ERR_ARG; }
   DM_CHECK_HIP(hipMemcpyAsync(h->m->P(h->m->te_freqs), freqs, (size_t)n * sizeof(float), hipMemcpyDefault,
                               (hipStream_t)stream));
   h->m->te_freqs_set = true;
+  if (h->m->plan) h->m->plan->invalidate_graph();  // launches read the flag at capture time
   return DM_OK;
 }
 
 extern "C" int dm_unet_profile(dm_unet* h, int enable) {
   if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
   if (!h->m->plan) { dm::set_error("no plan yet: run dm_unet_forward once first"); return DM_ERR_STATE; }
-  h->m->plan->profile_enable(enable != 0);
+  h->m->plan->profile_enable(enable);
   return DM_OK;
 }
 

@@ -275,8 +275,9 @@ def timestep_embedding(t: torch.Tensor, dim: int, kind: int, out: torch.Tensor, 
                                        stream_handle(t.device)), 'dm_timestep_embedding')
 
 
-def unet_profile_enable(handle, enable: bool, abi: str = 'dm_unet'):
-    """Per-launch HIP-event profiling of a model's cached plan (abi: 'dm_unet' or 'dm_dit')."""
+def unet_profile_enable(handle, enable, abi: str = 'dm_unet'):
+    """Per-launch HIP-event profiling of a model's cached plan (abi: 'dm_unet' or 'dm_dit').
+    enable: False/0 off, True/1 every forward, N > 1 every N-th forward."""
     check(getattr(load(), abi + '_profile')(handle, int(enable)), abi + '_profile')
 
 

@@ -99,8 +99,10 @@ int dm_unet_forward(dm_unet* m, const float* x, const int64_t* t, const int64_t*
  * `freqs` may be host or device memory; NULL reverts to the on-device expf. */
 int dm_unet_set_time_freqs(dm_unet* m, const float* freqs, int n, void* stream);
 /* Per-launch profiling of the cached plan (HIP events recorded on the launch
- * stream around every op of dm_unet_forward while enabled). Enabling resets
- * the accumulators; dm_unet_profile_get synchronises pending events. `label`
+ * stream around every op of dm_unet_forward while enabled). enable = N > 0
+ * observes every N-th forward (the events cost a few % of throughput; sampling
+ * keeps the measured run representative), 0 disables. Enabling resets the
+ * accumulators; dm_unet_profile_get synchronises pending events. `label`
  * names the kernel family/tile (matches the rocprof kernel name), `flops` /
  * `bytes` are the op's algorithmic work per launch. */
 int dm_unet_profile(dm_unet* m, int enable);
