@@ -202,6 +202,7 @@ def main():
     dmhip.unet_profile_enable(handle, False)
 
     roof, total_gpu_ms, total_flops, fam = None, 0.0, 0.0, {}
+    observed = max((op['launches'] for op in prof), default=0)  # forwards that ran with events
     if not args.no_profile:
         roof, total_gpu_ms, total_flops, fam = roofline(prof)
 
@@ -227,7 +228,9 @@ def main():
                         weights_gb=round(wbytes.value / 1e9, 3), workspace_gb=round(wsbytes.value / 1e9, 3)),
             roofline=roof,
             step_level=dict(model_tflops=round(total_flops / (total_gpu_ms * 1e-3) / 1e12, 2) if total_gpu_ms else None,
-                            kernel_time_frac=round(total_gpu_ms * 1e-3 / elapsed, 4) if total_gpu_ms else None),
+                            # observed forwards are 1 in PROFILE_EVERY: scale their kernel time to all forwards
+                            kernel_time_frac=round(total_gpu_ms * 1e-3 * (args.steps * args.respace_steps)
+                                                   / max(1, observed) / elapsed, 4) if total_gpu_ms else None),
         )
         if world == 1 and not args.no_cpu_baseline:
             line['cpu_baseline'] = cpu_baseline(sd_cpu, args.cpu_batch, args.respace_steps)

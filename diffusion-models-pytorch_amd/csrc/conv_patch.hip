@@ -267,6 +267,22 @@ conv_patch_kernel(ConvArgs a, PatchGeom g) {
     const float rv_blk = (a.rowvec && block_one_image) ? a.rowvec[(size_t)b0 * a.rowvec_pitch + n] : 0.f;
 #pragma unroll
     for (int i = 0; i < Cfg::TM; ++i) {
+      // residual rows of this 32-row group loaded branch-free (clamped) before the stores, so the
+      // 16 loads overlap; 16 extra VGPRs keep the kernel at 2 waves / SIMD
+      float rsd[16];
+      if (a.res) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = min(m0 + wm * WM + i * 32 + acc_row(r, lh), M - 1);
+          size_t mo = m;
+          if (SUB) {
+            const int bb = m / HWo, rr = m - bb * HWo;
+            const int iy = rr / Wo, ix = rr - (rr / Wo) * Wo;
+            mo = ((size_t)bb * a.Hout + 2 * iy + py) * a.Wout + 2 * ix + px;
+          }
+          rsd[r] = a.res[mo * a.res_pitch + n];
+        }
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm * WM + i * 32 + acc_row(r, lh);
@@ -280,7 +296,7 @@ conv_patch_kernel(ConvArgs a, PatchGeom g) {
         float v = acc[i][j][r];
         if (a.bias) v = v + bn;
         if (a.rowvec) v = v + (block_one_image ? rv_blk : a.rowvec[(size_t)(m / HWo) * a.rowvec_pitch + n]);
-        if (a.res) v = v + a.res[mo * a.res_pitch + n];
+        if (a.res) v = v + rsd[r];
         a.y[mo * a.y_pitch + n] = v;
       }
     }

@@ -159,12 +159,26 @@ gemm_kernel(GemmArgs g) {
     __syncthreads();
   }
 
+  // Epilogue: residual / gate loads of a column group issued branch-free (clamped rows) before
+  // any store, so their latencies overlap.
   const int lr = lane & 31, lh = lane >> 5;
 #pragma unroll
   for (int j = 0; j < Cfg::TN; ++j) {
     const int n = n0 + wn * WN + j * 32 + lr;
+    const int nc = min(n, g.N - 1);
+    const float bn = g.bias ? g.bias[nc] : 0.f;
+    float rsd[Cfg::TM][16], gt[Cfg::TM][16];
+    if (g.res) {
+#pragma unroll
+      for (int i = 0; i < Cfg::TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = min(m0 + wm * WM + i * 32 + acc_row(r, lh), g.M - 1);
+          rsd[i][r] = g.res[(size_t)(g.res_mod > 0 ? m % g.res_mod : m) * g.ld_res + nc];
+          gt[i][r] = g.gate ? g.gate[(size_t)(m / g.gate_rows) * g.gate_pitch + nc] : 0.f;
+        }
+    }
     if (n >= g.N) continue;
-    const float bn = g.bias ? g.bias[n] : 0.f;
 #pragma unroll
     for (int i = 0; i < Cfg::TM; ++i) {
 #pragma unroll
@@ -173,10 +187,7 @@ gemm_kernel(GemmArgs g) {
         if (m >= g.M) continue;
         float v = acc[i][j][r];
         if (g.bias) v = v + bn;
-        if (g.res) {
-          const float rv = g.res[(size_t)(g.res_mod > 0 ? m % g.res_mod : m) * g.ld_res + n];
-          v = g.gate ? rv + g.gate[(size_t)(m / g.gate_rows) * g.gate_pitch + n] * v : v + rv;
-        }
+        if (g.res) v = g.gate ? rsd[i][r] + gt[i][r] * v : v + rsd[i][r];
         if (g.act == 1) v = silu_f(v);
         else if (g.act == 2) v = gelu_tanh_f(v);
         C[(size_t)m * g.ldc + n] = v;

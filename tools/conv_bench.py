@@ -1,0 +1,87 @@
+"""Microbenchmark of the dominant conv shapes of the CIFAR-10 UNet at B=256 through the C ABI.
+
+    python tools/conv_bench.py [--iters 20] [--shape NAME]
+
+Times each shape with HIP events over `iters` launches on one stream and prints
+TFLOP/s against the 157.3 TF fp32 MFMA peak. Used for kernel tuning and as the
+target of rocprofv3 PMC passes (tools/gpu_conv_pmc.sh).
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, 'diffusion-models-pytorch_amd')]
+
+import torch  # noqa: E402
+
+import dmhip  # noqa: E402
+
+# name: (B, Cin, Cout, H, pro, upsample)
+SHAPES = {
+    'res32_256': (256, 256, 256, 32, True, 0),     # up-path ResBlock conv2 at 32x32 (K = 2304)
+    'res32_128': (256, 128, 128, 32, True, 0),     # down-path ResBlock at 32x32
+    'res32_384': (256, 384, 128, 32, True, 0),     # up-path conv1 with concat input
+    'res16_256': (256, 256, 256, 16, True, 0),
+    'res8_256': (256, 256, 256, 8, True, 0),
+    'res4_256': (256, 256, 256, 4, True, 0),
+    'up16_256': (256, 256, 256, 16, False, 2),     # sub-pixel upsample 16 -> 32
+}
+
+
+def run(name, iters):
+    B, Cin, Cout, H, pro, up = SHAPES[name]
+    dev = torch.device('cuda', 0)
+    g = torch.Generator(device='cpu').manual_seed(0)
+    x = torch.randn((B, H, H, Cin), generator=g).to(dev)
+    w = (torch.randn((Cout, Cin, 3, 3), generator=g) * 0.02).to(dev)
+    if up == 2:
+        wp = torch.zeros((4, Cout, 4 * Cin), device=dev)
+        dmhip.pack_conv_weight_subpixel(w, wp)
+        wp = wp.view(4 * Cout, 4 * Cin)
+        Ho = 2 * H
+    else:
+        wp = torch.zeros((Cout, 9 * Cin), device=dev)
+        dmhip.pack_conv_weight(w, wp, 9 * Cin, 0)
+        Ho = H
+    b = torch.zeros(Cout, device=dev)
+    y = torch.empty((B, Ho, Ho, Cout), device=dev)
+    sc = torch.rand((B, Cin), device=dev) + 0.5
+    sh = torch.rand((B, Cin), device=dev) - 0.5
+    d = dmhip.ConvDesc()
+    d.x, d.x_pitch, d.Cin, d.Hin, d.Win = x.data_ptr(), Cin, Cin, H, H
+    d.taps, d.stride, d.upsample = 9, 1, up
+    d.w, d.K = wp.data_ptr(), wp.shape[1]
+    d.y, d.y_pitch, d.Cout, d.B, d.Hout, d.Wout = y.data_ptr(), Cout, Cout, B, Ho, Ho
+    d.bias = b.data_ptr()
+    if pro:
+        d.pro_scale, d.pro_shift = sc.data_ptr(), sh.data_ptr()
+    for _ in range(3):
+        dmhip.conv2d_nhwc(d, dev)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        dmhip.conv2d_nhwc(d, dev)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    flops = 2.0 * B * Ho * Ho * Cout * wp.shape[1] * (1 if up != 2 else 1)
+    if up == 2:
+        flops = 2.0 * B * H * H * 4 * Cout * 4 * Cin  # executed sub-pixel work
+    tf = flops / ms / 1e9
+    print(f'{name:12s} {ms:8.4f} ms  {tf:6.1f} TF/s  {tf / 157.3 * 100:5.1f} %', flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--iters', type=int, default=20)
+    ap.add_argument('--shape', default=None)
+    args = ap.parse_args()
+    dmhip.load()
+    for name in ([args.shape] if args.shape else SHAPES):
+        run(name, args.iters)
+
+
+if __name__ == '__main__':
+    main()
