@@ -116,7 +116,9 @@ conv_igemm_kernel(ConvArgs a) {
       iy = min(max(iy, 0), a.Hin - 1);
       ix = min(max(ix, 0), a.Win - 1);
       a_ok[i] = ok;
-      arow[i] = a.x1 + ((size_t)(r_b[i] * a.Hin + iy) * a.Win + ix) * a.x1_pitch + 4 * lc4;
+      // zero padding by address (mfma_tile.h kZeroPage); rows >= M are clamped and discarded
+      arow[i] = (ok || !r_ok[i]) ? a.x1 + ((size_t)(r_b[i] * a.Hin + iy) * a.Win + ix) * a.x1_pitch + 4 * lc4
+                                 : kZeroPage + 4 * lc4;
     }
   };
   auto set_seg2 = [&]() {
@@ -164,10 +166,10 @@ conv_igemm_kernel(ConvArgs a) {
     float* Bs = As + Cfg::A_ELEMS;
 #pragma unroll
     for (int i = 0; i < Cfg::A_ITERS; ++i)
-      *reinterpret_cast<f4*>(As + (lrow + i * Cfg::ROWS_PER_PASS) * kLDK + 4 * lc4) = ra_ok[i] ? ra[i] : zero4;
+      *reinterpret_cast<f4*>(As + (lrow + i * Cfg::ROWS_PER_PASS) * kLDK + 4 * lc4) = ra[i];
 #pragma unroll
     for (int j = 0; j < Cfg::B_ITERS; ++j)
-      *reinterpret_cast<f4*>(Bs + (lrow + j * Cfg::ROWS_PER_PASS) * kLDK + 4 * lc4) = w_ok[j] ? rb[j] : zero4;
+      *reinterpret_cast<f4*>(Bs + (lrow + j * Cfg::ROWS_PER_PASS) * kLDK + 4 * lc4) = rb[j];  // rows >= N: discarded
   };
 
   f16v acc[Cfg::TM][Cfg::TN];
@@ -258,6 +260,7 @@ int conv2d_igemm(const ConvArgs& a, hipStream_t st) {
   DM_REQUIRE(!a.upsample || (a.taps == 9 && a.stride == 1), "conv: upsample needs 3x3 stride 1");
   DM_REQUIRE(a.upsample >= 0 && a.upsample <= 2, "conv: upsample must be 0, 1 (nearest) or 2 (sub-pixel)");
   DM_REQUIRE(a.Cin1 % kBK == 0 && a.Cin2 % kBK == 0, "conv: input channels must be multiples of 32");
+  DM_REQUIRE(a.Cin1 + kBK <= kZeroPageFloats, "conv: too many input channels for the zero-padding page");
   DM_REQUIRE(a.Cin1 > 0, "conv: no input channels");
   DM_REQUIRE(a.K == (a.upsample == 2 ? 4 : a.taps) * a.Cin1 + a.Cin2, "conv: K mismatch");
   DM_REQUIRE(a.upsample != 2 || a.Cin2 == 0, "conv: sub-pixel upsample has no second segment");

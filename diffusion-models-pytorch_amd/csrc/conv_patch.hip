@@ -95,7 +95,9 @@ conv_patch_kernel(ConvArgs a, PatchGeom g) {
     const int bc = min(b, a.B - 1);
     pimg[j] = bc;
     const int iyc = min(max(iy, 0), a.Hin - 1), ixc = min(max(ix, 0), a.Win - 1);
-    psrc[j] = a.x1 + ((size_t)(bc * a.Hin + iyc) * a.Win + ixc) * a.x1_pitch + 4 * lc4;
+    // padding pixels read the zero page (PRO re-zeroes them after the transform instead)
+    psrc[j] = (ok || PRO) ? a.x1 + ((size_t)(bc * a.Hin + iyc) * a.Win + ixc) * a.x1_pitch + 4 * lc4
+                          : kZeroPage + 4 * lc4;
   }
   // ---- weight loader
   const float* wrow[Cfg::B_ITERS];
@@ -145,7 +147,8 @@ conv_patch_kernel(ConvArgs a, PatchGeom g) {
 #pragma unroll
     for (int j = 0; j < PJ; ++j) {
       const int p = lrow + 32 * j;
-      if (j * 32 < MAXP && p < MAXP) *reinterpret_cast<f4*>(patch + p * kLDK + 4 * lc4) = pok[j] ? rp[j] : zero4;
+      if (j * 32 < MAXP && p < MAXP)
+        *reinterpret_cast<f4*>(patch + p * kLDK + 4 * lc4) = (!PRO || pok[j]) ? rp[j] : zero4;
     }
   };
   auto load_w = [&](int kt) {
@@ -156,7 +159,7 @@ conv_patch_kernel(ConvArgs a, PatchGeom g) {
     float* Bs = wbuf + buf * WSTAGE;
 #pragma unroll
     for (int j = 0; j < Cfg::B_ITERS; ++j)
-      *reinterpret_cast<f4*>(Bs + (lrow + j * Cfg::ROWS_PER_PASS) * kLDK + 4 * lc4) = w_ok[j] ? rb[j] : zero4;
+      *reinterpret_cast<f4*>(Bs + (lrow + j * Cfg::ROWS_PER_PASS) * kLDK + 4 * lc4) = rb[j];  // rows >= N: discarded
   };
 
   f16v acc[Cfg::TM][Cfg::TN];
@@ -249,7 +252,7 @@ conv_patch_kernel(ConvArgs a, PatchGeom g) {
       load_w((k2base + c2) / kBK);
 #pragma unroll
       for (int i = 0; i < Cfg::A_ITERS; ++i)
-        *reinterpret_cast<f4*>(As + (lrow + i * Cfg::ROWS_PER_PASS) * kLDK + 4 * lc4) = rok[i] ? ra[i] : zero4;
+        *reinterpret_cast<f4*>(As + (lrow + i * Cfg::ROWS_PER_PASS) * kLDK + 4 * lc4) = ra[i];  // rows >= M: discarded
       store_w(0);
       __syncthreads();
       mfma_slice<Cfg::TM, Cfg::TN>(As, wbuf, wm * WM, wn * WN, lane, acc);

@@ -76,6 +76,8 @@ gemm_kernel(GemmArgs g) {
   bool kn_ok[B_KN ? KN_ITERS : 1];
   int ld_k = 0;
 
+  // K tail: B reads the zero page (mfma_tile.h kZeroPage) so those products vanish; A reads a
+  // clamped, finite column. Rows >= M / columns >= N read clamped data and are never stored.
   auto load_tile = [&](int kt) {
     const int k = kt * kBK + 4 * lc4;
     k_ok = k < g.K;
@@ -85,15 +87,16 @@ gemm_kernel(GemmArgs g) {
     for (int i = 0; i < Cfg::A_ITERS; ++i) ra[i] = *reinterpret_cast<const f4*>(arow[i] + kofs);
     if constexpr (!B_KN) {
 #pragma unroll
-      for (int j = 0; j < Cfg::B_ITERS; ++j) rb[j] = *reinterpret_cast<const f4*>(brow[j] + kofs);
+      for (int j = 0; j < Cfg::B_ITERS; ++j)
+        rb[j] = *reinterpret_cast<const f4*>(k_ok ? brow[j] + kofs : kZeroPage);
     } else {
       const int n4 = t % KN_C4, kr = t / KN_C4;
       const int n = min(n0 + 4 * n4, g.N - 4);
 #pragma unroll
       for (int j = 0; j < KN_ITERS; ++j) {
         const int kk = kt * kBK + kr + j * KN_ROWS_PER_PASS;
-        kn_ok[j] = (kr + j * KN_ROWS_PER_PASS < kBK) && kk < g.K && n0 + 4 * n4 < g.N;
-        rb[j] = *reinterpret_cast<const f4*>(Bm + (size_t)min(kk, g.K - 1) * g.ldb + n);
+        kn_ok[j] = (kr + j * KN_ROWS_PER_PASS < kBK);
+        rb[j] = *reinterpret_cast<const f4*>(kk < g.K ? Bm + (size_t)kk * g.ldb + n : kZeroPage);
       }
     }
   };
@@ -117,20 +120,20 @@ gemm_kernel(GemmArgs g) {
         for (int q = 0; q < 4; ++q) v[q] = ((v[q] - a_ln[i].x) * a_ln[i].y) * (1.0f + sc[q]) + sh[q];
       }
       if (g.alpha != 1.0f) v = v * g.alpha;
-      *reinterpret_cast<f4*>(As + (lrow + i * Cfg::ROWS_PER_PASS) * kLDK + 4 * lc4) = (a_ok[i] && k_ok) ? v : zero4;
+      *reinterpret_cast<f4*>(As + (lrow + i * Cfg::ROWS_PER_PASS) * kLDK + 4 * lc4) = v;
     }
     if constexpr (!B_KN) {
 #pragma unroll
       for (int j = 0; j < Cfg::B_ITERS; ++j)
         *reinterpret_cast<f4*>(Bs + (lrow + j * Cfg::ROWS_PER_PASS) * kLDK + 4 * lc4) =
-            (b_ok[j] && k_ok) ? (g.b_scale != 0.0f && g.b_scale != 1.0f ? rb[j] * g.b_scale : rb[j]) : zero4;
+            (g.b_scale != 0.0f && g.b_scale != 1.0f) ? rb[j] * g.b_scale : rb[j];
     } else {
       const int n4 = t % KN_C4, kr = t / KN_C4;
 #pragma unroll
       for (int j = 0; j < KN_ITERS; ++j) {
         const int kk = kr + j * KN_ROWS_PER_PASS;
-        if (kk < kBK) {
-          const f4 v = kn_ok[j] ? rb[j] : zero4;
+        if (kn_ok[j]) {
+          const f4 v = rb[j];
 #pragma unroll
           for (int q = 0; q < 4; ++q) Bs[(4 * n4 + q) * kLDK + kk] = v[q];
         }

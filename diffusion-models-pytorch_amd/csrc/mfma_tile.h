@@ -23,6 +23,16 @@
 namespace dm {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
+
+// Zero padding by ADDRESS instead of by select: an out-of-range operand row
+// (conv zero padding, K tail) loads from this all-zero buffer, so the loaded
+// registers go to LDS unmodified. A select on loaded data lets the compiler
+// hoist it next to the load and drain vmcnt(0) in front of the MFMAs of the
+// current slice (observed in the ISA); an address select costs nothing there.
+// Rows beyond M / columns beyond N read clamped, valid data instead: their
+// results are never stored. One copy per translation unit (static), never written.
+constexpr int kZeroPageFloats = 16384;
+static __device__ __attribute__((aligned(16))) float kZeroPage[kZeroPageFloats];
 typedef float f16v __attribute__((ext_vector_type(16)));
 
 constexpr int kBK = 32;
