@@ -37,7 +37,7 @@ __device__ __forceinline__ int xcd_remap_p(int bid, int nblk) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
-template <int BM, int BN, int WM, int WN, int MODE, int MAXP, bool PRO>
+template <int BM, int BN, int WM, int WN, int MODE, int MAXP, bool PRO, bool KSPLIT = false>
 __global__ void __launch_bounds__(256)
 conv_patch_kernel(ConvArgs a, PatchGeom g) {
   using Cfg = TileCfg<BM, BN, WM, WN>;
@@ -55,6 +55,13 @@ conv_patch_kernel(ConvArgs a, PatchGeom g) {
   const int N = a.Cout;
   const int nN = ceil_div(N, BN);
   int bid = xcd_remap_p(blockIdx.x, gridDim.x);
+  const int ksplit = KSPLIT ? a.ksplit : 1;
+  int split = 0;
+  if (KSPLIT) {
+    const int per_split = gridDim.x / ksplit;
+    split = bid / per_split;
+    bid -= split * per_split;
+  }
   int par = 0;
   if (SUB) {
     const int per_par = ceil_div(M, BM) * nN;
@@ -205,14 +212,16 @@ conv_patch_kernel(ConvArgs a, PatchGeom g) {
   };
 
   const int nchunks = a.Cin1 / kBK;
-  load_patch(0);
-  load_w(0);
-  if (PRO) transform(0, 0, PJ);
+  const int c_begin = KSPLIT ? split * nchunks / ksplit : 0;
+  const int c_end = KSPLIT ? (split + 1) * nchunks / ksplit : nchunks;
+  load_patch(c_begin);
+  load_w(c_begin * NTAP);
+  if (PRO) transform(c_begin, 0, PJ);
   store_patch();
-  store_w(0);
+  store_w((c_begin * NTAP) & 1);
   __syncthreads();
-  for (int c = 0; c < nchunks; ++c) {
-    const bool more_chunks = c + 1 < nchunks;
+  for (int c = c_begin; c < c_end; ++c) {
+    const bool more_chunks = c + 1 < c_end;
 #pragma unroll
     for (int tap = 0; tap < NTAP; ++tap) {
       const int kt = c * NTAP + tap;
@@ -236,8 +245,8 @@ conv_patch_kernel(ConvArgs a, PatchGeom g) {
     }
   }
 
-  // ---- segment 2: 1x1 product of x2 (ResBlock shortcut), K = Cin2, un-pipelined.
-  if (a.Cin2 > 0) {
+  // ---- segment 2: 1x1 product of x2 (ResBlock shortcut), K = Cin2, un-pipelined (last split).
+  if (a.Cin2 > 0 && (!KSPLIT || split == ksplit - 1)) {
     const int k2base = 9 * a.Cin1;
     float* As = patch;  // BM x kLDK fits in the patch region (P >= BM for the stride-1 geometry)
     for (int c2 = 0; c2 < a.Cin2; c2 += kBK) {
@@ -258,6 +267,23 @@ conv_patch_kernel(ConvArgs a, PatchGeom g) {
       mfma_slice<Cfg::TM, Cfg::TN>(As, wbuf, wm * WM, wn * WN, lane, acc);
       __syncthreads();
     }
+  }
+
+  // ---- split-K: raw partial sums, epilogue in conv_splitk_reduce
+  if (KSPLIT) {
+#pragma unroll
+    for (int j = 0; j < Cfg::TN; ++j) {
+      const int n = n0 + wn * WN + j * 32 + lr;
+      if (n >= N) continue;
+#pragma unroll
+      for (int i = 0; i < Cfg::TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * WM + i * 32 + acc_row(r, lh);
+          if (m < M) a.kpart[((size_t)split * M + m) * N + n] = acc[i][j][r];
+        }
+    }
+    return;
   }
 
   // ---- epilogue (as conv.hip); SUB rows scatter to output pixel (2iy + py, 2ix + px)
@@ -306,8 +332,34 @@ conv_patch_kernel(ConvArgs a, PatchGeom g) {
   }
 }
 
+// Split-K reduction: y = sum_s kpart[s] (split order) + bias + rowvec + residual.
+__global__ void conv_splitk_reduce_kernel(ConvArgs a) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int N = a.Cout;
+  const long M = (long)a.B * a.Hout * a.Wout;
+  if (e >= M * N) return;
+  const long m = e / N;
+  const int n = e - m * N;
+  float v = a.kpart[e];
+  for (int s = 1; s < a.ksplit; ++s) v = v + a.kpart[(size_t)s * M * N + e];
+  if (a.bias) v = v + a.bias[n];
+  if (a.rowvec) v = v + a.rowvec[(size_t)(m / ((long)a.Hout * a.Wout)) * a.rowvec_pitch + n];
+  if (a.res) v = v + a.res[(size_t)m * a.res_pitch + n];
+  a.y[(size_t)m * a.y_pitch + n] = v;
+}
+
 template <int BM, int BN, int WM, int WN, int MODE, int MAXP>
 void launch_patch_mode(const ConvArgs& a, const PatchGeom& g, int blocks, hipStream_t st) {
+  // split-K variants only for MODE 0 (small maps); the unsplit kernels keep their register budget
+  if (MODE == 0 && a.ksplit > 1) {
+    if (a.pro_scale)
+      hipLaunchKernelGGL((conv_patch_kernel<BM, BN, WM, WN, 0, MAXP, true, true>), dim3(blocks), dim3(256), 0, st,
+                         a, g);
+    else
+      hipLaunchKernelGGL((conv_patch_kernel<BM, BN, WM, WN, 0, MAXP, false, true>), dim3(blocks), dim3(256), 0, st,
+                         a, g);
+    return;
+  }
   if (a.pro_scale)
     hipLaunchKernelGGL((conv_patch_kernel<BM, BN, WM, WN, MODE, MAXP, true>), dim3(blocks), dim3(256), 0, st, a, g);
   else
@@ -318,7 +370,10 @@ template <int BM, int BN, int WM, int WN, int MAXP>
 int launch_patch(const ConvArgs& a, const PatchGeom& g, hipStream_t st) {
   const bool sub = a.upsample == 2;
   const int M = sub ? a.B * a.Hin * a.Win : a.B * a.Hout * a.Wout;
-  const int blocks = ceil_div(M, BM) * ceil_div(a.Cout, BN) * (sub ? 4 : 1);
+  const int ks = a.ksplit > 1 ? a.ksplit : 1;
+  DM_REQUIRE(ks == 1 || (!a.upsample && a.kpart && ks <= a.Cin1 / kBK),
+             "conv: split-K needs a stride-1 3x3 conv, a workspace and at most one split per channel chunk");
+  const int blocks = ceil_div(M, BM) * ceil_div(a.Cout, BN) * (sub ? 4 : 1) * ks;
   if (sub)
     launch_patch_mode<BM, BN, WM, WN, 2, MAXP>(a, g, blocks, st);
   else if (a.upsample)
@@ -326,6 +381,11 @@ int launch_patch(const ConvArgs& a, const PatchGeom& g, hipStream_t st) {
   else
     launch_patch_mode<BM, BN, WM, WN, 0, MAXP>(a, g, blocks, st);
   DM_LAUNCH_CHECK();
+  if (ks > 1) {
+    const long total = (long)M * a.Cout;
+    hipLaunchKernelGGL(conv_splitk_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, a);
+    DM_LAUNCH_CHECK();
+  }
   return DM_OK;
 }
 

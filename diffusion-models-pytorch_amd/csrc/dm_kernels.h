@@ -34,6 +34,11 @@ struct ConvArgs {
   // (GroupNorm + SiLU of the ResBlock, fused into the conv's input load)
   const float* pro_scale;
   const float* pro_shift;
+  // split-K over input-channel chunks (halo-patch kernel, MODE 0/1): ksplit > 1 writes raw partial
+  // sums to kpart [ksplit][M][Cout] and a reduction pass sums them in split order and applies the
+  // epilogue. The split count is fixed per layer shape (not per batch), so results stay batch-invariant.
+  int ksplit;
+  float* kpart;
 };
 
 // Output tile = TB images x TH rows x full width; input patch PH x PW per image.

@@ -601,7 +601,25 @@ int UNetModel::build_plan(int B, int H, int W) {
     fl = 2.0 * Z * g.M * g.N * g.K;
     by = 4.0 * Z * ((double)g.M * g.K + (double)g.N * g.K + (double)g.M * g.N) + (g.res ? 4.0 * g.M * g.N : 0.0);
   };
-  auto add_conv = [&](const ConvArgs& c) {
+  // Split-K for convs on maps of <= 16 pixels (e.g. the 4x4 level at CIFAR size): without it a
+  // B=256 launch has only 256 tiles for 256 CUs. The split depends on the layer shape only, never on
+  // B, so every image's result is the same at any batch size.
+  float* kpart_ws = nullptr;
+  size_t kpart_floats = 0;
+  auto maybe_split = [&](ConvArgs& c) {
+    if (c.upsample == 2 || c.Hout * c.Wout > 16 || conv_pick(c) < 3) return;
+    const int ks = std::min(4, c.Cin1 / 32);
+    if (ks < 2) return;
+    const size_t need = (size_t)ks * c.B * c.Hout * c.Wout * c.Cout;
+    if (need > kpart_floats) {
+      kpart_ws = alloc(need * 4);
+      kpart_floats = need;
+    }
+    c.ksplit = ks;
+    c.kpart = kpart_ws;
+  };
+  auto add_conv = [&](ConvArgs c) {
+    maybe_split(c);
     double fl, by;
     conv_cost(c, fl, by);
     add(conv_label(c), fl, by, [=](hipStream_t st) { return conv2d_igemm(c, st); });
