@@ -143,10 +143,17 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    # DM_DIST_BACKEND=gloo rehearses the N > 1 path with several ranks on one GPU (host-side gather);
+    # the measured configuration is nccl (RCCL over xGMI), one rank per GPU.
+    backend = os.environ.get('DM_DIST_BACKEND', 'nccl')
+    gpu = local_rank % max(1, torch.cuda.device_count())
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
-    dev = torch.device('cuda', local_rank)
+        torch.cuda.set_device(gpu)
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', gpu))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device('cuda', gpu)
 
     import dmhip
     from dmhip._lib import check as _check
@@ -169,7 +176,12 @@ def main():
         noise = torch.randn((B, 3, 32, 32), device=dev, generator=gen)
         x = diffuser.sample(model, noise, tqdm_kwargs=dict(disable=True)).clamp(-1, 1)
         if world > 1:
-            dist.all_gather_into_tensor(gathered, x)
+            if backend == 'nccl':
+                dist.all_gather_into_tensor(gathered, x)
+            else:
+                parts = [torch.empty((B, 3, 32, 32)) for _ in range(world)]
+                dist.all_gather(parts, x.cpu())
+                gathered.copy_(torch.cat(parts))
             return gathered
         return x
 
@@ -193,7 +205,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        tt = torch.tensor([elapsed], device=dev if backend == 'nccl' else 'cpu', dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = tt.item()
     prof = dmhip.unet_profile_read(handle)

@@ -1,0 +1,53 @@
+"""Microbenchmark of the GEMM kernel on the attention shapes of the CIFAR-10 UNet (B=256, 16x16, C=256).
+
+    python tools/gemm_bench.py
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, 'diffusion-models-pytorch_amd')]
+
+import torch  # noqa: E402
+
+import dmhip  # noqa: E402
+
+
+def bench(name, M, N, K, Z1=1, Z2=1, b_kn=0, res=False, iters=20):
+    dev = torch.device('cuda', 0)
+    A = torch.randn((Z1 * Z2, M, K), device=dev)
+    B = torch.randn((Z1 * Z2, K, N) if b_kn else (Z1 * Z2, N, K), device=dev)
+    C = torch.empty((Z1 * Z2, M, N), device=dev)
+    R = torch.randn((M, N), device=dev) if res else None
+    d = dmhip.GemmDesc()
+    d.M, d.N, d.K, d.Z1, d.Z2 = M, N, K, Z1, Z2
+    d.A, d.a_s1, d.a_s2, d.lda = A.data_ptr(), Z2 * M * K, M * K, K
+    d.B, d.b_s1, d.b_s2, d.ldb, d.b_kn = B.data_ptr(), Z2 * K * N, K * N, (N if b_kn else K), b_kn
+    d.C, d.c_s1, d.c_s2, d.ldc = C.data_ptr(), Z2 * M * N, M * N, N
+    d.alpha = 1.0
+    if res:
+        d.res, d.ld_res = R.data_ptr(), N
+    for _ in range(3):
+        dmhip.gemm(d, dev)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        dmhip.gemm(d, dev)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    tf = 2.0 * Z1 * Z2 * M * N * K / ms / 1e9
+    print(f'{name:16s} {ms:8.4f} ms {tf:6.1f} TF/s', flush=True)
+
+
+if __name__ == '__main__':
+    dmhip.load()
+    bench('qkv_k256', 65536, 768, 256)
+    bench('qkv_k512', 65536, 768, 512)
+    bench('qkv_k1024', 65536, 768, 1024)
+    bench('proj_res', 65536, 256, 256, res=True)
+    bench('proj_nores', 65536, 256, 256)
+    bench('S', 256, 256, 256, Z1=256)
+    bench('PV_kn', 256, 256, 256, Z1=256, b_kn=1)
+    bench('big_4096', 4096, 4096, 4096, iters=5)
