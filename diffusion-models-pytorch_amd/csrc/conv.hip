@@ -281,6 +281,8 @@ int conv2d_igemm(const ConvArgs& a, hipStream_t st) {
   DM_REQUIRE(a.tile >= 0 && a.tile <= 6, "conv: tile must be 0..6");
   const int mode = conv_mode(a);
   const int pick = conv_pick(a);
+  DM_REQUIRE(!a.gn_part || conv_can_emit_gn(a), "conv: GroupNorm statistics need a 128-row halo-patch tile, "
+                                                 "whole 64-pixel chunks and groups within 32 channels");
   DM_REQUIRE(!a.pro_scale || (pick >= 3 && a.pro_shift && aligned16(a.pro_scale) && aligned16(a.pro_shift)),
              "conv: the GroupNorm prologue needs a halo-patch shape (3x3 stride 1 / upsample, whole-row tiles)");
   if (pick >= 3) {
@@ -315,6 +317,15 @@ int conv_pick(const ConvArgs& a) {
   const long b128x64 = ((M + 127) / 128) * ((a.Cout + 63) / 64);
   if (b128x64 >= 512) return 1;
   return 2;
+}
+
+bool conv_can_emit_gn(const ConvArgs& a) {
+  const int pick = conv_pick(a);
+  if (pick != 3 && pick != 4) return false;  // 128-row patch tiles: every wave owns 64 rows
+  if (a.upsample || (a.ksplit > 1)) return false;
+  if ((a.Hout * a.Wout) % 64 != 0 || a.gn_G <= 0 || a.Cout % a.gn_G != 0) return false;
+  const int cpg = a.Cout / a.gn_G;
+  return 32 % cpg == 0;
 }
 
 // The exact kernel instantiation (matches the rocprofv3 kernel name with spaces removed).

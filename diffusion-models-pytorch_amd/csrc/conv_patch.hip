@@ -288,10 +288,15 @@ conv_patch_kernel(ConvArgs a, PatchGeom g) {
 
   // ---- epilogue (as conv.hip); SUB rows scatter to output pixel (2iy + py, 2ix + px)
   const bool block_one_image = (HWo % BM) == 0;
+  // GroupNorm statistics of the stored values (MODE 0, WM = 64: this wave's rows are one chunk)
+  const bool emit = MODE == 0 && WM == 64 && a.gn_part != nullptr;
+  const int wrow0 = m0 + wm * WM;
 #pragma unroll
   for (int j = 0; j < Cfg::TN; ++j) {
-    const int n = n0 + wn * WN + j * 32 + lr;
-    if (n >= N) continue;
+    const int n_raw = n0 + wn * WN + j * 32 + lr;
+    const bool n_ok = n_raw < N;
+    const int n = n_ok ? n_raw : N - 1;
+    double gs = 0.0, gq = 0.0;
     const float bn = a.bias ? a.bias[n] : 0.f;
     const float rv_blk = (a.rowvec && block_one_image) ? a.rowvec[(size_t)b0 * a.rowvec_pitch + n] : 0.f;
 #pragma unroll
@@ -326,8 +331,19 @@ conv_patch_kernel(ConvArgs a, PatchGeom g) {
         if (a.bias) v = v + bn;
         if (a.rowvec) v = v + (block_one_image ? rv_blk : a.rowvec[(size_t)(m / HWo) * a.rowvec_pitch + n]);
         if (a.res) v = v + rsd[r];
-        a.y[mo * a.y_pitch + n] = v;
+        if (n_ok) a.y[mo * a.y_pitch + n] = v;
+        if (emit) {
+          gs += (double)v;
+          gq += (double)v * v;
+        }
       }
+    }
+    if (emit) {
+      const int cpg = N / a.gn_G;
+      const int nchunk = (HWo + 63) / 64;
+      const int bb = wrow0 / HWo, ch = (wrow0 - bb * HWo) / 64;
+      gn_emit_group(gs, gq, lr, lh, cpg, n_ok && wrow0 < M,
+                    a.gn_part + ((size_t)bb * nchunk + ch) * a.gn_G + n_raw / cpg);
     }
   }
 }

@@ -39,6 +39,12 @@ struct ConvArgs {
   // epilogue. The split count is fixed per layer shape (not per batch), so results stay batch-invariant.
   int ksplit;
   float* kpart;
+  // optional GroupNorm statistics of the stored output for the consumer's GroupNorm(G) over this
+  // view's Cout channels (cpg = Cout / G): per (image, 64-pixel chunk, group) {sum, sum of squares}
+  // in the gn_partial layout [B][nchunk][G], so the consumer skips its gn_partial pass.
+  // Used when HW % 64 == 0 and the tile's waves own 64 rows (halo-patch MODE 0, 128-row tiles).
+  double2* gn_part;
+  int gn_G;
 };
 
 // Output tile = TB images x TH rows x full width; input patch PH x PW per image.
@@ -80,6 +86,10 @@ struct GemmArgs {
   const float* gate;
   int gate_pitch, gate_rows;
   int res_mod;          // > 0: residual row = m % res_mod (broadcast table, e.g. DiT pos_embed)
+  // optional GroupNorm statistics of the output (as ConvArgs::gn_part): rows = pixels of images of
+  // gn_hw pixels each (gn_hw % 64 == 0), 128-row tiles, Z1 = Z2 = 1
+  double2* gn_part;
+  int gn_G, gn_hw;
 };
 
 struct StepArgs {
@@ -130,6 +140,8 @@ int gn_apply(const View& x, int G, const double2* part, int nchunk, float eps, c
              const View& y, hipStream_t st);
 int conv2d_igemm(const ConvArgs& a, hipStream_t st);
 int conv_pick(const ConvArgs& a);
+// whether the conv can emit GroupNorm(gn_G) statistics of its output from the epilogue
+bool conv_can_emit_gn(const ConvArgs& a);
 bool conv_patch_geom(const ConvArgs& a, int BM, PatchGeom& g);
 int conv_patch_pick(const ConvArgs& a, PatchGeom& g);
 int conv2d_patch(const ConvArgs& a, int which, const PatchGeom& g, hipStream_t st);

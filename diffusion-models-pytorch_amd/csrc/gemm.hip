@@ -165,10 +165,13 @@ gemm_kernel(GemmArgs g) {
   // Epilogue: residual / gate loads of a column group issued branch-free (clamped rows) before
   // any store, so their latencies overlap.
   const int lr = lane & 31, lh = lane >> 5;
+  const bool emit = WM == 64 && g.gn_part != nullptr;
+  const int wrow0 = m0 + wm * WM;
 #pragma unroll
   for (int j = 0; j < Cfg::TN; ++j) {
     const int n = n0 + wn * WN + j * 32 + lr;
     const int nc = min(n, g.N - 1);
+    double gs = 0.0, gq = 0.0;
     const float bn = g.bias ? g.bias[nc] : 0.f;
     float rsd[Cfg::TM][16], gt[Cfg::TM][16];
     if (g.res) {
@@ -181,7 +184,6 @@ gemm_kernel(GemmArgs g) {
           gt[i][r] = g.gate ? g.gate[(size_t)(m / g.gate_rows) * g.gate_pitch + nc] : 0.f;
         }
     }
-    if (n >= g.N) continue;
 #pragma unroll
     for (int i = 0; i < Cfg::TM; ++i) {
 #pragma unroll
@@ -193,8 +195,19 @@ gemm_kernel(GemmArgs g) {
         if (g.res) v = g.gate ? rsd[i][r] + gt[i][r] * v : v + rsd[i][r];
         if (g.act == 1) v = silu_f(v);
         else if (g.act == 2) v = gelu_tanh_f(v);
-        C[(size_t)m * g.ldc + n] = v;
+        if (n < g.N) C[(size_t)m * g.ldc + n] = v;
+        if (emit) {
+          gs += (double)v;
+          gq += (double)v * v;
+        }
       }
+    }
+    if (emit) {
+      const int cpg = g.N / g.gn_G;
+      const int nchunk = (g.gn_hw + 63) / 64;
+      const int bb = wrow0 / g.gn_hw, ch = (wrow0 - bb * g.gn_hw) / 64;
+      gn_emit_group(gs, gq, lr, lh, cpg, n < g.N && wrow0 < g.M,
+                    g.gn_part + ((size_t)bb * nchunk + ch) * g.gn_G + n / cpg);
     }
   }
 }
@@ -226,6 +239,9 @@ int gemm_batched(const GemmArgs& g, hipStream_t st) {
                              g.Z1 == 1 && g.Z2 == 1),
              "gemm: LayerNorm-modulate prologue needs stats, scale/shift tables and rows per image");
   DM_REQUIRE(!g.gate || (g.res && g.gate_rows > 0), "gemm: gated residual needs the residual and rows per image");
+  DM_REQUIRE(!g.gn_part || (gemm_pick(g) == 0 && g.Z1 == 1 && g.Z2 == 1 && g.gn_hw % 64 == 0 && g.gn_G > 0 &&
+                            g.N % g.gn_G == 0 && 32 % (g.N / g.gn_G) == 0),
+             "gemm: GroupNorm statistics need 128-row tiles, whole 64-pixel chunks and groups within 32 columns");
   if (gemm_pick(g) == 0) return launch_gemm<128, 128, 64, 64>(g, st);
   return launch_gemm<64, 64, 32, 32>(g, st);
 }

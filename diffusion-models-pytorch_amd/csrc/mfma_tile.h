@@ -32,6 +32,21 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 // Rows beyond M / columns beyond N read clamped, valid data instead: their
 // results are never stored. One copy per translation unit (static), never written.
 constexpr int kZeroPageFloats = 16384;
+
+// GroupNorm statistics from an MFMA epilogue. A wave owns 64 consecutive output rows (one
+// 64-pixel chunk of one image when HW % 64 == 0) and, per 32-column group j, lane (lr, lh) holds
+// column n = ... + lr summed over its rows. Combine the two half-waves (lh), then the cpg lanes of
+// each GroupNorm group, and let the group's first lane store {sum, sumsq}. All 64 lanes must call.
+__device__ __forceinline__ void gn_emit_group(double s, double q, int lr, int lh, int cpg, bool store,
+                                              double2* dst) {
+  s += __shfl_xor(s, 32);
+  q += __shfl_xor(q, 32);
+  for (int o = 1; o < cpg; o <<= 1) {
+    s += __shfl_xor(s, o);
+    q += __shfl_xor(q, o);
+  }
+  if (store && lh == 0 && (lr % cpg) == 0) *dst = make_double2(s, q);
+}
 static __device__ __attribute__((aligned(16))) float kZeroPage[kZeroPageFloats];
 typedef float f16v __attribute__((ext_vector_type(16)));
 

@@ -607,7 +607,7 @@ int UNetModel::build_plan(int B, int H, int W) {
   float* kpart_ws = nullptr;
   size_t kpart_floats = 0;
   auto maybe_split = [&](ConvArgs& c) {
-    if (c.upsample == 2 || c.Hout * c.Wout > 16 || conv_pick(c) < 3) return;
+    if (c.gn_part || c.upsample == 2 || c.Hout * c.Wout > 16 || conv_pick(c) < 3) return;
     const int ks = std::min(4, c.Cin1 / 32);
     if (ks < 2) return;
     const size_t need = (size_t)ks * c.B * c.Hout * c.Wout * c.Cout;
@@ -676,6 +676,44 @@ int UNetModel::build_plan(int B, int H, int W) {
     if (nx < (int)nodes.size() && nodes[nx].kind == N_RES && nodes[nx].pops_skip >= 0) return concat_x[nx];
     float* buf = alloc((size_t)B * Hl(lvl) * Wl(lvl) * C * 4);
     return View{buf, B, Hl(lvl), Wl(lvl), C, C};
+  };
+
+  // GroupNorm statistics emitted by producers (conv / GEMM epilogues): view pointer -> partials.
+  // A consumer whose input view has them skips its gn_partial pass; every other write to a view
+  // drops its entry.
+  std::map<const float*, std::pair<double2*, int>> gn_ready;
+  std::map<const float*, double2*> gn_bufs;
+  auto gn_buf_for = [&](const View& v) -> double2* {
+    auto it = gn_bufs.find(v.p);
+    if (it != gn_bufs.end()) return it->second;
+    double2* b = (double2*)alloc((size_t)B * gn_num_chunks(v.H * v.W) * G * sizeof(double2));
+    gn_bufs[v.p] = b;
+    return b;
+  };
+  auto emit_conv = [&](ConvArgs& c, const View& v) {
+    gn_ready.erase(v.p);
+    c.gn_part = gn_buf_for(v);
+    c.gn_G = G;
+    if (!conv_can_emit_gn(c)) {
+      c.gn_part = nullptr;
+      return;
+    }
+    gn_ready[v.p] = {c.gn_part, v.C};
+  };
+  auto emit_gemm = [&](GemmArgs& g, const View& v) {
+    gn_ready.erase(v.p);
+    const int hw = v.H * v.W, cpg = v.C / G;
+    if (gemm_pick(g) != 0 || hw % 64 != 0 || v.C % G != 0 || 32 % cpg != 0) return;
+    g.gn_part = gn_buf_for(v);
+    g.gn_G = G;
+    g.gn_hw = hw;
+    gn_ready[v.p] = {g.gn_part, v.C};
+  };
+  auto gn_stats = [&](const View& v) -> const double2* {
+    auto it = gn_ready.find(v.p);
+    if (it != gn_ready.end() && it->second.second == v.C) return it->second.first;
+    add("gn_partial", 0, gn_bytes(v, false), [=](hipStream_t st) { return gn_partial(v, G, part, st); });
+    return part;
   };
 
   // first conv -> skip 0
@@ -747,11 +785,11 @@ int UNetModel::build_plan(int B, int H, int W) {
       const float* ms = r.adagn ? projs + r.proj_col : nullptr;
       const float* mb = r.adagn ? projs + r.proj_col + r.cout : nullptr;
       const int mp = r.adagn ? proj_total : 0;
-      add("gn_partial", 0, gn_bytes(xin, false), [=](hipStream_t st) { return gn_partial(xin, G, part, st); });
+      const double2* st1 = gn_stats(xin);
       if (r.updown && !fuse1) {
         // normalise + SiLU + resample into a1, then a plain conv at the output resolution
         add("gn_finalize", 0, 8.0 * B * r.cin, [=](hipStream_t st) {
-          return gn_finalize(xin, G, part, 1e-5f, self->P(r.gn1.g), self->P(r.gn1.b), gsc, gsh, st);
+          return gn_finalize(xin, G, st1, 1e-5f, self->P(r.gn1.g), self->P(r.gn1.b), gsc, gsh, st);
         });
         const bool down = r.updown == 2;
         add("resample2x", 0, 4.0 * B * ((double)Hi * Wi + (double)Ho * Wo) * r.cin,
@@ -761,38 +799,40 @@ int UNetModel::build_plan(int B, int H, int W) {
       } else if (fuse1) {
         // GroupNorm + SiLU folded into conv1's patch load: x read once, normalised tensor never stored
         add("gn_finalize", 0, 8.0 * B * r.cin, [=](hipStream_t st) {
-          return gn_finalize(xin, G, part, 1e-5f, self->P(r.gn1.g), self->P(r.gn1.b), gsc, gsh, st);
+          return gn_finalize(xin, G, st1, 1e-5f, self->P(r.gn1.g), self->P(r.gn1.b), gsc, gsh, st);
         });
         c1.x1 = xin.p; c1.x1_pitch = xin.pitch;
         c1.pro_scale = gsc; c1.pro_shift = gsh;
       } else {
         add("gn_apply", 0, gn_bytes(xin, true), [=](hipStream_t st) {
-          return gn_apply(xin, G, part, nchunk, 1e-5f, self->P(r.gn1.g), self->P(r.gn1.b), nullptr, nullptr, 0, 1,
+          return gn_apply(xin, G, st1, nchunk, 1e-5f, self->P(r.gn1.g), self->P(r.gn1.b), nullptr, nullptr, 0, 1,
                           va1, st);
         });
         c1.x1 = a1;
       }
+      emit_conv(c1, vh);
       add_conv(c1);
-      add("gn_partial", 0, gn_bytes(vh, false), [=](hipStream_t st) { return gn_partial(vh, G, part, st); });
+      const double2* st2 = gn_stats(vh);
       if (fuse2) {
         add("gn_finalize", 0, 8.0 * B * r.cout, [=](hipStream_t st) {
-          return gn_finalize(vh, G, part, 1e-5f, self->P(r.gn2.g), self->P(r.gn2.b), gsc, gsh, st, ms, mb, mp);
+          return gn_finalize(vh, G, st2, 1e-5f, self->P(r.gn2.g), self->P(r.gn2.b), gsc, gsh, st, ms, mb, mp);
         });
         c2.x1 = hbuf;
         c2.pro_scale = gsc; c2.pro_shift = gsh;
       } else {
         add("gn_apply", 0, gn_bytes(vh, true), [=](hipStream_t st) {
-          return gn_apply(vh, G, part, nchunk_o, 1e-5f, self->P(r.gn2.g), self->P(r.gn2.b), ms, mb, mp, 1, va2, st);
+          return gn_apply(vh, G, st2, nchunk_o, 1e-5f, self->P(r.gn2.g), self->P(r.gn2.b), ms, mb, mp, 1, va2, st);
         });
       }
+      emit_conv(c2, y);
       add_conv(c2);
     } else if (n.kind == N_ATTN) {
       const AttnP p = attn[n.idx];
       const int C = p.C, heads = p.heads, Dh = C / heads;
       // GroupNorm folded into the QKV projection's A load (modules.py:91-94): one pass over x
-      add("gn_partial", 0, gn_bytes(xin, false), [=](hipStream_t st) { return gn_partial(xin, G, part, st); });
+      const double2* sta = gn_stats(xin);
       add("gn_finalize", 0, 8.0 * B * C, [=](hipStream_t st) {
-        return gn_finalize(xin, G, part, 1e-5f, self->P(p.gn.g), self->P(p.gn.b), gsc, gsh, st);
+        return gn_finalize(xin, G, sta, 1e-5f, self->P(p.gn.g), self->P(p.gn.b), gsc, gsh, st);
       });
       GemmArgs gq{};
       gq.M = B * hw; gq.N = 3 * C; gq.K = C; gq.Z1 = 1; gq.Z2 = 1;
@@ -825,10 +865,12 @@ int UNetModel::build_plan(int B, int H, int W) {
       gp.M = B * hw; gp.N = C; gp.K = C; gp.Z1 = 1; gp.Z2 = 1;
       gp.A = Ob; gp.lda = C; gp.Bm = P(p.wproj); gp.ldb = C; gp.C = y.p; gp.ldc = y.pitch;
       gp.alpha = 1.f; gp.bias = P(p.bproj); gp.res = xin.p; gp.ld_res = xin.pitch;
+      emit_gemm(gp, y);
       add_gemm(gp);
     } else if (n.idx < 0) {
       // resampling without a conv (adm/unet.py:126-128 nearest-2x, :153-155 avg-pool)
       const bool down = n.kind == N_DOWN;
+      gn_ready.erase(y.p);
       add("resample2x", 0, 4.0 * B * ((double)Hi * Wi + (double)y.H * y.W) * n.cin,
           [=](hipStream_t st) { return resample2x(xin, y, down, nullptr, nullptr, st); });
     } else {
@@ -845,6 +887,7 @@ int UNetModel::build_plan(int B, int H, int W) {
         s.upsample = 2; s.w = P(cv.w_sub); s.K = 4 * c.Cin1;
         if (conv_pick(s) >= 3) c = s;
       }
+      gn_ready.erase(y.p);
       add_conv(c);
     }
     x_cur = y;
@@ -859,9 +902,9 @@ int UNetModel::build_plan(int B, int H, int W) {
     const float* lw = P(last_w);
     const float* lb = P(last_b);
     const int oc = arch.out_channels;
-    add("gn_partial", 0, gn_bytes(xin, false), [=](hipStream_t st) { return gn_partial(xin, G, part, st); });
+    const double2* stl = gn_stats(xin);
     add("gn_finalize", 0, 8.0 * B * C, [=](hipStream_t st) {
-      return gn_finalize(xin, G, part, 1e-5f, self->P(lg.g), self->P(lg.b), gsc, gsh, st);
+      return gn_finalize(xin, G, stl, 1e-5f, self->P(lg.g), self->P(lg.b), gsc, gsh, st);
     });
     (void)va;
     (void)nchunk;
