@@ -11,7 +11,8 @@ from typing import Optional
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-lib_path = os.path.join(_HERE, 'libdm_hip.so')
+# DM_HIP_LIB: an alternative build of the same library (kernel-tuning experiments only)
+lib_path = os.environ.get('DM_HIP_LIB') or os.path.join(_HERE, 'libdm_hip.so')
 _HEADER = os.path.join(os.path.dirname(os.path.dirname(_HERE)), 'include', 'dm_hip.h')
 
 DM_OK = 0
