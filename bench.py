@@ -14,8 +14,11 @@ all ranks / that time.
 
 Roofline: HIP events around every launch of the forward during the timed
 region (dm_unet_profile) give each kernel family's average launch duration;
-the dominant family (most GPU time) is reported against the fp32 MFMA peak
-with its algorithmic FLOPs per launch.
+the dominant family (most GPU time) is reported with its algorithmic (fp32)
+FLOPs per launch against the peak of the instructions it issues: the fp32 MFMA
+peak (157.3 TF) for the fp32 kernels; for the split-bf16 kernels, which issue
+each fp32 product as 6 bf16 piece products, the dense bf16 MFMA peak / 6
+(2500 / 6 = 416.7 TF of fp32-equivalent work).
 
 CPU baseline: the oracle (a torch-CPU restatement of the reference path,
 bit-equal to it at equal thread count) timed on this host's cores, rank 0 /
@@ -40,6 +43,8 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = 'images/sec at DDIM-50, CIFAR-10 UNet 32×32, bs=256; 1/2/4/8 GPU'
 FP32_PEAK_TFLOPS = 157.3   # MI355X dense fp32 (MFMA f32 = vector rate), MI355X_MICROARCH.md
+BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (no sparsity), MI355X_MICROARCH.md
+SPLIT_PRODUCTS = 6         # split-bf16 kernels: one fp32 product = 6 bf16 piece products (conv_patch3.hip)
 HBM_PEAK_GBS = 8000.0
 PROFILE_EVERY = 10   # per-launch events cost ~5 % when on every launch; 1 forward in 10 is observed
 
@@ -123,8 +128,14 @@ def roofline(prof):
     bytes_per_launch = dom['bytes'] / max(1, dom['launches'])
     if flops_per_launch > 0:
         achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12
-        roof = dict(bound='mfma', achieved=round(achieved, 2), peak=FP32_PEAK_TFLOPS, unit='TFLOP/s',
-                    frac=round(achieved / FP32_PEAK_TFLOPS, 4), traffic=None)
+        split = dom_name.startswith('conv_patch3_kernel')
+        peak = round(BF16_PEAK_TFLOPS / SPLIT_PRODUCTS, 1) if split else FP32_PEAK_TFLOPS
+        roof = dict(bound='mfma', achieved=round(achieved, 2), peak=peak, unit='TFLOP/s',
+                    frac=round(achieved / peak, 4), traffic=None)
+        if split:
+            roof['peak_basis'] = (f'fp32-equivalent: dense bf16 MFMA {BF16_PEAK_TFLOPS:.0f} TF / {SPLIT_PRODUCTS} '
+                                  f'piece products per fp32 product; issued bf16 rate '
+                                  f'{achieved * SPLIT_PRODUCTS:.1f} TF')
     else:
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
         roof = dict(bound='hbm', achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit='GB/s',

@@ -91,7 +91,19 @@ extern "C" int dm_conv2d_nhwc(const dm_conv_desc* d, void* stream) {
   a.tile = d->tile;
   a.pro_scale = d->pro_scale;
   a.pro_shift = d->pro_shift;
+  a.ws = d->w_split;
   return dm::conv2d_igemm(a, (hipStream_t)stream);
+}
+
+extern "C" int64_t dm_conv_weight_split_bytes(int nmat, int Cout, int K) {
+  if (nmat <= 0 || Cout <= 0 || K <= 0 || K % 16 != 0) return 0;
+  return (int64_t)dm::split_conv_weights_elems(nmat, Cout, K) * 2;
+}
+
+extern "C" int dm_pack_conv_weight_split(const float* w, int nmat, int Cout, int K, int Cin, int taps, void* out,
+                                         void* stream) {
+  if (!w || !out) { dm::set_error("null tensor"); return DM_ERR_ARG; }
+  return dm::split_conv_weights(w, nmat, Cout, K, Cin, taps, out, (hipStream_t)stream);
 }
 
 extern "C" int dm_pack_conv_weight_subpixel(const float* w, int Cout, int Cin, float* out, void* stream) {

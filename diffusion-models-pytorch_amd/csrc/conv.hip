@@ -288,6 +288,7 @@ int conv2d_igemm(const ConvArgs& a, hipStream_t st) {
   if (pick >= 3) {
     PatchGeom g;
     conv_patch_pick(a, g);
+    if (conv_patch3_ok(a, pick + 1, g)) return conv2d_patch3(a, pick + 1, g, st);
     return conv2d_patch(a, pick + 1, g, st);
   }
   DM_REQUIRE(a.upsample != 2, "conv: the sub-pixel upsample runs on the halo-patch kernel only (shape has no "
@@ -335,10 +336,15 @@ std::string conv_label(const ConvArgs& a) {
                                 "conv_patch_kernel<128,64,64,32",   "conv_patch_kernel<64,64,32,32"};
   const int p = conv_pick(a);
   std::string s = names[p];
-  if (p >= 3) {  // <BM,BN,WM,WN,MODE,MAXP,PRO>; MAXP 288 for 128-row tiles, 160 for 64-row tiles
+  if (p >= 3) {  // <BM,BN,WM,WN,MODE,MAXP,PRO>; MAXP 288 (208 split-bf16) for 128-row tiles, 160 for 64-row
+    PatchGeom g;
+    conv_patch_pick(a, g);
+    const bool x3 = conv_patch3_ok(a, p + 1, g);
+    if (x3) s.replace(0, 17, "conv_patch3_kernel");
     s += "," + std::to_string(a.upsample);
-    s += p == 5 ? ",160" : ",288";
-    s += a.pro_scale ? ",true>" : ",false>";
+    s += p == 5 ? ",160" : (x3 ? ",208" : ",288");
+    s += a.pro_scale ? ",true" : ",false";
+    s += a.ksplit > 1 ? ",true>" : ">";
   }
   return s;
 }

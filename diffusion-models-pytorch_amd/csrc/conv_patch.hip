@@ -26,16 +26,11 @@
 #include "dm_common.h"
 #include "dm_kernels.h"
 #include "mfma_tile.h"
+#include "conv_epilogue.h"
 
 namespace dm {
 
 namespace {
-
-__device__ __forceinline__ int xcd_remap_p(int bid, int nblk) {
-  const int q = nblk >> 3, r = nblk & 7;
-  const int xcd = bid & 7, idx = bid >> 3;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
-}
 
 template <int BM, int BN, int WM, int WN, int MODE, int MAXP, bool PRO, bool KSPLIT = false>
 __global__ void __launch_bounds__(256)
@@ -269,83 +264,7 @@ conv_patch_kernel(ConvArgs a, PatchGeom g) {
     }
   }
 
-  // ---- split-K: raw partial sums, epilogue in conv_splitk_reduce
-  if (KSPLIT) {
-#pragma unroll
-    for (int j = 0; j < Cfg::TN; ++j) {
-      const int n = n0 + wn * WN + j * 32 + lr;
-      if (n >= N) continue;
-#pragma unroll
-      for (int i = 0; i < Cfg::TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = m0 + wm * WM + i * 32 + acc_row(r, lh);
-          if (m < M) a.kpart[((size_t)split * M + m) * N + n] = acc[i][j][r];
-        }
-    }
-    return;
-  }
-
-  // ---- epilogue (as conv.hip); SUB rows scatter to output pixel (2iy + py, 2ix + px)
-  const bool block_one_image = (HWo % BM) == 0;
-  // GroupNorm statistics of the stored values (MODE 0, WM = 64: this wave's rows are one chunk)
-  const bool emit = MODE == 0 && WM == 64 && a.gn_part != nullptr;
-  const int wrow0 = m0 + wm * WM;
-#pragma unroll
-  for (int j = 0; j < Cfg::TN; ++j) {
-    const int n_raw = n0 + wn * WN + j * 32 + lr;
-    const bool n_ok = n_raw < N;
-    const int n = n_ok ? n_raw : N - 1;
-    double gs = 0.0, gq = 0.0;
-    const float bn = a.bias ? a.bias[n] : 0.f;
-    const float rv_blk = (a.rowvec && block_one_image) ? a.rowvec[(size_t)b0 * a.rowvec_pitch + n] : 0.f;
-#pragma unroll
-    for (int i = 0; i < Cfg::TM; ++i) {
-      // residual rows of this 32-row group loaded branch-free (clamped) before the stores, so the
-      // 16 loads overlap; 16 extra VGPRs keep the kernel at 2 waves / SIMD
-      float rsd[16];
-      if (a.res) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = min(m0 + wm * WM + i * 32 + acc_row(r, lh), M - 1);
-          size_t mo = m;
-          if (SUB) {
-            const int bb = m / HWo, rr = m - bb * HWo;
-            const int iy = rr / Wo, ix = rr - (rr / Wo) * Wo;
-            mo = ((size_t)bb * a.Hout + 2 * iy + py) * a.Wout + 2 * ix + px;
-          }
-          rsd[r] = a.res[mo * a.res_pitch + n];
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * WM + i * 32 + acc_row(r, lh);
-        if (m >= M) continue;
-        size_t mo = m;
-        if (SUB) {
-          const int bb = m / HWo, rr = m - bb * HWo;
-          const int iy = rr / Wo, ix = rr - (rr / Wo) * Wo;
-          mo = ((size_t)bb * a.Hout + 2 * iy + py) * a.Wout + 2 * ix + px;
-        }
-        float v = acc[i][j][r];
-        if (a.bias) v = v + bn;
-        if (a.rowvec) v = v + (block_one_image ? rv_blk : a.rowvec[(size_t)(m / HWo) * a.rowvec_pitch + n]);
-        if (a.res) v = v + rsd[r];
-        if (n_ok) a.y[mo * a.y_pitch + n] = v;
-        if (emit) {
-          gs += (double)v;
-          gq += (double)v * v;
-        }
-      }
-    }
-    if (emit) {
-      const int cpg = N / a.gn_G;
-      const int nchunk = (HWo + 63) / 64;
-      const int bb = wrow0 / HWo, ch = (wrow0 - bb * HWo) / 64;
-      gn_emit_group(gs, gq, lr, lh, cpg, n_ok && wrow0 < M,
-                    a.gn_part + ((size_t)bb * nchunk + ch) * a.gn_G + n_raw / cpg);
-    }
-  }
+  conv_patch_epilogue<BM, BN, WM, WN, MODE, KSPLIT>(a, acc, M, HWo, Wo, m0, n0, b0, wm, wn, lr, lh, split, py, px);
 }
 
 // Split-K reduction: y = sum_s kpart[s] (split order) + bias + rowvec + residual.
@@ -363,6 +282,17 @@ __global__ void conv_splitk_reduce_kernel(ConvArgs a) {
   if (a.res) v = v + a.res[(size_t)m * a.res_pitch + n];
   a.y[(size_t)m * a.y_pitch + n] = v;
 }
+
+}  // namespace
+
+int conv_splitk_reduce(const ConvArgs& a, hipStream_t st) {
+  const long total = (long)a.B * a.Hout * a.Wout * a.Cout;
+  hipLaunchKernelGGL(conv_splitk_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, a);
+  DM_LAUNCH_CHECK();
+  return DM_OK;
+}
+
+namespace {
 
 template <int BM, int BN, int WM, int WN, int MODE, int MAXP>
 void launch_patch_mode(const ConvArgs& a, const PatchGeom& g, int blocks, hipStream_t st) {
@@ -399,8 +329,8 @@ int launch_patch(const ConvArgs& a, const PatchGeom& g, hipStream_t st) {
   DM_LAUNCH_CHECK();
   if (ks > 1) {
     const long total = (long)M * a.Cout;
-    hipLaunchKernelGGL(conv_splitk_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, a);
-    DM_LAUNCH_CHECK();
+    (void)total;
+    return conv_splitk_reduce(a, st);
   }
   return DM_OK;
 }
@@ -438,24 +368,33 @@ bool conv_patch_geom(const ConvArgs& a, int BM, PatchGeom& g) {
   return true;
 }
 
-constexpr int kPatchMax128 = 288;
-constexpr int kPatchMax64 = 160;
 
 int conv_patch_pick(const ConvArgs& a, PatchGeom& g) {
+  // the split-bf16 kernel's LDS image holds fewer patch pixels at 128-row tiles
+  const int max128 = a.ws ? kPatch3Max128 : kPatchMax128, max64 = a.ws ? kPatch3Max64 : kPatchMax64;
   if (a.tile == 4 || a.tile == 0) {
     const long M = (long)a.B * a.Hout * a.Wout;
     const long b128 = ((M + 127) / 128) * ((a.Cout + 127) / 128);
     const long b128x64 = ((M + 127) / 128) * ((a.Cout + 63) / 64);
-    if ((a.tile == 4 || (a.Cout >= 128 && b128 >= 512)) && conv_patch_geom(a, 128, g) && g.P <= kPatchMax128)
+    if ((a.tile == 4 || (a.Cout >= 128 && b128 >= 512)) && conv_patch_geom(a, 128, g) && g.P <= max128)
       return 4;
-    if (a.tile == 0 && b128x64 >= 512 && conv_patch_geom(a, 128, g) && g.P <= kPatchMax128) return 5;
-    if (a.tile == 0 && conv_patch_geom(a, 64, g) && g.P <= kPatchMax64) return 6;
+    if (a.tile == 0 && b128x64 >= 512 && conv_patch_geom(a, 128, g) && g.P <= max128) return 5;
+    if (a.tile == 0 && conv_patch_geom(a, 64, g) && g.P <= max64) return 6;
   } else if (a.tile == 5) {
-    if (conv_patch_geom(a, 128, g) && g.P <= kPatchMax128) return 5;
+    if (conv_patch_geom(a, 128, g) && g.P <= max128) return 5;
   } else if (a.tile == 6) {
-    if (conv_patch_geom(a, 64, g) && g.P <= kPatchMax64) return 6;
+    if (conv_patch_geom(a, 64, g) && g.P <= max64) return 6;
   }
   return 0;
+}
+
+// Whether a conv can run on the split-bf16 kernel at every batch size: the 64-row tile (the
+// picker's last resort) must fit, which depends on the layer shape only, so the fp32 / split choice
+// of a layer never changes with B and results stay batch-invariant.
+bool conv_split_eligible(const ConvArgs& a) {
+  if (a.taps != 9 || a.stride != 1 || a.upsample == 1 || a.Cin1 % 16 != 0 || a.Cin2 % 16 != 0) return false;
+  PatchGeom g;
+  return conv_patch_geom(a, 64, g) && g.P <= kPatch3Max64;
 }
 
 int conv2d_patch(const ConvArgs& a, int which, const PatchGeom& g, hipStream_t st) {

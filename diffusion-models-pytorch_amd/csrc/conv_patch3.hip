@@ -1,0 +1,430 @@
+// 3x3 convolution (stride 1, nearest-2x upsample, sub-pixel upsample) on the
+// halo-patch tiling of conv_patch.hip, with the products computed by the
+// bf16 matrix cores on a three-way split of every fp32 operand.
+//
+// Numerics (models/unet.py:16,26 — the reference convolves in fp32):
+// an fp32 value x is split exactly as x = x0 + x1 + x2 with
+// x0 = bf16(x), x1 = bf16(x - x0), x2 = bf16(x - x0 - x1) (round to nearest
+// even; both subtractions are exact), which carries the full 24-bit
+// significand. A product a*w is then the sum of the nine piece products; the
+// six with combined weight >= 2^-16 relative are issued
+//   a2w0 + a1w1 + a0w2 + a1w0 + a0w1 + a0w0   (smallest first)
+// as v_mfma_f32_32x32x16_bf16 into one fp32 accumulator. Each bf16 x bf16
+// piece product is exact in fp32; the three dropped ones are below
+// 2^-25 |a w| — under half an fp32 ulp of the product. The contraction
+// therefore keeps fp32 accuracy (errors of the same size as the fp32 MFMA
+// path's, tests/test_gpu_conv_split.py) while the six 32x32x16 bf16
+// MFMAs (6 x 32 cycles) replace eight 32x32x2 fp32 MFMAs (8 x 64 cycles) per
+// 16-deep k step: 2.7x fewer matrix-core cycles.
+//
+// Layout: K advances in 16-deep slices. A slice row (one pixel, or one output
+// channel) is 2 lane groups x 3 pieces x 8 bf16 = 96 B, stored with a 112 B
+// pitch (7 x 16 B: an odd number of 16-B slots keeps the ds_read_b128 lane
+// groups conflict-free). Lane (lr, lh) of a 32x32x16 MFMA reads, per piece,
+// the 16 B at row lr, group lh: k = 8 lh + j of the slice for both operands.
+// The weights are split once at plan build (split_conv_weights) into
+// [matrix][slice][Cout][48] bf16; the input patch is split when it is staged
+// in LDS (after the fused GroupNorm + SiLU prologue), once per 16-channel
+// chunk, and read by all 9 (or 4) taps from there. The patch is double
+// buffered, so one barrier per tap suffices. LDS per 128x128 block:
+// 2 x 208 x 112 + 2 x 128 x 112 = 73.5 KiB -> two blocks per CU.
+#include "dm_common.h"
+#include "dm_kernels.h"
+#include "mfma_tile.h"
+#include "conv_epilogue.h"
+
+namespace dm {
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+
+constexpr int kSK = 16;      // K per slice = channels per patch chunk
+constexpr int kSRow = 48;    // bf16 per slice row: 2 lane groups x 3 pieces x 8
+constexpr int kSPitch = 56;  // LDS row pitch in bf16 (112 B)
+
+// Exact three-way split of 8 fp32 values into bf16 pieces (hi, mid, lo).
+__device__ __forceinline__ void split3(const f4 lo4, const f4 hi4, bf16x8 (&p)[3]) {
+  const float x[8] = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const __bf16 b0 = (__bf16)x[e];
+    const float r1 = x[e] - (float)b0;
+    const __bf16 b1 = (__bf16)r1;
+    const float r2 = r1 - (float)b1;
+    p[0][e] = b0;
+    p[1][e] = b1;
+    p[2][e] = (__bf16)r2;
+  }
+}
+
+__device__ __forceinline__ void mfma6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f16v& acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
+}
+
+template <int BM, int BN, int WM, int WN, int MODE, int MAXP, bool PRO, bool KSPLIT = false>
+__global__ void __launch_bounds__(256)
+conv_patch3_kernel(ConvArgs a, PatchGeom g) {
+  constexpr int NWN = BN / WN;
+  constexpr int TM = WM / 32, TN = WN / 32;
+  static_assert((BM / WM) * NWN == 4, "4 waves per block");
+  constexpr bool UP = MODE == 1, SUB = MODE == 2;
+  constexpr int NTAP = SUB ? 4 : 9;
+  constexpr int PATCH = MAXP * kSPitch;
+  constexpr int WSTAGE = BN * kSPitch;
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * PATCH + 2 * WSTAGE];
+  __bf16* const patch = lds;
+  __bf16* const wbuf = lds + 2 * PATCH;
+
+  const int Ho = SUB ? a.Hin : a.Hout, Wo = SUB ? a.Win : a.Wout;
+  const int M = a.B * Ho * Wo;
+  const int N = a.Cout;
+  const int nN = ceil_div(N, BN);
+  int bid = xcd_remap_p(blockIdx.x, gridDim.x);
+  const int ksplit = KSPLIT ? a.ksplit : 1;
+  int split = 0;
+  if (KSPLIT) {
+    const int per_split = gridDim.x / ksplit;
+    split = bid / per_split;
+    bid -= split * per_split;
+  }
+  int par = 0;
+  if (SUB) {
+    const int per_par = ceil_div(M, BM) * nN;
+    par = bid / per_par;
+    bid -= par * per_par;
+  }
+  const int py = par >> 1, px = par & 1;
+  const int mt = bid / nN, nt = bid - (bid / nN) * nN;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int HWo = Ho * Wo;
+  const int b0 = m0 / HWo;
+  const int y0 = (m0 - b0 * HWo) / Wo;
+
+  const int t = threadIdx.x;
+  const int lane = t & 63, wave = t >> 6;
+  const int wm = wave / NWN, wn = wave % NWN;
+  const int lr = lane & 31, lh = lane >> 5;
+  // staging: two threads per pixel / row, 8 channels each
+  const int srow = t >> 1, shalf = t & 1;
+
+  // ---- patch loader geometry (pixel p = srow + 128 j)
+  constexpr int PJ = (MAXP + 127) / 128;
+  const int PHW = g.PH * g.PW;
+  const float* psrc[PJ];
+  bool pok[PJ];
+  int pimg[PJ];
+  const int iy_base = UP ? (y0 >> 1) - 1 : y0 - 1;
+#pragma unroll
+  for (int j = 0; j < PJ; ++j) {
+    const int p = srow + 128 * j;
+    const int img = p / PHW;
+    const int rem = p - img * PHW;
+    const int pr = rem / g.PW, pc = rem - (rem / g.PW) * g.PW;
+    const int b = b0 + img;
+    const int iy = iy_base + pr, ix = pc - 1;
+    const bool ok = p < g.P && b < a.B && iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
+    pok[j] = ok;
+    const int bc = min(b, a.B - 1);
+    pimg[j] = bc;
+    const int iyc = min(max(iy, 0), a.Hin - 1), ixc = min(max(ix, 0), a.Win - 1);
+    psrc[j] = (ok || PRO) ? a.x1 + ((size_t)(bc * a.Hin + iyc) * a.Win + ixc) * a.x1_pitch + 8 * shalf
+                          : kZeroPage + 8 * shalf;
+  }
+  // ---- weight loader: BN rows x 6 16-B pieces per slice
+  constexpr int WPIECES = BN * 6;
+  constexpr int WI = (WPIECES + 255) / 256;
+  const int nslices = a.K / kSK;
+  const size_t slice_stride = (size_t)N * kSRow;  // bf16 per slice of one weight matrix
+  const __bf16* wsrc[WI];
+  int wdst[WI];
+  bool wvalid[WI];
+#pragma unroll
+  for (int j = 0; j < WI; ++j) {
+    const int piece = t + 256 * j;
+    wvalid[j] = piece < WPIECES;
+    const int row = wvalid[j] ? piece / 6 : 0, col = piece - (piece / 6) * 6;
+    const int n = min(n0 + row, N - 1);
+    wsrc[j] = reinterpret_cast<const __bf16*>(a.ws) + (size_t)par * nslices * slice_stride + (size_t)n * kSRow +
+              col * 8;
+    wdst[j] = row * kSPitch + col * 8;
+  }
+
+  // ---- A-fragment patch coordinates of this lane's rows
+  int fy[TM], fx[TM], fimg[TM];
+  const int tile_rows = g.TH * Wo;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int ml = wm * WM + i * 32 + lr;
+    fimg[i] = ml / tile_rows;
+    const int rem = ml - fimg[i] * tile_rows;
+    fy[i] = rem / Wo;
+    fx[i] = rem - fy[i] * Wo;
+  }
+
+  f4 rp[PJ][2];
+  u4 rw[WI];
+  auto load_patch = [&](int chunk) {
+    const int co = chunk * kSK;
+#pragma unroll
+    for (int j = 0; j < PJ; ++j) {
+      rp[j][0] = *reinterpret_cast<const f4*>(psrc[j] + co);
+      rp[j][1] = *reinterpret_cast<const f4*>(psrc[j] + co + 4);
+    }
+  };
+  // GroupNorm + SiLU prologue on patch registers j in [j0, j1): silu(x * scale[b][c] + shift[b][c])
+  auto transform = [&](int chunk, int j0, int j1) {
+    const int cc = chunk * kSK + 8 * shalf;
+#pragma unroll
+    for (int j = 0; j < PJ; ++j) {
+      if (j >= j0 && j < j1) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f4 sc = *reinterpret_cast<const f4*>(a.pro_scale + (size_t)pimg[j] * a.Cin1 + cc + 4 * h);
+          const f4 sh = *reinterpret_cast<const f4*>(a.pro_shift + (size_t)pimg[j] * a.Cin1 + cc + 4 * h);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) rp[j][h][q] = silu_fast(rp[j][h][q] * sc[q] + sh[q]);
+        }
+      }
+    }
+  };
+  // split + store (padding stays exactly 0: applied after the transform)
+  auto store_patch = [&](int buf) {
+    __bf16* dst = patch + buf * PATCH;
+    const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < PJ; ++j) {
+      const int p = srow + 128 * j;
+      if (j * 128 < MAXP && p < MAXP) {
+        bf16x8 pc[3];
+        const bool z = PRO && !pok[j];
+        split3(z ? zero4 : rp[j][0], z ? zero4 : rp[j][1], pc);
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          *reinterpret_cast<bf16x8*>(dst + p * kSPitch + shalf * 24 + q * 8) = pc[q];
+      }
+    }
+  };
+  auto load_w = [&](int kt) {
+#pragma unroll
+    for (int j = 0; j < WI; ++j) rw[j] = *reinterpret_cast<const u4*>(wsrc[j] + (size_t)kt * slice_stride);
+  };
+  auto store_w = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < WI; ++j)
+      if (wvalid[j]) *reinterpret_cast<u4*>(wbuf + buf * WSTAGE + wdst[j]) = rw[j];
+  };
+
+  f16v acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // one 16-deep K slice: A rows at LDS offsets abase[i] (+ lane group), B rows from wbuf[buf]
+  auto compute = [&](const __bf16* As, const int (&abase)[TM], int buf) {
+    const __bf16* Bs = wbuf + buf * WSTAGE + (wn * WN + lr) * kSPitch + lh * 24;
+    bf16x8 av[TM][3], bv[TN][3];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) av[i][q] = *reinterpret_cast<const bf16x8*>(As + abase[i] + q * 8);
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        bv[j][q] = *reinterpret_cast<const bf16x8*>(Bs + j * 32 * kSPitch + q * 8);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) mfma6(av[i], bv[j], acc[i][j]);
+  };
+  auto compute_tap = [&](int ky, int kx, int pbuf, int wb) {
+    int abase[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      int pr, pc;
+      if (UP) {
+        pr = ((fy[i] + ky - 1) >> 1) + 1;
+        pc = ((fx[i] + kx - 1) >> 1) + 1;
+      } else {
+        pr = fy[i] + ky;
+        pc = fx[i] + kx;
+      }
+      abase[i] = ((fimg[i] * g.PH + pr) * g.PW + pc) * kSPitch + lh * 24;
+    }
+    compute(patch + pbuf * PATCH, abase, wb);
+  };
+
+  const int nchunks = a.Cin1 / kSK;
+  const int c_begin = KSPLIT ? split * nchunks / ksplit : 0;
+  const int c_end = KSPLIT ? (split + 1) * nchunks / ksplit : nchunks;
+  load_patch(c_begin);
+  load_w(c_begin * NTAP);
+  if (PRO) transform(c_begin, 0, PJ);
+  store_patch(c_begin & 1);
+  store_w((c_begin * NTAP) & 1);
+  __syncthreads();
+  for (int c = c_begin; c < c_end; ++c) {
+    const bool more_chunks = c + 1 < c_end;
+#pragma unroll
+    for (int tap = 0; tap < NTAP; ++tap) {
+      const int kt = c * NTAP + tap;
+      const bool more_w = (tap < NTAP - 1) || more_chunks;
+      if (more_w) load_w(kt + 1);
+      if (tap == 0 && more_chunks) load_patch(c + 1);
+      if (PRO && tap >= 1 && more_chunks) {
+        constexpr int per = (PJ + NTAP - 2) / (NTAP - 1);
+        transform(c + 1, (tap - 1) * per, tap == NTAP - 1 ? PJ : tap * per);
+      }
+      if (SUB)
+        compute_tap(py + (tap >> 1), px + (tap & 1), c & 1, kt & 1);
+      else
+        compute_tap(tap / 3, tap % 3, c & 1, kt & 1);
+      if (more_w) store_w((kt + 1) & 1);
+      if (tap == NTAP - 1 && more_chunks) store_patch((c + 1) & 1);
+      __syncthreads();
+    }
+  }
+
+  // ---- segment 2: 1x1 product of x2 (ResBlock shortcut), K = Cin2, un-pipelined (last split).
+  if (a.Cin2 > 0 && (!KSPLIT || split == ksplit - 1)) {
+    const int s2base = NTAP * a.Cin1 / kSK;
+    int abase[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) abase[i] = (wm * WM + i * 32 + lr) * kSPitch + lh * 24;
+    const bool arow_ok = srow < BM;
+    const int m = min(m0 + srow, M - 1);
+    const float* xsrc = a.x2 + (size_t)m * a.x2_pitch + 8 * shalf;
+    for (int c2 = 0; c2 < a.Cin2; c2 += kSK) {
+      const f4 r0 = *reinterpret_cast<const f4*>(xsrc + c2);
+      const f4 r1 = *reinterpret_cast<const f4*>(xsrc + c2 + 4);
+      load_w(s2base + c2 / kSK);
+      if (arow_ok) {  // rows >= M hold clamped data: never stored
+        bf16x8 pc[3];
+        split3(r0, r1, pc);
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          *reinterpret_cast<bf16x8*>(patch + srow * kSPitch + shalf * 24 + q * 8) = pc[q];
+      }
+      store_w(0);
+      __syncthreads();
+      compute(patch, abase, 0);
+      __syncthreads();
+    }
+  }
+
+  conv_patch_epilogue<BM, BN, WM, WN, MODE, KSPLIT>(a, acc, M, HWo, Wo, m0, n0, b0, wm, wn, lr, lh, split, py, px);
+}
+
+template <int BM, int BN, int WM, int WN, int MODE, int MAXP>
+void launch3_mode(const ConvArgs& a, const PatchGeom& g, int blocks, hipStream_t st) {
+  if (MODE == 0 && a.ksplit > 1) {
+    if (a.pro_scale)
+      hipLaunchKernelGGL((conv_patch3_kernel<BM, BN, WM, WN, 0, MAXP, true, true>), dim3(blocks), dim3(256), 0, st,
+                         a, g);
+    else
+      hipLaunchKernelGGL((conv_patch3_kernel<BM, BN, WM, WN, 0, MAXP, false, true>), dim3(blocks), dim3(256), 0,
+                         st, a, g);
+    return;
+  }
+  if (a.pro_scale)
+    hipLaunchKernelGGL((conv_patch3_kernel<BM, BN, WM, WN, MODE, MAXP, true>), dim3(blocks), dim3(256), 0, st, a, g);
+  else
+    hipLaunchKernelGGL((conv_patch3_kernel<BM, BN, WM, WN, MODE, MAXP, false>), dim3(blocks), dim3(256), 0, st, a,
+                       g);
+}
+
+template <int BM, int BN, int WM, int WN, int MAXP>
+int launch3(const ConvArgs& a, const PatchGeom& g, hipStream_t st) {
+  const bool sub = a.upsample == 2;
+  const int M = sub ? a.B * a.Hin * a.Win : a.B * a.Hout * a.Wout;
+  const int ks = a.ksplit > 1 ? a.ksplit : 1;
+  DM_REQUIRE(ks == 1 || (!a.upsample && a.kpart && ks <= a.Cin1 / kSK),
+             "conv: split-K needs a stride-1 3x3 conv, a workspace and at most one split per channel chunk");
+  DM_REQUIRE(g.P <= MAXP, "conv: patch larger than the split-bf16 kernel's LDS image");
+  const int blocks = ceil_div(M, BM) * ceil_div(a.Cout, BN) * (sub ? 4 : 1) * ks;
+  if (sub)
+    launch3_mode<BM, BN, WM, WN, 2, MAXP>(a, g, blocks, st);
+  else if (a.upsample)
+    launch3_mode<BM, BN, WM, WN, 1, MAXP>(a, g, blocks, st);
+  else
+    launch3_mode<BM, BN, WM, WN, 0, MAXP>(a, g, blocks, st);
+  DM_LAUNCH_CHECK();
+  if (ks > 1) return conv_splitk_reduce(a, st);
+  return DM_OK;
+}
+
+// [nmat][rows][K] fp32 packed conv weights (chunk-major over 32-channel chunks for the first
+// ntap * cin1 columns, then the 1x1 segment) -> [nmat][K / 16][rows][48] bf16 split slices in the
+// order conv_patch3_kernel walks them: slice c16 * ntap + tap holds channels 16 c16 .. 16 c16 + 15
+// of that tap. One thread per (matrix, slice, row, lane group).
+__global__ void split_conv_weights_kernel(const float* w, int nmat, int rows, int K, int cin1, int ntap,
+                                          __bf16* out) {
+  const int nsl = K / kSK;
+  const long total = (long)nmat * nsl * rows * 2;
+  const long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= total) return;
+  const int grp = id & 1;
+  long r = id >> 1;
+  const int row = r % rows;
+  r /= rows;
+  const int s = r % nsl;
+  const int mat = r / nsl;
+  const int main_sl = ntap * cin1 / kSK;
+  int k0;
+  if (s < main_sl) {
+    const int c16 = s / ntap, tap = s - (s / ntap) * ntap;
+    k0 = ((c16 >> 1) * ntap + tap) * 32 + (c16 & 1) * 16;
+  } else {
+    k0 = ntap * cin1 + (s - main_sl) * kSK;
+  }
+  const float* src = w + ((size_t)mat * rows + row) * K + k0 + 8 * grp;
+  const f4 lo = *reinterpret_cast<const f4*>(src);
+  const f4 hi = *reinterpret_cast<const f4*>(src + 4);
+  bf16x8 pc[3];
+  split3(lo, hi, pc);
+  __bf16* dst = out + (((size_t)mat * nsl + s) * rows + row) * kSRow + grp * 24;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x8*>(dst + q * 8) = pc[q];
+}
+
+}  // namespace
+
+bool conv_patch3_ok(const ConvArgs& a, int which, const PatchGeom& g) {
+  if (!a.ws || a.Cin1 % kSK != 0 || a.Cin2 % kSK != 0 || a.K % kSK != 0) return false;
+  return g.P <= (which == 6 ? kPatch3Max64 : kPatch3Max128);
+}
+
+int conv2d_patch3(const ConvArgs& a, int which, const PatchGeom& g, hipStream_t st) {
+  switch (which) {
+    case 4: return launch3<128, 128, 64, 64, kPatch3Max128>(a, g, st);
+    case 5: return launch3<128, 64, 64, 32, kPatch3Max128>(a, g, st);
+    default: return launch3<64, 64, 32, 32, kPatch3Max64>(a, g, st);
+  }
+}
+
+size_t split_conv_weights_elems(int nmat, int rows, int K) { return (size_t)nmat * rows * (K / kSK) * kSRow; }
+
+int split_conv_weights(const float* w, int nmat, int rows, int K, int cin1, int ntap, void* out, hipStream_t st) {
+  DM_REQUIRE(w && out && nmat > 0 && rows > 0, "split weights: empty");
+  DM_REQUIRE(K % kSK == 0 && cin1 % 32 == 0 && ntap * cin1 <= K && (ntap == 9 || ntap == 4 || ntap == 1),
+             "split weights: K must be ntap * cin1 (+ a second segment), cin1 a multiple of 32");
+  DM_REQUIRE((reinterpret_cast<uintptr_t>(w) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0,
+             "split weights: 16-byte alignment");
+  const long total = (long)nmat * (K / kSK) * rows * 2;
+  hipLaunchKernelGGL(split_conv_weights_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, w, nmat,
+                     rows, K, cin1, ntap, static_cast<__bf16*>(out));
+  DM_LAUNCH_CHECK();
+  return DM_OK;
+}
+
+}  // namespace dm

@@ -45,7 +45,16 @@ struct ConvArgs {
   // Used when HW % 64 == 0 and the tile's waves own 64 rows (halo-patch MODE 0, 128-row tiles).
   double2* gn_part;
   int gn_G;
+  // optional split-bf16 copy of w ([matrix][K / 16][Cout][48] bf16 from split_conv_weights): halo-patch
+  // shapes then run conv_patch3_kernel (three-way bf16 split, fp32-accurate products on bf16 MFMA)
+  const void* ws;
 };
+
+// Patch-pixel capacity of the halo-patch kernels' LDS images (fp32 / split-bf16; 128- / 64-row tiles)
+constexpr int kPatchMax128 = 288;
+constexpr int kPatchMax64 = 160;
+constexpr int kPatch3Max128 = 208;
+constexpr int kPatch3Max64 = 160;
 
 // Output tile = TB images x TH rows x full width; input patch PH x PW per image.
 struct PatchGeom {
@@ -145,6 +154,14 @@ bool conv_can_emit_gn(const ConvArgs& a);
 bool conv_patch_geom(const ConvArgs& a, int BM, PatchGeom& g);
 int conv_patch_pick(const ConvArgs& a, PatchGeom& g);
 int conv2d_patch(const ConvArgs& a, int which, const PatchGeom& g, hipStream_t st);
+// split-bf16 halo-patch kernel (conv_patch3.hip): whether it takes this shape / tile, and its launcher
+bool conv_patch3_ok(const ConvArgs& a, int which, const PatchGeom& g);
+bool conv_split_eligible(const ConvArgs& a);
+int conv2d_patch3(const ConvArgs& a, int which, const PatchGeom& g, hipStream_t st);
+int conv_splitk_reduce(const ConvArgs& a, hipStream_t st);
+// fp32 packed conv weights [nmat][rows][K] -> split-bf16 slices for conv_patch3_kernel
+size_t split_conv_weights_elems(int nmat, int rows, int K);
+int split_conv_weights(const float* w, int nmat, int rows, int K, int cin1, int ntap, void* out, hipStream_t st);
 std::string conv_label(const ConvArgs& a);
 int gemm_batched(const GemmArgs& g, hipStream_t st);
 int gemm_pick(const GemmArgs& g);

@@ -163,6 +163,12 @@ struct UNetModel {
     float* out = nullptr;
   };
   std::unique_ptr<Plan> plan;
+  // split-bf16 copies of the halo-patch conv weights (conv_patch3.hip), made at the first plan build;
+  // DM_CONV_MATH=fp32 keeps every conv on the fp32 MFMA kernels
+  bool split_math = !(std::getenv("DM_CONV_MATH") && std::string(std::getenv("DM_CONV_MATH")) == "fp32");
+  std::map<const float*, void*> split_w;
+  size_t split_bytes = 0;
+  const void* split_for(const ConvArgs& c);
 
   float* P(size_t off) const { return arena + off; }
   ~UNetModel();
@@ -171,7 +177,27 @@ struct UNetModel {
 
 UNetModel::~UNetModel() {
   plan.reset();
+  for (auto& kv : split_w) (void)hipFree(kv.second);
   if (arena) (void)hipFree(arena);
+}
+
+// Split copy of a halo-patch conv's packed weights (nullptr: the conv stays on the fp32 kernels).
+const void* UNetModel::split_for(const ConvArgs& c) {
+  if (!split_math || !conv_split_eligible(c)) return nullptr;
+  auto it = split_w.find(c.w);
+  if (it != split_w.end()) return it->second;
+  const int nmat = c.upsample == 2 ? 4 : 1;
+  const size_t nb = split_conv_weights_elems(nmat, c.Cout, c.K) * 2;
+  void* p = nullptr;
+  if (hipMalloc(&p, nb) != hipSuccess) return nullptr;
+  if (split_conv_weights(c.w, nmat, c.Cout, c.K, c.Cin1, c.upsample == 2 ? 4 : 9, p, nullptr) != DM_OK ||
+      hipDeviceSynchronize() != hipSuccess) {
+    (void)hipFree(p);
+    return nullptr;
+  }
+  split_w[c.w] = p;
+  split_bytes += nb;
+  return p;
 }
 
 // Channels of the first conv / last conv input: dim (models/unet.py:72) or
@@ -620,6 +646,7 @@ int UNetModel::build_plan(int B, int H, int W) {
   };
   auto add_conv = [&](ConvArgs c) {
     maybe_split(c);
+    c.ws = split_for(c);
     double fl, by;
     conv_cost(c, fl, by);
     add(conv_label(c), fl, by, [=](hipStream_t st) { return conv2d_igemm(c, st); });
@@ -971,7 +998,7 @@ extern "C" int dm_unet_forward(dm_unet* h, const float* x, const int64_t* t, con
 
 extern "C" int dm_unet_memory(const dm_unet* h, int64_t* weight_bytes, int64_t* workspace_bytes) {
   if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
-  if (weight_bytes) *weight_bytes = (int64_t)(h->m->arena_floats * sizeof(float));
+  if (weight_bytes) *weight_bytes = (int64_t)(h->m->arena_floats * sizeof(float) + h->m->split_bytes);
   if (workspace_bytes) *workspace_bytes = h->m->plan ? (int64_t)h->m->plan->bytes : 0;
   return DM_OK;
 }

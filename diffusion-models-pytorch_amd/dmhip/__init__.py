@@ -22,6 +22,7 @@ from dmhip._lib import (  # noqa: F401
     conv2d_nhwc,
     pack_conv_weight,
     pack_conv_weight_subpixel,
+    pack_conv_weight_split,
     gemm,
     softmax_rows,
     timestep_embedding,

@@ -90,6 +90,7 @@ class ConvDesc(ctypes.Structure):
         ('res', vp), ('res_pitch', ctypes.c_int),
         ('tile', ctypes.c_int),
         ('pro_scale', vp), ('pro_shift', vp),
+        ('w_split', vp),
     ]
 
 
@@ -136,6 +137,10 @@ def _declare(L: ctypes.CDLL):
                                       vp]
     L.dm_conv2d_nhwc.argtypes = [ctypes.POINTER(ConvDesc), vp]
     L.dm_pack_conv_weight_subpixel.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp]
+    L.dm_conv_weight_split_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    L.dm_conv_weight_split_bytes.restype = ctypes.c_int64
+    L.dm_pack_conv_weight_split.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_int, vp, vp]
     L.dm_gemm.argtypes = [ctypes.POINTER(GemmDesc), vp]
     L.dm_softmax_rows.argtypes = [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, vp]
     L.dm_timestep_embedding.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp, vp]
@@ -257,6 +262,20 @@ def pack_conv_weight_subpixel(w: torch.Tensor, out: torch.Tensor):
         raise ValueError('sub-pixel packing needs a 3x3 weight and a [4, Cout, 4 Cin] output')
     check(load().dm_pack_conv_weight_subpixel(w.data_ptr(), Cout, Cin, out.data_ptr(), stream_handle(w.device)),
           'dm_pack_conv_weight_subpixel')
+
+
+def pack_conv_weight_split(wp: torch.Tensor, nmat: int, Cin: int, taps: int) -> torch.Tensor:
+    """Packed fp32 conv weights [nmat * Cout, K] -> split-bf16 slices (a uint8 device tensor) for
+    ConvDesc.w_split; taps 9, or 4 for sub-pixel weights (nmat = 4)."""
+    rows, K = wp.shape
+    Cout = rows // nmat
+    nbytes = load().dm_conv_weight_split_bytes(nmat, Cout, K)
+    if nbytes <= 0 or Cout * nmat != rows:
+        raise ValueError('split packing needs [nmat * Cout, K] weights with K a multiple of 16')
+    out = torch.empty(nbytes, dtype=torch.uint8, device=wp.device)
+    check(load().dm_pack_conv_weight_split(wp.data_ptr(), nmat, Cout, K, Cin, taps, out.data_ptr(),
+                                           stream_handle(wp.device)), 'dm_pack_conv_weight_split')
+    return out
 
 
 def conv2d_nhwc(desc: ConvDesc, device=None):

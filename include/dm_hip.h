@@ -210,6 +210,14 @@ int dm_pack_conv_weight(const float* w, int Cout, int Cin, int taps, float* out,
  * out [4 output parities][Cout][4 * Cin], the 3x3 taps that read the same low-res pixel summed. */
 int dm_pack_conv_weight_subpixel(const float* w, int Cout, int Cin, float* out, void* stream);
 
+/* Split packed fp32 conv weights (nmat matrices [Cout][K] from dm_pack_conv_weight /
+ * dm_pack_conv_weight_subpixel, K = taps * Cin (+ Cin2 of a second segment), taps 9, or 4 for
+ * the sub-pixel form) into the bf16 slices of dm_conv_desc.w_split:
+ * dm_conv_weight_split_bytes(nmat, Cout, K) bytes at `out` (16-byte aligned). */
+int64_t dm_conv_weight_split_bytes(int nmat, int Cout, int K);
+int dm_pack_conv_weight_split(const float* w, int nmat, int Cout, int K, int Cin, int taps, void* out,
+                              void* stream);
+
 typedef struct dm_conv_desc {
   const float* x;  int x_pitch, Cin, Hin, Win;
   int taps, stride;
@@ -227,6 +235,10 @@ typedef struct dm_conv_desc {
    * [B][Cin] tables from dm_groupnorm_affine(); halo-patch shapes only (3x3 stride 1 / upsample) */
   const float* pro_scale;
   const float* pro_shift;
+  /* optional split-bf16 copy of w from dm_pack_conv_weight_split(): halo-patch shapes then compute
+   * their products on the bf16 matrix cores from an exact three-way bf16 split of both operands
+   * (six piece products per product, fp32-accurate); NULL keeps the fp32 MFMA kernels */
+  const void* w_split;
 } dm_conv_desc;
 int dm_conv2d_nhwc(const dm_conv_desc* d, void* stream);
 

@@ -29,7 +29,7 @@ SHAPES = {
 }
 
 
-def run(name, iters):
+def run(name, iters, split):
     B, Cin, Cout, H, pro, up = SHAPES[name]
     dev = torch.device('cuda', 0)
     g = torch.Generator(device='cpu').manual_seed(0)
@@ -56,6 +56,9 @@ def run(name, iters):
     d.bias = b.data_ptr()
     if pro:
         d.pro_scale, d.pro_shift = sc.data_ptr(), sh.data_ptr()
+    if split:
+        ws = dmhip.pack_conv_weight_split(wp, 4 if up == 2 else 1, Cin, 4 if up == 2 else 9)
+        d.w_split = ws.data_ptr()
     for _ in range(3):
         dmhip.conv2d_nhwc(d, dev)
     torch.cuda.synchronize()
@@ -70,17 +73,20 @@ def run(name, iters):
     if up == 2:
         flops = 2.0 * B * H * H * 4 * Cout * 4 * Cin  # executed sub-pixel work
     tf = flops / ms / 1e9
-    print(f'{name:12s} {ms:8.4f} ms  {tf:6.1f} TF/s  {tf / 157.3 * 100:5.1f} %', flush=True)
+    tag = 'bf16x3' if split else 'fp32'
+    print(f'{name:12s} {tag:7s} {ms:8.4f} ms  {tf:6.1f} TF/s  {tf / 157.3 * 100:5.1f} % of fp32 peak', flush=True)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--iters', type=int, default=20)
     ap.add_argument('--shape', default=None)
+    ap.add_argument('--math', choices=['fp32', 'bf16x3', 'both'], default='both')
     args = ap.parse_args()
     dmhip.load()
     for name in ([args.shape] if args.shape else SHAPES):
-        run(name, args.iters)
+        for split in ((False, True) if args.math == 'both' else (args.math == 'bf16x3', )):
+            run(name, args.iters, split)
 
 
 if __name__ == '__main__':
