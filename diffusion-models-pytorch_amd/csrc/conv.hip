@@ -331,12 +331,13 @@ bool conv_can_emit_gn(const ConvArgs& a) {
 
 // The exact kernel instantiation (matches the rocprofv3 kernel name with spaces removed).
 std::string conv_label(const ConvArgs& a) {
-  static const char* names[] = {"conv_igemm_kernel<128,128,64,64>", "conv_igemm_kernel<128,64,64,32>",
-                                "conv_igemm_kernel<64,64,32,32>",   "conv_patch_kernel<128,128,64,64",
-                                "conv_patch_kernel<128,64,64,32",   "conv_patch_kernel<64,64,32,32"};
+  static const char* names[] = {"conv_igemm_kernel<128,128,64,64", "conv_igemm_kernel<128,64,64,32",
+                                "conv_igemm_kernel<64,64,32,32",   "conv_patch_kernel<128,128,64,64",
+                                "conv_patch_kernel<128,64,64,32",  "conv_patch_kernel<64,64,32,32"};
   const int p = conv_pick(a);
   std::string s = names[p];
-  if (p >= 3) {  // <BM,BN,WM,WN,MODE,MAXP,PRO>; MAXP 288 (208 split-bf16) for 128-row tiles, 160 for 64-row
+  if (p < 3) s += "," + std::to_string(conv_mode(a)) + ">";  // <BM,BN,WM,WN,MODE>
+  if (p >= 3) {  // <BM,BN,WM,WN,MODE,MAXP,PRO,KSPLIT>; MAXP 288 (208 split-bf16) for 128-row tiles, 160 for 64-row
     PatchGeom g;
     conv_patch_pick(a, g);
     const bool x3 = conv_patch3_ok(a, p + 1, g);
@@ -344,7 +345,7 @@ std::string conv_label(const ConvArgs& a) {
     s += "," + std::to_string(a.upsample);
     s += p == 5 ? ",160" : (x3 ? ",208" : ",288");
     s += a.pro_scale ? ",true" : ",false";
-    s += a.ksplit > 1 ? ",true>" : ">";
+    s += a.ksplit > 1 ? ",true>" : ",false>";  // rocprofv3 prints the defaulted KSPLIT argument too
   }
   return s;
 }
