@@ -16,9 +16,10 @@ Roofline: HIP events around every launch of the forward during the timed
 region (dm_unet_profile) give each kernel family's average launch duration;
 the dominant family (most GPU time) is reported with its algorithmic (fp32)
 FLOPs per launch against the peak of the instructions it issues: the fp32 MFMA
-peak (157.3 TF) for the fp32 kernels; for the split-bf16 kernels, which issue
-each fp32 product as 6 bf16 piece products, the dense bf16 MFMA peak / 6
-(2500 / 6 = 416.7 TF of fp32-equivalent work).
+peak (157.3 TF) for the fp32 kernels; for the split kernels, which issue each
+fp32 product as P 16-bit piece products, the dense bf16/fp16 MFMA peak / P
+(fp16x2, the default: P = 3, 2500 / 3 = 833.3 TF of fp32-equivalent work;
+bf16x3: P = 6, 416.7 TF).
 
 CPU baseline: the oracle (a torch-CPU restatement of the reference path,
 bit-equal to it at equal thread count) timed on this host's cores, rank 0 /
@@ -44,7 +45,7 @@ import torch.distributed as dist  # noqa: E402
 METRIC = 'images/sec at DDIM-50, CIFAR-10 UNet 32×32, bs=256; 1/2/4/8 GPU'
 FP32_PEAK_TFLOPS = 157.3   # MI355X dense fp32 (MFMA f32 = vector rate), MI355X_MICROARCH.md
 BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (no sparsity), MI355X_MICROARCH.md
-SPLIT_PRODUCTS = 6         # split-bf16 kernels: one fp32 product = 6 bf16 piece products (conv_patch3.hip)
+SPLIT_PRODUCTS = {2: 3, 3: 6}  # conv_patch3_kernel<..., NP>: fp16x2 issues 3, bf16x3 6 piece products per product
 HBM_PEAK_GBS = 8000.0
 PROFILE_EVERY = 10   # per-launch events cost ~5 % when on every launch; 1 forward in 10 is observed
 
@@ -129,13 +130,17 @@ def roofline(prof):
     if flops_per_launch > 0:
         achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12
         split = dom_name.startswith('conv_patch3_kernel')
-        peak = round(BF16_PEAK_TFLOPS / SPLIT_PRODUCTS, 1) if split else FP32_PEAK_TFLOPS
+        np_ = int(dom_name.rstrip('>').split(',')[-1]) if split else 0
+        prods = SPLIT_PRODUCTS.get(np_, 0)
+        peak = round(BF16_PEAK_TFLOPS / prods, 1) if split else FP32_PEAK_TFLOPS
         roof = dict(bound='mfma', achieved=round(achieved, 2), peak=peak, unit='TFLOP/s',
                     frac=round(achieved / peak, 4), traffic=None)
         if split:
-            roof['peak_basis'] = (f'fp32-equivalent: dense bf16 MFMA {BF16_PEAK_TFLOPS:.0f} TF / {SPLIT_PRODUCTS} '
-                                  f'piece products per fp32 product; issued bf16 rate '
-                                  f'{achieved * SPLIT_PRODUCTS:.1f} TF')
+            kind = {2: 'fp16x2', 3: 'bf16x3'}[np_]
+            roof['peak_basis'] = (f'fp32-equivalent: dense 16-bit MFMA {BF16_PEAK_TFLOPS:.0f} TF / {prods} '
+                                  f'piece products per fp32 product ({kind}); issued 16-bit MFMA rate '
+                                  f'{achieved * prods:.1f} TF; vs the fp32 MFMA peak '
+                                  f'{achieved / FP32_PEAK_TFLOPS:.3f}')
     else:
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
         roof = dict(bound='hbm', achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit='GB/s',
@@ -248,7 +253,8 @@ def main():
                                  f'(dim 128, mults 1-2-2-2, 35.7M params, synthetic weights), 3x32x32, '
                                  f'B={B} per GPU',
                         global_batch=world * B, parallelism=f'dp{world}', denoise_steps=args.respace_steps,
-                        weights_gb=round(wbytes.value / 1e9, 3), workspace_gb=round(wsbytes.value / 1e9, 3)),
+                        weights_gb=round(wbytes.value / 1e9, 3), workspace_gb=round(wsbytes.value / 1e9, 3),
+                        conv_math=dmhip.unet_conv_math(handle)),
             roofline=roof,
             step_level=dict(model_tflops=round(total_flops / (total_gpu_ms * 1e-3) / 1e12, 2) if total_gpu_ms else None,
                             # observed forwards are 1 in PROFILE_EVERY: scale their kernel time to all forwards

@@ -92,18 +92,29 @@ extern "C" int dm_conv2d_nhwc(const dm_conv_desc* d, void* stream) {
   a.pro_scale = d->pro_scale;
   a.pro_shift = d->pro_shift;
   a.ws = d->w_split;
+  if (a.ws) {
+    if (d->w_split_kind != DM_SPLIT_BF16X3 && d->w_split_kind != DM_SPLIT_FP16X2) {
+      dm::set_error("conv: w_split_kind must be DM_SPLIT_BF16X3 or DM_SPLIT_FP16X2");
+      return DM_ERR_ARG;
+    }
+    a.ws_np = d->w_split_kind;
+    if (a.ws_np == DM_SPLIT_FP16X2)
+      a.ws_rowscale = dm::split_conv_rowscale(a.ws, a.upsample == 2 ? 4 : 1, a.Cout, a.K);
+    a.range_flag = d->range_flag;
+  }
   return dm::conv2d_igemm(a, (hipStream_t)stream);
 }
 
-extern "C" int64_t dm_conv_weight_split_bytes(int nmat, int Cout, int K) {
+extern "C" int64_t dm_conv_weight_split_bytes(int nmat, int Cout, int K, int kind) {
   if (nmat <= 0 || Cout <= 0 || K <= 0 || K % 16 != 0) return 0;
-  return (int64_t)dm::split_conv_weights_elems(nmat, Cout, K) * 2;
+  if (kind != DM_SPLIT_BF16X3 && kind != DM_SPLIT_FP16X2) return 0;
+  return (int64_t)dm::split_conv_weights_bytes(nmat, Cout, K, kind);
 }
 
-extern "C" int dm_pack_conv_weight_split(const float* w, int nmat, int Cout, int K, int Cin, int taps, void* out,
-                                         void* stream) {
+extern "C" int dm_pack_conv_weight_split(const float* w, int nmat, int Cout, int K, int Cin, int taps, int kind,
+                                         void* out, void* stream) {
   if (!w || !out) { dm::set_error("null tensor"); return DM_ERR_ARG; }
-  return dm::split_conv_weights(w, nmat, Cout, K, Cin, taps, out, (hipStream_t)stream);
+  return dm::split_conv_weights(w, nmat, Cout, K, Cin, taps, kind, out, (hipStream_t)stream);
 }
 
 extern "C" int dm_pack_conv_weight_subpixel(const float* w, int Cout, int Cin, float* out, void* stream) {

@@ -345,7 +345,8 @@ std::string conv_label(const ConvArgs& a) {
     s += "," + std::to_string(a.upsample);
     s += p == 5 ? ",160" : (x3 ? ",208" : ",288");
     s += a.pro_scale ? ",true" : ",false";
-    s += a.ksplit > 1 ? ",true>" : ",false>";  // rocprofv3 prints the defaulted KSPLIT argument too
+    s += a.ksplit > 1 ? ",true" : ",false";  // rocprofv3 prints the defaulted arguments too
+    s += x3 ? "," + std::to_string(a.ws_np) + ">" : ">";  // <..., NP>: 3 bf16x3, 2 fp16x2
   }
   return s;
 }

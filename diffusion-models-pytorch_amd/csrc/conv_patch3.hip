@@ -28,6 +28,20 @@
 // chunk, and read by all 9 (or 4) taps from there. The patch is double
 // buffered, so one barrier per tap suffices. LDS per 128x128 block:
 // 2 x 208 x 112 + 2 x 128 x 112 = 73.5 KiB -> two blocks per CU.
+//
+// fp16x2 variant (NP = 2, the default): x = h0 + h1 with h0 = fp16(x), h1 =
+// fp16(x - h0), 22 significant bits; a*w = a0w0 + a0w1 + a1w0 (+ a1w1, below
+// 2^-22 |a w|, dropped), three v_mfma_f32_32x32x16_f16 per 16-deep k step
+// instead of six. fp16's narrow exponent is handled on the weight side by a
+// per-output-channel power-of-two scale (max |w| * 2^e in [2^13, 2^14), so
+// w1 stays a normal fp16 for every weight above 2^-16 of the row maximum),
+// undone exactly in the epilogue; activations are split unscaled, their low
+// piece keeps an absolute floor of 2^-25 (fp16 subnormals), far below the
+// fp32 accumulation error of a K >= 288 contraction. Emulated over K = 1152
+// SiLU(N(0,1)) x U(+-1/sqrt(K)) dot products: max 4.3e-7 / rms 6.0e-8 vs
+// 3.1e-7 / 5.3e-8 for the fp32 path. An activation above 65504 (no fp16
+// image) sets ConvArgs::range_flag; the forward then re-runs in bf16x3.
+// LDS row: 2 lane groups x 2 pieces x 8 fp16 = 64 B, pitch 80 B (5 slots).
 #include "dm_common.h"
 #include "dm_kernels.h"
 #include "mfma_tile.h"
@@ -38,39 +52,80 @@ namespace dm {
 namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u4 __attribute__((ext_vector_type(4)));
 
-constexpr int kSK = 16;      // K per slice = channels per patch chunk
-constexpr int kSRow = 48;    // bf16 per slice row: 2 lane groups x 3 pieces x 8
-constexpr int kSPitch = 56;  // LDS row pitch in bf16 (112 B)
+constexpr int kSK = 16;  // K per slice = channels per patch chunk
 
-// Exact three-way split of 8 fp32 values into bf16 pieces (hi, mid, lo).
-__device__ __forceinline__ void split3(const f4 lo4, const f4 hi4, bf16x8 (&p)[3]) {
-  const float x[8] = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+// Piece format of one split variant. NP = 3: three bf16 pieces, six products; NP = 2: two fp16
+// pieces, three products, weights pre-scaled per output channel (see the file comment).
+template <int NP>
+struct Split;
+
+template <>
+struct Split<3> {
+  typedef __bf16 elem;
+  typedef bf16x8 vec;
+  static constexpr int kRow = 48;    // elements per slice row: 2 lane groups x 3 pieces x 8
+  static constexpr int kPitch = 56;  // LDS row pitch (112 B = 7 x 16 B)
+  // exact three-way split of 8 fp32 values
+  __device__ static __forceinline__ void split(const f4 lo4, const f4 hi4, vec (&p)[3], bool& bad) {
+    const float x[8] = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const __bf16 b0 = (__bf16)x[e];
-    const float r1 = x[e] - (float)b0;
-    const __bf16 b1 = (__bf16)r1;
-    const float r2 = r1 - (float)b1;
-    p[0][e] = b0;
-    p[1][e] = b1;
-    p[2][e] = (__bf16)r2;
+    for (int e = 0; e < 8; ++e) {
+      const __bf16 b0 = (__bf16)x[e];
+      const float r1 = x[e] - (float)b0;
+      const __bf16 b1 = (__bf16)r1;
+      const float r2 = r1 - (float)b1;
+      p[0][e] = b0;
+      p[1][e] = b1;
+      p[2][e] = (__bf16)r2;
+    }
   }
-}
+  __device__ static __forceinline__ void mma(const vec (&a)[3], const vec (&b)[3], f16v& acc) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
+  }
+};
 
-__device__ __forceinline__ void mfma6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f16v& acc) {
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
-}
+template <>
+struct Split<2> {
+  typedef _Float16 elem;
+  typedef f16x8 vec;
+  static constexpr int kRow = 32;    // 2 lane groups x 2 pieces x 8
+  static constexpr int kPitch = 40;  // 80 B = 5 x 16 B
+  // x = h0 + h1 with h0 = fp16(x), h1 = fp16(x - h0) (the subtraction is exact); |x| > 65504 has no
+  // fp16 image and raises `bad` (the forward's range flag: the caller re-runs in bf16x3)
+  __device__ static __forceinline__ void split(const f4 lo4, const f4 hi4, vec (&p)[2], bool& bad) {
+    const float x[8] = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+    float m = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const _Float16 h0 = (_Float16)x[e];
+      p[0][e] = h0;
+      p[1][e] = (_Float16)(x[e] - (float)h0);
+      m = fmaxf(m, fabsf(x[e]));
+    }
+    bad |= m > 65504.f;
+  }
+  __device__ static __forceinline__ void mma(const vec (&a)[2], const vec (&b)[2], f16v& acc) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[0], acc, 0, 0, 0);
+  }
+};
 
-template <int BM, int BN, int WM, int WN, int MODE, int MAXP, bool PRO, bool KSPLIT = false>
+template <int BM, int BN, int WM, int WN, int MODE, int MAXP, bool PRO, bool KSPLIT = false, int NP = 3>
 __global__ void __launch_bounds__(256)
 conv_patch3_kernel(ConvArgs a, PatchGeom g) {
+  typedef Split<NP> S;
+  typedef typename S::elem elem;
+  typedef typename S::vec vec;
+  constexpr int kSRow = S::kRow, kSPitch = S::kPitch, kGrp = NP * 8;  // kGrp: elements per lane group
   constexpr int NWN = BN / WN;
   constexpr int TM = WM / 32, TN = WN / 32;
   static_assert((BM / WM) * NWN == 4, "4 waves per block");
@@ -78,9 +133,9 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
   constexpr int NTAP = SUB ? 4 : 9;
   constexpr int PATCH = MAXP * kSPitch;
   constexpr int WSTAGE = BN * kSPitch;
-  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * PATCH + 2 * WSTAGE];
-  __bf16* const patch = lds;
-  __bf16* const wbuf = lds + 2 * PATCH;
+  __shared__ __attribute__((aligned(16))) elem lds[2 * PATCH + 2 * WSTAGE];
+  elem* const patch = lds;
+  elem* const wbuf = lds + 2 * PATCH;
 
   const int Ho = SUB ? a.Hin : a.Hout, Wo = SUB ? a.Win : a.Wout;
   const int M = a.B * Ho * Wo;
@@ -137,21 +192,21 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
     psrc[j] = (ok || PRO) ? a.x1 + ((size_t)(bc * a.Hin + iyc) * a.Win + ixc) * a.x1_pitch + 8 * shalf
                           : kZeroPage + 8 * shalf;
   }
-  // ---- weight loader: BN rows x 6 16-B pieces per slice
-  constexpr int WPIECES = BN * 6;
+  // ---- weight loader: BN rows x 2 NP 16-B pieces per slice
+  constexpr int WPIECES = BN * 2 * NP;
   constexpr int WI = (WPIECES + 255) / 256;
   const int nslices = a.K / kSK;
   const size_t slice_stride = (size_t)N * kSRow;  // bf16 per slice of one weight matrix
-  const __bf16* wsrc[WI];
+  const elem* wsrc[WI];
   int wdst[WI];
   bool wvalid[WI];
 #pragma unroll
   for (int j = 0; j < WI; ++j) {
     const int piece = t + 256 * j;
     wvalid[j] = piece < WPIECES;
-    const int row = wvalid[j] ? piece / 6 : 0, col = piece - (piece / 6) * 6;
+    const int row = wvalid[j] ? piece / (2 * NP) : 0, col = piece - (piece / (2 * NP)) * (2 * NP);
     const int n = min(n0 + row, N - 1);
-    wsrc[j] = reinterpret_cast<const __bf16*>(a.ws) + (size_t)par * nslices * slice_stride + (size_t)n * kSRow +
+    wsrc[j] = reinterpret_cast<const elem*>(a.ws) + (size_t)par * nslices * slice_stride + (size_t)n * kSRow +
               col * 8;
     wdst[j] = row * kSPitch + col * 8;
   }
@@ -195,19 +250,20 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
     }
   };
   // split + store (padding stays exactly 0: applied after the transform)
+  bool bad = false;
   auto store_patch = [&](int buf) {
-    __bf16* dst = patch + buf * PATCH;
+    elem* dst = patch + buf * PATCH;
     const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < PJ; ++j) {
       const int p = srow + 128 * j;
       if (j * 128 < MAXP && p < MAXP) {
-        bf16x8 pc[3];
+        vec pc[NP];
         const bool z = PRO && !pok[j];
-        split3(z ? zero4 : rp[j][0], z ? zero4 : rp[j][1], pc);
+        S::split(z ? zero4 : rp[j][0], z ? zero4 : rp[j][1], pc, bad);
 #pragma unroll
-        for (int q = 0; q < 3; ++q)
-          *reinterpret_cast<bf16x8*>(dst + p * kSPitch + shalf * 24 + q * 8) = pc[q];
+        for (int q = 0; q < NP; ++q)
+          *reinterpret_cast<vec*>(dst + p * kSPitch + shalf * kGrp + q * 8) = pc[q];
       }
     }
   };
@@ -230,22 +286,21 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   // one 16-deep K slice: A rows at LDS offsets abase[i] (+ lane group), B rows from wbuf[buf]
-  auto compute = [&](const __bf16* As, const int (&abase)[TM], int buf) {
-    const __bf16* Bs = wbuf + buf * WSTAGE + (wn * WN + lr) * kSPitch + lh * 24;
-    bf16x8 av[TM][3], bv[TN][3];
+  auto compute = [&](const elem* As, const int (&abase)[TM], int buf) {
+    const elem* Bs = wbuf + buf * WSTAGE + (wn * WN + lr) * kSPitch + lh * kGrp;
+    vec av[TM][NP], bv[TN][NP];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int q = 0; q < 3; ++q) av[i][q] = *reinterpret_cast<const bf16x8*>(As + abase[i] + q * 8);
+      for (int q = 0; q < NP; ++q) av[i][q] = *reinterpret_cast<const vec*>(As + abase[i] + q * 8);
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int q = 0; q < 3; ++q)
-        bv[j][q] = *reinterpret_cast<const bf16x8*>(Bs + j * 32 * kSPitch + q * 8);
+      for (int q = 0; q < NP; ++q) bv[j][q] = *reinterpret_cast<const vec*>(Bs + j * 32 * kSPitch + q * 8);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j) mfma6(av[i], bv[j], acc[i][j]);
+      for (int j = 0; j < TN; ++j) S::mma(av[i], bv[j], acc[i][j]);
   };
   auto compute_tap = [&](int ky, int kx, int pbuf, int wb) {
     int abase[TM];
@@ -259,7 +314,7 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
         pr = fy[i] + ky;
         pc = fx[i] + kx;
       }
-      abase[i] = ((fimg[i] * g.PH + pr) * g.PW + pc) * kSPitch + lh * 24;
+      abase[i] = ((fimg[i] * g.PH + pr) * g.PW + pc) * kSPitch + lh * kGrp;
     }
     compute(patch + pbuf * PATCH, abase, wb);
   };
@@ -300,7 +355,7 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
     const int s2base = NTAP * a.Cin1 / kSK;
     int abase[TM];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) abase[i] = (wm * WM + i * 32 + lr) * kSPitch + lh * 24;
+    for (int i = 0; i < TM; ++i) abase[i] = (wm * WM + i * 32 + lr) * kSPitch + lh * kGrp;
     const bool arow_ok = srow < BM;
     const int m = min(m0 + srow, M - 1);
     const float* xsrc = a.x2 + (size_t)m * a.x2_pitch + 8 * shalf;
@@ -309,11 +364,11 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
       const f4 r1 = *reinterpret_cast<const f4*>(xsrc + c2 + 4);
       load_w(s2base + c2 / kSK);
       if (arow_ok) {  // rows >= M hold clamped data: never stored
-        bf16x8 pc[3];
-        split3(r0, r1, pc);
+        vec pc[NP];
+        S::split(r0, r1, pc, bad);
 #pragma unroll
-        for (int q = 0; q < 3; ++q)
-          *reinterpret_cast<bf16x8*>(patch + srow * kSPitch + shalf * 24 + q * 8) = pc[q];
+        for (int q = 0; q < NP; ++q)
+          *reinterpret_cast<vec*>(patch + srow * kSPitch + shalf * kGrp + q * 8) = pc[q];
       }
       store_w(0);
       __syncthreads();
@@ -322,53 +377,106 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
     }
   }
 
+  if (NP == 2) {
+    // undo the per-output-channel power-of-two weight scale (exact)
+    if (bad && a.range_flag) *a.range_flag = 1;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const float sc = a.ws_rowscale[min(n0 + wn * WN + j * 32 + lr, N - 1)];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] *= sc;
+    }
+  }
   conv_patch_epilogue<BM, BN, WM, WN, MODE, KSPLIT>(a, acc, M, HWo, Wo, m0, n0, b0, wm, wn, lr, lh, split, py, px);
 }
 
-template <int BM, int BN, int WM, int WN, int MODE, int MAXP>
+template <int BM, int BN, int WM, int WN, int MODE, int MAXP, int NP>
 void launch3_mode(const ConvArgs& a, const PatchGeom& g, int blocks, hipStream_t st) {
   if (MODE == 0 && a.ksplit > 1) {
     if (a.pro_scale)
-      hipLaunchKernelGGL((conv_patch3_kernel<BM, BN, WM, WN, 0, MAXP, true, true>), dim3(blocks), dim3(256), 0, st,
-                         a, g);
-    else
-      hipLaunchKernelGGL((conv_patch3_kernel<BM, BN, WM, WN, 0, MAXP, false, true>), dim3(blocks), dim3(256), 0,
+      hipLaunchKernelGGL((conv_patch3_kernel<BM, BN, WM, WN, 0, MAXP, true, true, NP>), dim3(blocks), dim3(256), 0,
                          st, a, g);
+    else
+      hipLaunchKernelGGL((conv_patch3_kernel<BM, BN, WM, WN, 0, MAXP, false, true, NP>), dim3(blocks), dim3(256),
+                         0, st, a, g);
     return;
   }
   if (a.pro_scale)
-    hipLaunchKernelGGL((conv_patch3_kernel<BM, BN, WM, WN, MODE, MAXP, true>), dim3(blocks), dim3(256), 0, st, a, g);
+    hipLaunchKernelGGL((conv_patch3_kernel<BM, BN, WM, WN, MODE, MAXP, true, false, NP>), dim3(blocks), dim3(256), 0,
+                       st, a, g);
   else
-    hipLaunchKernelGGL((conv_patch3_kernel<BM, BN, WM, WN, MODE, MAXP, false>), dim3(blocks), dim3(256), 0, st, a,
-                       g);
+    hipLaunchKernelGGL((conv_patch3_kernel<BM, BN, WM, WN, MODE, MAXP, false, false, NP>), dim3(blocks), dim3(256),
+                       0, st, a, g);
 }
 
-template <int BM, int BN, int WM, int WN, int MAXP>
+template <int BM, int BN, int WM, int WN, int MAXP, int NP>
 int launch3(const ConvArgs& a, const PatchGeom& g, hipStream_t st) {
   const bool sub = a.upsample == 2;
   const int M = sub ? a.B * a.Hin * a.Win : a.B * a.Hout * a.Wout;
   const int ks = a.ksplit > 1 ? a.ksplit : 1;
   DM_REQUIRE(ks == 1 || (!a.upsample && a.kpart && ks <= a.Cin1 / kSK),
              "conv: split-K needs a stride-1 3x3 conv, a workspace and at most one split per channel chunk");
-  DM_REQUIRE(g.P <= MAXP, "conv: patch larger than the split-bf16 kernel's LDS image");
+  DM_REQUIRE(g.P <= MAXP, "conv: patch larger than the split kernel's LDS image");
+  DM_REQUIRE(NP == 3 || a.ws_rowscale, "conv: fp16x2 split weights need their row scales");
   const int blocks = ceil_div(M, BM) * ceil_div(a.Cout, BN) * (sub ? 4 : 1) * ks;
   if (sub)
-    launch3_mode<BM, BN, WM, WN, 2, MAXP>(a, g, blocks, st);
+    launch3_mode<BM, BN, WM, WN, 2, MAXP, NP>(a, g, blocks, st);
   else if (a.upsample)
-    launch3_mode<BM, BN, WM, WN, 1, MAXP>(a, g, blocks, st);
+    launch3_mode<BM, BN, WM, WN, 1, MAXP, NP>(a, g, blocks, st);
   else
-    launch3_mode<BM, BN, WM, WN, 0, MAXP>(a, g, blocks, st);
+    launch3_mode<BM, BN, WM, WN, 0, MAXP, NP>(a, g, blocks, st);
   DM_LAUNCH_CHECK();
   if (ks > 1) return conv_splitk_reduce(a, st);
   return DM_OK;
 }
 
-// [nmat][rows][K] fp32 packed conv weights (chunk-major over 32-channel chunks for the first
-// ntap * cin1 columns, then the 1x1 segment) -> [nmat][K / 16][rows][48] bf16 split slices in the
-// order conv_patch3_kernel walks them: slice c16 * ntap + tap holds channels 16 c16 .. 16 c16 + 15
-// of that tap. One thread per (matrix, slice, row, lane group).
+// Split slice s of matrix `mat` starts at this K column of the packed fp32 weights: slice
+// c16 * ntap + tap holds channels 16 c16 .. 16 c16 + 15 of that tap (packed chunk-major over
+// 32-channel chunks), then the 1x1 segment's slices in order.
+__device__ __forceinline__ int split_slice_k0(int s, int cin1, int ntap) {
+  const int main_sl = ntap * cin1 / kSK;
+  if (s < main_sl) {
+    const int c16 = s / ntap, tap = s - (s / ntap) * ntap;
+    return ((c16 >> 1) * ntap + tap) * 32 + (c16 & 1) * 16;
+  }
+  return ntap * cin1 + (s - main_sl) * kSK;
+}
+
+// fp16x2 row scales: per output channel n, 2^e with max_mat,k |w[mat][n][k]| * 2^e in [2^13, 2^14)
+// (1 for an all-zero row). rowscale[n] = 2^e (applied at the split), rowscale[rows + n] = 2^-e (the
+// epilogue's exact inverse). One block per row.
+__global__ void split_row_scale_kernel(const float* w, int nmat, int rows, int K, float* rowscale) {
+  const int n = blockIdx.x;
+  float m = 0.f;
+  for (int mat = 0; mat < nmat; ++mat)
+    for (int k = threadIdx.x; k < K; k += blockDim.x) m = fmaxf(m, fabsf(w[((size_t)mat * rows + n) * K + k]));
+  __shared__ float red[256];
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + o]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    int e = 0;
+    if (red[0] > 0.f) {
+      int ex;
+      frexpf(red[0], &ex);  // red[0] in [2^(ex-1), 2^ex)
+      e = min(max(14 - ex, -126), 126);
+    }
+    rowscale[n] = ldexpf(1.f, e);
+    rowscale[rows + n] = ldexpf(1.f, -e);
+  }
+}
+
+// [nmat][rows][K] fp32 packed conv weights -> [nmat][K / 16][rows][kRow] split slices in the order
+// conv_patch3_kernel walks them. One thread per (matrix, slice, row, lane group).
+template <int NP>
 __global__ void split_conv_weights_kernel(const float* w, int nmat, int rows, int K, int cin1, int ntap,
-                                          __bf16* out) {
+                                          const float* rowscale, typename Split<NP>::elem* out) {
+  typedef Split<NP> S;
   const int nsl = K / kSK;
   const long total = (long)nmat * nsl * rows * 2;
   const long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -379,22 +487,20 @@ __global__ void split_conv_weights_kernel(const float* w, int nmat, int rows, in
   r /= rows;
   const int s = r % nsl;
   const int mat = r / nsl;
-  const int main_sl = ntap * cin1 / kSK;
-  int k0;
-  if (s < main_sl) {
-    const int c16 = s / ntap, tap = s - (s / ntap) * ntap;
-    k0 = ((c16 >> 1) * ntap + tap) * 32 + (c16 & 1) * 16;
-  } else {
-    k0 = ntap * cin1 + (s - main_sl) * kSK;
+  const float* src = w + ((size_t)mat * rows + row) * K + split_slice_k0(s, cin1, ntap) + 8 * grp;
+  f4 lo = *reinterpret_cast<const f4*>(src);
+  f4 hi = *reinterpret_cast<const f4*>(src + 4);
+  if (NP == 2) {
+    const float sc = rowscale[row];  // a power of two: exact
+    lo *= sc;
+    hi *= sc;
   }
-  const float* src = w + ((size_t)mat * rows + row) * K + k0 + 8 * grp;
-  const f4 lo = *reinterpret_cast<const f4*>(src);
-  const f4 hi = *reinterpret_cast<const f4*>(src + 4);
-  bf16x8 pc[3];
-  split3(lo, hi, pc);
-  __bf16* dst = out + (((size_t)mat * nsl + s) * rows + row) * kSRow + grp * 24;
+  typename S::vec pc[NP];
+  bool bad = false;
+  S::split(lo, hi, pc, bad);
+  typename S::elem* dst = out + (((size_t)mat * nsl + s) * rows + row) * S::kRow + grp * NP * 8;
 #pragma unroll
-  for (int q = 0; q < 3; ++q) *reinterpret_cast<bf16x8*>(dst + q * 8) = pc[q];
+  for (int q = 0; q < NP; ++q) *reinterpret_cast<typename S::vec*>(dst + q * 8) = pc[q];
 }
 
 }  // namespace
@@ -405,24 +511,51 @@ bool conv_patch3_ok(const ConvArgs& a, int which, const PatchGeom& g) {
 }
 
 int conv2d_patch3(const ConvArgs& a, int which, const PatchGeom& g, hipStream_t st) {
+  if (a.ws_np == 2) {
+    switch (which) {
+      case 4: return launch3<128, 128, 64, 64, kPatch3Max128, 2>(a, g, st);
+      case 5: return launch3<128, 64, 64, 32, kPatch3Max128, 2>(a, g, st);
+      default: return launch3<64, 64, 32, 32, kPatch3Max64, 2>(a, g, st);
+    }
+  }
   switch (which) {
-    case 4: return launch3<128, 128, 64, 64, kPatch3Max128>(a, g, st);
-    case 5: return launch3<128, 64, 64, 32, kPatch3Max128>(a, g, st);
-    default: return launch3<64, 64, 32, 32, kPatch3Max64>(a, g, st);
+    case 4: return launch3<128, 128, 64, 64, kPatch3Max128, 3>(a, g, st);
+    case 5: return launch3<128, 64, 64, 32, kPatch3Max128, 3>(a, g, st);
+    default: return launch3<64, 64, 32, 32, kPatch3Max64, 3>(a, g, st);
   }
 }
 
-size_t split_conv_weights_elems(int nmat, int rows, int K) { return (size_t)nmat * rows * (K / kSK) * kSRow; }
+// Bytes of a split copy: the pieces, then (fp16x2) 2 x rows fp32 row scales at a 16-B aligned offset.
+size_t split_conv_weights_bytes(int nmat, int rows, int K, int np) {
+  const size_t pieces = (size_t)nmat * rows * (K / kSK) * (np == 2 ? Split<2>::kRow : Split<3>::kRow) * 2;
+  return np == 2 ? pieces + (size_t)2 * rows * sizeof(float) : pieces;
+}
 
-int split_conv_weights(const float* w, int nmat, int rows, int K, int cin1, int ntap, void* out, hipStream_t st) {
+const float* split_conv_rowscale(const void* ws, int nmat, int rows, int K) {
+  return reinterpret_cast<const float*>(static_cast<const char*>(ws) +
+                                        (size_t)nmat * rows * (K / kSK) * Split<2>::kRow * 2) + rows;
+}
+
+int split_conv_weights(const float* w, int nmat, int rows, int K, int cin1, int ntap, int np, void* out,
+                       hipStream_t st) {
   DM_REQUIRE(w && out && nmat > 0 && rows > 0, "split weights: empty");
+  DM_REQUIRE(np == 2 || np == 3, "split weights: kind must be 2 (fp16x2) or 3 (bf16x3)");
   DM_REQUIRE(K % kSK == 0 && cin1 % 32 == 0 && ntap * cin1 <= K && (ntap == 9 || ntap == 4 || ntap == 1),
              "split weights: K must be ntap * cin1 (+ a second segment), cin1 a multiple of 32");
   DM_REQUIRE((reinterpret_cast<uintptr_t>(w) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0,
              "split weights: 16-byte alignment");
   const long total = (long)nmat * (K / kSK) * rows * 2;
-  hipLaunchKernelGGL(split_conv_weights_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, w, nmat,
-                     rows, K, cin1, ntap, static_cast<__bf16*>(out));
+  const unsigned grid = (unsigned)((total + 255) / 256);
+  if (np == 2) {
+    float* rs = const_cast<float*>(split_conv_rowscale(out, nmat, rows, K)) - rows;
+    hipLaunchKernelGGL(split_row_scale_kernel, dim3(rows), dim3(256), 0, st, w, nmat, rows, K, rs);
+    DM_LAUNCH_CHECK();
+    hipLaunchKernelGGL(split_conv_weights_kernel<2>, dim3(grid), dim3(256), 0, st, w, nmat, rows, K, cin1, ntap,
+                       rs, static_cast<_Float16*>(out));
+  } else {
+    hipLaunchKernelGGL(split_conv_weights_kernel<3>, dim3(grid), dim3(256), 0, st, w, nmat, rows, K, cin1, ntap,
+                       nullptr, static_cast<__bf16*>(out));
+  }
   DM_LAUNCH_CHECK();
   return DM_OK;
 }

@@ -1,6 +1,8 @@
 // Internal kernel entry points (host-side launchers). The public C ABI in
 // include/dm_hip.h wraps these.
 #pragma once
+#include <cstdlib>
+#include <string>
 #include "dm_common.h"
 
 namespace dm {
@@ -45,9 +47,15 @@ struct ConvArgs {
   // Used when HW % 64 == 0 and the tile's waves own 64 rows (halo-patch MODE 0, 128-row tiles).
   double2* gn_part;
   int gn_G;
-  // optional split-bf16 copy of w ([matrix][K / 16][Cout][48] bf16 from split_conv_weights): halo-patch
-  // shapes then run conv_patch3_kernel (three-way bf16 split, fp32-accurate products on bf16 MFMA)
+  // optional split copy of w (split_conv_weights): halo-patch shapes then run conv_patch3_kernel with
+  // fp32-accurate products on the 16-bit matrix cores. ws_np 3: [matrix][K / 16][Cout][48] bf16
+  // (three-way bf16 split); ws_np 2: [matrix][K / 16][Cout][32] fp16 (two-way fp16 split of the
+  // weights scaled by ws_rowscale[-Cout + n]; ws_rowscale[n] is the epilogue's inverse scale)
   const void* ws;
+  int ws_np;
+  const float* ws_rowscale;
+  // optional device flag, set to 1 when an fp16x2 conv meets an activation beyond the fp16 range
+  int* range_flag;
 };
 
 // Patch-pixel capacity of the halo-patch kernels' LDS images (fp32 / split-bf16; 128- / 64-row tiles)
@@ -159,10 +167,20 @@ bool conv_patch3_ok(const ConvArgs& a, int which, const PatchGeom& g);
 bool conv_split_eligible(const ConvArgs& a);
 int conv2d_patch3(const ConvArgs& a, int which, const PatchGeom& g, hipStream_t st);
 int conv_splitk_reduce(const ConvArgs& a, hipStream_t st);
-// fp32 packed conv weights [nmat][rows][K] -> split-bf16 slices for conv_patch3_kernel
-size_t split_conv_weights_elems(int nmat, int rows, int K);
-int split_conv_weights(const float* w, int nmat, int rows, int K, int cin1, int ntap, void* out, hipStream_t st);
+// fp32 packed conv weights [nmat][rows][K] -> split slices for conv_patch3_kernel (np 3: bf16x3,
+// np 2: fp16x2 + row scales); split_conv_rowscale gives ConvArgs::ws_rowscale of an fp16x2 copy
+size_t split_conv_weights_bytes(int nmat, int rows, int K, int np);
+const float* split_conv_rowscale(const void* ws, int nmat, int rows, int K);
+int split_conv_weights(const float* w, int nmat, int rows, int K, int cin1, int ntap, int np, void* out,
+                       hipStream_t st);
 std::string conv_label(const ConvArgs& a);
+// DM_CONV_MATH: fp16x2 (default) -> 2, bf16x3 -> 3, fp32 -> 0 (ConvArgs::ws_np of the model's convs)
+inline int conv_math_from_env() {
+  const char* e = std::getenv("DM_CONV_MATH");
+  if (!e) return 2;
+  const std::string s(e);
+  return s == "fp32" ? 0 : s == "bf16x3" ? 3 : 2;
+}
 int gemm_batched(const GemmArgs& g, hipStream_t st);
 int gemm_pick(const GemmArgs& g);
 std::string gemm_label(const GemmArgs& g);

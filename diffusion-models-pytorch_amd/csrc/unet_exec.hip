@@ -163,12 +163,17 @@ struct UNetModel {
     float* out = nullptr;
   };
   std::unique_ptr<Plan> plan;
-  // split-bf16 copies of the halo-patch conv weights (conv_patch3.hip), made at the first plan build;
-  // DM_CONV_MATH=fp32 keeps every conv on the fp32 MFMA kernels
-  bool split_math = !(std::getenv("DM_CONV_MATH") && std::string(std::getenv("DM_CONV_MATH")) == "fp32");
-  std::map<const float*, void*> split_w;
+  // Split copies of the halo-patch conv weights (conv_patch3.hip), made at the first plan build.
+  // conv_math: 2 fp16x2 (default), 3 bf16x3, 0 fp32 MFMA kernels (DM_CONV_MATH=fp16x2|bf16x3|fp32).
+  // fp16x2 convs raise range_flag on an activation beyond the fp16 range; the forward then
+  // switches this model to bf16x3 and runs again (DM_RANGE_CHECK=0 skips the check and its sync).
+  int conv_math = conv_math_from_env();
+  bool range_check = !(std::getenv("DM_RANGE_CHECK") && std::string(std::getenv("DM_RANGE_CHECK")) == "0");
+  int* range_flag = nullptr;       // device
+  int* range_flag_host = nullptr;  // pinned
+  std::map<std::pair<const float*, int>, void*> split_w;
   size_t split_bytes = 0;
-  const void* split_for(const ConvArgs& c);
+  void split_for(ConvArgs& c);
 
   float* P(size_t off) const { return arena + off; }
   ~UNetModel();
@@ -178,26 +183,43 @@ struct UNetModel {
 UNetModel::~UNetModel() {
   plan.reset();
   for (auto& kv : split_w) (void)hipFree(kv.second);
+  if (range_flag) (void)hipFree(range_flag);
+  if (range_flag_host) (void)hipHostFree(range_flag_host);
   if (arena) (void)hipFree(arena);
 }
 
-// Split copy of a halo-patch conv's packed weights (nullptr: the conv stays on the fp32 kernels).
-const void* UNetModel::split_for(const ConvArgs& c) {
-  if (!split_math || !conv_split_eligible(c)) return nullptr;
-  auto it = split_w.find(c.w);
-  if (it != split_w.end()) return it->second;
+// Attach the split copy of a halo-patch conv's packed weights (none: the conv stays on the fp32
+// kernels).
+void UNetModel::split_for(ConvArgs& c) {
+  c.ws = nullptr;
+  c.ws_np = 0;
+  c.ws_rowscale = nullptr;
+  c.range_flag = nullptr;
+  if (!conv_math || !conv_split_eligible(c)) return;
   const int nmat = c.upsample == 2 ? 4 : 1;
-  const size_t nb = split_conv_weights_elems(nmat, c.Cout, c.K) * 2;
+  auto key = std::make_pair(c.w, conv_math);
+  auto it = split_w.find(key);
   void* p = nullptr;
-  if (hipMalloc(&p, nb) != hipSuccess) return nullptr;
-  if (split_conv_weights(c.w, nmat, c.Cout, c.K, c.Cin1, c.upsample == 2 ? 4 : 9, p, nullptr) != DM_OK ||
-      hipDeviceSynchronize() != hipSuccess) {
-    (void)hipFree(p);
-    return nullptr;
+  if (it != split_w.end()) {
+    p = it->second;
+  } else {
+    const size_t nb = split_conv_weights_bytes(nmat, c.Cout, c.K, conv_math);
+    if (hipMalloc(&p, nb) != hipSuccess) return;
+    if (split_conv_weights(c.w, nmat, c.Cout, c.K, c.Cin1, c.upsample == 2 ? 4 : 9, conv_math, p, nullptr) !=
+            DM_OK ||
+        hipDeviceSynchronize() != hipSuccess) {
+      (void)hipFree(p);
+      return;
+    }
+    split_w[key] = p;
+    split_bytes += nb;
   }
-  split_w[c.w] = p;
-  split_bytes += nb;
-  return p;
+  c.ws = p;
+  c.ws_np = conv_math;
+  if (conv_math == 2) {
+    c.ws_rowscale = split_conv_rowscale(p, nmat, c.Cout, c.K);
+    c.range_flag = range_flag;
+  }
 }
 
 // Channels of the first conv / last conv input: dim (models/unet.py:72) or
@@ -543,6 +565,11 @@ int UNetModel::build_plan(int B, int H, int W) {
   pl.B = B;
   pl.H = H;
   pl.W = W;
+  if (!range_flag) {
+    DM_CHECK_HIP(hipMalloc(&range_flag, sizeof(int)));
+    DM_CHECK_HIP(hipMemset(range_flag, 0, sizeof(int)));
+    DM_CHECK_HIP(hipHostMalloc(&range_flag_host, sizeof(int)));
+  }
   DM_REQUIRE(H % (1 << (n_levels - 1)) == 0 && W % (1 << (n_levels - 1)) == 0,
              "image size must be divisible by 2^(n_stages-1)");
   bool& alloc_failed = pl.alloc_failed;
@@ -646,7 +673,7 @@ int UNetModel::build_plan(int B, int H, int W) {
   };
   auto add_conv = [&](ConvArgs c) {
     maybe_split(c);
-    c.ws = split_for(c);
+    split_for(c);
     double fl, by;
     conv_cost(c, fl, by);
     add(conv_label(c), fl, by, [=](hipStream_t st) { return conv2d_igemm(c, st); });
@@ -973,6 +1000,10 @@ extern "C" int dm_unet_forward(dm_unet* h, const float* x, const int64_t* t, con
   if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
   if (!x || !t || !out) { dm::set_error("null tensor"); return DM_ERR_ARG; }
   if (B <= 0 || H <= 0 || W <= 0) { dm::set_error("empty batch or image"); return DM_ERR_ARG; }
+  if (static_cast<const void*>(out) == static_cast<const void*>(x)) {
+    dm::set_error("out must not alias x");
+    return DM_ERR_ARG;
+  }
   dm::UNetModel* m = h->m;
   if (!m->plan || m->plan->B != B || m->plan->H != H || m->plan->W != W) {
     int rc = m->build_plan(B, H, W);
@@ -993,6 +1024,17 @@ extern "C" int dm_unet_forward(dm_unet* h, const float* x, const int64_t* t, con
   const int rc = pl.run(st);
   if (rc) return rc;
   DM_CHECK_HIP(hipMemcpyAsync(out, pl.out, no * sizeof(float), hipMemcpyDeviceToDevice, st));
+  if (m->conv_math == 2 && m->range_check) {
+    // an fp16x2 conv met an activation beyond 65504: this model continues in bf16x3, from this call
+    DM_CHECK_HIP(hipMemcpyAsync(m->range_flag_host, m->range_flag, sizeof(int), hipMemcpyDeviceToHost, st));
+    DM_CHECK_HIP(hipStreamSynchronize(st));
+    if (*m->range_flag_host) {
+      DM_CHECK_HIP(hipMemsetAsync(m->range_flag, 0, sizeof(int), st));
+      m->conv_math = 3;
+      m->plan.reset();
+      return dm_unet_forward(h, x, t, y, B, H, W, out, stream);
+    }
+  }
   return DM_OK;
 }
 
@@ -1000,6 +1042,25 @@ extern "C" int dm_unet_memory(const dm_unet* h, int64_t* weight_bytes, int64_t* 
   if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
   if (weight_bytes) *weight_bytes = (int64_t)(h->m->arena_floats * sizeof(float) + h->m->split_bytes);
   if (workspace_bytes) *workspace_bytes = h->m->plan ? (int64_t)h->m->plan->bytes : 0;
+  return DM_OK;
+}
+
+extern "C" int dm_unet_set_conv_math(dm_unet* h, int kind) {
+  if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
+  if (kind != 0 && kind != DM_SPLIT_BF16X3 && kind != DM_SPLIT_FP16X2) {
+    dm::set_error("conv math must be 0 (fp32), DM_SPLIT_BF16X3 or DM_SPLIT_FP16X2");
+    return DM_ERR_ARG;
+  }
+  if (kind != h->m->conv_math) {
+    h->m->conv_math = kind;
+    h->m->plan.reset();
+  }
+  return DM_OK;
+}
+
+extern "C" int dm_unet_get_conv_math(const dm_unet* h, int* kind) {
+  if (!h || !h->m || !kind) { dm::set_error("null model"); return DM_ERR_STATE; }
+  *kind = h->m->conv_math;
   return DM_OK;
 }
 

@@ -90,7 +90,7 @@ class ConvDesc(ctypes.Structure):
         ('res', vp), ('res_pitch', ctypes.c_int),
         ('tile', ctypes.c_int),
         ('pro_scale', vp), ('pro_shift', vp),
-        ('w_split', vp),
+        ('w_split', vp), ('w_split_kind', ctypes.c_int), ('range_flag', vp),
     ]
 
 
@@ -137,10 +137,12 @@ def _declare(L: ctypes.CDLL):
                                       vp]
     L.dm_conv2d_nhwc.argtypes = [ctypes.POINTER(ConvDesc), vp]
     L.dm_pack_conv_weight_subpixel.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp]
-    L.dm_conv_weight_split_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    L.dm_conv_weight_split_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
     L.dm_conv_weight_split_bytes.restype = ctypes.c_int64
     L.dm_pack_conv_weight_split.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                            ctypes.c_int, vp, vp]
+                                            ctypes.c_int, ctypes.c_int, vp, vp]
+    L.dm_unet_set_conv_math.argtypes = [vp, ctypes.c_int]
+    L.dm_unet_get_conv_math.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
     L.dm_gemm.argtypes = [ctypes.POINTER(GemmDesc), vp]
     L.dm_softmax_rows.argtypes = [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, vp]
     L.dm_timestep_embedding.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp, vp]
@@ -264,18 +266,36 @@ def pack_conv_weight_subpixel(w: torch.Tensor, out: torch.Tensor):
           'dm_pack_conv_weight_subpixel')
 
 
-def pack_conv_weight_split(wp: torch.Tensor, nmat: int, Cin: int, taps: int) -> torch.Tensor:
-    """Packed fp32 conv weights [nmat * Cout, K] -> split-bf16 slices (a uint8 device tensor) for
-    ConvDesc.w_split; taps 9, or 4 for sub-pixel weights (nmat = 4)."""
+SPLIT_FP16X2 = 2  # DM_SPLIT_FP16X2
+SPLIT_BF16X3 = 3  # DM_SPLIT_BF16X3
+CONV_MATH = {'fp32': 0, 'fp16x2': SPLIT_FP16X2, 'bf16x3': SPLIT_BF16X3}
+
+
+def pack_conv_weight_split(wp: torch.Tensor, nmat: int, Cin: int, taps: int, kind: int = SPLIT_BF16X3) -> torch.Tensor:
+    """Packed fp32 conv weights [nmat * Cout, K] -> split slices (a uint8 device tensor) for
+    ConvDesc.w_split with ConvDesc.w_split_kind = kind; taps 9, or 4 for sub-pixel weights (nmat = 4)."""
     rows, K = wp.shape
     Cout = rows // nmat
-    nbytes = load().dm_conv_weight_split_bytes(nmat, Cout, K)
+    nbytes = load().dm_conv_weight_split_bytes(nmat, Cout, K, kind)
     if nbytes <= 0 or Cout * nmat != rows:
-        raise ValueError('split packing needs [nmat * Cout, K] weights with K a multiple of 16')
+        raise ValueError('split packing needs [nmat * Cout, K] weights with K a multiple of 16 and kind 2 or 3')
     out = torch.empty(nbytes, dtype=torch.uint8, device=wp.device)
-    check(load().dm_pack_conv_weight_split(wp.data_ptr(), nmat, Cout, K, Cin, taps, out.data_ptr(),
+    check(load().dm_pack_conv_weight_split(wp.data_ptr(), nmat, Cout, K, Cin, taps, kind, out.data_ptr(),
                                            stream_handle(wp.device)), 'dm_pack_conv_weight_split')
     return out
+
+
+def unet_conv_math(handle, kind: Optional[str] = None) -> str:
+    """Set (kind given) and return the conv arithmetic of a native UNet handle: 'fp16x2' (default),
+    'bf16x3' or 'fp32' (dm_unet_set_conv_math / dm_unet_get_conv_math)."""
+    L = load()
+    if kind is not None:
+        if kind not in CONV_MATH:
+            raise ValueError(f'conv math must be one of {sorted(CONV_MATH)}')
+        check(L.dm_unet_set_conv_math(handle, CONV_MATH[kind]), 'dm_unet_set_conv_math')
+    k = ctypes.c_int()
+    check(L.dm_unet_get_conv_math(handle, ctypes.byref(k)), 'dm_unet_get_conv_math')
+    return {v: n for n, v in CONV_MATH.items()}[k.value]
 
 
 def conv2d_nhwc(desc: ConvDesc, device=None):

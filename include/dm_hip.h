@@ -111,6 +111,12 @@ int dm_unet_profile_get(dm_unet* m, int i, char* label, int label_len, double* f
                         double* ms_total, int64_t* launches);
 /* Device bytes held by packed weights and by the cached workspace. */
 int dm_unet_memory(const dm_unet* m, int64_t* weight_bytes, int64_t* workspace_bytes);
+/* Arithmetic of the 3x3 halo-patch convs (all fp32-accurate, models/unet.py:16,26 convolve in fp32):
+ * DM_SPLIT_FP16X2 (default; env DM_CONV_MATH=fp16x2), DM_SPLIT_BF16X3 (bf16x3), 0 = fp32 MFMA (fp32).
+ * An fp16x2 forward that meets an activation beyond the fp16 range (|a| > 65504) is detected on the
+ * device and run again in bf16x3, which the model then keeps; get reports the current kind. */
+int dm_unet_set_conv_math(dm_unet* m, int kind);
+int dm_unet_get_conv_math(const dm_unet* m, int* kind);
 void dm_unet_destroy(dm_unet* m);
 
 /* Denoiser: DiT ------------------------------------------------------------
@@ -212,10 +218,15 @@ int dm_pack_conv_weight_subpixel(const float* w, int Cout, int Cin, float* out, 
 
 /* Split packed fp32 conv weights (nmat matrices [Cout][K] from dm_pack_conv_weight /
  * dm_pack_conv_weight_subpixel, K = taps * Cin (+ Cin2 of a second segment), taps 9, or 4 for
- * the sub-pixel form) into the bf16 slices of dm_conv_desc.w_split:
- * dm_conv_weight_split_bytes(nmat, Cout, K) bytes at `out` (16-byte aligned). */
-int64_t dm_conv_weight_split_bytes(int nmat, int Cout, int K);
-int dm_pack_conv_weight_split(const float* w, int nmat, int Cout, int K, int Cin, int taps, void* out,
+ * the sub-pixel form) into the 16-bit slices of dm_conv_desc.w_split:
+ * dm_conv_weight_split_bytes(nmat, Cout, K, kind) bytes at `out` (16-byte aligned).
+ * kind DM_SPLIT_BF16X3: exact three-way bf16 split (six piece products per product);
+ * kind DM_SPLIT_FP16X2: two-way fp16 split of the weights scaled per output channel by a power
+ * of two (three piece products per product; the scales follow the pieces in `out`). */
+#define DM_SPLIT_FP16X2 2
+#define DM_SPLIT_BF16X3 3
+int64_t dm_conv_weight_split_bytes(int nmat, int Cout, int K, int kind);
+int dm_pack_conv_weight_split(const float* w, int nmat, int Cout, int K, int Cin, int taps, int kind, void* out,
                               void* stream);
 
 typedef struct dm_conv_desc {
@@ -235,10 +246,12 @@ typedef struct dm_conv_desc {
    * [B][Cin] tables from dm_groupnorm_affine(); halo-patch shapes only (3x3 stride 1 / upsample) */
   const float* pro_scale;
   const float* pro_shift;
-  /* optional split-bf16 copy of w from dm_pack_conv_weight_split(): halo-patch shapes then compute
-   * their products on the bf16 matrix cores from an exact three-way bf16 split of both operands
-   * (six piece products per product, fp32-accurate); NULL keeps the fp32 MFMA kernels */
+  /* optional split copy of w from dm_pack_conv_weight_split() of kind w_split_kind: halo-patch shapes
+   * then compute their products on the 16-bit matrix cores from a split of both operands
+   * (fp32-accurate); NULL keeps the fp32 MFMA kernels */
   const void* w_split;
+  int w_split_kind;  /* DM_SPLIT_BF16X3 or DM_SPLIT_FP16X2 */
+  int* range_flag;   /* optional device int, set to 1 when an fp16x2 conv meets |x| > 65504 */
 } dm_conv_desc;
 int dm_conv2d_nhwc(const dm_conv_desc* d, void* stream);
 

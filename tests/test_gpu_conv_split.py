@@ -1,9 +1,10 @@
-"""The split-bf16 halo-patch convolution (conv_patch3.hip) against fp64 torch references.
+"""The split halo-patch convolutions (conv_patch3.hip: bf16x3 and fp16x2) against fp64 torch references.
 
-Structure: integer operands in [-2, 3) are exact in bf16 (the mid / lo pieces are zero), so
-indexing, padding, tap walk, segments and epilogues compare bit for bit as for the fp32 kernel.
-Numerics: on random fp32 operands the six-product split must be as accurate as the fp32 MFMA
-kernel (same order of error vs fp64), i.e. fp32-level, never bf16-level (~1e-2 relative)."""
+Structure: integer operands in [-2, 3) are exact in bf16 and fp16 (the low pieces are zero; the fp16x2
+weight row scales are powers of two), so indexing, padding, tap walk, segments and epilogues compare bit
+for bit as for the fp32 kernel. Numerics: on random fp32 operands both splits must be as accurate as the
+fp32 MFMA kernel (same order of error vs fp64), i.e. fp32-level, never bf16/fp16-level (~1e-2 / 1e-3
+relative). fp16x2 range: an activation beyond 65504 must raise the range flag."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -12,14 +13,16 @@ import dmhip
 from tests.test_gpu_ops import _ints, _nhwc, _pack, _pack_subpix, _run_conv
 
 pytestmark = pytest.mark.gpu
+KINDS = ['bf16x3', 'fp16x2']
 
 
+@pytest.mark.parametrize('kind', KINDS)
 @pytest.mark.parametrize('tile', [0, 4, 5, 6])
 @pytest.mark.parametrize('B,Cin,Cout,H,up', [
     (2, 32, 64, 8, 0), (1, 128, 256, 16, 0), (5, 64, 64, 4, 0), (3, 32, 96, 5, 0), (4, 64, 128, 32, 1 - 1),
     (3, 64, 64, 16, 1), (2, 32, 64, 8, 1), (2, 48, 32, 8, 0),
 ])
-def test_split_conv3x3_exact(cuda, B, Cin, Cout, H, up, tile):
+def test_split_conv3x3_exact(cuda, B, Cin, Cout, H, up, tile, kind):
     x = _ints((B, Cin, H, H), -2, 3, seed=10)
     w = _ints((Cout, Cin, 3, 3), -2, 3, seed=11)
     b = _ints((Cout, ), seed=12)
@@ -29,12 +32,13 @@ def test_split_conv3x3_exact(cuda, B, Cin, Cout, H, up, tile):
     wp = _pack(w, cuda) if Cin % 32 == 0 else None
     if wp is None:
         pytest.skip('packing needs Cin % 32 == 0')
-    y = _run_conv(cuda, _nhwc(x).to(cuda), wp, Cout, Ho, Ho, 9, 1, up, b.to(cuda), tile=tile, split=True)
+    y = _run_conv(cuda, _nhwc(x).to(cuda), wp, Cout, Ho, Ho, 9, 1, up, b.to(cuda), tile=tile, split=kind)
     assert torch.equal(y.cpu(), _nhwc(ref))
 
 
+@pytest.mark.parametrize('kind', KINDS)
 @pytest.mark.parametrize('tile', [0, 4, 5, 6])
-def test_split_conv_segments_rowvec_residual_pitch(cuda, tile):
+def test_split_conv_segments_rowvec_residual_pitch(cuda, tile, kind):
     B, C1, C2, Cout, H = 3, 64, 32, 64, 8
     h = _ints((B, C1, H, H), seed=20)
     x = _ints((B, C2, H, H), seed=21)
@@ -50,14 +54,15 @@ def test_split_conv_segments_rowvec_residual_pitch(cuda, tile):
     ref = (F.conv2d(h.double(), w2.double(), b.double(), padding=1) + rv.double()[:, :, None, None]
            + F.conv2d(x.double(), ws.double()) + res.double()).float()
     y = _run_conv(cuda, _nhwc(h).to(cuda), wp, Cout, H, H, 9, bias=b.to(cuda), rowvec=rv.to(cuda),
-                  res=_nhwc(res).to(cuda), x2=_nhwc(x).to(cuda), Cin2=C2, y_pitch=96, tile=tile, split=True)
+                  res=_nhwc(res).to(cuda), x2=_nhwc(x).to(cuda), Cin2=C2, y_pitch=96, tile=tile, split=kind)
     assert torch.equal(y[..., :Cout].cpu(), _nhwc(ref))
     assert torch.isnan(y[..., Cout:]).all()
 
 
+@pytest.mark.parametrize('kind', KINDS)
 @pytest.mark.parametrize('tile', [0, 4, 5, 6])
 @pytest.mark.parametrize('B,Cin,Cout,H', [(3, 64, 64, 16), (2, 32, 64, 8), (4, 64, 128, 8), (2, 96, 64, 4)])
-def test_split_conv_subpixel_exact(cuda, B, Cin, Cout, H, tile):
+def test_split_conv_subpixel_exact(cuda, B, Cin, Cout, H, tile, kind):
     x = _ints((B, Cin, H, H), -2, 3, seed=70)
     w = _ints((Cout, Cin, 3, 3), -1, 2, seed=71)  # summed sub-pixel weights stay within bf16's exact range
     b = _ints((Cout, ), seed=72)
@@ -65,18 +70,18 @@ def test_split_conv_subpixel_exact(cuda, B, Cin, Cout, H, tile):
                    padding=1).float()
     try:
         y = _run_conv(cuda, _nhwc(x).to(cuda), _pack_subpix(w, cuda), Cout, 2 * H, 2 * H, 9, 1, 2, b.to(cuda),
-                      tile=tile, split=True)
+                      tile=tile, split=kind)
     except ValueError as e:
         pytest.skip(str(e))
     assert torch.equal(y.cpu(), _nhwc(ref))
 
 
-def _rand_case(cuda, B, Cin, Cout, H, up, seed):
+def _rand_case(cuda, B, Cin, Cout, H, up, seed, wscale=1.0):
     g = torch.Generator().manual_seed(seed)
     x = torch.randn((B, Cin, H, H), generator=g) * 2 + 0.3
     gamma, beta = torch.randn(Cin, generator=g), torch.randn(Cin, generator=g)
-    w = torch.randn((Cout, Cin, 3, 3), generator=g) * (1.0 / (9 * Cin) ** 0.5)
-    b = torch.randn(Cout, generator=g) * 0.01
+    w = torch.randn((Cout, Cin, 3, 3), generator=g) * (wscale / (9 * Cin) ** 0.5)
+    b = torch.randn(Cout, generator=g) * 0.01 * wscale
     a = F.silu(F.group_norm(x.double(), 32, gamma.double(), beta.double(), 1e-5))
     if up:
         a = F.interpolate(a, scale_factor=2, mode='nearest')
@@ -90,13 +95,44 @@ def _rand_case(cuda, B, Cin, Cout, H, up, seed):
 @pytest.mark.parametrize('B,Cin,Cout,H,up', [(4, 128, 128, 32, 0), (8, 256, 256, 16, 0), (16, 256, 256, 8, 0),
                                              (4, 256, 128, 16, 2), (2, 384, 128, 32, 0)])
 def test_split_conv_fp32_accuracy(cuda, B, Cin, Cout, H, up):
-    """fused GN+SiLU conv on random data: split-bf16 error vs fp64 within 2x the fp32 kernel's error."""
+    """fused GN+SiLU conv on random data: split errors vs fp64 within 2x the fp32 kernel's error."""
     xd, wp, b, pro, ref = _rand_case(cuda, B, Cin, Cout, H, up, seed=90)
     Ho = ref.shape[-1]
     errs = []
-    for split in (False, True):
+    for split in (False, 'bf16x3', 'fp16x2'):
         y = _run_conv(cuda, xd, wp, Cout, Ho, Ho, 9, 1, up, b.to(cuda), pro=pro, split=split)
         errs.append((y.cpu().double() - _nhwc(ref)).abs().max().item())
     scale = ref.abs().max().item()
-    assert errs[1] < 2.0 * errs[0] + 1e-7 * scale, errs
-    assert errs[1] < 4e-6 * scale, (errs, scale)
+    for e in errs[1:]:
+        assert e < 2.0 * errs[0] + 1e-7 * scale, errs
+        assert e < 4e-6 * scale, (errs, scale)
+
+
+@pytest.mark.parametrize('wscale', [1.0, 1e-6, 3e4])
+def test_fp16x2_weight_scale_range(cuda, wscale):
+    """fp16x2 row scales: weights far below / above fp16's normal range keep fp32-level accuracy
+    (relative to the output scale), as the bf16x3 path does."""
+    xd, wp, b, pro, ref = _rand_case(cuda, 4, 64, 64, 8, 0, seed=91, wscale=wscale)
+    errs = []
+    for split in (False, 'bf16x3', 'fp16x2'):
+        y = _run_conv(cuda, xd, wp, 64, 8, 8, 9, 1, 0, b.to(cuda), pro=pro, split=split)
+        errs.append((y.cpu().double() - _nhwc(ref)).abs().max().item())
+    scale = ref.abs().max().item()
+    assert errs[2] < 2.0 * errs[0] + 1e-7 * scale, errs
+
+
+@pytest.mark.parametrize('peak,flagged', [(6.0e4, False), (1.0e5, True)])
+def test_fp16x2_range_flag(cuda, peak, flagged):
+    """an activation beyond fp16's largest finite value (65504) raises the range flag; below it the
+    fp16x2 result is fp32-accurate."""
+    B, C, H = 2, 64, 8
+    g = torch.Generator().manual_seed(92)
+    x = torch.randn((B, C, H, H), generator=g)
+    x[1, 5, 3, 4] = peak
+    w = torch.randn((C, C, 3, 3), generator=g) * 0.01
+    ref = F.conv2d(x.double(), w.double(), padding=1)
+    flag = torch.zeros(1, dtype=torch.int32, device=cuda)
+    y = _run_conv(cuda, _nhwc(x).to(cuda), _pack(w, cuda), C, H, H, 9, split='fp16x2', range_flag=flag)
+    assert bool(flag.item()) == flagged
+    if not flagged:
+        assert (y.cpu().double() - _nhwc(ref)).abs().max().item() < 4e-6 * ref.abs().max().item()

@@ -189,3 +189,43 @@ def test_batch_invariance_full_size(cuda, golden):
     y_again = model(x, t)
     assert torch.equal(y, y_again)  # deterministic
     assert torch.isfinite(y).all()
+
+
+@pytest.mark.parametrize('math', ['fp16x2', 'bf16x3', 'fp32'])
+def test_conv_math_vs_reference(cuda, golden, report, math):
+    """Every conv arithmetic (fp16x2 default, bf16x3, fp32 MFMA) meets the reference tolerance on the
+    full CIFAR-10 UNet."""
+    import dmhip
+    arrays, meta = golden('forward')
+    model, _ = _model(meta, 'cifar10', cuda)
+    h = model.native_handle(torch.device(cuda))
+    if math == 'fp16x2':
+        assert dmhip.unet_conv_math(h) == 'fp16x2'  # the default
+    assert dmhip.unet_conv_math(h, math) == math
+    y = model(torch.from_numpy(arrays['cifar10_x']).to(cuda), torch.from_numpy(arrays['cifar10_t']).to(cuda))
+    err = (y.cpu() - torch.from_numpy(arrays['cifar10_y'])).abs().max().item()
+    report(f'forward_cifar10_{math}_maxabs_vs_reference', err)
+    assert err <= TOL, err
+    assert dmhip.unet_conv_math(h) == math
+
+
+def test_fp16x2_range_fallback(cuda, golden):
+    """An activation beyond the fp16 range (first conv scaled by 1e5: the skip / shortcut inputs of
+    the up path carry ~1e5) makes the fp16x2 forward re-run in bf16x3: the result equals a forward
+    forced to bf16x3, and the model keeps bf16x3."""
+    import dmhip
+    _, meta = golden('forward')
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn((2, 3, 32, 32), generator=g).to(cuda)
+    t = torch.tensor([10, 700], device=cuda)
+    outs = {}
+    for math in ('fp16x2', 'bf16x3'):
+        model, _ = _model(meta, 'tiny', cuda)
+        with torch.no_grad():
+            model.state_dict(keep_vars=True)['first_conv.weight'].mul_(1e5)
+        h = model.native_handle(torch.device(cuda))
+        dmhip.unet_conv_math(h, math)
+        outs[math] = model(x, t).cpu()
+        assert dmhip.unet_conv_math(h) == 'bf16x3'
+    assert torch.isfinite(outs['bf16x3']).all()
+    assert torch.equal(outs['fp16x2'], outs['bf16x3'])

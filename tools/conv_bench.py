@@ -57,8 +57,9 @@ def run(name, iters, split):
     if pro:
         d.pro_scale, d.pro_shift = sc.data_ptr(), sh.data_ptr()
     if split:
-        ws = dmhip.pack_conv_weight_split(wp, 4 if up == 2 else 1, Cin, 4 if up == 2 else 9)
-        d.w_split = ws.data_ptr()
+        kind = dmhip.SPLIT_FP16X2 if split == 'fp16x2' else dmhip.SPLIT_BF16X3
+        ws = dmhip.pack_conv_weight_split(wp, 4 if up == 2 else 1, Cin, 4 if up == 2 else 9, kind)
+        d.w_split, d.w_split_kind = ws.data_ptr(), kind
     for _ in range(3):
         dmhip.conv2d_nhwc(d, dev)
     torch.cuda.synchronize()
@@ -73,7 +74,7 @@ def run(name, iters, split):
     if up == 2:
         flops = 2.0 * B * H * H * 4 * Cout * 4 * Cin  # executed sub-pixel work
     tf = flops / ms / 1e9
-    tag = 'bf16x3' if split else 'fp32'
+    tag = split or 'fp32'
     print(f'{name:12s} {tag:7s} {ms:8.4f} ms  {tf:6.1f} TF/s  {tf / 157.3 * 100:5.1f} % of fp32 peak', flush=True)
 
 
@@ -81,11 +82,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--iters', type=int, default=20)
     ap.add_argument('--shape', default=None)
-    ap.add_argument('--math', choices=['fp32', 'bf16x3', 'both'], default='both')
+    ap.add_argument('--math', choices=['fp32', 'bf16x3', 'fp16x2', 'all'], default='all')
     args = ap.parse_args()
     dmhip.load()
     for name in ([args.shape] if args.shape else SHAPES):
-        for split in ((False, True) if args.math == 'both' else (args.math == 'bf16x3', )):
+        kinds = (False, 'bf16x3', 'fp16x2') if args.math == 'all' else ({'fp32': False}.get(args.math, args.math), )
+        for split in kinds:
             run(name, args.iters, split)
 
 
