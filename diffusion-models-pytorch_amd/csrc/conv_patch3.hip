@@ -132,10 +132,7 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
   constexpr bool UP = MODE == 1, SUB = MODE == 2;
   constexpr int NTAP = SUB ? 4 : 9;
   constexpr int PATCH = MAXP * kSPitch;
-  constexpr int WSTAGE = BN * kSPitch;
-  __shared__ __attribute__((aligned(16))) elem lds[2 * PATCH + 2 * WSTAGE];
-  elem* const patch = lds;
-  elem* const wbuf = lds + 2 * PATCH;
+  __shared__ __attribute__((aligned(16))) elem patch[2 * PATCH];
 
   const int Ho = SUB ? a.Hin : a.Hout, Wo = SUB ? a.Win : a.Wout;
   const int M = a.B * Ho * Wo;
@@ -192,24 +189,30 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
     psrc[j] = (ok || PRO) ? a.x1 + ((size_t)(bc * a.Hin + iyc) * a.Win + ixc) * a.x1_pitch + 8 * shalf
                           : kZeroPage + 8 * shalf;
   }
-  // ---- weight loader: BN rows x 2 NP 16-B pieces per slice
-  constexpr int WPIECES = BN * 2 * NP;
-  constexpr int WI = (WPIECES + 255) / 256;
+  // ---- B operand: straight from global (L2) into MFMA fragment registers, no LDS stage. The split
+  // weights are laid out per (matrix, slice, 32-column group) as [NP pieces][2 lane groups][32 lanes]
+  // [8], so each (group, piece) load is one 16-B vector per lane, 1 KiB contiguous per wave.
   const int nslices = a.K / kSK;
-  const size_t slice_stride = (size_t)N * kSRow;  // bf16 per slice of one weight matrix
-  const elem* wsrc[WI];
-  int wdst[WI];
-  bool wvalid[WI];
+  const int ngrp = ceil_div(N, 32);
+  const size_t slice_stride = (size_t)ngrp * (NP * 512);  // elements per slice of one weight matrix
+  const elem* wsrc[TN];
 #pragma unroll
-  for (int j = 0; j < WI; ++j) {
-    const int piece = t + 256 * j;
-    wvalid[j] = piece < WPIECES;
-    const int row = wvalid[j] ? piece / (2 * NP) : 0, col = piece - (piece / (2 * NP)) * (2 * NP);
-    const int n = min(n0 + row, N - 1);
-    wsrc[j] = reinterpret_cast<const elem*>(a.ws) + (size_t)par * nslices * slice_stride + (size_t)n * kSRow +
-              col * 8;
-    wdst[j] = row * kSPitch + col * 8;
+  for (int j = 0; j < TN; ++j) {
+    const int grp = min((n0 + wn * WN + j * 32) >> 5, ngrp - 1);  // columns >= N: clamped, never stored
+    wsrc[j] = reinterpret_cast<const elem*>(a.ws) + (size_t)par * nslices * slice_stride + (size_t)grp * (NP * 512) +
+              (lh * 32 + lr) * 8;
   }
+  // slices ride a register ring of WD slots, loaded WD taps ahead of their use; WD divides NTAP, so a
+  // tap's slot index is a compile-time constant once the tap loop is unrolled
+  constexpr int WD = NTAP == 9 ? 3 : 2;
+  vec bq[WD][TN][NP];
+  auto load_b = [&](vec (&dst)[TN][NP], int kt) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < NP; ++q)
+        dst[j][q] = *reinterpret_cast<const vec*>(wsrc[j] + (size_t)kt * slice_stride + q * 512);
+  };
 
   // ---- A-fragment patch coordinates of this lane's rows
   int fy[TM], fx[TM], fimg[TM];
@@ -223,8 +226,11 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
     fx[i] = rem - fy[i] * Wo;
   }
 
+  // Patch registers of the next chunk and, with the GroupNorm prologue, their per-(image, channel)
+  // scale / shift, all loaded at the chunk's first tap and consumed taps later: a global load consumed
+  // right after issue would drain vmcnt (in order) through the B fragments prefetched before it.
   f4 rp[PJ][2];
-  u4 rw[WI];
+  f4 rs[PJ][2][2];
   auto load_patch = [&](int chunk) {
     const int co = chunk * kSK;
 #pragma unroll
@@ -232,20 +238,26 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
       rp[j][0] = *reinterpret_cast<const f4*>(psrc[j] + co);
       rp[j][1] = *reinterpret_cast<const f4*>(psrc[j] + co + 4);
     }
+    if (PRO) {
+      const int cc = co + 8 * shalf;
+#pragma unroll
+      for (int j = 0; j < PJ; ++j)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          rs[j][h][0] = *reinterpret_cast<const f4*>(a.pro_scale + (size_t)pimg[j] * a.Cin1 + cc + 4 * h);
+          rs[j][h][1] = *reinterpret_cast<const f4*>(a.pro_shift + (size_t)pimg[j] * a.Cin1 + cc + 4 * h);
+        }
+    }
   };
   // GroupNorm + SiLU prologue on patch registers j in [j0, j1): silu(x * scale[b][c] + shift[b][c])
-  auto transform = [&](int chunk, int j0, int j1) {
-    const int cc = chunk * kSK + 8 * shalf;
+  auto transform = [&](int j0, int j1) {
 #pragma unroll
     for (int j = 0; j < PJ; ++j) {
       if (j >= j0 && j < j1) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const f4 sc = *reinterpret_cast<const f4*>(a.pro_scale + (size_t)pimg[j] * a.Cin1 + cc + 4 * h);
-          const f4 sh = *reinterpret_cast<const f4*>(a.pro_shift + (size_t)pimg[j] * a.Cin1 + cc + 4 * h);
+        for (int h = 0; h < 2; ++h)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) rp[j][h][q] = silu_fast(rp[j][h][q] * sc[q] + sh[q]);
-        }
+          for (int q = 0; q < 4; ++q) rp[j][h][q] = silu_fast(rp[j][h][q] * rs[j][h][0][q] + rs[j][h][1][q]);
       }
     }
   };
@@ -267,16 +279,6 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
       }
     }
   };
-  auto load_w = [&](int kt) {
-#pragma unroll
-    for (int j = 0; j < WI; ++j) rw[j] = *reinterpret_cast<const u4*>(wsrc[j] + (size_t)kt * slice_stride);
-  };
-  auto store_w = [&](int buf) {
-#pragma unroll
-    for (int j = 0; j < WI; ++j)
-      if (wvalid[j]) *reinterpret_cast<u4*>(wbuf + buf * WSTAGE + wdst[j]) = rw[j];
-  };
-
   f16v acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -285,24 +287,19 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  // one 16-deep K slice: A rows at LDS offsets abase[i] (+ lane group), B rows from wbuf[buf]
-  auto compute = [&](const elem* As, const int (&abase)[TM], int buf) {
-    const elem* Bs = wbuf + buf * WSTAGE + (wn * WN + lr) * kSPitch + lh * kGrp;
-    vec av[TM][NP], bv[TN][NP];
+  // one 16-deep K slice: A rows at LDS offsets abase[i] (+ lane group), B fragments in registers
+  auto compute = [&](const elem* As, const int (&abase)[TM], const vec (&bv)[TN][NP]) {
+    vec av[TM][NP];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int q = 0; q < NP; ++q) av[i][q] = *reinterpret_cast<const vec*>(As + abase[i] + q * 8);
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int q = 0; q < NP; ++q) bv[j][q] = *reinterpret_cast<const vec*>(Bs + j * 32 * kSPitch + q * 8);
-#pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) S::mma(av[i], bv[j], acc[i][j]);
   };
-  auto compute_tap = [&](int ky, int kx, int pbuf, int wb) {
+  auto compute_tap = [&](int ky, int kx, int pbuf, const vec (&bv)[TN][NP]) {
     int abase[TM];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -316,38 +313,48 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
       }
       abase[i] = ((fimg[i] * g.PH + pr) * g.PW + pc) * kSPitch + lh * kGrp;
     }
-    compute(patch + pbuf * PATCH, abase, wb);
+    compute(patch + pbuf * PATCH, abase, bv);
   };
 
   const int nchunks = a.Cin1 / kSK;
   const int c_begin = KSPLIT ? split * nchunks / ksplit : 0;
   const int c_end = KSPLIT ? (split + 1) * nchunks / ksplit : nchunks;
+  const int kt_begin = c_begin * NTAP, kt_end = c_end * NTAP;
+  // Every load in the chunk loop is unconditional (indices clamped to the last slice / chunk, the
+  // surplus loads are never used): the waitcnt pass then sees one load sequence per tap and counts
+  // the B ring precisely, instead of assuming a skipped refill and waiting for the newest loads.
+#pragma unroll
+  for (int d = 0; d < WD; ++d) load_b(bq[d], min(kt_begin + d, kt_end - 1));
   load_patch(c_begin);
-  load_w(c_begin * NTAP);
-  if (PRO) transform(c_begin, 0, PJ);
+  if (PRO) transform(0, PJ);
   store_patch(c_begin & 1);
-  store_w((c_begin * NTAP) & 1);
   __syncthreads();
+  // The patch is double buffered and read by every tap of its chunk: one barrier per chunk. The patch
+  // of chunk c + 1 is loaded at tap 0, GroupNorm+SiLU'd over taps T0 .. NTAP-1, split and stored at
+  // the last tap into the other buffer (free: every wave passed the previous chunk's barrier).
+  constexpr int T0 = NTAP == 9 ? 3 : 1;
   for (int c = c_begin; c < c_end; ++c) {
-    const bool more_chunks = c + 1 < c_end;
 #pragma unroll
     for (int tap = 0; tap < NTAP; ++tap) {
       const int kt = c * NTAP + tap;
-      const bool more_w = (tap < NTAP - 1) || more_chunks;
-      if (more_w) load_w(kt + 1);
-      if (tap == 0 && more_chunks) load_patch(c + 1);
-      if (PRO && tap >= 1 && more_chunks) {
-        constexpr int per = (PJ + NTAP - 2) / (NTAP - 1);
-        transform(c + 1, (tap - 1) * per, tap == NTAP - 1 ? PJ : tap * per);
+      const int slot = tap % WD;
+      if (tap == 0) {
+        load_patch(min(c + 1, c_end - 1));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (PRO && tap >= T0) {
+        constexpr int per = (PJ + NTAP - T0 - 1) / (NTAP - T0);
+        transform((tap - T0) * per, tap == NTAP - 1 ? PJ : (tap - T0 + 1) * per);
       }
       if (SUB)
-        compute_tap(py + (tap >> 1), px + (tap & 1), c & 1, kt & 1);
+        compute_tap(py + (tap >> 1), px + (tap & 1), c & 1, bq[slot]);
       else
-        compute_tap(tap / 3, tap % 3, c & 1, kt & 1);
-      if (more_w) store_w((kt + 1) & 1);
-      if (tap == NTAP - 1 && more_chunks) store_patch((c + 1) & 1);
-      __syncthreads();
+        compute_tap(tap / 3, tap % 3, c & 1, bq[slot]);
+      load_b(bq[slot], min(kt + WD, kt_end - 1));
+      __builtin_amdgcn_sched_barrier(0);  // keep the refill WD taps ahead (the scheduler sinks loads to their use)
+      if (tap == NTAP - 1) store_patch((c + 1) & 1);  // after the last chunk: an unused buffer
     }
+    __syncthreads();
   }
 
   // ---- segment 2: 1x1 product of x2 (ResBlock shortcut), K = Cin2, un-pipelined (last split).
@@ -362,7 +369,7 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
     for (int c2 = 0; c2 < a.Cin2; c2 += kSK) {
       const f4 r0 = *reinterpret_cast<const f4*>(xsrc + c2);
       const f4 r1 = *reinterpret_cast<const f4*>(xsrc + c2 + 4);
-      load_w(s2base + c2 / kSK);
+      load_b(bq[0], s2base + c2 / kSK);
       if (arow_ok) {  // rows >= M hold clamped data: never stored
         vec pc[NP];
         S::split(r0, r1, pc, bad);
@@ -370,9 +377,8 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
         for (int q = 0; q < NP; ++q)
           *reinterpret_cast<vec*>(patch + srow * kSPitch + shalf * kGrp + q * 8) = pc[q];
       }
-      store_w(0);
       __syncthreads();
-      compute(patch, abase, 0);
+      compute(patch, abase, bq[0]);
       __syncthreads();
     }
   }
@@ -471,23 +477,25 @@ __global__ void split_row_scale_kernel(const float* w, int nmat, int rows, int K
   }
 }
 
-// [nmat][rows][K] fp32 packed conv weights -> [nmat][K / 16][rows][kRow] split slices in the order
-// conv_patch3_kernel walks them. One thread per (matrix, slice, row, lane group).
+// [nmat][rows][K] fp32 packed conv weights -> split slices in the order conv_patch3_kernel walks them,
+// each slice as B-fragment images [ceil(rows / 32) column groups][NP pieces][2 lane groups][32][8]
+// (rows past `rows` stay zero). One thread per (matrix, slice, row, lane group).
 template <int NP>
 __global__ void split_conv_weights_kernel(const float* w, int nmat, int rows, int K, int cin1, int ntap,
                                           const float* rowscale, typename Split<NP>::elem* out) {
   typedef Split<NP> S;
   const int nsl = K / kSK;
+  const int ngrp = (rows + 31) / 32;
   const long total = (long)nmat * nsl * rows * 2;
   const long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (id >= total) return;
-  const int grp = id & 1;
+  const int lg = id & 1;
   long r = id >> 1;
   const int row = r % rows;
   r /= rows;
   const int s = r % nsl;
   const int mat = r / nsl;
-  const float* src = w + ((size_t)mat * rows + row) * K + split_slice_k0(s, cin1, ntap) + 8 * grp;
+  const float* src = w + ((size_t)mat * rows + row) * K + split_slice_k0(s, cin1, ntap) + 8 * lg;
   f4 lo = *reinterpret_cast<const f4*>(src);
   f4 hi = *reinterpret_cast<const f4*>(src + 4);
   if (NP == 2) {
@@ -498,9 +506,9 @@ __global__ void split_conv_weights_kernel(const float* w, int nmat, int rows, in
   typename S::vec pc[NP];
   bool bad = false;
   S::split(lo, hi, pc, bad);
-  typename S::elem* dst = out + (((size_t)mat * nsl + s) * rows + row) * S::kRow + grp * NP * 8;
+  typename S::elem* dst = out + (((size_t)mat * nsl + s) * ngrp + (row >> 5)) * (NP * 512) + (lg * 32 + (row & 31)) * 8;
 #pragma unroll
-  for (int q = 0; q < NP; ++q) *reinterpret_cast<typename S::vec*>(dst + q * 8) = pc[q];
+  for (int q = 0; q < NP; ++q) *reinterpret_cast<typename S::vec*>(dst + q * 512) = pc[q];
 }
 
 }  // namespace
@@ -525,15 +533,19 @@ int conv2d_patch3(const ConvArgs& a, int which, const PatchGeom& g, hipStream_t 
   }
 }
 
-// Bytes of a split copy: the pieces, then (fp16x2) 2 x rows fp32 row scales at a 16-B aligned offset.
+// Bytes of a split copy: the pieces (rows padded to 32-column groups), then (fp16x2) 2 x rows fp32
+// row scales.
+static size_t split_piece_bytes(int nmat, int rows, int K, int np) {
+  return (size_t)nmat * (K / kSK) * ((rows + 31) / 32) * 32 * (np == 2 ? Split<2>::kRow : Split<3>::kRow) * 2;
+}
+
 size_t split_conv_weights_bytes(int nmat, int rows, int K, int np) {
-  const size_t pieces = (size_t)nmat * rows * (K / kSK) * (np == 2 ? Split<2>::kRow : Split<3>::kRow) * 2;
+  const size_t pieces = split_piece_bytes(nmat, rows, K, np);
   return np == 2 ? pieces + (size_t)2 * rows * sizeof(float) : pieces;
 }
 
 const float* split_conv_rowscale(const void* ws, int nmat, int rows, int K) {
-  return reinterpret_cast<const float*>(static_cast<const char*>(ws) +
-                                        (size_t)nmat * rows * (K / kSK) * Split<2>::kRow * 2) + rows;
+  return reinterpret_cast<const float*>(static_cast<const char*>(ws) + split_piece_bytes(nmat, rows, K, 2)) + rows;
 }
 
 int split_conv_weights(const float* w, int nmat, int rows, int K, int cin1, int ntap, int np, void* out,
@@ -546,6 +558,7 @@ int split_conv_weights(const float* w, int nmat, int rows, int K, int cin1, int 
              "split weights: 16-byte alignment");
   const long total = (long)nmat * (K / kSK) * rows * 2;
   const unsigned grid = (unsigned)((total + 255) / 256);
+  DM_CHECK_HIP(hipMemsetAsync(out, 0, split_piece_bytes(nmat, rows, K, np), st));  // padded column groups
   if (np == 2) {
     float* rs = const_cast<float*>(split_conv_rowscale(out, nmat, rows, K)) - rows;
     hipLaunchKernelGGL(split_row_scale_kernel, dim3(rows), dim3(256), 0, st, w, nmat, rows, K, rs);
