@@ -131,6 +131,7 @@ extern "C" int dm_gemm(const dm_gemm_desc* d, void* stream) {
   g.C = d->C; g.c_s1 = d->c_s1; g.c_s2 = d->c_s2; g.ldc = d->ldc;
   g.alpha = d->alpha; g.bias = d->bias; g.res = d->res; g.ld_res = d->ld_res; g.act = d->act;
   g.b_scale = d->b_scale;
+  g.split = d->split; g.split_ea = d->split_ea; g.split_eb = d->split_eb; g.range_flag = d->range_flag;
   return dm::gemm_batched(g, (hipStream_t)stream);
 }
 

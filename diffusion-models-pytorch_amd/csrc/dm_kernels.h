@@ -107,6 +107,13 @@ struct GemmArgs {
   // gn_hw pixels each (gn_hw % 64 == 0), 128-row tiles, Z1 = Z2 = 1
   double2* gn_part;
   int gn_G, gn_hw;
+  // split = 2: fp16x2 products (conv_patch3.hip's split, on the fly for both operands): A elements
+  // (after the prologue / alpha) are scaled by 2^split_ea, B elements (after b_scale) by 2^split_eb,
+  // both exact, split into two fp16 pieces each, three v_mfma_f32_32x32x16_f16 per product; the
+  // accumulator is scaled back by 2^-(ea + eb). |scaled value| > 65504 sets range_flag.
+  int split;
+  int split_ea, split_eb;
+  int* range_flag;
 };
 
 struct StepArgs {
@@ -182,6 +189,9 @@ inline int conv_math_from_env() {
   return s == "fp32" ? 0 : s == "bf16x3" ? 3 : 2;
 }
 int gemm_batched(const GemmArgs& g, hipStream_t st);
+// exponent e with max|x| * 2^e in [2^13, 2^14) (0 for all-zero x): fp16x2 operand scale of a weight
+// matrix, computed once at plan build (synchronous)
+int split_weight_exponent(const float* x, size_t n);
 int gemm_pick(const GemmArgs& g);
 std::string gemm_label(const GemmArgs& g);
 int timestep_embed(const int64_t* t, int B, int dim, int kind, const float* freqs, float* out, hipStream_t st);

@@ -8,19 +8,32 @@
 //       O = attn v^T         -> A = attn rows, B = v stored [k][n] ("BN")
 // Batch index z = z1 * Z2 + z2 with independent strides for both levels
 // (image, head).
+#include <cmath>
+#include <cstring>
 #include "dm_common.h"
 #include "dm_kernels.h"
 #include "mfma_tile.h"
+#include "split16.h"
 
 namespace dm {
 
 namespace {
 
-template <int BM, int BN, int WM, int WN, bool B_KN>
+// SPLIT (GemmArgs::split = 2): the LDS tiles hold fp16x2 pieces instead of fp32 values. A 32-deep
+// row of the fp32 tile (144 B with its pitch) holds the same 32 k as two 16-deep slices of
+// [2 lane groups][hi, lo][8] fp16 (128 B) in the same 144 B, so the stage geometry is unchanged.
+constexpr int kLDK16 = 2 * kLDK;  // fp16 elements per LDS row
+
+template <int BM, int BN, int WM, int WN, bool B_KN, bool SPLIT = false>
 __global__ void __launch_bounds__(256)
 gemm_kernel(GemmArgs g) {
   using Cfg = TileCfg<BM, BN, WM, WN>;
   __shared__ __attribute__((aligned(16))) float lds[Cfg::LDS_FLOATS];
+  const float a_pow = SPLIT ? ldexpf(1.f, g.split_ea) : 1.f;
+  const float b_pow = SPLIT ? ldexpf(1.f, g.split_eb) : 1.f;
+  bool bad = false;
+  // fp16 offset of k (0..31) in a split row: slice k / 16, lane group (k % 16) / 8, element k % 8
+  auto split_off = [](int k) { return (k >> 4) * 32 + ((k >> 3) & 1) * 16 + (k & 7); };
 
   const int z = blockIdx.z;
   const int z1 = z / g.Z2, z2 = z - (z / g.Z2) * g.Z2;
@@ -120,13 +133,31 @@ gemm_kernel(GemmArgs g) {
         for (int q = 0; q < 4; ++q) v[q] = ((v[q] - a_ln[i].x) * a_ln[i].y) * (1.0f + sc[q]) + sh[q];
       }
       if (g.alpha != 1.0f) v = v * g.alpha;
-      *reinterpret_cast<f4*>(As + (lrow + i * Cfg::ROWS_PER_PASS) * kLDK + 4 * lc4) = v;
+      if constexpr (SPLIT) {
+        f16x4 hi, lo;
+        Split<2>::split4(v * a_pow, hi, lo, bad);
+        _Float16* dst = reinterpret_cast<_Float16*>(As) + (lrow + i * Cfg::ROWS_PER_PASS) * kLDK16 + split_off(4 * lc4);
+        *reinterpret_cast<f16x4*>(dst) = hi;
+        *reinterpret_cast<f16x4*>(dst + 8) = lo;
+      } else {
+        *reinterpret_cast<f4*>(As + (lrow + i * Cfg::ROWS_PER_PASS) * kLDK + 4 * lc4) = v;
+      }
     }
     if constexpr (!B_KN) {
 #pragma unroll
-      for (int j = 0; j < Cfg::B_ITERS; ++j)
-        *reinterpret_cast<f4*>(Bs + (lrow + j * Cfg::ROWS_PER_PASS) * kLDK + 4 * lc4) =
-            (g.b_scale != 0.0f && g.b_scale != 1.0f) ? rb[j] * g.b_scale : rb[j];
+      for (int j = 0; j < Cfg::B_ITERS; ++j) {
+        const f4 v = (g.b_scale != 0.0f && g.b_scale != 1.0f) ? rb[j] * g.b_scale : rb[j];
+        if constexpr (SPLIT) {
+          f16x4 hi, lo;
+          Split<2>::split4(v * b_pow, hi, lo, bad);
+          _Float16* dst = reinterpret_cast<_Float16*>(Bs) + (lrow + j * Cfg::ROWS_PER_PASS) * kLDK16 +
+                          split_off(4 * lc4);
+          *reinterpret_cast<f16x4*>(dst) = hi;
+          *reinterpret_cast<f16x4*>(dst + 8) = lo;
+        } else {
+          *reinterpret_cast<f4*>(Bs + (lrow + j * Cfg::ROWS_PER_PASS) * kLDK + 4 * lc4) = v;
+        }
+      }
     } else {
       const int n4 = t % KN_C4, kr = t / KN_C4;
 #pragma unroll
@@ -134,8 +165,19 @@ gemm_kernel(GemmArgs g) {
         const int kk = kr + j * KN_ROWS_PER_PASS;
         if (kn_ok[j]) {
           const f4 v = rb[j];
+          if constexpr (SPLIT) {
+            f16x4 hi, lo;
+            Split<2>::split4(v * b_pow, hi, lo, bad);
+            _Float16* Bh = reinterpret_cast<_Float16*>(Bs);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) Bs[(4 * n4 + q) * kLDK + kk] = v[q];
+            for (int q = 0; q < 4; ++q) {
+              Bh[(4 * n4 + q) * kLDK16 + split_off(kk)] = hi[q];
+              Bh[(4 * n4 + q) * kLDK16 + split_off(kk) + 8] = lo[q];
+            }
+          } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) Bs[(4 * n4 + q) * kLDK + kk] = v[q];
+          }
         }
       }
     }
@@ -157,9 +199,43 @@ gemm_kernel(GemmArgs g) {
     if (kt + 1 < nk) load_tile(kt + 1);
     const float* As = lds + buf * Cfg::STAGE;
     const float* Bs = As + Cfg::A_ELEMS;
-    mfma_slice<Cfg::TM, Cfg::TN>(As, Bs, wm * WM, wn * WN, lane, acc);
+    if constexpr (SPLIT) {
+      const _Float16* Ah = reinterpret_cast<const _Float16*>(As);
+      const _Float16* Bh = reinterpret_cast<const _Float16*>(Bs);
+      const int l_r = lane & 31, l_h = lane >> 5;
+#pragma unroll
+      for (int sl = 0; sl < 2; ++sl) {
+        f16x8 av[Cfg::TM][2], bv[Cfg::TN][2];
+#pragma unroll
+        for (int i = 0; i < Cfg::TM; ++i)
+#pragma unroll
+          for (int q = 0; q < 2; ++q)
+            av[i][q] = *reinterpret_cast<const f16x8*>(Ah + (wm * WM + i * 32 + l_r) * kLDK16 + sl * 32 + l_h * 16 + q * 8);
+#pragma unroll
+        for (int j = 0; j < Cfg::TN; ++j)
+#pragma unroll
+          for (int q = 0; q < 2; ++q)
+            bv[j][q] = *reinterpret_cast<const f16x8*>(Bh + (wn * WN + j * 32 + l_r) * kLDK16 + sl * 32 + l_h * 16 + q * 8);
+#pragma unroll
+        for (int i = 0; i < Cfg::TM; ++i)
+#pragma unroll
+          for (int j = 0; j < Cfg::TN; ++j) Split<2>::mma(av[i], bv[j], acc[i][j]);
+      }
+    } else {
+      mfma_slice<Cfg::TM, Cfg::TN>(As, Bs, wm * WM, wn * WN, lane, acc);
+    }
     if (kt + 1 < nk) store_tile(buf ^ 1);
     __syncthreads();
+  }
+  if constexpr (SPLIT) {
+    if (bad && g.range_flag) *g.range_flag = 1;
+    const float unscale = ldexpf(1.f, -(g.split_ea + g.split_eb));  // exact
+#pragma unroll
+    for (int i = 0; i < Cfg::TM; ++i)
+#pragma unroll
+      for (int j = 0; j < Cfg::TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] *= unscale;
   }
 
   // Epilogue: residual / gate loads of a column group issued branch-free (clamped rows) before
@@ -216,10 +292,16 @@ template <int BM, int BN, int WM, int WN>
 int launch_gemm(const GemmArgs& g, hipStream_t st) {
   using Cfg = TileCfg<BM, BN, WM, WN>;
   dim3 grid(ceil_div(g.M, BM) * ceil_div(g.N, BN), 1, g.Z1 * g.Z2);
-  if (g.b_kn)
+  if (g.split == 2) {
+    if (g.b_kn)
+      hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, true, true>), grid, dim3(Cfg::NT), 0, st, g);
+    else
+      hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, false, true>), grid, dim3(Cfg::NT), 0, st, g);
+  } else if (g.b_kn) {
     hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, true>), grid, dim3(Cfg::NT), 0, st, g);
-  else
+  } else {
     hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, false>), grid, dim3(Cfg::NT), 0, st, g);
+  }
   DM_LAUNCH_CHECK();
   return DM_OK;
 }
@@ -239,6 +321,8 @@ int gemm_batched(const GemmArgs& g, hipStream_t st) {
                              g.Z1 == 1 && g.Z2 == 1),
              "gemm: LayerNorm-modulate prologue needs stats, scale/shift tables and rows per image");
   DM_REQUIRE(!g.gate || (g.res && g.gate_rows > 0), "gemm: gated residual needs the residual and rows per image");
+  DM_REQUIRE(g.split == 0 || (g.split == 2 && std::abs(g.split_ea) <= 100 && std::abs(g.split_eb) <= 100),
+             "gemm: split must be 0 (fp32) or 2 (fp16x2) with power-of-two scales 2^-100 .. 2^100");
   DM_REQUIRE(!g.gn_part || (gemm_pick(g) == 0 && g.Z1 == 1 && g.Z2 == 1 && g.gn_hw % 64 == 0 && g.gn_G > 0 &&
                             g.N % g.gn_G == 0 && 32 % (g.N / g.gn_G) == 0),
              "gemm: GroupNorm statistics need 128-row tiles, whole 64-pixel chunks and groups within 32 columns");
@@ -253,7 +337,33 @@ int gemm_pick(const GemmArgs& g) {
 
 std::string gemm_label(const GemmArgs& g) {
   std::string s = gemm_pick(g) == 0 ? "gemm_kernel<128,128,64,64" : "gemm_kernel<64,64,32,32";
-  return s + (g.b_kn ? ",true>" : ",false>");
+  return s + (g.b_kn ? ",true" : ",false") + (g.split == 2 ? ",true>" : ",false>");
+}
+
+namespace {
+__global__ void absmax_kernel(const float* x, size_t n, unsigned* out) {
+  float m = 0.f;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    m = fmaxf(m, fabsf(x[i]));
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));  // non-negative floats order as uints
+}
+}  // namespace
+
+int split_weight_exponent(const float* x, size_t n) {
+  unsigned* d = nullptr;
+  unsigned h = 0;
+  if (hipMalloc(&d, sizeof(unsigned)) != hipSuccess) return 0;
+  (void)hipMemset(d, 0, sizeof(unsigned));
+  hipLaunchKernelGGL(absmax_kernel, dim3(256), dim3(256), 0, nullptr, x, n, d);
+  (void)hipMemcpy(&h, d, sizeof(unsigned), hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  float m;
+  std::memcpy(&m, &h, sizeof m);
+  if (!(m > 0.f) || !std::isfinite(m)) return 0;
+  int ex;
+  std::frexp(m, &ex);
+  return std::min(std::max(14 - ex, -100), 100);
 }
 
 }  // namespace dm

@@ -174,6 +174,9 @@ struct UNetModel {
   std::map<std::pair<const float*, int>, void*> split_w;
   size_t split_bytes = 0;
   void split_for(ConvArgs& c);
+  // fp16x2 GEMMs (attention): operand exponents; weights by max |w| (cached), activations fixed
+  std::map<const float*, int> w_exp;
+  void split_gemm(GemmArgs& g, int ea, const float* weight, size_t weight_n, int eb_act = 0);
 
   float* P(size_t off) const { return arena + off; }
   ~UNetModel();
@@ -220,6 +223,25 @@ void UNetModel::split_for(ConvArgs& c) {
     c.ws_rowscale = split_conv_rowscale(p, nmat, c.Cout, c.K);
     c.range_flag = range_flag;
   }
+}
+
+// fp16x2 attention GEMMs (gemm.hip SPLIT): A scaled by 2^ea, B by the weight's exponent (max |w| *
+// 2^eb in [2^13, 2^14)) or, for an activation B, 2^eb_act. Activations use fixed exponents that keep
+// their low fp16 pieces normal down to ~2^-8 while leaving headroom to 65504 / 2^e (the range flag
+// catches the rest): GroupNorm'd inputs, q, k, v and the attention output 2^6, softmax rows (<= 1) 2^14.
+void UNetModel::split_gemm(GemmArgs& g, int ea, const float* weight, size_t weight_n, int eb_act) {
+  g.split = 0;
+  if (conv_math != 2) return;
+  int eb = eb_act;
+  if (weight) {
+    auto it = w_exp.find(weight);
+    if (it == w_exp.end()) it = w_exp.emplace(weight, split_weight_exponent(weight, weight_n)).first;
+    eb = it->second;
+  }
+  g.split = 2;
+  g.split_ea = ea;
+  g.split_eb = eb;
+  g.range_flag = range_flag;
 }
 
 // Channels of the first conv / last conv input: dim (models/unet.py:72) or
@@ -893,6 +915,7 @@ int UNetModel::build_plan(int B, int H, int W) {
       gq.A = xin.p; gq.lda = xin.pitch; gq.Bm = P(p.wqkv); gq.ldb = C; gq.C = qkv; gq.ldc = 3 * C;
       gq.alpha = 1.f; gq.bias = P(p.bqkv);
       gq.pro_scale = gsc; gq.pro_shift = gsh; gq.pro_rows = hw;
+      split_gemm(gq, 6, gq.Bm, (size_t)3 * C * C);
       add_gemm(gq);
       // head h of q / k / v: columns q0 + h * hs, k0 + h * hs, v0 + h * hs of the qkv rows
       // (q | k | v blocks: modules.py:92-94 and ADM QKVAttention; per-head [q; k; v]: QKVAttentionLegacy)
@@ -905,6 +928,7 @@ int UNetModel::build_plan(int B, int H, int W) {
       gs.C = Sb; gs.c_s1 = (long)heads * hw * hw; gs.c_s2 = (long)hw * hw; gs.ldc = hw;
       gs.alpha = p.sa;
       gs.b_scale = p.sb;
+      split_gemm(gs, 6, nullptr, 0, 6);
       add_gemm(gs);
       const long rows = (long)B * heads * hw;
       add("softmax_rows", 0, 8.0 * rows * hw, [=](hipStream_t st) { return softmax_rows(Sb, rows, hw, hw, st); });
@@ -914,11 +938,13 @@ int UNetModel::build_plan(int B, int H, int W) {
       go.Bm = qkv + v0; go.b_s1 = (long)hw * 3 * C; go.b_s2 = hs; go.ldb = 3 * C; go.b_kn = 1;
       go.C = Ob; go.c_s1 = (long)hw * C; go.c_s2 = Dh; go.ldc = C;
       go.alpha = 1.f;
+      split_gemm(go, 14, nullptr, 0, 6);
       add_gemm(go);
       GemmArgs gp{};
       gp.M = B * hw; gp.N = C; gp.K = C; gp.Z1 = 1; gp.Z2 = 1;
       gp.A = Ob; gp.lda = C; gp.Bm = P(p.wproj); gp.ldb = C; gp.C = y.p; gp.ldc = y.pitch;
       gp.alpha = 1.f; gp.bias = P(p.bproj); gp.res = xin.p; gp.ld_res = xin.pitch;
+      split_gemm(gp, 6, gp.Bm, (size_t)C * C);
       emit_gemm(gp, y);
       add_gemm(gp);
     } else if (n.idx < 0) {

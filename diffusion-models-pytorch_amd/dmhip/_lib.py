@@ -105,6 +105,7 @@ class GemmDesc(ctypes.Structure):
         ('res', vp), ('ld_res', ctypes.c_int),
         ('act', ctypes.c_int),
         ('b_scale', ctypes.c_float),
+        ('split', ctypes.c_int), ('split_ea', ctypes.c_int), ('split_eb', ctypes.c_int), ('range_flag', vp),
     ]
 
 

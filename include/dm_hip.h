@@ -265,6 +265,12 @@ typedef struct dm_gemm_desc {
   const float* res; int ld_res;
   int act;
   float b_scale;  /* 0: none; else multiplies B elements on load (B stored [n][k]) */
+  /* split = DM_SPLIT_FP16X2: products on the fp16 matrix cores from a two-way fp16 split of both
+   * operands (fp32-accurate), A scaled by 2^split_ea and B by 2^split_eb before the split (exact;
+   * choose them to keep the scaled operands well inside fp16's normal range), the result scaled back.
+   * |scaled element| > 65504 sets *range_flag (optional). 0 = fp32 MFMA. */
+  int split, split_ea, split_eb;
+  int* range_flag;
 } dm_gemm_desc;
 int dm_gemm(const dm_gemm_desc* d, void* stream);
 

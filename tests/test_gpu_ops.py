@@ -25,22 +25,27 @@ def _gemm_desc(**kw):
     return d
 
 
+SPLITS = [dict(), dict(split=2, split_ea=3, split_eb=-2)]  # fp32 MFMA; fp16x2 with power-of-two scales
+
+
+@pytest.mark.parametrize('sp', SPLITS)
 @pytest.mark.parametrize('M,N,K', [(64, 64, 32), (200, 136, 72), (256, 768, 256), (1024, 512, 128), (33, 40, 4)])
-def test_gemm_bt_exact(cuda, M, N, K):
+def test_gemm_bt_exact(cuda, M, N, K, sp):
     A = _ints((M, K), seed=1)
     B = _ints((N, K), seed=2)
     bias = _ints((N, ), seed=3)
     C = torch.empty((M, N), device=cuda)
     Ad, Bd, bd = A.to(cuda), B.to(cuda), bias.to(cuda)
     d = _gemm_desc(M=M, N=N, K=K, A=Ad.data_ptr(), lda=K, B=Bd.data_ptr(), ldb=K, C=C.data_ptr(), ldc=N,
-                   bias=bd.data_ptr())
+                   bias=bd.data_ptr(), **sp)
     dmhip.gemm(d, cuda)
     ref = (A.double() @ B.double().T + bias.double()).float()
     assert torch.equal(C.cpu(), ref)
 
 
+@pytest.mark.parametrize('sp', SPLITS)
 @pytest.mark.parametrize('M,N,K,Z1,Z2', [(256, 128, 256, 3, 2), (16, 64, 16, 4, 1), (100, 72, 100, 2, 3)])
-def test_gemm_batched_kn_alpha(cuda, M, N, K, Z1, Z2):
+def test_gemm_batched_kn_alpha(cuda, M, N, K, Z1, Z2, sp):
     A = _ints((Z1, Z2, M, K), seed=4)
     B = _ints((Z1, Z2, K, N), seed=5)
     C = torch.empty((Z1, Z2, M, N), device=cuda)
@@ -48,10 +53,53 @@ def test_gemm_batched_kn_alpha(cuda, M, N, K, Z1, Z2):
     d = _gemm_desc(M=M, N=N, K=K, Z1=Z1, Z2=Z2,
                    A=Ad.data_ptr(), a_s1=Z2 * M * K, a_s2=M * K, lda=K,
                    B=Bd.data_ptr(), b_s1=Z2 * K * N, b_s2=K * N, ldb=N, b_kn=1,
-                   C=C.data_ptr(), c_s1=Z2 * M * N, c_s2=M * N, ldc=N, alpha=0.5)
+                   C=C.data_ptr(), c_s1=Z2 * M * N, c_s2=M * N, ldc=N, alpha=0.5, **sp)
     dmhip.gemm(d, cuda)
     ref = ((A.double() * 0.5) @ B.double()).float()
     assert torch.equal(C.cpu(), ref)
+
+
+@pytest.mark.parametrize('case', ['qk', 'pv', 'xw'])
+def test_gemm_split_fp32_accuracy(cuda, case):
+    """fp16x2 GEMM with the plan's exponents (unet_exec.hip split_gemm) on the attention operand
+    distributions: error vs fp64 within 2x the fp32 MFMA kernel's (+ 1e-7 relative)."""
+    g = torch.Generator().manual_seed(7)
+    Z, M, N, K = 4, 256, 256, 256
+    if case == 'qk':  # S = (q * d^-1/2) k^T
+        A, B, kn, ea, eb, alpha = torch.randn((Z, M, K), generator=g), torch.randn((Z, N, K), generator=g), 0, 6, 6, K ** -0.5
+    elif case == 'pv':  # O = softmax(S) v, v stored [k][n]
+        A = torch.softmax(torch.randn((Z, M, K), generator=g) * 3, -1)
+        B, kn, ea, eb, alpha = torch.randn((Z, K, N), generator=g), 1, 14, 6, 1.0
+    else:  # x W^T with a U(+-1/sqrt(K)) weight
+        A = torch.randn((Z, M, K), generator=g)
+        B = (torch.rand((Z, N, K), generator=g) * 2 - 1) * K ** -0.5
+        kn, ea, alpha = 0, 6, 1.0
+        eb = 14 - int(torch.frexp(B.abs().max()).exponent)
+    ref = (A.double() * alpha) @ (B.double() if kn else B.double().transpose(1, 2))
+    errs = []
+    for sp in (dict(), dict(split=2, split_ea=ea, split_eb=eb)):
+        C = torch.empty((Z, M, N), device=cuda)
+        Ad, Bd = A.contiguous().to(cuda), B.contiguous().to(cuda)
+        d = _gemm_desc(M=M, N=N, K=K, Z1=Z, A=Ad.data_ptr(), a_s1=M * K, lda=K, B=Bd.data_ptr(), b_s1=K * N,
+                       ldb=N if kn else K, b_kn=kn, C=C.data_ptr(), c_s1=M * N, ldc=N, alpha=alpha, **sp)
+        dmhip.gemm(d, cuda)
+        errs.append((C.cpu().double() - ref).abs().max().item())
+    assert errs[1] < 2.0 * errs[0] + 1e-7 * ref.abs().max().item(), errs
+
+
+def test_gemm_split_range_flag(cuda):
+    """a scaled operand beyond 65504 raises the range flag; within range it stays clear."""
+    for big, flagged in ((1000.0, False), (1100.0, True)):  # x 2^6 -> 64000 / 70400
+        A = torch.randn((64, 32))
+        A[5, 7] = big
+        B = torch.randn((64, 32))
+        C = torch.empty((64, 64), device=cuda)
+        flag = torch.zeros(1, dtype=torch.int32, device=cuda)
+        Ad, Bd = A.to(cuda), B.to(cuda)
+        d = _gemm_desc(M=64, N=64, K=32, A=Ad.data_ptr(), lda=32, B=Bd.data_ptr(), ldb=32, C=C.data_ptr(), ldc=64,
+                       split=2, split_ea=6, split_eb=0, range_flag=flag.data_ptr())
+        dmhip.gemm(d, cuda)
+        assert bool(flag.item()) == flagged
 
 
 def test_gemm_silu_residual(cuda):
