@@ -13,7 +13,7 @@ import torch  # noqa: E402
 import dmhip  # noqa: E402
 
 
-def bench(name, M, N, K, Z1=1, Z2=1, b_kn=0, res=False, iters=20):
+def bench(name, M, N, K, Z1=1, Z2=1, b_kn=0, res=False, iters=20, split=False, pro=False, ea=6, eb=6):
     dev = torch.device('cuda', 0)
     A = torch.randn((Z1 * Z2, M, K), device=dev)
     B = torch.randn((Z1 * Z2, K, N) if b_kn else (Z1 * Z2, N, K), device=dev)
@@ -27,6 +27,11 @@ def bench(name, M, N, K, Z1=1, Z2=1, b_kn=0, res=False, iters=20):
     d.alpha = 1.0
     if res:
         d.res, d.ld_res = R.data_ptr(), N
+    if pro:  # GroupNorm affine prologue on A (the QKV projection), 256 rows per image
+        sc, sh = torch.rand((M // 256, K), device=dev) + 0.5, torch.rand((M // 256, K), device=dev) - 0.5
+        d.pro_scale, d.pro_shift, d.pro_rows = sc.data_ptr(), sh.data_ptr(), 256
+    if split:
+        d.split, d.split_ea, d.split_eb = 2, ea, eb
     for _ in range(3):
         dmhip.gemm(d, dev)
     torch.cuda.synchronize()
@@ -38,16 +43,15 @@ def bench(name, M, N, K, Z1=1, Z2=1, b_kn=0, res=False, iters=20):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / iters
     tf = 2.0 * Z1 * Z2 * M * N * K / ms / 1e9
-    print(f'{name:16s} {ms:8.4f} ms {tf:6.1f} TF/s', flush=True)
+    print(f'{name:16s} {"fp16x2" if split else "fp32":7s} {ms:8.4f} ms {tf:6.1f} TF/s', flush=True)
 
 
 if __name__ == '__main__':
     dmhip.load()
-    bench('qkv_k256', 65536, 768, 256)
-    bench('qkv_k512', 65536, 768, 512)
-    bench('qkv_k1024', 65536, 768, 1024)
-    bench('proj_res', 65536, 256, 256, res=True)
-    bench('proj_nores', 65536, 256, 256)
-    bench('S', 256, 256, 256, Z1=256)
-    bench('PV_kn', 256, 256, 256, Z1=256, b_kn=1)
-    bench('big_4096', 4096, 4096, 4096, iters=5)
+    for sp in (False, True):
+        bench('qkv_gn_k256', 65536, 768, 256, pro=True, split=sp)
+        bench('qkv_k256', 65536, 768, 256, split=sp)
+        bench('proj_res', 65536, 256, 256, res=True, split=sp)
+        bench('S', 256, 256, 256, Z1=256, split=sp)
+        bench('PV_kn', 256, 256, 256, Z1=256, b_kn=1, split=sp, ea=14)
+        bench('big_4096', 4096, 4096, 4096, iters=5, split=sp)
