@@ -285,6 +285,7 @@ int conv2d_igemm(const ConvArgs& a, hipStream_t st) {
                                                  "whole 64-pixel chunks and groups within 32 channels");
   DM_REQUIRE(!a.pro_scale || (pick >= 3 && a.pro_shift && aligned16(a.pro_scale) && aligned16(a.pro_shift)),
              "conv: the GroupNorm prologue needs a halo-patch shape (3x3 stride 1 / upsample, whole-row tiles)");
+  if (pick >= 3 && a.taps == 1) return conv2d_patch3(a, pick + 1, PatchGeom{}, st);  // MODE 3 (split 1x1)
   if (pick >= 3) {
     PatchGeom g;
     conv_patch_pick(a, g);
@@ -308,6 +309,10 @@ int conv2d_igemm(const ConvArgs& a, hipStream_t st) {
 // falls back to im2col when the shape does not tile.
 int conv_pick(const ConvArgs& a) {
   if (a.tile >= 1 && a.tile <= 3) return a.tile - 1;
+  if (conv_pw_ok(a)) {  // split 1x1: 128x128 tiles when they still give >= 2 blocks per CU, else 128x64
+    const long M = (long)a.B * a.Hout * a.Wout;
+    return (a.Cout >= 128 && ((M + 127) / 128) * ((a.Cout + 127) / 128) >= 512) ? 3 : 4;
+  }
   PatchGeom g;
   const int p = conv_patch_pick(a, g);
   if (p) return p - 1;
@@ -324,6 +329,7 @@ bool conv_can_emit_gn(const ConvArgs& a) {
   const int pick = conv_pick(a);
   if (pick != 3 && pick != 4) return false;  // 128-row patch tiles: every wave owns 64 rows
   if (a.upsample || (a.ksplit > 1)) return false;
+  if (a.taps == 1 && !conv_pw_ok(a)) return false;
   if ((a.Hout * a.Wout) % 64 != 0 || a.gn_G <= 0 || a.Cout % a.gn_G != 0) return false;
   const int cpg = a.Cout / a.gn_G;
   return 32 % cpg == 0;
@@ -337,6 +343,9 @@ std::string conv_label(const ConvArgs& a) {
   const int p = conv_pick(a);
   std::string s = names[p];
   if (p < 3) s += "," + std::to_string(conv_mode(a)) + ">";  // <BM,BN,WM,WN,MODE>
+  if (p >= 3 && a.taps == 1)  // split 1x1: conv_patch3_kernel<128,BN,64,WN,3,128,PRO,false,2>
+    return std::string(p == 3 ? "conv_patch3_kernel<128,128,64,64,3,128," : "conv_patch3_kernel<128,64,64,32,3,128,") +
+           (a.pro_scale ? "true" : "false") + ",false,2>";
   if (p >= 3) {  // <BM,BN,WM,WN,MODE,MAXP,PRO,KSPLIT>; MAXP 288 (208 split-bf16) for 128-row tiles, 160 for 64-row
     PatchGeom g;
     conv_patch_pick(a, g);

@@ -36,8 +36,8 @@ __device__ __forceinline__ void conv_patch_epilogue(const ConvArgs& a, f16v (&ac
 
   // SUB rows scatter to output pixel (2iy + py, 2ix + px)
   const bool block_one_image = (HWo % BM) == 0;
-  // GroupNorm statistics of the stored values (MODE 0, WM = 64: this wave's rows are one chunk)
-  const bool emit = MODE == 0 && WM == 64 && a.gn_part != nullptr;
+  // GroupNorm statistics of the stored values (MODE 0 / 3, WM = 64: this wave's rows are one chunk)
+  const bool emit = (MODE == 0 || MODE == 3) && WM == 64 && a.gn_part != nullptr;
   const int wrow0 = m0 + wm * WM;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {

@@ -392,6 +392,9 @@ int conv_patch_pick(const ConvArgs& a, PatchGeom& g) {
 // picker's last resort) must fit, which depends on the layer shape only, so the fp32 / split choice
 // of a layer never changes with B and results stay batch-invariant.
 bool conv_split_eligible(const ConvArgs& a) {
+  if (a.taps == 1)  // 1x1 / static-weight GEMM (MODE 3 of the split kernel)
+    return a.stride == 1 && !a.upsample && a.Cin2 == 0 && a.Cin1 % 32 == 0 && a.K == a.Cin1 && a.Hout == a.Hin &&
+           a.Wout == a.Win;
   if (a.taps != 9 || a.stride != 1 || a.upsample == 1 || a.Cin1 % 16 != 0 || a.Cin2 % 16 != 0) return false;
   PatchGeom g;
   return conv_patch_geom(a, 64, g) && g.P <= kPatch3Max64;

@@ -65,8 +65,14 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
   constexpr int TM = WM / 32, TN = WN / 32;
   static_assert((BM / WM) * NWN == 4, "4 waves per block");
   constexpr bool UP = MODE == 1, SUB = MODE == 2;
-  constexpr int NTAP = SUB ? 4 : 9;
-  constexpr int PATCH = MAXP * kSPitch;
+  // MODE 3: 1x1 (pointwise) conv / GEMM with static weights (the attention block's qkv and proj).
+  // The "patch" is the tile's own BM rows; a chunk is 32 channels stored as two 16-deep slices per
+  // row, which the two "taps" read.
+  constexpr bool PW1 = MODE == 3;
+  constexpr int NTAP = SUB ? 4 : (PW1 ? 2 : 9);
+  constexpr int CH = PW1 ? 2 * kSK : kSK;                    // input channels per chunk
+  constexpr int PROW = PW1 ? 2 * kSRow + 8 : kSPitch;        // LDS row pitch (an odd number of 16-B slots)
+  constexpr int PATCH = MAXP * PROW;
   __shared__ __attribute__((aligned(16))) elem patch[2 * PATCH];
 
   const int Ho = SUB ? a.Hin : a.Hout, Wo = SUB ? a.Win : a.Wout;
@@ -101,15 +107,23 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
   // staging: two threads per pixel / row, 8 channels each
   const int srow = t >> 1, shalf = t & 1;
 
-  // ---- patch loader geometry (pixel p = srow + 128 j)
-  constexpr int PJ = (MAXP + 127) / 128;
-  const int PHW = g.PH * g.PW;
+  // ---- patch loader geometry (pixel p = srow + 128 j; MODE 3: row srow, 16-channel slice j)
+  constexpr int PJ = PW1 ? 2 : (MAXP + 127) / 128;
   const float* psrc[PJ];
   bool pok[PJ];
   int pimg[PJ];
   const int iy_base = UP ? (y0 >> 1) - 1 : y0 - 1;
 #pragma unroll
   for (int j = 0; j < PJ; ++j) {
+    if constexpr (PW1) {
+      const int m = m0 + srow;
+      const int mc = min(m, M - 1);  // rows >= M: clamped, never stored
+      pok[j] = m < M;
+      pimg[j] = mc / HWo;
+      psrc[j] = a.x1 + (size_t)mc * a.x1_pitch + kSK * j + 8 * shalf;
+      continue;
+    }
+    const int PHW = g.PH * g.PW;
     const int p = srow + 128 * j;
     const int img = p / PHW;
     const int rem = p - img * PHW;
@@ -151,9 +165,13 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
 
   // ---- A-fragment patch coordinates of this lane's rows
   int fy[TM], fx[TM], fimg[TM];
-  const int tile_rows = g.TH * Wo;
+  const int tile_rows = PW1 ? 1 : g.TH * Wo;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
+    if constexpr (PW1) {
+      fy[i] = fx[i] = fimg[i] = 0;
+      continue;
+    }
     const int ml = wm * WM + i * 32 + lr;
     fimg[i] = ml / tile_rows;
     const int rem = ml - fimg[i] * tile_rows;
@@ -167,24 +185,26 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
   f4 rp[PJ][2];
   f4 rs[PJ][2][2];
   auto load_patch = [&](int chunk) {
-    const int co = chunk * kSK;
+    const int co = chunk * CH;
 #pragma unroll
     for (int j = 0; j < PJ; ++j) {
       rp[j][0] = *reinterpret_cast<const f4*>(psrc[j] + co);
       rp[j][1] = *reinterpret_cast<const f4*>(psrc[j] + co + 4);
     }
     if (PRO) {
-      const int cc = co + 8 * shalf;
 #pragma unroll
       for (int j = 0; j < PJ; ++j)
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
+          const int cc = co + 8 * shalf + (PW1 ? kSK * j : 0);
           rs[j][h][0] = *reinterpret_cast<const f4*>(a.pro_scale + (size_t)pimg[j] * a.Cin1 + cc + 4 * h);
           rs[j][h][1] = *reinterpret_cast<const f4*>(a.pro_shift + (size_t)pimg[j] * a.Cin1 + cc + 4 * h);
         }
     }
   };
   // GroupNorm + SiLU prologue on patch registers j in [j0, j1): silu(x * scale[b][c] + shift[b][c])
+  // (pro_nosilu: GroupNorm alone, the attention block's norm before qkv)
+  const bool pro_silu = !a.pro_nosilu;
   auto transform = [&](int j0, int j1) {
 #pragma unroll
     for (int j = 0; j < PJ; ++j) {
@@ -192,7 +212,10 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
 #pragma unroll
         for (int h = 0; h < 2; ++h)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) rp[j][h][q] = silu_fast(rp[j][h][q] * rs[j][h][0][q] + rs[j][h][1][q]);
+          for (int q = 0; q < 4; ++q) {
+            const float v = rp[j][h][q] * rs[j][h][0][q] + rs[j][h][1][q];
+            rp[j][h][q] = pro_silu ? silu_fast(v) : v;
+          }
       }
     }
   };
@@ -203,14 +226,15 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
     const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < PJ; ++j) {
-      const int p = srow + 128 * j;
-      if (j * 128 < MAXP && p < MAXP) {
+      const int p = PW1 ? srow : srow + 128 * j;
+      if (PW1 || (j * 128 < MAXP && p < MAXP)) {
         vec pc[NP];
         const bool z = PRO && !pok[j];
         S::split(z ? zero4 : rp[j][0], z ? zero4 : rp[j][1], pc, bad);
+        const int col = PW1 ? j * kSRow : 0;
 #pragma unroll
         for (int q = 0; q < NP; ++q)
-          *reinterpret_cast<vec*>(dst + p * kSPitch + shalf * kGrp + q * 8) = pc[q];
+          *reinterpret_cast<vec*>(dst + p * PROW + col + shalf * kGrp + q * 8) = pc[q];
       }
     }
   };
@@ -238,6 +262,10 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
     int abase[TM];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
+      if constexpr (PW1) {  // row of this lane, slice kx of the chunk
+        abase[i] = (wm * WM + i * 32 + lr) * PROW + kx * kSRow + lh * kGrp;
+        continue;
+      }
       int pr, pc;
       if (UP) {
         pr = ((fy[i] + ky - 1) >> 1) + 1;
@@ -251,7 +279,7 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
     compute(patch + pbuf * PATCH, abase, bv);
   };
 
-  const int nchunks = a.Cin1 / kSK;
+  const int nchunks = a.Cin1 / CH;
   const int c_begin = KSPLIT ? split * nchunks / ksplit : 0;
   const int c_end = KSPLIT ? (split + 1) * nchunks / ksplit : nchunks;
   const int kt_begin = c_begin * NTAP, kt_end = c_end * NTAP;
@@ -283,6 +311,8 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
       }
       if (SUB)
         compute_tap(py + (tap >> 1), px + (tap & 1), c & 1, bq[slot]);
+      else if (PW1)
+        compute_tap(0, tap, c & 1, bq[slot]);
       else
         compute_tap(tap / 3, tap % 3, c & 1, bq[slot]);
       load_b(bq[slot], min(kt + WD, kt_end - 1));
@@ -350,6 +380,22 @@ void launch3_mode(const ConvArgs& a, const PatchGeom& g, int blocks, hipStream_t
   else
     hipLaunchKernelGGL((conv_patch3_kernel<BM, BN, WM, WN, MODE, MAXP, false, false, NP>), dim3(blocks), dim3(256),
                        0, st, a, g);
+}
+
+// MODE 3 (1x1 / static-weight GEMM), 128-row tiles, fp16x2
+template <int BN, int WN>
+int launch_pw(const ConvArgs& a, hipStream_t st) {
+  const int M = a.B * a.Hout * a.Wout;
+  const int blocks = ceil_div(M, 128) * ceil_div(a.Cout, BN);
+  PatchGeom g{};
+  if (a.pro_scale)
+    hipLaunchKernelGGL((conv_patch3_kernel<128, BN, 64, WN, 3, 128, true, false, 2>), dim3(blocks), dim3(256), 0, st,
+                       a, g);
+  else
+    hipLaunchKernelGGL((conv_patch3_kernel<128, BN, 64, WN, 3, 128, false, false, 2>), dim3(blocks), dim3(256), 0,
+                       st, a, g);
+  DM_LAUNCH_CHECK();
+  return DM_OK;
 }
 
 template <int BM, int BN, int WM, int WN, int MAXP, int NP>
@@ -453,7 +499,16 @@ bool conv_patch3_ok(const ConvArgs& a, int which, const PatchGeom& g) {
   return g.P <= (which == 6 ? kPatch3Max64 : kPatch3Max128);
 }
 
+bool conv_pw_ok(const ConvArgs& a) {
+  return a.taps == 1 && a.ws && a.ws_np == 2 && a.ws_rowscale && a.stride == 1 && !a.upsample && a.Cin2 == 0 &&
+         a.Cin1 % (2 * kSK) == 0 && a.K == a.Cin1 && a.Hout == a.Hin && a.Wout == a.Win && a.ksplit <= 1;
+}
+
 int conv2d_patch3(const ConvArgs& a, int which, const PatchGeom& g, hipStream_t st) {
+  if (a.taps == 1) {
+    DM_REQUIRE(conv_pw_ok(a), "conv: the split 1x1 path needs fp16x2 weights, stride 1, K = Cin1 % 32 == 0");
+    return which == 4 ? launch_pw<128, 64>(a, st) : launch_pw<64, 32>(a, st);
+  }
   if (a.ws_np == 2) {
     switch (which) {
       case 4: return launch3<128, 128, 64, 64, kPatch3Max128, 2>(a, g, st);

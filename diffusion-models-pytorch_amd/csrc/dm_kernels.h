@@ -36,6 +36,7 @@ struct ConvArgs {
   // (GroupNorm + SiLU of the ResBlock, fused into the conv's input load)
   const float* pro_scale;
   const float* pro_shift;
+  int pro_nosilu;  // 1: the prologue is the affine alone (no SiLU)
   // split-K over input-channel chunks (halo-patch kernel, MODE 0/1): ksplit > 1 writes raw partial
   // sums to kpart [ksplit][M][Cout] and a reduction pass sums them in split order and applies the
   // epilogue. The split count is fixed per layer shape (not per batch), so results stay batch-invariant.
@@ -171,6 +172,8 @@ int conv_patch_pick(const ConvArgs& a, PatchGeom& g);
 int conv2d_patch(const ConvArgs& a, int which, const PatchGeom& g, hipStream_t st);
 // split-bf16 halo-patch kernel (conv_patch3.hip): whether it takes this shape / tile, and its launcher
 bool conv_patch3_ok(const ConvArgs& a, int which, const PatchGeom& g);
+// 1x1 convs / static-weight GEMMs on the fp16x2 split kernel (conv_patch3_kernel MODE 3)
+bool conv_pw_ok(const ConvArgs& a);
 bool conv_split_eligible(const ConvArgs& a);
 int conv2d_patch3(const ConvArgs& a, int which, const PatchGeom& g, hipStream_t st);
 int conv_splitk_reduce(const ConvArgs& a, hipStream_t st);

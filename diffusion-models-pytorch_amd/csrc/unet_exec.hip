@@ -199,7 +199,9 @@ void UNetModel::split_for(ConvArgs& c) {
   c.ws_rowscale = nullptr;
   c.range_flag = nullptr;
   if (!conv_math || !conv_split_eligible(c)) return;
+  if (c.taps == 1 && conv_math != 2) return;  // the split 1x1 path is fp16x2 only
   const int nmat = c.upsample == 2 ? 4 : 1;
+  const int ntap = c.upsample == 2 ? 4 : c.taps;
   auto key = std::make_pair(c.w, conv_math);
   auto it = split_w.find(key);
   void* p = nullptr;
@@ -208,7 +210,7 @@ void UNetModel::split_for(ConvArgs& c) {
   } else {
     const size_t nb = split_conv_weights_bytes(nmat, c.Cout, c.K, conv_math);
     if (hipMalloc(&p, nb) != hipSuccess) return;
-    if (split_conv_weights(c.w, nmat, c.Cout, c.K, c.Cin1, c.upsample == 2 ? 4 : 9, conv_math, p, nullptr) !=
+    if (split_conv_weights(c.w, nmat, c.Cout, c.K, c.Cin1, ntap, conv_math, p, nullptr) !=
             DM_OK ||
         hipDeviceSynchronize() != hipSuccess) {
       (void)hipFree(p);
@@ -682,7 +684,7 @@ int UNetModel::build_plan(int B, int H, int W) {
   float* kpart_ws = nullptr;
   size_t kpart_floats = 0;
   auto maybe_split = [&](ConvArgs& c) {
-    if (c.gn_part || c.upsample == 2 || c.Hout * c.Wout > 16 || conv_pick(c) < 3) return;
+    if (c.gn_part || c.upsample == 2 || c.taps != 9 || c.Hout * c.Wout > 16 || conv_pick(c) < 3) return;
     const int ks = std::min(4, c.Cin1 / 32);
     if (ks < 2) return;
     const size_t need = (size_t)ks * c.B * c.Hout * c.Wout * c.Cout;
@@ -915,8 +917,18 @@ int UNetModel::build_plan(int B, int H, int W) {
       gq.A = xin.p; gq.lda = xin.pitch; gq.Bm = P(p.wqkv); gq.ldb = C; gq.C = qkv; gq.ldc = 3 * C;
       gq.alpha = 1.f; gq.bias = P(p.bqkv);
       gq.pro_scale = gsc; gq.pro_shift = gsh; gq.pro_rows = hw;
-      split_gemm(gq, 6, gq.Bm, (size_t)3 * C * C);
-      add_gemm(gq);
+      // fp16x2: qkv = 1x1 conv of GroupNorm(x) on the split conv kernel (MODE 3, pre-split weights)
+      ConvArgs cq{};
+      cq.x1 = xin.p; cq.x1_pitch = xin.pitch; cq.Cin1 = C; cq.Hin = Hi; cq.Win = Wi; cq.taps = 1; cq.stride = 1;
+      cq.w = P(p.wqkv); cq.K = C; cq.y = qkv; cq.y_pitch = 3 * C; cq.Cout = 3 * C; cq.B = B; cq.Hout = Hi;
+      cq.Wout = Wi; cq.bias = P(p.bqkv); cq.pro_scale = gsc; cq.pro_shift = gsh; cq.pro_nosilu = 1;
+      split_for(cq);
+      if (conv_pw_ok(cq)) {
+        add_conv(cq);
+      } else {
+        split_gemm(gq, 6, gq.Bm, (size_t)3 * C * C);
+        add_gemm(gq);
+      }
       // head h of q / k / v: columns q0 + h * hs, k0 + h * hs, v0 + h * hs of the qkv rows
       // (q | k | v blocks: modules.py:92-94 and ADM QKVAttention; per-head [q; k; v]: QKVAttentionLegacy)
       const int hs = p.legacy ? 3 * Dh : Dh;
@@ -944,9 +956,19 @@ int UNetModel::build_plan(int B, int H, int W) {
       gp.M = B * hw; gp.N = C; gp.K = C; gp.Z1 = 1; gp.Z2 = 1;
       gp.A = Ob; gp.lda = C; gp.Bm = P(p.wproj); gp.ldb = C; gp.C = y.p; gp.ldc = y.pitch;
       gp.alpha = 1.f; gp.bias = P(p.bproj); gp.res = xin.p; gp.ld_res = xin.pitch;
-      split_gemm(gp, 6, gp.Bm, (size_t)C * C);
-      emit_gemm(gp, y);
-      add_gemm(gp);
+      ConvArgs cp{};
+      cp.x1 = Ob; cp.x1_pitch = C; cp.Cin1 = C; cp.Hin = Hi; cp.Win = Wi; cp.taps = 1; cp.stride = 1;
+      cp.w = P(p.wproj); cp.K = C; cp.y = y.p; cp.y_pitch = y.pitch; cp.Cout = C; cp.B = B; cp.Hout = Hi;
+      cp.Wout = Wi; cp.bias = P(p.bproj); cp.res = xin.p; cp.res_pitch = xin.pitch;
+      split_for(cp);
+      if (conv_pw_ok(cp)) {
+        emit_conv(cp, y);
+        add_conv(cp);
+      } else {
+        split_gemm(gp, 6, gp.Bm, (size_t)C * C);
+        emit_gemm(gp, y);
+        add_gemm(gp);
+      }
     } else if (n.idx < 0) {
       // resampling without a conv (adm/unet.py:126-128 nearest-2x, :153-155 avg-pool)
       const bool down = n.kind == N_DOWN;

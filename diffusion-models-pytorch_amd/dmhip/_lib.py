@@ -90,7 +90,7 @@ class ConvDesc(ctypes.Structure):
         ('res', vp), ('res_pitch', ctypes.c_int),
         ('tile', ctypes.c_int),
         ('pro_scale', vp), ('pro_shift', vp),
-        ('w_split', vp), ('w_split_kind', ctypes.c_int), ('range_flag', vp),
+        ('w_split', vp), ('w_split_kind', ctypes.c_int), ('range_flag', vp), ('pro_nosilu', ctypes.c_int),
     ]
 
 

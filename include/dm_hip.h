@@ -252,7 +252,10 @@ typedef struct dm_conv_desc {
   const void* w_split;
   int w_split_kind;  /* DM_SPLIT_BF16X3 or DM_SPLIT_FP16X2 */
   int* range_flag;   /* optional device int, set to 1 when an fp16x2 conv meets |x| > 65504 */
+  int pro_nosilu;    /* 1: the input prologue is x * pro_scale + pro_shift alone (no SiLU) */
 } dm_conv_desc;
+/* 1x1 convs (taps 1, K = Cin, Cin % 32 == 0) with DM_SPLIT_FP16X2 weights run on the split kernel
+ * with the same prologue / epilogue options: the static-weight GEMMs of the attention blocks. */
 int dm_conv2d_nhwc(const dm_conv_desc* d, void* stream);
 
 typedef struct dm_gemm_desc {

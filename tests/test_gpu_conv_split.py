@@ -136,3 +136,40 @@ def test_fp16x2_range_flag(cuda, peak, flagged):
     assert bool(flag.item()) == flagged
     if not flagged:
         assert (y.cpu().double() - _nhwc(ref)).abs().max().item() < 4e-6 * ref.abs().max().item()
+
+
+@pytest.mark.parametrize('B,Cin,Cout,H', [(2, 64, 96, 16), (3, 256, 768, 16), (5, 32, 64, 4), (1, 128, 256, 8),
+                                          (3, 96, 40, 5)])
+def test_split_pointwise_exact(cuda, B, Cin, Cout, H):
+    """1x1 conv on the split kernel (MODE 3, the attention qkv / proj): bias, residual, output pitch and
+    ragged M (rows not a multiple of the 128-row tile) bit-exact on integer operands."""
+    x = _ints((B, Cin, H, H), -2, 3, seed=30)
+    w = _ints((Cout, Cin, 1, 1), -2, 3, seed=31)
+    b = _ints((Cout, ), seed=32)
+    res = _ints((B, Cout, H, H), seed=33)
+    ref = (F.conv2d(x.double(), w.double(), b.double()) + res.double()).float()
+    y = _run_conv(cuda, _nhwc(x).to(cuda), _pack(w, cuda), Cout, H, H, 1, bias=b.to(cuda), res=_nhwc(res).to(cuda),
+                  y_pitch=Cout + 8, split='fp16x2')
+    assert torch.equal(y[..., :Cout].cpu(), _nhwc(ref))
+    assert torch.isnan(y[..., Cout:]).all()
+
+
+@pytest.mark.parametrize('silu', [0, 1])
+def test_split_pointwise_groupnorm_accuracy(cuda, silu):
+    """GroupNorm (+ optional SiLU) prologue + 1x1 conv on random data: fp32-level error vs fp64."""
+    B, C, Cout, H = 4, 256, 768, 16
+    g = torch.Generator().manual_seed(34)
+    x = torch.randn((B, C, H, H), generator=g) * 2 + 0.3
+    gamma, beta = torch.randn(C, generator=g), torch.randn(C, generator=g)
+    w = torch.randn((Cout, C, 1, 1), generator=g) * C ** -0.5
+    b = torch.randn(Cout, generator=g) * 0.01
+    a = F.group_norm(x.double(), 32, gamma.double(), beta.double(), 1e-5)
+    if silu:
+        a = F.silu(a)
+    ref = _nhwc(F.conv2d(a, w.double(), b.double()))
+    xd = _nhwc(x).to(cuda)
+    pro = dmhip.groupnorm_affine(xd, B, H * H, C, 32, 1e-5, gamma.to(cuda), beta.to(cuda))
+    y = _run_conv(cuda, xd, _pack(w, cuda), Cout, H, H, 1, bias=b.to(cuda), pro=pro, pro_nosilu=1 - silu,
+                  split='fp16x2')
+    err = (y.cpu().double() - ref).abs().max().item()
+    assert err < 2e-6 * ref.abs().max().item(), err

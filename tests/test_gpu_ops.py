@@ -127,7 +127,7 @@ def _pack(w, cuda, K=None, col0=0, out=None):
 
 def _run_conv(cuda, x_nhwc, w_packed, Cout, Hout, Wout, taps, stride=1, upsample=0, bias=None, rowvec=None,
               res=None, x2=None, Cin2=0, y_pitch=None, x_pitch=None, tile=0, pro=None, split=False,
-              range_flag=None):
+              range_flag=None, pro_nosilu=0):
     B, Hin, Win, Cin = x_nhwc.shape[0], x_nhwc.shape[1], x_nhwc.shape[2], x_nhwc.shape[3]
     x_pitch = x_pitch or Cin
     y_pitch = y_pitch or Cout
@@ -146,9 +146,10 @@ def _run_conv(cuda, x_nhwc, w_packed, Cout, Hout, Wout, taps, stride=1, upsample
     d.tile = tile
     if pro is not None:
         d.pro_scale, d.pro_shift = pro[0].data_ptr(), pro[1].data_ptr()
+        d.pro_nosilu = pro_nosilu
     if split:  # split weights (True = 'bf16x3', or 'fp16x2'): halo-patch shapes run conv_patch3_kernel
         kind = dmhip.SPLIT_FP16X2 if split == 'fp16x2' else dmhip.SPLIT_BF16X3
-        nmat, ntap = (4, 4) if upsample == 2 else (1, 9)
+        nmat, ntap = (4, 4) if upsample == 2 else (1, taps)
         ws = dmhip.pack_conv_weight_split(w_packed, nmat, Cin, ntap, kind)
         d.w_split, d.w_split_kind = ws.data_ptr(), kind
         if range_flag is not None:
