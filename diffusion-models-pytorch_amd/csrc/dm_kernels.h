@@ -201,7 +201,9 @@ int timestep_embed(const int64_t* t, int B, int dim, int kind, const float* freq
 int softmax_rows(float* x, long rows, int L, int ld, hipStream_t st);
 int conv3x3_small_in(const float* x, int B, int Cin, int H, int W, const float* w, const float* bias,
                      int Cout, const View& y, hipStream_t st);
-int conv3x3_small_out(const View& x, const float* w, const float* bias, int Cout, float* y, hipStream_t st,
+// last conv weights torch [Cout][Cin][3][3] -> [9][Cin][CO], CO = 4 (Cout <= 4) or 8; wp holds 9 * Cin * CO floats
+int small_out_pack(const float* w, int Cout, int Cin, float* wp, hipStream_t st);
+int conv3x3_small_out(const View& x, const float* wp, const float* bias, int Cout, float* y, hipStream_t st,
                       const float* pro_scale = nullptr, const float* pro_shift = nullptr);
 int sampler_step(const StepArgs& s, hipStream_t st);
 int nchw_to_nhwc(const float* x, int B, int C, int HW, float* y, int y_pitch, hipStream_t st);

@@ -119,23 +119,27 @@ __global__ void __launch_bounds__(256) conv3x3_small_in_kernel(const float* __re
 // chunk the (TH+2) x (TW+2) halo patch and the chunk's weights ([tap][c][8]) are
 // staged in LDS; each thread accumulates its Cout outputs from the patch.
 constexpr int kSoTW = 32, kSoTH = 8, kSoPP = (kSoTH + 2) * (kSoTW + 2), kSoLD = 36;
+// Last conv (Cout <= 8): one output pixel per thread, CO = Cout rounded up to 4 accumulators. The
+// input patch (GroupNorm + SiLU applied) is staged in LDS per 32-channel chunk; the weights come
+// pre-packed [tap][Cin][CO] (small_out_pack) and are read with wave-uniform addresses, so they are
+// scalar loads (constant cache, SGPR operands) rather than LDS traffic.
+template <int CO>
 __global__ void __launch_bounds__(256) conv3x3_small_out_kernel(const float* __restrict__ x, int B, int H, int W,
-                                                                int Cin, int pitch, const float* __restrict__ w,
+                                                                int Cin, int pitch, const float* __restrict__ wp,
                                                                 const float* __restrict__ bias, int Cout,
                                                                 float* __restrict__ y,
                                                                 const float* __restrict__ pro_scale,
                                                                 const float* __restrict__ pro_shift) {
   __shared__ __attribute__((aligned(16))) float patch[kSoPP * kSoLD];
-  __shared__ __attribute__((aligned(16))) float wl[9 * 32 * 8];
   const int tiles_x = ceil_div(W, kSoTW), tiles_y = ceil_div(H, kSoTH);
   const int b = blockIdx.x / (tiles_x * tiles_y);
   const int trem = blockIdx.x - b * tiles_x * tiles_y;
   const int ty0 = (trem / tiles_x) * kSoTH, tx0 = (trem % tiles_x) * kSoTW;
   const int t = threadIdx.x;
   const int py = t / kSoTW, px = t % kSoTW;
-  float acc[8];
+  float acc[CO];
 #pragma unroll
-  for (int c = 0; c < 8; ++c) acc[c] = 0.f;
+  for (int c = 0; c < CO; ++c) acc[c] = 0.f;
   for (int c0 = 0; c0 < Cin; c0 += 32) {
     __syncthreads();
     for (int i = t; i < kSoPP * 8; i += blockDim.x) {
@@ -147,41 +151,42 @@ __global__ void __launch_bounds__(256) conv3x3_small_out_kernel(const float* __r
         if (pro_scale) {  // GroupNorm + SiLU of last_conv (models/unet.py:115-119), padding stays 0
           const float4 sc = *reinterpret_cast<const float4*>(pro_scale + (size_t)b * Cin + c0 + 4 * c4);
           const float4 sh = *reinterpret_cast<const float4*>(pro_shift + (size_t)b * Cin + c0 + 4 * c4);
-          v.x = silu_f(v.x * sc.x + sh.x); v.y = silu_f(v.y * sc.y + sh.y);
-          v.z = silu_f(v.z * sc.z + sh.z); v.w = silu_f(v.w * sc.w + sh.w);
+          v.x = silu_fast(v.x * sc.x + sh.x); v.y = silu_fast(v.y * sc.y + sh.y);
+          v.z = silu_fast(v.z * sc.z + sh.z); v.w = silu_fast(v.w * sc.w + sh.w);
         }
       }
       *reinterpret_cast<float4*>(patch + p * kSoLD + 4 * c4) = v;
     }
-    for (int i = t; i < 9 * 32 * 8; i += blockDim.x) {
-      const int co = i & 7, c = (i >> 3) & 31, tap = i >> 8;
-      wl[i] = (co < Cout && c0 + c < Cin) ? w[((size_t)co * Cin + c0 + c) * 9 + tap] : 0.f;
-    }
     __syncthreads();
-#pragma unroll 1
+#pragma unroll 3
     for (int tap = 0; tap < 9; ++tap) {
       const float* pr = patch + ((py + tap / 3) * (kSoTW + 2) + px + tap % 3) * kSoLD;
-      const float* wt = wl + tap * 256;
+      const float* wt = wp + ((size_t)tap * Cin + c0) * CO;  // wave-uniform
 #pragma unroll
       for (int c4 = 0; c4 < 8; ++c4) {
         const float4 v = *reinterpret_cast<const float4*>(pr + 4 * c4);
         const float vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float4 wa = *reinterpret_cast<const float4*>(wt + (4 * c4 + q) * 8);
-          const float4 wb = *reinterpret_cast<const float4*>(wt + (4 * c4 + q) * 8 + 4);
-          acc[0] += vv[q] * wa.x; acc[1] += vv[q] * wa.y; acc[2] += vv[q] * wa.z; acc[3] += vv[q] * wa.w;
-          acc[4] += vv[q] * wb.x; acc[5] += vv[q] * wb.y; acc[6] += vv[q] * wb.z; acc[7] += vv[q] * wb.w;
-        }
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int co = 0; co < CO; ++co) acc[co] = fmaf(vv[q], wt[(4 * c4 + q) * CO + co], acc[co]);
       }
     }
   }
   const int oy = ty0 + py, ox = tx0 + px;
   if (oy < H && ox < W) {
 #pragma unroll
-    for (int c = 0; c < 8; ++c)
+    for (int c = 0; c < CO; ++c)
       if (c < Cout) y[(((size_t)b * Cout + c) * H + oy) * W + ox] = acc[c] + bias[c];
   }
+}
+
+// torch [Cout][Cin][3][3] -> [9][Cin][CO] (zero-padded to CO outputs)
+__global__ void small_out_pack_kernel(const float* w, int Cout, int Cin, int CO, float* wp) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 9 * Cin * CO) return;
+  const int co = i % CO, c = (i / CO) % Cin, tap = i / (CO * Cin);
+  wp[i] = co < Cout ? w[((size_t)co * Cin + c) * 9 + tap] : 0.f;
 }
 
 __global__ void sampler_step_kernel(StepArgs s) {
@@ -412,14 +417,26 @@ int conv3x3_small_in(const float* x, int B, int Cin, int H, int W, const float* 
   return DM_OK;
 }
 
-int conv3x3_small_out(const View& x, const float* w, const float* bias, int Cout, float* y, hipStream_t st,
+int small_out_pack(const float* w, int Cout, int Cin, float* wp, hipStream_t st) {
+  DM_REQUIRE(Cout >= 1 && Cout <= 8 && Cin > 0, "last conv: Cout out of range");
+  const int CO = Cout <= 4 ? 4 : 8;
+  hipLaunchKernelGGL(small_out_pack_kernel, dim3((9 * Cin * CO + 255) / 256), dim3(256), 0, st, w, Cout, Cin, CO, wp);
+  DM_LAUNCH_CHECK();
+  return DM_OK;
+}
+
+int conv3x3_small_out(const View& x, const float* wp, const float* bias, int Cout, float* y, hipStream_t st,
                       const float* pro_scale, const float* pro_shift) {
   DM_REQUIRE(Cout >= 1 && Cout <= 8, "last conv: Cout out of range");
-  DM_REQUIRE(x.C % 4 == 0 && x.pitch % 4 == 0, "last conv: channel alignment");
+  DM_REQUIRE(x.C % 32 == 0 && x.pitch % 4 == 0, "last conv: Cin must be a multiple of 32");
   DM_REQUIRE((reinterpret_cast<uintptr_t>(x.p) & 15) == 0, "last conv: input must be 16-byte aligned");
   const long tiles = (long)x.B * ceil_div(x.H, kSoTH) * ceil_div(x.W, kSoTW);
-  hipLaunchKernelGGL(conv3x3_small_out_kernel, dim3((unsigned)tiles), dim3(256), 0, st, x.p, x.B, x.H, x.W, x.C,
-                     x.pitch, w, bias, Cout, y, pro_scale, pro_shift);
+  if (Cout <= 4)
+    hipLaunchKernelGGL(conv3x3_small_out_kernel<4>, dim3((unsigned)tiles), dim3(256), 0, st, x.p, x.B, x.H, x.W, x.C,
+                       x.pitch, wp, bias, Cout, y, pro_scale, pro_shift);
+  else
+    hipLaunchKernelGGL(conv3x3_small_out_kernel<8>, dim3((unsigned)tiles), dim3(256), 0, st, x.p, x.B, x.H, x.W, x.C,
+                       x.pitch, wp, bias, Cout, y, pro_scale, pro_shift);
   DM_LAUNCH_CHECK();
   return DM_OK;
 }

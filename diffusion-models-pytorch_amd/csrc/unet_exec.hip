@@ -1010,6 +1010,11 @@ int UNetModel::build_plan(int B, int H, int W) {
     });
     (void)va;
     (void)nchunk;
+    float* lwp = alloc((size_t)9 * C * 8 * sizeof(float));  // packed [9][C][CO] copy of the last conv weight
+    if (!lwp) return DM_ERR_HIP;
+    DM_REQUIRE(small_out_pack(lw, oc, C, lwp, nullptr) == DM_OK, "last conv: weight packing failed");
+    DM_CHECK_HIP(hipDeviceSynchronize());
+    lw = lwp;
     add("conv3x3_small_out", 2.0 * B * H * W * oc * 9 * C, 4.0 * B * H * W * (C + oc),
         [=](hipStream_t st) { return conv3x3_small_out(xin, lw, lb, oc, P_->out, st, gsc, gsh); });
   }
