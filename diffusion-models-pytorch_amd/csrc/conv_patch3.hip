@@ -53,6 +53,8 @@ namespace dm {
 namespace {
 
 constexpr int kSK = 16;  // K per slice = channels per patch chunk
+constexpr int kPwSlices = 2;        // MODE 3: 16-channel slices per chunk (32 channels; 4 measured no faster)
+constexpr int kPwTabFloats = 10240;  // GroupNorm table capacity (40 KiB) of the LDS-staged prologue tables
 
 template <int BM, int BN, int WM, int WN, int MODE, int MAXP, bool PRO, bool KSPLIT = false, int NP = 3>
 __global__ void __launch_bounds__(256)
@@ -66,14 +68,20 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
   static_assert((BM / WM) * NWN == 4, "4 waves per block");
   constexpr bool UP = MODE == 1, SUB = MODE == 2;
   // MODE 3: 1x1 (pointwise) conv / GEMM with static weights (the attention block's qkv and proj).
-  // The "patch" is the tile's own BM rows; a chunk is 32 channels stored as two 16-deep slices per
-  // row, which the two "taps" read.
+  // The "patch" is the tile's own BM rows; a chunk is kPwSlices x 16 channels stored as 16-deep
+  // slices per row, which the chunk's kPwSlices "taps" read.
   constexpr bool PW1 = MODE == 3;
-  constexpr int NTAP = SUB ? 4 : (PW1 ? 2 : 9);
-  constexpr int CH = PW1 ? 2 * kSK : kSK;                    // input channels per chunk
-  constexpr int PROW = PW1 ? 2 * kSRow + 8 : kSPitch;        // LDS row pitch (an odd number of 16-B slots)
+  constexpr int NTAP = SUB ? 4 : (PW1 ? kPwSlices : 9);
+  constexpr int CH = PW1 ? kPwSlices * kSK : kSK;            // input channels per chunk
+  constexpr int PROW = PW1 ? kPwSlices * kSRow + 8 : kSPitch;  // LDS row pitch (an odd number of 16-B slots)
   constexpr int PATCH = MAXP * PROW;
   __shared__ __attribute__((aligned(16))) elem patch[2 * PATCH];
+  // GroupNorm prologue tables (fp16x2, and MODE 3 always): the tile's (image, channel) scale / shift
+  // staged in LDS once per block; per-thread global loads of them cost as many VMEM instructions as
+  // the activations themselves (and in MODE 3, with no tap reuse, twice the activation bytes)
+  constexpr bool LTAB = PRO && (PW1 || NP == 2);
+  constexpr int GTAB = LTAB ? kPwTabFloats : 1;
+  __shared__ __attribute__((aligned(16))) float gtab[GTAB];
 
   const int Ho = SUB ? a.Hin : a.Hout, Wo = SUB ? a.Win : a.Wout;
   const int M = a.B * Ho * Wo;
@@ -108,7 +116,7 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
   const int srow = t >> 1, shalf = t & 1;
 
   // ---- patch loader geometry (pixel p = srow + 128 j; MODE 3: row srow, 16-channel slice j)
-  constexpr int PJ = PW1 ? 2 : (MAXP + 127) / 128;
+  constexpr int PJ = PW1 ? kPwSlices : (MAXP + 127) / 128;
   const float* psrc[PJ];
   bool pok[PJ];
   int pimg[PJ];
@@ -191,12 +199,12 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
       rp[j][0] = *reinterpret_cast<const f4*>(psrc[j] + co);
       rp[j][1] = *reinterpret_cast<const f4*>(psrc[j] + co + 4);
     }
-    if (PRO) {
+    if (PRO && !LTAB) {
 #pragma unroll
       for (int j = 0; j < PJ; ++j)
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          const int cc = co + 8 * shalf + (PW1 ? kSK * j : 0);
+          const int cc = co + 8 * shalf;
           rs[j][h][0] = *reinterpret_cast<const f4*>(a.pro_scale + (size_t)pimg[j] * a.Cin1 + cc + 4 * h);
           rs[j][h][1] = *reinterpret_cast<const f4*>(a.pro_shift + (size_t)pimg[j] * a.Cin1 + cc + 4 * h);
         }
@@ -205,10 +213,21 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
   // GroupNorm + SiLU prologue on patch registers j in [j0, j1): silu(x * scale[b][c] + shift[b][c])
   // (pro_nosilu: GroupNorm alone, the attention block's norm before qkv)
   const bool pro_silu = !a.pro_nosilu;
-  auto transform = [&](int j0, int j1) {
+  const int tab_img0 = m0 / HWo;
+  // images of the tile (MODE 3) or of its patch
+  const int tab_n = !LTAB ? 0 : PW1 ? (min(m0 + BM, M) - 1) / HWo - tab_img0 + 1 : min(b0 + g.TB, a.B) - b0;
+  auto transform = [&](int chunk, int j0, int j1) {
 #pragma unroll
     for (int j = 0; j < PJ; ++j) {
       if (j >= j0 && j < j1) {
+        if constexpr (LTAB) {  // tables from LDS: [image][Cin] scales, then the shifts
+          const float* ts = gtab + (pimg[j] - tab_img0) * a.Cin1 + chunk * CH + (PW1 ? kSK * j : 0) + 8 * shalf;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            rs[j][h][0] = *reinterpret_cast<const f4*>(ts + 4 * h);
+            rs[j][h][1] = *reinterpret_cast<const f4*>(ts + tab_n * a.Cin1 + 4 * h);
+          }
+        }
 #pragma unroll
         for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -288,8 +307,15 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
   // the B ring precisely, instead of assuming a skipped refill and waiting for the newest loads.
 #pragma unroll
   for (int d = 0; d < WD; ++d) load_b(bq[d], min(kt_begin + d, kt_end - 1));
+  if (LTAB) {
+    for (int i = t; i < tab_n * a.Cin1; i += 256) {
+      gtab[i] = a.pro_scale[(size_t)tab_img0 * a.Cin1 + i];
+      gtab[tab_n * a.Cin1 + i] = a.pro_shift[(size_t)tab_img0 * a.Cin1 + i];
+    }
+    __syncthreads();
+  }
   load_patch(c_begin);
-  if (PRO) transform(0, PJ);
+  if (PRO) transform(c_begin, 0, PJ);
   store_patch(c_begin & 1);
   __syncthreads();
   // The patch is double buffered and read by every tap of its chunk: one barrier per chunk. The patch
@@ -305,9 +331,9 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
         load_patch(min(c + 1, c_end - 1));
         __builtin_amdgcn_sched_barrier(0);
       }
-      if (PRO && tap >= T0) {
+      if (PRO && !PW1 && tap >= T0) {
         constexpr int per = (PJ + NTAP - T0 - 1) / (NTAP - T0);
-        transform((tap - T0) * per, tap == NTAP - 1 ? PJ : (tap - T0 + 1) * per);
+        transform(min(c + 1, c_end - 1), (tap - T0) * per, tap == NTAP - 1 ? PJ : (tap - T0 + 1) * per);
       }
       if (SUB)
         compute_tap(py + (tap >> 1), px + (tap & 1), c & 1, bq[slot]);
@@ -317,6 +343,8 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
         compute_tap(tap / 3, tap % 3, c & 1, bq[slot]);
       load_b(bq[slot], min(kt + WD, kt_end - 1));
       __builtin_amdgcn_sched_barrier(0);  // keep the refill WD taps ahead (the scheduler sinks loads to their use)
+      // MODE 3: the next chunk's prologue after the last tap's MFMAs (two taps of load latency hidden)
+      if (PW1 && PRO && tap == NTAP - 1) transform(min(c + 1, c_end - 1), 0, PJ);
       if (tap == NTAP - 1) store_patch((c + 1) & 1);  // after the last chunk: an unused buffer
     }
     __syncthreads();
@@ -496,17 +524,22 @@ __global__ void split_conv_weights_kernel(const float* w, int nmat, int rows, in
 
 bool conv_patch3_ok(const ConvArgs& a, int which, const PatchGeom& g) {
   if (!a.ws || a.Cin1 % kSK != 0 || a.Cin2 % kSK != 0 || a.K % kSK != 0) return false;
+  if (a.ws_np == 2 && a.pro_scale && (long)g.TB * a.Cin1 * 2 > kPwTabFloats) return false;  // LDS GroupNorm tables
   return g.P <= (which == 6 ? kPatch3Max64 : kPatch3Max128);
 }
 
 bool conv_pw_ok(const ConvArgs& a) {
-  return a.taps == 1 && a.ws && a.ws_np == 2 && a.ws_rowscale && a.stride == 1 && !a.upsample && a.Cin2 == 0 &&
-         a.Cin1 % (2 * kSK) == 0 && a.K == a.Cin1 && a.Hout == a.Hin && a.Wout == a.Win && a.ksplit <= 1;
+  if (!(a.taps == 1 && a.ws && a.ws_np == 2 && a.ws_rowscale && a.stride == 1 && !a.upsample && a.Cin2 == 0 &&
+        a.Cin1 % (kPwSlices * kSK) == 0 && a.K == a.Cin1 && a.Hout == a.Hin && a.Wout == a.Win && a.ksplit <= 1))
+    return false;
+  // the GroupNorm tables of every image a 128-row tile can touch fit the kernel's LDS table
+  const int hw = a.Hout * a.Wout;
+  return !a.pro_scale || (long)(127 / hw + 2) * a.Cin1 * 2 <= kPwTabFloats;
 }
 
 int conv2d_patch3(const ConvArgs& a, int which, const PatchGeom& g, hipStream_t st) {
   if (a.taps == 1) {
-    DM_REQUIRE(conv_pw_ok(a), "conv: the split 1x1 path needs fp16x2 weights, stride 1, K = Cin1 % 32 == 0");
+    DM_REQUIRE(conv_pw_ok(a), "conv: the split 1x1 path needs fp16x2 weights, stride 1, K = Cin1 % 32 == 0 and LDS room for the GroupNorm tables");
     return which == 4 ? launch_pw<128, 64>(a, st) : launch_pw<64, 32>(a, st);
   }
   if (a.ws_np == 2) {

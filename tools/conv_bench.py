@@ -26,6 +26,8 @@ SHAPES = {
     'res8_256': (256, 256, 256, 8, True, 0),
     'res4_256': (256, 256, 256, 4, True, 0),
     'up16_256': (256, 256, 256, 16, False, 2),     # sub-pixel upsample 16 -> 32
+    'qkv16': (256, 256, 768, 16, True, -1),        # attention qkv: 1x1 conv (GroupNorm prologue, no SiLU)
+    'proj16': (256, 256, 256, 16, False, -1),      # attention proj: 1x1 conv
 }
 
 
@@ -34,8 +36,15 @@ def run(name, iters, split):
     dev = torch.device('cuda', 0)
     g = torch.Generator(device='cpu').manual_seed(0)
     x = torch.randn((B, H, H, Cin), generator=g).to(dev)
-    w = (torch.randn((Cout, Cin, 3, 3), generator=g) * 0.02).to(dev)
-    if up == 2:
+    taps = 1 if up < 0 else 9
+    w = (torch.randn((Cout, Cin, 3, 3) if taps == 9 else (Cout, Cin, 1, 1), generator=g) * 0.02).to(dev)
+    if up < 0:  # 1x1 (only the split path runs it with the prologue)
+        if not split:
+            return
+        wp = torch.zeros((Cout, Cin), device=dev)
+        dmhip.pack_conv_weight(w, wp, Cin, 0)
+        Ho, up = H, 0
+    elif up == 2:
         wp = torch.zeros((4, Cout, 4 * Cin), device=dev)
         dmhip.pack_conv_weight_subpixel(w, wp)
         wp = wp.view(4 * Cout, 4 * Cin)
@@ -50,7 +59,8 @@ def run(name, iters, split):
     sh = torch.rand((B, Cin), device=dev) - 0.5
     d = dmhip.ConvDesc()
     d.x, d.x_pitch, d.Cin, d.Hin, d.Win = x.data_ptr(), Cin, Cin, H, H
-    d.taps, d.stride, d.upsample = 9, 1, up
+    d.taps, d.stride, d.upsample = taps, 1, up
+    d.pro_nosilu = int(taps == 1)
     d.w, d.K = wp.data_ptr(), wp.shape[1]
     d.y, d.y_pitch, d.Cout, d.B, d.Hout, d.Wout = y.data_ptr(), Cout, Cout, B, Ho, Ho
     d.bias = b.data_ptr()
@@ -58,7 +68,7 @@ def run(name, iters, split):
         d.pro_scale, d.pro_shift = sc.data_ptr(), sh.data_ptr()
     if split:
         kind = dmhip.SPLIT_FP16X2 if split == 'fp16x2' else dmhip.SPLIT_BF16X3
-        ws = dmhip.pack_conv_weight_split(wp, 4 if up == 2 else 1, Cin, 4 if up == 2 else 9, kind)
+        ws = dmhip.pack_conv_weight_split(wp, 4 if up == 2 else 1, Cin, 4 if up == 2 else taps, kind)
         d.w_split, d.w_split_kind = ws.data_ptr(), kind
     for _ in range(3):
         dmhip.conv2d_nhwc(d, dev)
