@@ -55,6 +55,7 @@ namespace {
 constexpr int kSK = 16;  // K per slice = channels per patch chunk
 constexpr int kPwSlices = 2;        // MODE 3: 16-channel slices per chunk (32 channels; 4 measured no faster)
 constexpr int kPwTabFloats = 10240;  // GroupNorm table capacity (40 KiB) of the LDS-staged prologue tables
+constexpr int kGinStats = 512;       // (image, group) pairs of the in-kernel GroupNorm finalize
 
 template <int BM, int BN, int WM, int WN, int MODE, int MAXP, bool PRO, bool KSPLIT = false, int NP = 3>
 __global__ void __launch_bounds__(256)
@@ -82,6 +83,7 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
   constexpr bool LTAB = PRO && (PW1 || NP == 2);
   constexpr int GTAB = LTAB ? kPwTabFloats : 1;
   __shared__ __attribute__((aligned(16))) float gtab[GTAB];
+  __shared__ float gstat[LTAB ? 2 * kGinStats : 1];  // in-kernel finalize: (mean, rstd) per (image, group)
 
   const int Ho = SUB ? a.Hin : a.Hout, Wo = SUB ? a.Win : a.Wout;
   const int M = a.B * Ho * Wo;
@@ -308,9 +310,45 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
 #pragma unroll
   for (int d = 0; d < WD; ++d) load_b(bq[d], min(kt_begin + d, kt_end - 1));
   if (LTAB) {
-    for (int i = t; i < tab_n * a.Cin1; i += 256) {
-      gtab[i] = a.pro_scale[(size_t)tab_img0 * a.Cin1 + i];
-      gtab[tab_n * a.Cin1 + i] = a.pro_shift[(size_t)tab_img0 * a.Cin1 + i];
+    if (a.gin_part) {
+      // gn_finalize (gn.hip) for the tile's images, same expressions: per (image, group) mean and
+      // 1/sqrt(var + eps) from the chunk partials, then per channel the affine (+ modulation)
+      const int G = a.gin_G, cpg = a.Cin1 / G;
+      for (int i = t; i < tab_n * G; i += 256) {
+        const int b = tab_img0 + i / G, gg = i - (i / G) * G;
+        double s1 = 0, s2 = 0;
+        for (int k = 0; k < a.gin_nchunk; ++k) {
+          const double2 v = a.gin_part[((size_t)b * a.gin_nchunk + k) * G + gg];
+          s1 += v.x;
+          s2 += v.y;
+        }
+        const double m = s1 / a.gin_n;
+        double var = s2 / a.gin_n - m * m;
+        if (var < 0) var = 0;
+        gstat[2 * i] = (float)m;
+        gstat[2 * i + 1] = (float)(1.0 / sqrt(var + (double)a.gin_eps));
+      }
+      __syncthreads();
+      for (int i = t; i < tab_n * a.Cin1; i += 256) {
+        const int bi = i / a.Cin1, c = i - (i / a.Cin1) * a.Cin1;
+        const int si = 2 * (bi * G + c / cpg);
+        const float mu = gstat[si], rs = gstat[si + 1];
+        float sc = rs * (a.gin_gamma ? a.gin_gamma[c] : 1.0f);
+        float sh = -sc * mu + (a.gin_beta ? a.gin_beta[c] : 0.0f);
+        if (a.gin_ms) {
+          const size_t mo = (size_t)(tab_img0 + bi) * a.gin_mp + c;
+          const float f = 1.0f + a.gin_ms[mo];
+          sc = sc * f;
+          sh = sh * f + (a.gin_mb ? a.gin_mb[mo] : 0.0f);
+        }
+        gtab[i] = sc;
+        gtab[tab_n * a.Cin1 + i] = sh;
+      }
+    } else {
+      for (int i = t; i < tab_n * a.Cin1; i += 256) {
+        gtab[i] = a.pro_scale[(size_t)tab_img0 * a.Cin1 + i];
+        gtab[tab_n * a.Cin1 + i] = a.pro_shift[(size_t)tab_img0 * a.Cin1 + i];
+      }
     }
     __syncthreads();
   }
@@ -537,7 +575,22 @@ bool conv_pw_ok(const ConvArgs& a) {
   return !a.pro_scale || (long)(127 / hw + 2) * a.Cin1 * 2 <= kPwTabFloats;
 }
 
+bool conv_lds_tables(const ConvArgs& a) {
+  if (!a.pro_scale || a.ws_np != 2) return false;
+  if (a.taps == 1) return conv_pw_ok(a);
+  if (a.taps != 9 || conv_pick(a) < 3) return false;
+  PatchGeom g;
+  conv_patch_pick(a, g);
+  return conv_patch3_ok(a, conv_pick(a) + 1, g);
+}
+
 int conv2d_patch3(const ConvArgs& a, int which, const PatchGeom& g, hipStream_t st) {
+  if (a.gin_part) {
+    const long hw = (long)a.Hout * a.Wout;
+    const long imgs = a.taps == 1 ? 127 / hw + 2 : g.TB;
+    DM_REQUIRE(conv_lds_tables(a) && a.gin_G > 0 && a.Cin1 % a.gin_G == 0 && imgs * a.gin_G <= kGinStats,
+               "conv: in-kernel GroupNorm finalize needs the LDS-table path and <= 512 (image, group) pairs");
+  }
   if (a.taps == 1) {
     DM_REQUIRE(conv_pw_ok(a), "conv: the split 1x1 path needs fp16x2 weights, stride 1, K = Cin1 % 32 == 0 and LDS room for the GroupNorm tables");
     return which == 4 ? launch_pw<128, 64>(a, st) : launch_pw<64, 32>(a, st);

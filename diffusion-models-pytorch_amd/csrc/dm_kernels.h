@@ -37,6 +37,15 @@ struct ConvArgs {
   const float* pro_scale;
   const float* pro_shift;
   int pro_nosilu;  // 1: the prologue is the affine alone (no SiLU)
+  // optional: the kernel computes its GroupNorm prologue tables itself from gn_partial-layout statistics
+  // of x1 ([B][gin_nchunk][gin_G] {sum, sumsq}), exactly as gn_finalize would (same expressions), into
+  // LDS; the finalize launch is skipped. Only where conv_lds_tables() holds.
+  const double2* gin_part;
+  int gin_G, gin_nchunk;
+  double gin_n;
+  float gin_eps;
+  const float *gin_gamma, *gin_beta, *gin_ms, *gin_mb;
+  int gin_mp;
   // split-K over input-channel chunks (halo-patch kernel, MODE 0/1): ksplit > 1 writes raw partial
   // sums to kpart [ksplit][M][Cout] and a reduction pass sums them in split order and applies the
   // epilogue. The split count is fixed per layer shape (not per batch), so results stay batch-invariant.
@@ -174,6 +183,9 @@ int conv2d_patch(const ConvArgs& a, int which, const PatchGeom& g, hipStream_t s
 bool conv_patch3_ok(const ConvArgs& a, int which, const PatchGeom& g);
 // 1x1 convs / static-weight GEMMs on the fp16x2 split kernel (conv_patch3_kernel MODE 3)
 bool conv_pw_ok(const ConvArgs& a);
+// whether the conv stages its GroupNorm prologue tables in LDS (and so can take ConvArgs::gin_* instead
+// of finalized tables)
+bool conv_lds_tables(const ConvArgs& a);
 bool conv_split_eligible(const ConvArgs& a);
 int conv2d_patch3(const ConvArgs& a, int which, const PatchGeom& g, hipStream_t st);
 int conv_splitk_reduce(const ConvArgs& a, hipStream_t st);

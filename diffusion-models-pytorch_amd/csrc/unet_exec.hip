@@ -793,6 +793,28 @@ int UNetModel::build_plan(int B, int H, int W) {
     add("gn_partial", 0, gn_bytes(v, false), [=](hipStream_t st) { return gn_partial(v, G, part, st); });
     return part;
   };
+  // GroupNorm(G) of v feeding conv c's prologue (tables gsc / gsh): either the conv finalizes the
+  // statistics itself into its LDS tables (conv_lds_tables: no gn_finalize launch) or gn_finalize runs.
+  auto gn_prologue = [&](ConvArgs& c, const View& v, const double2* stp, size_t gamma, size_t beta,
+                         const float* ms, const float* mb, int mp) {
+    c.pro_scale = gsc;
+    c.pro_shift = gsh;
+    split_for(c);
+    const long imgs = c.taps == 1 ? 127 / ((long)c.Hout * c.Wout) + 2 : [&] {
+      PatchGeom gg;
+      conv_patch_pick(c, gg);
+      return (long)gg.TB;
+    }();
+    if (conv_lds_tables(c) && imgs * G <= 512 && v.C == c.Cin1) {
+      c.gin_part = stp; c.gin_G = G; c.gin_nchunk = gn_num_chunks(v.H * v.W);
+      c.gin_n = (double)v.H * v.W * (v.C / G); c.gin_eps = 1e-5f;
+      c.gin_gamma = P(gamma); c.gin_beta = P(beta); c.gin_ms = ms; c.gin_mb = mb; c.gin_mp = mp;
+      return;
+    }
+    add("gn_finalize", 0, 8.0 * B * v.C, [=](hipStream_t st) {
+      return gn_finalize(v, G, stp, 1e-5f, self->P(gamma), self->P(beta), gsc, gsh, st, ms, mb, mp);
+    });
+  };
 
   // first conv -> skip 0
   View x_cur = skip_view[0];
@@ -876,11 +898,8 @@ int UNetModel::build_plan(int B, int H, int W) {
         c1.w = P(r.conv1.w); c1.K = r.conv1.K;
       } else if (fuse1) {
         // GroupNorm + SiLU folded into conv1's patch load: x read once, normalised tensor never stored
-        add("gn_finalize", 0, 8.0 * B * r.cin, [=](hipStream_t st) {
-          return gn_finalize(xin, G, st1, 1e-5f, self->P(r.gn1.g), self->P(r.gn1.b), gsc, gsh, st);
-        });
         c1.x1 = xin.p; c1.x1_pitch = xin.pitch;
-        c1.pro_scale = gsc; c1.pro_shift = gsh;
+        gn_prologue(c1, xin, st1, r.gn1.g, r.gn1.b, nullptr, nullptr, 0);
       } else {
         add("gn_apply", 0, gn_bytes(xin, true), [=](hipStream_t st) {
           return gn_apply(xin, G, st1, nchunk, 1e-5f, self->P(r.gn1.g), self->P(r.gn1.b), nullptr, nullptr, 0, 1,
@@ -892,11 +911,8 @@ int UNetModel::build_plan(int B, int H, int W) {
       add_conv(c1);
       const double2* st2 = gn_stats(vh);
       if (fuse2) {
-        add("gn_finalize", 0, 8.0 * B * r.cout, [=](hipStream_t st) {
-          return gn_finalize(vh, G, st2, 1e-5f, self->P(r.gn2.g), self->P(r.gn2.b), gsc, gsh, st, ms, mb, mp);
-        });
         c2.x1 = hbuf;
-        c2.pro_scale = gsc; c2.pro_shift = gsh;
+        gn_prologue(c2, vh, st2, r.gn2.g, r.gn2.b, ms, mb, mp);
       } else {
         add("gn_apply", 0, gn_bytes(vh, true), [=](hipStream_t st) {
           return gn_apply(vh, G, st2, nchunk_o, 1e-5f, self->P(r.gn2.g), self->P(r.gn2.b), ms, mb, mp, 1, va2, st);
@@ -909,9 +925,6 @@ int UNetModel::build_plan(int B, int H, int W) {
       const int C = p.C, heads = p.heads, Dh = C / heads;
       // GroupNorm folded into the QKV projection's A load (modules.py:91-94): one pass over x
       const double2* sta = gn_stats(xin);
-      add("gn_finalize", 0, 8.0 * B * C, [=](hipStream_t st) {
-        return gn_finalize(xin, G, sta, 1e-5f, self->P(p.gn.g), self->P(p.gn.b), gsc, gsh, st);
-      });
       GemmArgs gq{};
       gq.M = B * hw; gq.N = 3 * C; gq.K = C; gq.Z1 = 1; gq.Z2 = 1;
       gq.A = xin.p; gq.lda = xin.pitch; gq.Bm = P(p.wqkv); gq.ldb = C; gq.C = qkv; gq.ldc = 3 * C;
@@ -924,8 +937,12 @@ int UNetModel::build_plan(int B, int H, int W) {
       cq.Wout = Wi; cq.bias = P(p.bqkv); cq.pro_scale = gsc; cq.pro_shift = gsh; cq.pro_nosilu = 1;
       split_for(cq);
       if (conv_pw_ok(cq)) {
+        gn_prologue(cq, xin, sta, p.gn.g, p.gn.b, nullptr, nullptr, 0);
         add_conv(cq);
       } else {
+        add("gn_finalize", 0, 8.0 * B * C, [=](hipStream_t st) {
+          return gn_finalize(xin, G, sta, 1e-5f, self->P(p.gn.g), self->P(p.gn.b), gsc, gsh, st);
+        });
         split_gemm(gq, 6, gq.Bm, (size_t)3 * C * C);
         add_gemm(gq);
       }
