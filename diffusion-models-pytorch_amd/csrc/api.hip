@@ -32,6 +32,10 @@ extern "C" int dm_sampler_step(const dm_step_desc* d, void* stream) {
   s.add_noise = d->add_noise; s.noise = d->noise;
   s.sample = d->sample; s.mean_out = d->mean; s.x0_out = d->pred_x0; s.eps_out = d->pred_eps;
   s.var_out = d->var;
+  s.euler = d->euler; s.e_st1 = d->e_st1; s.e_sig_t = d->e_sig_t; s.e_dsig = d->e_dsig; s.e_sp1 = d->e_sp1;
+  s.e_sig_p = d->e_sig_p; s.e_d1 = d->e_d1; s.e_x1 = d->e_x1; s.e_dout = d->e_dout;
+  if (s.euler < 0 || s.euler > 2) { dm::set_error("invalid euler mode"); return DM_ERR_ARG; }
+  if (s.euler == 2 && (!s.e_d1 || !s.e_x1)) { dm::set_error("Heun second order needs e_d1 and e_x1"); return DM_ERR_ARG; }
   if (s.objective < 0 || s.objective > 2) { dm::set_error("invalid objective"); return DM_ERR_ARG; }
   if (s.kind < 0 || s.kind > 1) { dm::set_error("invalid sampler kind"); return DM_ERR_ARG; }
   if (s.B < 0 || s.C <= 0 || s.HW <= 0) { dm::set_error("invalid shape"); return DM_ERR_ARG; }

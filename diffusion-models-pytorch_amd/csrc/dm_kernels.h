@@ -147,6 +147,11 @@ struct StepArgs {
   float* x0_out;
   float* eps_out;
   float* var_out;
+  int euler;            // 1: Euler / Heun first order, 2: Heun second order (dm_step_desc)
+  float e_st1, e_sig_t, e_dsig, e_sp1, e_sig_p;
+  const float* e_d1;
+  const float* e_x1;
+  float* e_dout;
 };
 
 int gn_num_chunks(int HW);

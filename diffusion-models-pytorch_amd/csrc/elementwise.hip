@@ -222,6 +222,26 @@ __global__ void sampler_step_kernel(StepArgs s) {
     predict(s.out_c[mo], s.objective, x0, eps);
   }
 
+  if (s.euler) {
+    // euler.py:60-64 / heun.py:66-70 (first order), heun.py:89-100 (second order), reference op order
+    float sample, d;
+    if (s.euler == 1) {
+      const float bar = s.e_st1 * xt;
+      d = (bar - x0) / s.e_sig_t;
+      sample = (bar + d * s.e_dsig) / s.e_sp1;
+      if (s.e_dout) s.e_dout[e] = d;
+    } else {
+      const float barp = s.e_sp1 * xt;
+      d = (barp - x0) / s.e_sig_p;
+      d = (d + s.e_d1[e]) / 2.0f;
+      const float bar = s.e_st1 * s.e_x1[e];
+      sample = (bar + d * s.e_dsig) / s.e_sp1;
+    }
+    s.sample[e] = sample;
+    if (s.x0_out) s.x0_out[e] = x0;
+    if (s.eps_out) s.eps_out[e] = eps;
+    return;
+  }
   float mean, sample;
   if (s.kind == 0) {
     mean = s.m1 * x0 + s.m2 * eps;  // ddim.py:72-73

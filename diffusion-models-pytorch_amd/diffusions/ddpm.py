@@ -161,7 +161,8 @@ class DDPM:
     def _step(self, model_output: Tensor, xt: Tensor, t: int, t_prev: int,
               model_output_uncond: Tensor = None, guidance_scale: float = 1.0,
               objective: str = None, want_noise: bool = True, predict_only: bool = False,
-              coefs: dict = None):
+              coefs: dict = None, euler: int = 0, ecoefs: dict = None, d1: Tensor = None, x1: Tensor = None,
+              dout: Tensor = None):
         dmhip.require_device_tensor(xt, 'xt')
         dmhip.require_device_tensor(model_output, 'model_output')
         if model_output_uncond is not None:
@@ -172,10 +173,10 @@ class DDPM:
         if model_output.shape[0] != B or model_output.shape[2:] != xt.shape[2:] or Cm not in (C, 2 * C):
             raise ValueError(f'model output shape {tuple(model_output.shape)} does not match xt {tuple(xt.shape)}')
         c = coefs if coefs is not None else self._coefs(t, t_prev)
-        learned = (not predict_only) and self.var_type == 'learned_range' and self.kind == 1 and t != 0
+        learned = (not predict_only) and not euler and self.var_type == 'learned_range' and self.kind == 1 and t != 0
         if learned and Cm != 2 * C:
             raise ValueError('var_type learned_range requires the model to output 2C channels')
-        add_noise = (not predict_only) and t != 0
+        add_noise = (not predict_only) and not euler and t != 0
         needed = add_noise and (learned or c['std'] != 0.0)
         noise = self._draw_noise(xt, needed) if want_noise and not predict_only else None
 
@@ -206,6 +207,13 @@ class DDPM:
         d.noise = noise.data_ptr() if noise is not None else None
         d.sample, d.mean, d.pred_x0, d.pred_eps = sample.data_ptr(), mean.data_ptr(), x0.data_ptr(), eps.data_ptr()
         d.var = var_t.data_ptr() if var_t is not None else None
+        if euler:
+            d.euler = euler
+            d.e_st1, d.e_sig_t, d.e_dsig = ecoefs['st1'], ecoefs['sig_t'], ecoefs['dsig']
+            d.e_sp1, d.e_sig_p = ecoefs['sp1'], ecoefs['sig_p']
+            d.e_d1 = d1.data_ptr() if d1 is not None else None
+            d.e_x1 = x1.data_ptr() if x1 is not None else None
+            d.e_dout = dout.data_ptr() if dout is not None else None
         dmhip.sampler_step(d, xt.device)
         if learned:
             var = var_t

@@ -75,6 +75,9 @@ class StepDesc(ctypes.Structure):
         ('min_logvar', ctypes.c_float), ('max_logvar', ctypes.c_float),
         ('add_noise', ctypes.c_int), ('noise', vp),
         ('sample', vp), ('mean', vp), ('pred_x0', vp), ('pred_eps', vp), ('var', vp),
+        ('euler', ctypes.c_int), ('e_st1', ctypes.c_float), ('e_sig_t', ctypes.c_float),
+        ('e_dsig', ctypes.c_float), ('e_sp1', ctypes.c_float), ('e_sig_p', ctypes.c_float),
+        ('e_d1', vp), ('e_x1', vp), ('e_dout', vp),
     ]
 
 

@@ -187,6 +187,17 @@ typedef struct dm_step_desc {
   float* pred_x0;
   float* pred_eps;
   float* var;
+  /* Karras-style samplers on the VP schedule (sigma_t = sqrt((1 - ac_t) / ac_t)):
+   * euler 1: EulerSampler.denoise / HeunSampler.denoise_1st_order (diffusions/euler.py:50-66,
+   *          heun.py:56-77): sample = (st1*xt + (st1*xt - x0)/sig_t * dsig) / sp1, derivative -> e_dout;
+   * euler 2: HeunSampler.denoise_2nd_order (heun.py:79-106) with xt = x_{t-1} and x0 predicted at
+   *          t_prev: d = ((sp1*xt - x0)/sig_p + e_d1) / 2, sample = (st1*e_x1 + d*dsig) / sp1.
+   * st1 = sqrt(1+sig_t^2), sp1 = sqrt(1+sig_p^2), dsig = sig_p - sig_t (host 0-dim float32 ops). */
+  int euler;
+  float e_st1, e_sig_t, e_dsig, e_sp1, e_sig_p;
+  const float* e_d1;
+  const float* e_x1;
+  float* e_dout;
 } dm_step_desc;
 
 int dm_sampler_step(const dm_step_desc* d, void* stream);

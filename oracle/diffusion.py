@@ -143,3 +143,36 @@ def sample_loop(model: Callable, ac: Tensor, seq: Tensor, init_noise: Tensor, sa
             res = ddpm_denoise(ac, out, img, t, tp, var_type, obj, clip, noise_fn)
         img = res['sample']
         yield res
+
+
+def sigmas(ac: Tensor) -> Tensor:
+    """diffusions/euler.py:48, heun.py:51"""
+    return ((1 - ac) / ac).sqrt()
+
+
+def euler_denoise(ac: Tensor, sig: Tensor, out: Tensor, xt: Tensor, t: int, t_prev: int,
+                  objective='pred_eps', clip=True) -> Dict[str, Tensor]:
+    """diffusions/euler.py:50-66 (= HeunSampler.denoise_1st_order, heun.py:56-77, which keeps `derivative`)"""
+    sigmas_t = sig[t]
+    sigmas_t_prev = sig[t_prev] if t_prev >= 0 else torch.tensor(0.0)
+    pred_x0, _, _ = predict(ac, out, xt, t, objective, clip)
+    bar_xt = (1 + sigmas_t ** 2).sqrt() * xt
+    derivative = (bar_xt - pred_x0) / sigmas_t
+    bar_sample = bar_xt + derivative * (sigmas_t_prev - sigmas_t)
+    sample = bar_sample / (1 + sigmas_t_prev ** 2).sqrt()
+    return dict(sample=sample, pred_x0=pred_x0, derivative=derivative)
+
+
+def heun_denoise_2nd(ac: Tensor, sig: Tensor, out: Tensor, xt_prev: Tensor, t: int, t_prev: int,
+                     d1: Tensor, xt1: Tensor, objective='pred_eps', clip=True) -> Dict[str, Tensor]:
+    """diffusions/heun.py:79-106"""
+    sigmas_t = sig[t]
+    sigmas_t_prev = sig[t_prev] if t_prev >= 0 else torch.tensor(0.0)
+    pred_x0, _, _ = predict(ac, out, xt_prev, t_prev, objective, clip)
+    bar_xt_prev = (1 + sigmas_t_prev ** 2).sqrt() * xt_prev
+    derivative = (bar_xt_prev - pred_x0) / sigmas_t_prev
+    derivative = (derivative + d1) / 2
+    bar_xt = (1 + sigmas_t ** 2).sqrt() * xt1
+    bar_sample = bar_xt + derivative * (sigmas_t_prev - sigmas_t)
+    sample = bar_sample / (1 + sigmas_t_prev ** 2).sqrt()
+    return dict(sample=sample, pred_x0=pred_x0)

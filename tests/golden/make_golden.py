@@ -385,8 +385,53 @@ def make_adm(full=True):
     save('adm', meta, **fx)
 
 
+def make_samplers():
+    """EulerSampler / HeunSampler (diffusions/euler.py, heun.py): per-step trajectories on the tiny UNet
+    and single updates on fixed inputs."""
+    torch.set_num_threads(8)
+    schedule, ddpm, ddim, unet = import_reference()
+    import diffusions.euler as euler  # noqa: E402
+    import diffusions.heun as heun  # noqa: E402
+    meta = dict(torch=torch.__version__, threads=torch.get_num_threads(), coef_probe_sha=coef_probe_sha(),
+                reference='xyfJASON/diffusion-models-pytorch @ 2024-12-20 (/root/reference)')
+    arr = {}
+    # single updates: Euler (= Heun 1st order) and Heun 2nd order at several (t, t_prev), fixed inputs
+    g = torch.Generator().manual_seed(23)
+    shape = (2, 3, 4, 4)
+    e = euler.EulerSampler(respace_type='uniform', respace_steps=10)
+    pairs = [(900, 800), (500, 400), (100, 0), (0, -1)]
+    meta['update_pairs'] = pairs
+    for i, (t, tp) in enumerate(pairs):
+        xt, out = torch.randn(shape, generator=g), torch.randn(shape, generator=g)
+        arr[f'upd{i}_xt'], arr[f'upd{i}_out'] = xt, out
+        r = e.denoise(out, xt, t, tp)
+        arr[f'upd{i}_euler_sample'], arr[f'upd{i}_euler_x0'] = r['sample'], r['pred_x0']
+        if tp >= 0:
+            h = heun.HeunSampler(respace_type='uniform', respace_steps=10)
+            h.denoise_1st_order(out, xt, t, tp)
+            xp, out2 = torch.randn(shape, generator=g), torch.randn(shape, generator=g)
+            arr[f'upd{i}_xprev'], arr[f'upd{i}_out2'] = xp, out2
+            r2 = h.denoise_2nd_order(out2, xp, t, tp)
+            arr[f'upd{i}_heun2_sample'], arr[f'upd{i}_heun2_x0'] = r2['sample'], r2['pred_x0']
+    # trajectories on the tiny UNet, 5 uniform steps, B=2
+    model = unet.UNet(**ARCHS['tiny']).eval()
+    meta['tiny_weights_sha256'] = synthetic(model)
+    for name, cls in (('euler5', euler.EulerSampler), ('heun5', heun.HeunSampler)):
+        d = cls(respace_type='uniform', respace_steps=5)
+        torch.manual_seed(11)
+        init = torch.randn((2, 3, 16, 16))
+        arr[f'{name}_init'] = init
+        with torch.no_grad():
+            for i, out in enumerate(d.sample_loop(model, init, tqdm_kwargs=dict(disable=True))):
+                arr[f'{name}_step{i}_sample'] = out['sample']
+                arr[f'{name}_step{i}_pred_x0'] = out['pred_x0']
+    save('samplers', meta, **arr)
+
+
 if __name__ == '__main__':
-    if sys.argv[1:] == ['adagn']:
+    if sys.argv[1:] == ['samplers']:
+        make_samplers()
+    elif sys.argv[1:] == ['adagn']:
         make_adagn()
     elif sys.argv[1:] == ['adm']:
         make_adm()
@@ -394,3 +439,4 @@ if __name__ == '__main__':
         main()
         make_adagn()
         make_adm()
+        make_samplers()

@@ -1,0 +1,64 @@
+"""Euler and Heun samplers (reference diffusions/euler.py, heun.py) on the engine.
+
+Golden fixtures: tests/golden/samplers.npz, generated from the reference modules themselves
+(tests/golden/make_golden.py samplers). Updates: bit-identical to the oracle (oracle/diffusion.py,
+reference op order) on this host and within a few ulp of the golden file from the build container's CPU
+(torch 0-dim sqrt/pow round host-dependently). Trajectories: per step <= 1e-4.
+"""
+import numpy as np
+import pytest
+import torch
+
+from diffusions import EulerSampler, HeunSampler
+from tests.test_gpu_parity import TOL, _model
+
+pytestmark = pytest.mark.gpu
+
+
+def test_euler_heun_updates_bit_exact(cuda, golden):
+    from oracle import diffusion as od
+    arrays, meta = golden('samplers')
+    ac = od.alphas_cumprod(od.beta_schedule(1000, 'linear'))
+    sig = od.sigmas(ac)
+    for i, (t, tp) in enumerate(meta['update_pairs']):
+        xt, out = (torch.from_numpy(arrays[f'upd{i}_{k}']) for k in ('xt', 'out'))
+        e = EulerSampler(respace_type='uniform', respace_steps=10, device=cuda)
+        got = e.denoise(out.to(cuda), xt.to(cuda), t, tp)
+        ref = od.euler_denoise(ac, sig, out.clone(), xt, t, tp)
+        for k, gk in (('sample', 'euler_sample'), ('pred_x0', 'euler_x0')):
+            g = got[k].cpu().numpy()
+            assert np.array_equal(g, ref[k].numpy()), (t, k, np.abs(g - ref[k].numpy()).max())
+            assert np.allclose(g, arrays[f'upd{i}_{gk}'], rtol=1e-5, atol=2e-5), (t, k)
+        if tp < 0:
+            continue
+        h = HeunSampler(respace_type='uniform', respace_steps=10, device=cuda)
+        h.denoise_1st_order(out.to(cuda), xt.to(cuda), t, tp)
+        xp, out2 = (torch.from_numpy(arrays[f'upd{i}_{k}']) for k in ('xprev', 'out2'))
+        got2 = h.denoise_2nd_order(out2.to(cuda), xp.to(cuda), t, tp)
+        ref2 = od.heun_denoise_2nd(ac, sig, out2.clone(), xp, t, tp, ref['derivative'], xt)
+        for k, gk in (('sample', 'heun2_sample'), ('pred_x0', 'heun2_x0')):
+            g = got2[k].cpu().numpy()
+            assert np.array_equal(g, ref2[k].numpy()), (t, k, np.abs(g - ref2[k].numpy()).max())
+            assert np.allclose(g, arrays[f'upd{i}_{gk}'], rtol=1e-5, atol=2e-5), (t, k)
+
+
+def test_heun_second_order_needs_first():
+    h = HeunSampler(respace_type='uniform', respace_steps=10)
+    with pytest.raises(RuntimeError):
+        h.denoise_2nd_order(torch.zeros(1), torch.zeros(1), 900, 800)
+
+
+@pytest.mark.parametrize('name,cls', [('euler5', EulerSampler), ('heun5', HeunSampler)])
+def test_euler_heun_trajectories(cuda, golden, report, name, cls):
+    arrays, meta = golden('samplers')
+    fmeta = golden('forward')[1]
+    model, sha = _model(fmeta, 'tiny', cuda)
+    assert sha == meta['tiny_weights_sha256']
+    d = cls(respace_type='uniform', respace_steps=5, device=cuda)
+    init = torch.from_numpy(arrays[f'{name}_init']).to(cuda)
+    worst = 0.0
+    for i, out in enumerate(d.sample_loop(model, init, tqdm_kwargs=dict(disable=True))):
+        err = np.abs(out['sample'].cpu().numpy() - arrays[f'{name}_step{i}_sample']).max()
+        worst = max(worst, err)
+        assert err <= TOL, (name, i, err)
+    report(f'{name}_tiny_worst_step_maxabs_vs_reference', worst)
