@@ -9,7 +9,7 @@ config overrides. Launch one process per GPU:
         --weights ckpt.pt --n_samples 2048 --batch_size 256 --sampler ddim --respace_steps 50 --save_dir out
 
 `--weights synthetic` uses the deterministic synthetic weights (no checkpoint
-offline). Supported modes: sample, denoise, progressive (DDPM / DDIM).
+offline). Samplers: ddpm, ddim, euler, heun. Modes: sample, denoise, progressive, interpolate.
 """
 import argparse
 import math
@@ -36,14 +36,16 @@ def get_parser():
     p.add_argument('--n_samples', type=int, required=True, help='Number of samples')
     p.add_argument('--save_dir', type=str, required=True, help='Path to directory saving samples')
     p.add_argument('--batch_size', type=int, default=500, help='Batch size on each process')
-    p.add_argument('--sampler', type=str, choices=['ddpm', 'ddim'], default='ddpm', help='Type of sampler')
+    p.add_argument('--sampler', type=str, choices=['ddpm', 'ddim', 'euler', 'heun'], default='ddpm',
+                   help='Type of sampler')
     p.add_argument('--respace_type', type=str, default='uniform', help='Type of respaced timestep sequence')
     p.add_argument('--respace_steps', type=int, default=None, help='Length of respaced timestep sequence')
     p.add_argument('--var_type', type=str, default=None, help='Type of variance of the reverse process')
     p.add_argument('--ddim_eta', type=float, default=0.0, help='Parameter eta in DDIM sampling')
-    p.add_argument('--mode', type=str, default='sample', choices=['sample', 'denoise', 'progressive'])
+    p.add_argument('--mode', type=str, default='sample', choices=['sample', 'denoise', 'progressive', 'interpolate'])
     p.add_argument('--n_denoise', type=int, default=20)
     p.add_argument('--n_progressive', type=int, default=20)
+    p.add_argument('--n_interpolate', type=int, default=16, help='Number of intermediate images (interpolate)')
     return p
 
 
@@ -58,7 +60,28 @@ def build_diffuser(args, conf, device):
     )
     if args.sampler == 'ddpm':
         return diffusions.ddpm.DDPM(var_type=args.var_type or dp.get('var_type', None), **params)
-    return diffusions.ddim.DDIM(eta=args.ddim_eta, **params)
+    if args.sampler == 'ddim':
+        return diffusions.ddim.DDIM(eta=args.ddim_eta, **params)
+    if args.sampler == 'euler':
+        return diffusions.euler.EulerSampler(**params)
+    if args.sampler == 'heun':
+        return diffusions.heun.HeunSampler(**params)
+    raise ValueError(f'Unknown sampler: {args.sampler}')
+
+
+# reference sample_uncond.py:22-27 (reconstruction needs an image directory + data loaders: not provided)
+COMPATIBLE_SAMPLER_MODE = dict(
+    ddpm=['sample', 'denoise', 'progressive'],
+    ddim=['sample', 'denoise', 'progressive', 'interpolate', 'reconstruction'],
+    euler=['sample', 'denoise', 'progressive', 'interpolate'],
+    heun=['sample', 'denoise', 'progressive', 'interpolate'],
+)
+
+
+def slerp(t, z1, z2):
+    """Spherical interpolation of two noise batches (reference sample_uncond.py:253-255)."""
+    theta = torch.acos(torch.sum(z1 * z2) / (torch.linalg.norm(z1) * torch.linalg.norm(z2)))
+    return torch.sin((1 - t) * theta) / torch.sin(theta) * z1 + torch.sin(t * theta) / torch.sin(theta) * z2
 
 
 def build_model(conf, weights, device):
@@ -89,10 +112,26 @@ def main(argv=None):
     bspp = per_process_batch(args.n_samples, args.batch_size, env.world)
     folds = amortize(args.n_samples, bspp * env.world)
     n_seq = len(diffuser.respaced_seq)
+    if args.mode not in COMPATIBLE_SAMPLER_MODE[args.sampler] and env.is_main:
+        print(f'`{args.mode}` mode is not designed for `{args.sampler}` sampler, unexpected behavior may occur.')
     idx = 0
     for i, bs in enumerate(folds):
-        init_noise = torch.randn((bspp, *img_shape), device=env.device)
         tq = dict(desc=f'Fold {i}/{len(folds)}', disable=not env.is_main)
+        if args.mode == 'interpolate':  # reference sample_uncond.py:248-276
+            z1 = torch.randn((bspp, *img_shape), device=env.device)
+            z2 = torch.randn((bspp, *img_shape), device=env.device)
+            samples = torch.stack([
+                diffuser.sample(model=model, init_noise=slerp(t, z1, z2), tqdm_kwargs=tq).clamp(-1, 1)
+                for t in torch.linspace(0, 1, args.n_interpolate)
+            ], dim=1)
+            samples = env.gather(samples)[:bs]
+            if env.is_main:
+                for x in samples:
+                    save_image(image_norm_to_float(torch.cat(list(x), dim=-1).float().cpu()),
+                               os.path.join(args.save_dir, f'{idx}.png'))
+                    idx += 1
+            continue
+        init_noise = torch.randn((bspp, *img_shape), device=env.device)
         if args.mode == 'sample':
             samples = diffuser.sample(model=model, init_noise=init_noise, tqdm_kwargs=tq).clamp(-1, 1)
         else:

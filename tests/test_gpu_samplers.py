@@ -62,3 +62,18 @@ def test_euler_heun_trajectories(cuda, golden, report, name, cls):
         worst = max(worst, err)
         assert err <= TOL, (name, i, err)
     report(f'{name}_tiny_worst_step_maxabs_vs_reference', worst)
+
+
+@pytest.mark.parametrize('sampler,mode', [('euler', 'interpolate'), ('heun', 'sample'), ('ddim', 'progressive')])
+def test_sample_uncond_script(cuda, tmp_path, sampler, mode):
+    """scripts/sample_uncond.py end to end on the engine (MNIST config, synthetic weights, 2 steps):
+    the reference's sampler x mode matrix (sample_uncond.py:22-27, 179-276) writes one PNG per image."""
+    import os
+    from scripts import sample_uncond
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cfg = os.path.join(root, 'diffusion-models-pytorch_amd', 'configs', 'ddpm_mnist.yaml')
+    sample_uncond.main(['-c', cfg, '--weights', 'synthetic', '--n_samples', '3', '--batch_size', '2',
+                        '--save_dir', str(tmp_path), '--sampler', sampler, '--mode', mode,
+                        '--respace_steps', '4', '--n_interpolate', '3', '--n_progressive', '2'])
+    files = sorted(os.listdir(tmp_path))
+    assert files == ['0.png', '1.png', '2.png'], files
