@@ -18,6 +18,7 @@
 #include <memory>
 #include <vector>
 
+#include <map>
 #include "dm_common.h"
 #include "dm_kernels.h"
 #include "plan.h"
@@ -56,6 +57,14 @@ struct DiTModel {
   size_t pos, xw, xb, tw1, tb1, tw2, tb2, ytab, freqs, ada_w, ada_b, fin_w, fin_b;
   bool freqs_set = false;
   std::vector<BlockP> blocks;
+  // Arithmetic of the token GEMMs (qkv, attention, proj, fc1, fc2, final): 2 = fp16x2 split (gemm.hip
+  // SPLIT; default unless DM_CONV_MATH=fp32|bf16x3), 0 = fp32 MFMA. A forward that raises range_flag
+  // (an operand beyond the fp16 range) runs again in fp32 and the model stays there.
+  int math = conv_math_from_env() == 2 ? 2 : 0;
+  bool range_check = !(std::getenv("DM_RANGE_CHECK") && std::string(std::getenv("DM_RANGE_CHECK")) == "0");
+  int* range_flag = nullptr;
+  int* range_flag_host = nullptr;
+  std::map<const float*, int> w_exp;
 
   struct Plan : PlanBase {
     int B = 0;
@@ -70,6 +79,8 @@ struct DiTModel {
   float* P(size_t off) const { return arena + off; }
   ~DiTModel() {
     plan.reset();
+    if (range_flag) (void)hipFree(range_flag);
+    if (range_flag_host) (void)hipHostFree(range_flag_host);
     if (arena) (void)hipFree(arena);
   }
   int build_plan(int B);
@@ -171,6 +182,11 @@ int DiTModel::build_plan(int B) {
   const long M = (long)B * T;
   DM_REQUIRE((long)B * heads <= 65535, "batch * heads too large for one attention launch");
 
+  if (!range_flag) {
+    DM_CHECK_HIP(hipMalloc(&range_flag, sizeof(int)));
+    DM_CHECK_HIP(hipMemset(range_flag, 0, sizeof(int)));
+    DM_CHECK_HIP(hipHostMalloc(&range_flag_host, sizeof(int)));
+  }
   pl.x = pl.alloc((size_t)B * C * S * S * 4);
   pl.t = (int64_t*)pl.alloc((size_t)B * 8);
   pl.y = (int64_t*)pl.alloc((size_t)B * 8);
@@ -198,6 +214,18 @@ int DiTModel::build_plan(int B) {
     const double by = 4.0 * Z * ((double)g.M * g.K + (double)g.N * g.K + (double)g.M * g.N) +
                       (g.res ? 4.0 * g.M * g.N : 0.0);
     pl.add(gemm_label(g), fl, by, [=](hipStream_t st) { return gemm_batched(g, st); });
+  };
+  // fp16x2 operand exponents (unet_exec.hip split_gemm): weights by max |w|, activations fixed (2^6 for
+  // LayerNorm-modulated tokens, q, k, v, attention and MLP outputs; 2^14 for softmax rows)
+  auto split = [&](GemmArgs& g, int ea, size_t w, size_t wn, int eb_act) {
+    if (math != 2) return;
+    int eb = eb_act;
+    if (wn) {
+      auto it = w_exp.find(P(w));
+      if (it == w_exp.end()) it = w_exp.emplace(P(w), split_weight_exponent(P(w), wn)).first;
+      eb = it->second;
+    }
+    g.split = 2; g.split_ea = ea; g.split_eb = eb; g.range_flag = range_flag;
   };
   auto linear = [&](const float* A, int lda, long rows, size_t w, size_t bias, int N, int K, float* out, int ldc) {
     GemmArgs g{};
@@ -248,6 +276,7 @@ int DiTModel::build_plan(int B) {
     {
       GemmArgs g = linear(x, D, M, bp.qkv_w, bp.qkv_b, 3 * D, D, qkv, 3 * D);
       g.ln_stats = stats; g.ln_shift = mb; g.ln_scale = mb + D; g.ln_pitch = ada_total; g.ln_rows = T;
+      split(g, 6, bp.qkv_w, (size_t)3 * D * D, 0);
       add_gemm(g);
     }
     {
@@ -258,6 +287,7 @@ int DiTModel::build_plan(int B) {
       gs.Bm = qkv + D; gs.b_s1 = (long)T * 3 * D; gs.b_s2 = Dh; gs.ldb = 3 * D;
       gs.C = Sb; gs.c_s1 = (long)heads * T * T; gs.c_s2 = (long)T * T; gs.ldc = T;
       gs.alpha = (float)std::pow((double)Dh, -0.5);
+      split(gs, 6, 0, 0, 6);
       add_gemm(gs);
       const long rows = (long)B * heads * T;
       const int L = T;
@@ -268,11 +298,13 @@ int DiTModel::build_plan(int B) {
       go.Bm = qkv + 2 * D; go.b_s1 = (long)T * 3 * D; go.b_s2 = Dh; go.ldb = 3 * D; go.b_kn = 1;
       go.C = Ob; go.c_s1 = (long)T * D; go.c_s2 = Dh; go.ldc = D;
       go.alpha = 1.f;
+      split(go, 14, 0, 0, 6);
       add_gemm(go);
     }
     {
       GemmArgs g = linear(Ob, D, M, bp.proj_w, bp.proj_b, D, D, x, D);
       g.res = x; g.ld_res = D; g.gate = mb + 2 * D; g.gate_pitch = ada_total; g.gate_rows = T;
+      split(g, 6, bp.proj_w, (size_t)D * D, 0);
       add_gemm(g);
     }
     // MLP branch
@@ -281,11 +313,13 @@ int DiTModel::build_plan(int B) {
       GemmArgs g = linear(x, D, M, bp.fc1_w, bp.fc1_b, Hm, D, hb, Hm);
       g.ln_stats = stats; g.ln_shift = mb + 3 * D; g.ln_scale = mb + 4 * D; g.ln_pitch = ada_total; g.ln_rows = T;
       g.act = 2;
+      split(g, 6, bp.fc1_w, (size_t)Hm * D, 0);
       add_gemm(g);
     }
     {
       GemmArgs g = linear(hb, Hm, M, bp.fc2_w, bp.fc2_b, D, Hm, x, D);
       g.res = x; g.ld_res = D; g.gate = mb + 5 * D; g.gate_pitch = ada_total; g.gate_rows = T;
+      split(g, 6, bp.fc2_w, (size_t)D * Hm, 0);
       add_gemm(g);
     }
   }
@@ -295,6 +329,7 @@ int DiTModel::build_plan(int B) {
     const float* mf = mods + (size_t)a.depth * 6 * D;  // shift, scale
     GemmArgs g = linear(x, D, M, fin_w, fin_b, PP * OC, D, lin, PP * OC);
     g.ln_stats = stats; g.ln_shift = mf; g.ln_scale = mf + D; g.ln_pitch = ada_total; g.ln_rows = T;
+    split(g, 6, fin_w, (size_t)PP * OC * D, 0);
     add_gemm(g);
   }
   const int oc = OC;
@@ -335,6 +370,10 @@ extern "C" int dm_dit_forward(dm_dit* h, const float* x, const int64_t* t, const
   if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
   if (!x || !t || !out) { dm::set_error("null tensor"); return DM_ERR_ARG; }
   if (B <= 0) { dm::set_error("empty batch"); return DM_ERR_ARG; }
+  if (static_cast<const void*>(out) == static_cast<const void*>(x)) {
+    dm::set_error("out must not alias x");
+    return DM_ERR_ARG;
+  }
   dm::DiTModel* m = h->m;
   if (!m->plan || m->plan->B != B) {
     int rc = m->build_plan(B);
@@ -356,6 +395,32 @@ extern "C" int dm_dit_forward(dm_dit* h, const float* x, const int64_t* t, const
   const int rc = pl.run(st);
   if (rc) return rc;
   DM_CHECK_HIP(hipMemcpyAsync(out, pl.out, no * sizeof(float), hipMemcpyDeviceToDevice, st));
+  if (m->math == 2 && m->range_check) {
+    DM_CHECK_HIP(hipMemcpyAsync(m->range_flag_host, m->range_flag, sizeof(int), hipMemcpyDeviceToHost, st));
+    DM_CHECK_HIP(hipStreamSynchronize(st));
+    if (*m->range_flag_host) {  // an fp16x2 GEMM met an operand beyond the fp16 range: fp32 from here on
+      DM_CHECK_HIP(hipMemsetAsync(m->range_flag, 0, sizeof(int), st));
+      m->math = 0;
+      m->plan.reset();
+      return dm_dit_forward(h, x, t, y, B, out, stream);
+    }
+  }
+  return DM_OK;
+}
+
+extern "C" int dm_dit_set_math(dm_dit* h, int kind) {
+  if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
+  if (kind != 0 && kind != DM_SPLIT_FP16X2) { dm::set_error("DiT math must be 0 (fp32) or DM_SPLIT_FP16X2"); return DM_ERR_ARG; }
+  if (kind != h->m->math) {
+    h->m->math = kind;
+    h->m->plan.reset();
+  }
+  return DM_OK;
+}
+
+extern "C" int dm_dit_get_math(const dm_dit* h, int* kind) {
+  if (!h || !h->m || !kind) { dm::set_error("null model"); return DM_ERR_STATE; }
+  *kind = h->m->math;
   return DM_OK;
 }
 

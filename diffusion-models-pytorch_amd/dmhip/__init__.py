@@ -24,6 +24,7 @@ from dmhip._lib import (  # noqa: F401
     pack_conv_weight_subpixel,
     pack_conv_weight_split,
     unet_conv_math,
+    dit_math,
     SPLIT_FP16X2,
     SPLIT_BF16X3,
     gemm,

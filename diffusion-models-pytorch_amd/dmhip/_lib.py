@@ -147,6 +147,8 @@ def _declare(L: ctypes.CDLL):
                                             ctypes.c_int, ctypes.c_int, vp, vp]
     L.dm_unet_set_conv_math.argtypes = [vp, ctypes.c_int]
     L.dm_unet_get_conv_math.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
+    L.dm_dit_set_math.argtypes = [vp, ctypes.c_int]
+    L.dm_dit_get_math.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
     L.dm_gemm.argtypes = [ctypes.POINTER(GemmDesc), vp]
     L.dm_softmax_rows.argtypes = [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, vp]
     L.dm_timestep_embedding.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp, vp]
@@ -287,6 +289,20 @@ def pack_conv_weight_split(wp: torch.Tensor, nmat: int, Cin: int, taps: int, kin
     check(load().dm_pack_conv_weight_split(wp.data_ptr(), nmat, Cout, K, Cin, taps, kind, out.data_ptr(),
                                            stream_handle(wp.device)), 'dm_pack_conv_weight_split')
     return out
+
+
+def dit_math(handle, kind: Optional[str] = None) -> str:
+    """Set (kind given) and return the GEMM arithmetic of a native DiT handle: 'fp16x2' (default) or
+    'fp32' (dm_dit_set_math / dm_dit_get_math)."""
+    L = load()
+    kinds = {'fp32': 0, 'fp16x2': SPLIT_FP16X2}
+    if kind is not None:
+        if kind not in kinds:
+            raise ValueError(f'DiT math must be one of {sorted(kinds)}')
+        check(L.dm_dit_set_math(handle, kinds[kind]), 'dm_dit_set_math')
+    k = ctypes.c_int()
+    check(L.dm_dit_get_math(handle, ctypes.byref(k)), 'dm_dit_get_math')
+    return {v: n for n, v in kinds.items()}[k.value]
 
 
 def unet_conv_math(handle, kind: Optional[str] = None) -> str:

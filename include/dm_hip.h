@@ -148,6 +148,11 @@ int dm_dit_create(const dm_dit_arch* arch, const float* const* params, const int
 /* x: [B, in_channels, S, S] f32 latents, t: [B] int64, y: [B] int64 labels or NULL (NULL / y[b] < 0 = the
  * null class, dit/model.py:241-242), out: [B, out_channels, S, S] f32. */
 int dm_dit_forward(dm_dit* m, const float* x, const int64_t* t, const int64_t* y, int B, float* out, void* stream);
+/* Arithmetic of the DiT token GEMMs: DM_SPLIT_FP16X2 (default, fp32-accurate products from an fp16 split
+ * on the matrix cores) or 0 (fp32 MFMA; also DM_CONV_MATH=fp32|bf16x3). A forward whose operands leave
+ * the fp16 range is re-run in fp32, which the model then keeps. */
+int dm_dit_set_math(dm_dit* m, int kind);
+int dm_dit_get_math(const dm_dit* m, int* kind);
 /* 128-entry table exp(-ln(1e4) * i / 128) of the 256-wide frequency embedding (dit/model.py:51-54). */
 int dm_dit_set_time_freqs(dm_dit* m, const float* freqs, int n, void* stream);
 int dm_dit_profile(dm_dit* m, int enable);

@@ -97,3 +97,43 @@ def test_dit_forward_with_cfg(cuda, golden):
     ce, ue = full[:2, :3], full[2:, :3]
     torch.testing.assert_close(out[:2, :3], ue + 1.5 * (ce - ue), rtol=0, atol=1e-6)
     assert torch.equal(out[:, 3:], full[:, 3:])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('math', ['fp16x2', 'fp32'])
+def test_dit_math_vs_oracle(cuda, golden, report, math):
+    """The token GEMMs in fp16x2 (default) and fp32 both meet the tolerance on DiT-XL/2 geometry."""
+    import dmhip
+    g, meta = golden('dit')
+    model, _ = _model(meta, 'dit_xl2')
+    model = model.to(cuda)
+    h = model.native_handle(torch.device(cuda))
+    assert dmhip.dit_math(h) == 'fp16x2'
+    assert dmhip.dit_math(h, math) == math
+    x, t, y = (torch.from_numpy(g[f'dit_xl2_{k}']).to(cuda) for k in ('x', 't', 'labels'))
+    err = (model(x, t, y).cpu() - torch.from_numpy(g['dit_xl2_out_y'])).abs().max().item()
+    report(f'dit_forward_dit_xl2_{math}_maxabs_vs_oracle', err)
+    assert err <= TOL, err
+    assert dmhip.dit_math(h) == math
+
+
+@pytest.mark.gpu
+def test_dit_range_fallback(cuda, golden):
+    """fc1 weights x 1e5 push the GELU output (fc2's input, x 2^6) beyond fp16: the fp16x2 forward is
+    re-run in fp32 and equals a forward forced to fp32."""
+    import dmhip
+    g, meta = golden('dit')
+    x, t, y = (torch.from_numpy(g[f'dit_tiny_{k}']).to(cuda) for k in ('x', 't', 'labels'))
+    outs = {}
+    for math in ('fp16x2', 'fp32'):
+        model, _ = _model(meta, 'dit_tiny')
+        with torch.no_grad():
+            for k, v in model.state_dict(keep_vars=True).items():
+                if k.endswith('mlp.fc1.weight'):
+                    v.mul_(1e5)
+        model = model.to(cuda)
+        h = model.native_handle(torch.device(cuda))
+        dmhip.dit_math(h, math)
+        outs[math] = model(x, t, y).cpu()
+        assert dmhip.dit_math(h) == 'fp32'
+    assert torch.equal(outs['fp16x2'], outs['fp32'])
