@@ -351,8 +351,8 @@ std::string conv_label(const ConvArgs& a) {
     conv_patch_pick(a, g);
     const bool x3 = conv_patch3_ok(a, p + 1, g);
     if (x3) s.replace(0, 17, "conv_patch3_kernel");
-    s += "," + std::to_string(a.upsample);
-    s += p == 5 ? ",160" : (x3 ? ",208" : ",288");
+    s += "," + std::to_string(a.stride == 2 ? 4 : a.upsample);
+    s += a.stride == 2 ? ",384" : p == 5 ? ",160" : (x3 ? ",208" : ",288");
     s += a.pro_scale ? ",true" : ",false";
     s += a.ksplit > 1 ? ",true" : ",false";  // rocprofv3 prints the defaulted arguments too
     s += x3 ? "," + std::to_string(a.ws_np) + ">" : ">";  // <..., NP>: 3 bf16x3, 2 fp16x2

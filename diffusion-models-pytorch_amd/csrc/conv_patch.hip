@@ -340,7 +340,26 @@ int launch_patch(const ConvArgs& a, const PatchGeom& g, hipStream_t st) {
 // Patch geometry for a BM-row tile, or false when the shape does not tile
 // (then the im2col kernel is used).
 bool conv_patch_geom(const ConvArgs& a, int BM, PatchGeom& g) {
-  if (a.taps != 9 || a.stride != 1) return false;
+  if (a.taps != 9) return false;
+  if (a.stride == 2) {  // split kernel MODE 4: output rows of 2 TH + 1 input rows, parity-split columns
+    const int Ho = a.Hout, Wo = a.Wout;
+    if (a.upsample || a.Cin2 || a.Hin != 2 * Ho || a.Win != 2 * Wo || Wo > BM || BM % Wo != 0) return false;
+    const int rows = BM / Wo;
+    if (rows <= Ho) {
+      if (Ho % rows != 0) return false;
+      g.TB = 1;
+      g.TH = rows;
+    } else {
+      if (rows % Ho != 0) return false;
+      g.TB = rows / Ho;
+      g.TH = Ho;
+    }
+    g.PH = 2 * g.TH + 1;
+    g.PW = 2 * (Wo + 1);
+    g.P = g.TB * g.PH * g.PW;
+    return true;
+  }
+  if (a.stride != 1) return false;
   const bool sub = a.upsample == 2;  // tiles over the low-res pixels of one parity class
   const int Ho = sub ? a.Hin : a.Hout, Wo = sub ? a.Win : a.Wout;
   if (Wo > BM || BM % Wo != 0) return false;
@@ -370,6 +389,10 @@ bool conv_patch_geom(const ConvArgs& a, int BM, PatchGeom& g) {
 
 
 int conv_patch_pick(const ConvArgs& a, PatchGeom& g) {
+  if (a.stride == 2) {  // only the fp16x2 split kernel has a stride-2 mode (64-row tiles)
+    if (!(a.ws && a.ws_np == 2) || (a.tile != 0 && a.tile != 6)) return 0;
+    return conv_patch_geom(a, 64, g) && g.P <= kPatchS2Max ? 6 : 0;
+  }
   // the split-bf16 kernel's LDS image holds fewer patch pixels at 128-row tiles
   const int max128 = a.ws ? kPatch3Max128 : kPatchMax128, max64 = a.ws ? kPatch3Max64 : kPatchMax64;
   if (a.tile == 4 || a.tile == 0) {
@@ -395,6 +418,10 @@ bool conv_split_eligible(const ConvArgs& a) {
   if (a.taps == 1)  // 1x1 / static-weight GEMM (MODE 3 of the split kernel)
     return a.stride == 1 && !a.upsample && a.Cin2 == 0 && a.Cin1 % 32 == 0 && a.K == a.Cin1 && a.Hout == a.Hin &&
            a.Wout == a.Win;
+  if (a.taps == 9 && a.stride == 2) {  // MODE 4 of the split kernel
+    PatchGeom g;
+    return a.Cin1 % 32 == 0 && conv_patch_geom(a, 64, g) && g.P <= kPatchS2Max;
+  }
   if (a.taps != 9 || a.stride != 1 || a.upsample == 1 || a.Cin1 % 16 != 0 || a.Cin2 % 16 != 0) return false;
   PatchGeom g;
   return conv_patch_geom(a, 64, g) && g.P <= kPatch3Max64;

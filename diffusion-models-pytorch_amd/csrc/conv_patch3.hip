@@ -68,6 +68,10 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
   constexpr int TM = WM / 32, TN = WN / 32;
   static_assert((BM / WM) * NWN == 4, "4 waves per block");
   constexpr bool UP = MODE == 1, SUB = MODE == 2;
+  // MODE 4: stride-2 3x3 (Downsample, models/modules.py:72). The patch holds the (2 TH + 1) input rows
+  // of the tile with each row's columns split by parity ([even | odd], g.PW / 2 each), so the 32 lanes
+  // of a fragment (consecutive output columns) read consecutive LDS rows for every tap.
+  constexpr bool S2 = MODE == 4;
   // MODE 3: 1x1 (pointwise) conv / GEMM with static weights (the attention block's qkv and proj).
   // The "patch" is the tile's own BM rows; a chunk is kPwSlices x 16 channels stored as 16-deep
   // slices per row, which the chunk's kPwSlices "taps" read.
@@ -122,7 +126,7 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
   const float* psrc[PJ];
   bool pok[PJ];
   int pimg[PJ];
-  const int iy_base = UP ? (y0 >> 1) - 1 : y0 - 1;
+  const int iy_base = UP ? (y0 >> 1) - 1 : S2 ? 2 * y0 - 1 : y0 - 1;
 #pragma unroll
   for (int j = 0; j < PJ; ++j) {
     if constexpr (PW1) {
@@ -139,7 +143,9 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
     const int rem = p - img * PHW;
     const int pr = rem / g.PW, pc = rem - (rem / g.PW) * g.PW;
     const int b = b0 + img;
-    const int iy = iy_base + pr, ix = pc - 1;
+    const int half = g.PW >> 1;
+    const int col = S2 ? 2 * (pc - (pc >= half ? half : 0)) + (pc >= half ? 1 : 0) : pc;  // input column + 1
+    const int iy = iy_base + pr, ix = col - 1;
     const bool ok = p < g.P && b < a.B && iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
     pok[j] = ok;
     const int bc = min(b, a.B - 1);
@@ -288,7 +294,10 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
         continue;
       }
       int pr, pc;
-      if (UP) {
+      if (S2) {  // input (2 fy + ky - 1, 2 fx + kx - 1): column parity kx & 1, index fx + kx / 2
+        pr = 2 * fy[i] + ky;
+        pc = (kx & 1) * (g.PW >> 1) + fx[i] + (kx >> 1);
+      } else if (UP) {
         pr = ((fy[i] + ky - 1) >> 1) + 1;
         pc = ((fx[i] + kx - 1) >> 1) + 1;
       } else {
@@ -476,6 +485,8 @@ int launch3(const ConvArgs& a, const PatchGeom& g, hipStream_t st) {
   const int blocks = ceil_div(M, BM) * ceil_div(a.Cout, BN) * (sub ? 4 : 1) * ks;
   if (sub)
     launch3_mode<BM, BN, WM, WN, 2, MAXP, NP>(a, g, blocks, st);
+  else if (a.stride == 2)
+    launch3_mode<BM, BN, WM, WN, 4, MAXP, NP>(a, g, blocks, st);
   else if (a.upsample)
     launch3_mode<BM, BN, WM, WN, 1, MAXP, NP>(a, g, blocks, st);
   else
@@ -562,6 +573,7 @@ __global__ void split_conv_weights_kernel(const float* w, int nmat, int rows, in
 
 bool conv_patch3_ok(const ConvArgs& a, int which, const PatchGeom& g) {
   if (!a.ws || a.Cin1 % kSK != 0 || a.Cin2 % kSK != 0 || a.K % kSK != 0) return false;
+  if (a.stride == 2) return a.ws_np == 2 && which == 6 && g.P <= kPatchS2Max;  // MODE 4: fp16x2, 64-row tiles
   if (a.ws_np == 2 && a.pro_scale && (long)g.TB * a.Cin1 * 2 > kPwTabFloats) return false;  // LDS GroupNorm tables
   return g.P <= (which == 6 ? kPatch3Max64 : kPatch3Max128);
 }
@@ -594,6 +606,10 @@ int conv2d_patch3(const ConvArgs& a, int which, const PatchGeom& g, hipStream_t 
   if (a.taps == 1) {
     DM_REQUIRE(conv_pw_ok(a), "conv: the split 1x1 path needs fp16x2 weights, stride 1, K = Cin1 % 32 == 0 and LDS room for the GroupNorm tables");
     return which == 4 ? launch_pw<128, 64>(a, st) : launch_pw<64, 32>(a, st);
+  }
+  if (a.stride == 2) {
+    DM_REQUIRE(a.ws_np == 2 && which == 6, "conv: the split stride-2 conv runs fp16x2 on 64-row tiles");
+    return launch3<64, 64, 32, 32, kPatchS2Max, 2>(a, g, st);
   }
   if (a.ws_np == 2) {
     switch (which) {

@@ -73,6 +73,7 @@ constexpr int kPatchMax128 = 288;
 constexpr int kPatchMax64 = 160;
 constexpr int kPatch3Max128 = 208;
 constexpr int kPatch3Max64 = 160;
+constexpr int kPatchS2Max = 384;  // stride-2 split conv (64-row tiles): (2 TH + 1) x 2 (Wo + 1) per image (3 loader passes)
 
 // Output tile = TB images x TH rows x full width; input patch PH x PW per image.
 struct PatchGeom {

@@ -199,7 +199,7 @@ void UNetModel::split_for(ConvArgs& c) {
   c.ws_rowscale = nullptr;
   c.range_flag = nullptr;
   if (!conv_math || !conv_split_eligible(c)) return;
-  if (c.taps == 1 && conv_math != 2) return;  // the split 1x1 path is fp16x2 only
+  if ((c.taps == 1 || c.stride == 2) && conv_math != 2) return;  // the split 1x1 / stride-2 paths are fp16x2 only
   const int nmat = c.upsample == 2 ? 4 : 1;
   const int ntap = c.upsample == 2 ? 4 : c.taps;
   auto key = std::make_pair(c.w, conv_math);

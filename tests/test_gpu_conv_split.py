@@ -173,3 +173,31 @@ def test_split_pointwise_groupnorm_accuracy(cuda, silu):
                   split='fp16x2')
     err = (y.cpu().double() - ref).abs().max().item()
     assert err < 2e-6 * ref.abs().max().item(), err
+
+
+@pytest.mark.parametrize('B,Cin,Cout,H', [(2, 32, 64, 32), (3, 64, 128, 16), (5, 64, 64, 8), (3, 96, 32, 4),
+                                          (2, 128, 256, 16)])
+def test_split_conv_stride2_exact(cuda, B, Cin, Cout, H):
+    """stride-2 3x3 (Downsample) on the split kernel (MODE 4, parity-split patch columns, several images
+    per tile at 4x4 outputs) bit-exact on integer operands."""
+    x = _ints((B, Cin, H, H), -2, 3, seed=40)
+    w = _ints((Cout, Cin, 3, 3), -2, 3, seed=41)
+    b = _ints((Cout, ), seed=42)
+    ref = F.conv2d(x.double(), w.double(), b.double(), stride=2, padding=1).float()
+    Ho = ref.shape[-1]
+    y = _run_conv(cuda, _nhwc(x).to(cuda), _pack(w, cuda), Cout, Ho, Ho, 9, 2, 0, b.to(cuda), split='fp16x2')
+    assert torch.equal(y.cpu(), _nhwc(ref))
+
+
+def test_split_conv_stride2_fp32_accuracy(cuda):
+    """random stride-2 conv: split error vs fp64 within 2x the fp32 kernel's."""
+    g = torch.Generator().manual_seed(43)
+    B, Cin, Cout, H = 8, 128, 128, 32
+    x = torch.randn((B, Cin, H, H), generator=g) * 3
+    w = torch.randn((Cout, Cin, 3, 3), generator=g) * (1.0 / (9 * Cin) ** 0.5)
+    ref = _nhwc(F.conv2d(x.double(), w.double(), stride=2, padding=1))
+    errs = []
+    for split in (False, 'fp16x2'):
+        y = _run_conv(cuda, _nhwc(x).to(cuda), _pack(w, cuda), Cout, H // 2, H // 2, 9, 2, split=split)
+        errs.append((y.cpu().double() - ref).abs().max().item())
+    assert errs[1] < 2.0 * errs[0] + 1e-7 * ref.abs().max().item(), errs
