@@ -9,7 +9,8 @@ config overrides. Launch one process per GPU:
         --weights ckpt.pt --n_samples 2048 --batch_size 256 --sampler ddim --respace_steps 50 --save_dir out
 
 `--weights synthetic` uses the deterministic synthetic weights (no checkpoint
-offline). Samplers: ddpm, ddim, euler, heun. Modes: sample, denoise, progressive, interpolate.
+offline). Samplers: ddpm, ddim, euler, heun. Modes: sample, denoise, progressive, interpolate,
+reconstruction (DDIM inversion of the images under --input_dir, then sampling back).
 """
 import argparse
 import math
@@ -42,10 +43,12 @@ def get_parser():
     p.add_argument('--respace_steps', type=int, default=None, help='Length of respaced timestep sequence')
     p.add_argument('--var_type', type=str, default=None, help='Type of variance of the reverse process')
     p.add_argument('--ddim_eta', type=float, default=0.0, help='Parameter eta in DDIM sampling')
-    p.add_argument('--mode', type=str, default='sample', choices=['sample', 'denoise', 'progressive', 'interpolate'])
+    p.add_argument('--mode', type=str, default='sample', choices=['sample', 'denoise', 'progressive', 'interpolate',
+                                                                          'reconstruction'])
     p.add_argument('--n_denoise', type=int, default=20)
     p.add_argument('--n_progressive', type=int, default=20)
     p.add_argument('--n_interpolate', type=int, default=16, help='Number of intermediate images (interpolate)')
+    p.add_argument('--input_dir', type=str, required=False, help='Directory of images (reconstruction)')
     return p
 
 
@@ -69,7 +72,7 @@ def build_diffuser(args, conf, device):
     raise ValueError(f'Unknown sampler: {args.sampler}')
 
 
-# reference sample_uncond.py:22-27 (reconstruction needs an image directory + data loaders: not provided)
+# reference sample_uncond.py:22-27
 COMPATIBLE_SAMPLER_MODE = dict(
     ddpm=['sample', 'denoise', 'progressive'],
     ddim=['sample', 'denoise', 'progressive', 'interpolate', 'reconstruction'],
@@ -101,6 +104,35 @@ def parse_with_overrides(argv=None):
 
 
 @torch.no_grad()
+def reconstruction(args, conf, env, diffuser, model):
+    """Reference sample_uncond.py:279-312: DDIM-invert each batch of input images to noise, sample it back,
+    save [input, reconstruction] side by side. Batches are dealt to ranks round-robin as accelerate's
+    prepared DataLoader does (batch k*world + rank), gathered in rank order, and the padding of the last
+    round is dropped (gather_for_metrics)."""
+    from utils.imagedir import ImageDir
+    dataset = ImageDir(args.input_dir, conf.data.params.img_size)
+    n = min(args.n_samples, len(dataset))
+    bspp = min(args.batch_size, math.ceil(n / env.world))
+    n_batches = math.ceil(n / bspp)
+    idx = 0
+    for rnd in range(math.ceil(n_batches / env.world)):
+        b = rnd * env.world + env.rank
+        lo = b * bspp
+        ids = [(lo + j) % n for j in range(bspp)]   # padding wraps to the start, like even_batches
+        X = torch.stack([dataset[k] for k in ids]).to(env.device)
+        tq = dict(desc=f'img2noise {rnd}', disable=not env.is_main)
+        noise = diffuser.sample_inversion(model=model, img=X, tqdm_kwargs=tq)
+        recX = diffuser.sample(model=model, init_noise=noise, tqdm_kwargs=dict(tq, desc=f'noise2img {rnd}'))
+        keep = max(0, min(n - rnd * env.world * bspp, env.world * bspp))
+        X, recX = env.gather(X)[:keep], env.gather(recX)[:keep]
+        if env.is_main:
+            for x, r in zip(X, recX):
+                save_image([image_norm_to_float(x).cpu(), image_norm_to_float(r).cpu()],
+                           os.path.join(args.save_dir, f'{idx}.png'), nrow=2)
+                idx += 1
+
+
+@torch.no_grad()
 def main(argv=None):
     args, conf = parse_with_overrides(argv)
     env = DistEnv()
@@ -114,6 +146,13 @@ def main(argv=None):
     n_seq = len(diffuser.respaced_seq)
     if args.mode not in COMPATIBLE_SAMPLER_MODE[args.sampler] and env.is_main:
         print(f'`{args.mode}` mode is not designed for `{args.sampler}` sampler, unexpected behavior may occur.')
+    if args.mode == 'reconstruction':
+        if args.input_dir is None:
+            raise ValueError('input_dir is required for mode `reconstruction`')
+        reconstruction(args, conf, env, diffuser, model)
+        env.barrier()
+        env.close()
+        return
     idx = 0
     for i, bs in enumerate(folds):
         tq = dict(desc=f'Fold {i}/{len(folds)}', disable=not env.is_main)
@@ -127,8 +166,8 @@ def main(argv=None):
             samples = env.gather(samples)[:bs]
             if env.is_main:
                 for x in samples:
-                    save_image(image_norm_to_float(torch.cat(list(x), dim=-1).float().cpu()),
-                               os.path.join(args.save_dir, f'{idx}.png'))
+                    save_image(image_norm_to_float(x.float().cpu()), os.path.join(args.save_dir, f'{idx}.png'),
+                               nrow=len(x))
                     idx += 1
             continue
         init_noise = torch.randn((bspp, *img_shape), device=env.device)
@@ -143,10 +182,9 @@ def main(argv=None):
             samples = torch.stack(keep, dim=1).clamp(-1, 1)
         samples = env.gather(samples)[:bs]
         if env.is_main:
-            for x in samples:
-                if x.ndim == 4:  # a row of intermediate images -> one strip
-                    x = torch.cat(list(x), dim=-1)
-                save_image(image_norm_to_float(x.float().cpu()), os.path.join(args.save_dir, f'{idx}.png'))
+            for x in samples:   # a row of intermediate images is one nrow=len(x) grid
+                save_image(image_norm_to_float(x.float().cpu()), os.path.join(args.save_dir, f'{idx}.png'),
+                           nrow=len(x) if x.ndim == 4 else 1)
                 idx += 1
     env.barrier()
     env.close()

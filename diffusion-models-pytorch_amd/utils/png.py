@@ -1,8 +1,10 @@
 """Minimal PNG writer (torchvision is absent here).
 
-Matches torchvision.utils.save_image for a single image: float [0, 1] ->
-uint8 via x * 255 + 0.5 clamped and truncated; 1-channel images are
-replicated to RGB (make_grid does this for one image, no padding).
+Restates torchvision 0.16 utils.make_grid / save_image (torchvision is absent, so
+byte parity with it is unpinned): a [B, C, H, W] tensor or a list of [C, H, W]
+images is tiled nrow per row with `padding` pixels of `pad_value` around every
+tile (a single image is returned as is, no padding); 1-channel images are
+replicated to RGB; float [0, 1] -> uint8 via x * 255 + 0.5 clamped and truncated.
 """
 import struct
 import zlib
@@ -15,6 +17,35 @@ def _chunk(tag: bytes, data: bytes) -> bytes:
     return struct.pack('>I', len(data)) + tag + data + struct.pack('>I', zlib.crc32(tag + data) & 0xFFFFFFFF)
 
 
+def make_grid(tensor, nrow: int = 8, padding: int = 2, pad_value: float = 0.0) -> torch.Tensor:
+    """torchvision/utils.py make_grid (0.16), normalize=False."""
+    if isinstance(tensor, (list, tuple)):
+        tensor = torch.stack(list(tensor), dim=0)
+    if tensor.dim() == 2:
+        tensor = tensor.unsqueeze(0)
+    if tensor.dim() == 3:
+        if tensor.shape[0] == 1:
+            tensor = torch.cat((tensor, tensor, tensor), 0)
+        tensor = tensor.unsqueeze(0)
+    if tensor.dim() == 4 and tensor.shape[1] == 1:
+        tensor = torch.cat((tensor, tensor, tensor), 1)
+    if tensor.shape[0] == 1:
+        return tensor.squeeze(0)
+    n = tensor.shape[0]
+    xmaps = min(nrow, n)
+    ymaps = (n + xmaps - 1) // xmaps
+    height, width = tensor.shape[2] + padding, tensor.shape[3] + padding
+    grid = tensor.new_full((tensor.shape[1], height * ymaps + padding, width * xmaps + padding), pad_value)
+    k = 0
+    for y in range(ymaps):
+        for x in range(xmaps):
+            if k >= n:
+                break
+            grid[:, y * height + padding:(y + 1) * height, x * width + padding:(x + 1) * width] = tensor[k]
+            k += 1
+    return grid
+
+
 def to_uint8(image: torch.Tensor) -> np.ndarray:
     """[C, H, W] float in [0, 1] -> [H, W, 3] uint8."""
     x = image.detach().to('cpu', torch.float32)
@@ -23,7 +54,10 @@ def to_uint8(image: torch.Tensor) -> np.ndarray:
     return x.mul(255).add_(0.5).clamp_(0, 255).permute(1, 2, 0).to(torch.uint8).numpy()
 
 
-def save_image(image: torch.Tensor, path: str):
+def save_image(image, path: str, nrow: int = 8, padding: int = 2, pad_value: float = 0.0):
+    """torchvision/utils.py save_image (0.16): make_grid, then one 8-bit RGB PNG."""
+    if isinstance(image, (list, tuple)) or image.dim() == 4:
+        image = make_grid(image, nrow=nrow, padding=padding, pad_value=pad_value)
     rgb = to_uint8(image)
     h, w, _ = rgb.shape
     raw = b''.join(b'\x00' + rgb[y].tobytes() for y in range(h))

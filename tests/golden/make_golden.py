@@ -428,9 +428,36 @@ def make_samplers():
     save('samplers', meta, **arr)
 
 
+def make_inversion():
+    """DDIM inversion + reconstruction (diffusions/ddim.py:88-132, scripts/sample_uncond.py:279-312):
+    per-step sample_inversion_loop and sample_loop outputs on the tiny UNet, 5 uniform steps, B=2."""
+    torch.set_num_threads(8)
+    schedule, ddpm, ddim, unet = import_reference()
+    meta = dict(torch=torch.__version__, threads=torch.get_num_threads(), coef_probe_sha=coef_probe_sha(),
+                reference='xyfJASON/diffusion-models-pytorch @ 2024-12-20 (/root/reference)')
+    model = unet.UNet(**ARCHS['tiny']).eval()
+    meta['tiny_weights_sha256'] = synthetic(model)
+    d = ddim.DDIM(respace_type='uniform', respace_steps=5, eta=0.0)
+    g = torch.Generator().manual_seed(31)
+    img = torch.rand((2, 3, 16, 16), generator=g) * 2 - 1   # an "image" in [-1, 1]
+    arr = dict(img=img)
+    with torch.no_grad():
+        x = img
+        for i, out in enumerate(d.sample_inversion_loop(model, img, tqdm_kwargs=dict(disable=True))):
+            arr[f'inv_step{i}_sample'], arr[f'inv_step{i}_pred_x0'] = out['sample'], out['pred_x0']
+            x = out['sample']
+        meta['inv_steps'] = i + 1
+        for i, out in enumerate(d.sample_loop(model, x, tqdm_kwargs=dict(disable=True))):
+            arr[f'rec_step{i}_sample'] = out['sample']
+        meta['rec_steps'] = i + 1
+    save('inversion', meta, **arr)
+
+
 if __name__ == '__main__':
     if sys.argv[1:] == ['samplers']:
         make_samplers()
+    elif sys.argv[1:] == ['inversion']:
+        make_inversion()
     elif sys.argv[1:] == ['adagn']:
         make_adagn()
     elif sys.argv[1:] == ['adm']:
@@ -440,3 +467,4 @@ if __name__ == '__main__':
         make_adagn()
         make_adm()
         make_samplers()
+        make_inversion()

@@ -77,3 +77,70 @@ def test_sample_uncond_script(cuda, tmp_path, sampler, mode):
                         '--respace_steps', '4', '--n_interpolate', '3', '--n_progressive', '2'])
     files = sorted(os.listdir(tmp_path))
     assert files == ['0.png', '1.png', '2.png'], files
+
+
+def test_ddim_inversion_reconstruction_trajectory(cuda, golden, report):
+    """DDIM.sample_inversion_loop then sample_loop on the engine vs the reference (ddim.py:88-132,
+    sample_uncond.py:297-304; tests/golden/inversion.npz). Every step teacher-forced from the reference's
+    previous sample <= 1e-4; free-running (inversion feeding reconstruction) <= 5e-4: x0 = sqrt(1/ac_t) x - ...
+    amplifies a 1e-6 forward difference by up to ~160 at t ~ 960 (as for the CFG loops)."""
+    from diffusions import DDIM
+    arrays, meta = golden('inversion')
+    model, sha = _model(golden('forward')[1], 'tiny', cuda)
+    assert sha == meta['tiny_weights_sha256']
+    d = DDIM(respace_type='uniform', respace_steps=5, eta=0.0, device=cuda)
+    seq = d.respaced_seq.tolist()
+    ref = lambda k: torch.from_numpy(arrays[k]).to(cuda)  # noqa: E731
+    tb = lambda t: torch.full((2, ), t, dtype=torch.long, device=cuda)  # noqa: E731
+    forced = 0.0
+    for i, (t, tn) in enumerate(zip(seq[:-1], seq[1:])):
+        x = ref('img') if i == 0 else ref(f'inv_step{i - 1}_sample')
+        out = d.denoise_inversion(model(x, tb(t)), x, t, tn)
+        err = np.abs(out['sample'].cpu().numpy() - arrays[f'inv_step{i}_sample']).max()
+        forced = max(forced, err)
+        assert err <= TOL, ('inv', i, err)
+    prev = [-1] + seq[:-1]
+    for i, (t, tp) in enumerate(zip(reversed(seq), reversed(prev))):
+        x = ref(f'inv_step{meta["inv_steps"] - 1}_sample') if i == 0 else ref(f'rec_step{i - 1}_sample')
+        out = d.denoise(model(x, tb(t)), x, t, tp)
+        err = np.abs(out['sample'].cpu().numpy() - arrays[f'rec_step{i}_sample']).max()
+        forced = max(forced, err)
+        assert err <= TOL, ('rec', i, err)
+    free = 0.0
+    x = ref('img')
+    for i, out in enumerate(d.sample_inversion_loop(model, x, tqdm_kwargs=dict(disable=True))):
+        free = max(free, np.abs(out['sample'].cpu().numpy() - arrays[f'inv_step{i}_sample']).max())
+        x = out['sample']
+    assert i + 1 == meta['inv_steps']
+    for i, out in enumerate(d.sample_loop(model, x, tqdm_kwargs=dict(disable=True))):
+        free = max(free, np.abs(out['sample'].cpu().numpy() - arrays[f'rec_step{i}_sample']).max())
+    assert free <= 5 * TOL, free
+    report('ddim_inversion_reconstruction_tiny_teacher_forced_maxabs_vs_reference', forced)
+    report('ddim_inversion_reconstruction_tiny_free_running_maxabs_vs_reference', free)
+
+
+def test_sample_uncond_reconstruction(cuda, tmp_path):
+    """--mode reconstruction (sample_uncond.py:279-336): inverts every image under --input_dir and writes
+    [input, reconstruction] as one nrow=2 grid per image; a missing --input_dir is a ValueError."""
+    import os
+    from PIL import Image
+    from scripts import sample_uncond
+    from utils.png import read_png_rgb
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cfg = os.path.join(root, 'diffusion-models-pytorch_amd', 'configs', 'ddpm_cifar10.yaml')
+    src = tmp_path / 'in'
+    src.mkdir()
+    rng = np.random.default_rng(1)
+    for k in range(3):
+        Image.fromarray(rng.integers(0, 256, (32, 32, 3), dtype=np.uint8)).save(src / f'{k}.png')
+    out = tmp_path / 'out'
+    args = ['-c', cfg, '--weights', 'synthetic', '--n_samples', '3', '--batch_size', '2', '--save_dir', str(out),
+            '--sampler', 'ddim', '--respace_steps', '3', '--mode', 'reconstruction']
+    with pytest.raises(ValueError):
+        sample_uncond.main(args)
+    sample_uncond.main(args + ['--input_dir', str(src)])
+    assert sorted(os.listdir(out)) == ['0.png', '1.png', '2.png']
+    grid = read_png_rgb(str(out / '1.png'))
+    assert grid.shape == (36, 70, 3)
+    # the left tile is the input image itself ((x+1)/2 of its normalised value round-trips the bytes)
+    assert np.array_equal(grid[2:34, 2:34], np.asarray(Image.open(src / '1.png')))
