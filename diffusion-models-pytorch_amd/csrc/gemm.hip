@@ -83,8 +83,15 @@ gemm_kernel(GemmArgs g) {
       brow[j] = Bm + (size_t)min(n, g.N - 1) * g.ldb + 4 * lc4;
     }
   }
+  // SPLIT with the [k][n] B layout: each thread loads a 4 (k) x 4 (n) block (rows 4 kq .. 4 kq + 3,
+  // columns 4 n4 ..) and stores it transposed as 4 rows of 4 consecutive k per piece (ds_write_b64),
+  // instead of 2-byte scatter stores; lanes kq = t % 8 of one n4 hit distinct banks
+  constexpr bool KN4 = B_KN && SPLIT;
+  constexpr int KN4_THREADS = 2 * BN;  // (kBK / 4) x (BN / 4)
+  static_assert(!KN4 || (kBK == 32 && KN4_THREADS <= Cfg::NT), "KN4 loader geometry");
+  const int kq = t & 7, n4k = t >> 3;
   f4 ra[Cfg::A_ITERS];
-  f4 rb[B_KN ? KN_ITERS : Cfg::B_ITERS];
+  f4 rb[KN4 ? 4 : B_KN ? KN_ITERS : Cfg::B_ITERS];
   bool k_ok = true;
   bool kn_ok[B_KN ? KN_ITERS : 1];
   int ld_k = 0;
@@ -102,6 +109,13 @@ gemm_kernel(GemmArgs g) {
 #pragma unroll
       for (int j = 0; j < Cfg::B_ITERS; ++j)
         rb[j] = *reinterpret_cast<const f4*>(k_ok ? brow[j] + kofs : kZeroPage);
+    } else if constexpr (KN4) {
+      const int n = min(n0 + 4 * min(n4k, BN / 4 - 1), g.N - 4);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int kk = kt * kBK + 4 * kq + r;
+        rb[r] = *reinterpret_cast<const f4*>(kk < g.K ? Bm + (size_t)kk * g.ldb + n : kZeroPage);
+      }
     } else {
       const int n4 = t % KN_C4, kr = t / KN_C4;
       const int n = min(n0 + 4 * n4, g.N - 4);
@@ -156,6 +170,19 @@ gemm_kernel(GemmArgs g) {
           *reinterpret_cast<f16x4*>(dst + 8) = lo;
         } else {
           *reinterpret_cast<f4*>(Bs + (lrow + j * Cfg::ROWS_PER_PASS) * kLDK + 4 * lc4) = v;
+        }
+      }
+    } else if constexpr (KN4) {
+      if (t < KN4_THREADS) {
+        _Float16* Bh = reinterpret_cast<_Float16*>(Bs);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f4 col = {rb[0][q], rb[1][q], rb[2][q], rb[3][q]};  // k = 4 kq .. 4 kq + 3 of column q
+          f16x4 hi, lo;
+          Split<2>::split4(col * b_pow, hi, lo, bad);
+          _Float16* dst = Bh + (4 * n4k + q) * kLDK16 + split_off(4 * kq);
+          *reinterpret_cast<f16x4*>(dst) = hi;
+          *reinterpret_cast<f16x4*>(dst + 8) = lo;
         }
       }
     } else {
