@@ -236,13 +236,27 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
             rs[j][h][1] = *reinterpret_cast<const f4*>(ts + tab_n * a.Cin1 + 4 * h);
           }
         }
+        // MODE 3: two code paths behind a uniform branch (a select would evaluate the SiLU, 2
+        // transcendentals per value, for the GroupNorm-only prologue of the attention qkv as well)
+        if (!PW1) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
+          for (int h = 0; h < 2; ++h)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float v = rp[j][h][q] * rs[j][h][0][q] + rs[j][h][1][q];
-            rp[j][h][q] = pro_silu ? silu_fast(v) : v;
-          }
+            for (int q = 0; q < 4; ++q) {
+              const float v = rp[j][h][q] * rs[j][h][0][q] + rs[j][h][1][q];
+              rp[j][h][q] = pro_silu ? silu_fast(v) : v;
+            }
+        } else if (pro_silu) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) rp[j][h][q] = silu_fast(rp[j][h][q] * rs[j][h][0][q] + rs[j][h][1][q]);
+        } else {
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) rp[j][h][q] = rp[j][h][q] * rs[j][h][0][q] + rs[j][h][1][q];
+        }
       }
     }
   };
