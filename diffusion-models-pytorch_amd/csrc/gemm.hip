@@ -10,6 +10,7 @@
 // (image, head).
 #include <cmath>
 #include <cstring>
+#include <type_traits>
 #include "dm_common.h"
 #include "dm_kernels.h"
 #include "mfma_tile.h"
@@ -25,7 +26,7 @@ namespace {
 constexpr int kLDK16 = 2 * kLDK;  // fp16 elements per LDS row
 
 template <int BM, int BN, int WM, int WN, bool B_KN, bool SPLIT = false>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, 2)
 gemm_kernel(GemmArgs g) {
   using Cfg = TileCfg<BM, BN, WM, WN>;
   __shared__ __attribute__((aligned(16))) float lds[Cfg::LDS_FLOATS];
@@ -90,31 +91,34 @@ gemm_kernel(GemmArgs g) {
   constexpr int KN4_THREADS = 2 * BN;  // (kBK / 4) x (BN / 4)
   static_assert(!KN4 || (kBK == 32 && KN4_THREADS <= Cfg::NT), "KN4 loader geometry");
   const int kq = t & 7, n4k = t >> 3;
-  f4 ra[Cfg::A_ITERS];
-  f4 rb[KN4 ? 4 : B_KN ? KN_ITERS : Cfg::B_ITERS];
-  bool k_ok = true;
+  // SPLIT ([n][k] B): two register sets, tiles loaded two K steps ahead (a step's MFMAs alone do not cover the
+  // load latency at K = 256); set index = K step parity, a compile-time constant (loop unrolled by 2)
+  constexpr int NSET = SPLIT && !B_KN ? 2 : 1;  // (the [k][n] loader's second set spilled)
+  f4 ra[NSET][Cfg::A_ITERS];
+  f4 rb[NSET][KN4 ? 4 : B_KN ? KN_ITERS : Cfg::B_ITERS];
   bool kn_ok[B_KN ? KN_ITERS : 1];
-  int ld_k = 0;
+  int ld_k[NSET];
 
   // K tail: B reads the zero page (mfma_tile.h kZeroPage) so those products vanish; A reads a
   // clamped, finite column. Rows >= M / columns >= N read clamped data and are never stored.
-  auto load_tile = [&](int kt) {
+  auto load_tile = [&](int kt, auto set_c) {
+    constexpr int S = decltype(set_c)::value;
     const int k = kt * kBK + 4 * lc4;
-    k_ok = k < g.K;
-    ld_k = k_ok ? k : 0;
-    const int kofs = ld_k - 4 * lc4;
+    const bool k_ok = k < g.K;
+    ld_k[S] = k_ok ? k : 0;
+    const int kofs = ld_k[S] - 4 * lc4;
 #pragma unroll
-    for (int i = 0; i < Cfg::A_ITERS; ++i) ra[i] = *reinterpret_cast<const f4*>(arow[i] + kofs);
+    for (int i = 0; i < Cfg::A_ITERS; ++i) ra[S][i] = *reinterpret_cast<const f4*>(arow[i] + kofs);
     if constexpr (!B_KN) {
 #pragma unroll
       for (int j = 0; j < Cfg::B_ITERS; ++j)
-        rb[j] = *reinterpret_cast<const f4*>(k_ok ? brow[j] + kofs : kZeroPage);
+        rb[S][j] = *reinterpret_cast<const f4*>(k_ok ? brow[j] + kofs : kZeroPage);
     } else if constexpr (KN4) {
       const int n = min(n0 + 4 * min(n4k, BN / 4 - 1), g.N - 4);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int kk = kt * kBK + 4 * kq + r;
-        rb[r] = *reinterpret_cast<const f4*>(kk < g.K ? Bm + (size_t)kk * g.ldb + n : kZeroPage);
+        rb[S][r] = *reinterpret_cast<const f4*>(kk < g.K ? Bm + (size_t)kk * g.ldb + n : kZeroPage);
       }
     } else {
       const int n4 = t % KN_C4, kr = t / KN_C4;
@@ -123,26 +127,27 @@ gemm_kernel(GemmArgs g) {
       for (int j = 0; j < KN_ITERS; ++j) {
         const int kk = kt * kBK + kr + j * KN_ROWS_PER_PASS;
         kn_ok[j] = (kr + j * KN_ROWS_PER_PASS < kBK);
-        rb[j] = *reinterpret_cast<const f4*>(kk < g.K ? Bm + (size_t)kk * g.ldb + n : kZeroPage);
+        rb[S][j] = *reinterpret_cast<const f4*>(kk < g.K ? Bm + (size_t)kk * g.ldb + n : kZeroPage);
       }
     }
   };
 
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](int buf, auto set_c) {
+    constexpr int S = decltype(set_c)::value;
     float* As = lds + buf * Cfg::STAGE;
     float* Bs = As + Cfg::A_ELEMS;
 #pragma unroll
     for (int i = 0; i < Cfg::A_ITERS; ++i) {
-      f4 v = ra[i];
+      f4 v = ra[S][i];
       if (g.pro_scale) {  // fused GroupNorm (no activation): x * scale[img][k] + shift[img][k]
-        const f4 sc = *reinterpret_cast<const f4*>(g.pro_scale + (size_t)a_img[i] * g.K + ld_k);
-        const f4 sh = *reinterpret_cast<const f4*>(g.pro_shift + (size_t)a_img[i] * g.K + ld_k);
+        const f4 sc = *reinterpret_cast<const f4*>(g.pro_scale + (size_t)a_img[i] * g.K + ld_k[S]);
+        const f4 sh = *reinterpret_cast<const f4*>(g.pro_shift + (size_t)a_img[i] * g.K + ld_k[S]);
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = v[q] * sc[q] + sh[q];
       }
       if (g.ln_stats) {  // LayerNorm (no affine) + modulate x * (1 + scale) + shift
-        const f4 sc = *reinterpret_cast<const f4*>(g.ln_scale + (size_t)a_img[i] * g.ln_pitch + ld_k);
-        const f4 sh = *reinterpret_cast<const f4*>(g.ln_shift + (size_t)a_img[i] * g.ln_pitch + ld_k);
+        const f4 sc = *reinterpret_cast<const f4*>(g.ln_scale + (size_t)a_img[i] * g.ln_pitch + ld_k[S]);
+        const f4 sh = *reinterpret_cast<const f4*>(g.ln_shift + (size_t)a_img[i] * g.ln_pitch + ld_k[S]);
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = ((v[q] - a_ln[i].x) * a_ln[i].y) * (1.0f + sc[q]) + sh[q];
       }
@@ -160,7 +165,7 @@ gemm_kernel(GemmArgs g) {
     if constexpr (!B_KN) {
 #pragma unroll
       for (int j = 0; j < Cfg::B_ITERS; ++j) {
-        const f4 v = (g.b_scale != 0.0f && g.b_scale != 1.0f) ? rb[j] * g.b_scale : rb[j];
+        const f4 v = (g.b_scale != 0.0f && g.b_scale != 1.0f) ? rb[S][j] * g.b_scale : rb[S][j];
         if constexpr (SPLIT) {
           f16x4 hi, lo;
           Split<2>::split4(v * b_pow, hi, lo, bad);
@@ -177,7 +182,7 @@ gemm_kernel(GemmArgs g) {
         _Float16* Bh = reinterpret_cast<_Float16*>(Bs);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const f4 col = {rb[0][q], rb[1][q], rb[2][q], rb[3][q]};  // k = 4 kq .. 4 kq + 3 of column q
+          const f4 col = {rb[S][0][q], rb[S][1][q], rb[S][2][q], rb[S][3][q]};  // k = 4 kq .. 4 kq + 3 of column q
           f16x4 hi, lo;
           Split<2>::split4(col * b_pow, hi, lo, bad);
           _Float16* dst = Bh + (4 * n4k + q) * kLDK16 + split_off(4 * kq);
@@ -191,7 +196,7 @@ gemm_kernel(GemmArgs g) {
       for (int j = 0; j < KN_ITERS; ++j) {
         const int kk = kr + j * KN_ROWS_PER_PASS;
         if (kn_ok[j]) {
-          const f4 v = rb[j];
+          const f4 v = rb[S][j];
           if constexpr (SPLIT) {
             f16x4 hi, lo;
             Split<2>::split4(v * b_pow, hi, lo, bad);
@@ -218,12 +223,7 @@ gemm_kernel(GemmArgs g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  load_tile(0);
-  store_tile(0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) load_tile(kt + 1);
+  auto compute_tile = [&](int buf) {
     const float* As = lds + buf * Cfg::STAGE;
     const float* Bs = As + Cfg::A_ELEMS;
     if constexpr (SPLIT) {
@@ -251,8 +251,35 @@ gemm_kernel(GemmArgs g) {
     } else {
       mfma_slice<Cfg::TM, Cfg::TN>(As, Bs, wm * WM, wn * WN, lane, acc);
     }
-    if (kt + 1 < nk) store_tile(buf ^ 1);
+  };
+  const std::integral_constant<int, 0> set0{};
+  const std::integral_constant<int, 1> set1{};
+  load_tile(0, set0);
+  store_tile(0, set0);
+  if constexpr (NSET == 2) {
+    if (nk > 1) load_tile(1, set1);
     __syncthreads();
+    // step kt: set (kt & 1) held tile kt (already in LDS) and receives tile kt + 2; the other set
+    // holds tile kt + 1, stored after this step's MFMAs
+    auto step = [&](int kt, auto cur, auto nxt) {
+      if (kt + 2 < nk) load_tile(kt + 2, cur);
+      compute_tile(decltype(cur)::value);
+      if (kt + 1 < nk) store_tile(decltype(nxt)::value, nxt);
+      __syncthreads();
+    };
+    for (int kt = 0; kt < nk; kt += 2) {
+      step(kt, set0, set1);
+      if (kt + 1 < nk) step(kt + 1, set1, set0);
+    }
+  } else {
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int buf = kt & 1;
+      if (kt + 1 < nk) load_tile(kt + 1, set0);
+      compute_tile(buf);
+      if (kt + 1 < nk) store_tile(buf ^ 1, set0);
+      __syncthreads();
+    }
   }
   if constexpr (SPLIT) {
     if (bad && g.range_flag) *g.range_flag = 1;
