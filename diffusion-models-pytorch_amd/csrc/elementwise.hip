@@ -55,6 +55,35 @@ __global__ void softmax_rows_kernel(float* __restrict__ x, long rows, int L, int
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
   float* r = x + row * ld;
+  if (L <= 512) {
+    // the row in registers (8 per lane): one read and one write of S instead of five passes; same
+    // per-lane order of the max / exp / sum / scale as the loop below, so the same bits
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j = lane + 64 * u;
+      v[u] = j < L ? r[j] : -INFINITY;
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) mx = fmaxf(mx, v[u]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    float sum = 0.f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (lane + 64 * u < L) {
+        v[u] = expf(v[u] - mx);
+        sum += v[u];
+      }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+    const float inv = 1.0f / sum;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (lane + 64 * u < L) r[lane + 64 * u] = v[u] * inv;
+    return;
+  }
   float mx = -INFINITY;
   for (int j = lane; j < L; j += 64) mx = fmaxf(mx, r[j]);
 #pragma unroll

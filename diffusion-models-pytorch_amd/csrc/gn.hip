@@ -38,12 +38,22 @@ __global__ void gn_partial_kernel(const float* __restrict__ x, int HW, int C, in
   const int p_end = min(HW, p_beg + pix_per_chunk);
   if (py < PY) {
     const float* base = x + (size_t)b * HW * pitch + 4 * c4;
-    for (int p = p_beg + py; p < p_end; p += PY) {
-      float4 v = *reinterpret_cast<const float4*>(base + (size_t)p * pitch);
+    // four pixels' loads in flight before their (in-order) accumulation: the loop otherwise keeps
+    // one 16-B load per thread outstanding and runs latency-bound
+    auto acc4 = [&](const float4 v) {
       s0 += v.x; s1 += v.y; s2 += v.z; s3 += v.w;
       q0 += (double)v.x * v.x; q1 += (double)v.y * v.y;
       q2 += (double)v.z * v.z; q3 += (double)v.w * v.w;
+    };
+    int p = p_beg + py;
+    for (; p + 3 * PY < p_end; p += 4 * PY) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(base + (size_t)(p + u * PY) * pitch);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc4(v[u]);
     }
+    for (; p < p_end; p += PY) acc4(*reinterpret_cast<const float4*>(base + (size_t)p * pitch));
     double* S = smem_d;
     double* Q = smem_d + PY * C;
     S[py * C + 4 * c4 + 0] = s0; S[py * C + 4 * c4 + 1] = s1;

@@ -234,7 +234,7 @@ def test_groupnorm(cuda, B, C, HW, silu, mod):
 
 def test_softmax_rows(cuda):
     g = torch.Generator().manual_seed(50)
-    for L in (16, 256, 1024, 1000):
+    for L in (16, 256, 500, 512, 1024, 1000):
         x = torch.randn((37, L), generator=g) * 5
         xd = x.to(cuda)
         dmhip.softmax_rows(xd, 37, L, L)
