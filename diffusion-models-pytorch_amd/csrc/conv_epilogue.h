@@ -96,11 +96,5 @@ __device__ __forceinline__ void conv_patch_epilogue(const ConvArgs& a, f16v (&ac
   }
 }
 
-// XCD-aware bijective block remap: consecutive logical tiles land on one XCD (shared L2).
-__device__ __forceinline__ int xcd_remap_p(int bid, int nblk) {
-  const int q = nblk >> 3, r = nblk & 7;
-  const int xcd = bid & 7, idx = bid >> 3;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
-}
 
 }  // namespace dm

@@ -48,6 +48,13 @@ __device__ __forceinline__ void gn_emit_group(double s, double q, int lr, int lh
   if (store && lh == 0 && (lr % cpg) == 0) *dst = make_double2(s, q);
 }
 static __device__ __attribute__((aligned(16))) float kZeroPage[kZeroPageFloats];
+
+// XCD-aware bijective block remap: consecutive logical tiles land on one XCD (shared L2).
+__device__ __forceinline__ int xcd_remap_p(int bid, int nblk) {
+  const int q = nblk >> 3, r = nblk & 7;
+  const int xcd = bid & 7, idx = bid >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
 typedef float f16v __attribute__((ext_vector_type(16)));
 
 constexpr int kBK = 32;
