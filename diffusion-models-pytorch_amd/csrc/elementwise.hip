@@ -130,15 +130,40 @@ __global__ void __launch_bounds__(256) conv3x3_small_in_kernel(const float* __re
 #pragma unroll
     for (int k = 0; k < CIN * 9; ++k) wr[k] = w[(size_t)co * CIN * 9 + k];
     const float bc = bias[co];
-    for (int ox = threadIdx.x / lanes_per_px; ox < W; ox += px_par) {
+    // a contiguous run of pixels per thread with a sliding 3x3 window in registers: one new LDS
+    // column (3 CIN broadcasts) per pixel instead of 9 CIN; same products in the same order
+    const int R = (W + px_par - 1) / px_par;
+    const int x0 = (threadIdx.x / lanes_per_px) * R, x1 = min(x0 + R, W);
+    float win[CIN][3][3];
+    if (x0 < x1) {
+#pragma unroll
+      for (int ci = 0; ci < CIN; ++ci)
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+          win[ci][ky][0] = rows[(ci * 3 + ky) * Wp + x0];
+          win[ci][ky][1] = rows[(ci * 3 + ky) * Wp + x0 + 1];
+        }
+    }
+    for (int ox = x0; ox < x1; ++ox) {
+#pragma unroll
+      for (int ci = 0; ci < CIN; ++ci)
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) win[ci][ky][2] = rows[(ci * 3 + ky) * Wp + ox + 2];
       float acc = 0.f;
 #pragma unroll
       for (int ci = 0; ci < CIN; ++ci)
 #pragma unroll
         for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-          for (int kx = 0; kx < 3; ++kx) acc += wr[(ci * 3 + ky) * 3 + kx] * rows[(ci * 3 + ky) * Wp + ox + kx];
+          for (int kx = 0; kx < 3; ++kx) acc += wr[(ci * 3 + ky) * 3 + kx] * win[ci][ky][kx];
       y[(((size_t)b * H + oy) * W + ox) * y_pitch + co] = acc + bc;
+#pragma unroll
+      for (int ci = 0; ci < CIN; ++ci)
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+          win[ci][ky][0] = win[ci][ky][1];
+          win[ci][ky][1] = win[ci][ky][2];
+        }
     }
   }
 }
