@@ -326,6 +326,9 @@ int conv_pick(const ConvArgs& a) {
 }
 
 bool conv_can_emit_gn(const ConvArgs& a) {
+  if (a.ksplit > 1)  // the split-K reduction emits them (conv_splitk_reduce_gn_kernel): one chunk per image
+    return !a.upsample && a.Hout * a.Wout <= kGnPixPerChunk && a.gn_G > 0 && a.Cout % a.gn_G == 0 &&
+           a.Cout <= 1024;
   const int pick = conv_pick(a);
   if (pick != 3 && pick != 4) return false;  // 128-row patch tiles: every wave owns 64 rows
   if (a.upsample || (a.ksplit > 1)) return false;

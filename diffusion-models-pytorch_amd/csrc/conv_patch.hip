@@ -23,6 +23,7 @@
 // with its own combined weights [4][Cout][chunk][4 taps][32]: 4/9 of the MFMA
 // work of convolving the upsampled image. Blocks are split over the 4 parities;
 // the epilogue scatters rows to (2iy + py, 2ix + px).
+#include <algorithm>
 #include "dm_common.h"
 #include "dm_kernels.h"
 #include "mfma_tile.h"
@@ -283,9 +284,61 @@ __global__ void conv_splitk_reduce_kernel(ConvArgs a) {
   a.y[(size_t)m * a.y_pitch + n] = v;
 }
 
+// The same reduction, one block per image, also emitting the GroupNorm statistics of the stored
+// values (maps of <= 64 pixels: the image is one gn_partial chunk, layout [B][1][G]), so the
+// consumer skips its gn_partial launch.
+__global__ void __launch_bounds__(1024) conv_splitk_reduce_gn_kernel(ConvArgs a) {
+  extern __shared__ double red_d[];  // [PG][2][Cout]
+  const int b = blockIdx.x;
+  const int N = a.Cout, HW = a.Hout * a.Wout;
+  const long M = (long)a.B * HW;
+  const int PG = max(1, (int)blockDim.x / N);  // pixel groups: thread (pg, n) sums pixels pg, pg + PG, ..
+  const int t = threadIdx.x;
+  for (int n0 = 0; n0 < N; n0 += blockDim.x) {
+    const int n = n0 + t % min(N, (int)blockDim.x), pg = t / min(N, (int)blockDim.x);
+    if (pg < PG && n < N) {
+      double s1 = 0.0, s2 = 0.0;
+      for (int p = pg; p < HW; p += PG) {
+        const long m = (long)b * HW + p;
+        const long e = m * N + n;
+        float v = a.kpart[e];
+        for (int s = 1; s < a.ksplit; ++s) v = v + a.kpart[(size_t)s * M * N + e];
+        if (a.bias) v = v + a.bias[n];
+        if (a.rowvec) v = v + a.rowvec[(size_t)b * a.rowvec_pitch + n];
+        if (a.res) v = v + a.res[(size_t)m * a.res_pitch + n];
+        a.y[(size_t)m * a.y_pitch + n] = v;
+        s1 += (double)v;
+        s2 += (double)v * v;
+      }
+      red_d[(size_t)pg * 2 * N + n] = s1;
+      red_d[(size_t)pg * 2 * N + N + n] = s2;
+    }
+  }
+  __syncthreads();
+  const int cpg = N / a.gn_G;
+  for (int g = t; g < a.gn_G; g += blockDim.x) {
+    double s1 = 0.0, s2 = 0.0;
+    for (int q = 0; q < PG; ++q)
+      for (int j = 0; j < cpg; ++j) {
+        s1 += red_d[(size_t)q * 2 * N + g * cpg + j];
+        s2 += red_d[(size_t)q * 2 * N + N + g * cpg + j];
+      }
+    a.gn_part[(size_t)b * a.gn_G + g] = make_double2(s1, s2);
+  }
+}
+
 }  // namespace
 
 int conv_splitk_reduce(const ConvArgs& a, hipStream_t st) {
+  if (a.gn_part) {
+    DM_REQUIRE(a.Hout * a.Wout <= kGnPixPerChunk && a.gn_G > 0 && a.Cout % a.gn_G == 0 && a.Cout <= 1024,
+               "conv: split-K GroupNorm statistics need maps of <= 64 pixels and whole groups");
+    const int threads = 1024, pg = std::max(1, threads / a.Cout);
+    hipLaunchKernelGGL(conv_splitk_reduce_gn_kernel, dim3(a.B), dim3(threads), (size_t)pg * 2 * a.Cout * sizeof(double),
+                       st, a);
+    DM_LAUNCH_CHECK();
+    return DM_OK;
+  }
   const long total = (long)a.B * a.Hout * a.Wout * a.Cout;
   hipLaunchKernelGGL(conv_splitk_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, a);
   DM_LAUNCH_CHECK();

@@ -684,7 +684,7 @@ int UNetModel::build_plan(int B, int H, int W) {
   float* kpart_ws = nullptr;
   size_t kpart_floats = 0;
   auto maybe_split = [&](ConvArgs& c) {
-    if (c.gn_part || c.upsample == 2 || c.taps != 9 || c.Hout * c.Wout > 16 || conv_pick(c) < 3) return;
+    if (c.upsample == 2 || c.taps != 9 || c.Hout * c.Wout > 16 || conv_pick(c) < 3) return;
     const int ks = std::min(4, c.Cin1 / 32);
     if (ks < 2) return;
     const size_t need = (size_t)ks * c.B * c.Hout * c.Wout * c.Cout;
@@ -772,7 +772,9 @@ int UNetModel::build_plan(int B, int H, int W) {
     gn_ready.erase(v.p);
     c.gn_part = gn_buf_for(v);
     c.gn_G = G;
-    if (!conv_can_emit_gn(c)) {
+    ConvArgs sk = c;
+    maybe_split(sk);  // split-K is shape-determined; its reduction emits the statistics
+    if (!conv_can_emit_gn(sk)) {
       c.gn_part = nullptr;
       return;
     }
