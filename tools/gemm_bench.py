@@ -13,7 +13,7 @@ import torch  # noqa: E402
 import dmhip  # noqa: E402
 
 
-def bench(name, M, N, K, Z1=1, Z2=1, b_kn=0, res=False, iters=20, split=False, pro=False, ea=6, eb=6):
+def bench(name, M, N, K, Z1=1, Z2=1, b_kn=0, res=False, iters=20, split=False, pro=False, ea=6, eb=6, qkv=False):
     dev = torch.device('cuda', 0)
     A = torch.randn((Z1 * Z2, M, K), device=dev)
     B = torch.randn((Z1 * Z2, K, N) if b_kn else (Z1 * Z2, N, K), device=dev)
@@ -23,6 +23,11 @@ def bench(name, M, N, K, Z1=1, Z2=1, b_kn=0, res=False, iters=20, split=False, p
     d.M, d.N, d.K, d.Z1, d.Z2 = M, N, K, Z1, Z2
     d.A, d.a_s1, d.a_s2, d.lda = A.data_ptr(), Z2 * M * K, M * K, K
     d.B, d.b_s1, d.b_s2, d.ldb, d.b_kn = B.data_ptr(), Z2 * K * N, K * N, (N if b_kn else K), b_kn
+    if qkv:  # the UNet's layout: q / k (/ v) are column blocks of one [Z][L][3C] qkv buffer (C = K = N here)
+        Q = torch.randn((Z1 * Z2, M, 3 * K), device=dev)
+        if not b_kn:  # S = q k^T; PV keeps its contiguous A (the softmax rows) and reads v from qkv
+            d.A, d.a_s1, d.a_s2, d.lda = Q.data_ptr(), M * 3 * K, 0, 3 * K
+        d.B, d.b_s1, d.b_s2, d.ldb = Q.data_ptr() + (4 * 2 * K if b_kn else 4 * K), M * 3 * K, 0, 3 * K
     d.C, d.c_s1, d.c_s2, d.ldc = C.data_ptr(), Z2 * M * N, M * N, N
     d.alpha = 1.0
     if res:
@@ -54,4 +59,6 @@ if __name__ == '__main__':
         bench('proj_res', 65536, 256, 256, res=True, split=sp)
         bench('S', 256, 256, 256, Z1=256, split=sp)
         bench('PV_kn', 256, 256, 256, Z1=256, b_kn=1, split=sp, ea=14)
+        bench('S_qkv', 256, 256, 256, Z1=256, split=sp, qkv=True)
+        bench('PV_kn_qkv', 256, 256, 256, Z1=256, b_kn=1, split=sp, ea=14, qkv=True)
         bench('big_4096', 4096, 4096, 4096, iters=5, split=sp)
