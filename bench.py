@@ -22,8 +22,9 @@ fp32 product as P 16-bit piece products, the dense bf16/fp16 MFMA peak / P
 bf16x3: P = 6, 416.7 TF).
 
 CPU baseline: the oracle (a torch-CPU restatement of the reference path,
-bit-equal to it at equal thread count) timed on this host's cores, rank 0 /
-N=1 only, on one denoising step of the same B=256 fold, extrapolated x50.
+bit-equal to it at equal thread count) timed on all usable host cores, rank 0 /
+N=1 only: one warm-up step and 3 timed denoising steps of the same B=256 fold,
+extrapolated x50.
 """
 import argparse
 import ctypes
@@ -94,24 +95,48 @@ def cpu_model_name():
     return platform.processor() or 'unknown'
 
 
-def cpu_baseline(sd, batch, n_steps):
-    """Oracle (reference op sequence on torch CPU): one DDIM step at `batch`, extrapolated."""
+def usable_cores():
+    """CPUs this process may run on: the affinity mask, capped by a cgroup v2 CPU quota if one is set."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open('/sys/fs/cgroup/cpu.max') as f:
+            quota, period = f.read().split()[:2]
+        if quota != 'max':
+            n = min(n, max(1, int(-(-int(quota) // int(period)))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_baseline(sd, batch, n_steps, timed_steps=3):
+    """Oracle (reference op sequence on torch CPU) per BASELINE.md §4: all usable host cores, one warm-up
+    step at the config's batch, then `timed_steps` denoising steps (forward + DDIM update) timed at that
+    batch; images/sec = batch / (t_step x n_steps) (the per-step cost does not depend on t)."""
     from oracle.unet import OracleUNet
     from oracle import diffusion as od
-    model = OracleUNet(sd, dim=128)
-    ac = od.alphas_cumprod(od.beta_schedule(1000, 'linear'))
-    g = torch.Generator().manual_seed(2022)
-    x_small = torch.randn((8, 3, 32, 32), generator=g)
-    with torch.no_grad():
-        od.ddim_denoise(ac, model(x_small, torch.full((8, ), 980)), x_small, 980, 960)  # warm-up
+    threads = usable_cores()
+    prev_threads = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        model = OracleUNet(sd, dim=128)
+        ac = od.alphas_cumprod(od.beta_schedule(1000, 'linear'))
+        seq = od.respaced_seq(1000, 'uniform', n_steps).tolist()
+        g = torch.Generator().manual_seed(2022)
         x = torch.randn((batch, 3, 32, 32), generator=g)
-        t0 = time.perf_counter()
-        out = model(x, torch.full((batch, ), 980))
-        od.ddim_denoise(ac, out, x, 980, 960)
-        dt = time.perf_counter() - t0
-    return dict(value=batch / (dt * n_steps), unit='images/sec', cores=torch.get_num_threads(), kind='port',
-                sample=f'1 of {n_steps} DDIM steps (UNet forward + update) at B={batch} on torch CPU '
-                       f'({cpu_model_name()}), extrapolated x{n_steps}; {dt:.2f} s measured')
+        pairs = list(zip(reversed(seq), reversed([-1] + seq[:-1])))
+        with torch.no_grad():
+            t, tp = pairs[0]
+            x = od.ddim_denoise(ac, model(x, torch.full((batch, ), t)), x, t, tp)['sample']  # warm-up
+            t0 = time.perf_counter()
+            for t, tp in pairs[1:1 + timed_steps]:
+                x = od.ddim_denoise(ac, model(x, torch.full((batch, ), t)), x, t, tp)['sample']
+            dt = (time.perf_counter() - t0) / timed_steps
+    finally:
+        torch.set_num_threads(prev_threads)
+    return dict(value=batch / (dt * n_steps), unit='images/sec', cores=threads, kind='port',
+                sample=f'{timed_steps} of {n_steps} DDIM steps (UNet forward + update) timed at B={batch} after '
+                       f'1 warm-up step, torch CPU on {threads} threads ({cpu_model_name()}, '
+                       f'{os.cpu_count()} logical CPUs on the host); {dt:.2f} s per step, extrapolated x{n_steps}')
 
 
 def roofline(prof):
@@ -247,14 +272,16 @@ def main():
             higher_is_better=True,
             scaling='weak',
             vs_baseline=None,
-            dtype='f32',
+            dtype=f'f32 via {dmhip.unet_conv_math(handle)} split MFMA',
             data='synthetic',
             config=dict(workload=f'DDIM-{args.respace_steps} (eta=0) sampling fold, CIFAR-10 UNet '
                                  f'(dim 128, mults 1-2-2-2, 35.7M params, synthetic weights), 3x32x32, '
                                  f'B={B} per GPU',
                         global_batch=world * B, parallelism=f'dp{world}', denoise_steps=args.respace_steps,
                         weights_gb=round(wbytes.value / 1e9, 3), workspace_gb=round(wsbytes.value / 1e9, 3),
-                        conv_math=dmhip.unet_conv_math(handle)),
+                        conv_math=dmhip.unet_conv_math(handle),
+                        # the reference draws randn_like every step even at eta=0 (ddim.py:76): so does the bench
+                        skip_unused_noise=diffuser.skip_unused_noise),
             roofline=roof,
             step_level=dict(model_tflops=round(total_flops / (total_gpu_ms * 1e-3) / 1e12, 2) if total_gpu_ms else None,
                             # observed forwards are 1 in PROFILE_EVERY: scale their kernel time to all forwards

@@ -64,6 +64,7 @@ struct DiTModel {
   bool range_check = !(std::getenv("DM_RANGE_CHECK") && std::string(std::getenv("DM_RANGE_CHECK")) == "0");
   int* range_flag = nullptr;
   int* range_flag_host = nullptr;
+  bool range_deferred = false;  // dm_dit_set_range_deferred / dm_dit_range_poll, as for the UNet
   std::map<const float*, int> w_exp;
 
   struct Plan : PlanBase {
@@ -395,7 +396,7 @@ extern "C" int dm_dit_forward(dm_dit* h, const float* x, const int64_t* t, const
   const int rc = pl.run(st);
   if (rc) return rc;
   DM_CHECK_HIP(hipMemcpyAsync(out, pl.out, no * sizeof(float), hipMemcpyDeviceToDevice, st));
-  if (m->math == 2 && m->range_check) {
+  if (m->math == 2 && m->range_check && !m->range_deferred) {
     DM_CHECK_HIP(hipMemcpyAsync(m->range_flag_host, m->range_flag, sizeof(int), hipMemcpyDeviceToHost, st));
     DM_CHECK_HIP(hipStreamSynchronize(st));
     if (*m->range_flag_host) {  // an fp16x2 GEMM met an operand beyond the fp16 range: fp32 from here on
@@ -403,6 +404,31 @@ extern "C" int dm_dit_forward(dm_dit* h, const float* x, const int64_t* t, const
       m->math = 0;
       m->plan.reset();
       return dm_dit_forward(h, x, t, y, B, out, stream);
+    }
+  }
+  return DM_OK;
+}
+
+extern "C" int dm_dit_set_range_deferred(dm_dit* h, int deferred) {
+  if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
+  h->m->range_deferred = deferred != 0;
+  return DM_OK;
+}
+
+extern "C" int dm_dit_range_poll(dm_dit* h, void* stream, int* flagged) {
+  if (!h || !h->m || !flagged) { dm::set_error("null model / argument"); return DM_ERR_STATE; }
+  dm::DiTModel* m = h->m;
+  *flagged = 0;
+  if (!m->range_flag) return DM_OK;
+  hipStream_t st = (hipStream_t)stream;
+  DM_CHECK_HIP(hipMemcpyAsync(m->range_flag_host, m->range_flag, sizeof(int), hipMemcpyDeviceToHost, st));
+  DM_CHECK_HIP(hipStreamSynchronize(st));
+  if (*m->range_flag_host) {
+    DM_CHECK_HIP(hipMemsetAsync(m->range_flag, 0, sizeof(int), st));
+    *flagged = 1;
+    if (m->math == 2) {
+      m->math = 0;
+      m->plan.reset();
     }
   }
   return DM_OK;

@@ -171,6 +171,9 @@ struct UNetModel {
   bool range_check = !(std::getenv("DM_RANGE_CHECK") && std::string(std::getenv("DM_RANGE_CHECK")) == "0");
   int* range_flag = nullptr;       // device
   int* range_flag_host = nullptr;  // pinned
+  // Deferred mode (dm_unet_set_range_deferred): forwards neither read the flag nor sync; the caller
+  // polls it once per sampling loop (dm_unet_range_poll) and re-runs the loop if it was raised.
+  bool range_deferred = false;
   std::map<std::pair<const float*, int>, void*> split_w;
   size_t split_bytes = 0;
   void split_for(ConvArgs& c);
@@ -1096,7 +1099,7 @@ extern "C" int dm_unet_forward(dm_unet* h, const float* x, const int64_t* t, con
   const int rc = pl.run(st);
   if (rc) return rc;
   DM_CHECK_HIP(hipMemcpyAsync(out, pl.out, no * sizeof(float), hipMemcpyDeviceToDevice, st));
-  if (m->conv_math == 2 && m->range_check) {
+  if (m->conv_math == 2 && m->range_check && !m->range_deferred) {
     // an fp16x2 conv met an activation beyond 65504: this model continues in bf16x3, from this call
     DM_CHECK_HIP(hipMemcpyAsync(m->range_flag_host, m->range_flag, sizeof(int), hipMemcpyDeviceToHost, st));
     DM_CHECK_HIP(hipStreamSynchronize(st));
@@ -1105,6 +1108,31 @@ extern "C" int dm_unet_forward(dm_unet* h, const float* x, const int64_t* t, con
       m->conv_math = 3;
       m->plan.reset();
       return dm_unet_forward(h, x, t, y, B, H, W, out, stream);
+    }
+  }
+  return DM_OK;
+}
+
+extern "C" int dm_unet_set_range_deferred(dm_unet* h, int deferred) {
+  if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
+  h->m->range_deferred = deferred != 0;
+  return DM_OK;
+}
+
+extern "C" int dm_unet_range_poll(dm_unet* h, void* stream, int* flagged) {
+  if (!h || !h->m || !flagged) { dm::set_error("null model / argument"); return DM_ERR_STATE; }
+  dm::UNetModel* m = h->m;
+  *flagged = 0;
+  if (!m->range_flag) return DM_OK;  // no fp16x2 plan was ever built
+  hipStream_t st = (hipStream_t)stream;
+  DM_CHECK_HIP(hipMemcpyAsync(m->range_flag_host, m->range_flag, sizeof(int), hipMemcpyDeviceToHost, st));
+  DM_CHECK_HIP(hipStreamSynchronize(st));
+  if (*m->range_flag_host) {
+    DM_CHECK_HIP(hipMemsetAsync(m->range_flag, 0, sizeof(int), st));
+    *flagged = 1;
+    if (m->conv_math == 2) {  // continue in bf16x3; the caller re-runs what it computed since the last poll
+      m->conv_math = 3;
+      m->plan.reset();
     }
   }
   return DM_OK;

@@ -84,9 +84,11 @@ class DDPM:
         # Parity runs install a CPU-generator source here.
         self.noise_fn: Optional[Callable[[Tensor], Tensor]] = None
         # The reference draws reverse_eps every step even when it is
-        # multiplied by zero (DDIM eta=0, t=0). Drawing it only matters for
-        # the RNG stream; set False to reproduce upstream RNG consumption.
-        self.skip_unused_noise = True
+        # multiplied by zero (DDIM eta=0, t=0; ddim.py:76, ddpm.py:251), which
+        # moves the RNG stream (later folds' init noise depends on it). The
+        # default does the same; True skips the unused draw (the output is
+        # unchanged, reverse_eps is then None).
+        self.skip_unused_noise = False
         self._coef_cache: Dict[Any, dict] = {}
 
     # ------------------------------------------------------------------ setup
@@ -263,10 +265,29 @@ class DDPM:
             self, model, init_noise: Tensor,
             tqdm_kwargs: Dict = None, model_kwargs: Dict = None,
     ):
-        sample = None
-        for out in self.sample_loop(model, init_noise, tqdm_kwargs, model_kwargs):
-            sample = out['sample']
-        return sample
+        def run():
+            sample = None
+            for out in self.sample_loop(model, init_noise, tqdm_kwargs, model_kwargs):
+                sample = out['sample']
+            return sample
+        return self._range_guarded(run, init_noise)
+
+    def _range_guarded(self, run: Callable[[], Tensor], init_noise: Tensor) -> Tensor:
+        """Run a whole sampling loop with the fp16x2 range check of the native models deferred to its
+        end: one host sync per loop instead of one per forward. If any forward met an activation
+        beyond the fp16 range, those models have switched to their exact fallback arithmetic and the
+        loop runs again from the same device RNG state, so the result is what the fallback gives.
+        A caller-installed noise source cannot be rewound: then every forward checks as it goes."""
+        if self.noise_fn is not None or not isinstance(init_noise, Tensor) or init_noise.device.type != 'cuda':
+            return run()
+        dev = init_noise.device
+        rng = torch.cuda.get_rng_state(dev)
+        with dmhip.deferred_range_check() as scope:
+            result = run()
+        if scope.flagged:
+            torch.cuda.set_rng_state(rng, dev)
+            result = run()
+        return result
 
 
 class _CFGMixin:
@@ -310,7 +331,8 @@ class _CFGMixin:
         for t, t_prev in zip(reversed(seq), reversed(seq_prev)):
             if batched:
                 t2 = torch.full((2 * B, ), t, device=img.device, dtype=torch.long)
-                both = model(torch.cat([img, img]), t2, **{self.cond_kwarg: y2})
+                with dmhip.null_label_scope():
+                    both = model(torch.cat([img, img]), t2, **{self.cond_kwarg: y2})
                 out_c, out_u = both[:B], both[B:]
             else:
                 t_batch = torch.full((B, ), t, device=img.device, dtype=torch.long)
@@ -327,10 +349,12 @@ class _CFGMixin:
             self, model, init_noise: Tensor, uncond_conditioning: Any = None,
             tqdm_kwargs: Dict = None, model_kwargs: Dict = None,
     ):
-        sample = None
-        for out in self.sample_loop(model, init_noise, uncond_conditioning, tqdm_kwargs, model_kwargs):
-            sample = out['sample']
-        return sample
+        def run():
+            sample = None
+            for out in self.sample_loop(model, init_noise, uncond_conditioning, tqdm_kwargs, model_kwargs):
+                sample = out['sample']
+            return sample
+        return self._range_guarded(run, init_noise)
 
     @contextmanager
     def hack_objective(self, objective: str):

@@ -32,4 +32,7 @@ from dmhip._lib import (  # noqa: F401
     timestep_embedding,
     unet_profile_enable,
     unet_profile_read,
+    null_label_scope,
+    null_labels_allowed,
+    deferred_range_check,
 )

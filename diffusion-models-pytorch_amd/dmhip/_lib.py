@@ -114,6 +114,67 @@ class GemmDesc(ctypes.Structure):
 
 _lib: Optional[ctypes.CDLL] = None
 
+# Batched classifier-free guidance marks the unconditional half of a 2B batch with label -1.
+# That convention is private to the CFG samplers: a public forward with a negative label raises
+# IndexError as nn.Embedding does upstream. The samplers open this scope around their 2B forward.
+_null_label_depth = 0
+
+
+class null_label_scope:
+    """Context manager: inside it, native denoisers accept y[b] = -1 as "no label" for row b."""
+
+    def __enter__(self):
+        global _null_label_depth
+        _null_label_depth += 1
+        return self
+
+    def __exit__(self, *exc):
+        global _null_label_depth
+        _null_label_depth -= 1
+        return False
+
+
+def null_labels_allowed() -> bool:
+    return _null_label_depth > 0
+
+
+class deferred_range_check:
+    """Context manager over one sampling loop: native forwards inside it do not sync on the fp16x2
+    range flag; on exit every model handle used inside is polled once (dm_*_range_poll) and
+    ``flagged`` tells whether any forward met an activation beyond the fp16 range (those models
+    have then switched to their exact fallback arithmetic and the loop must be re-run)."""
+    active = None
+
+    def __init__(self):
+        self.handles = {}
+        self.flagged = False
+        self._outer = None
+
+    def register(self, handle, abi: str, device):
+        key = int(handle.value if isinstance(handle, ctypes.c_void_p) else handle)
+        if key not in self.handles:
+            check(getattr(load(), abi + '_set_range_deferred')(handle, 1), abi + '_set_range_deferred')
+            self.handles[key] = (handle, abi, device)
+
+    def __enter__(self):
+        self._outer = deferred_range_check.active
+        deferred_range_check.active = self
+        return self
+
+    def __exit__(self, exc_type, *exc):
+        deferred_range_check.active = self._outer
+        L = load()
+        for handle, abi, device in self.handles.values():
+            flag = ctypes.c_int()
+            check(getattr(L, abi + '_set_range_deferred')(handle, 0), abi + '_set_range_deferred')
+            if exc_type is None:
+                check(getattr(L, abi + '_range_poll')(handle, stream_handle(device), ctypes.byref(flag)),
+                      abi + '_range_poll')
+                self.flagged |= bool(flag.value)
+        if self._outer is not None and self.flagged:
+            self._outer.flagged = True
+        return False
+
 
 def _declare(L: ctypes.CDLL):
     L.dm_abi_version.restype = ctypes.c_int
@@ -147,6 +208,10 @@ def _declare(L: ctypes.CDLL):
                                             ctypes.c_int, ctypes.c_int, vp, vp]
     L.dm_unet_set_conv_math.argtypes = [vp, ctypes.c_int]
     L.dm_unet_get_conv_math.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
+    L.dm_unet_set_range_deferred.argtypes = [vp, ctypes.c_int]
+    L.dm_unet_range_poll.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_int)]
+    L.dm_dit_set_range_deferred.argtypes = [vp, ctypes.c_int]
+    L.dm_dit_range_poll.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_int)]
     L.dm_dit_set_math.argtypes = [vp, ctypes.c_int]
     L.dm_dit_get_math.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
     L.dm_gemm.argtypes = [ctypes.POINTER(GemmDesc), vp]

@@ -8,17 +8,15 @@ it is instantiated lazily, only when ``decode_latent`` is called.
 """
 from typing import Any, Mapping
 
-import torch
-import torch.nn as nn
 from torch import Tensor
 
 from utils.misc import instantiate_from_config
+from ..base_latent import BaseLatent
 
 
-class DiT(nn.Module):
+class DiT(BaseLatent):
     def __init__(self, vae_config, vit_config, scale_factor: float = 0.18215):
-        super().__init__()
-        self.register_buffer('scale_factor', torch.tensor(scale_factor))
+        super().__init__(scale_factor=scale_factor)
         self.vae_config = vae_config
         self.vae = None
         self.vit = instantiate_from_config(vit_config)

@@ -6,7 +6,8 @@ mlp_ratio, class_dropout_prob, num_classes, learn_sigma), the DiT_models
 table, and the same state_dict names/shapes, including the timm~=0.9.12
 submodule names the reference builds on (``x_embedder.proj``,
 ``blocks.N.attn.qkv``, ``blocks.N.mlp.fc1`` ...), so DiT checkpoints load
-unchanged. ``forward(x, t, y=None)``: y None (or y[b] < 0) selects the null
+unchanged. ``forward(x, t, y=None)``: y None (or, inside the CFG samplers'
+``dmhip.null_label_scope()``, y[b] = -1) selects the null
 class ``num_classes`` (model.py:241-242); ``forward_with_cfg`` as upstream.
 
 The modules are parameter containers; the forward pass is one dm_dit_forward

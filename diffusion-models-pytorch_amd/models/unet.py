@@ -10,7 +10,8 @@ Drop-in for the reference models/unet.py:46-152:
 The torch modules below are parameter containers only. ``forward`` hands the
 parameters to the native executor (dm_unet_create packs them once into the
 library's own layout) and runs the whole network as one C-ABI call
-(dm_unet_forward): NHWC activations, fp32 MFMA implicit-GEMM convolutions,
+(dm_unet_forward): NHWC activations, implicit-GEMM convolutions on the matrix cores (fp16x2 split
+of the fp32 operands by default),
 fused GroupNorm+SiLU, zero-copy skip concatenation. Inference only
 (Dropout = identity, i.e. the reference in eval mode). No CPU fallback.
 """
@@ -190,19 +191,29 @@ class NativeDenoiser(nn.Module):
             self._check_labels(y)
             y_ptr = y.data_ptr()
         handle = self.native_handle(X.device)
+        scope = dmhip.deferred_range_check.active
+        if scope is not None:   # inside a sampler's sample(): the range flag is polled once per loop
+            scope.register(handle, self._abi, X.device)
         out = torch.empty((B, self.arch['out_channels'], H, W), device=X.device, dtype=torch.float32)
         self._launch(handle, X, T, y_ptr, out)
         return out
 
     def _check_labels(self, y: Tensor):
-        """nn.Embedding raises IndexError on an out-of-range label; so do we (negative = no label).
-        The check syncs once per distinct label tensor (labels are fixed across a sampling loop)."""
-        key = (y.data_ptr(), y._version, y.numel())
+        """nn.Embedding raises IndexError on an out-of-range label; so do we. y[b] = -1 ("no label"
+        for row b) is accepted only inside dmhip.null_label_scope(), which the CFG samplers open
+        around their batched 2B forward. The check syncs once per distinct label tensor (labels are
+        fixed across a sampling loop)."""
+        null_ok = dmhip.null_labels_allowed()
+        key = (y.data_ptr(), y._version, y.numel(), null_ok)
         if getattr(self, '_labels_ok', None) == key:
             return
         n = self.arch.get('label_rows', self.arch.get('num_classes', 0) or 0)
-        if y.numel() and int(y.max()) >= n:
-            raise IndexError(f'class label {int(y.max())} out of range for num_classes={n}')
+        if y.numel():
+            hi, lo = int(y.max()), int(y.min())
+            if hi >= n:
+                raise IndexError(f'class label {hi} out of range for num_classes={n}')
+            if lo < (-1 if null_ok else 0):
+                raise IndexError(f'class label {lo} out of range for num_classes={n}')
         self._labels_ok = key
 
 

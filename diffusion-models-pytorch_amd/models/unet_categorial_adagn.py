@@ -6,10 +6,12 @@ Drop-in for the reference models/unet_categorial_adagn.py:75-208:
     the same parameter names/shapes (``class_embed.weight``,
     ``down_blocks.0.0.adagn.proj.1.weight`` ...), so reference configs and
     checkpoints load unchanged;
-  * ``forward(X, T, y=None)``: y [B] int64 class labels or None. A negative
-    label marks a row as unconditional, which lets the classifier-free-guidance
-    sampler run both branches as one 2B batch (the reference runs two calls,
-    one with y and one with y=None; the per-row result is identical).
+  * ``forward(X, T, y=None)``: y [B] int64 class labels or None. Inside
+    ``dmhip.null_label_scope()`` (opened only by the CFG samplers) a label -1
+    marks a row as unconditional, which lets classifier-free guidance run both
+    branches as one 2B batch (the reference runs two calls, one with y and one
+    with y=None; the per-row result is identical). Outside it a negative label
+    raises IndexError, as nn.Embedding does upstream.
 
 Executor differences from models/unet.py (variant 1 of dm_unet_arch):
   * AdaGN (modules.py:105-123) before conv2: gn(h) * (1 + ys) + yb with
@@ -65,7 +67,7 @@ class ResBlockDownsample(ResBlock):
 class UNetCategorialAdaGN(NativeDenoiser):
     """UNet conditioned on categorial labels with AdaGN (unet_categorial_adagn.py:75-208)."""
 
-    supports_null_label = True  # y[b] < 0 = no label for row b (batched CFG)
+    supports_null_label = True  # y[b] = -1 = no label for row b (batched CFG, dmhip.null_label_scope)
 
     def __init__(
             self,

@@ -88,9 +88,11 @@ def slerp(t, z1, z2):
 
 
 def build_model(conf, weights, device):
+    from models.base_latent import BaseLatent
     model = instantiate_from_config(conf.model)
     if weights == 'synthetic':
-        init_synthetic_(model)
+        # a latent wrapper's checkpoint is its denoiser's (models/dit/dit.py load_state_dict -> vit)
+        init_synthetic_(model.vit if isinstance(model, BaseLatent) else model)
     else:
         model.load_state_dict(load_weights(weights))
     return model.to(device).eval()

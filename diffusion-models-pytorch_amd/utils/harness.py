@@ -26,14 +26,17 @@ class DistEnv:
         self.rank = int(os.environ.get('RANK', '0'))
         self.local_rank = int(os.environ.get('LOCAL_RANK', '0'))
         if torch.cuda.is_available():
-            self.device = torch.device('cuda', self.local_rank)
+            # one GPU per rank; more ranks than GPUs (a rehearsal of the N-GPU path) share them round-robin
+            self.device = torch.device('cuda', self.local_rank % torch.cuda.device_count())
             torch.cuda.set_device(self.device)
         else:
             self.device = torch.device('cpu')
+        # RCCL ("nccl") on GPUs; DM_DIST_BACKEND=gloo rehearses the multi-rank path over host memory
+        self.backend = backend or os.environ.get('DM_DIST_BACKEND') or (
+            'nccl' if self.device.type == 'cuda' else 'gloo')
         if self.world > 1 and not dist.is_initialized():
-            backend = backend or ('nccl' if self.device.type == 'cuda' else 'gloo')
-            kw = dict(device_id=self.device) if backend == 'nccl' else {}
-            dist.init_process_group(backend, **kw)
+            kw = dict(device_id=self.device) if self.backend == 'nccl' else {}
+            dist.init_process_group(self.backend, **kw)
 
     @property
     def is_main(self):
@@ -49,10 +52,13 @@ class DistEnv:
             return x
         x = x.contiguous()
         out = torch.empty((self.world * x.shape[0], *x.shape[1:]), dtype=x.dtype, device=x.device)
-        if x.device.type == 'cuda':
-            dist.all_gather_into_tensor(out, x)
+        if x.device.type == 'cuda' and self.backend == 'nccl':
+            dist.all_gather_into_tensor(out, x)   # one RCCL all-gather over xGMI
         else:
-            dist.all_gather(list(out.chunk(self.world)), x)
+            host = out.cpu() if out.device.type != 'cpu' else out
+            dist.all_gather(list(host.chunk(self.world)), x.cpu())
+            if host is not out:
+                out.copy_(host)
         return out
 
     def close(self):

@@ -87,8 +87,9 @@ int dm_unet_param_count(const dm_unet_arch* arch, int* n_params);
 int dm_unet_create(const dm_unet_arch* arch, const float* const* params, const int64_t* numels,
                    int n_params, void* stream, dm_unet** out);
 /* x: [B, in_channels, H, W] f32, t: [B] int64, out: [B, out_channels, H, W] f32.
- * y: [B] int64 class labels or NULL (variant 1; y[b] < 0 = no class for that row, which lets
- * the conditional and unconditional CFG branches run as one 2B batch).
+ * y: [B] int64 class labels or NULL (variants 1/2; y[b] = -1 = no class for that row, which lets
+ * the conditional and unconditional CFG branches run as one 2B batch; the Python layer accepts -1
+ * only from the CFG samplers and raises IndexError otherwise, as nn.Embedding does).
  * Workspace for batch B at H x W is allocated on first use and cached. */
 int dm_unet_forward(dm_unet* m, const float* x, const int64_t* t, const int64_t* y, int B, int H, int W,
                     float* out, void* stream);
@@ -117,6 +118,13 @@ int dm_unet_memory(const dm_unet* m, int64_t* weight_bytes, int64_t* workspace_b
  * device and run again in bf16x3, which the model then keeps; get reports the current kind. */
 int dm_unet_set_conv_math(dm_unet* m, int kind);
 int dm_unet_get_conv_math(const dm_unet* m, int* kind);
+/* Deferred range check: with deferred != 0 a forward does not read the fp16x2 range flag (no host
+ * sync per forward); the caller polls it once per sampling loop. dm_unet_range_poll synchronises
+ * `stream`, reports whether any forward since the last poll met an activation beyond the fp16 range,
+ * clears the flag and, if it was set, switches the model to bf16x3: the caller then re-runs what it
+ * computed since the last poll (diffusions.DDPM.sample re-runs the loop from the same RNG state). */
+int dm_unet_set_range_deferred(dm_unet* m, int deferred);
+int dm_unet_range_poll(dm_unet* m, void* stream, int* flagged);
 void dm_unet_destroy(dm_unet* m);
 
 /* Denoiser: DiT ------------------------------------------------------------
@@ -153,6 +161,9 @@ int dm_dit_forward(dm_dit* m, const float* x, const int64_t* t, const int64_t* y
  * the fp16 range is re-run in fp32, which the model then keeps. */
 int dm_dit_set_math(dm_dit* m, int kind);
 int dm_dit_get_math(const dm_dit* m, int* kind);
+/* As dm_unet_set_range_deferred / dm_unet_range_poll (a raised flag switches the DiT to fp32). */
+int dm_dit_set_range_deferred(dm_dit* m, int deferred);
+int dm_dit_range_poll(dm_dit* m, void* stream, int* flagged);
 /* 128-entry table exp(-ln(1e4) * i / 128) of the 256-wide frequency embedding (dit/model.py:51-54). */
 int dm_dit_set_time_freqs(dm_dit* m, const float* freqs, int n, void* stream);
 int dm_dit_profile(dm_dit* m, int enable);

@@ -26,6 +26,16 @@ def load_golden(name):
     return arrays, meta
 
 
+TOL = 1e-4   # BASELINE.json north_star: fp32 max-abs vs the reference
+
+
+def drift_bound(drift):
+    """Per-step bound of a free-running trajectory: the 1e-4 budget, or 1.5x the reference's own
+    float32-vs-float64 drift on the same trajectory (tests/golden/drift.npz, ddpm1000.npz, ddpmcfg.npz,
+    made by make_golden_r2.py) where that drift alone already approaches the budget."""
+    return max(TOL, 1.5 * float(drift))
+
+
 @pytest.fixture(scope='session')
 def golden():
     cache = {}

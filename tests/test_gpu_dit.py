@@ -56,9 +56,17 @@ def test_dit_forward_vs_oracle(cuda, golden, report, name):
     report(f'dit_forward_{name}_y_maxabs_vs_oracle', e_y)
     report(f'dit_forward_{name}_null_maxabs_vs_oracle', e_n)
     assert e_y <= TOL and e_n <= TOL, (e_y, e_n)
-    # y[b] < 0 selects the null class row, the same as y=None
-    neg = model(x, t, torch.full_like(y, -1)).cpu()
+    # inside the CFG samplers' null-label scope y[b] = -1 selects the null class row, the same as
+    # y=None; outside it a negative label is an IndexError (nn.Embedding upstream)
+    import dmhip
+    with dmhip.null_label_scope():
+        neg = model(x, t, torch.full_like(y, -1)).cpu()
     assert torch.equal(neg, out_n)
+    with pytest.raises(IndexError):
+        model(x, t, torch.full_like(y, -1))
+    # the null class index itself is a valid label (model.py:241-242)
+    nul = model(x, t, torch.full_like(y, meta['archs'][name]['num_classes'])).cpu()
+    assert torch.equal(nul, out_n)
     del model
     torch.cuda.empty_cache()
 
@@ -91,7 +99,8 @@ def test_dit_forward_with_cfg(cuda, golden):
     gen = torch.Generator().manual_seed(5)
     x = torch.randn((4, 4, 8, 8), generator=gen).to(cuda)
     t = torch.full((4, ), 500, dtype=torch.long, device=cuda)
-    y = torch.tensor([1, 2, -1, -1], device=cuda)
+    nc = meta['archs']['dit_tiny']['num_classes']
+    y = torch.tensor([1, 2, nc, nc], device=cuda)   # null class for the second half, as reference callers pass it
     out = model.forward_with_cfg(x, t, y, 1.5)
     full = model(torch.cat([x[:2], x[:2]]), t, y)
     ce, ue = full[:2, :3], full[2:, :3]

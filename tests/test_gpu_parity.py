@@ -135,6 +135,58 @@ def test_ddim50_cifar_trajectory(cuda, golden, report):
     report('ddim50_cifar_B2_worst_step_maxabs_vs_reference', worst)
 
 
+@pytest.mark.parametrize('math', ['fp16x2', 'bf16x3', 'fp32'])
+def test_ddim50_cifar_all_steps(cuda, golden, report, math):
+    """All 50 steps of the C3 trajectory (DDIM-50, CIFAR-10 UNet, B=2; tests/golden/drift.npz) under each
+    conv arithmetic, side by side: sample and pred_eps <= 1e-4 at every step. The report also records
+    the reference's own fp32-vs-fp64 drift on the same trajectory for scale."""
+    import dmhip
+    d_arr, d_meta = golden('drift')
+    model, sha = _model(golden('forward')[1], 'cifar10', cuda)
+    assert sha == d_meta['cifar10_weights_sha256']
+    dmhip.unet_conv_math(model.native_handle(torch.device(cuda)), math)
+    d = DDIM(respace_type='uniform', respace_steps=50, eta=0.0, device=cuda)
+    worst = {'sample': 0.0, 'pred_eps': 0.0}
+    for i, out in enumerate(d.sample_loop(model, torch.from_numpy(d_arr['ddim50_init']).to(cuda),
+                                          tqdm_kwargs=dict(disable=True))):
+        for k in worst:
+            err = float(np.abs(out[k].cpu().numpy() - d_arr[f'ddim50_{k}'][i]).max())
+            worst[k] = max(worst[k], err)
+            assert err <= TOL, (math, i, k, err)
+    assert i == 49
+    report(f'ddim50_cifar_B2_all_steps_{math}_sample_maxabs_vs_reference', worst['sample'])
+    report(f'ddim50_cifar_B2_all_steps_{math}_pred_eps_maxabs_vs_reference', worst['pred_eps'])
+    report('ddim50_cifar_B2_reference_fp32_vs_fp64_drift', float(d_arr['ddim50_drift_sample'].max()))
+
+
+def test_ddpm1000_cifar_trajectory(cuda, golden, report):
+    """BASELINE config C2's path: the CIFAR-10 UNet through DDPM fixed_large, all 1000 steps (reference
+    diffusions/ddpm.py:205-281), B=2, free-running from the reference's init noise with the per-step noise
+    pinned (tests/golden/noise.py StepNoise, the same draws the reference consumed when
+    make_golden_r2.py ran it). 31 steps from t = 999 to t = 0 are checked: sample and pred_eps
+    <= max(1e-4, 1.5 x the reference's fp32-vs-fp64 drift at that step)."""
+    from tests.conftest import drift_bound
+    from tests.golden.noise import StepNoise
+    g, meta = golden('ddpm1000')
+    model, sha = _model(golden('forward')[1], 'cifar10', cuda)
+    assert sha == meta['cifar10_weights_sha256']
+    d = DDPM(var_type='fixed_large', device=cuda)
+    src = StepNoise(meta['noise_seed'])
+    d.noise_fn = src
+    keep = set(meta['keep'])
+    worst = 0.0
+    for i, out in enumerate(d.sample_loop(model, torch.from_numpy(g['init']).to(cuda),
+                                          tqdm_kwargs=dict(disable=True))):
+        if i in keep:
+            for k in ('sample', 'pred_eps'):
+                err = float(np.abs(out[k].cpu().numpy() - g[f'step{i}_{k}']).max())
+                worst = max(worst, err)
+                assert err <= drift_bound(g[f'drift_{k}'][i]), (i, k, err)
+    assert i == 999 and src.k == 1000
+    report('ddpm1000_cifar_B2_worst_kept_step_maxabs_vs_reference', worst)
+    report('ddpm1000_cifar_B2_reference_fp32_vs_fp64_drift', float(g['drift_sample'].max()))
+
+
 def test_ddpm10_mnist_trajectory(cuda, golden, report):
     """BASELINE config C1 (MNIST UNet, DDPM T=200 fixed_small, 10 steps) with the reference's CPU noise."""
     arrays, meta = golden('trajectory')
@@ -229,3 +281,45 @@ def test_fp16x2_range_fallback(cuda, golden):
         assert dmhip.unet_conv_math(h) == 'bf16x3'
     assert torch.isfinite(outs['bf16x3']).all()
     assert torch.equal(outs['fp16x2'], outs['bf16x3'])
+
+
+def test_fp16x2_range_fallback_deferred(cuda, golden):
+    """Inside DDPM.sample the range flag is polled once per loop (no per-forward host sync): a loop
+    whose forwards leave the fp16 range is re-run from the same RNG state in bf16x3, so sample()
+    returns exactly what a model forced to bf16x3 gives (eta > 0: the re-run must replay the noise)."""
+    import dmhip
+    _, meta = golden('forward')
+    outs = {}
+    for math in ('fp16x2', 'bf16x3'):
+        model, _ = _model(meta, 'tiny', cuda)
+        with torch.no_grad():
+            model.state_dict(keep_vars=True)['first_conv.weight'].mul_(1e5)
+        h = model.native_handle(torch.device(cuda))
+        dmhip.unet_conv_math(h, math)
+        d = DDIM(respace_type='uniform', respace_steps=4, eta=0.7, device=cuda)
+        torch.manual_seed(9)
+        init = torch.randn((2, 3, 16, 16), device=cuda)
+        outs[math] = d.sample(model, init, tqdm_kwargs=dict(disable=True)).cpu()
+        assert dmhip.unet_conv_math(model.native_handle(torch.device(cuda))) == 'bf16x3'
+    assert torch.isfinite(outs['bf16x3']).all()
+    assert torch.equal(outs['fp16x2'], outs['bf16x3'])
+
+
+def test_public_forward_rejects_negative_labels(cuda, golden):
+    """nn.Embedding raises IndexError on a negative label upstream; the engine accepts -1 ("no label")
+    only inside dmhip.null_label_scope(), which the CFG samplers open for their batched 2B forward."""
+    import dmhip
+    from models.unet_categorial_adagn import UNetCategorialAdaGN
+    _, meta = golden('adagn')
+    m = UNetCategorialAdaGN(**meta['archs']['tiny_updown']).eval()
+    init_synthetic_(m)
+    m = m.to(cuda)
+    x = torch.zeros((2, 3, 16, 16), device=cuda)
+    t = torch.tensor([5, 6], device=cuda)
+    with pytest.raises(IndexError):
+        m(x, t, torch.tensor([-1, 0], device=cuda))
+    with pytest.raises(IndexError):
+        m(x, t, torch.tensor([0, meta['archs']['tiny_updown']['num_classes']], device=cuda))
+    with dmhip.null_label_scope():
+        a = m(x, t, torch.tensor([-1, -1], device=cuda))
+    assert torch.equal(a, m(x, t, None))

@@ -1,0 +1,225 @@
+"""The sampling scripts end to end on the engine, checked pixel by pixel.
+
+* scripts/sample_uncond.py (reference scripts/sample_uncond.py:179-195) and
+  scripts/sample_cfg.py (reference scripts/sample_cfg.py:157-182) write PNGs;
+  the expected images come from the CPU oracle (oracle/, pinned to the
+  reference by tests/golden) on the same init noise, which the test recovers
+  by replaying the device RNG exactly as the script consumed it: the init
+  draw of every fold, then one randn_like per denoising step (the reference
+  draws it even at eta = 0, ddim.py:76). PNG quantisation (x * 255 + 0.5,
+  truncated) turns the 1e-4 budget into at most one level.
+* The world-size-2 runs launch 2 ranks on the one GPU (gloo process group,
+  DM_DIST_BACKEND=gloo) with the real engine: the gathered images are the two
+  single-process runs seeded 2022 and 2023, byte for byte (seed + rank,
+  gather in rank order; sample_cfg keeps rank 0's fold, the reference quirk
+  at sample_cfg.py:171,177).
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from utils.png import read_png_rgb
+from utils.synthetic import init_synthetic_
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, 'diffusion-models-pytorch_amd')
+CONFIGS = os.path.join(PKG, 'configs')
+# a reduced class-conditional AdaGN network on the CFG-CIFAR config (dotlist overrides, as the reference CLI takes)
+TINY_ADAGN = ['--model.params.dim', '32', '--model.params.dim_mults', '[1,2]', '--model.params.use_attn',
+              '[false,true]', '--model.params.num_res_blocks', '1', '--model.params.attn_head_dims', '32']
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _quantize(x: torch.Tensor) -> np.ndarray:
+    """torchvision save_image of one image in [-1, 1] (utils/png.py to_uint8)."""
+    x = (x.clamp(-1, 1) + 1) / 2
+    if x.shape[0] == 1:
+        x = x.expand(3, -1, -1)
+    return x.mul(255).add_(0.5).clamp_(0, 255).permute(1, 2, 0).to(torch.uint8).numpy()
+
+
+def _compare_png(path, expect: torch.Tensor):
+    got = read_png_rgb(str(path)).astype(np.int16)
+    want = _quantize(expect).astype(np.int16)
+    assert got.shape == want.shape, (path, got.shape, want.shape)
+    diff = np.abs(got - want)
+    assert diff.max() <= 1, (path, int(diff.max()))
+    assert (diff > 0).mean() < 0.01, (path, float((diff > 0).mean()))
+
+
+def _conf(path, overrides=()):
+    from utils.misc import load_config
+    ov = [(a[2:] if a.startswith('--') else a) for a in overrides]
+    return load_config(path, [f'{k}={v}' for k, v in zip(ov[::2], ov[1::2])])
+
+
+def test_sample_uncond_pixels_vs_oracle(cuda, tmp_path):
+    """sample mode, DDIM-3 on the CIFAR-10 config, 3 images in folds of 2 and 1 (bspp = 2): every PNG
+    equals the oracle's image from the replayed init noise within one quantisation level."""
+    from oracle import diffusion as od
+    from oracle.unet import OracleUNet
+    from scripts import sample_uncond
+    from models.unet import UNet
+    cfg = os.path.join(CONFIGS, 'ddpm_cifar10.yaml')
+    sample_uncond.main(['-c', cfg, '--weights', 'synthetic', '--n_samples', '3', '--batch_size', '2',
+                        '--save_dir', str(tmp_path), '--sampler', 'ddim', '--respace_steps', '3'])
+    assert sorted(os.listdir(tmp_path)) == ['0.png', '1.png', '2.png']
+    conf = _conf(cfg)
+    m = UNet(**conf.model.params)
+    init_synthetic_(m)
+    oracle = OracleUNet(m.state_dict(), **conf.model.params)
+    ac = od.alphas_cumprod(od.beta_schedule(1000, conf.diffusion.params.beta_schedule))
+    seq = od.respaced_seq(1000, 'uniform', 3)
+    torch.manual_seed(2022)
+    idx = 0
+    for bs in (2, 1):   # amortize(3, 2) = [2, 1]; every fold draws bspp = 2 images (sample_uncond.py:185)
+        init = torch.randn((2, 3, 32, 32), device=cuda)
+        for _ in range(len(seq)):
+            torch.randn((2, 3, 32, 32), device=cuda)   # the per-step reverse_eps draws
+        *_, last = od.sample_loop(oracle, ac, seq, init.cpu(), sampler='ddim')
+        for x in last['sample'][:bs]:
+            _compare_png(tmp_path / f'{idx}.png', x)
+            idx += 1
+    assert idx == 3
+
+
+@pytest.mark.parametrize('shard', [False, True])
+def test_sample_cfg_pixels_vs_oracle(cuda, tmp_path, shard):
+    """scripts/sample_cfg.py (reference sample_cfg.py:157-182): classes 1 and 4, 3 images each in folds of
+    2 and 1. Reference mode draws `bs` images per fold (:171; the 1-image fold draws 1), --shard draws
+    bspp (2) and keeps the first bs; DDIMCFG s = 3 with the batched 2B forward. PNGs vs the oracle's CFG
+    loop on the replayed noise, per class directory."""
+    from oracle import diffusion as od
+    from oracle.unet import OracleUNetCategorialAdaGN
+    from scripts import sample_cfg
+    from models.unet_categorial_adagn import UNetCategorialAdaGN
+    cfg = os.path.join(CONFIGS, 'ddpm_cfg_cifar10.yaml')
+    args = ['-c', cfg, '--weights', 'synthetic', '--guidance_scale', '3', '--class_ids', '1', '4',
+            '--n_samples_each_class', '3', '--batch_size', '2', '--save_dir', str(tmp_path), '--sampler', 'ddim',
+            '--respace_steps', '3'] + (['--shard'] if shard else []) + TINY_ADAGN
+    sample_cfg.main(args)
+    conf = _conf(cfg, TINY_ADAGN)
+    m = UNetCategorialAdaGN(**conf.model.params)
+    init_synthetic_(m)
+    oracle = OracleUNetCategorialAdaGN(m.state_dict(), **conf.model.params)
+    ac = od.alphas_cumprod(od.beta_schedule(1000, conf.diffusion.params.beta_schedule))
+    seq = od.respaced_seq(1000, 'uniform', 3)
+    torch.manual_seed(2022)
+    for c in (1, 4):
+        assert sorted(os.listdir(tmp_path / f'class{c}')) == ['0.png', '1.png', '2.png']
+        idx = 0
+        for bs in (2, 1):
+            n = 2 if shard else bs
+            init = torch.randn((n, 3, 32, 32), device=cuda)
+            for _ in range(len(seq)):
+                torch.randn((n, 3, 32, 32), device=cuda)
+            *_, last = od.sample_loop(oracle, ac, seq, init.cpu(), sampler='ddim', guidance_scale=3.0,
+                                      y=torch.full((n, ), c, dtype=torch.long))
+            for x in last['sample'][:bs]:
+                _compare_png(tmp_path / f'class{c}' / f'{idx}.png', x)
+                idx += 1
+
+
+def _launch_world2(script, args, tmp_path):
+    env = dict(os.environ, DM_DIST_BACKEND='gloo', MASTER_ADDR='127.0.0.1', HSA_ENABLE_IPC_MODE_LEGACY='0')
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
+           '--master-addr', '127.0.0.1', '--master-port', str(_free_port()), os.path.join(PKG, 'scripts', script)]
+    r = subprocess.run(cmd + args, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+
+
+def _bytes(path):
+    with open(path, 'rb') as f:
+        return f.read()
+
+
+def test_sample_uncond_world2_equals_single_rank_runs(cuda, tmp_path):
+    """2 ranks, 4 images, batch 2: bspp = 2, one fold of 4 = rank 0's 2 images (seed 2022) then rank 1's
+    (seed 2023), gathered in rank order (sample_uncond.py:179-195); bit-equal PNGs to single-process runs."""
+    from scripts import sample_uncond
+    cfg = os.path.join(CONFIGS, 'ddpm_cifar10.yaml')
+    common = ['-c', cfg, '--weights', 'synthetic', '--batch_size', '2', '--sampler', 'ddim', '--respace_steps', '4']
+    _launch_world2('sample_uncond.py', common + ['--n_samples', '4', '--save_dir', str(tmp_path / 'w2')], tmp_path)
+    for seed in (2022, 2023):
+        sample_uncond.main(common + ['--n_samples', '2', '--seed', str(seed), '--save_dir', str(tmp_path / f's{seed}')])
+    assert sorted(os.listdir(tmp_path / 'w2')) == ['0.png', '1.png', '2.png', '3.png']
+    for k in range(4):
+        single = tmp_path / f's{2022 + k // 2}' / f'{k % 2}.png'
+        assert _bytes(tmp_path / 'w2' / f'{k}.png') == _bytes(single), k
+    assert _bytes(tmp_path / 'w2' / '0.png') != _bytes(tmp_path / 'w2' / '2.png')
+
+
+def test_sample_cfg_world2_keeps_rank0_fold(cuda, tmp_path):
+    """Reference sample_cfg semantics at world size 2 (sample_cfg.py:159,169-177): batch 2 gives bspp = 2 and
+    one fold of 3 (amortize(3, 2 x 2)); every rank draws the whole fold (bs = 3 images, :171) from seed +
+    rank and gather(...)[:bs] keeps rank 0's. That is the single-process run with batch 3 (one fold of
+    3, seed 2022), byte for byte."""
+    from scripts import sample_cfg
+    cfg = os.path.join(CONFIGS, 'ddpm_cfg_cifar10.yaml')
+    common = ['-c', cfg, '--weights', 'synthetic', '--guidance_scale', '2', '--class_ids', '3',
+              '--n_samples_each_class', '3', '--sampler', 'ddim', '--respace_steps', '3'] + TINY_ADAGN
+    _launch_world2('sample_cfg.py', common + ['--batch_size', '2', '--save_dir', str(tmp_path / 'w2')], tmp_path)
+    sample_cfg.main(common + ['--batch_size', '3', '--save_dir', str(tmp_path / 's')])
+    files = sorted(os.listdir(tmp_path / 's' / 'class3'))
+    assert files == ['0.png', '1.png', '2.png'] == sorted(os.listdir(tmp_path / 'w2' / 'class3'))
+    for f in files:
+        assert _bytes(tmp_path / 'w2' / 'class3' / f) == _bytes(tmp_path / 's' / 'class3' / f), f
+
+
+# a reduced DiT on the DiT-XL/2 config (latent 4 x 8 x 8 from img_size 64, 2 blocks of width 64)
+TINY_DIT = ['--data.params.img_size', '64', '--data.num_classes', '10',
+            '--model.params.vit_config.params.input_size', '8', '--model.params.vit_config.params.hidden_size', '64',
+            '--model.params.vit_config.params.depth', '2', '--model.params.vit_config.params.num_heads', '4',
+            '--model.params.vit_config.params.num_classes', '10']
+
+
+def test_sample_cfg_latent_dit_vs_oracle(cuda, tmp_path):
+    """BASELINE config C5's driver: scripts/sample_cfg.py on the DiT config (configs/dit_xl2_256.yaml, reduced
+    by overrides). Latent noise (4, img/8, img/8) (Streamlit page 2 :91-95), the YAML's clip_denoised false
+    and learned sigma honoured, DDIMCFG s = 4 with cond + null-class rows as one 2B forward, seed + rank
+    sharding (bspp per rank). The written latents equal the oracle's DDIMCFG loop (oracle/dit.py: parity
+    unpinned, timm absent) on the replayed noise within 1e-4; the VAE is a network download, so the
+    script keeps latents (.npy)."""
+    from oracle import diffusion as od
+    from oracle.dit import OracleDiT
+    from scripts import sample_cfg
+    from models.dit.model import DiT
+    cfg = os.path.join(CONFIGS, 'dit_xl2_256.yaml')
+    sample_cfg.main(['-c', cfg, '--weights', 'synthetic', '--guidance_scale', '4', '--class_ids', '7',
+                     '--n_samples_each_class', '3', '--batch_size', '2', '--save_dir', str(tmp_path),
+                     '--sampler', 'ddim', '--respace_steps', '5'] + TINY_DIT)
+    assert sorted(os.listdir(tmp_path / 'class7')) == ['0.npy', '1.npy', '2.npy']
+    conf = _conf(cfg, TINY_DIT)
+    vit = DiT(**conf.model.params.vit_config.params)
+    init_synthetic_(vit)
+    oracle = OracleDiT(vit.state_dict(), out_channels=vit.out_channels, **conf.model.params.vit_config.params)
+    ac = od.alphas_cumprod(od.beta_schedule(1000, 'linear'))
+    seq = od.respaced_seq(1000, 'uniform', 5)
+    torch.manual_seed(2022)
+    idx = 0
+    worst = 0.0
+    for bs in (2, 1):
+        init = torch.randn((2, 4, 8, 8), device=cuda)
+        for _ in range(len(seq)):
+            torch.randn((2, 4, 8, 8), device=cuda)
+        *_, last = od.sample_loop(oracle, ac, seq, init.cpu(), sampler='ddim', guidance_scale=4.0, clip=False,
+                                  y=torch.full((2, ), 7, dtype=torch.long))
+        for z in last['sample'][:bs]:
+            got = np.load(tmp_path / 'class7' / f'{idx}.npy', allow_pickle=False)
+            worst = max(worst, float(np.abs(got - z.numpy()).max()))
+            idx += 1
+    assert worst <= 1e-4, worst
+    # clip_denoised false is honoured: unclamped latents leave [-1, 1]
+    assert max(abs(np.load(tmp_path / 'class7' / f'{k}.npy')).max() for k in range(3)) > 1.0
