@@ -56,8 +56,10 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=3, help='timed folds')
     ap.add_argument('--warmup', type=int, default=1, help='untimed folds')
-    ap.add_argument('--batch', type=int, default=256, help='images per GPU per fold')
-    ap.add_argument('--respace-steps', type=int, default=50)
+    ap.add_argument('--workload', default='c3', choices=sorted(WORKLOADS),
+                    help='; '.join(f'{k}: {v}' for k, v in sorted(WORKLOADS.items())))
+    ap.add_argument('--batch', type=int, default=None, help='images per GPU per fold (default: the workload\'s)')
+    ap.add_argument('--respace-steps', type=int, default=None, help='denoising steps (default: the workload\'s)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-batch', type=int, default=256, help='batch of the timed CPU denoising step')
     ap.add_argument('--profile-json', default=None, help='write the per-op profile here (rank 0)')
@@ -156,6 +158,8 @@ def roofline(prof):
         achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12
         split = dom_name.startswith('conv_patch3_kernel')
         np_ = int(dom_name.rstrip('>').split(',')[-1]) if split else 0
+        if dom_name.startswith('gemm_kernel') and dom_name.endswith(',true>'):   # <..., B_KN, SPLIT>: fp16x2
+            split, np_ = True, 2
         prods = SPLIT_PRODUCTS.get(np_, 0)
         peak = round(BF16_PEAK_TFLOPS / prods, 1) if split else FP32_PEAK_TFLOPS
         roof = dict(bound='mfma', achieved=round(achieved, 2), peak=peak, unit='TFLOP/s',
@@ -179,6 +183,103 @@ def roofline(prof):
     return roof, total_gpu_ms, total_flops, fam
 
 
+WORKLOADS = {
+    'c3': 'DDIM-50 CIFAR-10 UNet, B=256 per GPU (BASELINE configs[2]; the headline metric)',
+    'c2': 'DDPM-1000 fixed_large CIFAR-10 UNet, B=256 (BASELINE configs[1])',
+    'c4': 'ADM guided-diffusion 256x256 UNetCombined, DDIMCFG-100 s=3, B=64 (BASELINE configs[3])',
+    'c5': 'DiT-XL/2 latent 4x32x32, DDIMCFG-250 s=3, clip_denoised false, B=32 per GPU (BASELINE configs[4])',
+}
+
+
+def build_workload(name, args, dev, rank):
+    """-> dict(metric, fold(), handles [(handle, abi, forwards per fold)], images, workload, config, sd_cpu).
+    Every workload is one sampling fold of the reference harness on device-resident synthetic inputs."""
+    from diffusions import DDIM, DDIMCFG, DDPM
+    from utils.misc import instantiate_from_config, load_config
+    from utils.synthetic import init_synthetic_
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(2022 + rank)
+    cfgdir = os.path.join(PKG, 'configs')
+    if name in ('c2', 'c3'):
+        from models.unet import UNet
+        model = UNet().eval()
+        init_synthetic_(model)
+        sd_cpu = {k: v.clone() for k, v in model.state_dict().items()}
+        model = model.to(dev)
+        B = args.batch or 256
+        steps = args.respace_steps or (50 if name == 'c3' else 1000)
+        if name == 'c3':
+            diffuser = DDIM(respace_type='uniform', respace_steps=steps, eta=0.0, device=dev)
+            label = f'DDIM-{steps} (eta=0)'
+            metric = METRIC
+        else:
+            diffuser = DDPM(var_type='fixed_large', respace_type=None if steps == 1000 else 'uniform',
+                            respace_steps=steps, device=dev)
+            label = f'DDPM-{steps} fixed_large'
+            metric = f'images/sec at DDPM-{steps}, CIFAR-10 UNet 32x32, bs={B}'
+        shape = (B, 3, 32, 32)
+
+        def fold():
+            return diffuser.sample(model, torch.randn(shape, device=dev, generator=gen),
+                                   tqdm_kwargs=dict(disable=True)).clamp(-1, 1)
+        model(torch.zeros(shape, device=dev), torch.zeros((B, ), dtype=torch.long, device=dev))  # plan
+        return dict(metric=metric, fold=fold, images=B, shape=shape, diffuser=diffuser, sd_cpu=sd_cpu,
+                    handles=[(model.native_handle(dev), 'dm_unet', len(diffuser.respaced_seq))],
+                    workload=f'{label} sampling fold, CIFAR-10 UNet (dim 128, mults 1-2-2-2, 35.7M params, '
+                             f'synthetic weights), 3x32x32, B={B} per GPU', denoise_steps=steps)
+    if name == 'c4':
+        conf = load_config(os.path.join(cfgdir, 'adm256_combined.yaml'))
+        model = instantiate_from_config(conf.model).eval()
+        init_synthetic_(model)
+        model = model.to(dev)
+        B = args.batch or 64
+        steps = args.respace_steps or 100
+        diffuser = DDIMCFG(guidance_scale=3.0, respace_type='uniform', respace_steps=steps, eta=0.0, device=dev)
+        shape = (B, 3, 256, 256)
+        y = torch.zeros((B, ), dtype=torch.long, device=dev)
+
+        def fold():
+            return diffuser.sample(model, torch.randn(shape, device=dev, generator=gen), model_kwargs=dict(y=y),
+                                   tqdm_kwargs=dict(disable=True)).clamp(-1, 1)
+        t0 = torch.zeros((B, ), dtype=torch.long, device=dev)
+        model(torch.zeros(shape, device=dev), t0, y)
+        model(torch.zeros(shape, device=dev), t0, None)
+        return dict(metric=f'images/sec at ADM-256 UNetCombined DDIMCFG-{steps} (s=3), bs={B}', fold=fold, images=B,
+                    shape=shape, diffuser=diffuser, sd_cpu=None,
+                    handles=[(model.unet_cond.native_handle(dev), 'dm_unet', len(diffuser.respaced_seq)),
+                             (model.unet_uncond.native_handle(dev), 'dm_unet', len(diffuser.respaced_seq))],
+                    workload=f'DDIMCFG-{steps} (s=3, eta=0) sampling fold, guided-diffusion 256x256 UNetCombined '
+                             f'(2 x 552.8M params, synthetic weights; cond + uncond forwards per step), 3x256x256, '
+                             f'B={B} per GPU', denoise_steps=steps)
+    if name == 'c5':
+        conf = load_config(os.path.join(cfgdir, 'dit_xl2_256.yaml'))
+        model = instantiate_from_config(conf.model).eval()
+        init_synthetic_(model.vit)
+        model = model.to(dev)
+        B = args.batch or 32
+        steps = args.respace_steps or 250
+        dp = conf.diffusion.params
+        diffuser = DDIMCFG(guidance_scale=3.0, respace_type='uniform', respace_steps=steps, eta=0.0,
+                           clip_denoised=dp.clip_denoised, device=dev)
+        shape = (B, 4, 32, 32)   # latent 4 x img/8 x img/8 (streamlit page 2 :91-95)
+        y = torch.zeros((B, ), dtype=torch.long, device=dev)
+
+        def fold():
+            return diffuser.sample(model, torch.randn(shape, device=dev, generator=gen), model_kwargs=dict(y=y),
+                                   tqdm_kwargs=dict(disable=True))
+        import dmhip
+        with dmhip.null_label_scope():   # the 2B batched CFG forward's plan
+            model(torch.zeros((2 * B, 4, 32, 32), device=dev), torch.zeros((2 * B, ), dtype=torch.long, device=dev),
+                  torch.cat([y, torch.full_like(y, -1)]))
+        return dict(metric=f'images/sec at DiT-XL/2 DDIMCFG-{steps} (s=3), latent 4x32x32, bs={B}', fold=fold,
+                    images=B, shape=shape, diffuser=diffuser, sd_cpu=None,
+                    handles=[(model.vit.native_handle(dev), 'dm_dit', len(diffuser.respaced_seq))],
+                    workload=f'DDIMCFG-{steps} (s=3, eta=0, clip_denoised false) sampling fold, DiT-XL/2 (675M '
+                             f'params, synthetic weights; cond + null-class rows as one 2B forward), latent 4x32x32, '
+                             f'B={B} per GPU', denoise_steps=steps)
+    raise ValueError(f'unknown workload {name}')
+
+
 def main():
     args = parse()
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -198,29 +299,19 @@ def main():
 
     import dmhip
     from dmhip._lib import check as _check
-    from diffusions import DDIM
-    from models.unet import UNet
-    from utils.synthetic import init_synthetic_
 
     dmhip.load()
-    model = UNet().eval()
-    init_synthetic_(model)
-    sd_cpu = {k: v.clone() for k, v in model.state_dict().items()}
-    model = model.to(dev)
-    diffuser = DDIM(respace_type='uniform', respace_steps=args.respace_steps, eta=0.0, device=dev)
-    B = args.batch
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(2022 + rank)
-    gathered = torch.empty((world * B, 3, 32, 32), device=dev) if world > 1 else None
+    wl = build_workload(args.workload, args, dev, rank)
+    B, shape = wl['images'], wl['shape']
+    gathered = torch.empty((world * B, *shape[1:]), device=dev) if world > 1 else None
 
     def fold():
-        noise = torch.randn((B, 3, 32, 32), device=dev, generator=gen)
-        x = diffuser.sample(model, noise, tqdm_kwargs=dict(disable=True)).clamp(-1, 1)
-        if world > 1:
+        x = wl['fold']()
+        if world > 1:   # the reference's accelerator.gather of the fold (sample_uncond.py:190): one all-gather
             if backend == 'nccl':
                 dist.all_gather_into_tensor(gathered, x)
             else:
-                parts = [torch.empty((B, 3, 32, 32)) for _ in range(world)]
+                parts = [torch.empty(tuple(x.shape)) for _ in range(world)]
                 dist.all_gather(parts, x.cpu())
                 gathered.copy_(torch.cat(parts))
             return gathered
@@ -232,16 +323,14 @@ def main():
 
     for _ in range(args.warmup):
         fold()
-    if args.warmup == 0:  # build the B-sized plan outside the timed region
-        model(torch.zeros((B, 3, 32, 32), device=dev), torch.zeros((B, ), dtype=torch.long, device=dev))
-    handle = model.native_handle(dev)
     # HIP events around every launch of every PROFILE_EVERY-th forward of the timed region
-    dmhip.unet_profile_enable(handle, 0 if args.no_profile else PROFILE_EVERY)
+    for h, abi, _ in wl['handles']:
+        dmhip.unet_profile_enable(h, 0 if args.no_profile else PROFILE_EVERY, abi=abi)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        out = fold()
+        fold()
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -249,21 +338,30 @@ def main():
         tt = torch.tensor([elapsed], device=dev if backend == 'nccl' else 'cpu', dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = tt.item()
-    prof = dmhip.unet_profile_read(handle)
-    wbytes, wsbytes = ctypes.c_int64(), ctypes.c_int64()
-    _check(dmhip.load().dm_unet_memory(handle, ctypes.byref(wbytes), ctypes.byref(wsbytes)), 'dm_unet_memory')
-    dmhip.unet_profile_enable(handle, False)
+    prof, kernel_s, wbytes_t, wsbytes_t = [], 0.0, 0, 0
+    for h, abi, fwd_per_fold in wl['handles']:
+        p = dmhip.unet_profile_read(h, abi=abi)
+        prof += p
+        observed = max((op['launches'] for op in p), default=0)   # forwards of this handle that ran with events
+        if observed:
+            kernel_s += sum(op['ms_total'] for op in p) * 1e-3 * fwd_per_fold * args.steps / observed
+        wbytes, wsbytes = ctypes.c_int64(), ctypes.c_int64()
+        _check(getattr(dmhip.load(), abi + '_memory')(h, ctypes.byref(wbytes), ctypes.byref(wsbytes)), abi + '_memory')
+        wbytes_t += wbytes.value
+        wsbytes_t += wsbytes.value
+        dmhip.unet_profile_enable(h, False, abi=abi)
 
     roof, total_gpu_ms, total_flops, fam = None, 0.0, 0.0, {}
-    observed = max((op['launches'] for op in prof), default=0)  # forwards that ran with events
     if not args.no_profile:
         roof, total_gpu_ms, total_flops, fam = roofline(prof)
 
     if rank == 0:
         images = world * B * args.steps
+        h0, abi0, _ = wl['handles'][0]
+        math = dmhip.unet_conv_math(h0) if abi0 == 'dm_unet' else dmhip.dit_math(h0)
         line = dict(
-            metric=METRIC,
-            value=round(images / elapsed, 3),
+            metric=wl['metric'],
+            value=round(images / elapsed, 4),
             unit='images/sec',
             n_gpus=world,
             steps=args.steps,
@@ -272,24 +370,22 @@ def main():
             higher_is_better=True,
             scaling='weak',
             vs_baseline=None,
-            dtype=f'f32 via {dmhip.unet_conv_math(handle)} split MFMA',
+            dtype=f'f32 via {math} split MFMA' if math != 'fp32' else 'f32',
             data='synthetic',
-            config=dict(workload=f'DDIM-{args.respace_steps} (eta=0) sampling fold, CIFAR-10 UNet '
-                                 f'(dim 128, mults 1-2-2-2, 35.7M params, synthetic weights), 3x32x32, '
-                                 f'B={B} per GPU',
-                        global_batch=world * B, parallelism=f'dp{world}', denoise_steps=args.respace_steps,
-                        weights_gb=round(wbytes.value / 1e9, 3), workspace_gb=round(wsbytes.value / 1e9, 3),
-                        conv_math=dmhip.unet_conv_math(handle),
+            config=dict(workload=wl['workload'], global_batch=world * B, parallelism=f'dp{world}',
+                        denoise_steps=wl['denoise_steps'], weights_gb=round(wbytes_t / 1e9, 3),
+                        workspace_gb=round(wsbytes_t / 1e9, 3), conv_math=math,
                         # the reference draws randn_like every step even at eta=0 (ddim.py:76): so does the bench
-                        skip_unused_noise=diffuser.skip_unused_noise),
+                        skip_unused_noise=wl['diffuser'].skip_unused_noise),
             roofline=roof,
             step_level=dict(model_tflops=round(total_flops / (total_gpu_ms * 1e-3) / 1e12, 2) if total_gpu_ms else None,
-                            # observed forwards are 1 in PROFILE_EVERY: scale their kernel time to all forwards
-                            kernel_time_frac=round(total_gpu_ms * 1e-3 * (args.steps * args.respace_steps)
-                                                   / max(1, observed) / elapsed, 4) if total_gpu_ms else None),
+                            # observed forwards are 1 in PROFILE_EVERY: their kernel time scaled to all forwards
+                            kernel_time_frac=round(kernel_s / elapsed, 4) if kernel_s else None),
         )
-        if world == 1 and not args.no_cpu_baseline:
-            line['cpu_baseline'] = cpu_baseline(sd_cpu, args.cpu_batch, args.respace_steps)
+        if args.workload != 'c3':
+            line['config']['bench_workload'] = args.workload
+        if world == 1 and not args.no_cpu_baseline and wl['sd_cpu'] is not None and args.workload == 'c3':
+            line['cpu_baseline'] = cpu_baseline(wl['sd_cpu'], args.cpu_batch, wl['denoise_steps'])
             line['gpu_over_cpu'] = round(line['value'] / line['cpu_baseline']['value'], 1)
         else:
             line['cpu_baseline'] = None

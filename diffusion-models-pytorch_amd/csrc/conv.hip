@@ -310,14 +310,14 @@ int conv2d_igemm(const ConvArgs& a, hipStream_t st) {
 int conv_pick(const ConvArgs& a) {
   if (a.tile >= 1 && a.tile <= 3) return a.tile - 1;
   if (conv_pw_ok(a)) {  // split 1x1: 128x128 tiles when they still give >= 2 blocks per CU, else 128x64
-    const long M = (long)a.B * a.Hout * a.Wout;
+    const long M = (long)(a.pick_B > 0 ? a.pick_B : a.B) * a.Hout * a.Wout;
     return (a.Cout >= 128 && ((M + 127) / 128) * ((a.Cout + 127) / 128) >= 512) ? 3 : 4;
   }
   PatchGeom g;
   const int p = conv_patch_pick(a, g);
   if (p) return p - 1;
   if (a.tile >= 4) return a.tile - 4;
-  const long M = (long)a.B * a.Hout * a.Wout;
+  const long M = (long)(a.pick_B > 0 ? a.pick_B : a.B) * a.Hout * a.Wout;
   const long b128 = ((M + 127) / 128) * ((a.Cout + 127) / 128);
   if (a.Cout >= 128 && b128 >= 512) return 0;
   const long b128x64 = ((M + 127) / 128) * ((a.Cout + 63) / 64);

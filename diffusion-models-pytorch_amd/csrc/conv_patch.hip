@@ -449,7 +449,7 @@ int conv_patch_pick(const ConvArgs& a, PatchGeom& g) {
   // the split-bf16 kernel's LDS image holds fewer patch pixels at 128-row tiles
   const int max128 = a.ws ? kPatch3Max128 : kPatchMax128, max64 = a.ws ? kPatch3Max64 : kPatchMax64;
   if (a.tile == 4 || a.tile == 0) {
-    const long M = (long)a.B * a.Hout * a.Wout;
+    const long M = (long)(a.pick_B > 0 ? a.pick_B : a.B) * a.Hout * a.Wout;
     const long b128 = ((M + 127) / 128) * ((a.Cout + 127) / 128);
     const long b128x64 = ((M + 127) / 128) * ((a.Cout + 63) / 64);
     if ((a.tile == 4 || (a.Cout >= 128 && b128 >= 512)) && conv_patch_geom(a, 128, g) && g.P <= max128)

@@ -230,7 +230,7 @@ int DiTModel::build_plan(int B) {
   };
   auto linear = [&](const float* A, int lda, long rows, size_t w, size_t bias, int N, int K, float* out, int ldc) {
     GemmArgs g{};
-    g.M = (int)rows; g.N = N; g.K = K; g.Z1 = 1; g.Z2 = 1;
+    g.M = (int)rows; g.N = N; g.K = K; g.Z1 = 1; g.Z2 = 1; g.pick_M = rows / B * kPickBatch;  // rows = B or B*T
     g.A = A; g.lda = lda; g.Bm = P(w); g.ldb = K; g.C = out; g.ldc = ldc; g.alpha = 1.f;
     g.bias = bias != (size_t)-1 ? P(bias) : nullptr;
     return g;
@@ -283,7 +283,7 @@ int DiTModel::build_plan(int B) {
     {
       // timm Attention: qkv.reshape(B, N, 3, heads, d): q / k / v of head h at columns h*d, D + h*d, 2D + h*d
       GemmArgs gs{};
-      gs.M = T; gs.N = T; gs.K = Dh; gs.Z1 = B; gs.Z2 = heads;
+      gs.M = T; gs.N = T; gs.K = Dh; gs.Z1 = B; gs.Z2 = heads; gs.pick_Z = (long)kPickBatch * heads;
       gs.A = qkv; gs.a_s1 = (long)T * 3 * D; gs.a_s2 = Dh; gs.lda = 3 * D;
       gs.Bm = qkv + D; gs.b_s1 = (long)T * 3 * D; gs.b_s2 = Dh; gs.ldb = 3 * D;
       gs.C = Sb; gs.c_s1 = (long)heads * T * T; gs.c_s2 = (long)T * T; gs.ldc = T;
@@ -294,7 +294,7 @@ int DiTModel::build_plan(int B) {
       const int L = T;
       pl.add("softmax_rows", 0, 8.0 * rows * L, [=](hipStream_t st) { return softmax_rows(Sb, rows, L, L, st); });
       GemmArgs go{};
-      go.M = T; go.N = Dh; go.K = T; go.Z1 = B; go.Z2 = heads;
+      go.M = T; go.N = Dh; go.K = T; go.Z1 = B; go.Z2 = heads; go.pick_Z = (long)kPickBatch * heads;
       go.A = Sb; go.a_s1 = (long)heads * T * T; go.a_s2 = (long)T * T; go.lda = T;
       go.Bm = qkv + 2 * D; go.b_s1 = (long)T * 3 * D; go.b_s2 = Dh; go.ldb = 3 * D; go.b_kn = 1;
       go.C = Ob; go.c_s1 = (long)T * D; go.c_s2 = Dh; go.ldc = D;

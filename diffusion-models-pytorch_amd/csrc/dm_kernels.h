@@ -9,6 +9,11 @@ namespace dm {
 
 constexpr int kGnPixPerChunk = 64;
 
+// Nominal batch of the plans' tile heuristics (ConvArgs::pick_B, GemmArgs::pick_M / pick_Z): every layer
+// runs the kernel it would at B = kPickBatch, whatever B is, so each image's result is bit-identical at
+// any batch size (the reference parity pinned at B = 1..2 holds at the benchmark's B).
+constexpr int kPickBatch = 256;
+
 struct ConvArgs {
   // segment 1: NHWC input view (channel pitch x1_pitch), source resolution Hin x Win
   const float* x1;
@@ -31,6 +36,8 @@ struct ConvArgs {
   const float* res;     // residual at output resolution or null
   int res_pitch;
   int tile;             // 0 auto; 1..3 force an im2col tile, 4..6 a halo-patch tile
+  int pick_B;           // batch the tile heuristics assume (0: B). Plans pass a fixed one, so a layer's
+                        // kernel (and its summation order) never changes with B: batch-invariant results
   // optional operand prologue on segment 1 (halo-patch kernel only):
   // x -> silu(x * pro_scale[b][c] + pro_shift[b][c]) before the product
   // (GroupNorm + SiLU of the ResBlock, fused into the conv's input load)
@@ -83,6 +90,8 @@ struct PatchGeom {
 struct GemmArgs {
   int M, N, K;
   int Z1, Z2;
+  long pick_M;  // M and Z1 * Z2 the tile heuristic assumes (0: the actual ones); plans pass values for a
+  long pick_Z;  // fixed nominal batch so the kernel choice (and GN-statistics routing) is batch-invariant
   const float* A;
   long a_s1, a_s2;
   int lda;

@@ -392,8 +392,9 @@ int gemm_batched(const GemmArgs& g, hipStream_t st) {
 }
 
 int gemm_pick(const GemmArgs& g) {
-  const long tiles128 = (long)ceil_div(g.M, 128) * ceil_div(g.N, 128) * g.Z1 * g.Z2;
-  return (g.M >= 128 && g.N >= 128 && tiles128 >= 512) ? 0 : 1;
+  const long M = g.pick_M > 0 ? g.pick_M : g.M, Z = g.pick_Z > 0 ? g.pick_Z : (long)g.Z1 * g.Z2;
+  const long tiles128 = ((M + 127) / 128) * ceil_div(g.N, 128) * Z;
+  return (M >= 128 && g.N >= 128 && tiles128 >= 512) ? 0 : 1;
 }
 
 std::string gemm_label(const GemmArgs& g) {

@@ -725,7 +725,7 @@ int UNetModel::build_plan(int B, int H, int W) {
   });
   {
     GemmArgs g{};
-    g.M = B; g.N = TD; g.K = D; g.Z1 = 1; g.Z2 = 1;
+    g.M = B; g.N = TD; g.K = D; g.Z1 = 1; g.Z2 = 1; g.pick_M = kPickBatch;
     g.A = e0; g.lda = D; g.Bm = P(te_w1); g.ldb = D; g.C = e1; g.ldc = TD; g.alpha = 1.f;
     g.bias = P(te_b1); g.act = 1;
     add_gemm(g);
@@ -862,7 +862,7 @@ int UNetModel::build_plan(int B, int H, int W) {
       c1.x1_pitch = r.cin; c1.Cin1 = r.cin; c1.Hin = Ho; c1.Win = Wo;
       c1.taps = 9; c1.stride = 1; c1.upsample = 0;
       c1.w = P(r.conv1.w); c1.K = r.conv1.K;
-      c1.y = hbuf; c1.y_pitch = r.cout; c1.Cout = r.cout; c1.B = B; c1.Hout = Ho; c1.Wout = Wo;
+      c1.y = hbuf; c1.y_pitch = r.cout; c1.Cout = r.cout; c1.B = B; c1.pick_B = kPickBatch; c1.Hout = Ho; c1.Wout = Wo;
       c1.bias = P(r.conv1.bias);
       if (!r.adagn) { c1.rowvec = projs + r.proj_col; c1.rowvec_pitch = proj_total; }
       if (r.updown == 1) { c1.upsample = 1; c1.Hin = Hi; c1.Win = Wi; }
@@ -877,7 +877,7 @@ int UNetModel::build_plan(int B, int H, int W) {
       c2.x1 = a2; c2.x1_pitch = r.cout; c2.Cin1 = r.cout; c2.Hin = Ho; c2.Win = Wo;
       c2.taps = 9; c2.stride = 1;
       c2.w = P(r.conv2.w); c2.K = r.conv2.K;
-      c2.y = y.p; c2.y_pitch = y.pitch; c2.Cout = r.cout; c2.B = B; c2.Hout = Ho; c2.Wout = Wo;
+      c2.y = y.p; c2.y_pitch = y.pitch; c2.Cout = r.cout; c2.B = B; c2.pick_B = kPickBatch; c2.Hout = Ho; c2.Wout = Wo;
       c2.bias = P(r.conv2.bias);
       if (r.cin != r.cout) {
         c2.x2 = xres.p; c2.x2_pitch = xres.pitch; c2.Cin2 = r.cin;
@@ -931,14 +931,14 @@ int UNetModel::build_plan(int B, int H, int W) {
       // GroupNorm folded into the QKV projection's A load (modules.py:91-94): one pass over x
       const double2* sta = gn_stats(xin);
       GemmArgs gq{};
-      gq.M = B * hw; gq.N = 3 * C; gq.K = C; gq.Z1 = 1; gq.Z2 = 1;
+      gq.M = B * hw; gq.N = 3 * C; gq.K = C; gq.Z1 = 1; gq.Z2 = 1; gq.pick_M = (long)kPickBatch * hw;
       gq.A = xin.p; gq.lda = xin.pitch; gq.Bm = P(p.wqkv); gq.ldb = C; gq.C = qkv; gq.ldc = 3 * C;
       gq.alpha = 1.f; gq.bias = P(p.bqkv);
       gq.pro_scale = gsc; gq.pro_shift = gsh; gq.pro_rows = hw;
       // fp16x2: qkv = 1x1 conv of GroupNorm(x) on the split conv kernel (MODE 3, pre-split weights)
       ConvArgs cq{};
       cq.x1 = xin.p; cq.x1_pitch = xin.pitch; cq.Cin1 = C; cq.Hin = Hi; cq.Win = Wi; cq.taps = 1; cq.stride = 1;
-      cq.w = P(p.wqkv); cq.K = C; cq.y = qkv; cq.y_pitch = 3 * C; cq.Cout = 3 * C; cq.B = B; cq.Hout = Hi;
+      cq.w = P(p.wqkv); cq.K = C; cq.y = qkv; cq.y_pitch = 3 * C; cq.Cout = 3 * C; cq.B = B; cq.pick_B = kPickBatch; cq.Hout = Hi;
       cq.Wout = Wi; cq.bias = P(p.bqkv); cq.pro_scale = gsc; cq.pro_shift = gsh; cq.pro_nosilu = 1;
       split_for(cq);
       if (conv_pw_ok(cq)) {
@@ -956,7 +956,7 @@ int UNetModel::build_plan(int B, int H, int W) {
       const int hs = p.legacy ? 3 * Dh : Dh;
       const int k0 = p.legacy ? Dh : C, v0 = p.legacy ? 2 * Dh : 2 * C;
       GemmArgs gs{};
-      gs.M = hw; gs.N = hw; gs.K = Dh; gs.Z1 = B; gs.Z2 = heads;
+      gs.M = hw; gs.N = hw; gs.K = Dh; gs.Z1 = B; gs.Z2 = heads; gs.pick_Z = (long)kPickBatch * heads;
       gs.A = qkv; gs.a_s1 = (long)hw * 3 * C; gs.a_s2 = hs; gs.lda = 3 * C;
       gs.Bm = qkv + k0; gs.b_s1 = (long)hw * 3 * C; gs.b_s2 = hs; gs.ldb = 3 * C;
       gs.C = Sb; gs.c_s1 = (long)heads * hw * hw; gs.c_s2 = (long)hw * hw; gs.ldc = hw;
@@ -967,7 +967,7 @@ int UNetModel::build_plan(int B, int H, int W) {
       const long rows = (long)B * heads * hw;
       add("softmax_rows", 0, 8.0 * rows * hw, [=](hipStream_t st) { return softmax_rows(Sb, rows, hw, hw, st); });
       GemmArgs go{};
-      go.M = hw; go.N = Dh; go.K = hw; go.Z1 = B; go.Z2 = heads;
+      go.M = hw; go.N = Dh; go.K = hw; go.Z1 = B; go.Z2 = heads; go.pick_Z = (long)kPickBatch * heads;
       go.A = Sb; go.a_s1 = (long)heads * hw * hw; go.a_s2 = (long)hw * hw; go.lda = hw;
       go.Bm = qkv + v0; go.b_s1 = (long)hw * 3 * C; go.b_s2 = hs; go.ldb = 3 * C; go.b_kn = 1;
       go.C = Ob; go.c_s1 = (long)hw * C; go.c_s2 = Dh; go.ldc = C;
@@ -975,12 +975,12 @@ int UNetModel::build_plan(int B, int H, int W) {
       split_gemm(go, 14, nullptr, 0, 6);
       add_gemm(go);
       GemmArgs gp{};
-      gp.M = B * hw; gp.N = C; gp.K = C; gp.Z1 = 1; gp.Z2 = 1;
+      gp.M = B * hw; gp.N = C; gp.K = C; gp.Z1 = 1; gp.Z2 = 1; gp.pick_M = (long)kPickBatch * hw;
       gp.A = Ob; gp.lda = C; gp.Bm = P(p.wproj); gp.ldb = C; gp.C = y.p; gp.ldc = y.pitch;
       gp.alpha = 1.f; gp.bias = P(p.bproj); gp.res = xin.p; gp.ld_res = xin.pitch;
       ConvArgs cp{};
       cp.x1 = Ob; cp.x1_pitch = C; cp.Cin1 = C; cp.Hin = Hi; cp.Win = Wi; cp.taps = 1; cp.stride = 1;
-      cp.w = P(p.wproj); cp.K = C; cp.y = y.p; cp.y_pitch = y.pitch; cp.Cout = C; cp.B = B; cp.Hout = Hi;
+      cp.w = P(p.wproj); cp.K = C; cp.y = y.p; cp.y_pitch = y.pitch; cp.Cout = C; cp.B = B; cp.pick_B = kPickBatch; cp.Hout = Hi;
       cp.Wout = Wi; cp.bias = P(p.bproj); cp.res = xin.p; cp.res_pitch = xin.pitch;
       split_for(cp);
       if (conv_pw_ok(cp)) {
@@ -1003,7 +1003,7 @@ int UNetModel::build_plan(int B, int H, int W) {
       c.x1 = xin.p; c.x1_pitch = xin.pitch; c.Cin1 = n.cin; c.Hin = Hi; c.Win = Wi;
       c.taps = 9; c.stride = n.kind == N_DOWN ? 2 : 1; c.upsample = n.kind == N_UP;
       c.w = P(cv.w); c.K = cv.K;
-      c.y = y.p; c.y_pitch = y.pitch; c.Cout = n.cout; c.B = B;
+      c.y = y.p; c.y_pitch = y.pitch; c.Cout = n.cout; c.B = B; c.pick_B = kPickBatch;
       c.Hout = Hl(n.level_out); c.Wout = Wl(n.level_out);
       c.bias = P(cv.bias);
       if (c.upsample && cv.w_sub) {

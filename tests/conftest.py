@@ -29,11 +29,24 @@ def load_golden(name):
 TOL = 1e-4   # BASELINE.json north_star: fp32 max-abs vs the reference
 
 
-def drift_bound(drift):
-    """Per-step bound of a free-running trajectory: the 1e-4 budget, or 1.5x the reference's own
-    float32-vs-float64 drift on the same trajectory (tests/golden/drift.npz, ddpm1000.npz, ddpmcfg.npz,
-    made by make_golden_r2.py) where that drift alone already approaches the budget."""
-    return max(TOL, 1.5 * float(drift))
+def check_free_running(got, ref32, ref64, drift, i):
+    """Step i of a free-running trajectory against the reference (tests/golden/drift.npz, ddpm1000.npz,
+    ddpmcfg.npz; make_golden_r2.py ran the reference module in float32 AND in float64 on the same inputs).
+
+    Where the reference's own fp32 run stays within 1e-4 of its float64 run, the engine must match the
+    fp32 reference within 1e-4. Where the reference itself drifts further (x0 = sqrt(1/a_t) x - ...
+    amplifies rounding ~160x at t ~ 1000, CFG adds a (2s - 1) gain), the engine must be at least as
+    accurate as the reference: its distance to the float64 trajectory at most 1.5x the drift the fp32
+    reference has accumulated by step i (max over steps <= i), and hence within 2.5x of that drift of
+    the fp32 reference. Returns (error vs fp32 reference, error vs float64 run)."""
+    import numpy as np
+    got = np.asarray(got, dtype=np.float64)
+    d = float(np.max(drift[:i + 1]))
+    e32 = float(np.abs(got - ref32).max())
+    e64 = float(np.abs(got - ref64).max())
+    assert e64 <= max(TOL, 1.5 * d), f'step {i}: {e64:.3e} from the float64 run, reference drift {d:.3e}'
+    assert e32 <= max(TOL, 2.5 * d), f'step {i}: {e32:.3e} from the fp32 reference, reference drift {d:.3e}'
+    return e32, e64
 
 
 @pytest.fixture(scope='session')

@@ -14,8 +14,10 @@ and runs the reference's own sampler and model classes on CPU. New here:
   whose engine error is largest (DDIM-50 CIFAR, all 50 steps; ADM UNetCombined
   DDIMCFG-6; AdaGN DDIMCFG-10; DDIM inversion + reconstruction; DDPM-1000 is in
   ddpm1000.npz). Each is run twice with the same inputs: the reference module
-  as is (fp32) and the same module in float64 (see `Float64Reference`). The
-  GPU tests bound the engine's error at every step by max(1e-4, 1.5 x drift).
+  as is (fp32) and the same module in float64 (see `Float64Reference`); both
+  trajectories are stored (the float64 one rounded to float32). The GPU tests
+  require the engine to be at least as close to the float64 trajectory as
+  the reference's fp32 run is, within 1.5x (tests/conftest.py check_free_running).
 * ddpmcfg.npz — DDPMCFG (diffusions/ddpm.py:319-351) with learned_range,
   i.e. the concat of the conditional branch's variance channels (:344-345):
   through UNetCombined (two calls) and through a learned-range
@@ -89,13 +91,10 @@ class Float64Reference:
             torch.Tensor.float = orig
 
 
-def _d64(x):
-    return x.double() if torch.is_tensor(x) else x
-
-
 def run_pair(loop_fn, model, init, noise_seed=None, keys=('sample', 'pred_eps')):
     """Run loop_fn(model, init) -> iterable of step dicts with the fp32 reference and its float64
-    copy on the same inputs. Returns (fp32 per-step dicts, per-step max-abs drift per key)."""
+    copy on the same inputs. Returns (fp32 per-step dicts, per-step max-abs drift per key, float64
+    per-step dicts)."""
     out32, out64 = [], []
     for m, x, dst in ((model, init, out32), (Float64Reference(model), init.double(), out64)):
         src = StepNoise(noise_seed) if noise_seed is not None else None
@@ -105,7 +104,7 @@ def run_pair(loop_fn, model, init, noise_seed=None, keys=('sample', 'pred_eps'))
                 dst.append({k: out[k].detach().clone() for k in keys if out.get(k) is not None})
     drift = {k: np.array([float((a[k].double() - b[k]).abs().max()) for a, b in zip(out32, out64)])
              for k in keys if k in out32[0]}
-    return out32, drift
+    return out32, drift, out64
 
 
 @contextmanager
@@ -123,7 +122,7 @@ def make_ddpm1000():
     torch.manual_seed(2022)
     init = torch.randn((2, 3, 32, 32))
     seed = 1000
-    outs, drift = run_pair(lambda m, x: d.sample_loop(m, x, tqdm_kwargs=dict(disable=True)), model, init,
+    outs, drift, o64 = run_pair(lambda m, x: d.sample_loop(m, x, tqdm_kwargs=dict(disable=True)), model, init,
                            noise_seed=seed)
     assert len(outs) == 1000
     keep = sorted(set(range(0, 1000, 40)) | {1, 2, 997, 998, 999})
@@ -131,6 +130,9 @@ def make_ddpm1000():
     for i in keep:
         arr[f'step{i}_sample'] = outs[i]['sample']
         arr[f'step{i}_pred_eps'] = outs[i]['pred_eps']
+        arr[f'step{i}_sample64'] = o64[i]['sample'].float()   # float64 run, rounded for storage
+        if i > 0:   # the input of step i, for the teacher-forced check
+            arr[f'step{i - 1}_sample'] = outs[i - 1]['sample']
     meta.update(keep=keep, noise_seed=seed, sampler=dict(var_type='fixed_large', total_steps=1000),
                 noise='tests/golden/noise.py StepNoise(noise_seed): draw k = PCG64([seed, k]) float32 normal',
                 max_drift_sample=float(drift['sample'].max()), max_drift_pred_eps=float(drift['pred_eps'].max()))
@@ -150,11 +152,12 @@ def make_drift():
     d = ddim.DDIM(respace_type='uniform', respace_steps=50, eta=0.0)
     torch.manual_seed(2022)
     init = torch.randn((2, 3, 32, 32))
-    outs, drift = run_pair(lambda m, x: d.sample_loop(m, x, tqdm_kwargs=dict(disable=True)), model, init)
+    outs, drift, o64 = run_pair(lambda m, x: d.sample_loop(m, x, tqdm_kwargs=dict(disable=True)), model, init)
     arr['ddim50_init'] = init
     arr['ddim50_sample'] = torch.stack([o['sample'] for o in outs])
     arr['ddim50_pred_eps'] = torch.stack([o['pred_eps'] for o in outs])
     arr['ddim50_drift_sample'], arr['ddim50_drift_pred_eps'] = drift['sample'], drift['pred_eps']
+    arr['ddim50_sample64'] = torch.stack([o['sample'] for o in o64]).float()
     # ADM UNetCombined (adm_tiny arch), DDIMCFG-6 s=2.5 (adm.npz cfg6)
     comb = admc.UNetCombined(**mg.ADM_ARCHS['adm_tiny']).eval()
     meta['combined_tiny_weights_sha256'] = mg.synthetic(comb)
@@ -162,10 +165,11 @@ def make_drift():
     torch.manual_seed(37)
     init = torch.randn((2, 3, 16, 16))
     labels = torch.tensor([2, 3])
-    outs, drift = run_pair(lambda m, x: d.sample_loop(m, x, model_kwargs=dict(y=labels),
+    outs, drift, o64 = run_pair(lambda m, x: d.sample_loop(m, x, model_kwargs=dict(y=labels),
                                                       tqdm_kwargs=dict(disable=True)), comb, init)
     arr['cfg6_sample'] = torch.stack([o['sample'] for o in outs])
     arr['cfg6_drift_sample'] = drift['sample']
+    arr['cfg6_sample64'] = torch.stack([o['sample'] for o in o64]).float()
     # AdaGN DDIMCFG-10 s=3 on tiny_updown (adagn.npz cfg)
     model = ua.UNetCategorialAdaGN(**mg.ADAGN_ARCHS['tiny_updown']).eval()
     meta['tiny_updown_weights_sha256'] = mg.synthetic(model)
@@ -173,10 +177,11 @@ def make_drift():
     torch.manual_seed(5)
     init = torch.randn((2, 3, 16, 16))
     labels = torch.tensor([1, 4])
-    outs, drift = run_pair(lambda m, x: d.sample_loop(m, x, model_kwargs=dict(y=labels),
+    outs, drift, o64 = run_pair(lambda m, x: d.sample_loop(m, x, model_kwargs=dict(y=labels),
                                                       tqdm_kwargs=dict(disable=True)), model, init)
     arr['adagn_cfg10_sample'] = torch.stack([o['sample'] for o in outs])
     arr['adagn_cfg10_drift_sample'] = drift['sample']
+    arr['adagn_cfg10_sample64'] = torch.stack([o['sample'] for o in o64]).float()
     # DDIM inversion (4 steps) feeding reconstruction (5 steps) on the tiny UNet (inversion.npz)
     model = unet.UNet(**mg.ARCHS['tiny']).eval()
     meta['tiny_weights_sha256'] = mg.synthetic(model)
@@ -189,9 +194,10 @@ def make_drift():
             x = out['sample']
             yield out
         yield from d.sample_loop(m, x, tqdm_kwargs=dict(disable=True))
-    outs, drift = run_pair(inv_rec, model, img)
+    outs, drift, o64 = run_pair(inv_rec, model, img)
     arr['invrec_sample'] = torch.stack([o['sample'] for o in outs])
     arr['invrec_drift_sample'] = drift['sample']
+    arr['invrec_sample64'] = torch.stack([o['sample'] for o in o64]).float()
     meta['invrec_steps'] = [4, 5]
     mg.save('drift', meta, **arr)
 
@@ -210,13 +216,14 @@ def make_ddpmcfg():
     torch.manual_seed(41)
     init = torch.randn((2, 3, 16, 16))
     labels = torch.tensor([2, 3])
-    outs, drift = run_pair(lambda m, x: d.sample_loop(m, x, model_kwargs=dict(y=labels),
+    outs, drift, o64 = run_pair(lambda m, x: d.sample_loop(m, x, model_kwargs=dict(y=labels),
                                                       tqdm_kwargs=dict(disable=True)), comb, init, noise_seed=41,
                            keys=('sample', 'pred_eps', 'reverse_eps'))
     arr['adm_init'], arr['adm_labels'] = init, labels
     for i, o in enumerate(outs):
         arr[f'adm_step{i}_sample'], arr[f'adm_step{i}_pred_eps'] = o['sample'], o['pred_eps']
     arr['adm_drift_sample'] = drift['sample']
+    arr['adm_sample64'] = torch.stack([o['sample'] for o in o64]).float()
     meta['adm'] = dict(guidance_scale=2.5, var_type='learned_range', respace_type='uniform', respace_steps=8,
                        noise_seed=41)
     # UNetCategorialAdaGN with learned-sigma outputs (out_channels = 2C), cosine schedule (the CFG-CIFAR
@@ -230,13 +237,14 @@ def make_ddpmcfg():
     torch.manual_seed(43)
     init = torch.randn((2, 3, 16, 16))
     labels = torch.tensor([1, 4])
-    outs, drift = run_pair(lambda m, x: d.sample_loop(m, x, model_kwargs=dict(y=labels),
+    outs, drift, o64 = run_pair(lambda m, x: d.sample_loop(m, x, model_kwargs=dict(y=labels),
                                                       tqdm_kwargs=dict(disable=True)), model, init, noise_seed=43,
                            keys=('sample', 'pred_eps', 'reverse_eps'))
     arr['adagn_init'], arr['adagn_labels'] = init, labels
     for i, o in enumerate(outs):
         arr[f'adagn_step{i}_sample'], arr[f'adagn_step{i}_pred_eps'] = o['sample'], o['pred_eps']
     arr['adagn_drift_sample'] = drift['sample']
+    arr['adagn_sample64'] = torch.stack([o['sample'] for o in o64]).float()
     meta['adagn'] = dict(guidance_scale=3.0, beta_schedule='cosine', var_type='learned_range',
                          respace_type='uniform', respace_steps=6, noise_seed=43)
     mg.save('ddpmcfg', meta, **arr)

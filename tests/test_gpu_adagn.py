@@ -80,10 +80,11 @@ def test_adagn_label_out_of_range(cuda, golden):
 @pytest.mark.parametrize('batched', [True, False])
 def test_ddimcfg_trajectory_vs_reference(cuda, golden, report, batched):
     """DDIMCFG-10 (s = 3). Every step is checked teacher-forced (from the reference's previous
-    sample) against the 1e-4 bound, and free-running against max(1e-4, 1.5 x the reference's own
-    fp32-vs-fp64 drift at that step) (tests/golden/drift.npz adagn_cfg10)."""
-    from tests.conftest import drift_bound
-    drift = golden('drift')[0]['adagn_cfg10_drift_sample']
+    sample) against the 1e-4 bound, and free-running with tests/conftest.py check_free_running
+    (tests/golden/drift.npz adagn_cfg10: the reference's fp32 and float64 runs)."""
+    from tests.conftest import check_free_running
+    dg = golden('drift')[0]
+    drift = dg['adagn_cfg10_drift_sample']
     g, meta = golden('adagn')
     model, _ = _model(meta, 'tiny_updown')
     model = model.to(cuda)
@@ -104,9 +105,9 @@ def test_ddimcfg_trajectory_vs_reference(cuda, golden, report, batched):
         assert err <= TOL, (i, err)
     worst = 0.0
     for i, out in enumerate(d.sample_loop(model, init, model_kwargs=dict(y=labels))):
-        err = float(np.abs(out['sample'].cpu().numpy() - g[f'cfg_step{i}_sample']).max())
-        worst = max(worst, err)
-        assert err <= drift_bound(drift[i]), (i, err, drift[i])
+        e32, _ = check_free_running(out['sample'].cpu().numpy(), g[f'cfg_step{i}_sample'],
+                                    dg['adagn_cfg10_sample64'][i], drift, i)
+        worst = max(worst, e32)
     tag = 'batched' if batched else 'two_calls'
     report(f'ddimcfg10_adagn_{tag}_single_step_maxabs_vs_reference', worst_step)
     report(f'ddimcfg10_adagn_{tag}_free_running_maxabs_vs_reference', worst)
@@ -152,10 +153,10 @@ def test_ddpmcfg_learned_range_trajectory(cuda, golden, report, batched):
     UNetCategorialAdaGN (out_channels = 2C, cosine schedule), noise pinned per step: the CFG combine of
     the eps halves, the concat of the CONDITIONAL branch's variance channels (:344-345) and the
     learned-range variance (:240-246), through the batched 2B forward (null-label rows) and the
-    two-call path. Free-running, every step <= max(1e-4, 1.5 x the reference's fp32-vs-fp64 drift)
-    (tests/golden/ddpmcfg.npz, make_golden_r2.py)."""
+    two-call path (tests/golden/ddpmcfg.npz, make_golden_r2.py). Every step teacher-forced: sample and
+    pred_eps <= 1e-4; free-running: tests/conftest.py check_free_running on the sample."""
     from diffusions import DDPMCFG
-    from tests.conftest import drift_bound
+    from tests.conftest import check_free_running
     g, meta = golden('ddpmcfg')
     model = UNetCategorialAdaGN(**meta['adagn_learned_arch']).eval()
     assert init_synthetic_(model) == meta['adagn_learned_weights_sha256']
@@ -166,13 +167,28 @@ def test_ddpmcfg_learned_range_trajectory(cuda, golden, report, batched):
     d.batch_cfg = batched
     n = len(d.respaced_seq)
     from tests.golden.noise import StepNoise
+    labels = torch.from_numpy(g['adagn_labels']).to(cuda)
+    seq = d.respaced_seq.tolist()
+    worst_step = 0.0
+    for i, (t, tp) in enumerate(zip(reversed(seq), reversed([-1] + seq[:-1]))):
+        x = torch.from_numpy(g['adagn_init'] if i == 0 else g[f'adagn_step{i - 1}_sample']).to(cuda)
+        src = StepNoise(c['noise_seed'])
+        src.k = i
+        d.noise_fn = src
+        out = _one_step(d, model, x, labels, t, tp, batched)
+        for k in ('sample', 'pred_eps'):
+            err = float(np.abs(out[k].cpu().numpy() - g[f'adagn_step{i}_{k}']).max())
+            worst_step = max(worst_step, err)
+            assert err <= TOL, (i, k, err)
     d.noise_fn = StepNoise(c['noise_seed'])
     worst = 0.0
     for i, out in enumerate(d.sample_loop(model, torch.from_numpy(g['adagn_init']).to(cuda),
-                                          model_kwargs=dict(y=torch.from_numpy(g['adagn_labels']).to(cuda)))):
-        err = float(np.abs(out['sample'].cpu().numpy() - g[f'adagn_step{i}_sample']).max())
-        worst = max(worst, err)
-        assert err <= drift_bound(g['adagn_drift_sample'][i]), (i, err)
+                                          model_kwargs=dict(y=labels))):
+        e32, _ = check_free_running(out['sample'].cpu().numpy(), g[f'adagn_step{i}_sample'], g['adagn_sample64'][i],
+                                    g['adagn_drift_sample'], i)
+        worst = max(worst, e32)
     assert i + 1 == n
+    report(f'ddpmcfg6_learned_adagn_{"batched" if batched else "two_calls"}_single_step_maxabs_vs_reference',
+           worst_step)
     report(f'ddpmcfg6_learned_adagn_{"batched" if batched else "two_calls"}_maxabs_vs_reference', worst)
 

@@ -108,12 +108,12 @@ def test_adm_ddpm_learned_range_trajectory(cuda, golden, report):
 @pytest.mark.gpu
 def test_adm_combined_ddimcfg_trajectory(cuda, golden, report):
     """DDIMCFG-6 through UNetCombined. Every step teacher-forced (from the reference's previous
-    sample) <= 1e-4; free-running, every step <= max(1e-4, 1.5 x the reference's own fp32-vs-fp64
-    drift at that step): the reference itself drifts 1.6e-4 from its float64 evaluation on this
-    trajectory (x0 = sqrt(1/a_t) x - ... with sqrt(1/a_t) ~ 160 at t = 996, times the (2s - 1) CFG
-    gain; tests/golden/drift.npz cfg6, make_golden_r2.py)."""
-    from tests.conftest import drift_bound
-    drift = golden('drift')[0]['cfg6_drift_sample']
+    sample) <= 1e-4; free-running, tests/conftest.py check_free_running: the reference's own fp32 run
+    drifts 1.6e-4 from its float64 run on this trajectory (x0 = sqrt(1/a_t) x - ... with
+    sqrt(1/a_t) ~ 160 at t = 996, times the (2s - 1) CFG gain; tests/golden/drift.npz cfg6)."""
+    from tests.conftest import check_free_running
+    dg = golden('drift')[0]
+    drift = dg['cfg6_drift_sample']
     g, meta = golden('adm')
     model = UNetCombined(**meta['archs']['adm_tiny']).eval()
     assert init_synthetic_(model) == meta['combined_tiny_weights_sha256']
@@ -136,12 +136,13 @@ def test_adm_combined_ddimcfg_trajectory(cuda, golden, report):
         worst_step = max(worst_step, err)
         assert err <= TOL, (i, err)
     report('adm_combined_ddimcfg6_single_step_maxabs_vs_reference', worst_step)
-    worst = 0.0
+    worst, worst64 = 0.0, 0.0
     for i, out in enumerate(d.sample_loop(model, init, model_kwargs=dict(y=labels))):
-        err = float(np.abs(out['sample'].cpu().numpy() - g[f'cfg6_step{i}_sample']).max())
-        worst = max(worst, err)
-        assert err <= drift_bound(drift[i]), (i, err, drift[i])
+        e32, e64 = check_free_running(out['sample'].cpu().numpy(), g[f'cfg6_step{i}_sample'],
+                                      dg['cfg6_sample64'][i], drift, i)
+        worst, worst64 = max(worst, e32), max(worst64, e64)
     report('adm_combined_ddimcfg6_free_running_maxabs_vs_reference', worst)
+    report('adm_combined_ddimcfg6_free_running_maxabs_vs_reference_float64', worst64)
     report('adm_combined_ddimcfg6_reference_fp32_vs_fp64_drift', float(drift.max()))
 
 
@@ -150,10 +151,10 @@ def test_adm_combined_ddpmcfg_learned_range_trajectory(cuda, golden, report):
     """DDPMCFG-8 (s = 2.5) with var_type learned_range through UNetCombined (two weight sets, two calls
     per step, reference diffusions/ddpm.py:319-351): eps halves combined, the CONDITIONAL branch's
     variance channels concatenated (:344-345), learned-range variance (:240-246), noise pinned per
-    step. Free-running, every step <= max(1e-4, 1.5 x the reference's fp32-vs-fp64 drift)
-    (tests/golden/ddpmcfg.npz)."""
+    step (tests/golden/ddpmcfg.npz). Every step teacher-forced (from the reference's previous sample):
+    sample and pred_eps <= 1e-4; free-running: tests/conftest.py check_free_running on the sample."""
     from diffusions import DDPMCFG
-    from tests.conftest import drift_bound
+    from tests.conftest import check_free_running
     from tests.golden.noise import StepNoise
     g, meta = golden('ddpmcfg')
     model = UNetCombined(**golden('adm')[1]['archs']['adm_tiny']).eval()
@@ -162,17 +163,32 @@ def test_adm_combined_ddpmcfg_learned_range_trajectory(cuda, golden, report):
     c = meta['adm']
     d = DDPMCFG(guidance_scale=c['guidance_scale'], var_type=c['var_type'], respace_type=c['respace_type'],
                 respace_steps=c['respace_steps'], device=cuda)
+    labels = torch.from_numpy(g['adm_labels']).to(cuda)
+    seq = d.respaced_seq.tolist()
+    worst_step = 0.0
+    for i, (t, tp) in enumerate(zip(reversed(seq), reversed([-1] + seq[:-1]))):
+        x = torch.from_numpy(g['adm_init'] if i == 0 else g[f'adm_step{i - 1}_sample']).to(cuda)
+        src = StepNoise(c['noise_seed'])
+        src.k = i   # the i-th draw of the trajectory
+        d.noise_fn = src
+        tb = torch.full((2, ), t, dtype=torch.long, device=cuda)
+        out = d._step(model(x, tb, labels), x, t, tp, model_output_uncond=model(x, tb, None),
+                      guidance_scale=d.guidance_scale)
+        for k in ('sample', 'pred_eps'):
+            err = float(np.abs(out[k].cpu().numpy() - g[f'adm_step{i}_{k}']).max())
+            worst_step = max(worst_step, err)
+            assert err <= TOL, (i, k, err)
     src = StepNoise(c['noise_seed'])
     d.noise_fn = src
     worst = 0.0
     for i, out in enumerate(d.sample_loop(model, torch.from_numpy(g['adm_init']).to(cuda),
-                                          model_kwargs=dict(y=torch.from_numpy(g['adm_labels']).to(cuda)))):
-        for k in ('sample', 'pred_eps'):
-            err = float(np.abs(out[k].cpu().numpy() - g[f'adm_step{i}_{k}']).max())
-            worst = max(worst, err)
-            assert err <= drift_bound(g['adm_drift_sample'][i]), (i, k, err)
-    assert i + 1 == len(d.respaced_seq) and src.k == i + 1
-    report('adm_combined_ddpmcfg8_learned_range_maxabs_vs_reference', worst)
+                                          model_kwargs=dict(y=labels))):
+        e32, _ = check_free_running(out['sample'].cpu().numpy(), g[f'adm_step{i}_sample'], g['adm_sample64'][i],
+                                    g['adm_drift_sample'], i)
+        worst = max(worst, e32)
+    assert i + 1 == len(seq) and src.k == i + 1
+    report('adm_combined_ddpmcfg8_learned_range_single_step_maxabs_vs_reference', worst_step)
+    report('adm_combined_ddpmcfg8_learned_range_free_running_maxabs_vs_reference', worst)
 
 
 @pytest.mark.gpu

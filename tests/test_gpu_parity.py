@@ -163,27 +163,40 @@ def test_ddpm1000_cifar_trajectory(cuda, golden, report):
     """BASELINE config C2's path: the CIFAR-10 UNet through DDPM fixed_large, all 1000 steps (reference
     diffusions/ddpm.py:205-281), B=2, free-running from the reference's init noise with the per-step noise
     pinned (tests/golden/noise.py StepNoise, the same draws the reference consumed when
-    make_golden_r2.py ran it). 31 steps from t = 999 to t = 0 are checked: sample and pred_eps
-    <= max(1e-4, 1.5 x the reference's fp32-vs-fp64 drift at that step)."""
-    from tests.conftest import drift_bound
+    make_golden_r2.py ran it). At 30 steps from t = 999 to t = 0: teacher-forced (from the reference's
+    previous sample, with that step's noise draw) sample and pred_eps <= 1e-4; free-running, the sample
+    with tests/conftest.py check_free_running (fp32 and float64 reference runs)."""
+    from tests.conftest import check_free_running
     from tests.golden.noise import StepNoise
     g, meta = golden('ddpm1000')
     model, sha = _model(golden('forward')[1], 'cifar10', cuda)
     assert sha == meta['cifar10_weights_sha256']
     d = DDPM(var_type='fixed_large', device=cuda)
+    keep = meta['keep']
+    worst_step = 0.0
+    for i in keep:
+        t = 999 - i
+        x = torch.from_numpy(g['init'] if i == 0 else g[f'step{i - 1}_sample']).to(cuda)
+        src = StepNoise(meta['noise_seed'])
+        src.k = i
+        d.noise_fn = src
+        out = d.denoise(model(x, torch.full((2, ), t, dtype=torch.long, device=cuda)), x, t, t - 1)
+        for k in ('sample', 'pred_eps'):
+            err = float(np.abs(out[k].cpu().numpy() - g[f'step{i}_{k}']).max())
+            worst_step = max(worst_step, err)
+            assert err <= TOL, (i, k, err)
     src = StepNoise(meta['noise_seed'])
     d.noise_fn = src
-    keep = set(meta['keep'])
     worst = 0.0
     for i, out in enumerate(d.sample_loop(model, torch.from_numpy(g['init']).to(cuda),
                                           tqdm_kwargs=dict(disable=True))):
         if i in keep:
-            for k in ('sample', 'pred_eps'):
-                err = float(np.abs(out[k].cpu().numpy() - g[f'step{i}_{k}']).max())
-                worst = max(worst, err)
-                assert err <= drift_bound(g[f'drift_{k}'][i]), (i, k, err)
+            e32, _ = check_free_running(out['sample'].cpu().numpy(), g[f'step{i}_sample'], g[f'step{i}_sample64'],
+                                        g['drift_sample'], i)
+            worst = max(worst, e32)
     assert i == 999 and src.k == 1000
-    report('ddpm1000_cifar_B2_worst_kept_step_maxabs_vs_reference', worst)
+    report('ddpm1000_cifar_B2_single_step_maxabs_vs_reference', worst_step)
+    report('ddpm1000_cifar_B2_free_running_worst_kept_step_maxabs_vs_reference', worst)
     report('ddpm1000_cifar_B2_reference_fp32_vs_fp64_drift', float(g['drift_sample'].max()))
 
 

@@ -82,12 +82,13 @@ def test_sample_uncond_script(cuda, tmp_path, sampler, mode):
 def test_ddim_inversion_reconstruction_trajectory(cuda, golden, report):
     """DDIM.sample_inversion_loop then sample_loop on the engine vs the reference (ddim.py:88-132,
     sample_uncond.py:297-304; tests/golden/inversion.npz). Every step teacher-forced from the reference's
-    previous sample <= 1e-4; free-running (inversion feeding reconstruction) every step <= max(1e-4, 1.5 x
-    the reference's own fp32-vs-fp64 drift at that step): x0 = sqrt(1/ac_t) x - ... amplifies a 1e-6
-    forward difference by up to ~160 at t ~ 960 and the reference itself drifts 3e-4 from its float64
-    evaluation here (tests/golden/drift.npz invrec, make_golden_r2.py)."""
-    from tests.conftest import drift_bound
-    drift = golden('drift')[0]['invrec_drift_sample']
+    previous sample <= 1e-4; free-running (inversion feeding reconstruction): tests/conftest.py
+    check_free_running. x0 = sqrt(1/ac_t) x - ... amplifies a 1e-6 forward difference by up to ~160 at
+    t ~ 960 and the reference's own fp32 run drifts 3e-4 from its float64 run here
+    (tests/golden/drift.npz invrec, make_golden_r2.py)."""
+    from tests.conftest import check_free_running
+    dg = golden('drift')[0]
+    drift = dg['invrec_drift_sample']
     from diffusions import DDIM
     arrays, meta = golden('inversion')
     model, sha = _model(golden('forward')[1], 'tiny', cuda)
@@ -113,15 +114,15 @@ def test_ddim_inversion_reconstruction_trajectory(cuda, golden, report):
     free = 0.0
     x = ref('img')
     for i, out in enumerate(d.sample_inversion_loop(model, x, tqdm_kwargs=dict(disable=True))):
-        err = np.abs(out['sample'].cpu().numpy() - arrays[f'inv_step{i}_sample']).max()
-        assert err <= drift_bound(drift[i]), ('inv', i, err, drift[i])
+        err, _ = check_free_running(out['sample'].cpu().numpy(), arrays[f'inv_step{i}_sample'],
+                                    dg['invrec_sample64'][i], drift, i)
         free = max(free, err)
         x = out['sample']
     n_inv = i + 1
     assert n_inv == meta['inv_steps']
     for i, out in enumerate(d.sample_loop(model, x, tqdm_kwargs=dict(disable=True))):
-        err = np.abs(out['sample'].cpu().numpy() - arrays[f'rec_step{i}_sample']).max()
-        assert err <= drift_bound(drift[n_inv + i]), ('rec', i, err, drift[n_inv + i])
+        err, _ = check_free_running(out['sample'].cpu().numpy(), arrays[f'rec_step{i}_sample'],
+                                    dg['invrec_sample64'][n_inv + i], drift, n_inv + i)
         free = max(free, err)
     report('ddim_inversion_reconstruction_tiny_teacher_forced_maxabs_vs_reference', forced)
     report('ddim_inversion_reconstruction_tiny_free_running_maxabs_vs_reference', free)
