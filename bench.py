@@ -68,9 +68,10 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(label):
-    """HBM bytes per launch of `label` from the newest committed PMC summary (profiles/rNN_vM_pmc.json,
-    FETCH_SIZE x2 + WRITE_SIZE passes of this bench, tools/gpu_profile.sh)."""
+def pmc_traffic(label, workload='c3'):
+    """HBM bytes per launch of `label` from the newest committed PMC summary of this workload
+    (profiles/rNN_vM_pmc.json, FETCH_SIZE x2 + WRITE_SIZE passes of this bench, tools/gpu_profile.sh;
+    summaries without a "workload" field are of the default c3 run)."""
     import glob
     import re
 
@@ -80,7 +81,10 @@ def pmc_traffic(label):
     files = sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*_v*_pmc.json')), key=order)
     for path in reversed(files):
         with open(path) as f:
-            k = json.load(f).get('kernels', {}).get(label)
+            summary = json.load(f)
+        if summary.get('workload', 'c3') != workload:
+            continue
+        k = summary.get('kernels', {}).get(label)
         if k and k.get('hbm_bytes_per_launch'):
             return float(k['hbm_bytes_per_launch']), os.path.relpath(path, ROOT)
     return None, None
@@ -141,7 +145,7 @@ def cpu_baseline(sd, batch, n_steps, timed_steps=3):
                        f'{os.cpu_count()} logical CPUs on the host); {dt:.2f} s per step, extrapolated x{n_steps}')
 
 
-def roofline(prof):
+def roofline(prof, workload='c3'):
     """Roofline of the dominant kernel family (most GPU time in the timed region)."""
     fam = {}
     for op in prof:
@@ -174,7 +178,7 @@ def roofline(prof):
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
         roof = dict(bound='hbm', achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit='GB/s',
                     frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None)
-    traffic, traffic_src = pmc_traffic(dom_name)
+    traffic, traffic_src = pmc_traffic(dom_name, workload)
     roof.update(traffic=traffic, traffic_source=traffic_src, algorithmic_bytes_per_launch=bytes_per_launch,
                 kernel=dom_name, avg_launch_ms=round(avg_ms, 4), launches=dom['launches'],
                 algorithmic_per_launch=flops_per_launch if flops_per_launch > 0 else bytes_per_launch)
@@ -353,7 +357,7 @@ def main():
 
     roof, total_gpu_ms, total_flops, fam = None, 0.0, 0.0, {}
     if not args.no_profile:
-        roof, total_gpu_ms, total_flops, fam = roofline(prof)
+        roof, total_gpu_ms, total_flops, fam = roofline(prof, args.workload)
 
     if rank == 0:
         images = world * B * args.steps
