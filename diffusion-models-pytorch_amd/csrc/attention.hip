@@ -1,0 +1,446 @@
+// Fused self-attention core for 16 x 16 maps (L = 256 tokens): S = (alpha q) (b_scale k)^T, row softmax,
+// O = P v, in one kernel, S never leaving the CU.
+//
+// Reference: models/modules.py:89-102 (SelfAttentionBlock: q * scale, bmm(q^T, k), softmax(-1),
+// bmm(v, attn^T)), models/adm/unet.py:347-408 (QKVAttention[Legacy]: q, k each * ch^-1/4, softmax in
+// fp32). The unfused path (gemm.hip S GEMM, softmax_rows, PV GEMM) writes S (B x heads x L x L fp32)
+// to HBM, reads and rewrites it for the softmax and reads it again for PV: 4 x 67 MB per CIFAR block
+// at B = 256. Here one block owns 32 (head dim 256) or 64 (head dim 64) query rows of one (image, head):
+//   1. S [QT x L]: q rows and k rows staged through LDS as fp16x2 pieces (the split GEMM's operand
+//      format and exponents, split16.h), 4 waves x (QT rows x L/4 keys), 3 MFMAs per 16-deep slice;
+//   2. S -> LDS (fp32 rows), softmax per row exactly as softmax_rows (elementwise.hip): the same
+//      per-lane max / expf / sum order and the same v * (1 / sum), so P is bit-identical; P is split
+//      (x 2^14) in place into the A-operand layout of step 3;
+//   3. O [QT x Dh] = P v: v rows staged transposed ([d][key], KN4 loader of gemm.hip), waves over
+//      output columns (Dh = 256: 64 columns each; Dh = 64: 2 x 2 waves of 32 x 32).
+// The operand tiles of both contractions are prefetched two k steps ahead into registers.
+// Every contraction runs the same MFMA sequence in the same k order as the unfused GEMMs, so the
+// output equals the unfused path bit for bit (tests/test_gpu_parity.py test_fused_attention_bit_identical).
+// LDS (head dim 256, 32 query rows per block): 41 KB staging + 37 KB S / P rows -> two blocks per CU.
+#include "dm_common.h"
+#include "dm_kernels.h"
+#include "mfma_tile.h"
+#include "split16.h"
+
+namespace dm {
+
+namespace {
+
+constexpr int kAL = 256;             // tokens
+constexpr int kAK = 32;              // k per staged tile
+constexpr int kAP = 72;              // fp16 pitch of a staged 32-k row (two 16-deep slices + pad: 144 B)
+constexpr int kSP = 8 * kAP / 2;     // fp32 pitch of an S row = one P row of 8 key blocks (1152 B)
+
+__device__ __forceinline__ int split_off(int k) { return (k >> 4) * 32 + ((k >> 3) & 1) * 16 + (k & 7); }
+
+// QT query rows per block: 32 for DH = 256 (78 KB of LDS: two blocks per CU), 64 for DH = 64 (the PV
+// wave layout needs 64 rows there). Operand tiles are prefetched two k steps ahead into registers.
+template <int DH, int QT>
+__global__ void __launch_bounds__(256) attn_fused_kernel(AttnArgs a) {
+  static_assert((DH == 256 && QT == 32) || (DH == 64 && QT == 64), "head dims 64 / 256");
+  constexpr int kAQ = QT;
+  constexpr int STAGE_H = (kAQ + kAL) * kAP;      // Q + K tiles (fp16 elements)
+  constexpr int VSTAGE_H = DH * kAP;              // V^T tile
+  constexpr int REGION_H = STAGE_H > VSTAGE_H ? STAGE_H : VSTAGE_H;
+  __shared__ __attribute__((aligned(16))) _Float16 stg[REGION_H];
+  __shared__ __attribute__((aligned(16))) float sp[kAQ * kSP];
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int lr = lane & 31, lh = lane >> 5;
+  // block -> (image, head, query tile); consecutive blocks of one (image, head) share its k / v in L2
+  const int nq = kAL / kAQ;
+  const int bid = xcd_remap_p(blockIdx.x, gridDim.x);
+  const int qt = bid % nq, bh = bid / nq;
+  const int h = bh % a.heads, b = bh / a.heads;
+  const float* rows = a.qkv + (size_t)b * kAL * a.ld;
+  const float* qsrc = rows + (size_t)qt * kAQ * a.ld + a.q0 + h * a.hs;
+  const float* ksrc = rows + a.k0 + h * a.hs;
+  const float* vsrc = rows + a.v0 + h * a.hs;
+  const float pa = ldexpf(1.f, a.ea), pb = ldexpf(1.f, a.eb), pp = ldexpf(1.f, a.ep), pv = ldexpf(1.f, a.ev);
+  bool bad = false;
+
+  // ---------------------------------------------------------------- 1. S = (alpha q)(b_scale k)^T
+  const int lc4 = t & 7, lrow = t >> 3;   // loader: 8 threads per 32-k row, 32 rows per pass
+  f4 rq[2][kAQ / 32], rk[2][kAL / 32];    // two register sets: tiles kt and kt + 1 in flight
+  auto load_s = [&](int kt, int set) {
+    const int k = kt * kAK + 4 * lc4;
+#pragma unroll
+    for (int i = 0; i < kAQ / 32; ++i)
+      rq[set][i] = *reinterpret_cast<const f4*>(qsrc + (size_t)(lrow + 32 * i) * a.ld + k);
+#pragma unroll
+    for (int i = 0; i < kAL / 32; ++i)
+      rk[set][i] = *reinterpret_cast<const f4*>(ksrc + (size_t)(lrow + 32 * i) * a.ld + k);
+  };
+  auto store_s = [&](int set) {
+#pragma unroll
+    for (int i = 0; i < kAQ / 32; ++i) {
+      f4 v = rq[set][i];
+      if (a.alpha != 1.0f) v = v * a.alpha;
+      f16x4 hi, lo;
+      Split<2>::split4(v * pa, hi, lo, bad);
+      _Float16* dst = stg + (lrow + 32 * i) * kAP + split_off(4 * lc4);
+      *reinterpret_cast<f16x4*>(dst) = hi;
+      *reinterpret_cast<f16x4*>(dst + 8) = lo;
+    }
+#pragma unroll
+    for (int i = 0; i < kAL / 32; ++i) {
+      const f4 v = (a.b_scale != 0.0f && a.b_scale != 1.0f) ? rk[set][i] * a.b_scale : rk[set][i];
+      f16x4 hi, lo;
+      Split<2>::split4(v * pb, hi, lo, bad);
+      _Float16* dst = stg + (kAQ + lrow + 32 * i) * kAP + split_off(4 * lc4);
+      *reinterpret_cast<f16x4*>(dst) = hi;
+      *reinterpret_cast<f16x4*>(dst + 8) = lo;
+    }
+  };
+  constexpr int SM = kAQ / 32;   // 32-row tiles of S per wave
+  f16v acc[SM][2];
+#pragma unroll
+  for (int i = 0; i < SM; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  // wave w: all query rows of the tile, keys 64 w .. 64 w + 63 (2 x 32)
+  constexpr int nkt = DH / kAK;   // even
+  auto s_step = [&](int kt, int set) {
+    store_s(set);
+    __syncthreads();
+    if (kt + 2 < nkt) load_s(kt + 2, set);
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) {
+      f16x8 av[SM][2], bv[2][2];
+#pragma unroll
+      for (int i = 0; i < SM; ++i)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          av[i][q] = *reinterpret_cast<const f16x8*>(stg + (i * 32 + lr) * kAP + sl * 32 + lh * 16 + q * 8);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          bv[j][q] = *reinterpret_cast<const f16x8*>(stg + (kAQ + wave * 64 + j * 32 + lr) * kAP + sl * 32 + lh * 16 +
+                                                     q * 8);
+#pragma unroll
+      for (int i = 0; i < SM; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) Split<2>::mma(av[i], bv[j], acc[i][j]);
+    }
+    __syncthreads();
+  };
+  load_s(0, 0);
+  load_s(1, 1);
+  for (int kt = 0; kt < nkt; kt += 2) {
+    s_step(kt, 0);
+    s_step(kt + 1, 1);
+  }
+  // S rows to LDS (fp32, exact unscale)
+  {
+    const float unscale = ldexpf(1.f, -(a.ea + a.eb));
+#pragma unroll
+    for (int i = 0; i < SM; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          sp[(i * 32 + acc_row(r, lh)) * kSP + wave * 64 + j * 32 + lr] = acc[i][j][r] * unscale;
+  }
+  __syncthreads();
+
+  // ---------------------------------------------------------------- 2. softmax rows -> P pieces in place
+  for (int row = wave * (kAQ / 4); row < (wave + 1) * (kAQ / 4); ++row) {
+    float* srow = sp + row * kSP;
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = u < 4 ? srow[lane + 64 * u] : -INFINITY;   // softmax_rows' 8 slots
+    float mx = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) mx = fmaxf(mx, v[u]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    float sum = 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      v[u] = expf(v[u] - mx);
+      sum += v[u];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+    const float inv = 1.0f / sum;
+    _Float16* prow = reinterpret_cast<_Float16*>(srow);   // P row: 8 key blocks x kAP fp16 (same bytes)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = lane + 64 * u;
+      const float x = (v[u] * inv) * pp;
+      const _Float16 h0 = (_Float16)x;
+      _Float16* dst = prow + (k >> 5) * kAP + split_off(k & 31);
+      dst[0] = h0;
+      dst[8] = (_Float16)(x - (float)h0);
+    }
+  }
+  __syncthreads();
+
+  // ---------------------------------------------------------------- 3. O = P v
+  // waves: DH = 256: all rows x 64 columns each; DH = 64 (64 rows): 2 x 2 waves of 32 x 32
+  constexpr int TM = DH == 256 ? kAQ / 32 : 1, TN = DH == 256 ? 2 : 1;
+  const int orow0 = DH == 256 ? 0 : (wave >> 1) * 32;
+  const int ocol0 = DH == 256 ? wave * 64 : (wave & 1) * 32;
+  f16v oacc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) oacc[i][j][r] = 0.f;
+  // V tile loader (gemm.hip KN4): thread -> 4 keys (4 kq ..) x 4 columns (4 n4 ..), stored transposed
+  constexpr int NB = DH / 4 * 8;            // (32 / 4 key quads) x (DH / 4 column quads) blocks
+  constexpr int VB = (NB + 255) / 256;       // blocks per thread
+  f4 rv[2][VB][4];
+  auto load_v = [&](int kb, int set) {
+#pragma unroll
+    for (int p = 0; p < VB; ++p) {
+      const int blk = min(t + 256 * p, NB - 1);
+      const int kq = blk & 7, n4 = blk >> 3;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        rv[set][p][r] = *reinterpret_cast<const f4*>(vsrc + (size_t)(kb * kAK + 4 * kq + r) * a.ld + 4 * n4);
+    }
+  };
+  auto store_v = [&](int set) {
+#pragma unroll
+    for (int p = 0; p < VB; ++p) {
+      const int blk = t + 256 * p;
+      if (blk >= NB) continue;
+      const int kq = blk & 7, n4 = blk >> 3;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f4 col = {rv[set][p][0][q], rv[set][p][1][q], rv[set][p][2][q], rv[set][p][3][q]};
+        f16x4 hi, lo;
+        Split<2>::split4(col * pv, hi, lo, bad);
+        _Float16* dst = stg + (4 * n4 + q) * kAP + split_off(4 * kq);
+        *reinterpret_cast<f16x4*>(dst) = hi;
+        *reinterpret_cast<f16x4*>(dst + 8) = lo;
+      }
+    }
+  };
+  const _Float16* P = reinterpret_cast<const _Float16*>(sp);
+  constexpr int PPITCH = 2 * kSP;  // fp16 elements per P row
+  constexpr int nkb = kAL / kAK;   // even
+  auto pv_step = [&](int kb, int set) {
+    store_v(set);
+    __syncthreads();
+    if (kb + 2 < nkb) load_v(kb + 2, set);
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) {
+      f16x8 av[TM][2], bv[TN][2];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          av[i][q] = *reinterpret_cast<const f16x8*>(P + (orow0 + i * 32 + lr) * PPITCH + kb * kAP + sl * 32 + lh * 16 +
+                                                     q * 8);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          bv[j][q] = *reinterpret_cast<const f16x8*>(stg + (ocol0 + j * 32 + lr) * kAP + sl * 32 + lh * 16 + q * 8);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) Split<2>::mma(av[i], bv[j], oacc[i][j]);
+    }
+    __syncthreads();
+  };
+  load_v(0, 0);
+  load_v(1, 1);
+  for (int kb = 0; kb < nkb; kb += 2) {
+    pv_step(kb, 0);
+    pv_step(kb + 1, 1);
+  }
+  if (bad && a.range_flag) *a.range_flag = 1;
+  const float ounscale = ldexpf(1.f, -(a.ep + a.ev));
+  float* out = a.out + ((size_t)b * kAL + qt * kAQ) * a.ldo + h * DH;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        out[(size_t)(orow0 + i * 32 + acc_row(r, lh)) * a.ldo + ocol0 + j * 32 + lr] = oacc[i][j][r] * ounscale;
+}
+
+// Pre-split operands (AttnArgs::pq / pk / pv, written by the qkv conv's epilogue, conv_epilogue.h): every
+// MFMA operand fragment is one 16-B load from global (L2) per lane and piece, no LDS staging and no split
+// on the VALU. 64 query rows per block (74 KB of LDS for the S / P rows: two blocks per CU); q, k and
+// v^T slices ride a register ring RD slices ahead of their use. Same MFMA sequence as the unfused GEMMs.
+template <int DH>
+__global__ void __launch_bounds__(256) attn_presplit_kernel(AttnArgs a) {
+  static_assert(DH == 64 || DH == 256, "head dims 64 / 256");
+  constexpr int QT = 64, NS = DH / 16, RD = 4;
+  __shared__ __attribute__((aligned(16))) float sp[QT * kSP];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int nq = kAL / QT;
+  const int bid = xcd_remap_p(blockIdx.x, gridDim.x);
+  const int qt = bid % nq, bh = bid / nq;
+  const size_t plane = (size_t)kAL * DH;
+  const _Float16* Q = a.pq + (size_t)bh * 2 * plane + (size_t)(qt * QT) * DH;
+  const _Float16* K = a.pk + (size_t)bh * 2 * plane;
+  const _Float16* V = a.pv + (size_t)bh * 2 * plane;
+
+  // ---------------------------------------------------------------- 1. S: wave w = 64 rows x keys 64 w ..
+  f16x8 ra[RD][2][2], rb[RD][2][2];   // [slot][tile][piece]
+  auto load_s = [&](int s, int slot) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        ra[slot][i][q] = *reinterpret_cast<const f16x8*>(Q + q * plane + (size_t)(i * 32 + lr) * DH + 16 * s + 8 * lh);
+        rb[slot][i][q] =
+            *reinterpret_cast<const f16x8*>(K + q * plane + (size_t)(wave * 64 + i * 32 + lr) * DH + 16 * s + 8 * lh);
+      }
+  };
+  f16v acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+#pragma unroll
+  for (int s = 0; s < RD; ++s) load_s(min(s, NS - 1), s);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int slot = s % RD;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) Split<2>::mma(ra[slot][i], rb[slot][j], acc[i][j]);
+    load_s(min(s + RD, NS - 1), slot);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  {
+    const float unscale = ldexpf(1.f, -(a.ea + a.eb));
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          sp[(i * 32 + acc_row(r, lh)) * kSP + wave * 64 + j * 32 + lr] = acc[i][j][r] * unscale;
+  }
+  __syncthreads();
+
+  // ---------------------------------------------------------------- 2. softmax rows -> P pieces in place
+  const float pp = ldexpf(1.f, a.ep);
+  for (int row = wave * (QT / 4); row < (wave + 1) * (QT / 4); ++row) {
+    float* srow = sp + row * kSP;
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = u < 4 ? srow[lane + 64 * u] : -INFINITY;   // softmax_rows' 8 slots
+    float mx = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) mx = fmaxf(mx, v[u]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    float sum = 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      v[u] = expf(v[u] - mx);
+      sum += v[u];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+    const float inv = 1.0f / sum;
+    _Float16* prow = reinterpret_cast<_Float16*>(srow);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = lane + 64 * u;
+      const float x = (v[u] * inv) * pp;
+      const _Float16 h0 = (_Float16)x;
+      _Float16* dst = prow + (k >> 5) * kAP + split_off(k & 31);
+      dst[0] = h0;
+      dst[8] = (_Float16)(x - (float)h0);
+    }
+  }
+  __syncthreads();
+
+  // ---------------------------------------------------------------- 3. O = P v
+  constexpr int TM = DH == 256 ? 2 : 1, TN = DH == 256 ? 2 : 1, NK = kAL / 16;
+  const int orow0 = DH == 256 ? 0 : (wave >> 1) * 32;
+  const int ocol0 = DH == 256 ? wave * 64 : (wave & 1) * 32;
+  const _Float16* P = reinterpret_cast<const _Float16*>(sp);
+  constexpr int PPITCH = 2 * kSP;
+  f16x8 rv[RD][TN][2];
+  auto load_v = [&](int s, int slot) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        rv[slot][j][q] =
+            *reinterpret_cast<const f16x8*>(V + q * plane + (size_t)(ocol0 + j * 32 + lr) * kAL + 16 * s + 8 * lh);
+  };
+  f16v oacc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) oacc[i][j][r] = 0.f;
+#pragma unroll
+  for (int s = 0; s < RD; ++s) load_v(s, s);
+#pragma unroll
+  for (int s = 0; s < NK; ++s) {
+    const int slot = s % RD;
+    f16x8 av[TM][2];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        av[i][q] = *reinterpret_cast<const f16x8*>(P + (orow0 + i * 32 + lr) * PPITCH + (s >> 1) * kAP + (s & 1) * 32 +
+                                                   lh * 16 + q * 8);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) Split<2>::mma(av[i], rv[slot][j], oacc[i][j]);
+    load_v(min(s + RD, NK - 1), slot);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  const float ounscale = ldexpf(1.f, -(a.ep + a.ev));
+  const int h = bh % a.heads, b = bh / a.heads;
+  float* out = a.out + ((size_t)b * kAL + qt * QT) * a.ldo + h * DH;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        out[(size_t)(orow0 + i * 32 + acc_row(r, lh)) * a.ldo + ocol0 + j * 32 + lr] = oacc[i][j][r] * ounscale;
+}
+
+}  // namespace
+
+bool attn_fused_ok(int L, int Dh) { return L == kAL && (Dh == 64 || Dh == 256); }
+
+int attn_fused(const AttnArgs& a, hipStream_t st) {
+  DM_REQUIRE(attn_fused_ok(a.L, a.Dh), "fused attention: L must be 256 and the head dim 64 or 256");
+  DM_REQUIRE((a.qkv || a.pq) && a.out && a.B > 0 && a.heads > 0 && a.ld % 4 == 0 && a.ldo % 4 == 0 &&
+             (a.q0 + 0) % 4 == 0 && a.k0 % 4 == 0 && a.v0 % 4 == 0 && a.hs % 4 == 0,
+             "fused attention: operands must be float4-aligned rows");
+  if (a.pq) {
+    DM_REQUIRE(a.pk && a.pv, "fused attention: all three operand planes");
+    if (a.Dh == 256)
+      hipLaunchKernelGGL(attn_presplit_kernel<256>, dim3(a.B * a.heads * (kAL / 64)), dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL(attn_presplit_kernel<64>, dim3(a.B * a.heads * (kAL / 64)), dim3(256), 0, st, a);
+    DM_LAUNCH_CHECK();
+    return DM_OK;
+  }
+  if (a.Dh == 256)
+    hipLaunchKernelGGL((attn_fused_kernel<256, 32>), dim3(a.B * a.heads * (kAL / 32)), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((attn_fused_kernel<64, 64>), dim3(a.B * a.heads * (kAL / 64)), dim3(256), 0, st, a);
+  DM_LAUNCH_CHECK();
+  return DM_OK;
+}
+
+}  // namespace dm

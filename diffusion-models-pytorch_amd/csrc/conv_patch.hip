@@ -446,6 +446,12 @@ int conv_patch_pick(const ConvArgs& a, PatchGeom& g) {
     if (!(a.ws && a.ws_np == 2) || (a.tile != 0 && a.tile != 6)) return 0;
     return conv_patch_geom(a, 64, g) && g.P <= kPatchS2Max ? 6 : 0;
   }
+  // big-tile fp16x2 split kernels (one wave per SIMD): forced by tile 7 / 8 only (for now)
+  if (a.tile == 7 || a.tile == 8) {
+    if (!(a.ws && a.ws_np == 2)) return 0;
+    if (a.tile == 7) return conv_patch_geom(a, 256, g) && g.P <= kPatch3Max256 ? 7 : 0;
+    return conv_patch_geom(a, 512, g) && g.P <= kPatch3Max512 ? 8 : 0;
+  }
   // the split-bf16 kernel's LDS image holds fewer patch pixels at 128-row tiles
   const int max128 = a.ws ? kPatch3Max128 : kPatchMax128, max64 = a.ws ? kPatch3Max64 : kPatchMax64;
   if (a.tile == 4 || a.tile == 0) {

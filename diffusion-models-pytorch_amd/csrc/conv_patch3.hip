@@ -57,6 +57,94 @@ constexpr int kPwSlices = 2;        // MODE 3: 16-channel slices per chunk (32 c
 constexpr int kPwTabFloats = 10240;  // GroupNorm table capacity (40 KiB) of the LDS-staged prologue tables
 constexpr int kGinStats = 512;       // (image, group) pairs of the in-kernel GroupNorm finalize
 
+// MODE 3 qkv conv feeding the fused attention (attention.hip): this wave's WM x WN tile of y = acc * rowscale
+// + bias goes to its own LDS region (fp32, pitch WN + 8), then each lane takes 8 consecutive columns of
+// a row (q, k: [L][Dh] planes) or 8 consecutive rows of a column (v: [Dh][L] planes), scales and splits
+// them exactly as conv_store_attn_planes / the attention GEMMs' loaders, and stores 16-B pieces.
+template <int WM, int WN>
+__device__ __forceinline__ void attn_plane_epilogue(const ConvArgs& a, f16v (&acc)[WM / 32][WN / 32], int M,
+                                                    int wm0, int wn0, int lr, int lh, float* wl) {
+  constexpr int TM = WM / 32, TN = WN / 32, PITCH = WN + 8;
+  const int N = a.Cout, lane = lr + 32 * lh;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = min(wn0 + j * 32 + lr, N - 1);
+    const float cs = a.ws_rowscale[n], bn = a.bias ? a.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float v = acc[i][j][r] * cs;
+        if (a.bias) v = v + bn;
+        wl[(i * 32 + acc_row(r, lh)) * PITCH + j * 32 + lr] = v;
+      }
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes are visible to its reads
+  __builtin_amdgcn_wave_barrier();
+  if (wn0 >= N) return;
+  // the wave's columns lie in one of q / k / v (3C, C and Dh are multiples of 32) and in one head
+  const int Dh = a.ap_Dh, C = a.ap_heads * Dh;
+  int part, h, d0;
+  if (a.ap_legacy) {
+    h = wn0 / (3 * Dh);
+    part = (wn0 - h * 3 * Dh) / Dh;
+    d0 = wn0 - h * 3 * Dh - part * Dh;
+  } else {
+    part = wn0 / C;
+    h = (wn0 - part * C) / Dh;
+    d0 = wn0 - part * C - h * Dh;
+  }
+  const float scale = part == 0 ? a.ap_alpha : part == 1 ? a.ap_bscale : 1.f;
+  const bool use_scale = part == 0 ? a.ap_alpha != 1.0f : part == 1 && a.ap_bscale != 0.0f && a.ap_bscale != 1.0f;
+  const float pw = ldexpf(1.f, part == 0 ? a.ap_ea : part == 1 ? a.ap_eb : a.ap_ev);
+  const size_t plane = (size_t)a.ap_L * Dh;
+  bool bad = false;
+  auto split8 = [&](const float (&x)[8], f16x8& hi, f16x8& lo) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float y = (use_scale ? x[e] * scale : x[e]) * pw;
+      const _Float16 h0 = (_Float16)y;
+      hi[e] = h0;
+      lo[e] = (_Float16)(y - (float)h0);
+      bad |= fabsf(y) > 65504.f;
+    }
+  };
+  if (part < 2) {  // q / k planes [b][h][piece][token][d]: 8 consecutive d of one token per lane
+    _Float16* dst = part == 0 ? a.ap_q : a.ap_k;
+    constexpr int G = WN / 8;
+    for (int g = lane; g < WM * G; g += 64) {
+      const int row = g / G, c8 = g - row * G;
+      const int m = wm0 + row;
+      if (m >= M) continue;
+      const f4 x0 = *reinterpret_cast<const f4*>(wl + row * PITCH + 8 * c8);
+      const f4 x1 = *reinterpret_cast<const f4*>(wl + row * PITCH + 8 * c8 + 4);
+      const float x[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+      f16x8 hi, lo;
+      split8(x, hi, lo);
+      const int b = m / a.ap_L, tok = m - b * a.ap_L;
+      _Float16* p = dst + ((size_t)b * a.ap_heads + h) * 2 * plane + (size_t)tok * Dh + d0 + 8 * c8;
+      *reinterpret_cast<f16x8*>(p) = hi;
+      *reinterpret_cast<f16x8*>(p + plane) = lo;
+    }
+  } else {  // v planes [b][h][piece][d][token]: 8 consecutive tokens of one d per lane
+    for (int g = lane; g < WN * (WM / 8); g += 64) {
+      const int col = g % WN, r8 = g / WN;
+      const int m = wm0 + 8 * r8;   // tokens m .. m + 7 lie in one image (L % 8 == 0)
+      if (m >= M) continue;
+      float x[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = wl[(8 * r8 + e) * PITCH + col];
+      f16x8 hi, lo;
+      split8(x, hi, lo);
+      const int b = m / a.ap_L, tok = m - b * a.ap_L;
+      _Float16* p = a.ap_v + ((size_t)b * a.ap_heads + h) * 2 * plane + (size_t)(d0 + col) * a.ap_L + tok;
+      *reinterpret_cast<f16x8*>(p) = hi;
+      *reinterpret_cast<f16x8*>(p + plane) = lo;
+    }
+  }
+  if (bad && a.range_flag) *a.range_flag = 1;
+}
+
 template <int BM, int BN, int WM, int WN, int MODE, int MAXP, bool PRO, bool KSPLIT = false, int NP = 3>
 __global__ void __launch_bounds__(256)
 conv_patch3_kernel(ConvArgs a, PatchGeom g) {
@@ -85,7 +173,7 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
   // staged in LDS once per block; per-thread global loads of them cost as many VMEM instructions as
   // the activations themselves (and in MODE 3, with no tap reuse, twice the activation bytes)
   constexpr bool LTAB = PRO && (PW1 || NP == 2);
-  constexpr int GTAB = LTAB ? kPwTabFloats : 1;
+  constexpr int GTAB = (LTAB || PW1) ? kPwTabFloats : 1;  // MODE 3: also the plane epilogue's staging
   __shared__ __attribute__((aligned(16))) float gtab[GTAB];
   __shared__ float gstat[LTAB ? 2 * kGinStats : 1];  // in-kernel finalize: (mean, rstd) per (image, group)
 
@@ -167,9 +255,13 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
     wsrc[j] = reinterpret_cast<const elem*>(a.ws) + (size_t)par * nslices * slice_stride + (size_t)grp * (NP * 512) +
               (lh * 32 + lr) * 8;
   }
-  // slices ride a register ring of WD slots, loaded WD taps ahead of their use; WD divides NTAP, so a
-  // tap's slot index is a compile-time constant once the tap loop is unrolled
-  constexpr int WD = NTAP == 9 ? 3 : 2;
+  // slices ride a register ring of WD slots, loaded WD taps ahead of their use. The one-wave-per-SIMD
+  // big tiles (128 x 128 wave tiles: 48 MFMAs per tap already cover the L2 latency) keep 2 slots for
+  // register room. The chunk loop runs CPI chunks per iteration so that a tap's slot index is a
+  // compile-time constant once the loops are unrolled (CPI * NTAP divides by WD).
+  constexpr bool BIG = TM * TN >= 8;
+  constexpr int WD = BIG ? 2 : (NTAP == 9 ? 3 : 2);
+  constexpr int CPI = NTAP % WD == 0 ? 1 : WD;
   vec bq[WD][TN][NP];
   auto load_b = [&](vec (&dst)[TN][NP], int kt) {
 #pragma unroll
@@ -383,11 +475,15 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
   // of chunk c + 1 is loaded at tap 0, GroupNorm+SiLU'd over taps T0 .. NTAP-1, split and stored at
   // the last tap into the other buffer (free: every wave passed the previous chunk's barrier).
   constexpr int T0 = NTAP == 9 ? 3 : 1;
-  for (int c = c_begin; c < c_end; ++c) {
+  for (int c0 = c_begin; c0 < c_end; c0 += CPI) {
+#pragma unroll
+  for (int cc = 0; cc < CPI; ++cc) {
+    const int c = c0 + cc;
+    if (CPI > 1 && c >= c_end) break;
 #pragma unroll
     for (int tap = 0; tap < NTAP; ++tap) {
       const int kt = c * NTAP + tap;
-      const int slot = tap % WD;
+      const int slot = (cc * NTAP + tap) % WD;
       if (tap == 0) {
         load_patch(min(c + 1, c_end - 1));
         __builtin_amdgcn_sched_barrier(0);
@@ -410,6 +506,7 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
     }
     __syncthreads();
   }
+  }
 
   // ---- segment 2: 1x1 product of x2 (ResBlock shortcut), K = Cin2, un-pipelined (last split).
   if (a.Cin2 > 0 && (!KSPLIT || split == ksplit - 1)) {
@@ -417,19 +514,29 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
     int abase[TM];
 #pragma unroll
     for (int i = 0; i < TM; ++i) abase[i] = (wm * WM + i * 32 + lr) * kSPitch + lh * kGrp;
-    const bool arow_ok = srow < BM;
-    const int m = min(m0 + srow, M - 1);
-    const float* xsrc = a.x2 + (size_t)m * a.x2_pitch + 8 * shalf;
-    for (int c2 = 0; c2 < a.Cin2; c2 += kSK) {
-      const f4 r0 = *reinterpret_cast<const f4*>(xsrc + c2);
-      const f4 r1 = *reinterpret_cast<const f4*>(xsrc + c2 + 4);
-      load_b(bq[0], s2base + c2 / kSK);
-      if (arow_ok) {  // rows >= M hold clamped data: never stored
-        vec pc[NP];
-        S::split(r0, r1, pc, bad);
+    constexpr int RJ = (BM + 127) / 128;  // staging passes of 128 rows
+    const float* xsrc[RJ];
 #pragma unroll
-        for (int q = 0; q < NP; ++q)
-          *reinterpret_cast<vec*>(patch + srow * kSPitch + shalf * kGrp + q * 8) = pc[q];
+    for (int j = 0; j < RJ; ++j)
+      xsrc[j] = a.x2 + (size_t)min(m0 + srow + 128 * j, M - 1) * a.x2_pitch + 8 * shalf;
+    for (int c2 = 0; c2 < a.Cin2; c2 += kSK) {
+      f4 r0[RJ], r1[RJ];
+#pragma unroll
+      for (int j = 0; j < RJ; ++j) {
+        r0[j] = *reinterpret_cast<const f4*>(xsrc[j] + c2);
+        r1[j] = *reinterpret_cast<const f4*>(xsrc[j] + c2 + 4);
+      }
+      load_b(bq[0], s2base + c2 / kSK);
+#pragma unroll
+      for (int j = 0; j < RJ; ++j) {
+        const int row = srow + 128 * j;
+        if (row < BM) {  // rows >= M hold clamped data: never stored
+          vec pc[NP];
+          S::split(r0[j], r1[j], pc, bad);
+#pragma unroll
+          for (int q = 0; q < NP; ++q)
+            *reinterpret_cast<vec*>(patch + row * kSPitch + shalf * kGrp + q * 8) = pc[q];
+        }
       }
       __syncthreads();
       compute(patch, abase, bq[0]);
@@ -437,23 +544,33 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
     }
   }
 
-  if (NP == 2) {
-    // undo the per-output-channel power-of-two weight scale (exact)
-    if (bad && a.range_flag) *a.range_flag = 1;
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const float sc = a.ws_rowscale[min(n0 + wn * WN + j * 32 + lr, N - 1)];
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] *= sc;
+  if (NP == 2 && bad && a.range_flag) *a.range_flag = 1;
+  if constexpr (PW1 && NP == 2) {
+    if (a.ap_q) {  // the attention operand planes (ConvArgs::ap_*), written in 16-B pieces through LDS
+      attn_plane_epilogue<WM, WN>(a, acc, M, m0 + wm * WM, n0 + wn * WN, lr, lh,
+                                  wave < 2 ? reinterpret_cast<float*>(patch) + wave * WM * (WN + 8)
+                                           : gtab + (wave - 2) * WM * (WN + 8));
+      return;
     }
   }
-  conv_patch_epilogue<BM, BN, WM, WN, MODE, KSPLIT>(a, acc, M, HWo, Wo, m0, n0, b0, wm, wn, lr, lh, split, py, px);
+  // fp16x2: the epilogue undoes the per-output-channel power-of-two weight scale (exact) as it reads acc
+  conv_patch_epilogue<BM, BN, WM, WN, MODE, KSPLIT>(a, acc, M, HWo, Wo, m0, n0, b0, wm, wn, lr, lh, split, py, px,
+                                                    NP == 2 ? a.ws_rowscale : nullptr);
 }
 
 template <int BM, int BN, int WM, int WN, int MODE, int MAXP, int NP>
 void launch3_mode(const ConvArgs& a, const PatchGeom& g, int blocks, hipStream_t st) {
+  if constexpr (BM > 128) {  // big tiles: stride-1 / upsample modes, no split-K (checked by the caller)
+    if constexpr (MODE <= 2) {
+      if (a.pro_scale)
+        hipLaunchKernelGGL((conv_patch3_kernel<BM, BN, WM, WN, MODE, MAXP, true, false, NP>), dim3(blocks),
+                           dim3(256), 0, st, a, g);
+      else
+        hipLaunchKernelGGL((conv_patch3_kernel<BM, BN, WM, WN, MODE, MAXP, false, false, NP>), dim3(blocks),
+                           dim3(256), 0, st, a, g);
+    }
+    return;
+  }
   if (MODE == 0 && a.ksplit > 1) {
     if (a.pro_scale)
       hipLaunchKernelGGL((conv_patch3_kernel<BM, BN, WM, WN, 0, MAXP, true, true, NP>), dim3(blocks), dim3(256), 0,
@@ -496,6 +613,7 @@ int launch3(const ConvArgs& a, const PatchGeom& g, hipStream_t st) {
              "conv: split-K needs a stride-1 3x3 conv, a workspace and at most one split per channel chunk");
   DM_REQUIRE(g.P <= MAXP, "conv: patch larger than the split kernel's LDS image");
   DM_REQUIRE(NP == 3 || a.ws_rowscale, "conv: fp16x2 split weights need their row scales");
+  DM_REQUIRE(BM <= 128 || (ks == 1 && a.stride == 1), "conv: the big split tiles run stride-1 convs without split-K");
   const int blocks = ceil_div(M, BM) * ceil_div(a.Cout, BN) * (sub ? 4 : 1) * ks;
   if (sub)
     launch3_mode<BM, BN, WM, WN, 2, MAXP, NP>(a, g, blocks, st);
@@ -588,6 +706,10 @@ __global__ void split_conv_weights_kernel(const float* w, int nmat, int rows, in
 bool conv_patch3_ok(const ConvArgs& a, int which, const PatchGeom& g) {
   if (!a.ws || a.Cin1 % kSK != 0 || a.Cin2 % kSK != 0 || a.K % kSK != 0) return false;
   if (a.stride == 2) return a.ws_np == 2 && which == 6 && g.P <= kPatchS2Max;  // MODE 4: fp16x2, 64-row tiles
+  if (which == 7 || which == 8) {  // one wave per SIMD, 128 x 128 wave tiles: fp16x2 only
+    if (a.ws_np != 2 || (a.pro_scale && (long)g.TB * a.Cin1 * 2 > kPwTabFloats)) return false;
+    return g.P <= (which == 7 ? kPatch3Max256 : kPatch3Max512);
+  }
   if (a.ws_np == 2 && a.pro_scale && (long)g.TB * a.Cin1 * 2 > kPwTabFloats) return false;  // LDS GroupNorm tables
   return g.P <= (which == 6 ? kPatch3Max64 : kPatch3Max128);
 }
@@ -627,6 +749,8 @@ int conv2d_patch3(const ConvArgs& a, int which, const PatchGeom& g, hipStream_t 
   }
   if (a.ws_np == 2) {
     switch (which) {
+      case 7: return launch3<256, 256, 128, 128, kPatch3Max256, 2>(a, g, st);
+      case 8: return launch3<512, 128, 128, 128, kPatch3Max512, 2>(a, g, st);
       case 4: return launch3<128, 128, 64, 64, kPatch3Max128, 2>(a, g, st);
       case 5: return launch3<128, 64, 64, 32, kPatch3Max128, 2>(a, g, st);
       default: return launch3<64, 64, 32, 32, kPatch3Max64, 2>(a, g, st);

@@ -73,6 +73,15 @@ struct ConvArgs {
   const float* ws_rowscale;
   // optional device flag, set to 1 when an fp16x2 conv meets an activation beyond the fp16 range
   int* range_flag;
+  // attention operand planes (MODE 3 qkv conv feeding attn_fused): instead of y, the epilogue writes
+  // q * alpha * 2^ea and k * b_scale * 2^eb as fp16x2 planes [B][heads][2][L][Dh] and v * 2^ev
+  // transposed, [B][heads][2][Dh][L] (plane 0 = fp16(x), plane 1 = fp16(x - plane 0)): the split the
+  // attention GEMMs would do on load, done once by the producer. Columns: q | k | v blocks of C, or
+  // per head [q; k; v] (ap_legacy, QKVAttentionLegacy).
+  _Float16 *ap_q, *ap_k, *ap_v;
+  int ap_L, ap_heads, ap_Dh, ap_legacy;
+  float ap_alpha, ap_bscale;
+  int ap_ea, ap_eb, ap_ev;
 };
 
 // Patch-pixel capacity of the halo-patch kernels' LDS images (fp32 / split-bf16; 128- / 64-row tiles)
@@ -80,6 +89,10 @@ constexpr int kPatchMax128 = 288;
 constexpr int kPatchMax64 = 160;
 constexpr int kPatch3Max128 = 208;
 constexpr int kPatch3Max64 = 160;
+// fp16x2 split kernel, one wave per SIMD with 128 x 128 wave tiles: 256 x 256 blocks (32^2 maps: 8 rows,
+// 10 x 34 patch; 16^2: one image, 18 x 18) and 512 x 128 blocks (32^2: 16 rows, 18 x 34; 16^2: two images)
+constexpr int kPatch3Max256 = 352;
+constexpr int kPatch3Max512 = 656;
 constexpr int kPatchS2Max = 384;  // stride-2 split conv (64-row tiles): (2 TH + 1) x 2 (Wo + 1) per image (3 loader passes)
 
 // Output tile = TB images x TH rows x full width; input patch PH x PW per image.
@@ -226,6 +239,24 @@ int gemm_pick(const GemmArgs& g);
 std::string gemm_label(const GemmArgs& g);
 int timestep_embed(const int64_t* t, int B, int dim, int kind, const float* freqs, float* out, hipStream_t st);
 int softmax_rows(float* x, long rows, int L, int ld, hipStream_t st);
+
+// Fused attention core (attention.hip): per (image, head) S = (alpha q)(b_scale k)^T, softmax rows,
+// O = P v with S kept on the CU, fp16x2 split operands (exponents ea / eb for S, ep / ev for PV, as
+// the split GEMMs). q / k / v of token i, head h: qkv[(b L + i) ld + {q0, k0, v0} + h hs + d].
+struct AttnArgs {
+  const float* qkv;
+  int ld, L, Dh, heads, B;
+  int q0, k0, v0, hs;
+  float alpha, b_scale;
+  float* out;  // out[(b L + i) ldo + h Dh + d]
+  int ldo;
+  int ea, eb, ep, ev;
+  int* range_flag;
+  // pre-split operand planes written by the qkv conv (ConvArgs::ap_*); when set, qkv is not read
+  const _Float16 *pq, *pk, *pv;
+};
+bool attn_fused_ok(int L, int Dh);
+int attn_fused(const AttnArgs& a, hipStream_t st);
 int conv3x3_small_in(const float* x, int B, int Cin, int H, int W, const float* w, const float* bias,
                      int Cout, const View& y, hipStream_t st);
 // last conv weights torch [Cout][Cin][3][3] -> [9][Cin][CO], CO = 4 (Cout <= 4) or 8; wp holds 9 * Cin * CO floats

@@ -941,6 +941,18 @@ int UNetModel::build_plan(int B, int H, int W) {
       cq.w = P(p.wqkv); cq.K = C; cq.y = qkv; cq.y_pitch = 3 * C; cq.Cout = 3 * C; cq.B = B; cq.pick_B = kPickBatch; cq.Hout = Hi;
       cq.Wout = Wi; cq.bias = P(p.bqkv); cq.pro_scale = gsc; cq.pro_shift = gsh; cq.pro_nosilu = 1;
       split_for(cq);
+      // Fused attention (attention.hip) on 16 x 16 maps; with the qkv conv on the split kernel, its epilogue
+      // writes q / k / v as the fp16x2 operand planes the fused kernel reads (over the qkv buffer: same bytes)
+      const bool fuse_attn = conv_math == 2 && attn_fused_ok(hw, Dh) && !std::getenv("DM_ATTN_UNFUSED");
+      const bool presplit = fuse_attn && conv_pw_ok(cq) && !std::getenv("DM_ATTN_NO_PRESPLIT");
+      _Float16* planes = reinterpret_cast<_Float16*>(qkv);
+      const size_t plane_n = (size_t)B * hw * C * 2;  // fp16 elements of one operand's two planes
+      if (presplit) {
+        cq.ap_q = planes; cq.ap_k = planes + plane_n; cq.ap_v = planes + 2 * plane_n;
+        cq.ap_L = hw; cq.ap_heads = heads; cq.ap_Dh = Dh; cq.ap_legacy = p.legacy ? 1 : 0;
+        cq.ap_alpha = p.sa; cq.ap_bscale = p.sb;
+        cq.ap_ea = 6; cq.ap_eb = 6; cq.ap_ev = 6;
+      }
       if (conv_pw_ok(cq)) {
         gn_prologue(cq, xin, sta, p.gn.g, p.gn.b, nullptr, nullptr, 0);
         add_conv(cq);
@@ -955,6 +967,23 @@ int UNetModel::build_plan(int B, int H, int W) {
       // (q | k | v blocks: modules.py:92-94 and ADM QKVAttention; per-head [q; k; v]: QKVAttentionLegacy)
       const int hs = p.legacy ? 3 * Dh : Dh;
       const int k0 = p.legacy ? Dh : C, v0 = p.legacy ? 2 * Dh : 2 * C;
+      if (fuse_attn) {
+        // S, softmax and PV in one kernel (attention.hip), bit-identical to the three launches below
+        AttnArgs at{};
+        if (presplit) {
+          at.pq = planes; at.pk = planes + plane_n; at.pv = planes + 2 * plane_n;
+        }
+        at.qkv = qkv; at.ld = 3 * C; at.L = hw; at.Dh = Dh; at.heads = heads; at.B = B;
+        at.q0 = 0; at.k0 = k0; at.v0 = v0; at.hs = hs;
+        at.alpha = p.sa; at.b_scale = p.sb;
+        at.out = Ob; at.ldo = C;
+        at.ea = 6; at.eb = 6; at.ep = 14; at.ev = 6;
+        at.range_flag = range_flag;
+        const double fl = 4.0 * B * heads * (double)hw * hw * Dh;
+        const double by = 4.0 * B * hw * (3.0 * C + C);
+        add((presplit ? "attn_presplit_kernel<" : "attn_fused_kernel<") + std::to_string(Dh) + ">", fl, by,
+            [=](hipStream_t st) { return attn_fused(at, st); });
+      } else {
       GemmArgs gs{};
       gs.M = hw; gs.N = hw; gs.K = Dh; gs.Z1 = B; gs.Z2 = heads; gs.pick_Z = (long)kPickBatch * heads;
       gs.A = qkv; gs.a_s1 = (long)hw * 3 * C; gs.a_s2 = hs; gs.lda = 3 * C;
@@ -974,6 +1003,7 @@ int UNetModel::build_plan(int B, int H, int W) {
       go.alpha = 1.f;
       split_gemm(go, 14, nullptr, 0, 6);
       add_gemm(go);
+      }
       GemmArgs gp{};
       gp.M = B * hw; gp.N = C; gp.K = C; gp.Z1 = 1; gp.Z2 = 1; gp.pick_M = (long)kPickBatch * hw;
       gp.A = Ob; gp.lda = C; gp.Bm = P(p.wproj); gp.ldb = C; gp.C = y.p; gp.ldc = y.pitch;

@@ -17,7 +17,7 @@ KINDS = ['bf16x3', 'fp16x2']
 
 
 @pytest.mark.parametrize('kind', KINDS)
-@pytest.mark.parametrize('tile', [0, 4, 5, 6])
+@pytest.mark.parametrize('tile', [0, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize('B,Cin,Cout,H,up', [
     (2, 32, 64, 8, 0), (1, 128, 256, 16, 0), (5, 64, 64, 4, 0), (3, 32, 96, 5, 0), (4, 64, 128, 32, 1 - 1),
     (3, 64, 64, 16, 1), (2, 32, 64, 8, 1), (2, 48, 32, 8, 0),
@@ -37,7 +37,7 @@ def test_split_conv3x3_exact(cuda, B, Cin, Cout, H, up, tile, kind):
 
 
 @pytest.mark.parametrize('kind', KINDS)
-@pytest.mark.parametrize('tile', [0, 4, 5, 6])
+@pytest.mark.parametrize('tile', [0, 4, 5, 6, 7, 8])
 def test_split_conv_segments_rowvec_residual_pitch(cuda, tile, kind):
     B, C1, C2, Cout, H = 3, 64, 32, 64, 8
     h = _ints((B, C1, H, H), seed=20)
@@ -60,7 +60,7 @@ def test_split_conv_segments_rowvec_residual_pitch(cuda, tile, kind):
 
 
 @pytest.mark.parametrize('kind', KINDS)
-@pytest.mark.parametrize('tile', [0, 4, 5, 6])
+@pytest.mark.parametrize('tile', [0, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize('B,Cin,Cout,H', [(3, 64, 64, 16), (2, 32, 64, 8), (4, 64, 128, 8), (2, 96, 64, 4)])
 def test_split_conv_subpixel_exact(cuda, B, Cin, Cout, H, tile, kind):
     x = _ints((B, Cin, H, H), -2, 3, seed=70)

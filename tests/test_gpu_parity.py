@@ -336,3 +336,44 @@ def test_public_forward_rejects_negative_labels(cuda, golden):
     with dmhip.null_label_scope():
         a = m(x, t, torch.tensor([-1, -1], device=cuda))
     assert torch.equal(a, m(x, t, None))
+
+
+@pytest.mark.parametrize('arch', ['cifar10', 'adagn'])
+def test_fused_attention_bit_identical(cuda, golden, arch, monkeypatch):
+    """The fused attention kernels (attention.hip: S, softmax and PV on the CU; with q / k / v either split
+    by the kernel or pre-split into operand planes by the qkv conv's epilogue) give the same bits as the
+    three-launch path (split S GEMM, softmax_rows, split PV GEMM) they replace: CIFAR-10 (one head of
+    256 at 16x16) and CFG-CIFAR AdaGN (heads of 64 at 16x16) forwards."""
+    from models.unet_categorial_adagn import UNetCategorialAdaGN
+    outs = {}
+    kernel = {'unfused': None, 'fused': 'attn_fused_kernel', 'presplit': 'attn_presplit_kernel'}
+    for mode in ('unfused', 'fused', 'presplit'):
+        monkeypatch.delenv('DM_ATTN_UNFUSED', raising=False)
+        monkeypatch.delenv('DM_ATTN_NO_PRESPLIT', raising=False)
+        if mode == 'unfused':
+            monkeypatch.setenv('DM_ATTN_UNFUSED', '1')
+        elif mode == 'fused':
+            monkeypatch.setenv('DM_ATTN_NO_PRESPLIT', '1')
+        if arch == 'cifar10':
+            m, _ = _model(golden('forward')[1], 'cifar10', cuda)
+        else:
+            m = UNetCategorialAdaGN(**golden('adagn')[1]['archs']['cfg_cifar10']).eval()
+            init_synthetic_(m)
+            m = m.to(cuda)
+        g = torch.Generator().manual_seed(4)
+        x = torch.randn((8, 3, 32, 32), generator=g).to(cuda)
+        t = torch.tensor([999, 800, 600, 400, 200, 100, 10, 0], device=cuda)
+        outs[mode] = (m(x, t) if arch == 'cifar10' else m(x, t, torch.arange(8, device=cuda) % 10)).cpu()
+        labels = [op['label'] for op in _plan_labels(m, cuda)]
+        for name in ('attn_fused_kernel', 'attn_presplit_kernel'):
+            assert any(lb.startswith(name) for lb in labels) == (kernel[mode] == name), (mode, labels)
+    assert torch.equal(outs['fused'], outs['unfused'])
+    assert torch.equal(outs['presplit'], outs['unfused'])
+
+
+def _plan_labels(m, cuda):
+    import dmhip
+    h = m.native_handle(torch.device(cuda))
+    dmhip.unet_profile_enable(h, 1)
+    dmhip.unet_profile_enable(h, 0)
+    return dmhip.unet_profile_read(h)

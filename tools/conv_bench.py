@@ -31,7 +31,7 @@ SHAPES = {
 }
 
 
-def run(name, iters, split):
+def run(name, iters, split, tile=0):
     B, Cin, Cout, H, pro, up = SHAPES[name]
     dev = torch.device('cuda', 0)
     g = torch.Generator(device='cpu').manual_seed(0)
@@ -64,6 +64,7 @@ def run(name, iters, split):
     d.w, d.K = wp.data_ptr(), wp.shape[1]
     d.y, d.y_pitch, d.Cout, d.B, d.Hout, d.Wout = y.data_ptr(), Cout, Cout, B, Ho, Ho
     d.bias = b.data_ptr()
+    d.tile = tile
     if pro:
         d.pro_scale, d.pro_shift = sc.data_ptr(), sh.data_ptr()
     if split:
@@ -85,6 +86,7 @@ def run(name, iters, split):
         flops = 2.0 * B * H * H * 4 * Cout * 4 * Cin  # executed sub-pixel work
     tf = flops / ms / 1e9
     tag = split or 'fp32'
+    tag = f'{tag}/t{tile}' if tile else tag
     print(f'{name:12s} {tag:7s} {ms:8.4f} ms  {tf:6.1f} TF/s  {tf / 157.3 * 100:5.1f} % of fp32 peak', flush=True)
 
 
@@ -93,12 +95,14 @@ def main():
     ap.add_argument('--iters', type=int, default=20)
     ap.add_argument('--shape', default=None)
     ap.add_argument('--math', choices=['fp32', 'bf16x3', 'fp16x2', 'all'], default='all')
+    ap.add_argument('--tiles', default='0', help='comma-separated ConvDesc.tile values (0 = auto)')
     args = ap.parse_args()
     dmhip.load()
     for name in ([args.shape] if args.shape else SHAPES):
         kinds = (False, 'bf16x3', 'fp16x2') if args.math == 'all' else ({'fp32': False}.get(args.math, args.math), )
         for split in kinds:
-            run(name, args.iters, split)
+            for tile in [int(v) for v in args.tiles.split(',')]:
+                run(name, args.iters, split, tile)
 
 
 if __name__ == '__main__':
