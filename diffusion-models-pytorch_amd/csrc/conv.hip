@@ -278,7 +278,7 @@ int conv2d_igemm(const ConvArgs& a, hipStream_t st) {
   }
   const long M = (long)a.B * a.Hout * a.Wout;
   DM_REQUIRE(M > 0 && M < (1L << 31), "conv: M out of range");
-  DM_REQUIRE(a.tile >= 0 && a.tile <= 8, "conv: tile must be 0..8");
+  DM_REQUIRE(a.tile >= 0 && a.tile <= 9, "conv: tile must be 0..9");
   const int mode = conv_mode(a);
   const int pick = conv_pick(a);
   DM_REQUIRE(!a.gn_part || conv_can_emit_gn(a), "conv: GroupNorm statistics need a 128-row halo-patch tile, "
@@ -290,7 +290,8 @@ int conv2d_igemm(const ConvArgs& a, hipStream_t st) {
     PatchGeom g;
     conv_patch_pick(a, g);
     if (conv_patch3_ok(a, pick + 1, g)) return conv2d_patch3(a, pick + 1, g, st);
-    return conv2d_patch(a, pick + 1, g, st);
+    if (pick + 1 <= 6) return conv2d_patch(a, pick + 1, g, st);
+    return launch_conv_tile<128, 128, 64, 64>(a, mode, st);  // a split-only tile that does not fit
   }
   DM_REQUIRE(a.upsample != 2, "conv: the sub-pixel upsample runs on the halo-patch kernel only (shape has no "
                               "whole-row tiling)");
@@ -317,7 +318,7 @@ int conv_pick(const ConvArgs& a) {
   const int p = conv_patch_pick(a, g);
   if (p) return p - 1;
   if (a.tile >= 4 && a.tile <= 6) return a.tile - 4;  // a forced patch tile that does not fit: its im2col shape
-  if (a.tile >= 7) return 0;                           // a forced big split tile that does not fit: 128 x 128
+  if (a.tile >= 7) return 0;                           // a forced big / segment split tile that does not fit
   const long M = (long)(a.pick_B > 0 ? a.pick_B : a.B) * a.Hout * a.Wout;
   const long b128 = ((M + 127) / 128) * ((a.Cout + 127) / 128);
   if (a.Cout >= 128 && b128 >= 512) return 0;
@@ -331,7 +332,7 @@ bool conv_can_emit_gn(const ConvArgs& a) {
     return !a.upsample && a.Hout * a.Wout <= kGnPixPerChunk && a.gn_G > 0 && a.Cout % a.gn_G == 0 &&
            a.Cout <= 1024;
   const int pick = conv_pick(a);
-  if (pick != 3 && pick != 4 && pick != 6 && pick != 7) return false;  // waves own whole 64-row chunks
+  if (pick != 3 && pick != 4 && pick != 6 && pick != 7 && pick != 8) return false;  // waves own whole 64-row chunks
   if (a.upsample || (a.ksplit > 1)) return false;
   if (a.taps == 1 && !conv_pw_ok(a)) return false;
   if ((a.Hout * a.Wout) % 64 != 0 || a.gn_G <= 0 || a.Cout % a.gn_G != 0) return false;
@@ -344,7 +345,8 @@ std::string conv_label(const ConvArgs& a) {
   static const char* names[] = {"conv_igemm_kernel<128,128,64,64", "conv_igemm_kernel<128,64,64,32",
                                 "conv_igemm_kernel<64,64,32,32",   "conv_patch_kernel<128,128,64,64",
                                 "conv_patch_kernel<128,64,64,32",  "conv_patch_kernel<64,64,32,32",
-                                "conv_patch_kernel<256,256,128,128", "conv_patch_kernel<512,128,128,128"};
+                                "conv_patch_kernel<256,256,128,128", "conv_patch_kernel<512,128,128,128",
+                                "conv_patch_kernel<128,128,64,64"};
   const int p = conv_pick(a);
   std::string s = names[p];
   if (p < 3) s += "," + std::to_string(conv_mode(a)) + ">";  // <BM,BN,WM,WN,MODE>
@@ -357,7 +359,8 @@ std::string conv_label(const ConvArgs& a) {
     const bool x3 = conv_patch3_ok(a, p + 1, g);
     if (x3) s.replace(0, 17, "conv_patch3_kernel");
     s += "," + std::to_string(a.stride == 2 ? 4 : a.upsample);
-    s += a.stride == 2 ? ",384" : p == 5 ? ",160" : p == 6 ? ",352" : p == 7 ? ",656" : (x3 ? ",208" : ",288");
+    s += a.stride == 2 ? ",384" : p == 5 ? ",160" : p == 6 ? ",352" : p == 7 ? ",656" : p == 8 ? ",392" :
+         (x3 ? ",208" : ",288");
     s += a.pro_scale ? ",true" : ",false";
     s += a.ksplit > 1 ? ",true" : ",false";  // rocprofv3 prints the defaulted arguments too
     s += x3 ? "," + std::to_string(a.ws_np) + ">" : ">";  // <..., NP>: 3 bf16x3, 2 fp16x2

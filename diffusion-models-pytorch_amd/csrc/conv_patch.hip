@@ -410,12 +410,24 @@ bool conv_patch_geom(const ConvArgs& a, int BM, PatchGeom& g) {
     g.PH = 2 * g.TH + 1;
     g.PW = 2 * (Wo + 1);
     g.P = g.TB * g.PH * g.PW;
+    g.TW = Wo;
     return true;
   }
   if (a.stride != 1) return false;
   const bool sub = a.upsample == 2;  // tiles over the low-res pixels of one parity class
   const int Ho = sub ? a.Hin : a.Hout, Wo = sub ? a.Win : a.Wout;
-  if (Wo > BM || BM % Wo != 0) return false;
+  if (Wo > BM) {  // row segments of BM pixels: one image, one output row, BM consecutive columns
+    if (Wo % BM != 0 || a.upsample == 1) return false;
+    g.TB = 1;
+    g.TH = 1;
+    g.TW = BM;
+    g.PH = 3;
+    g.PW = BM + 2;
+    g.P = g.PH * g.PW;
+    return !(sub && a.Cin2 != 0);
+  }
+  g.TW = Wo;
+  if (BM % Wo != 0) return false;
   const int rows = BM / Wo;  // output rows per tile (across images)
   if (rows <= Ho) {
     if (Ho % rows != 0) return false;
@@ -452,6 +464,15 @@ int conv_patch_pick(const ConvArgs& a, PatchGeom& g) {
     if (a.tile == 7) return conv_patch_geom(a, 256, g) && g.P <= kPatch3Max256 ? 7 : 0;
     return conv_patch_geom(a, 512, g) && g.P <= kPatch3Max512 ? 8 : 0;
   }
+  // wide maps (ADM 256^2 / 128^2): 128-pixel row segments on the fp16x2 split kernel
+  {
+    const bool sub = a.upsample == 2;
+    const int Wo = sub ? a.Win : a.Wout;
+    if (Wo > 128) {
+      if (!(a.ws && a.ws_np == 2) || (a.tile != 0 && a.tile != 9)) return 0;
+      return conv_patch_geom(a, 128, g) && g.P <= kPatch3Seg ? 9 : 0;
+    }
+  }
   // the split-bf16 kernel's LDS image holds fewer patch pixels at 128-row tiles
   const int max128 = a.ws ? kPatch3Max128 : kPatchMax128, max64 = a.ws ? kPatch3Max64 : kPatchMax64;
   if (a.tile == 4 || a.tile == 0) {
@@ -461,6 +482,11 @@ int conv_patch_pick(const ConvArgs& a, PatchGeom& g) {
     if ((a.tile == 4 || (a.Cout >= 128 && b128 >= 512)) && conv_patch_geom(a, 128, g) && g.P <= max128)
       return 4;
     if (a.tile == 0 && b128x64 >= 512 && conv_patch_geom(a, 128, g) && g.P <= max128) return 5;
+    // 64-pixel-wide maps (ADM 64^2): two whole rows per 128-row tile need the row-segment kernel's LDS image
+    const int Wo = a.upsample == 2 ? a.Win : a.Wout;
+    if (a.tile == 0 && a.ws && a.ws_np == 2 && Wo >= 64 && conv_patch_geom(a, 128, g) && g.TB == 1 &&
+        g.P <= kPatch3Seg && g.P > max128)
+      return 9;
     if (a.tile == 0 && conv_patch_geom(a, 64, g) && g.P <= max64) return 6;
   } else if (a.tile == 5) {
     if (conv_patch_geom(a, 128, g) && g.P <= max128) return 5;
@@ -484,6 +510,16 @@ bool conv_split_eligible(const ConvArgs& a) {
   if (a.taps != 9 || a.stride != 1 || a.upsample == 1 || a.Cin1 % 16 != 0 || a.Cin2 % 16 != 0) return false;
   PatchGeom g;
   return conv_patch_geom(a, 64, g) && g.P <= kPatch3Max64;
+}
+
+// Whether a conv runs on the fp16x2 row-segment / wide-row split kernel (which 9) at every batch size:
+// a shape-only test like conv_split_eligible.
+bool conv_seg_eligible(const ConvArgs& a) {
+  if (a.taps != 9 || a.stride != 1 || a.Cin1 % 16 != 0 || a.Cin2 % 16 != 0) return false;
+  const int Wo = a.upsample == 2 ? a.Win : a.Wout;
+  if (Wo < 64) return false;
+  PatchGeom g;
+  return conv_patch_geom(a, 128, g) && g.TB == 1 && g.P <= kPatch3Seg;
 }
 
 int conv2d_patch(const ConvArgs& a, int which, const PatchGeom& g, hipStream_t st) {

@@ -173,7 +173,8 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
   // staged in LDS once per block; per-thread global loads of them cost as many VMEM instructions as
   // the activations themselves (and in MODE 3, with no tap reuse, twice the activation bytes)
   constexpr bool LTAB = PRO && (PW1 || NP == 2);
-  constexpr int GTAB = (LTAB || PW1) ? kPwTabFloats : 1;  // MODE 3: also the plane epilogue's staging
+  // MODE 3: also the plane epilogue's staging; row-segment tiles (MAXP = kPatch3Seg): one image's tables
+  constexpr int GTAB = (LTAB || PW1) ? (MAXP == kPatch3Seg ? kSegTabFloats : kPwTabFloats) : 1;
   __shared__ __attribute__((aligned(16))) float gtab[GTAB];
   __shared__ float gstat[LTAB ? 2 * kGinStats : 1];  // in-kernel finalize: (mean, rstd) per (image, group)
 
@@ -201,6 +202,7 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
   const int HWo = Ho * Wo;
   const int b0 = m0 / HWo;
   const int y0 = (m0 - b0 * HWo) / Wo;
+  const int x0 = (m0 - b0 * HWo) - y0 * Wo;  // row-segment tiles (g.TW < Wo); 0 for whole-row tiles
 
   const int t = threadIdx.x;
   const int lane = t & 63, wave = t >> 6;
@@ -233,7 +235,7 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
     const int b = b0 + img;
     const int half = g.PW >> 1;
     const int col = S2 ? 2 * (pc - (pc >= half ? half : 0)) + (pc >= half ? 1 : 0) : pc;  // input column + 1
-    const int iy = iy_base + pr, ix = col - 1;
+    const int iy = iy_base + pr, ix = x0 + col - 1;
     const bool ok = p < g.P && b < a.B && iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
     pok[j] = ok;
     const int bc = min(b, a.B - 1);
@@ -273,7 +275,7 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
 
   // ---- A-fragment patch coordinates of this lane's rows
   int fy[TM], fx[TM], fimg[TM];
-  const int tile_rows = PW1 ? 1 : g.TH * Wo;
+  const int tile_rows = PW1 ? 1 : g.TH * g.TW;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     if constexpr (PW1) {
@@ -283,8 +285,8 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
     const int ml = wm * WM + i * 32 + lr;
     fimg[i] = ml / tile_rows;
     const int rem = ml - fimg[i] * tile_rows;
-    fy[i] = rem / Wo;
-    fx[i] = rem - fy[i] * Wo;
+    fy[i] = rem / g.TW;
+    fx[i] = rem - fy[i] * g.TW;
   }
 
   // Patch registers of the next chunk and, with the GroupNorm prologue, their per-(image, channel)
@@ -560,8 +562,8 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
 
 template <int BM, int BN, int WM, int WN, int MODE, int MAXP, int NP>
 void launch3_mode(const ConvArgs& a, const PatchGeom& g, int blocks, hipStream_t st) {
-  if constexpr (BM > 128) {  // big tiles: stride-1 / upsample modes, no split-K (checked by the caller)
-    if constexpr (MODE <= 2) {
+  if constexpr (BM > 128 || MAXP == kPatch3Seg) {  // big / segment tiles: stride 1, no split-K (caller checks)
+    if constexpr (MODE <= 2 && (MAXP != kPatch3Seg || MODE != 1)) {
       if (a.pro_scale)
         hipLaunchKernelGGL((conv_patch3_kernel<BM, BN, WM, WN, MODE, MAXP, true, false, NP>), dim3(blocks),
                            dim3(256), 0, st, a, g);
@@ -613,7 +615,8 @@ int launch3(const ConvArgs& a, const PatchGeom& g, hipStream_t st) {
              "conv: split-K needs a stride-1 3x3 conv, a workspace and at most one split per channel chunk");
   DM_REQUIRE(g.P <= MAXP, "conv: patch larger than the split kernel's LDS image");
   DM_REQUIRE(NP == 3 || a.ws_rowscale, "conv: fp16x2 split weights need their row scales");
-  DM_REQUIRE(BM <= 128 || (ks == 1 && a.stride == 1), "conv: the big split tiles run stride-1 convs without split-K");
+  DM_REQUIRE((BM <= 128 && MAXP != kPatch3Seg) || (ks == 1 && a.stride == 1 && !(MAXP == kPatch3Seg && a.upsample == 1)),
+             "conv: the big / row-segment split tiles run stride-1 convs without split-K");
   const int blocks = ceil_div(M, BM) * ceil_div(a.Cout, BN) * (sub ? 4 : 1) * ks;
   if (sub)
     launch3_mode<BM, BN, WM, WN, 2, MAXP, NP>(a, g, blocks, st);
@@ -706,6 +709,10 @@ __global__ void split_conv_weights_kernel(const float* w, int nmat, int rows, in
 bool conv_patch3_ok(const ConvArgs& a, int which, const PatchGeom& g) {
   if (!a.ws || a.Cin1 % kSK != 0 || a.Cin2 % kSK != 0 || a.K % kSK != 0) return false;
   if (a.stride == 2) return a.ws_np == 2 && which == 6 && g.P <= kPatchS2Max;  // MODE 4: fp16x2, 64-row tiles
+  if (which == 9) {  // 128-pixel row segments: fp16x2, one image's GroupNorm tables
+    if (a.ws_np != 2 || (a.pro_scale && (long)g.TB * a.Cin1 * 2 > kSegTabFloats)) return false;
+    return g.P <= kPatch3Seg;
+  }
   if (which == 7 || which == 8) {  // one wave per SIMD, 128 x 128 wave tiles: fp16x2 only
     if (a.ws_np != 2 || (a.pro_scale && (long)g.TB * a.Cin1 * 2 > kPwTabFloats)) return false;
     return g.P <= (which == 7 ? kPatch3Max256 : kPatch3Max512);
@@ -749,6 +756,7 @@ int conv2d_patch3(const ConvArgs& a, int which, const PatchGeom& g, hipStream_t 
   }
   if (a.ws_np == 2) {
     switch (which) {
+      case 9: return launch3<128, 128, 64, 64, kPatch3Seg, 2>(a, g, st);
       case 7: return launch3<256, 256, 128, 128, kPatch3Max256, 2>(a, g, st);
       case 8: return launch3<512, 128, 128, 128, kPatch3Max512, 2>(a, g, st);
       case 4: return launch3<128, 128, 64, 64, kPatch3Max128, 2>(a, g, st);

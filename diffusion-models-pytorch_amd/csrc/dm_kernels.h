@@ -92,12 +92,18 @@ constexpr int kPatch3Max64 = 160;
 // fp16x2 split kernel, one wave per SIMD with 128 x 128 wave tiles: 256 x 256 blocks (32^2 maps: 8 rows,
 // 10 x 34 patch; 16^2: one image, 18 x 18) and 512 x 128 blocks (32^2: 16 rows, 18 x 34; 16^2: two images)
 constexpr int kPatch3Max256 = 352;
+// fp16x2 split kernel, 128 x 128 blocks over 128-pixel row segments of wide maps (ADM 256^2 / 128^2):
+// 3 x 130 patch pixels
+constexpr int kPatch3Seg = 392;
+constexpr int kSegTabFloats = 2048;  // its GroupNorm tables (one image, Cin <= 1024)
 constexpr int kPatch3Max512 = 656;
 constexpr int kPatchS2Max = 384;  // stride-2 split conv (64-row tiles): (2 TH + 1) x 2 (Wo + 1) per image (3 loader passes)
 
 // Output tile = TB images x TH rows x full width; input patch PH x PW per image.
+// Halo-patch tile geometry: TB images x TH output rows x TW output columns per tile (TW = Wo for whole
+// rows; TW < Wo: row segments of wide maps, TB = TH = 1), patch PH x PW pixels per image, P in total.
 struct PatchGeom {
-  int TB, TH, PH, PW, P;
+  int TB, TH, PH, PW, P, TW;
 };
 
 struct GemmArgs {
@@ -215,6 +221,7 @@ bool conv_pw_ok(const ConvArgs& a);
 // of finalized tables)
 bool conv_lds_tables(const ConvArgs& a);
 bool conv_split_eligible(const ConvArgs& a);
+bool conv_seg_eligible(const ConvArgs& a);
 int conv2d_patch3(const ConvArgs& a, int which, const PatchGeom& g, hipStream_t st);
 int conv_splitk_reduce(const ConvArgs& a, hipStream_t st);
 // fp32 packed conv weights [nmat][rows][K] -> split slices for conv_patch3_kernel (np 3: bf16x3,

@@ -201,7 +201,7 @@ void UNetModel::split_for(ConvArgs& c) {
   c.ws_np = 0;
   c.ws_rowscale = nullptr;
   c.range_flag = nullptr;
-  if (!conv_math || !conv_split_eligible(c)) return;
+  if (!conv_math || !(conv_split_eligible(c) || (conv_math == 2 && conv_seg_eligible(c)))) return;
   if ((c.taps == 1 || c.stride == 2) && conv_math != 2) return;  // the split 1x1 / stride-2 paths are fp16x2 only
   const int nmat = c.upsample == 2 ? 4 : 1;
   const int ntap = c.upsample == 2 ? 4 : c.taps;
@@ -810,7 +810,9 @@ int UNetModel::build_plan(int B, int H, int W) {
       conv_patch_pick(c, gg);
       return (long)gg.TB;
     }();
-    if (conv_lds_tables(c) && imgs * G <= 512 && v.C == c.Cin1) {
+    // in-kernel finalize: every block re-reduces its images' chunk partials, so only for small maps
+    // (CIFAR: <= 16 chunks per image); the 256^2 maps of ADM have 1024 and take the finalize launch
+    if (conv_lds_tables(c) && imgs * G <= 512 && v.C == c.Cin1 && gn_num_chunks(v.H * v.W) <= 64) {
       c.gin_part = stp; c.gin_G = G; c.gin_nchunk = gn_num_chunks(v.H * v.W);
       c.gin_n = (double)v.H * v.W * (v.C / G); c.gin_eps = 1e-5f;
       c.gin_gamma = P(gamma); c.gin_beta = P(beta); c.gin_ms = ms; c.gin_mb = mb; c.gin_mp = mp;
@@ -871,6 +873,7 @@ int UNetModel::build_plan(int B, int H, int W) {
         if (!c.upsample || !w_sub) return;
         ConvArgs s = c;
         s.upsample = 2; s.w = P(w_sub); s.K = 4 * c.Cin1;
+        split_for(s);  // the tile choice depends on the split copy (fp16x2-only tiles)
         if (conv_pick(s) >= 3) c = s;
       };
       ConvArgs c2{};
@@ -884,6 +887,8 @@ int UNetModel::build_plan(int B, int H, int W) {
       } else {
         c2.res = xres.p; c2.res_pitch = xres.pitch;
       }
+      split_for(c1);
+      split_for(c2);
       try_subpix(c1, r.conv1.w_sub);
       const bool fuse1 = r.updown != 2 && conv_pick(c1) >= 3, fuse2 = conv_pick(c2) >= 3;
       // AdaGN modulation gn(h) * (1 + ys) + yb, [ys | yb] from the fused projection (modules.py:114-123)
@@ -1039,6 +1044,7 @@ int UNetModel::build_plan(int B, int H, int W) {
       if (c.upsample && cv.w_sub) {
         ConvArgs s = c;
         s.upsample = 2; s.w = P(cv.w_sub); s.K = 4 * c.Cin1;
+        split_for(s);
         if (conv_pick(s) >= 3) c = s;
       }
       gn_ready.erase(y.p);

@@ -201,3 +201,50 @@ def test_split_conv_stride2_fp32_accuracy(cuda):
         y = _run_conv(cuda, _nhwc(x).to(cuda), _pack(w, cuda), Cout, H // 2, H // 2, 9, 2, split=split)
         errs.append((y.cpu().double() - ref).abs().max().item())
     assert errs[1] < 2.0 * errs[0] + 1e-7 * ref.abs().max().item(), errs
+
+
+@pytest.mark.parametrize('tile', [0, 9])
+@pytest.mark.parametrize('B,Cin,Cout,H,W', [(1, 32, 64, 4, 256), (2, 64, 32, 3, 128), (1, 32, 64, 4, 64),
+                                            (1, 32, 32, 2, 512)])
+def test_split_conv_row_segments_exact(cuda, B, Cin, Cout, H, W, tile):
+    """Wide maps (ADM 256^2 / 128^2 / 64^2) on the fp16x2 split kernel: 128-pixel row segments with a
+    3 x 130 halo patch (or two whole 64-wide rows), bias + GroupNorm-free prologue, integer operands
+    exact (bit-equal to the fp64 reference)."""
+    x = _ints((B, Cin, H, W), -2, 3, seed=90)
+    w = _ints((Cout, Cin, 3, 3), -2, 3, seed=91)
+    b = _ints((Cout, ), seed=92)
+    if Cin % 32:
+        pytest.skip('packing needs Cin % 32 == 0')
+    ref = F.conv2d(x.double(), w.double(), b.double(), padding=1).float()
+    y = _run_conv(cuda, _nhwc(x).to(cuda), _pack(w, cuda), Cout, H, W, 9, 1, 0, b.to(cuda), tile=tile,
+                  split='fp16x2')
+    assert torch.equal(y.cpu(), _nhwc(ref))
+
+
+@pytest.mark.parametrize('tile', [0, 9])
+def test_split_conv_row_segments_shortcut_residual_prologue(cuda, tile):
+    """Row segments with the ResBlock epilogue pieces: 1x1 shortcut as a second K segment, per-image
+    rowvec, residual, and the GroupNorm-affine + SiLU prologue (scale 1, shift 0 on small integers:
+    SiLU values are not integers, so this part checks against an fp64 SiLU with fp32 tolerance)."""
+    B, C1, C2, Cout, H, W = 2, 64, 32, 64, 3, 256
+    h = _ints((B, C1, H, W), seed=94)
+    x = _ints((B, C2, H, W), seed=95)
+    w2 = _ints((Cout, C1, 3, 3), -2, 3, seed=96)
+    ws = _ints((Cout, C2, 1, 1), seed=97)
+    b = _ints((Cout, ), seed=98)
+    rv = _ints((B, Cout), seed=99)
+    K = 9 * C1 + C2
+    wp = torch.zeros((Cout, K), device=cuda)
+    _pack(w2, cuda, K, 0, wp)
+    _pack(ws, cuda, K, 9 * C1, wp)
+    ref = (F.conv2d(h.double(), w2.double(), b.double(), padding=1) + rv.double()[:, :, None, None]
+           + F.conv2d(x.double(), ws.double())).float()
+    y = _run_conv(cuda, _nhwc(h).to(cuda), wp, Cout, H, W, 9, bias=b.to(cuda), rowvec=rv.to(cuda),
+                  x2=_nhwc(x).to(cuda), Cin2=C2, tile=tile, split='fp16x2')
+    assert torch.equal(y.cpu(), _nhwc(ref))
+    sc = torch.ones((B, C1), device=cuda)
+    sh = torch.zeros((B, C1), device=cuda)
+    refp = (F.conv2d(F.silu(h.double()), w2.double(), b.double(), padding=1)).float()
+    y2 = _run_conv(cuda, _nhwc(h).to(cuda), _pack(w2, cuda), Cout, H, W, 9, bias=b.to(cuda), tile=tile,
+                   pro=(sc, sh), split='fp16x2')
+    assert (y2.cpu() - _nhwc(refp)).abs().max().item() <= 2e-4 * float(refp.abs().max())
