@@ -21,6 +21,7 @@
 #include "dm_kernels.h"
 #include "mfma_tile.h"
 #include "split16.h"
+#include "conv_epilogue.h"
 
 namespace dm {
 
@@ -268,12 +269,94 @@ __global__ void __launch_bounds__(256) attn_fused_kernel(AttnArgs a) {
         out[(size_t)(orow0 + i * 32 + acc_row(r, lh)) * a.ldo + ocol0 + j * 32 + lr] = oacc[i][j][r] * ounscale;
 }
 
+// The attention block's output projection for one head of C = 256 channels (models/modules.py:101,
+// proj 1x1 conv + residual; ADM proj_out), on the block's 64 O rows: O (wave w holds rows 0..63, columns
+// 64 w ..) goes through LDS (fp32 rows, then split in place into the A-operand layout, the O rows split
+// unscaled exactly as the MODE 3 conv splits its input), then each wave computes 64 rows x 64 output
+// channels from the pre-split weights (the conv's B-fragment images, same slice order) and runs the
+// conv epilogue (row scale, bias, residual, GroupNorm statistics): bit-identical to proj as its own launch.
+__device__ __forceinline__ void attn_proj(const ConvArgs& c, f16v (&oacc)[2][2], float ounscale, float* sp, int m0,
+                                          int wave, int lr, int lh) {
+  __syncthreads();  // every wave is done reading P
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        sp[(i * 32 + acc_row(r, lh)) * kSP + wave * 64 + j * 32 + lr] = oacc[i][j][r] * ounscale;
+  __syncthreads();
+  const int lane = lr + 32 * lh;
+  bool bad = false;
+  for (int row = wave * 16; row < wave * 16 + 16; ++row) {
+    float* srow = sp + row * kSP;
+    f4 v = *reinterpret_cast<const f4*>(srow + 4 * lane);   // 256 values: 4 per lane
+    _Float16* prow = reinterpret_cast<_Float16*>(srow);
+    f16x4 hi, lo;
+    Split<2>::split4(v, hi, lo, bad);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // the whole row is in registers before it is overwritten
+    __builtin_amdgcn_wave_barrier();
+    const int k = 4 * lane;
+    _Float16* dst = prow + (k >> 5) * kAP + split_off(k & 31);
+    *reinterpret_cast<f16x4*>(dst) = hi;
+    *reinterpret_cast<f16x4*>(dst + 8) = lo;
+  }
+  __syncthreads();
+  // 64 x 256 output tile: wave w owns columns 64 w .. 64 w + 63; K = 256 = 16 slices
+  const _Float16* A = reinterpret_cast<const _Float16*>(sp);
+  constexpr int PPITCH = 2 * kSP;
+  const int ngrp = c.Cout / 32;
+  const size_t slice_stride = (size_t)ngrp * (2 * 512);
+  const _Float16* wsrc[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+    wsrc[j] = reinterpret_cast<const _Float16*>(c.ws) + (size_t)((wave * 64 + j * 32) >> 5) * (2 * 512) + (lh * 32 + lr) * 8;
+  f16v acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  constexpr int RD = 4;
+  f16x8 bq[RD][2][2];
+  auto load_b = [&](int s, int slot) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) bq[slot][j][q] = *reinterpret_cast<const f16x8*>(wsrc[j] + (size_t)s * slice_stride + q * 512);
+  };
+#pragma unroll
+  for (int s = 0; s < RD; ++s) load_b(s, s);
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const int slot = s % RD;
+    f16x8 av[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        av[i][q] = *reinterpret_cast<const f16x8*>(A + (i * 32 + lr) * PPITCH + (s >> 1) * kAP + (s & 1) * 32 + lh * 16 +
+                                                   q * 8);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) Split<2>::mma(av[i], bq[slot][j], acc[i][j]);
+    load_b(min(s + RD, 15), slot);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (bad && c.range_flag) *c.range_flag = 1;
+  const int M = c.B * c.Hout * c.Wout, HWo = c.Hout * c.Wout;
+  conv_patch_epilogue<64, 256, 64, 64, 3, false, true>(c, acc, M, HWo, c.Wout, m0, 0, m0 / HWo, 0, wave, lr, lh, 0, 0, 0,
+                                                 c.ws_rowscale);
+}
+
 // Pre-split operands (AttnArgs::pq / pk / pv, written by the qkv conv's epilogue, conv_epilogue.h): every
 // MFMA operand fragment is one 16-B load from global (L2) per lane and piece, no LDS staging and no split
 // on the VALU. 64 query rows per block (74 KB of LDS for the S / P rows: two blocks per CU); q, k and
 // v^T slices ride a register ring RD slices ahead of their use. Same MFMA sequence as the unfused GEMMs.
 template <int DH>
-__global__ void __launch_bounds__(256) attn_presplit_kernel(AttnArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) attn_presplit_kernel(AttnArgs a) {
   static_assert(DH == 64 || DH == 256, "head dims 64 / 256");
   constexpr int QT = 64, NS = DH / 16, RD = 4;
   __shared__ __attribute__((aligned(16))) float sp[QT * kSP];
@@ -407,6 +490,12 @@ __global__ void __launch_bounds__(256) attn_presplit_kernel(AttnArgs a) {
   }
   const float ounscale = ldexpf(1.f, -(a.ep + a.ev));
   const int h = bh % a.heads, b = bh / a.heads;
+  if constexpr (DH == 256) {
+    if (a.fuse_proj) {  // 4. y = x + proj(O): the MODE 3 1x1 conv on this block's 64 O rows
+      attn_proj(a.proj, oacc, ounscale, sp, b * kAL + qt * QT, wave, lr, lh);
+      return;
+    }
+  }
   float* out = a.out + ((size_t)b * kAL + qt * QT) * a.ldo + h * DH;
 #pragma unroll
   for (int i = 0; i < TM; ++i)

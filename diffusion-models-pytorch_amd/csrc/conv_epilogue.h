@@ -49,7 +49,8 @@ __device__ __forceinline__ void conv_store_attn_planes(const ConvArgs& a, int m,
 // colscale (fp16x2 split kernels): the per-output-channel power-of-two weight scale to undo, applied to
 // each accumulator as it is read (exact), so the 16 x 16 accumulators of a 128 x 128 wave tile are never
 // materialised scaled all at once.
-template <int BM, int BN, int WM, int WN, int MODE, bool KSPLIT>
+// LEAN: no per-image row vector and no attention operand planes (the fused attention's proj)
+template <int BM, int BN, int WM, int WN, int MODE, bool KSPLIT, bool LEAN = false>
 __device__ __forceinline__ void conv_patch_epilogue(const ConvArgs& a, f16v (&acc)[WM / 32][WN / 32], int M,
                                                     int HWo, int Wo, int m0, int n0, int b0, int wm, int wn,
                                                     int lr, int lh, int split, int py, int px,
@@ -89,7 +90,7 @@ __device__ __forceinline__ void conv_patch_epilogue(const ConvArgs& a, f16v (&ac
     double gs = 0.0, gq = 0.0;
     const float bn = a.bias ? a.bias[n] : 0.f;
     const float cs = colscale ? colscale[n] : 1.f;
-    const float rv_blk = (a.rowvec && block_one_image) ? a.rowvec[(size_t)b0 * a.rowvec_pitch + n] : 0.f;
+    const float rv_blk = (!LEAN && a.rowvec && block_one_image) ? a.rowvec[(size_t)b0 * a.rowvec_pitch + n] : 0.f;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       // residual rows of this 32-row group loaded branch-free (clamped) before the stores, so the
@@ -120,9 +121,9 @@ __device__ __forceinline__ void conv_patch_epilogue(const ConvArgs& a, f16v (&ac
         }
         float v = colscale ? acc[i][j][r] * cs : acc[i][j][r];
         if (a.bias) v = v + bn;
-        if (a.rowvec) v = v + (block_one_image ? rv_blk : a.rowvec[(size_t)(m / HWo) * a.rowvec_pitch + n]);
+        if (!LEAN && a.rowvec) v = v + (block_one_image ? rv_blk : a.rowvec[(size_t)(m / HWo) * a.rowvec_pitch + n]);
         if (a.res) v = v + rsd[r];
-        if (MODE == 3 && a.ap_q) {
+        if (!LEAN && MODE == 3 && a.ap_q) {
           if (n_ok) conv_store_attn_planes(a, m, n, v);
           continue;
         }

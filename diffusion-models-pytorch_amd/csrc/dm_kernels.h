@@ -261,6 +261,11 @@ struct AttnArgs {
   int* range_flag;
   // pre-split operand planes written by the qkv conv (ConvArgs::ap_*); when set, qkv is not read
   const _Float16 *pq, *pk, *pv;
+  // one head of C channels (heads == 1): the attention output projection (a 1x1 MODE 3 conv with fp16x2
+  // split weights, bias, residual, GroupNorm statistics) applied by the same kernel to its O rows, so O
+  // never goes to HBM (`out` unused); proj.x1 is ignored
+  int fuse_proj;
+  ConvArgs proj;
 };
 bool attn_fused_ok(int L, int Dh);
 int attn_fused(const AttnArgs& a, hipStream_t st);

@@ -972,9 +972,28 @@ int UNetModel::build_plan(int B, int H, int W) {
       // (q | k | v blocks: modules.py:92-94 and ADM QKVAttention; per-head [q; k; v]: QKVAttentionLegacy)
       const int hs = p.legacy ? 3 * Dh : Dh;
       const int k0 = p.legacy ? Dh : C, v0 = p.legacy ? 2 * Dh : 2 * C;
+      // proj (1x1 conv, + bias + residual x): built here so that the fused kernel can apply it
+      GemmArgs gp{};
+      gp.M = B * hw; gp.N = C; gp.K = C; gp.Z1 = 1; gp.Z2 = 1; gp.pick_M = (long)kPickBatch * hw;
+      gp.A = Ob; gp.lda = C; gp.Bm = P(p.wproj); gp.ldb = C; gp.C = y.p; gp.ldc = y.pitch;
+      gp.alpha = 1.f; gp.bias = P(p.bproj); gp.res = xin.p; gp.ld_res = xin.pitch;
+      ConvArgs cp{};
+      cp.x1 = Ob; cp.x1_pitch = C; cp.Cin1 = C; cp.Hin = Hi; cp.Win = Wi; cp.taps = 1; cp.stride = 1;
+      cp.w = P(p.wproj); cp.K = C; cp.y = y.p; cp.y_pitch = y.pitch; cp.Cout = C; cp.B = B; cp.pick_B = kPickBatch; cp.Hout = Hi;
+      cp.Wout = Wi; cp.bias = P(p.bproj); cp.res = xin.p; cp.res_pitch = xin.pitch;
+      split_for(cp);
+      const bool proj_conv = conv_pw_ok(cp);
+      if (proj_conv) emit_conv(cp, y);
+      // one head of 256 channels (the CIFAR UNet's 16 x 16 attention): proj runs inside the fused kernel on
+      // its O rows (O never goes to HBM), same MFMA sequence and epilogue as the MODE 3 launch
+      const bool fuse_proj = presplit && proj_conv && heads == 1 && Dh == 256 && !std::getenv("DM_ATTN_NO_PROJ");
       if (fuse_attn) {
         // S, softmax and PV in one kernel (attention.hip), bit-identical to the three launches below
         AttnArgs at{};
+        if (fuse_proj) {
+          at.fuse_proj = 1;
+          at.proj = cp;
+        }
         if (presplit) {
           at.pq = planes; at.pk = planes + plane_n; at.pv = planes + 2 * plane_n;
         }
@@ -984,10 +1003,14 @@ int UNetModel::build_plan(int B, int H, int W) {
         at.out = Ob; at.ldo = C;
         at.ea = 6; at.eb = 6; at.ep = 14; at.ev = 6;
         at.range_flag = range_flag;
-        const double fl = 4.0 * B * heads * (double)hw * hw * Dh;
-        const double by = 4.0 * B * hw * (3.0 * C + C);
-        add((presplit ? "attn_presplit_kernel<" : "attn_fused_kernel<") + std::to_string(Dh) + ">", fl, by,
-            [=](hipStream_t st) { return attn_fused(at, st); });
+        double fl = 4.0 * B * heads * (double)hw * hw * Dh;
+        double by = 4.0 * B * hw * (3.0 * C + C);
+        if (fuse_proj) {  // + the proj GEMM; reads x (residual) and the weights, writes y instead of O
+          fl += 2.0 * B * hw * (double)C * C;
+          by += 4.0 * B * hw * C + 4.0 * C * C;
+        }
+        add((presplit ? "attn_presplit_kernel<" : "attn_fused_kernel<") + std::to_string(Dh) + (fuse_proj ? ",proj>" : ">"),
+            fl, by, [=](hipStream_t st) { return attn_fused(at, st); });
       } else {
       GemmArgs gs{};
       gs.M = hw; gs.N = hw; gs.K = Dh; gs.Z1 = B; gs.Z2 = heads; gs.pick_Z = (long)kPickBatch * heads;
@@ -1009,17 +1032,8 @@ int UNetModel::build_plan(int B, int H, int W) {
       split_gemm(go, 14, nullptr, 0, 6);
       add_gemm(go);
       }
-      GemmArgs gp{};
-      gp.M = B * hw; gp.N = C; gp.K = C; gp.Z1 = 1; gp.Z2 = 1; gp.pick_M = (long)kPickBatch * hw;
-      gp.A = Ob; gp.lda = C; gp.Bm = P(p.wproj); gp.ldb = C; gp.C = y.p; gp.ldc = y.pitch;
-      gp.alpha = 1.f; gp.bias = P(p.bproj); gp.res = xin.p; gp.ld_res = xin.pitch;
-      ConvArgs cp{};
-      cp.x1 = Ob; cp.x1_pitch = C; cp.Cin1 = C; cp.Hin = Hi; cp.Win = Wi; cp.taps = 1; cp.stride = 1;
-      cp.w = P(p.wproj); cp.K = C; cp.y = y.p; cp.y_pitch = y.pitch; cp.Cout = C; cp.B = B; cp.pick_B = kPickBatch; cp.Hout = Hi;
-      cp.Wout = Wi; cp.bias = P(p.bproj); cp.res = xin.p; cp.res_pitch = xin.pitch;
-      split_for(cp);
-      if (conv_pw_ok(cp)) {
-        emit_conv(cp, y);
+      if (fuse_proj) {
+      } else if (proj_conv) {
         add_conv(cp);
       } else {
         split_gemm(gp, 6, gp.Bm, (size_t)C * C);

@@ -343,17 +343,22 @@ def test_fused_attention_bit_identical(cuda, golden, arch, monkeypatch):
     """The fused attention kernels (attention.hip: S, softmax and PV on the CU; with q / k / v either split
     by the kernel or pre-split into operand planes by the qkv conv's epilogue) give the same bits as the
     three-launch path (split S GEMM, softmax_rows, split PV GEMM) they replace: CIFAR-10 (one head of
-    256 at 16x16) and CFG-CIFAR AdaGN (heads of 64 at 16x16) forwards."""
+    256 at 16x16) and CFG-CIFAR AdaGN (heads of 64 at 16x16) forwards. With one head of 256 the presplit
+    kernel also applies the block's output projection (+ bias + residual, GroupNorm statistics) to its O
+    rows; that too is bit-identical to the projection as its own MODE 3 launch (`noproj`)."""
     from models.unet_categorial_adagn import UNetCategorialAdaGN
     outs = {}
-    kernel = {'unfused': None, 'fused': 'attn_fused_kernel', 'presplit': 'attn_presplit_kernel'}
-    for mode in ('unfused', 'fused', 'presplit'):
-        monkeypatch.delenv('DM_ATTN_UNFUSED', raising=False)
-        monkeypatch.delenv('DM_ATTN_NO_PRESPLIT', raising=False)
+    kernel = {'unfused': None, 'fused': 'attn_fused_kernel', 'presplit': 'attn_presplit_kernel',
+              'noproj': 'attn_presplit_kernel'}
+    for mode in ('unfused', 'fused', 'noproj', 'presplit'):
+        for var in ('DM_ATTN_UNFUSED', 'DM_ATTN_NO_PRESPLIT', 'DM_ATTN_NO_PROJ'):
+            monkeypatch.delenv(var, raising=False)
         if mode == 'unfused':
             monkeypatch.setenv('DM_ATTN_UNFUSED', '1')
         elif mode == 'fused':
             monkeypatch.setenv('DM_ATTN_NO_PRESPLIT', '1')
+        elif mode == 'noproj':
+            monkeypatch.setenv('DM_ATTN_NO_PROJ', '1')
         if arch == 'cifar10':
             m, _ = _model(golden('forward')[1], 'cifar10', cuda)
         else:
@@ -367,7 +372,10 @@ def test_fused_attention_bit_identical(cuda, golden, arch, monkeypatch):
         labels = [op['label'] for op in _plan_labels(m, cuda)]
         for name in ('attn_fused_kernel', 'attn_presplit_kernel'):
             assert any(lb.startswith(name) for lb in labels) == (kernel[mode] == name), (mode, labels)
+        fused_proj = any(lb.endswith(',proj>') for lb in labels)
+        assert fused_proj == (mode == 'presplit' and arch == 'cifar10'), (mode, labels)
     assert torch.equal(outs['fused'], outs['unfused'])
+    assert torch.equal(outs['noproj'], outs['unfused'])
     assert torch.equal(outs['presplit'], outs['unfused'])
 
 
