@@ -59,11 +59,13 @@ def main():
     ap.add_argument('--write')
     ap.add_argument('--tag', default='r01')
     ap.add_argument('--command', default='')
+    ap.add_argument('--workload', default='c3')
     args = ap.parse_args()
     out_dir = os.path.join(ROOT, 'profiles')
     os.makedirs(out_dir, exist_ok=True)
     rows = kernel_stats(args.trace)
     path = os.path.join(out_dir, f'{args.tag}_kernel_stats.csv')
+    # (the workload is in the tag of the run's files; the CSV keeps rocprofv3's --stats columns)
     with open(path, 'w', newline='') as f:
         w = csv.DictWriter(f, fieldnames=list(rows[0].keys()))
         w.writeheader()
@@ -82,7 +84,7 @@ def main():
                                     fetch_size_kib=fetch.get(name), write_size_kib=write.get(name))
         meta = dict(note='read = 2 x FETCH_SIZE (gfx950 half-count of 16B/lane coalesced reads); '
                          'write = WRITE_SIZE (exact for 16B stores, uncalibrated for 4B stores)',
-                    command=args.command, kernels=res)
+                    command=args.command, workload=args.workload, kernels=res)
         path = os.path.join(out_dir, f'{args.tag}_pmc.json')
         with open(path, 'w') as f:
             json.dump(meta, f, indent=1, sort_keys=True)
