@@ -278,13 +278,14 @@ int conv2d_igemm(const ConvArgs& a, hipStream_t st) {
   }
   const long M = (long)a.B * a.Hout * a.Wout;
   DM_REQUIRE(M > 0 && M < (1L << 31), "conv: M out of range");
-  DM_REQUIRE(a.tile >= 0 && a.tile <= 9, "conv: tile must be 0..9");
+  DM_REQUIRE(a.tile >= 0 && a.tile <= 11, "conv: tile must be 0..11");
   const int mode = conv_mode(a);
   const int pick = conv_pick(a);
   DM_REQUIRE(!a.gn_part || conv_can_emit_gn(a), "conv: GroupNorm statistics need a 128-row halo-patch tile, "
                                                  "whole 64-pixel chunks and groups within 32 channels");
   DM_REQUIRE(!a.pro_scale || (pick >= 3 && a.pro_shift && aligned16(a.pro_scale) && aligned16(a.pro_shift)),
              "conv: the GroupNorm prologue needs a halo-patch shape (3x3 stride 1 / upsample, whole-row tiles)");
+  if (const int k32 = conv_k32_pick(a)) return conv2d_k32(a, k32, st);
   if (pick >= 3 && a.taps == 1) return conv2d_patch3(a, pick + 1, PatchGeom{}, st);  // MODE 3 (split 1x1)
   if (pick >= 3) {
     PatchGeom g;
@@ -310,6 +311,7 @@ int conv2d_igemm(const ConvArgs& a, hipStream_t st) {
 // falls back to im2col when the shape does not tile.
 int conv_pick(const ConvArgs& a) {
   if (a.tile >= 1 && a.tile <= 3) return a.tile - 1;
+  if ((a.tile == 10 || a.tile == 11) && conv_k32_ok(a)) return a.tile - 7;  // forced K = 32 split tiles (conv_k32.hip)
   if (conv_pw_ok(a)) {  // split 1x1: 128x128 tiles when they still give >= 2 blocks per CU, else 128x64
     const long M = (long)(a.pick_B > 0 ? a.pick_B : a.B) * a.Hout * a.Wout;
     return (a.Cout >= 128 && ((M + 127) / 128) * ((a.Cout + 127) / 128) >= 512) ? 3 : 4;
@@ -333,6 +335,7 @@ bool conv_can_emit_gn(const ConvArgs& a) {
            a.Cout <= 1024;
   const int pick = conv_pick(a);
   if (pick != 3 && pick != 4 && pick != 6 && pick != 7 && pick != 8) return false;  // waves own whole 64-row chunks
+  if (conv_k32_pick(a) && a.Cout % a.gn_G == 0 && a.Cout / a.gn_G > 16) return false;  // K32: groups within 16 columns
   if (a.upsample || (a.ksplit > 1)) return false;
   if (a.taps == 1 && !conv_pw_ok(a)) return false;
   if ((a.Hout * a.Wout) % 64 != 0 || a.gn_G <= 0 || a.Cout % a.gn_G != 0) return false;
@@ -347,6 +350,9 @@ std::string conv_label(const ConvArgs& a) {
                                 "conv_patch_kernel<128,64,64,32",  "conv_patch_kernel<64,64,32,32",
                                 "conv_patch_kernel<256,256,128,128", "conv_patch_kernel<512,128,128,128",
                                 "conv_patch_kernel<128,128,64,64"};
+  if (const int k32 = conv_k32_pick(a))  // conv_k32_kernel<BN,WN,PRO>
+    return std::string(k32 == 128 ? "conv_k32_kernel<128,64," : "conv_k32_kernel<64,32,") +
+           (a.pro_scale ? "true>" : "false>");
   const int p = conv_pick(a);
   std::string s = names[p];
   if (p < 3) s += "," + std::to_string(conv_mode(a)) + ">";  // <BM,BN,WM,WN,MODE>

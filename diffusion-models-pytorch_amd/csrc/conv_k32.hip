@@ -1,0 +1,431 @@
+// 3x3 stride-1 convolution on the fp16x2 split matrix cores with 32-channel K steps:
+// v_mfma_f32_16x16x32_f16 instead of conv_patch3.hip's v_mfma_f32_32x32x16_f16.
+//
+// Same numerics as conv_patch3.hip's fp16x2 variant (models/unet.py:16,26 convolve in fp32): every
+// fp32 operand x = h0 + h1 (h0 = fp16(x), h1 = fp16(x - h0)), a*w = a1w0 + a0w1 + a0w0 issued as three
+// MFMAs into one fp32 accumulator, weights scaled per output channel by a power of two that the
+// epilogue undoes. What changes is the MFMA shape and with it the loop structure:
+//
+// * Shape. 16x16x32 and 32x32x16 take the same cycles per FLOP, but on random operands the chip holds
+//   a higher clock under 16x16x32 (tools/mfma_peak.hip on MI355X: 1.87 vs 1.70 PF dense fp16,
+//   MI355X_MICROARCH.md "DVFS give-back" (7)).
+// * K per barrier. One chunk is 32 input channels: each of the 9 taps is one K = 32 step (48 MFMAs
+//   per wave for a 64 x 64 wave tile), so a chunk is twice the matrix work of conv_patch3's 16-channel
+//   chunk per barrier, and the next chunk's patch loads have twice as long to land.
+//
+// Operands. A (activations): per chunk the (TH + 2) x (W + 2) input patch is loaded once, GroupNorm +
+// SiLU'd (tables in LDS), split and stored in LDS as rows of [piece][4 k-groups][8 fp16] with a
+// 160-B pitch (10 x 16-B slots: the ds_read_b128 lane groups of a 16-row fragment are conflict free,
+// the ds_write_b128 of the loader 2-way); all 9 taps read shifted fragments from it. Lane (r, q) of
+// a 16x16x32 MFMA reads row r, k-group q (channels 8q .. 8q+7 of the chunk). B (weights): the fp16x2
+// fragment images split_conv_weights already builds for conv_patch3 ([16-deep slice][32-column
+// group][piece][2 lane groups][32][8]); lane (r, q) of column group j reads column r of the 16, k-group
+// q & 1 of 16-slice (2c + (q >> 1)) * 9 + tap -- k = 8q + e of the 32-deep step, the same relabelling
+// as A. Loaded from L2 into a 2-deep register ring, no LDS stage.
+//
+// Tiles: 128 x BN blocks (BN 128 or 64) of 4 waves, 64 x WN wave tiles, whole image rows of 16- or
+// 32-pixel-wide maps (a 16-pixel fragment never straddles an image row). LDS: 2 x 208 x 160 B patch
+// buffers + 4.5 KiB of GroupNorm tables = 71 KiB -> two blocks per CU.
+#include <cstdlib>
+
+#include "dm_common.h"
+#include "dm_kernels.h"
+#include "mfma_tile.h"
+#include "split16.h"
+
+namespace dm {
+
+namespace {
+
+constexpr int BM_K32 = 128;   // block rows (output pixels)
+constexpr int kC = 32;          // input channels per chunk = K of one tap's MFMA step
+constexpr int kRowH = 80;       // LDS row pitch in fp16: 160 B; [piece][k-group][8] (piece at +32)
+constexpr int kMaxP = 208;      // patch pixels: 32^2 maps 6 x 34, 16^2 maps 10 x 18
+constexpr int kTab = 1024;      // GroupNorm table floats (one image: Cin1 scales + Cin1 shifts)
+constexpr int kStats = 128;     // (image, group) pairs of the in-kernel finalize
+
+template <int BN, int WN, bool PRO>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) conv_k32_kernel(ConvArgs a, PatchGeom g) {
+  constexpr int BM = 128, WM = 64;
+  constexpr int NWN = BN / WN;
+  static_assert((BM / WM) * NWN == 4, "4 waves per block");
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int PJ = (kMaxP + 63) / 64;  // loader passes of 64 pixels (4 threads per pixel)
+  constexpr int PATCH = kMaxP * kRowH;
+  constexpr int NTAP = 9, WD = 2, CPI = 2;  // B ring depth; chunks per loop iteration (slot = compile-time)
+  __shared__ __attribute__((aligned(16))) _Float16 patch[2 * PATCH];
+  __shared__ __attribute__((aligned(16))) float gtab[PRO ? kTab : 4];
+  __shared__ float gstat[PRO ? 2 * kStats : 2];
+
+  const int Ho = a.Hout, Wo = a.Wout;
+  const int M = a.B * Ho * Wo, N = a.Cout;
+  const int nN = ceil_div(N, BN);
+  const int bid = xcd_remap_p(blockIdx.x, gridDim.x);
+  const int mt = bid / nN, nt = bid - (bid / nN) * nN;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int HWo = Ho * Wo;
+  const int b0 = m0 / HWo;
+  const int y0 = (m0 - b0 * HWo) / Wo;
+
+  const int t = threadIdx.x;
+  const int lane = t & 63, wave = t >> 6;
+  const int wm = wave / NWN, wn = wave % NWN;
+  const int l16 = lane & 15, q = lane >> 4;
+  const int srow = t >> 2, sq = t & 3;  // loader: pixel slot, 8-channel quarter of the chunk
+
+  // ---- patch loader geometry: pixel p = srow + 64 j of the TB x PH x PW patch
+  const float* psrc[PJ];
+  bool pok[PJ];
+  int pimg[PJ];
+#pragma unroll
+  for (int j = 0; j < PJ; ++j) {
+    const int PHW = g.PH * g.PW;
+    const int p = srow + 64 * j;
+    const int img = p / PHW;
+    const int rem = p - img * PHW;
+    const int pr = rem / g.PW, pc = rem - (rem / g.PW) * g.PW;
+    const int b = b0 + img;
+    const int iy = y0 - 1 + pr, ix = pc - 1;
+    const bool ok = p < g.P && b < a.B && iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
+    pok[j] = ok;
+    const int bc = min(b, a.B - 1);
+    pimg[j] = bc;
+    const int iyc = min(max(iy, 0), a.Hin - 1), ixc = min(max(ix, 0), a.Win - 1);
+    psrc[j] = (ok || PRO) ? a.x1 + ((size_t)(bc * a.Hin + iyc) * a.Win + ixc) * a.x1_pitch + 8 * sq
+                          : kZeroPage + 8 * sq;
+  }
+
+  // ---- B operand: conv_patch3's fp16x2 fragment images, 16-column halves of the 32-column groups
+  const int ngrp = ceil_div(N, 32);
+  const size_t sl = (size_t)ngrp * 1024;  // fp16 elements per 16-deep slice
+  const _Float16* wbase[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + wn * WN + j * 16 + l16;
+    const int grp = min(col >> 5, ngrp - 1);  // columns >= N: clamped / zero padding, never stored
+    wbase[j] = reinterpret_cast<const _Float16*>(a.ws) + (size_t)grp * 1024 + ((q & 1) * 32 + (col & 31)) * 8;
+  }
+  const size_t qoff = (size_t)(q >> 1) * NTAP * sl;  // k-groups 2, 3: the chunk's second 16-slice of the tap
+  // step kt = c * 9 + tap of the main segment: 16-slices 2c * 9 + tap (+ 9 for k-groups 2, 3)
+  auto slice_off = [&](int kt) { return (size_t)(kt + (kt / NTAP) * NTAP) * sl + qoff; };
+  f16x8 bq[WD][TN][2];
+  auto load_b = [&](f16x8 (&dst)[TN][2], size_t off) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) dst[j][p] = *reinterpret_cast<const f16x8*>(wbase[j] + off + p * 512);
+  };
+
+  // ---- A-fragment patch rows of this lane (row l16 of each 16-row tile)
+  int fy[TM], fx[TM], fimg[TM];
+  const int tile_rows = g.TH * g.TW;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int ml = wm * WM + i * 16 + l16;
+    fimg[i] = ml / tile_rows;
+    const int rem = ml - fimg[i] * tile_rows;
+    fy[i] = rem / g.TW;
+    fx[i] = rem - fy[i] * g.TW;
+  }
+
+  // patch registers of two loader passes: passes 0, 1 and 2, 3 of the next chunk take turns
+  f4 rp[2][2];
+  auto load_patch = [&](int chunk, int j0) {
+    const int co = chunk * kC;
+#pragma unroll
+    for (int j = j0; j < j0 + 2; ++j) {
+      rp[j & 1][0] = *reinterpret_cast<const f4*>(psrc[j] + co);
+      rp[j & 1][1] = *reinterpret_cast<const f4*>(psrc[j] + co + 4);
+    }
+  };
+  const bool pro_silu = !a.pro_nosilu;
+  const int tab_img0 = b0;
+  const int tab_n = PRO ? min(b0 + g.TB, a.B) - b0 : 0;
+  // GroupNorm + SiLU of passes j0, j0 + 1 (tables from LDS), then split and store them into buffer buf
+  // (padding stays exactly 0: applied after the transform)
+  bool bad = false;
+  auto finish_patch = [&](int chunk, int j0, int buf) {
+    _Float16* dst = patch + buf * PATCH;
+    const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = j0; j < j0 + 2; ++j) {
+      if (PRO) {
+        const float* ts = gtab + min(pimg[j] - tab_img0, tab_n - 1) * a.Cin1 + chunk * kC + 8 * sq;
+        f4 sc[2], sh[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          sc[h] = *reinterpret_cast<const f4*>(ts + 4 * h);
+          sh[h] = *reinterpret_cast<const f4*>(ts + tab_n * a.Cin1 + 4 * h);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float v = rp[j & 1][h][e] * sc[h][e] + sh[h][e];
+            rp[j & 1][h][e] = pro_silu ? silu_fast(v) : v;
+          }
+      }
+      const int p = srow + 64 * j;
+      if (j * 64 < kMaxP && p < kMaxP) {
+        f16x8 pc[2];
+        const bool z = PRO && !pok[j];
+        Split<2>::split(z ? zero4 : rp[j & 1][0], z ? zero4 : rp[j & 1][1], pc, bad);
+        *reinterpret_cast<f16x8*>(dst + p * kRowH + sq * 8) = pc[0];
+        *reinterpret_cast<f16x8*>(dst + p * kRowH + 32 + sq * 8) = pc[1];
+      }
+    }
+  };
+
+  f4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  // one K = 32 step: A rows at LDS element offsets abase[i] (lane's k-group included), B in registers
+  auto compute = [&](const _Float16* As, const int (&abase)[TM], const f16x8 (&bv)[TN][2]) {
+    f16x8 av[TM][2];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) av[i][p] = *reinterpret_cast<const f16x8*>(As + abase[i] + p * 32);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[i][1], bv[j][0], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[i][0], bv[j][1], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[i][0], bv[j][0], acc[i][j], 0, 0, 0);
+      }
+  };
+  auto compute_tap = [&](int ky, int kx, int pbuf, const f16x8 (&bv)[TN][2]) {
+    int abase[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+      abase[i] = ((fimg[i] * g.PH + fy[i] + ky) * g.PW + fx[i] + kx) * kRowH + q * 8;
+    compute(patch + pbuf * PATCH, abase, bv);
+  };
+
+  const int nchunks = a.Cin1 / kC;
+  const int kt_end = nchunks * NTAP;
+#pragma unroll
+  for (int d = 0; d < WD; ++d) load_b(bq[d], slice_off(min(d, kt_end - 1)));
+  if (PRO) {
+    if (a.gin_part) {
+      // gn_finalize (gn.hip) for the tile's images, same expressions (conv_patch3.hip's in-kernel finalize)
+      const int G = a.gin_G, cpg = a.Cin1 / G;
+      for (int i = t; i < tab_n * G; i += 256) {
+        const int b = tab_img0 + i / G, gg = i - (i / G) * G;
+        double s1 = 0, s2 = 0;
+        for (int k = 0; k < a.gin_nchunk; ++k) {
+          const double2 v = a.gin_part[((size_t)b * a.gin_nchunk + k) * G + gg];
+          s1 += v.x;
+          s2 += v.y;
+        }
+        const double mu = s1 / a.gin_n;
+        double var = s2 / a.gin_n - mu * mu;
+        if (var < 0) var = 0;
+        gstat[2 * i] = (float)mu;
+        gstat[2 * i + 1] = (float)(1.0 / sqrt(var + (double)a.gin_eps));
+      }
+      __syncthreads();
+      for (int i = t; i < tab_n * a.Cin1; i += 256) {
+        const int bi = i / a.Cin1, c = i - (i / a.Cin1) * a.Cin1;
+        const int si = 2 * (bi * G + c / cpg);
+        const float mu = gstat[si], rs = gstat[si + 1];
+        float sc = rs * (a.gin_gamma ? a.gin_gamma[c] : 1.0f);
+        float sh = -sc * mu + (a.gin_beta ? a.gin_beta[c] : 0.0f);
+        if (a.gin_ms) {
+          const size_t mo = (size_t)(tab_img0 + bi) * a.gin_mp + c;
+          const float f = 1.0f + a.gin_ms[mo];
+          sc = sc * f;
+          sh = sh * f + (a.gin_mb ? a.gin_mb[mo] : 0.0f);
+        }
+        gtab[i] = sc;
+        gtab[tab_n * a.Cin1 + i] = sh;
+      }
+    } else {
+      for (int i = t; i < tab_n * a.Cin1; i += 256) {
+        gtab[i] = a.pro_scale[(size_t)tab_img0 * a.Cin1 + i];
+        gtab[tab_n * a.Cin1 + i] = a.pro_shift[(size_t)tab_img0 * a.Cin1 + i];
+      }
+    }
+    __syncthreads();
+  }
+  load_patch(0, 0);
+  finish_patch(0, 0, 0);
+  load_patch(0, 2);
+  finish_patch(0, 2, 0);
+  __syncthreads();
+  // One barrier per chunk (double-buffered patch; the other buffer is free once every wave has passed
+  // the previous chunk's barrier). The next chunk's patch goes in two halves: passes 0, 1 loaded at tap
+  // 0 and finished (GroupNorm + SiLU, split, LDS store) at tap 2, passes 2, 3 loaded at tap 3 and
+  // finished at tap 5 -- each load has two taps (96 MFMAs) to land.
+  for (int c0 = 0; c0 < nchunks; c0 += CPI) {
+#pragma unroll
+    for (int cc = 0; cc < CPI; ++cc) {
+      const int c = c0 + cc;
+      if (c >= nchunks) break;
+      const int cn = min(c + 1, nchunks - 1);  // after the last chunk: reloaded into an unused buffer
+#pragma unroll
+      for (int tap = 0; tap < NTAP; ++tap) {
+        const int kt = c * NTAP + tap;
+        const int slot = (cc * NTAP + tap) % WD;
+        if (tap == 0 || tap == 3) {
+          load_patch(cn, tap == 0 ? 0 : 2);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        compute_tap(tap / 3, tap % 3, c & 1, bq[slot]);
+        load_b(bq[slot], slice_off(min(kt + WD, kt_end - 1)));
+        __builtin_amdgcn_sched_barrier(0);  // keep the refill WD taps ahead
+        if (tap == 2 || tap == 5) finish_patch(cn, tap == 2 ? 0 : 2, (c + 1) & 1);
+      }
+      __syncthreads();
+    }
+  }
+
+  // ---- segment 2: 1x1 product of x2 (the ResBlock shortcut), K = Cin2 in 32-channel steps, un-pipelined
+  if (a.Cin2 > 0) {
+    const size_t s2 = (size_t)(NTAP * a.Cin1 / 16) * sl + (size_t)(q >> 1) * sl;  // 16-slices 9 Cin1/16 + 2 c2 + (q>>1)
+    int abase[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) abase[i] = (wm * WM + i * 16 + l16) * kRowH + q * 8;
+    const float* xsrc[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      xsrc[j] = a.x2 + (size_t)min(m0 + srow + 64 * j, M - 1) * a.x2_pitch + 8 * sq;
+    for (int c2 = 0; c2 < a.Cin2 / kC; ++c2) {
+      f4 r[2][2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        r[j][0] = *reinterpret_cast<const f4*>(xsrc[j] + c2 * kC);
+        r[j][1] = *reinterpret_cast<const f4*>(xsrc[j] + c2 * kC + 4);
+      }
+      load_b(bq[0], s2 + (size_t)(2 * c2) * sl);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {  // rows >= M hold clamped data: never stored
+        f16x8 pc[2];
+        Split<2>::split(r[j][0], r[j][1], pc, bad);
+        const int row = srow + 64 * j;
+        *reinterpret_cast<f16x8*>(patch + row * kRowH + sq * 8) = pc[0];
+        *reinterpret_cast<f16x8*>(patch + row * kRowH + 32 + sq * 8) = pc[1];
+      }
+      __syncthreads();
+      compute(patch, abase, bq[0]);
+      __syncthreads();
+    }
+  }
+  if (bad && a.range_flag) *a.range_flag = 1;
+
+  // ---- epilogue: lane (l16, q) holds column l16 of each 16-column tile, rows 4q .. 4q+3 of each
+  // 16-row tile. Row scale undo, bias, per-image row vector, residual, GroupNorm statistics of the
+  // stored values (the wave's 64 rows are one 64-pixel chunk of one image when HW % 64 == 0).
+  const bool block_one_image = (HWo % BM) == 0;
+  const bool emit = a.gn_part != nullptr;
+  const int wrow0 = m0 + wm * WM;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n_raw = n0 + wn * WN + j * 16 + l16;
+    const bool n_ok = n_raw < N;
+    const int n = n_ok ? n_raw : N - 1;
+    const float bn = a.bias ? a.bias[n] : 0.f;
+    const float cs = a.ws_rowscale[n];
+    const float rv_blk = (a.rowvec && block_one_image) ? a.rowvec[(size_t)b0 * a.rowvec_pitch + n] : 0.f;
+    double gs = 0.0, gq = 0.0;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      float rsd[4];
+      if (a.res) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = min(wrow0 + i * 16 + 4 * q + r, M - 1);
+          rsd[r] = a.res[(size_t)m * a.res_pitch + n];
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = wrow0 + i * 16 + 4 * q + r;
+        if (m >= M) continue;
+        float v = acc[i][j][r] * cs;
+        if (a.bias) v = v + bn;
+        if (a.rowvec) v = v + (block_one_image ? rv_blk : a.rowvec[(size_t)(m / HWo) * a.rowvec_pitch + n]);
+        if (a.res) v = v + rsd[r];
+        if (n_ok) a.y[(size_t)m * a.y_pitch + n] = v;
+        if (emit) {
+          gs += (double)v;
+          gq += (double)v * v;
+        }
+      }
+    }
+    if (emit) {  // the wave's 64 rows: combine the four row quarters, then the group's columns
+      gs += __shfl_xor(gs, 16);
+      gq += __shfl_xor(gq, 16);
+      gs += __shfl_xor(gs, 32);
+      gq += __shfl_xor(gq, 32);
+      const int cpg = N / a.gn_G;
+      for (int o = 1; o < cpg; o <<= 1) {
+        gs += __shfl_xor(gs, o);
+        gq += __shfl_xor(gq, o);
+      }
+      const int nchunk = (HWo + 63) / 64;
+      const int bb = wrow0 / HWo, ch = (wrow0 - bb * HWo) / 64;
+      if (q == 0 && (l16 % cpg) == 0 && n_ok && wrow0 < M)
+        a.gn_part[((size_t)bb * nchunk + ch) * a.gn_G + n_raw / cpg] = make_double2(gs, gq);
+    }
+  }
+}
+
+}  // namespace
+
+bool conv_k32_ok(const ConvArgs& a) {
+  if (!(a.ws && a.ws_np == 2 && a.ws_rowscale && a.taps == 9 && a.stride == 1 && a.upsample == 0 && a.ksplit <= 1))
+    return false;
+  if (a.Cin1 < kC || a.Cin1 % kC != 0 || a.Cin2 % kC != 0 || a.K != 9 * a.Cin1 + a.Cin2) return false;
+  if (a.Wout < 16 || a.Wout % 16 != 0 || BM_K32 % a.Wout != 0) return false;
+  PatchGeom g;
+  if (!conv_patch_geom(a, BM_K32, g) || g.P > kMaxP || g.TB != 1) return false;
+  if (a.pro_scale && 2 * a.Cin1 > kTab) return false;
+  if (a.gin_part && a.gin_G > kStats) return false;
+  if (a.gn_part && (a.gn_G <= 0 || a.Cout % a.gn_G != 0 || a.Cout / a.gn_G > 16 || (a.Hout * a.Wout) % 64 != 0))
+    return false;
+  return true;
+}
+
+// Which conv_k32 tile (128: 128 x 128, 64: 128 x 64) runs this conv, 0 = none. Forced by tile 10 / 11;
+// otherwise it replaces conv_patch3's fp16x2 128 x 128 / 128 x 64 tiles (picks 3 / 4) unless
+// DM_CONV_K32=0.
+int conv_k32_pick(const ConvArgs& a) {
+  if (a.tile == 10 || a.tile == 11) return conv_k32_ok(a) ? (a.tile == 10 ? 128 : 64) : 0;
+  if (a.tile != 0) return 0;
+  static const bool off = [] {
+    const char* e = std::getenv("DM_CONV_K32");
+    return e && e[0] == '0';
+  }();
+  if (off || !conv_k32_ok(a)) return 0;
+  const int p = conv_pick(a);
+  return p == 3 ? 128 : p == 4 ? 64 : 0;
+}
+
+int conv2d_k32(const ConvArgs& a, int bn, hipStream_t st) {
+  DM_REQUIRE(conv_k32_ok(a), "conv: shape not supported by the K = 32 split kernel");
+  DM_REQUIRE(bn == 128 || bn == 64, "conv: K = 32 split kernel tiles are 128 x 128 and 128 x 64");
+  PatchGeom g;
+  conv_patch_geom(a, BM_K32, g);
+  const int M = a.B * a.Hout * a.Wout;
+  const int blocks = ceil_div(M, BM_K32) * ceil_div(a.Cout, bn);
+  if (bn == 128) {
+    if (a.pro_scale)
+      hipLaunchKernelGGL((conv_k32_kernel<128, 64, true>), dim3(blocks), dim3(256), 0, st, a, g);
+    else
+      hipLaunchKernelGGL((conv_k32_kernel<128, 64, false>), dim3(blocks), dim3(256), 0, st, a, g);
+  } else {
+    if (a.pro_scale)
+      hipLaunchKernelGGL((conv_k32_kernel<64, 32, true>), dim3(blocks), dim3(256), 0, st, a, g);
+    else
+      hipLaunchKernelGGL((conv_k32_kernel<64, 32, false>), dim3(blocks), dim3(256), 0, st, a, g);
+  }
+  DM_LAUNCH_CHECK();
+  return DM_OK;
+}
+
+}  // namespace dm

@@ -1,0 +1,84 @@
+"""The K = 32 fp16x2 split conv (conv_k32.hip: v_mfma_f32_16x16x32_f16, 32-channel chunks) against fp64
+torch references, as tests/test_gpu_conv_split.py does for conv_patch3: integer operands compare bit for
+bit (indexing, padding, tap walk, both K segments, epilogue), random operands must keep fp32-level
+accuracy (within 2x of the fp32 MFMA kernel's error vs fp64), and an activation beyond fp16's range must
+raise the range flag. Tiles: 10 = 128 x 128, 11 = 128 x 64 (forced); 0 = the automatic choice, which
+takes this kernel for the 16- / 32-pixel-wide maps the UNets run at 128-row tiles."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from tests.test_gpu_conv_split import _rand_case
+from tests.test_gpu_ops import _ints, _nhwc, _pack, _run_conv
+
+pytestmark = pytest.mark.gpu
+TILES = [10, 11, 0]
+
+
+@pytest.mark.parametrize('tile', TILES)
+@pytest.mark.parametrize('B,Cin,Cout,H', [
+    (1, 128, 256, 16), (2, 32, 64, 16), (2, 96, 96, 32), (1, 64, 128, 32), (3, 160, 64, 16), (1, 256, 160, 32),
+])
+def test_k32_conv3x3_exact(cuda, B, Cin, Cout, H, tile):
+    x = _ints((B, Cin, H, H), -2, 3, seed=10)
+    w = _ints((Cout, Cin, 3, 3), -2, 3, seed=11)
+    b = _ints((Cout, ), seed=12)
+    ref = F.conv2d(x.double(), w.double(), b.double(), padding=1).float()
+    y = _run_conv(cuda, _nhwc(x).to(cuda), _pack(w, cuda), Cout, H, H, 9, 1, 0, b.to(cuda), tile=tile,
+                  split='fp16x2')
+    assert torch.equal(y.cpu(), _nhwc(ref))
+
+
+@pytest.mark.parametrize('tile', TILES)
+@pytest.mark.parametrize('C1,C2,H', [(64, 32, 16), (96, 64, 32), (32, 128, 16)])
+def test_k32_segments_rowvec_residual_pitch(cuda, tile, C1, C2, H):
+    """ResBlock conv2: 3x3 over h + the 1x1 shortcut of x as a second K segment, temb row vector,
+    residual, pitched output (untouched beyond Cout)."""
+    B, Cout = 3, 64
+    h = _ints((B, C1, H, H), seed=20)
+    x = _ints((B, C2, H, H), seed=21)
+    w2 = _ints((Cout, C1, 3, 3), -2, 3, seed=22)
+    ws = _ints((Cout, C2, 1, 1), seed=23)
+    b = _ints((Cout, ), seed=24)
+    rv = _ints((B, Cout), seed=25)
+    res = _ints((B, Cout, H, H), seed=26)
+    K = 9 * C1 + C2
+    wp = torch.zeros((Cout, K), device=cuda)
+    _pack(w2, cuda, K, 0, wp)
+    _pack(ws, cuda, K, 9 * C1, wp)
+    ref = (F.conv2d(h.double(), w2.double(), b.double(), padding=1) + rv.double()[:, :, None, None]
+           + F.conv2d(x.double(), ws.double()) + res.double()).float()
+    y = _run_conv(cuda, _nhwc(h).to(cuda), wp, Cout, H, H, 9, bias=b.to(cuda), rowvec=rv.to(cuda),
+                  res=_nhwc(res).to(cuda), x2=_nhwc(x).to(cuda), Cin2=C2, y_pitch=96, tile=tile, split='fp16x2')
+    assert torch.equal(y[..., :Cout].cpu(), _nhwc(ref))
+    assert torch.isnan(y[..., Cout:]).all()
+
+
+@pytest.mark.parametrize('B,Cin,Cout,H', [(4, 128, 128, 32), (8, 256, 256, 16), (2, 384, 128, 32),
+                                          (4, 512, 256, 16)])
+def test_k32_fp32_accuracy(cuda, B, Cin, Cout, H):
+    """fused GroupNorm + SiLU conv on random data: the K = 32 kernel's error vs fp64 is within 2x the
+    fp32 MFMA kernel's (and of the same size as conv_patch3's fp16x2 128-row tile)."""
+    xd, wp, b, pro, ref = _rand_case(cuda, B, Cin, Cout, H, 0, seed=90)
+    errs = {}
+    for name, split, tile in (('fp32', False, 0), ('patch3', 'fp16x2', 4), ('k32', 'fp16x2', 10),
+                              ('k32_64', 'fp16x2', 11)):
+        y = _run_conv(cuda, xd, wp, Cout, H, H, 9, 1, 0, b.to(cuda), pro=pro, split=split, tile=tile)
+        errs[name] = (y.cpu().double() - _nhwc(ref)).abs().max().item()
+    scale = ref.abs().max().item()
+    for k in ('k32', 'k32_64'):
+        assert errs[k] < 2.0 * errs['fp32'] + 1e-7 * scale, errs
+        assert errs[k] < 4e-6 * scale, (errs, scale)
+
+
+def test_k32_range_flag(cuda):
+    """An activation beyond 65504 (no fp16 image) raises the range flag; in range it stays clear."""
+    B, C, H = 2, 64, 16
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn((B, C, H, H), generator=g)
+    w = torch.randn((C, C, 3, 3), generator=g) * 0.05
+    wp = _pack(w, cuda)
+    for scale, expect in ((1.0, 0), (1e5, 1)):
+        flag = torch.zeros(1, dtype=torch.int32, device=cuda)
+        _run_conv(cuda, _nhwc(x * scale).to(cuda), wp, C, H, H, 9, 1, 0, tile=10, split='fp16x2', range_flag=flag)
+        assert int(flag.item()) == expect
