@@ -350,9 +350,7 @@ std::string conv_label(const ConvArgs& a) {
                                 "conv_patch_kernel<128,64,64,32",  "conv_patch_kernel<64,64,32,32",
                                 "conv_patch_kernel<256,256,128,128", "conv_patch_kernel<512,128,128,128",
                                 "conv_patch_kernel<128,128,64,64"};
-  if (const int k32 = conv_k32_pick(a))  // conv_k32_kernel<BN,WN,PRO>
-    return std::string(k32 == 128 ? "conv_k32_kernel<128,64," : "conv_k32_kernel<64,32,") +
-           (a.pro_scale ? "true>" : "false>");
+  if (const int k32 = conv_k32_pick(a)) return conv_k32_label(a, k32);
   const int p = conv_pick(a);
   std::string s = names[p];
   if (p < 3) s += "," + std::to_string(conv_mode(a)) + ">";  // <BM,BN,WM,WN,MODE>

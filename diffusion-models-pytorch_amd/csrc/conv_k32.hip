@@ -27,6 +27,7 @@
 // 32-pixel-wide maps (a 16-pixel fragment never straddles an image row). LDS: 2 x 208 x 160 B patch
 // buffers + 4.5 KiB of GroupNorm tables = 71 KiB -> two blocks per CU.
 #include <cstdlib>
+#include <string>
 
 #include "dm_common.h"
 #include "dm_kernels.h"
@@ -44,9 +45,28 @@ constexpr int kMaxP = 208;      // patch pixels: 32^2 maps 6 x 34, 16^2 maps 10 
 constexpr int kTab = 1024;      // GroupNorm table floats (one image: Cin1 scales + Cin1 shifts)
 constexpr int kStats = 128;     // (image, group) pairs of the in-kernel finalize
 
-template <int BN, int WN, bool PRO>
+
+#ifdef DM_K32_STAMPS
+// Diagnostic build only (-DDM_K32_STAMPS, tools/k32_stamps.py): per block, wave 0's s_memtime at the
+// kernel start, after the prologue, after the main loop, before and after the epilogue, and
+// s_memrealtime at the start and the end. Written to this buffer only; no output reads them.
+__device__ unsigned long long g_k32_stamps[65536][8];
+#define K32_STAMP(k)                                                                        \
+  do {                                                                                      \
+    if (threadIdx.x == 0 && blockIdx.x < 65536) g_k32_stamps[blockIdx.x][k] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#define K32_RSTAMP(k)                                                                       \
+  do {                                                                                      \
+    if (threadIdx.x == 0 && blockIdx.x < 65536) g_k32_stamps[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define K32_STAMP(k) do {} while (0)
+#define K32_RSTAMP(k) do {} while (0)
+#endif
+
+template <int BN, int WM, int WN, bool PRO>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) conv_k32_kernel(ConvArgs a, PatchGeom g) {
-  constexpr int BM = 128, WM = 64;
+  constexpr int BM = 128;
   constexpr int NWN = BN / WN;
   static_assert((BM / WM) * NWN == 4, "4 waves per block");
   constexpr int TM = WM / 16, TN = WN / 16;
@@ -67,6 +87,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   const int b0 = m0 / HWo;
   const int y0 = (m0 - b0 * HWo) / Wo;
 
+  K32_RSTAMP(5);
+  K32_STAMP(0);
   const int t = threadIdx.x;
   const int lane = t & 63, wave = t >> 6;
   const int wm = wave / NWN, wn = wave % NWN;
@@ -198,18 +220,52 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[i][0], bv[j][0], acc[i][j], 0, 0, 0);
       }
   };
-  auto compute_tap = [&](int ky, int kx, int pbuf, const f16x8 (&bv)[TN][2]) {
-    int abase[TM];
+  // A row offsets of tap (ky, kx) for the lane's row of tile i
+  auto a_off = [&](int i, int ky, int kx) {
+    return ((fimg[i] * g.PH + fy[i] + ky) * g.PW + fx[i] + kx) * kRowH + q * 8;
+  };
+  // One tap of the main loop. a0 holds tile 0's fragment of this tap on entry (read ahead) and, for
+  // taps 0 .. 7, tile 0's fragment of the next tap on exit, so a tap never opens on an LDS-read wait.
+  f16x8 a0[2];
+  auto read_a0 = [&](int tap, int pbuf) {
+    const _Float16* As = patch + pbuf * PATCH + a_off(0, tap / 3, tap % 3);
+    a0[0] = *reinterpret_cast<const f16x8*>(As);
+    a0[1] = *reinterpret_cast<const f16x8*>(As + 32);
+  };
+  auto compute_tap = [&](int tap, int pbuf, const f16x8 (&bv)[TN][2]) {
+    const _Float16* As = patch + pbuf * PATCH;
+    f16x8 av[TM][2];
+    av[0][0] = a0[0];
+    av[0][1] = a0[1];
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
-      abase[i] = ((fimg[i] * g.PH + fy[i] + ky) * g.PW + fx[i] + kx) * kRowH + q * 8;
-    compute(patch + pbuf * PATCH, abase, bv);
+    for (int i = 1; i < TM; ++i)
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+        av[i][p] = *reinterpret_cast<const f16x8*>(As + a_off(i, tap / 3, tap % 3) + p * 32);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[i][1], bv[j][0], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[i][0], bv[j][1], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[i][0], bv[j][0], acc[i][j], 0, 0, 0);
+      }
+      if (i == TM - 2 && tap + 1 < NTAP) read_a0(tap + 1, pbuf);
+    }
   };
 
   const int nchunks = a.Cin1 / kC;
   const int kt_end = nchunks * NTAP;
 #pragma unroll
   for (int d = 0; d < WD; ++d) load_b(bq[d], slice_off(min(d, kt_end - 1)));
+  // the first chunk's patch (all four passes) is in flight while the GroupNorm tables are built
+  load_patch(0, 0);
+  f4 rq[2][2];
+#pragma unroll
+  for (int j = 2; j < 4; ++j) {
+    rq[j & 1][0] = *reinterpret_cast<const f4*>(psrc[j]);
+    rq[j & 1][1] = *reinterpret_cast<const f4*>(psrc[j] + 4);
+  }
   if (PRO) {
     if (a.gin_part) {
       // gn_finalize (gn.hip) for the tile's images, same expressions (conv_patch3.hip's in-kernel finalize)
@@ -217,6 +273,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
       for (int i = t; i < tab_n * G; i += 256) {
         const int b = tab_img0 + i / G, gg = i - (i / G) * G;
         double s1 = 0, s2 = 0;
+#pragma unroll 4
         for (int k = 0; k < a.gin_nchunk; ++k) {
           const double2 v = a.gin_part[((size_t)b * a.gin_nchunk + k) * G + gg];
           s1 += v.x;
@@ -252,11 +309,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     }
     __syncthreads();
   }
-  load_patch(0, 0);
   finish_patch(0, 0, 0);
-  load_patch(0, 2);
+  rp[0][0] = rq[0][0];
+  rp[0][1] = rq[0][1];
+  rp[1][0] = rq[1][0];
+  rp[1][1] = rq[1][1];
   finish_patch(0, 2, 0);
   __syncthreads();
+  K32_STAMP(1);
   // One barrier per chunk (double-buffered patch; the other buffer is free once every wave has passed
   // the previous chunk's barrier). The next chunk's patch goes in two halves: passes 0, 1 loaded at tap
   // 0 and finished (GroupNorm + SiLU, split, LDS store) at tap 2, passes 2, 3 loaded at tap 3 and
@@ -275,7 +335,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
           load_patch(cn, tap == 0 ? 0 : 2);
           __builtin_amdgcn_sched_barrier(0);
         }
-        compute_tap(tap / 3, tap % 3, c & 1, bq[slot]);
+        if (tap == 0) read_a0(0, c & 1);
+        compute_tap(tap, c & 1, bq[slot]);
         load_b(bq[slot], slice_off(min(kt + WD, kt_end - 1)));
         __builtin_amdgcn_sched_barrier(0);  // keep the refill WD taps ahead
         if (tap == 2 || tap == 5) finish_patch(cn, tap == 2 ? 0 : 2, (c + 1) & 1);
@@ -284,6 +345,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     }
   }
 
+  K32_STAMP(2);
   // ---- segment 2: 1x1 product of x2 (the ResBlock shortcut), K = Cin2 in 32-channel steps, un-pipelined
   if (a.Cin2 > 0) {
     const size_t s2 = (size_t)(NTAP * a.Cin1 / 16) * sl + (size_t)(q >> 1) * sl;  // 16-slices 9 Cin1/16 + 2 c2 + (q>>1)
@@ -316,66 +378,111 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     }
   }
   if (bad && a.range_flag) *a.range_flag = 1;
+  K32_STAMP(3);
 
-  // ---- epilogue: lane (l16, q) holds column l16 of each 16-column tile, rows 4q .. 4q+3 of each
-  // 16-row tile. Row scale undo, bias, per-image row vector, residual, GroupNorm statistics of the
-  // stored values (the wave's 64 rows are one 64-pixel chunk of one image when HW % 64 == 0).
+  // ---- epilogue, staged through LDS so every lane stores 16 B: per 32 of the wave's WM rows, the
+  // accumulators (lane (l16, q) holds column l16 of each 16-column tile, rows 4q .. 4q+3 of each 16-row
+  // tile) go to this wave's region of the (now free) patch buffers as a [32][WN + 4] fp32 tile with the
+  // row scale undone; then each lane reads 4 consecutive columns of a row (LPR lanes per row), adds bias,
+  // per-image row vector and residual (16-B loads) and stores 16 B. GroupNorm statistics of the stored
+  // values: every 64 of the wave's rows are one 64-pixel chunk of one image (HW % 64 == 0).
+  constexpr int EP = WN + 4;               // staging pitch (floats)
+  constexpr int LPR = WN / 4;              // lanes per row
+  constexpr int RPI = 64 / LPR;            // rows per wave instruction
+  float* st = reinterpret_cast<float*>(patch) + wave * 32 * EP;
   const bool block_one_image = (HWo % BM) == 0;
   const bool emit = a.gn_part != nullptr;
   const int wrow0 = m0 + wm * WM;
+  const int c4 = lane % LPR, rsub = lane / LPR;
+  const int ncol = n0 + wn * WN + 4 * c4;  // this lane's 4 output columns (N % 4 == 0: all valid or none)
+  const bool c_ok = ncol < N;
+  const int nc = c_ok ? ncol : 0;
+  const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  const f4 bias4 = a.bias ? *reinterpret_cast<const f4*>(a.bias + nc) : zero4;
+  const f4 rv4 = (a.rowvec && block_one_image) ? *reinterpret_cast<const f4*>(a.rowvec + (size_t)b0 * a.rowvec_pitch + nc)
+                                               : zero4;
+  float cs[TN];
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n_raw = n0 + wn * WN + j * 16 + l16;
-    const bool n_ok = n_raw < N;
-    const int n = n_ok ? n_raw : N - 1;
-    const float bn = a.bias ? a.bias[n] : 0.f;
-    const float cs = a.ws_rowscale[n];
-    const float rv_blk = (a.rowvec && block_one_image) ? a.rowvec[(size_t)b0 * a.rowvec_pitch + n] : 0.f;
-    double gs = 0.0, gq = 0.0;
+  for (int j = 0; j < TN; ++j) cs[j] = a.ws_rowscale[min(n0 + wn * WN + j * 16 + l16, N - 1)];
+  double gs[4] = {0.0, 0.0, 0.0, 0.0}, gq[4] = {0.0, 0.0, 0.0, 0.0};
+  // GroupNorm statistics of one 64-row chunk: per channel over the lane's rows, then the wave's other
+  // row lanes, then the group's channels
+  auto emit_chunk = [&](int crow0) {
+    const int cpg = N / a.gn_G;  // 4, 8 or 16 (conv_k32_ok)
+    double s = 0.0, sq2 = 0.0;
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      float rsd[4];
-      if (a.res) {
+    for (int e = 0; e < 4; ++e) {
+      s += gs[e];
+      sq2 += gq[e];
+      gs[e] = 0.0;
+      gq[e] = 0.0;
+    }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = min(wrow0 + i * 16 + 4 * q + r, M - 1);
-          rsd[r] = a.res[(size_t)m * a.res_pitch + n];
-        }
+    for (int o = LPR; o < 64; o <<= 1) {
+      s += __shfl_xor(s, o);
+      sq2 += __shfl_xor(sq2, o);
+    }
+    for (int o = 1; o < cpg / 4; o <<= 1) {
+      s += __shfl_xor(s, o);
+      sq2 += __shfl_xor(sq2, o);
+    }
+    const int nchunk = (HWo + 63) / 64;
+    const int bb = crow0 / HWo, ch = (crow0 - bb * HWo) / 64;
+    if (rsub == 0 && (c4 % (cpg / 4)) == 0 && c_ok && crow0 < M)
+      a.gn_part[((size_t)bb * nchunk + ch) * a.gn_G + ncol / cpg] = make_double2(s, sq2);
+  };
+#pragma unroll
+  for (int h = 0; h < WM / 32; ++h) {
+#pragma unroll
+    for (int i = 2 * h; i < 2 * h + 2; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) st[((i - 2 * h) * 16 + 4 * q + r) * EP + j * 16 + l16] = acc[i][j][r] * cs[j];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes are visible to its reads
+    __builtin_amdgcn_wave_barrier();
+    f4 rs4[32 / RPI];
+    if (a.res) {
+#pragma unroll
+      for (int it = 0; it < 32 / RPI; ++it) {
+        const int m = min(wrow0 + 32 * h + it * RPI + rsub, M - 1);
+        rs4[it] = *reinterpret_cast<const f4*>(a.res + (size_t)m * a.res_pitch + nc);
       }
+    }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = wrow0 + i * 16 + 4 * q + r;
-        if (m >= M) continue;
-        float v = acc[i][j][r] * cs;
-        if (a.bias) v = v + bn;
-        if (a.rowvec) v = v + (block_one_image ? rv_blk : a.rowvec[(size_t)(m / HWo) * a.rowvec_pitch + n]);
-        if (a.res) v = v + rsd[r];
-        if (n_ok) a.y[(size_t)m * a.y_pitch + n] = v;
-        if (emit) {
-          gs += (double)v;
-          gq += (double)v * v;
+    for (int it = 0; it < 32 / RPI; ++it) {
+      const int row = it * RPI + rsub;
+      const int m = wrow0 + 32 * h + row;
+      f4 v = *reinterpret_cast<const f4*>(st + row * EP + 4 * c4);
+      if (a.bias) v = v + bias4;
+      if (a.rowvec) v = v + (block_one_image ? rv4
+                                             : *reinterpret_cast<const f4*>(a.rowvec + (size_t)(min(m, M - 1) / HWo) *
+                                                                                           a.rowvec_pitch + nc));
+      if (a.res) v = v + rs4[it];
+      if (m < M && c_ok) *reinterpret_cast<f4*>(a.y + (size_t)m * a.y_pitch + ncol) = v;
+      if (emit && m < M) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          gs[e] += (double)v[e];
+          gq[e] += (double)v[e] * v[e];
         }
       }
     }
-    if (emit) {  // the wave's 64 rows: combine the four row quarters, then the group's columns
-      gs += __shfl_xor(gs, 16);
-      gq += __shfl_xor(gq, 16);
-      gs += __shfl_xor(gs, 32);
-      gq += __shfl_xor(gq, 32);
-      const int cpg = N / a.gn_G;
-      for (int o = 1; o < cpg; o <<= 1) {
-        gs += __shfl_xor(gs, o);
-        gq += __shfl_xor(gq, o);
-      }
-      const int nchunk = (HWo + 63) / 64;
-      const int bb = wrow0 / HWo, ch = (wrow0 - bb * HWo) / 64;
-      if (q == 0 && (l16 % cpg) == 0 && n_ok && wrow0 < M)
-        a.gn_part[((size_t)bb * nchunk + ch) * a.gn_G + n_raw / cpg] = make_double2(gs, gq);
-    }
+    __builtin_amdgcn_wave_barrier();  // the next half's writes reuse the region
+    if (emit && (h & 1)) emit_chunk(wrow0 + 32 * (h - 1));
   }
+  K32_STAMP(4);
+  K32_RSTAMP(6);
 }
 
 }  // namespace
+
+#ifdef DM_K32_STAMPS
+extern "C" int dm_debug_k32_stamps(void* host, int nblocks) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_k32_stamps), (size_t)nblocks * 8 * sizeof(unsigned long long)) ==
+                 hipSuccess ? 0 : -2;
+}
+#endif
 
 bool conv_k32_ok(const ConvArgs& a) {
   if (!(a.ws && a.ws_np == 2 && a.ws_rowscale && a.taps == 9 && a.stride == 1 && a.upsample == 0 && a.ksplit <= 1))
@@ -386,7 +493,13 @@ bool conv_k32_ok(const ConvArgs& a) {
   if (!conv_patch_geom(a, BM_K32, g) || g.P > kMaxP || g.TB != 1) return false;
   if (a.pro_scale && 2 * a.Cin1 > kTab) return false;
   if (a.gin_part && a.gin_G > kStats) return false;
-  if (a.gn_part && (a.gn_G <= 0 || a.Cout % a.gn_G != 0 || a.Cout / a.gn_G > 16 || (a.Hout * a.Wout) % 64 != 0))
+  if (a.gn_part && (a.gn_G <= 0 || a.Cout % a.gn_G != 0 || a.Cout / a.gn_G > 16 || (a.Cout / a.gn_G) % 4 != 0 ||
+                    (a.Hout * a.Wout) % 64 != 0))
+    return false;
+  // the epilogue's 16-byte loads / stores of 4 consecutive channels
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (a.Cout % 4 != 0 || a.y_pitch % 4 != 0 || !al16(a.y) || (a.bias && !al16(a.bias)) ||
+      (a.res && (a.res_pitch % 4 != 0 || !al16(a.res))) || (a.rowvec && (a.rowvec_pitch % 4 != 0 || !al16(a.rowvec))))
     return false;
   return true;
 }
@@ -406,6 +519,12 @@ int conv_k32_pick(const ConvArgs& a) {
   return p == 3 ? 128 : p == 4 ? 64 : 0;
 }
 
+// rocprofv3's name of the instantiation conv2d_k32 launches (spaces removed)
+std::string conv_k32_label(const ConvArgs& a, int bn) {
+  std::string s = bn == 128 ? "conv_k32_kernel<128,64,64," : "conv_k32_kernel<64,64,32,";
+  return s + (a.pro_scale ? "true>" : "false>");
+}
+
 int conv2d_k32(const ConvArgs& a, int bn, hipStream_t st) {
   DM_REQUIRE(conv_k32_ok(a), "conv: shape not supported by the K = 32 split kernel");
   DM_REQUIRE(bn == 128 || bn == 64, "conv: K = 32 split kernel tiles are 128 x 128 and 128 x 64");
@@ -415,14 +534,14 @@ int conv2d_k32(const ConvArgs& a, int bn, hipStream_t st) {
   const int blocks = ceil_div(M, BM_K32) * ceil_div(a.Cout, bn);
   if (bn == 128) {
     if (a.pro_scale)
-      hipLaunchKernelGGL((conv_k32_kernel<128, 64, true>), dim3(blocks), dim3(256), 0, st, a, g);
+      hipLaunchKernelGGL((conv_k32_kernel<128, 64, 64, true>), dim3(blocks), dim3(256), 0, st, a, g);
     else
-      hipLaunchKernelGGL((conv_k32_kernel<128, 64, false>), dim3(blocks), dim3(256), 0, st, a, g);
+      hipLaunchKernelGGL((conv_k32_kernel<128, 64, 64, false>), dim3(blocks), dim3(256), 0, st, a, g);
   } else {
     if (a.pro_scale)
-      hipLaunchKernelGGL((conv_k32_kernel<64, 32, true>), dim3(blocks), dim3(256), 0, st, a, g);
+      hipLaunchKernelGGL((conv_k32_kernel<64, 64, 32, true>), dim3(blocks), dim3(256), 0, st, a, g);
     else
-      hipLaunchKernelGGL((conv_k32_kernel<64, 32, false>), dim3(blocks), dim3(256), 0, st, a, g);
+      hipLaunchKernelGGL((conv_k32_kernel<64, 64, 32, false>), dim3(blocks), dim3(256), 0, st, a, g);
   }
   DM_LAUNCH_CHECK();
   return DM_OK;

@@ -229,6 +229,7 @@ int conv2d_patch3(const ConvArgs& a, int which, const PatchGeom& g, hipStream_t 
 bool conv_k32_ok(const ConvArgs& a);
 int conv_k32_pick(const ConvArgs& a);
 int conv2d_k32(const ConvArgs& a, int bn, hipStream_t st);
+std::string conv_k32_label(const ConvArgs& a, int bn);
 int conv_splitk_reduce(const ConvArgs& a, hipStream_t st);
 // fp32 packed conv weights [nmat][rows][K] -> split slices for conv_patch3_kernel (np 3: bf16x3,
 // np 2: fp16x2 + row scales); split_conv_rowscale gives ConvArgs::ws_rowscale of an fp16x2 copy
