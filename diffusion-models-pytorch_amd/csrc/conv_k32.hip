@@ -23,9 +23,10 @@
 // q & 1 of 16-slice (2c + (q >> 1)) * 9 + tap -- k = 8q + e of the 32-deep step, the same relabelling
 // as A. Loaded from L2 into a 2-deep register ring, no LDS stage.
 //
-// Tiles: 128 x BN blocks (BN 128 or 64) of 4 waves, 64 x WN wave tiles, whole image rows of 16- or
-// 32-pixel-wide maps (a 16-pixel fragment never straddles an image row). LDS: 2 x 208 x 160 B patch
-// buffers + 4.5 KiB of GroupNorm tables = 71 KiB -> two blocks per CU.
+// Tiles: 128 x BN blocks (BN 128 or 64) of 4 waves, 64 x WN wave tiles, whole image rows of 32-, 16- or
+// 8-pixel-wide maps (8^2 maps: two images per tile; each lane addresses its own patch row, so a 16-pixel
+// fragment may span image rows). LDS: 2 x 208 x 160 B patch buffers + 4.5 KiB of GroupNorm tables
+// = 71 KiB -> two blocks per CU.
 #include <cstdlib>
 #include <string>
 
@@ -41,8 +42,8 @@ namespace {
 constexpr int BM_K32 = 128;   // block rows (output pixels)
 constexpr int kC = 32;          // input channels per chunk = K of one tap's MFMA step
 constexpr int kRowH = 80;       // LDS row pitch in fp16: 160 B; [piece][k-group][8] (piece at +32)
-constexpr int kMaxP = 208;      // patch pixels: 32^2 maps 6 x 34, 16^2 maps 10 x 18
-constexpr int kTab = 1024;      // GroupNorm table floats (one image: Cin1 scales + Cin1 shifts)
+constexpr int kMaxP = 208;      // patch pixels: 32^2 maps 6 x 34, 16^2 maps 10 x 18, 8^2 maps 2 x 10 x 10
+constexpr int kTab = 1024;      // GroupNorm table floats (per image of the tile: Cin1 scales, then the shifts)
 constexpr int kStats = 128;     // (image, group) pairs of the in-kernel finalize
 
 
@@ -488,11 +489,11 @@ bool conv_k32_ok(const ConvArgs& a) {
   if (!(a.ws && a.ws_np == 2 && a.ws_rowscale && a.taps == 9 && a.stride == 1 && a.upsample == 0 && a.ksplit <= 1))
     return false;
   if (a.Cin1 < kC || a.Cin1 % kC != 0 || a.Cin2 % kC != 0 || a.K != 9 * a.Cin1 + a.Cin2) return false;
-  if (a.Wout < 16 || a.Wout % 16 != 0 || BM_K32 % a.Wout != 0) return false;
+  if (a.Wout < 8 || a.Wout % 8 != 0 || BM_K32 % a.Wout != 0) return false;
   PatchGeom g;
-  if (!conv_patch_geom(a, BM_K32, g) || g.P > kMaxP || g.TB != 1) return false;
-  if (a.pro_scale && 2 * a.Cin1 > kTab) return false;
-  if (a.gin_part && a.gin_G > kStats) return false;
+  if (!conv_patch_geom(a, BM_K32, g) || g.P > kMaxP || g.TB > 2) return false;
+  if (a.pro_scale && 2 * g.TB * a.Cin1 > kTab) return false;
+  if (a.gin_part && g.TB * a.gin_G > kStats) return false;
   if (a.gn_part && (a.gn_G <= 0 || a.Cout % a.gn_G != 0 || a.Cout / a.gn_G > 16 || (a.Cout / a.gn_G) % 4 != 0 ||
                     (a.Hout * a.Wout) % 64 != 0))
     return false;
@@ -516,7 +517,11 @@ int conv_k32_pick(const ConvArgs& a) {
   }();
   if (off || !conv_k32_ok(a)) return 0;
   const int p = conv_pick(a);
-  return p == 3 ? 128 : p == 4 ? 64 : 0;
+  if (p != 3 && p != 4) return 0;
+  // 128 x 128 tiles down to one block per CU (measured on 8^2 maps at B = 256: 256 blocks of 128 x 128 beat
+  // 512 of 128 x 64 by 6 %); the nominal batch (pick_B) keeps the choice batch-invariant
+  const long M = (long)(a.pick_B > 0 ? a.pick_B : a.B) * a.Hout * a.Wout;
+  return ((M + 127) / 128) * ((a.Cout + 127) / 128) >= 256 ? 128 : 64;
 }
 
 // rocprofv3's name of the instantiation conv2d_k32 launches (spaces removed)

@@ -3,7 +3,7 @@ torch references, as tests/test_gpu_conv_split.py does for conv_patch3: integer 
 bit (indexing, padding, tap walk, both K segments, epilogue), random operands must keep fp32-level
 accuracy (within 2x of the fp32 MFMA kernel's error vs fp64), and an activation beyond fp16's range must
 raise the range flag. Tiles: 10 = 128 x 128, 11 = 128 x 64 (forced); 0 = the automatic choice, which
-takes this kernel for the 16- / 32-pixel-wide maps the UNets run at 128-row tiles."""
+takes this kernel for the 8- / 16- / 32-pixel-wide maps the UNets run at 128-row tiles."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -18,6 +18,7 @@ TILES = [10, 11, 0]
 @pytest.mark.parametrize('tile', TILES)
 @pytest.mark.parametrize('B,Cin,Cout,H', [
     (1, 128, 256, 16), (2, 32, 64, 16), (2, 96, 96, 32), (1, 64, 128, 32), (3, 160, 64, 16), (1, 256, 160, 32),
+    (3, 64, 64, 8), (2, 256, 128, 8),
 ])
 def test_k32_conv3x3_exact(cuda, B, Cin, Cout, H, tile):
     x = _ints((B, Cin, H, H), -2, 3, seed=10)
@@ -30,7 +31,7 @@ def test_k32_conv3x3_exact(cuda, B, Cin, Cout, H, tile):
 
 
 @pytest.mark.parametrize('tile', TILES)
-@pytest.mark.parametrize('C1,C2,H', [(64, 32, 16), (96, 64, 32), (32, 128, 16)])
+@pytest.mark.parametrize('C1,C2,H', [(64, 32, 16), (96, 64, 32), (32, 128, 16), (64, 64, 8)])
 def test_k32_segments_rowvec_residual_pitch(cuda, tile, C1, C2, H):
     """ResBlock conv2: 3x3 over h + the 1x1 shortcut of x as a second K segment, temb row vector,
     residual, pitched output (untouched beyond Cout)."""
@@ -55,7 +56,7 @@ def test_k32_segments_rowvec_residual_pitch(cuda, tile, C1, C2, H):
 
 
 @pytest.mark.parametrize('B,Cin,Cout,H', [(4, 128, 128, 32), (8, 256, 256, 16), (2, 384, 128, 32),
-                                          (4, 512, 256, 16)])
+                                          (4, 512, 256, 16), (5, 256, 256, 8)])
 def test_k32_fp32_accuracy(cuda, B, Cin, Cout, H):
     """fused GroupNorm + SiLU conv on random data: the K = 32 kernel's error vs fp64 is within 2x the
     fp32 MFMA kernel's (and of the same size as conv_patch3's fp16x2 128-row tile)."""
