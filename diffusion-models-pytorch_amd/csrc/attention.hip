@@ -32,6 +32,24 @@ constexpr int kAK = 32;              // k per staged tile
 constexpr int kAP = 72;              // fp16 pitch of a staged 32-k row (two 16-deep slices + pad: 144 B)
 constexpr int kSP = 8 * kAP / 2;     // fp32 pitch of an S row = one P row of 8 key blocks (1152 B)
 
+
+#ifdef DM_K32_STAMPS
+// Diagnostic build only (tools/k32_stamps.py --attn): per block, wave 0's s_memtime at phase boundaries
+// of attn_presplit_kernel and s_memrealtime at start / end. Written to this buffer only.
+__device__ unsigned long long g_attn_stamps[8192][10];
+#define AT_STAMP(k)                                                                                      \
+  do {                                                                                                   \
+    if (threadIdx.x == 0 && blockIdx.x < 8192) g_attn_stamps[blockIdx.x][k] = __builtin_amdgcn_s_memtime();  \
+  } while (0)
+#define AT_RSTAMP(k)                                                                                     \
+  do {                                                                                                   \
+    if (threadIdx.x == 0 && blockIdx.x < 8192) g_attn_stamps[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define AT_STAMP(k) do {} while (0)
+#define AT_RSTAMP(k) do {} while (0)
+#endif
+
 __device__ __forceinline__ int split_off(int k) { return (k >> 4) * 32 + ((k >> 3) & 1) * 16 + (k & 7); }
 
 // QT query rows per block: 32 for DH = 256 (78 KB of LDS: two blocks per CU), 64 for DH = 64 (the PV
@@ -276,7 +294,7 @@ __global__ void __launch_bounds__(256) attn_fused_kernel(AttnArgs a) {
 // channels from the pre-split weights (the conv's B-fragment images, same slice order) and runs the
 // conv epilogue (row scale, bias, residual, GroupNorm statistics): bit-identical to proj as its own launch.
 __device__ __forceinline__ void attn_proj(const ConvArgs& c, f16v (&oacc)[2][2], float ounscale, float* sp, int m0,
-                                          int wave, int lr, int lh) {
+                                          int wave, int lr, int lh, bool staged) {
   __syncthreads();  // every wave is done reading P
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -302,6 +320,7 @@ __device__ __forceinline__ void attn_proj(const ConvArgs& c, f16v (&oacc)[2][2],
     *reinterpret_cast<f16x4*>(dst + 8) = lo;
   }
   __syncthreads();
+  AT_STAMP(4);
   // 64 x 256 output tile: wave w owns columns 64 w .. 64 w + 63; K = 256 = 16 slices
   const _Float16* A = reinterpret_cast<const _Float16*>(sp);
   constexpr int PPITCH = 2 * kSP;
@@ -346,9 +365,33 @@ __device__ __forceinline__ void attn_proj(const ConvArgs& c, f16v (&oacc)[2][2],
     __builtin_amdgcn_sched_barrier(0);
   }
   if (bad && c.range_flag) *c.range_flag = 1;
+  AT_STAMP(5);
   const int M = c.B * c.Hout * c.Wout, HWo = c.Hout * c.Wout;
-  conv_patch_epilogue<64, 256, 64, 64, 3, false, true>(c, acc, M, HWo, c.Wout, m0, 0, m0 / HWo, 0, wave, lr, lh, 0, 0, 0,
-                                                 c.ws_rowscale);
+  if (!staged) {
+    conv_patch_epilogue<64, 256, 64, 64, 3, false, true>(c, acc, M, HWo, c.Wout, m0, 0, m0 / HWo, 0, wave, lr, lh, 0, 0,
+                                                         0, c.ws_rowscale);
+    return;
+  }
+  // LDS-staged epilogue (16-B stores): per 32-row slab i, this wave's 32 x 64 tile of acc * rowscale
+  typedef StagedEpilogue<64> Epi;
+  __syncthreads();  // every wave is done reading the O rows
+  float* st = sp + wave * 32 * Epi::EP;
+  Epi epi(c, M, HWo, m0 / HWo, (HWo % 64) == 0, wave * 64, lr + 32 * lh);
+  float cs[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) cs[j] = c.ws_rowscale[wave * 64 + j * 32 + lr];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) st[acc_row(r, lh) * Epi::EP + j * 32 + lr] = acc[i][j][r] * cs[j];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes are visible to its reads
+    __builtin_amdgcn_wave_barrier();
+    epi.rows(st, m0 + 32 * i);
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (c.gn_part) epi.emit(m0);
 }
 
 // Pre-split operands (AttnArgs::pq / pk / pv, written by the qkv conv's epilogue, conv_epilogue.h): every
@@ -358,8 +401,11 @@ __device__ __forceinline__ void attn_proj(const ConvArgs& c, f16v (&oacc)[2][2],
 template <int DH>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) attn_presplit_kernel(AttnArgs a) {
   static_assert(DH == 64 || DH == 256, "head dims 64 / 256");
-  constexpr int QT = 64, NS = DH / 16, RD = 4;
+  constexpr int QT = 64, NS = DH / 16, RD = 6;
   __shared__ __attribute__((aligned(16))) float sp[QT * kSP];
+  static_assert(QT * (2 * DH + 8) * 2 <= QT * kSP * 4, "the staged q tile fits the S rows");
+  AT_RSTAMP(6);
+  AT_STAMP(0);
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int lr = lane & 31, lh = lane >> 5;
   const int nq = kAL / QT;
@@ -371,17 +417,39 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   const _Float16* V = a.pv + (size_t)bh * 2 * plane;
 
   // ---------------------------------------------------------------- 1. S: wave w = 64 rows x keys 64 w ..
-  f16x8 ra[RD][2][2], rb[RD][2][2];   // [slot][tile][piece]
-  auto load_s = [&](int s, int slot) {
+  // The block's 64 q rows are read by all four waves: staged once in LDS (over the S / P rows, free until
+  // S is written), rows of [16-deep slice][piece][lane group][8] fp16 with a 16-B pad (an odd number of
+  // 16-B slots: conflict-free fragment reads). k rows (64 per wave, no reuse) ride a register ring RD
+  // slices ahead. Same operands and MFMA sequence as before: S is unchanged bit for bit.
+  constexpr int QP = 2 * DH + 8;
+  _Float16* Qs = reinterpret_cast<_Float16*>(sp);
+  f16x8 rb[RD][2][2];   // [slot][tile][piece]
+  auto load_k = [&](int s, int slot) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        ra[slot][i][q] = *reinterpret_cast<const f16x8*>(Q + q * plane + (size_t)(i * 32 + lr) * DH + 16 * s + 8 * lh);
+      for (int q = 0; q < 2; ++q)
         rb[slot][i][q] =
             *reinterpret_cast<const f16x8*>(K + q * plane + (size_t)(wave * 64 + i * 32 + lr) * DH + 16 * s + 8 * lh);
-      }
   };
+#pragma unroll
+  for (int s = 0; s < RD; ++s) load_k(min(s, NS - 1), s);
+  {
+    constexpr int QCH = 64 * DH / 8;  // 16-B chunks of one piece plane of the tile
+    f16x8 qv[2 * QCH / 256];
+#pragma unroll
+    for (int u = 0; u < 2 * QCH / 256; ++u) {
+      const int c = t + 256 * u, piece = c / QCH, rem = c - piece * QCH;
+      const int row = rem / (DH / 8), d8 = rem - row * (DH / 8);
+      qv[u] = *reinterpret_cast<const f16x8*>(Q + piece * plane + (size_t)row * DH + 8 * d8);
+    }
+#pragma unroll
+    for (int u = 0; u < 2 * QCH / 256; ++u) {
+      const int c = t + 256 * u, piece = c / QCH, rem = c - piece * QCH;
+      const int row = rem / (DH / 8), d8 = rem - row * (DH / 8);
+      *reinterpret_cast<f16x8*>(Qs + row * QP + (d8 >> 1) * 32 + piece * 16 + (d8 & 1) * 8) = qv[u];
+    }
+  }
   f16v acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -389,18 +457,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-#pragma unroll
-  for (int s = 0; s < RD; ++s) load_s(min(s, NS - 1), s);
+  __syncthreads();
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     const int slot = s % RD;
+    f16x8 av[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) Split<2>::mma(ra[slot][i], rb[slot][j], acc[i][j]);
-    load_s(min(s + RD, NS - 1), slot);
+      for (int q = 0; q < 2; ++q) av[i][q] = *reinterpret_cast<const f16x8*>(Qs + (i * 32 + lr) * QP + s * 32 + q * 16 + lh * 8);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) Split<2>::mma(av[i], rb[slot][j], acc[i][j]);
+    load_k(min(s + RD, NS - 1), slot);
     __builtin_amdgcn_sched_barrier(0);
   }
+  __syncthreads();  // every wave is done reading the q tile before S overwrites it
   {
     const float unscale = ldexpf(1.f, -(a.ea + a.eb));
 #pragma unroll
@@ -412,40 +485,60 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
           sp[(i * 32 + acc_row(r, lh)) * kSP + wave * 64 + j * 32 + lr] = acc[i][j][r] * unscale;
   }
   __syncthreads();
+  AT_STAMP(1);
 
   // ---------------------------------------------------------------- 2. softmax rows -> P pieces in place
   const float pp = ldexpf(1.f, a.ep);
-  for (int row = wave * (QT / 4); row < (wave + 1) * (QT / 4); ++row) {
-    float* srow = sp + row * kSP;
-    float v[8];
+  // four rows at a time: independent max / sum shuffle chains overlap (per row the same operations in the
+  // same order as softmax_rows, so P stays bit-identical)
+  constexpr int RI = 4;
+  for (int row0 = wave * (QT / 4); row0 < (wave + 1) * (QT / 4); row0 += RI) {
+    float v[RI][4], mx[RI], sum[RI];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = u < 4 ? srow[lane + 64 * u] : -INFINITY;   // softmax_rows' 8 slots
-    float mx = -INFINITY;
+    for (int ri = 0; ri < RI; ++ri) {
+      const float* srow = sp + (row0 + ri) * kSP;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) mx = fmaxf(mx, v[u]);
+      for (int u = 0; u < 4; ++u) v[ri][u] = srow[lane + 64 * u];
+      mx[ri] = -INFINITY;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-    float sum = 0.f;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      v[u] = expf(v[u] - mx);
-      sum += v[u];
+      for (int u = 0; u < 8; ++u) mx[ri] = fmaxf(mx[ri], u < 4 ? v[ri][u & 3] : -INFINITY);  // softmax_rows' 8 slots
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
-    const float inv = 1.0f / sum;
-    _Float16* prow = reinterpret_cast<_Float16*>(srow);
+    for (int o = 32; o > 0; o >>= 1)
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int k = lane + 64 * u;
-      const float x = (v[u] * inv) * pp;
-      const _Float16 h0 = (_Float16)x;
-      _Float16* dst = prow + (k >> 5) * kAP + split_off(k & 31);
-      dst[0] = h0;
-      dst[8] = (_Float16)(x - (float)h0);
+      for (int ri = 0; ri < RI; ++ri) mx[ri] = fmaxf(mx[ri], __shfl_xor(mx[ri], o));
+#pragma unroll
+    for (int ri = 0; ri < RI; ++ri) {
+      sum[ri] = 0.f;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        v[ri][u] = expf(v[ri][u] - mx[ri]);
+        sum[ri] += v[ri][u];
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+      for (int ri = 0; ri < RI; ++ri) sum[ri] += __shfl_xor(sum[ri], o);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // every row's S values are in registers before P overwrites the rows
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int ri = 0; ri < RI; ++ri) {
+      const float inv = 1.0f / sum[ri];
+      _Float16* prow = reinterpret_cast<_Float16*>(sp + (row0 + ri) * kSP);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = lane + 64 * u;
+        const float x = (v[ri][u] * inv) * pp;
+        const _Float16 h0 = (_Float16)x;
+        _Float16* dst = prow + (k >> 5) * kAP + split_off(k & 31);
+        dst[0] = h0;
+        dst[8] = (_Float16)(x - (float)h0);
+      }
     }
   }
   __syncthreads();
+  AT_STAMP(2);
 
   // ---------------------------------------------------------------- 3. O = P v
   constexpr int TM = DH == 256 ? 2 : 1, TN = DH == 256 ? 2 : 1, NK = kAL / 16;
@@ -488,11 +581,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     load_v(min(s + RD, NK - 1), slot);
     __builtin_amdgcn_sched_barrier(0);
   }
+  AT_STAMP(3);
   const float ounscale = ldexpf(1.f, -(a.ep + a.ev));
   const int h = bh % a.heads, b = bh / a.heads;
   if constexpr (DH == 256) {
     if (a.fuse_proj) {  // 4. y = x + proj(O): the MODE 3 1x1 conv on this block's 64 O rows
-      attn_proj(a.proj, oacc, ounscale, sp, b * kAL + qt * QT, wave, lr, lh);
+      attn_proj(a.proj, oacc, ounscale, sp, b * kAL + qt * QT, wave, lr, lh, a.proj_staged != 0);
+      AT_STAMP(8);
+      AT_RSTAMP(7);
       return;
     }
   }
@@ -508,9 +604,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 
 }  // namespace
 
+#ifdef DM_K32_STAMPS
+extern "C" int dm_debug_attn_stamps(void* host, int nblocks) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_attn_stamps), (size_t)nblocks * 10 * sizeof(unsigned long long)) ==
+                 hipSuccess ? 0 : -2;
+}
+#endif
+
 bool attn_fused_ok(int L, int Dh) { return L == kAL && (Dh == 64 || Dh == 256); }
 
-int attn_fused(const AttnArgs& a, hipStream_t st) {
+int attn_fused(const AttnArgs& args, hipStream_t st) {
+  AttnArgs a = args;
+  a.proj_staged = a.fuse_proj && staged_epilogue_ok(a.proj) ? 1 : 0;
   DM_REQUIRE(attn_fused_ok(a.L, a.Dh), "fused attention: L must be 256 and the head dim 64 or 256");
   DM_REQUIRE((a.qkv || a.pq) && a.out && a.B > 0 && a.heads > 0 && a.ld % 4 == 0 && a.ldo % 4 == 0 &&
              (a.q0 + 0) % 4 == 0 && a.k0 % 4 == 0 && a.v0 % 4 == 0 && a.hs % 4 == 0,

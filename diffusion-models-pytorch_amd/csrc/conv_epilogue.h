@@ -5,6 +5,7 @@
 // residual / GroupNorm-statistics epilogue (models/unet.py:16,26,41,43) and
 // the split-K partial store are written once here.
 #pragma once
+#include <cstdint>
 #include "dm_kernels.h"
 #include "mfma_tile.h"
 
@@ -44,6 +45,109 @@ __device__ __forceinline__ void conv_store_attn_planes(const ConvArgs& a, int m,
     dst[0] = h0;
     dst[plane] = h1;
   }
+}
+
+
+// LDS-staged epilogue (conv_k32.hip, the fused attention's proj): a wave's tile of acc * rowscale is put
+// in LDS as 32-row slabs [32][WN + 4] fp32 by the kernel (in whatever MFMA layout it has), then each
+// lane takes 4 consecutive output columns of a row (WN / 4 lanes per row), adds bias, per-image row
+// vector and residual with 16-B loads and stores 16 B -- instead of one 4-B store per accumulator
+// register (store-issue bound: 27k -> 8.5k cycles per K32 block). GroupNorm statistics of the stored
+// values per 64-row chunk: per channel over the lane's rows, then across the wave's row lanes, then
+// across the group's 4-channel quads (cpg = Cout / gn_G in {4, 8, 16}).
+template <int WN>
+struct StagedEpilogue {
+  static constexpr int EP = WN + 4;     // slab pitch (floats)
+  static constexpr int LPR = WN / 4;    // lanes per row
+  static constexpr int RPI = 64 / LPR;  // rows per wave instruction
+  const ConvArgs& a;
+  int M, HWo, b0, c4, rsub, ncol, nc;
+  bool c_ok, one_image;
+  f4 bias4, rv4;
+  double gs[4], gq[4];
+
+  // ncol0: the wave's first output column; b0: the tile's first image; one_image: every row of the tile
+  // lies in image b0
+  __device__ __forceinline__ StagedEpilogue(const ConvArgs& a_, int M_, int HWo_, int b0_, bool one_image_,
+                                            int ncol0, int lane)
+      : a(a_), M(M_), HWo(HWo_), b0(b0_), one_image(one_image_) {
+    c4 = lane % LPR;
+    rsub = lane / LPR;
+    ncol = ncol0 + 4 * c4;
+    c_ok = ncol < a.Cout;  // Cout % 4 == 0: the 4 columns are all valid or none
+    nc = c_ok ? ncol : 0;
+    const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
+    bias4 = a.bias ? *reinterpret_cast<const f4*>(a.bias + nc) : zero4;
+    rv4 = (a.rowvec && one_image) ? *reinterpret_cast<const f4*>(a.rowvec + (size_t)b0 * a.rowvec_pitch + nc) : zero4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) gs[e] = gq[e] = 0.0;
+  }
+  // the slab's rows are output rows row0 .. row0 + 31 (this wave's slab written and visible)
+  __device__ __forceinline__ void rows(const float* st, int row0) {
+    f4 rs4[32 / RPI];
+    if (a.res) {
+#pragma unroll
+      for (int it = 0; it < 32 / RPI; ++it) {
+        const int m = min(row0 + it * RPI + rsub, M - 1);
+        rs4[it] = *reinterpret_cast<const f4*>(a.res + (size_t)m * a.res_pitch + nc);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < 32 / RPI; ++it) {
+      const int row = it * RPI + rsub;
+      const int m = row0 + row;
+      f4 v = *reinterpret_cast<const f4*>(st + row * EP + 4 * c4);
+      if (a.bias) v = v + bias4;
+      if (a.rowvec)
+        v = v + (one_image ? rv4
+                           : *reinterpret_cast<const f4*>(a.rowvec + (size_t)(min(m, M - 1) / HWo) * a.rowvec_pitch + nc));
+      if (a.res) v = v + rs4[it];
+      if (m < M && c_ok) *reinterpret_cast<f4*>(a.y + (size_t)m * a.y_pitch + ncol) = v;
+      if (a.gn_part && m < M) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          gs[e] += (double)v[e];
+          gq[e] += (double)v[e] * v[e];
+        }
+      }
+    }
+  }
+  // statistics of the 64-row chunk starting at crow0 (all 64 lanes call; resets the sums)
+  __device__ __forceinline__ void emit(int crow0) {
+    const int cpg = a.Cout / a.gn_G;
+    double s = 0.0, q = 0.0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      s += gs[e];
+      q += gq[e];
+      gs[e] = gq[e] = 0.0;
+    }
+#pragma unroll
+    for (int o = LPR; o < 64; o <<= 1) {
+      s += __shfl_xor(s, o);
+      q += __shfl_xor(q, o);
+    }
+    for (int o = 1; o < cpg / 4; o <<= 1) {
+      s += __shfl_xor(s, o);
+      q += __shfl_xor(q, o);
+    }
+    const int nchunk = (HWo + 63) / 64;
+    const int bb = crow0 / HWo, ch = (crow0 - bb * HWo) / 64;
+    if (rsub == 0 && (c4 % (cpg / 4)) == 0 && c_ok && crow0 < M)
+      a.gn_part[((size_t)bb * nchunk + ch) * a.gn_G + ncol / cpg] = make_double2(s, q);
+  }
+};
+
+// whether StagedEpilogue takes this conv's output (16-B columns, GroupNorm groups of 4, 8 or 16 channels)
+inline bool staged_epilogue_ok(const ConvArgs& a) {
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (a.Cout % 4 != 0 || a.y_pitch % 4 != 0 || !al16(a.y) || (a.bias && !al16(a.bias)) ||
+      (a.res && (a.res_pitch % 4 != 0 || !al16(a.res))) || (a.rowvec && (a.rowvec_pitch % 4 != 0 || !al16(a.rowvec))))
+    return false;
+  if (a.gn_part && (a.gn_G <= 0 || a.Cout % a.gn_G != 0 || a.Cout / a.gn_G > 16 || (a.Cout / a.gn_G) % 4 != 0 ||
+                    (a.Hout * a.Wout) % 64 != 0))
+    return false;
+  return true;
 }
 
 // colscale (fp16x2 split kernels): the per-output-channel power-of-two weight scale to undo, applied to

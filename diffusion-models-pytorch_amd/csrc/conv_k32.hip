@@ -34,6 +34,7 @@
 #include "dm_kernels.h"
 #include "mfma_tile.h"
 #include "split16.h"
+#include "conv_epilogue.h"
 
 namespace dm {
 
@@ -387,51 +388,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   // row scale undone; then each lane reads 4 consecutive columns of a row (LPR lanes per row), adds bias,
   // per-image row vector and residual (16-B loads) and stores 16 B. GroupNorm statistics of the stored
   // values: every 64 of the wave's rows are one 64-pixel chunk of one image (HW % 64 == 0).
-  constexpr int EP = WN + 4;               // staging pitch (floats)
-  constexpr int LPR = WN / 4;              // lanes per row
-  constexpr int RPI = 64 / LPR;            // rows per wave instruction
-  float* st = reinterpret_cast<float*>(patch) + wave * 32 * EP;
-  const bool block_one_image = (HWo % BM) == 0;
-  const bool emit = a.gn_part != nullptr;
+  typedef StagedEpilogue<WN> Epi;
+  float* st = reinterpret_cast<float*>(patch) + wave * 32 * Epi::EP;
   const int wrow0 = m0 + wm * WM;
-  const int c4 = lane % LPR, rsub = lane / LPR;
-  const int ncol = n0 + wn * WN + 4 * c4;  // this lane's 4 output columns (N % 4 == 0: all valid or none)
-  const bool c_ok = ncol < N;
-  const int nc = c_ok ? ncol : 0;
-  const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
-  const f4 bias4 = a.bias ? *reinterpret_cast<const f4*>(a.bias + nc) : zero4;
-  const f4 rv4 = (a.rowvec && block_one_image) ? *reinterpret_cast<const f4*>(a.rowvec + (size_t)b0 * a.rowvec_pitch + nc)
-                                               : zero4;
+  Epi epi(a, M, HWo, b0, (HWo % BM) == 0, n0 + wn * WN, lane);
   float cs[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) cs[j] = a.ws_rowscale[min(n0 + wn * WN + j * 16 + l16, N - 1)];
-  double gs[4] = {0.0, 0.0, 0.0, 0.0}, gq[4] = {0.0, 0.0, 0.0, 0.0};
-  // GroupNorm statistics of one 64-row chunk: per channel over the lane's rows, then the wave's other
-  // row lanes, then the group's channels
-  auto emit_chunk = [&](int crow0) {
-    const int cpg = N / a.gn_G;  // 4, 8 or 16 (conv_k32_ok)
-    double s = 0.0, sq2 = 0.0;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      s += gs[e];
-      sq2 += gq[e];
-      gs[e] = 0.0;
-      gq[e] = 0.0;
-    }
-#pragma unroll
-    for (int o = LPR; o < 64; o <<= 1) {
-      s += __shfl_xor(s, o);
-      sq2 += __shfl_xor(sq2, o);
-    }
-    for (int o = 1; o < cpg / 4; o <<= 1) {
-      s += __shfl_xor(s, o);
-      sq2 += __shfl_xor(sq2, o);
-    }
-    const int nchunk = (HWo + 63) / 64;
-    const int bb = crow0 / HWo, ch = (crow0 - bb * HWo) / 64;
-    if (rsub == 0 && (c4 % (cpg / 4)) == 0 && c_ok && crow0 < M)
-      a.gn_part[((size_t)bb * nchunk + ch) * a.gn_G + ncol / cpg] = make_double2(s, sq2);
-  };
 #pragma unroll
   for (int h = 0; h < WM / 32; ++h) {
 #pragma unroll
@@ -439,38 +402,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 #pragma unroll
       for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) st[((i - 2 * h) * 16 + 4 * q + r) * EP + j * 16 + l16] = acc[i][j][r] * cs[j];
+        for (int r = 0; r < 4; ++r) st[((i - 2 * h) * 16 + 4 * q + r) * Epi::EP + j * 16 + l16] = acc[i][j][r] * cs[j];
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes are visible to its reads
     __builtin_amdgcn_wave_barrier();
-    f4 rs4[32 / RPI];
-    if (a.res) {
-#pragma unroll
-      for (int it = 0; it < 32 / RPI; ++it) {
-        const int m = min(wrow0 + 32 * h + it * RPI + rsub, M - 1);
-        rs4[it] = *reinterpret_cast<const f4*>(a.res + (size_t)m * a.res_pitch + nc);
-      }
-    }
-#pragma unroll
-    for (int it = 0; it < 32 / RPI; ++it) {
-      const int row = it * RPI + rsub;
-      const int m = wrow0 + 32 * h + row;
-      f4 v = *reinterpret_cast<const f4*>(st + row * EP + 4 * c4);
-      if (a.bias) v = v + bias4;
-      if (a.rowvec) v = v + (block_one_image ? rv4
-                                             : *reinterpret_cast<const f4*>(a.rowvec + (size_t)(min(m, M - 1) / HWo) *
-                                                                                           a.rowvec_pitch + nc));
-      if (a.res) v = v + rs4[it];
-      if (m < M && c_ok) *reinterpret_cast<f4*>(a.y + (size_t)m * a.y_pitch + ncol) = v;
-      if (emit && m < M) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          gs[e] += (double)v[e];
-          gq[e] += (double)v[e] * v[e];
-        }
-      }
-    }
-    __builtin_amdgcn_wave_barrier();  // the next half's writes reuse the region
-    if (emit && (h & 1)) emit_chunk(wrow0 + 32 * (h - 1));
+    epi.rows(st, wrow0 + 32 * h);
+    __builtin_amdgcn_wave_barrier();  // the next slab's writes reuse the region
+    if (a.gn_part && (h & 1)) epi.emit(wrow0 + 32 * (h - 1));
   }
   K32_STAMP(4);
   K32_RSTAMP(6);
@@ -494,15 +431,7 @@ bool conv_k32_ok(const ConvArgs& a) {
   if (!conv_patch_geom(a, BM_K32, g) || g.P > kMaxP || g.TB > 2) return false;
   if (a.pro_scale && 2 * g.TB * a.Cin1 > kTab) return false;
   if (a.gin_part && g.TB * a.gin_G > kStats) return false;
-  if (a.gn_part && (a.gn_G <= 0 || a.Cout % a.gn_G != 0 || a.Cout / a.gn_G > 16 || (a.Cout / a.gn_G) % 4 != 0 ||
-                    (a.Hout * a.Wout) % 64 != 0))
-    return false;
-  // the epilogue's 16-byte loads / stores of 4 consecutive channels
-  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-  if (a.Cout % 4 != 0 || a.y_pitch % 4 != 0 || !al16(a.y) || (a.bias && !al16(a.bias)) ||
-      (a.res && (a.res_pitch % 4 != 0 || !al16(a.res))) || (a.rowvec && (a.rowvec_pitch % 4 != 0 || !al16(a.rowvec))))
-    return false;
-  return true;
+  return staged_epilogue_ok(a);  // the epilogue's 16-byte loads / stores of 4 consecutive channels
 }
 
 // Which conv_k32 tile (128: 128 x 128, 64: 128 x 64) runs this conv, 0 = none. Forced by tile 10 / 11;

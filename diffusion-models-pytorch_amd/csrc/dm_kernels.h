@@ -273,6 +273,7 @@ struct AttnArgs {
   // never goes to HBM (`out` unused); proj.x1 is ignored
   int fuse_proj;
   ConvArgs proj;
+  int proj_staged;  // set by attn_fused: proj runs the LDS-staged 16-B epilogue (staged_epilogue_ok)
 };
 bool attn_fused_ok(int L, int Dh);
 int attn_fused(const AttnArgs& a, hipStream_t st);
