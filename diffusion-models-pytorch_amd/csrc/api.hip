@@ -96,6 +96,8 @@ extern "C" int dm_conv2d_nhwc(const dm_conv_desc* d, void* stream) {
   a.pro_scale = d->pro_scale;
   a.pro_shift = d->pro_shift;
   a.pro_nosilu = d->pro_nosilu;
+  a.ksplit = d->ksplit;
+  a.kpart = d->kpart;
   a.ws = d->w_split;
   if (a.ws) {
     if (d->w_split_kind != DM_SPLIT_BF16X3 && d->w_split_kind != DM_SPLIT_FP16X2) {

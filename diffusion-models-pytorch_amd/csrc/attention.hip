@@ -491,7 +491,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   const float pp = ldexpf(1.f, a.ep);
   // four rows at a time: independent max / sum shuffle chains overlap (per row the same operations in the
   // same order as softmax_rows, so P stays bit-identical)
-  constexpr int RI = 4;
+  constexpr int RI = QT / 4;
   for (int row0 = wave * (QT / 4); row0 < (wave + 1) * (QT / 4); row0 += RI) {
     float v[RI][4], mx[RI], sum[RI];
 #pragma unroll

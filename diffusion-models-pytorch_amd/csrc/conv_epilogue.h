@@ -112,6 +112,16 @@ struct StagedEpilogue {
       }
     }
   }
+  // split-K partial sums: the slab as it stands to dst (pitch `pitch`), no bias / row vector / residual
+  __device__ __forceinline__ void rows_raw(const float* st, int row0, float* dst, int pitch) {
+#pragma unroll
+    for (int it = 0; it < 32 / RPI; ++it) {
+      const int row = it * RPI + rsub;
+      const int m = row0 + row;
+      const f4 v = *reinterpret_cast<const f4*>(st + row * EP + 4 * c4);
+      if (m < M && c_ok) *reinterpret_cast<f4*>(dst + (size_t)m * pitch + ncol) = v;
+    }
+  }
   // statistics of the 64-row chunk starting at crow0 (all 64 lanes call; resets the sums)
   __device__ __forceinline__ void emit(int crow0) {
     const int cpg = a.Cout / a.gn_G;

@@ -66,9 +66,10 @@ __device__ unsigned long long g_k32_stamps[65536][8];
 #define K32_RSTAMP(k) do {} while (0)
 #endif
 
-template <int BN, int WM, int WN, bool PRO>
+// KSPLIT: split-K over 32-channel chunks for maps of <= 16 pixels (64-row tiles of 4 images): raw partial
+// sums to kpart [ksplit][M][Cout], the epilogue in conv_splitk_reduce (conv_patch.hip), as conv_patch3.
+template <int BM, int BN, int WM, int WN, bool PRO, bool KSPLIT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) conv_k32_kernel(ConvArgs a, PatchGeom g) {
-  constexpr int BM = 128;
   constexpr int NWN = BN / WN;
   static_assert((BM / WM) * NWN == 4, "4 waves per block");
   constexpr int TM = WM / 16, TN = WN / 16;
@@ -82,7 +83,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   const int Ho = a.Hout, Wo = a.Wout;
   const int M = a.B * Ho * Wo, N = a.Cout;
   const int nN = ceil_div(N, BN);
-  const int bid = xcd_remap_p(blockIdx.x, gridDim.x);
+  int bid = xcd_remap_p(blockIdx.x, gridDim.x);
+  int split = 0;
+  if (KSPLIT) {
+    const int per_split = gridDim.x / a.ksplit;
+    split = bid / per_split;
+    bid -= split * per_split;
+  }
   const int mt = bid / nN, nt = bid - (bid / nN) * nN;
   const int m0 = mt * BM, n0 = nt * BN;
   const int HWo = Ho * Wo;
@@ -163,8 +170,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     }
   };
   const bool pro_silu = !a.pro_nosilu;
+  // input-channel chunks of this block (a K split: its share of them)
+  const int nchunks_all = a.Cin1 / kC;
+  const int c_begin = KSPLIT ? split * nchunks_all / a.ksplit : 0;
+  const int c_end = KSPLIT ? (split + 1) * nchunks_all / a.ksplit : nchunks_all;
+  // GroupNorm tables: [image of the tile][channel of the block's chunks] scales, then the shifts
   const int tab_img0 = b0;
   const int tab_n = PRO ? min(b0 + g.TB, a.B) - b0 : 0;
+  const int tab_c0 = c_begin * kC, tab_c = (c_end - c_begin) * kC;
   // GroupNorm + SiLU of passes j0, j0 + 1 (tables from LDS), then split and store them into buffer buf
   // (padding stays exactly 0: applied after the transform)
   bool bad = false;
@@ -174,12 +187,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 #pragma unroll
     for (int j = j0; j < j0 + 2; ++j) {
       if (PRO) {
-        const float* ts = gtab + min(pimg[j] - tab_img0, tab_n - 1) * a.Cin1 + chunk * kC + 8 * sq;
+        const float* ts = gtab + min(pimg[j] - tab_img0, tab_n - 1) * tab_c + chunk * kC - tab_c0 + 8 * sq;
         f4 sc[2], sh[2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           sc[h] = *reinterpret_cast<const f4*>(ts + 4 * h);
-          sh[h] = *reinterpret_cast<const f4*>(ts + tab_n * a.Cin1 + 4 * h);
+          sh[h] = *reinterpret_cast<const f4*>(ts + tab_n * tab_c + 4 * h);
         }
 #pragma unroll
         for (int h = 0; h < 2; ++h)
@@ -256,17 +269,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     }
   };
 
-  const int nchunks = a.Cin1 / kC;
-  const int kt_end = nchunks * NTAP;
+  const int kt_begin = c_begin * NTAP, kt_end = c_end * NTAP;
 #pragma unroll
-  for (int d = 0; d < WD; ++d) load_b(bq[d], slice_off(min(d, kt_end - 1)));
+  for (int d = 0; d < WD; ++d) load_b(bq[d], slice_off(min(kt_begin + d, kt_end - 1)));
   // the first chunk's patch (all four passes) is in flight while the GroupNorm tables are built
-  load_patch(0, 0);
+  load_patch(c_begin, 0);
   f4 rq[2][2];
 #pragma unroll
   for (int j = 2; j < 4; ++j) {
-    rq[j & 1][0] = *reinterpret_cast<const f4*>(psrc[j]);
-    rq[j & 1][1] = *reinterpret_cast<const f4*>(psrc[j] + 4);
+    rq[j & 1][0] = *reinterpret_cast<const f4*>(psrc[j] + tab_c0);
+    rq[j & 1][1] = *reinterpret_cast<const f4*>(psrc[j] + tab_c0 + 4);
   }
   if (PRO) {
     if (a.gin_part) {
@@ -288,8 +300,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
         gstat[2 * i + 1] = (float)(1.0 / sqrt(var + (double)a.gin_eps));
       }
       __syncthreads();
-      for (int i = t; i < tab_n * a.Cin1; i += 256) {
-        const int bi = i / a.Cin1, c = i - (i / a.Cin1) * a.Cin1;
+      for (int i = t; i < tab_n * tab_c; i += 256) {
+        const int bi = i / tab_c, c = tab_c0 + i - (i / tab_c) * tab_c;
         const int si = 2 * (bi * G + c / cpg);
         const float mu = gstat[si], rs = gstat[si + 1];
         float sc = rs * (a.gin_gamma ? a.gin_gamma[c] : 1.0f);
@@ -301,34 +313,35 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
           sh = sh * f + (a.gin_mb ? a.gin_mb[mo] : 0.0f);
         }
         gtab[i] = sc;
-        gtab[tab_n * a.Cin1 + i] = sh;
+        gtab[tab_n * tab_c + i] = sh;
       }
     } else {
-      for (int i = t; i < tab_n * a.Cin1; i += 256) {
-        gtab[i] = a.pro_scale[(size_t)tab_img0 * a.Cin1 + i];
-        gtab[tab_n * a.Cin1 + i] = a.pro_shift[(size_t)tab_img0 * a.Cin1 + i];
+      for (int i = t; i < tab_n * tab_c; i += 256) {
+        const int bi = i / tab_c, c = tab_c0 + i - (i / tab_c) * tab_c;
+        gtab[i] = a.pro_scale[(size_t)(tab_img0 + bi) * a.Cin1 + c];
+        gtab[tab_n * tab_c + i] = a.pro_shift[(size_t)(tab_img0 + bi) * a.Cin1 + c];
       }
     }
     __syncthreads();
   }
-  finish_patch(0, 0, 0);
+  finish_patch(c_begin, 0, c_begin & 1);
   rp[0][0] = rq[0][0];
   rp[0][1] = rq[0][1];
   rp[1][0] = rq[1][0];
   rp[1][1] = rq[1][1];
-  finish_patch(0, 2, 0);
+  finish_patch(c_begin, 2, c_begin & 1);
   __syncthreads();
   K32_STAMP(1);
   // One barrier per chunk (double-buffered patch; the other buffer is free once every wave has passed
   // the previous chunk's barrier). The next chunk's patch goes in two halves: passes 0, 1 loaded at tap
   // 0 and finished (GroupNorm + SiLU, split, LDS store) at tap 2, passes 2, 3 loaded at tap 3 and
   // finished at tap 5 -- each load has two taps (96 MFMAs) to land.
-  for (int c0 = 0; c0 < nchunks; c0 += CPI) {
+  for (int c0 = c_begin; c0 < c_end; c0 += CPI) {
 #pragma unroll
     for (int cc = 0; cc < CPI; ++cc) {
       const int c = c0 + cc;
-      if (c >= nchunks) break;
-      const int cn = min(c + 1, nchunks - 1);  // after the last chunk: reloaded into an unused buffer
+      if (c >= c_end) break;
+      const int cn = min(c + 1, c_end - 1);  // after the last chunk: reloaded into an unused buffer
 #pragma unroll
       for (int tap = 0; tap < NTAP; ++tap) {
         const int kt = c * NTAP + tap;
@@ -349,25 +362,26 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 
   K32_STAMP(2);
   // ---- segment 2: 1x1 product of x2 (the ResBlock shortcut), K = Cin2 in 32-channel steps, un-pipelined
-  if (a.Cin2 > 0) {
+  if (a.Cin2 > 0 && (!KSPLIT || split == a.ksplit - 1)) {
+    constexpr int RJ = BM / 64;  // staging passes of 64 rows
     const size_t s2 = (size_t)(NTAP * a.Cin1 / 16) * sl + (size_t)(q >> 1) * sl;  // 16-slices 9 Cin1/16 + 2 c2 + (q>>1)
     int abase[TM];
 #pragma unroll
     for (int i = 0; i < TM; ++i) abase[i] = (wm * WM + i * 16 + l16) * kRowH + q * 8;
-    const float* xsrc[2];
+    const float* xsrc[RJ];
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < RJ; ++j)
       xsrc[j] = a.x2 + (size_t)min(m0 + srow + 64 * j, M - 1) * a.x2_pitch + 8 * sq;
     for (int c2 = 0; c2 < a.Cin2 / kC; ++c2) {
-      f4 r[2][2];
+      f4 r[RJ][2];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < RJ; ++j) {
         r[j][0] = *reinterpret_cast<const f4*>(xsrc[j] + c2 * kC);
         r[j][1] = *reinterpret_cast<const f4*>(xsrc[j] + c2 * kC + 4);
       }
       load_b(bq[0], s2 + (size_t)(2 * c2) * sl);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {  // rows >= M hold clamped data: never stored
+      for (int j = 0; j < RJ; ++j) {  // rows >= M hold clamped data: never stored
         f16x8 pc[2];
         Split<2>::split(r[j][0], r[j][1], pc, bad);
         const int row = srow + 64 * j;
@@ -405,9 +419,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
         for (int r = 0; r < 4; ++r) st[((i - 2 * h) * 16 + 4 * q + r) * Epi::EP + j * 16 + l16] = acc[i][j][r] * cs[j];
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes are visible to its reads
     __builtin_amdgcn_wave_barrier();
-    epi.rows(st, wrow0 + 32 * h);
+    if (KSPLIT)
+      epi.rows_raw(st, wrow0 + 32 * h, a.kpart + (size_t)split * M * N, N);
+    else
+      epi.rows(st, wrow0 + 32 * h);
     __builtin_amdgcn_wave_barrier();  // the next slab's writes reuse the region
-    if (a.gn_part && (h & 1)) epi.emit(wrow0 + 32 * (h - 1));
+    if (!KSPLIT && a.gn_part && (h & 1)) epi.emit(wrow0 + 32 * (h - 1));
   }
   K32_STAMP(4);
   K32_RSTAMP(6);
@@ -422,62 +439,84 @@ extern "C" int dm_debug_k32_stamps(void* host, int nblocks) {
 }
 #endif
 
-bool conv_k32_ok(const ConvArgs& a) {
-  if (!(a.ws && a.ws_np == 2 && a.ws_rowscale && a.taps == 9 && a.stride == 1 && a.upsample == 0 && a.ksplit <= 1))
-    return false;
-  if (a.Cin1 < kC || a.Cin1 % kC != 0 || a.Cin2 % kC != 0 || a.K != 9 * a.Cin1 + a.Cin2) return false;
-  if (a.Wout < 8 || a.Wout % 8 != 0 || BM_K32 % a.Wout != 0) return false;
+// Variants: 1 = 128 x 128 tiles, 2 = 128 x 64 (whole K), 3 = 64 x 64 and 4 = 64 x 128 split-K tiles.
+int conv_k32_variant_ok(const ConvArgs& a, int v) {
+  if (!(a.ws && a.ws_np == 2 && a.ws_rowscale && a.taps == 9 && a.stride == 1 && a.upsample == 0)) return 0;
+  if (a.Cin1 < kC || a.Cin1 % kC != 0 || a.Cin2 % kC != 0 || a.K != 9 * a.Cin1 + a.Cin2) return 0;
+  const bool split = v >= 3;
+  const int bm = split ? 64 : BM_K32;
+  if (split ? !(a.ksplit > 1 && a.kpart && a.ksplit <= a.Cin1 / kC) : a.ksplit > 1) return 0;
+  if (a.Wout > bm || bm % a.Wout != 0) return 0;
   PatchGeom g;
-  if (!conv_patch_geom(a, BM_K32, g) || g.P > kMaxP || g.TB > 2) return false;
-  if (a.pro_scale && 2 * g.TB * a.Cin1 > kTab) return false;
-  if (a.gin_part && g.TB * a.gin_G > kStats) return false;
-  return staged_epilogue_ok(a);  // the epilogue's 16-byte loads / stores of 4 consecutive channels
+  if (!conv_patch_geom(a, bm, g) || g.P > kMaxP || g.TB > (split ? 4 : 2)) return 0;
+  const int nch = a.Cin1 / kC, tab_c = split ? ceil_div(nch, a.ksplit) * kC : a.Cin1;
+  if (a.pro_scale && 2 * g.TB * tab_c > kTab) return 0;
+  if (a.gin_part && g.TB * a.gin_G > kStats) return 0;
+  if (split) {  // raw partial sums with 16-byte stores
+    if (a.Cout % 4 != 0 || (reinterpret_cast<uintptr_t>(a.kpart) & 15) != 0) return 0;
+    return 1;
+  }
+  if (a.Wout % 8 != 0) return 0;
+  return staged_epilogue_ok(a) ? 1 : 0;  // the epilogue's 16-byte loads / stores of 4 consecutive channels
 }
 
-// Which conv_k32 tile (128: 128 x 128, 64: 128 x 64) runs this conv, 0 = none. Forced by tile 10 / 11;
-// otherwise it replaces conv_patch3's fp16x2 128 x 128 / 128 x 64 tiles (picks 3 / 4) unless
-// DM_CONV_K32=0.
-int conv_k32_pick(const ConvArgs& a) {
-  if (a.tile == 10 || a.tile == 11) return conv_k32_ok(a) ? (a.tile == 10 ? 128 : 64) : 0;
-  if (a.tile != 0) return 0;
-  static const bool off = [] {
+bool conv_k32_ok(const ConvArgs& a) { return conv_k32_variant_ok(a, 1) != 0; }
+
+// Which conv_k32 variant runs this conv, 0 = none. Forced by tile 10 / 11 (128-row tiles) and 12 / 13
+// (split-K 64-row tiles); otherwise it replaces conv_patch3's fp16x2 tiles for 3x3 stride-1 convs
+// unless DM_CONV_K32=0.
+bool conv_k32_enabled() {
+  static const bool on = [] {
     const char* e = std::getenv("DM_CONV_K32");
-    return e && e[0] == '0';
+    return !(e && e[0] == '0');
   }();
-  if (off || !conv_k32_ok(a)) return 0;
+  return on;
+}
+
+int conv_k32_pick(const ConvArgs& a) {
+  if (a.tile >= 10 && a.tile <= 13) return conv_k32_variant_ok(a, a.tile - 9) ? a.tile - 9 : 0;
+  if (a.tile != 0 || !conv_k32_enabled()) return 0;
+  // split-K convs of maps of <= 16 pixels: 64 x 128 tiles (4x4 maps at B = 256, K split 2: 32.5 us vs
+  // 34.2 us for 64 x 64 and for conv_patch3's 64 x 64 split tiles)
+  if (a.ksplit > 1) return conv_k32_variant_ok(a, 4) ? 4 : conv_k32_variant_ok(a, 3) ? 3 : 0;
+  if (!conv_k32_ok(a)) return 0;
   const int p = conv_pick(a);
   if (p != 3 && p != 4) return 0;
   // 128 x 128 tiles down to one block per CU (measured on 8^2 maps at B = 256: 256 blocks of 128 x 128 beat
   // 512 of 128 x 64 by 6 %); the nominal batch (pick_B) keeps the choice batch-invariant
   const long M = (long)(a.pick_B > 0 ? a.pick_B : a.B) * a.Hout * a.Wout;
-  return ((M + 127) / 128) * ((a.Cout + 127) / 128) >= 256 ? 128 : 64;
+  return ((M + 127) / 128) * ((a.Cout + 127) / 128) >= 256 ? 1 : 2;
 }
 
 // rocprofv3's name of the instantiation conv2d_k32 launches (spaces removed)
-std::string conv_k32_label(const ConvArgs& a, int bn) {
-  std::string s = bn == 128 ? "conv_k32_kernel<128,64,64," : "conv_k32_kernel<64,64,32,";
-  return s + (a.pro_scale ? "true>" : "false>");
+std::string conv_k32_label(const ConvArgs& a, int v) {
+  static const char* names[] = {"", "conv_k32_kernel<128,128,64,64,", "conv_k32_kernel<128,64,64,32,",
+                                "conv_k32_kernel<64,64,32,32,", "conv_k32_kernel<64,128,32,64,"};
+  return std::string(names[v]) + (a.pro_scale ? "true," : "false,") + (v >= 3 ? "true>" : "false>");
 }
 
-int conv2d_k32(const ConvArgs& a, int bn, hipStream_t st) {
-  DM_REQUIRE(conv_k32_ok(a), "conv: shape not supported by the K = 32 split kernel");
-  DM_REQUIRE(bn == 128 || bn == 64, "conv: K = 32 split kernel tiles are 128 x 128 and 128 x 64");
-  PatchGeom g;
-  conv_patch_geom(a, BM_K32, g);
+template <int BM, int BN, int WM, int WN, bool KSPLIT>
+static void launch_k32(const ConvArgs& a, const PatchGeom& g, hipStream_t st) {
   const int M = a.B * a.Hout * a.Wout;
-  const int blocks = ceil_div(M, BM_K32) * ceil_div(a.Cout, bn);
-  if (bn == 128) {
-    if (a.pro_scale)
-      hipLaunchKernelGGL((conv_k32_kernel<128, 64, 64, true>), dim3(blocks), dim3(256), 0, st, a, g);
-    else
-      hipLaunchKernelGGL((conv_k32_kernel<128, 64, 64, false>), dim3(blocks), dim3(256), 0, st, a, g);
-  } else {
-    if (a.pro_scale)
-      hipLaunchKernelGGL((conv_k32_kernel<64, 64, 32, true>), dim3(blocks), dim3(256), 0, st, a, g);
-    else
-      hipLaunchKernelGGL((conv_k32_kernel<64, 64, 32, false>), dim3(blocks), dim3(256), 0, st, a, g);
+  const int blocks = ceil_div(M, BM) * ceil_div(a.Cout, BN) * (KSPLIT ? a.ksplit : 1);
+  if (a.pro_scale)
+    hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, true, KSPLIT>), dim3(blocks), dim3(256), 0, st, a, g);
+  else
+    hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, false, KSPLIT>), dim3(blocks), dim3(256), 0, st, a, g);
+}
+
+int conv2d_k32(const ConvArgs& a, int v, hipStream_t st) {
+  DM_REQUIRE(v >= 1 && v <= 4 && conv_k32_variant_ok(a, v), "conv: shape not supported by the K = 32 split kernel");
+  PatchGeom g;
+  conv_patch_geom(a, v >= 3 ? 64 : BM_K32, g);
+  switch (v) {
+    case 1: launch_k32<128, 128, 64, 64, false>(a, g, st); break;
+    case 2: launch_k32<128, 64, 64, 32, false>(a, g, st); break;
+    case 3: launch_k32<64, 64, 32, 32, true>(a, g, st); break;
+    default: launch_k32<64, 128, 32, 64, true>(a, g, st); break;
   }
   DM_LAUNCH_CHECK();
+  if (v >= 3) return conv_splitk_reduce(a, st);
   return DM_OK;
 }
 

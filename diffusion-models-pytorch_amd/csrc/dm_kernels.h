@@ -224,12 +224,15 @@ bool conv_split_eligible(const ConvArgs& a);
 bool conv_seg_eligible(const ConvArgs& a);
 int conv2d_patch3(const ConvArgs& a, int which, const PatchGeom& g, hipStream_t st);
 // fp16x2 split conv with K = 32 steps on v_mfma_f32_16x16x32_f16 (conv_k32.hip): 3x3 stride-1 MODE 0
-// shapes of 16- / 32-pixel-wide maps. conv_k32_pick: 128 (128 x 128 tile), 64 (128 x 64) or 0 (not this
-// kernel; forced by ConvArgs::tile 10 / 11, else replaces conv_patch3's 128-row tiles unless DM_CONV_K32=0)
+// shapes. conv_k32_pick -> variant 1 (128 x 128 tiles), 2 (128 x 64), 3 (64 x 64 split-K), 4 (64 x 128
+// split-K) or 0 (not this kernel); forced by ConvArgs::tile 10..13, else it replaces conv_patch3's
+// 128-row and split-K tiles unless DM_CONV_K32=0)
 bool conv_k32_ok(const ConvArgs& a);
+int conv_k32_variant_ok(const ConvArgs& a, int v);
 int conv_k32_pick(const ConvArgs& a);
-int conv2d_k32(const ConvArgs& a, int bn, hipStream_t st);
-std::string conv_k32_label(const ConvArgs& a, int bn);
+bool conv_k32_enabled();  // DM_CONV_K32 != 0
+int conv2d_k32(const ConvArgs& a, int v, hipStream_t st);
+std::string conv_k32_label(const ConvArgs& a, int v);
 int conv_splitk_reduce(const ConvArgs& a, hipStream_t st);
 // fp32 packed conv weights [nmat][rows][K] -> split slices for conv_patch3_kernel (np 3: bf16x3,
 // np 2: fp16x2 + row scales); split_conv_rowscale gives ConvArgs::ws_rowscale of an fp16x2 copy

@@ -688,7 +688,9 @@ int UNetModel::build_plan(int B, int H, int W) {
   size_t kpart_floats = 0;
   auto maybe_split = [&](ConvArgs& c) {
     if (c.upsample == 2 || c.taps != 9 || c.Hout * c.Wout > 16 || conv_pick(c) < 3) return;
-    const int ks = std::min(4, c.Cin1 / 32);
+    // K32 split tiles (conv_k32.hip): 2 splits (4x4 maps, B = 256: 32.5 us vs 37.8 us with 4, the
+    // reduction included); conv_patch3's 16-channel chunks: 4
+    const int ks = std::min(conv_k32_enabled() ? 2 : 4, c.Cin1 / 32);
     if (ks < 2) return;
     const size_t need = (size_t)ks * c.B * c.Hout * c.Wout * c.Cout;
     if (need > kpart_floats) {

@@ -94,6 +94,7 @@ class ConvDesc(ctypes.Structure):
         ('tile', ctypes.c_int),
         ('pro_scale', vp), ('pro_shift', vp),
         ('w_split', vp), ('w_split_kind', ctypes.c_int), ('range_flag', vp), ('pro_nosilu', ctypes.c_int),
+        ('ksplit', ctypes.c_int), ('kpart', vp),
     ]
 
 

@@ -280,6 +280,10 @@ typedef struct dm_conv_desc {
   int w_split_kind;  /* DM_SPLIT_BF16X3 or DM_SPLIT_FP16X2 */
   int* range_flag;   /* optional device int, set to 1 when an fp16x2 conv meets |x| > 65504 */
   int pro_nosilu;    /* 1: the input prologue is x * pro_scale + pro_shift alone (no SiLU) */
+  /* optional split-K of a 3x3 stride-1 conv (0 / 1: none): partial sums of ksplit input-channel
+   * ranges go to kpart ([ksplit][B * Hout * Wout][Cout] floats), then one reduction applies the epilogue */
+  int ksplit;
+  float* kpart;
 } dm_conv_desc;
 /* 1x1 convs (taps 1, K = Cin, Cin % 32 == 0) with DM_SPLIT_FP16X2 weights run on the split kernel
  * with the same prologue / epilogue options: the static-weight GEMMs of the attention blocks. */

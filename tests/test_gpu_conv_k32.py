@@ -2,8 +2,9 @@
 torch references, as tests/test_gpu_conv_split.py does for conv_patch3: integer operands compare bit for
 bit (indexing, padding, tap walk, both K segments, epilogue), random operands must keep fp32-level
 accuracy (within 2x of the fp32 MFMA kernel's error vs fp64), and an activation beyond fp16's range must
-raise the range flag. Tiles: 10 = 128 x 128, 11 = 128 x 64 (forced); 0 = the automatic choice, which
-takes this kernel for the 8- / 16- / 32-pixel-wide maps the UNets run at 128-row tiles."""
+raise the range flag. Tiles: 10 = 128 x 128, 11 = 128 x 64, 12 / 13 = 64 x 64 / 64 x 128 split-K (forced);
+0 = the automatic choice, which takes this kernel for the 8- / 16- / 32-pixel-wide maps the UNets run at
+128-row tiles and for the split-K convs of maps of <= 16 pixels."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -83,3 +84,52 @@ def test_k32_range_flag(cuda):
         flag = torch.zeros(1, dtype=torch.int32, device=cuda)
         _run_conv(cuda, _nhwc(x * scale).to(cuda), wp, C, H, H, 9, 1, 0, tile=10, split='fp16x2', range_flag=flag)
         assert int(flag.item()) == expect
+
+
+@pytest.mark.parametrize('tile', [12, 13, 0])
+@pytest.mark.parametrize('ksplit', [2, 4])
+@pytest.mark.parametrize('B,Cin,Cout,H', [(5, 256, 256, 4), (3, 128, 64, 4), (2, 256, 128, 2)])
+def test_k32_splitk_exact(cuda, B, Cin, Cout, H, ksplit, tile):
+    """split-K tiles (maps of <= 16 pixels): partial sums over input-channel ranges, reduced with bias."""
+    x = _ints((B, Cin, H, H), -2, 3, seed=30)
+    w = _ints((Cout, Cin, 3, 3), -2, 3, seed=31)
+    b = _ints((Cout, ), seed=32)
+    ref = F.conv2d(x.double(), w.double(), b.double(), padding=1).float()
+    y = _run_conv(cuda, _nhwc(x).to(cuda), _pack(w, cuda), Cout, H, H, 9, 1, 0, b.to(cuda), tile=tile,
+                  split='fp16x2', ksplit=ksplit)
+    assert torch.equal(y.cpu(), _nhwc(ref))
+
+
+@pytest.mark.parametrize('tile', [12, 13])
+def test_k32_splitk_segments_rowvec_residual(cuda, tile):
+    B, C1, C2, Cout, H = 3, 256, 64, 128, 4
+    h = _ints((B, C1, H, H), seed=40)
+    x = _ints((B, C2, H, H), seed=41)
+    w2 = _ints((Cout, C1, 3, 3), -2, 3, seed=42)
+    ws = _ints((Cout, C2, 1, 1), seed=43)
+    b = _ints((Cout, ), seed=44)
+    rv = _ints((B, Cout), seed=45)
+    res = _ints((B, Cout, H, H), seed=46)
+    K = 9 * C1 + C2
+    wp = torch.zeros((Cout, K), device=cuda)
+    _pack(w2, cuda, K, 0, wp)
+    _pack(ws, cuda, K, 9 * C1, wp)
+    ref = (F.conv2d(h.double(), w2.double(), b.double(), padding=1) + rv.double()[:, :, None, None]
+           + F.conv2d(x.double(), ws.double()) + res.double()).float()
+    y = _run_conv(cuda, _nhwc(h).to(cuda), wp, Cout, H, H, 9, bias=b.to(cuda), rowvec=rv.to(cuda),
+                  res=_nhwc(res).to(cuda), x2=_nhwc(x).to(cuda), Cin2=C2, tile=tile, split='fp16x2', ksplit=4)
+    assert torch.equal(y.cpu(), _nhwc(ref))
+
+
+@pytest.mark.parametrize('B,Cin,Cout,H', [(16, 256, 256, 4), (8, 512, 256, 4)])
+def test_k32_splitk_fp32_accuracy(cuda, B, Cin, Cout, H):
+    xd, wp, b, pro, ref = _rand_case(cuda, B, Cin, Cout, H, 0, seed=92)
+    errs = {}
+    for name, split, tile in (('fp32', False, 0), ('k32s', 'fp16x2', 12), ('k32s128', 'fp16x2', 13)):
+        y = _run_conv(cuda, xd, wp, Cout, H, H, 9, 1, 0, b.to(cuda), pro=pro, split=split, tile=tile,
+                      ksplit=4 if split else 0)
+        errs[name] = (y.cpu().double() - _nhwc(ref)).abs().max().item()
+    scale = ref.abs().max().item()
+    for k in ('k32s', 'k32s128'):
+        assert errs[k] < 2.0 * errs['fp32'] + 1e-7 * scale, errs
+        assert errs[k] < 4e-6 * scale, (errs, scale)

@@ -25,13 +25,14 @@ SHAPES = {
     'res16_256': (256, 256, 256, 16, True, 0),
     'res8_256': (256, 256, 256, 8, True, 0),
     'res4_256': (256, 256, 256, 4, True, 0),
+    'res4_512': (256, 512, 256, 4, True, 0),      # up-path conv1 at 4x4 with concat input
     'up16_256': (256, 256, 256, 16, False, 2),     # sub-pixel upsample 16 -> 32
     'qkv16': (256, 256, 768, 16, True, -1),        # attention qkv: 1x1 conv (GroupNorm prologue, no SiLU)
     'proj16': (256, 256, 256, 16, False, -1),      # attention proj: 1x1 conv
 }
 
 
-def run(name, iters, split, tile=0):
+def run(name, iters, split, tile=0, ksplit=0):
     B, Cin, Cout, H, pro, up = SHAPES[name]
     dev = torch.device('cuda', 0)
     g = torch.Generator(device='cpu').manual_seed(0)
@@ -71,6 +72,9 @@ def run(name, iters, split, tile=0):
         kind = dmhip.SPLIT_FP16X2 if split == 'fp16x2' else dmhip.SPLIT_BF16X3
         ws = dmhip.pack_conv_weight_split(wp, 4 if up == 2 else 1, Cin, 4 if up == 2 else taps, kind)
         d.w_split, d.w_split_kind = ws.data_ptr(), kind
+    if ksplit > 1:
+        kpart = torch.empty((ksplit, B * Ho * Ho, Cout), device=dev)
+        d.ksplit, d.kpart = ksplit, kpart.data_ptr()
     for _ in range(3):
         dmhip.conv2d_nhwc(d, dev)
     torch.cuda.synchronize()
@@ -87,6 +91,7 @@ def run(name, iters, split, tile=0):
     tf = flops / ms / 1e9
     tag = split or 'fp32'
     tag = f'{tag}/t{tile}' if tile else tag
+    tag = f'{tag}/k{ksplit}' if ksplit > 1 else tag
     print(f'{name:12s} {tag:7s} {ms:8.4f} ms  {tf:6.1f} TF/s  {tf / 157.3 * 100:5.1f} % of fp32 peak', flush=True)
 
 
@@ -96,13 +101,14 @@ def main():
     ap.add_argument('--shape', default=None)
     ap.add_argument('--math', choices=['fp32', 'bf16x3', 'fp16x2', 'all'], default='all')
     ap.add_argument('--tiles', default='0', help='comma-separated ConvDesc.tile values (0 = auto)')
+    ap.add_argument('--ksplit', type=int, default=0, help='split-K (ConvDesc.ksplit; with a workspace)')
     args = ap.parse_args()
     dmhip.load()
     for name in ([args.shape] if args.shape else SHAPES):
         kinds = (False, 'bf16x3', 'fp16x2') if args.math == 'all' else ({'fp32': False}.get(args.math, args.math), )
         for split in kinds:
             for tile in [int(v) for v in args.tiles.split(',')]:
-                run(name, args.iters, split, tile)
+                run(name, args.iters, split, tile, args.ksplit)
 
 
 if __name__ == '__main__':
