@@ -63,6 +63,7 @@ struct StagedEpilogue {
   const ConvArgs& a;
   int M, HWo, b0, c4, rsub, ncol, nc;
   bool c_ok, one_image;
+  int sub_w = 0, sub_ho = 0, sub_wo = 0, sub_py = 0, sub_px = 0;  // sub-pixel scatter (sub())
   f4 bias4, rv4;
   double gs[4], gq[4];
 
@@ -82,6 +83,21 @@ struct StagedEpilogue {
 #pragma unroll
     for (int e = 0; e < 4; ++e) gs[e] = gq[e] = 0.0;
   }
+  // sub-pixel upsample conv: tile row m = low-res pixel (b, iy, ix) of width w stores to output pixel
+  // (b, 2 iy + py, 2 ix + px) of the ho x wo map
+  __device__ __forceinline__ void sub(int w, int ho, int wo, int py, int px) {
+    sub_w = w;
+    sub_ho = ho;
+    sub_wo = wo;
+    sub_py = py;
+    sub_px = px;
+  }
+  __device__ __forceinline__ size_t out_row(int m) const {
+    if (!sub_w) return (size_t)m;
+    const int bb = m / HWo, rr = m - bb * HWo;
+    const int iy = rr / sub_w, ix = rr - iy * sub_w;
+    return ((size_t)bb * sub_ho + 2 * iy + sub_py) * sub_wo + 2 * ix + sub_px;
+  }
   // the slab's rows are output rows row0 .. row0 + 31 (this wave's slab written and visible)
   __device__ __forceinline__ void rows(const float* st, int row0) {
     f4 rs4[32 / RPI];
@@ -89,7 +105,7 @@ struct StagedEpilogue {
 #pragma unroll
       for (int it = 0; it < 32 / RPI; ++it) {
         const int m = min(row0 + it * RPI + rsub, M - 1);
-        rs4[it] = *reinterpret_cast<const f4*>(a.res + (size_t)m * a.res_pitch + nc);
+        rs4[it] = *reinterpret_cast<const f4*>(a.res + out_row(m) * a.res_pitch + nc);
       }
     }
 #pragma unroll
@@ -102,7 +118,7 @@ struct StagedEpilogue {
         v = v + (one_image ? rv4
                            : *reinterpret_cast<const f4*>(a.rowvec + (size_t)(min(m, M - 1) / HWo) * a.rowvec_pitch + nc));
       if (a.res) v = v + rs4[it];
-      if (m < M && c_ok) *reinterpret_cast<f4*>(a.y + (size_t)m * a.y_pitch + ncol) = v;
+      if (m < M && c_ok) *reinterpret_cast<f4*>(a.y + out_row(m) * a.y_pitch + ncol) = v;
       if (a.gn_part && m < M) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {

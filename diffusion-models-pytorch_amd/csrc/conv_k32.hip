@@ -68,19 +68,22 @@ __device__ unsigned long long g_k32_stamps[65536][8];
 
 // KSPLIT: split-K over 32-channel chunks for maps of <= 16 pixels (64-row tiles of 4 images): raw partial
 // sums to kpart [ksplit][M][Cout], the epilogue in conv_splitk_reduce (conv_patch.hip), as conv_patch3.
-template <int BM, int BN, int WM, int WN, bool PRO, bool KSPLIT>
+// SUB: the sub-pixel form of nearest-2x + 3x3 (models/modules.py:60-63; conv_patch3 MODE 2): per output
+// parity (py, px) a 2x2-tap conv of the low-res input with pre-combined weights (repack_subpixel), tiles
+// over low-res pixels, the epilogue scattering row (iy, ix) to output pixel (2 iy + py, 2 ix + px).
+template <int BM, int BN, int WM, int WN, bool PRO, bool KSPLIT, bool SUB = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) conv_k32_kernel(ConvArgs a, PatchGeom g) {
   constexpr int NWN = BN / WN;
   static_assert((BM / WM) * NWN == 4, "4 waves per block");
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int PJ = (kMaxP + 63) / 64;  // loader passes of 64 pixels (4 threads per pixel)
   constexpr int PATCH = kMaxP * kRowH;
-  constexpr int NTAP = 9, WD = 2, CPI = 2;  // B ring depth; chunks per loop iteration (slot = compile-time)
+  constexpr int NTAP = SUB ? 4 : 9, WD = 2, CPI = 2;  // B ring depth; chunks per loop iteration (slot = compile-time)
   __shared__ __attribute__((aligned(16))) _Float16 patch[2 * PATCH];
   __shared__ __attribute__((aligned(16))) float gtab[PRO ? kTab : 4];
   __shared__ float gstat[PRO ? 2 * kStats : 2];
 
-  const int Ho = a.Hout, Wo = a.Wout;
+  const int Ho = SUB ? a.Hin : a.Hout, Wo = SUB ? a.Win : a.Wout;  // the tiled (GEMM-row) resolution
   const int M = a.B * Ho * Wo, N = a.Cout;
   const int nN = ceil_div(N, BN);
   int bid = xcd_remap_p(blockIdx.x, gridDim.x);
@@ -90,6 +93,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     split = bid / per_split;
     bid -= split * per_split;
   }
+  int par = 0;
+  if (SUB) {
+    const int per_par = ceil_div(M, BM) * nN;
+    par = bid / per_par;
+    bid -= par * per_par;
+  }
+  const int py = par >> 1, px = par & 1;
   const int mt = bid / nN, nt = bid - (bid / nN) * nN;
   const int m0 = mt * BM, n0 = nt * BN;
   const int HWo = Ho * Wo;
@@ -134,7 +144,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   for (int j = 0; j < TN; ++j) {
     const int col = n0 + wn * WN + j * 16 + l16;
     const int grp = min(col >> 5, ngrp - 1);  // columns >= N: clamped / zero padding, never stored
-    wbase[j] = reinterpret_cast<const _Float16*>(a.ws) + (size_t)grp * 1024 + ((q & 1) * 32 + (col & 31)) * 8;
+    wbase[j] = reinterpret_cast<const _Float16*>(a.ws) + (size_t)par * (a.K / 16) * sl + (size_t)grp * 1024 +
+               ((q & 1) * 32 + (col & 31)) * 8;
   }
   const size_t qoff = (size_t)(q >> 1) * NTAP * sl;  // k-groups 2, 3: the chunk's second 16-slice of the tap
   // step kt = c * 9 + tap of the main segment: 16-slices 2c * 9 + tap (+ 9 for k-groups 2, 3)
@@ -242,8 +253,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   // One tap of the main loop. a0 holds tile 0's fragment of this tap on entry (read ahead) and, for
   // taps 0 .. 7, tile 0's fragment of the next tap on exit, so a tap never opens on an LDS-read wait.
   f16x8 a0[2];
+  auto tap_y = [&](int tap) { return SUB ? py + (tap >> 1) : tap / 3; };
+  auto tap_x = [&](int tap) { return SUB ? px + (tap & 1) : tap % 3; };
   auto read_a0 = [&](int tap, int pbuf) {
-    const _Float16* As = patch + pbuf * PATCH + a_off(0, tap / 3, tap % 3);
+    const _Float16* As = patch + pbuf * PATCH + a_off(0, tap_y(tap), tap_x(tap));
     a0[0] = *reinterpret_cast<const f16x8*>(As);
     a0[1] = *reinterpret_cast<const f16x8*>(As + 32);
   };
@@ -256,7 +269,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     for (int i = 1; i < TM; ++i)
 #pragma unroll
       for (int p = 0; p < 2; ++p)
-        av[i][p] = *reinterpret_cast<const f16x8*>(As + a_off(i, tap / 3, tap % 3) + p * 32);
+        av[i][p] = *reinterpret_cast<const f16x8*>(As + a_off(i, tap_y(tap), tap_x(tap)) + p * 32);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -346,7 +359,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
       for (int tap = 0; tap < NTAP; ++tap) {
         const int kt = c * NTAP + tap;
         const int slot = (cc * NTAP + tap) % WD;
-        if (tap == 0 || tap == 3) {
+        // passes 0, 1: loaded at tap 0, finished at F1; passes 2, 3: loaded at L2, finished at F2
+        constexpr int F1 = SUB ? 1 : 2, L2 = SUB ? 2 : 3, F2 = SUB ? 3 : 5;
+        if (tap == 0 || tap == L2) {
           load_patch(cn, tap == 0 ? 0 : 2);
           __builtin_amdgcn_sched_barrier(0);
         }
@@ -354,7 +369,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
         compute_tap(tap, c & 1, bq[slot]);
         load_b(bq[slot], slice_off(min(kt + WD, kt_end - 1)));
         __builtin_amdgcn_sched_barrier(0);  // keep the refill WD taps ahead
-        if (tap == 2 || tap == 5) finish_patch(cn, tap == 2 ? 0 : 2, (c + 1) & 1);
+        if (tap == F1 || tap == F2) finish_patch(cn, tap == F1 ? 0 : 2, (c + 1) & 1);
       }
       __syncthreads();
     }
@@ -406,6 +421,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   float* st = reinterpret_cast<float*>(patch) + wave * 32 * Epi::EP;
   const int wrow0 = m0 + wm * WM;
   Epi epi(a, M, HWo, b0, (HWo % BM) == 0, n0 + wn * WN, lane);
+  if (SUB) epi.sub(Wo, a.Hout, a.Wout, py, px);
   float cs[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) cs[j] = a.ws_rowscale[min(n0 + wn * WN + j * 16 + l16, N - 1)];
@@ -441,12 +457,16 @@ extern "C" int dm_debug_k32_stamps(void* host, int nblocks) {
 
 // Variants: 1 = 128 x 128 tiles, 2 = 128 x 64 (whole K), 3 = 64 x 64 and 4 = 64 x 128 split-K tiles.
 int conv_k32_variant_ok(const ConvArgs& a, int v) {
-  if (!(a.ws && a.ws_np == 2 && a.ws_rowscale && a.taps == 9 && a.stride == 1 && a.upsample == 0)) return 0;
-  if (a.Cin1 < kC || a.Cin1 % kC != 0 || a.Cin2 % kC != 0 || a.K != 9 * a.Cin1 + a.Cin2) return 0;
+  const bool sub = a.upsample == 2;  // sub-pixel nearest-2x + 3x3: 4 parity convs of 4 taps
+  if (!(a.ws && a.ws_np == 2 && a.ws_rowscale && a.taps == 9 && a.stride == 1 && (a.upsample == 0 || sub))) return 0;
+  if (a.Cin1 < kC || a.Cin1 % kC != 0 || a.Cin2 % kC != 0) return 0;
+  if (sub ? (a.Cin2 != 0 || a.K != 4 * a.Cin1) : a.K != 9 * a.Cin1 + a.Cin2) return 0;
   const bool split = v >= 3;
+  if (split && sub) return 0;
   const int bm = split ? 64 : BM_K32;
   if (split ? !(a.ksplit > 1 && a.kpart && a.ksplit <= a.Cin1 / kC) : a.ksplit > 1) return 0;
-  if (a.Wout > bm || bm % a.Wout != 0) return 0;
+  const int wt = sub ? a.Win : a.Wout;  // tiled width
+  if (wt > bm || bm % wt != 0) return 0;
   PatchGeom g;
   if (!conv_patch_geom(a, bm, g) || g.P > kMaxP || g.TB > (split ? 4 : 2)) return 0;
   const int nch = a.Cin1 / kC, tab_c = split ? ceil_div(nch, a.ksplit) * kC : a.Cin1;
@@ -456,7 +476,7 @@ int conv_k32_variant_ok(const ConvArgs& a, int v) {
     if (a.Cout % 4 != 0 || (reinterpret_cast<uintptr_t>(a.kpart) & 15) != 0) return 0;
     return 1;
   }
-  if (a.Wout % 8 != 0) return 0;
+  if (wt % 8 != 0) return 0;
   return staged_epilogue_ok(a) ? 1 : 0;  // the epilogue's 16-byte loads / stores of 4 consecutive channels
 }
 
@@ -492,13 +512,24 @@ int conv_k32_pick(const ConvArgs& a) {
 std::string conv_k32_label(const ConvArgs& a, int v) {
   static const char* names[] = {"", "conv_k32_kernel<128,128,64,64,", "conv_k32_kernel<128,64,64,32,",
                                 "conv_k32_kernel<64,64,32,32,", "conv_k32_kernel<64,128,32,64,"};
-  return std::string(names[v]) + (a.pro_scale ? "true," : "false,") + (v >= 3 ? "true>" : "false>");
+  return std::string(names[v]) + (a.pro_scale ? "true," : "false,") + (v >= 3 ? "true," : "false,") +
+         (a.upsample == 2 ? "true>" : "false>");
 }
 
 template <int BM, int BN, int WM, int WN, bool KSPLIT>
 static void launch_k32(const ConvArgs& a, const PatchGeom& g, hipStream_t st) {
-  const int M = a.B * a.Hout * a.Wout;
-  const int blocks = ceil_div(M, BM) * ceil_div(a.Cout, BN) * (KSPLIT ? a.ksplit : 1);
+  const bool sub = a.upsample == 2;
+  const int M = sub ? a.B * a.Hin * a.Win : a.B * a.Hout * a.Wout;
+  const int blocks = ceil_div(M, BM) * ceil_div(a.Cout, BN) * (KSPLIT ? a.ksplit : 1) * (sub ? 4 : 1);
+  if constexpr (!KSPLIT) {
+    if (sub) {
+      if (a.pro_scale)
+        hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, true, false, true>), dim3(blocks), dim3(256), 0, st, a, g);
+      else
+        hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, false, false, true>), dim3(blocks), dim3(256), 0, st, a, g);
+      return;
+    }
+  }
   if (a.pro_scale)
     hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, true, KSPLIT>), dim3(blocks), dim3(256), 0, st, a, g);
   else

@@ -10,7 +10,7 @@ import torch
 import torch.nn.functional as F
 
 from tests.test_gpu_conv_split import _rand_case
-from tests.test_gpu_ops import _ints, _nhwc, _pack, _run_conv
+from tests.test_gpu_ops import _ints, _nhwc, _pack, _pack_subpix, _run_conv
 
 pytestmark = pytest.mark.gpu
 TILES = [10, 11, 0]
@@ -131,5 +131,32 @@ def test_k32_splitk_fp32_accuracy(cuda, B, Cin, Cout, H):
         errs[name] = (y.cpu().double() - _nhwc(ref)).abs().max().item()
     scale = ref.abs().max().item()
     for k in ('k32s', 'k32s128'):
+        assert errs[k] < 2.0 * errs['fp32'] + 1e-7 * scale, errs
+        assert errs[k] < 4e-6 * scale, (errs, scale)
+
+
+@pytest.mark.parametrize('tile', TILES)
+@pytest.mark.parametrize('B,Cin,Cout,H', [(3, 64, 64, 16), (2, 256, 128, 8), (1, 96, 96, 16), (4, 64, 128, 8)])
+def test_k32_subpixel_exact(cuda, B, Cin, Cout, H, tile):
+    """sub-pixel form of nearest-2x + 3x3 (4 parity convs of 4 taps), output pixels scattered by parity."""
+    x = _ints((B, Cin, H, H), -2, 3, seed=70)
+    w = _ints((Cout, Cin, 3, 3), -1, 2, seed=71)  # summed sub-pixel weights stay exact in fp16
+    b = _ints((Cout, ), seed=72)
+    ref = F.conv2d(F.interpolate(x, scale_factor=2, mode='nearest').double(), w.double(), b.double(),
+                   padding=1).float()
+    y = _run_conv(cuda, _nhwc(x).to(cuda), _pack_subpix(w, cuda), Cout, 2 * H, 2 * H, 9, 1, 2, b.to(cuda),
+                  tile=tile, split='fp16x2')
+    assert torch.equal(y.cpu(), _nhwc(ref))
+
+
+@pytest.mark.parametrize('B,Cin,Cout,H', [(4, 256, 128, 16), (16, 256, 256, 8)])
+def test_k32_subpixel_fp32_accuracy(cuda, B, Cin, Cout, H):
+    xd, wp, b, pro, ref = _rand_case(cuda, B, Cin, Cout, H, 1, seed=93)
+    errs = {}
+    for name, split, tile in (('fp32', False, 0), ('k32', 'fp16x2', 10), ('k32_64', 'fp16x2', 11)):
+        y = _run_conv(cuda, xd, wp, Cout, 2 * H, 2 * H, 9, 1, 2, b.to(cuda), pro=pro, split=split, tile=tile)
+        errs[name] = (y.cpu().double() - _nhwc(ref)).abs().max().item()
+    scale = ref.abs().max().item()
+    for k in ('k32', 'k32_64'):
         assert errs[k] < 2.0 * errs['fp32'] + 1e-7 * scale, errs
         assert errs[k] < 4e-6 * scale, (errs, scale)
