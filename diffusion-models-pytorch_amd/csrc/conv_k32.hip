@@ -25,8 +25,8 @@
 //
 // Tiles: 128 x BN blocks (BN 128 or 64) of 4 waves, 64 x WN wave tiles, whole image rows of 32-, 16- or
 // 8-pixel-wide maps (8^2 maps: two images per tile; each lane addresses its own patch row, so a 16-pixel
-// fragment may span image rows). LDS: 2 x 208 x 160 B patch buffers + 4.5 KiB of GroupNorm tables
-// = 71 KiB -> two blocks per CU.
+// fragment may span image rows). LDS: 2 x 208 x 160 B patch buffers + 9 KiB of GroupNorm tables
+// = 74 KiB -> two blocks per CU.
 #include <cstdlib>
 #include <string>
 
@@ -44,7 +44,7 @@ constexpr int BM_K32 = 128;   // block rows (output pixels)
 constexpr int kC = 32;          // input channels per chunk = K of one tap's MFMA step
 constexpr int kRowH = 80;       // LDS row pitch in fp16: 160 B; [piece][k-group][8] (piece at +32)
 constexpr int kMaxP = 208;      // patch pixels: 32^2 maps 6 x 34, 16^2 maps 10 x 18, 8^2 maps 2 x 10 x 10
-constexpr int kTab = 1024;      // GroupNorm table floats (per image of the tile: Cin1 scales, then the shifts)
+constexpr int kTab = 2048;      // GroupNorm table floats (per image of the tile: its channels' scales, then the shifts)
 constexpr int kStats = 128;     // (image, group) pairs of the in-kernel finalize
 
 

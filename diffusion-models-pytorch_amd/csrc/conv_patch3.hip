@@ -52,6 +52,23 @@ namespace dm {
 
 namespace {
 
+#ifdef DM_K32_STAMPS
+// Diagnostic build only (tools/k32_stamps.py --kernel pw): per block of the split 1x1 conv (MODE 3), wave
+// 0's s_memtime at the start, before the main loop, after it, after the epilogue; realtime start / end.
+__device__ unsigned long long g_pw_stamps[65536][8];
+#define PW_STAMP(k)                                                                                   \
+  do {                                                                                                \
+    if (PW1 && threadIdx.x == 0 && blockIdx.x < 65536) g_pw_stamps[blockIdx.x][k] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#define PW_RSTAMP(k)                                                                                  \
+  do {                                                                                                \
+    if (PW1 && threadIdx.x == 0 && blockIdx.x < 65536) g_pw_stamps[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define PW_STAMP(k) do {} while (0)
+#define PW_RSTAMP(k) do {} while (0)
+#endif
+
 constexpr int kSK = 16;  // K per slice = channels per patch chunk
 constexpr int kPwSlices = 2;        // MODE 3: 16-channel slices per chunk (32 channels; 4 measured no faster)
 constexpr int kPwTabFloats = 10240;  // GroupNorm table capacity (40 KiB) of the LDS-staged prologue tables
@@ -178,6 +195,8 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
   __shared__ __attribute__((aligned(16))) float gtab[GTAB];
   __shared__ float gstat[LTAB ? 2 * kGinStats : 1];  // in-kernel finalize: (mean, rstd) per (image, group)
 
+  PW_RSTAMP(5);
+  PW_STAMP(0);
   const int Ho = SUB ? a.Hin : a.Hout, Wo = SUB ? a.Win : a.Wout;
   const int M = a.B * Ho * Wo;
   const int N = a.Cout;
@@ -473,6 +492,7 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
   if (PRO) transform(c_begin, 0, PJ);
   store_patch(c_begin & 1);
   __syncthreads();
+  PW_STAMP(1);
   // The patch is double buffered and read by every tap of its chunk: one barrier per chunk. The patch
   // of chunk c + 1 is loaded at tap 0, GroupNorm+SiLU'd over taps T0 .. NTAP-1, split and stored at
   // the last tap into the other buffer (free: every wave passed the previous chunk's barrier).
@@ -510,6 +530,7 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
   }
   }
 
+  PW_STAMP(2);
   // ---- segment 2: 1x1 product of x2 (ResBlock shortcut), K = Cin2, un-pipelined (last split).
   if (a.Cin2 > 0 && (!KSPLIT || split == ksplit - 1)) {
     const int s2base = NTAP * a.Cin1 / kSK;
@@ -552,6 +573,8 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
       attn_plane_epilogue<WM, WN>(a, acc, M, m0 + wm * WM, n0 + wn * WN, lr, lh,
                                   wave < 2 ? reinterpret_cast<float*>(patch) + wave * WM * (WN + 8)
                                            : gtab + (wave - 2) * WM * (WN + 8));
+      PW_STAMP(3);
+      PW_RSTAMP(6);
       return;
     }
   }
@@ -705,6 +728,13 @@ __global__ void split_conv_weights_kernel(const float* w, int nmat, int rows, in
 }
 
 }  // namespace
+
+#ifdef DM_K32_STAMPS
+extern "C" int dm_debug_pw_stamps(void* host, int nblocks) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pw_stamps), (size_t)nblocks * 8 * sizeof(unsigned long long)) ==
+                 hipSuccess ? 0 : -2;
+}
+#endif
 
 bool conv_patch3_ok(const ConvArgs& a, int which, const PatchGeom& g) {
   if (!a.ws || a.Cin1 % kSK != 0 || a.Cin2 % kSK != 0 || a.K % kSK != 0) return false;

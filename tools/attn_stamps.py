@@ -45,6 +45,19 @@ def main():
         v = s[:, j] - s[:, i]
         print(f'  {n:18s} cycles mean {v.mean():9.0f} p10 {np.percentile(v, 10):9.0f} p90 {np.percentile(v, 90):9.0f}'
               f'  share {v.mean() / tot.mean():.3f}')
+    # the qkv 1x1 conv (conv_patch3 MODE 3, attention-plane epilogue) of the same forward
+    nq = (B * 256 // 128) * (768 // 128)
+    buf = np.zeros((nq, 8), dtype=np.uint64)
+    L.dm_debug_pw_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    assert L.dm_debug_pw_stamps(buf.ctypes.data, nq) == 0
+    s = buf.astype(np.int64)
+    tot = s[:, 3] - s[:, 0]
+    print(f'qkv conv_patch3 MODE 3: {nq} blocks, wall (stamps) {(s[:, 6].max() - s[:, 5].min()) / 100.0:.1f} us, '
+          f'block cycles mean {tot.mean():.0f}')
+    for n, (i, j) in zip(['prologue', 'main loop', 'plane epilogue'], [(0, 1), (1, 2), (2, 3)]):
+        v = s[:, j] - s[:, i]
+        print(f'  {n:18s} cycles mean {v.mean():9.0f} p10 {np.percentile(v, 10):9.0f} p90 {np.percentile(v, 90):9.0f}'
+              f'  share {v.mean() / tot.mean():.3f}')
 
 
 if __name__ == '__main__':
