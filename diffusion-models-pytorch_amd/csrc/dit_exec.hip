@@ -66,6 +66,10 @@ struct DiTModel {
   int* range_flag_host = nullptr;
   bool range_deferred = false;  // dm_dit_set_range_deferred / dm_dit_range_poll, as for the UNet
   std::map<const float*, int> w_exp;
+  // fp16x2 fragment images of the token-GEMM weights (split_conv_weights, taps 1), built once: those GEMMs
+  // run linear_k32 (K = 32 MFMA steps, no per-load split of the weights); DM_DIT_LINEAR_K32=0 keeps gemm.hip
+  std::map<const float*, void*> split_w;
+  bool linear_k32_on = !(std::getenv("DM_DIT_LINEAR_K32") && std::string(std::getenv("DM_DIT_LINEAR_K32")) == "0");
 
   struct Plan : PlanBase {
     int B = 0;
@@ -80,6 +84,7 @@ struct DiTModel {
   float* P(size_t off) const { return arena + off; }
   ~DiTModel() {
     plan.reset();
+    for (auto& kv : split_w) (void)hipFree(kv.second);
     if (range_flag) (void)hipFree(range_flag);
     if (range_flag_host) (void)hipHostFree(range_flag_host);
     if (arena) (void)hipFree(arena);
@@ -227,6 +232,27 @@ int DiTModel::build_plan(int B) {
       eb = it->second;
     }
     g.split = 2; g.split_ea = ea; g.split_eb = eb; g.range_flag = range_flag;
+    // static weight [N][K]: pre-split once for linear_k32 (the gemm.hip path stays the fallback)
+    if (wn && linear_k32_on && g.K % 64 == 0 && g.N % 4 == 0) {
+      const float* wp = P(w);
+      auto it = split_w.find(wp);
+      if (it == split_w.end()) {
+        void* buf = nullptr;
+        const size_t nb = split_conv_weights_bytes(1, g.N, g.K, 2);
+        if (hipMalloc(&buf, nb) != hipSuccess) return;
+        if (split_conv_weights(wp, 1, g.N, g.K, g.K, 1, 2, buf, nullptr) != DM_OK || hipDeviceSynchronize() != hipSuccess) {
+          (void)hipFree(buf);
+          return;
+        }
+        it = split_w.emplace(wp, buf).first;
+      }
+      g.ws = it->second;
+      g.ws_rowscale = split_conv_rowscale(it->second, 1, g.N, g.K);
+      if (!linear_k32_ok(g)) {
+        g.ws = nullptr;
+        g.ws_rowscale = nullptr;
+      }
+    }
   };
   auto linear = [&](const float* A, int lda, long rows, size_t w, size_t bias, int N, int K, float* out, int ldc) {
     GemmArgs g{};

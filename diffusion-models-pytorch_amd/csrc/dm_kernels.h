@@ -152,6 +152,10 @@ struct GemmArgs {
   // accumulator is scaled back by 2^-(ea + eb). |scaled value| > 65504 sets range_flag.
   int split;
   int split_ea, split_eb;
+  // optional pre-split weights (split = 2, [n][k] B, Z = 1): split_conv_weights' fragment images of Bm with
+  // their inverse row scales; such GEMMs run linear_k32 (linear_k32.hip) and split_eb is unused
+  const void* ws;
+  const float* ws_rowscale;
   int* range_flag;
 };
 
@@ -233,6 +237,9 @@ int conv_k32_pick(const ConvArgs& a);
 bool conv_k32_enabled();  // DM_CONV_K32 != 0
 int conv2d_k32(const ConvArgs& a, int v, hipStream_t st);
 std::string conv_k32_label(const ConvArgs& a, int v);
+// static-weight GEMM on pre-split weights with K = 32 MFMA steps (linear_k32.hip)
+bool linear_k32_ok(const GemmArgs& g);
+int linear_k32(const GemmArgs& g, hipStream_t st);
 int conv_splitk_reduce(const ConvArgs& a, hipStream_t st);
 // fp32 packed conv weights [nmat][rows][K] -> split slices for conv_patch3_kernel (np 3: bf16x3,
 // np 2: fp16x2 + row scales); split_conv_rowscale gives ConvArgs::ws_rowscale of an fp16x2 copy

@@ -371,6 +371,7 @@ int launch_gemm(const GemmArgs& g, hipStream_t st) {
 
 int gemm_batched(const GemmArgs& g, hipStream_t st) {
   DM_REQUIRE(g.M > 0 && g.N > 0 && g.K > 0, "gemm: empty problem");
+  if (g.ws) return linear_k32(g, st);  // pre-split static weights (linear_k32.hip)
   DM_REQUIRE(g.K % 4 == 0 && g.lda % 4 == 0 && g.ldb % 4 == 0, "gemm: K and leading dims must be multiples of 4");
   DM_REQUIRE(!g.b_kn || g.N % 4 == 0, "gemm: N must be a multiple of 4 for the [k][n] B layout");
   DM_REQUIRE((reinterpret_cast<uintptr_t>(g.A) & 15) == 0 && (reinterpret_cast<uintptr_t>(g.Bm) & 15) == 0,
@@ -398,6 +399,7 @@ int gemm_pick(const GemmArgs& g) {
 }
 
 std::string gemm_label(const GemmArgs& g) {
+  if (g.ws) return std::string("linear_k32_kernel<") + (g.pro_scale ? "1>" : g.ln_stats ? "2>" : "0>");
   std::string s = gemm_pick(g) == 0 ? "gemm_kernel<128,128,64,64" : "gemm_kernel<64,64,32,32";
   return s + (g.b_kn ? ",true" : ",false") + (g.split == 2 ? ",true>" : ",false>");
 }

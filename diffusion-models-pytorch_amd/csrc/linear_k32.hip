@@ -1,0 +1,266 @@
+// Static-weight GEMM C = prologue(A) W^T (+ bias, residual / gated residual, activation) on the fp16x2
+// split matrix cores with K = 32 steps on v_mfma_f32_16x16x32_f16 -- the token GEMMs of DiT (qkv, proj,
+// fc1, fc2, final layer: models/dit/model.py:118-142) and other static-weight linears. The weights are
+// split ONCE at plan build (split_conv_weights, taps 1: conv_patch3's fragment images with per-row
+// power-of-two scales) instead of on every load as gemm.hip's SPLIT path does (16-18 VALU per MFMA there).
+//
+// Numerics as everywhere on the fp16x2 path: an fp32 operand x = h0 + h1 (h0 = fp16(x), h1 = fp16(x - h0)),
+// a*w = a1w0 + a0w1 + a0w0 into one fp32 accumulator; activations scaled by 2^split_ea before the split,
+// weights by their row scale, both undone exactly in the epilogue. |scaled activation| > 65504 raises
+// range_flag (the caller re-runs in fp32 / bf16x3).
+//
+// Block 128 x 128, four waves of 64 x 64 (4 x 4 tiles of 16 x 16). K is staged 64 channels at a time
+// (two K = 32 steps per barrier), double-buffered in LDS as rows of [step][piece][4 k-groups][8] fp16 with
+// a 288-B pitch (18 x 16-B slots: the 16-row fragment reads are conflict free, searched offline); the
+// prologue (GroupNorm affine, or LayerNorm + adaLN modulate with per-row statistics) is applied on the
+// way into LDS with its per-(image, channel) tables staged per K stage. B fragments from L2 into a 2-deep
+// register ring. Epilogue staged through LDS so every lane stores 16 B.
+#include "dm_common.h"
+#include "dm_kernels.h"
+#include "mfma_tile.h"
+#include "split16.h"
+
+namespace dm {
+
+namespace {
+
+constexpr int kLP = 144;   // LDS row pitch in fp16 (288 B) of one 64-channel stage
+constexpr int kLBM = 128;  // block rows
+
+template <int PRO>  // 0 none, 1 GroupNorm affine (pro_scale / pro_shift [img][K]), 2 LayerNorm + modulate
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) linear_k32_kernel(GemmArgs g) {
+  constexpr int BM = kLBM, BN = 128, WM = 64, WN = 64, TM = 4, TN = 4, WD = 2;
+  constexpr int STAGE = BM * kLP;  // fp16 elements per buffer
+  __shared__ __attribute__((aligned(16))) _Float16 abuf[2 * STAGE];
+  // prologue tables of three K stages (staged two stages ahead): [stage % 3][image of the tile][scale, shift][ch]
+  __shared__ __attribute__((aligned(16))) float tab[3][2][2][64];
+
+  const int M = g.M, N = g.N, K = g.K;
+  const int nN = ceil_div(N, BN);
+  const int bid = xcd_remap_p(blockIdx.x, gridDim.x);
+  const int mt = bid / nN, nt = bid - (bid / nN) * nN;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int l16 = lane & 15, q = lane >> 4;
+  const int lrow = t >> 1, lh = t & 1;  // loader: row, 32-channel half of the stage (= K32 step)
+
+  // ---- A loader: row lrow of the tile, channels 64 st + 32 lh .. + 31
+  const int am = min(m0 + lrow, M - 1);  // rows >= M: clamped, never stored
+  const float* asrc = g.A + (size_t)am * g.lda + 32 * lh;
+  const int rows_img = PRO == 1 ? g.pro_rows : PRO == 2 ? g.ln_rows : 1;
+  const int img0 = PRO ? m0 / rows_img : 0;
+  const int aimg = PRO ? am / rows_img - img0 : 0;  // 0 or 1 (rows per image >= 128)
+  const float2 lns = PRO == 2 ? g.ln_stats[am] : make_float2(0.f, 1.f);
+  const float apow = ldexpf(1.f, g.split_ea);
+  f4 ra[8];
+  f4 rt;  // threads 0 .. 63: one f4 of a stage's tables
+  const int ti = t >> 4, tk = (t & 15) * 4;  // table loader: (image, scale | shift) pair ti, channels tk
+  auto load_a = [&](int st) {
+    const float* p = asrc + 64 * st;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) ra[u] = *reinterpret_cast<const f4*>(p + 4 * u);
+  };
+  auto load_tab = [&](int st) {
+    if (PRO && t < 64) {
+      const int im = min(img0 + (ti >> 1), (M - 1) / rows_img);
+      const int kk = 64 * st + tk;
+      if (PRO == 1)
+        rt = *reinterpret_cast<const f4*>(((ti & 1) ? g.pro_shift : g.pro_scale) + (size_t)im * K + kk);
+      else
+        rt = *reinterpret_cast<const f4*>(((ti & 1) ? g.ln_shift : g.ln_scale) + (size_t)im * g.ln_pitch + kk);
+    }
+  };
+  auto store_tab = [&](int buf) {
+    if (PRO && t < 64) *reinterpret_cast<f4*>(&tab[buf][ti >> 1][ti & 1][tk]) = rt;
+  };
+  bool bad = false;
+  // prologue + split + LDS store of this thread's 32 channels (tables of the stage in tab[buf])
+  auto finish_a = [&](int buf, int tb) {
+    _Float16* dst = abuf + buf * STAGE + lrow * kLP + lh * 64;
+#pragma unroll
+    for (int u = 0; u < 8; u += 2) {  // k-group u / 2: channels 8 (u / 2) .. + 7 of the step
+      f4 v0 = ra[u], v1 = ra[u + 1];
+      if (PRO) {
+        const float* sc = &tab[tb][aimg][0][32 * lh + 4 * u];
+        const float* sh = &tab[tb][aimg][1][32 * lh + 4 * u];
+        const f4 s0 = *reinterpret_cast<const f4*>(sc), s1 = *reinterpret_cast<const f4*>(sc + 4);
+        const f4 h0 = *reinterpret_cast<const f4*>(sh), h1 = *reinterpret_cast<const f4*>(sh + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (PRO == 1) {  // GroupNorm affine, as gemm.hip's prologue
+            v0[e] = v0[e] * s0[e] + h0[e];
+            v1[e] = v1[e] * s1[e] + h1[e];
+          } else {  // LayerNorm (no affine) + modulate, as gemm.hip's prologue
+            v0[e] = ((v0[e] - lns.x) * lns.y) * (1.0f + s0[e]) + h0[e];
+            v1[e] = ((v1[e] - lns.x) * lns.y) * (1.0f + s1[e]) + h1[e];
+          }
+        }
+      }
+      if (g.alpha != 1.0f) {
+        v0 = v0 * g.alpha;
+        v1 = v1 * g.alpha;
+      }
+      f16x8 pc[2];
+      Split<2>::split(v0 * apow, v1 * apow, pc, bad);
+      *reinterpret_cast<f16x8*>(dst + (u >> 1) * 8) = pc[0];       // piece 0 at slot 8 s + q
+      *reinterpret_cast<f16x8*>(dst + 32 + (u >> 1) * 8) = pc[1];  // piece 1 at slot 8 s + 4 + q
+    }
+  };
+
+  // ---- B: fragment images [16-slice][32-col group][piece][lane group][32][8]; K32 step kk reads
+  // 16-slices 2 kk + (q >> 1), lane group q & 1
+  const int ngrp = ceil_div(N, 32);
+  const size_t sl = (size_t)ngrp * 1024;
+  const _Float16* wbase[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + wn * WN + j * 16 + l16;
+    const int grp = min(col >> 5, ngrp - 1);
+    wbase[j] = reinterpret_cast<const _Float16*>(g.ws) + (size_t)(q >> 1) * sl + (size_t)grp * 1024 +
+               ((q & 1) * 32 + (col & 31)) * 8;
+  }
+  f16x8 bq[WD][TN][2];
+  auto load_b = [&](f16x8 (&dst)[TN][2], int kk) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) dst[j][p] = *reinterpret_cast<const f16x8*>(wbase[j] + (size_t)(2 * kk) * sl + p * 512);
+  };
+
+  f4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](int buf, int s, const f16x8 (&bv)[TN][2]) {
+    const _Float16* As = abuf + buf * STAGE + (wm * WM + l16) * kLP + s * 64 + q * 8;
+    f16x8 av[TM][2];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) av[i][p] = *reinterpret_cast<const f16x8*>(As + i * 16 * kLP + p * 32);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[i][1], bv[j][0], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[i][0], bv[j][1], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[i][0], bv[j][0], acc[i][j], 0, 0, 0);
+      }
+  };
+
+  const int nst = K / 64, nkk = K / 32;
+#pragma unroll
+  for (int d = 0; d < WD; ++d) load_b(bq[d], min(d, nkk - 1));
+  load_a(0);
+  load_tab(0);
+  store_tab(0);
+  load_tab(min(1, nst - 1));
+  store_tab(1);
+  __syncthreads();
+  finish_a(0, 0);
+  __syncthreads();
+  // One barrier per stage. Stage st: the next stage's A rows and the tables of stage st + 2 are loaded
+  // before step 0; after step 1 the tables go to LDS and the next stage is finished into the other
+  // buffer (its tables were stored a stage earlier, visible since the last barrier).
+  for (int st = 0; st < nst; ++st) {
+    const int nx = min(st + 1, nst - 1);
+    load_a(nx);
+    load_tab(min(st + 2, nst - 1));
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int kk = 2 * st + s;
+      compute(st & 1, s, bq[s]);
+      load_b(bq[s], min(kk + WD, nkk - 1));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    store_tab((st + 2) % 3);
+    finish_a((st + 1) & 1, (st + 1) % 3);
+    __syncthreads();
+  }
+  if (bad && g.range_flag) *g.range_flag = 1;
+
+  // ---- epilogue: per 32-row slab of the wave's 64 rows, acc * rowscale * 2^-ea to LDS ([32][68] fp32),
+  // then 4 consecutive columns per lane: bias, residual / gated residual, activation, 16-B store
+  constexpr int EP = WN + 4, LPR = WN / 4, RPI = 64 / LPR;
+  float* stg = reinterpret_cast<float*>(abuf) + wave * 32 * EP;
+  const float unscale = ldexpf(1.f, -g.split_ea);
+  float cs[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) cs[j] = g.ws_rowscale[min(n0 + wn * WN + j * 16 + l16, N - 1)] * unscale;
+  const int c4 = lane % LPR, rsub = lane / LPR;
+  const int ncol = n0 + wn * WN + 4 * c4;
+  const bool c_ok = ncol < N;  // N % 4 == 0
+  const int nc = c_ok ? ncol : 0;
+  const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  const f4 bias4 = g.bias ? *reinterpret_cast<const f4*>(g.bias + nc) : zero4;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int i = 2 * h; i < 2 * h + 2; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) stg[((i - 2 * h) * 16 + 4 * q + r) * EP + j * 16 + l16] = acc[i][j][r] * cs[j];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's slab is visible to its reads
+    __builtin_amdgcn_wave_barrier();
+    const int row0 = m0 + wm * WM + 32 * h;
+    f4 rs4[32 / RPI], gt4[32 / RPI];
+    if (g.res) {
+#pragma unroll
+      for (int it = 0; it < 32 / RPI; ++it) {
+        const int m = min(row0 + it * RPI + rsub, M - 1);
+        rs4[it] = *reinterpret_cast<const f4*>(g.res + (size_t)(g.res_mod > 0 ? m % g.res_mod : m) * g.ld_res + nc);
+        gt4[it] = g.gate ? *reinterpret_cast<const f4*>(g.gate + (size_t)(m / g.gate_rows) * g.gate_pitch + nc) : zero4;
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < 32 / RPI; ++it) {
+      const int row = it * RPI + rsub;
+      const int m = row0 + row;
+      f4 v = *reinterpret_cast<const f4*>(stg + row * EP + 4 * c4);
+      if (g.bias) v = v + bias4;
+      if (g.res) v = g.gate ? rs4[it] + gt4[it] * v : v + rs4[it];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (g.act == 1) v[e] = silu_f(v[e]);
+        else if (g.act == 2) v[e] = gelu_tanh_f(v[e]);
+      }
+      if (m < M && c_ok) *reinterpret_cast<f4*>(g.C + (size_t)m * g.ldc + ncol) = v;
+    }
+    __builtin_amdgcn_wave_barrier();  // the next slab reuses the region
+  }
+}
+
+}  // namespace
+
+bool linear_k32_ok(const GemmArgs& g) {
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (!(g.ws && g.ws_rowscale && g.split == 2 && g.Z1 == 1 && g.Z2 == 1 && !g.b_kn && g.b_scale == 0.0f)) return false;
+  if (g.K % 64 != 0 || g.N % 4 != 0 || g.lda % 4 != 0 || g.ldc % 4 != 0 || !al16(g.A) || !al16(g.C)) return false;
+  if (g.bias && !al16(g.bias)) return false;
+  if (g.res && (g.ld_res % 4 != 0 || !al16(g.res))) return false;
+  if (g.gate && (g.gate_pitch % 4 != 0 || !al16(g.gate))) return false;
+  if (g.gn_part) return false;
+  if (g.pro_scale && (g.pro_rows < kLBM || !al16(g.pro_scale) || !al16(g.pro_shift))) return false;
+  if (g.ln_stats && (g.ln_rows < kLBM || g.ln_pitch % 4 != 0 || !al16(g.ln_scale) || !al16(g.ln_shift))) return false;
+  if (g.pro_scale && g.ln_stats) return false;
+  return true;
+}
+
+int linear_k32(const GemmArgs& g, hipStream_t st) {
+  DM_REQUIRE(linear_k32_ok(g), "linear_k32: needs pre-split weights, K % 64 == 0, 16-byte aligned 4-column rows");
+  const int blocks = ceil_div(g.M, kLBM) * ceil_div(g.N, 128);
+  if (g.pro_scale)
+    hipLaunchKernelGGL(linear_k32_kernel<1>, dim3(blocks), dim3(256), 0, st, g);
+  else if (g.ln_stats)
+    hipLaunchKernelGGL(linear_k32_kernel<2>, dim3(blocks), dim3(256), 0, st, g);
+  else
+    hipLaunchKernelGGL(linear_k32_kernel<0>, dim3(blocks), dim3(256), 0, st, g);
+  DM_LAUNCH_CHECK();
+  return DM_OK;
+}
+
+}  // namespace dm
