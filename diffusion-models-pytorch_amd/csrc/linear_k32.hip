@@ -26,22 +26,34 @@ namespace {
 
 constexpr int kLP = 144;   // LDS row pitch in fp16 (288 B) of one 64-channel stage
 constexpr int kLBM = 128;  // block rows
+constexpr int kLGM = 4;    // M tiles per group of the tile order
 
-template <int PRO>  // 0 none, 1 GroupNorm affine (pro_scale / pro_shift [img][K]), 2 LayerNorm + modulate
+// PRO: 0 none, 1 GroupNorm affine (pro_scale / pro_shift [img][K]), 2 LayerNorm + modulate.
+// Wave tiles WM x WN: 128 x 32 (each wave all 128 rows from LDS, its own 32 weight columns: every B
+// fragment fetched once per block, half the L2 traffic of 64 x 64 wave tiles, where each weight fragment is
+// loaded by both row waves) or 64 x 64.
+template <int PRO, int WM = 128, int WN = 32>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) linear_k32_kernel(GemmArgs g) {
-  constexpr int BM = kLBM, BN = 128, WM = 64, WN = 64, TM = 4, TN = 4, WD = 2;
+  constexpr int BM = kLBM, BN = 128, TM = WM / 16, TN = WN / 16, WD = 2, NWN = BN / WN;
+  static_assert((BM / WM) * NWN == 4, "4 waves");
   constexpr int STAGE = BM * kLP;  // fp16 elements per buffer
   __shared__ __attribute__((aligned(16))) _Float16 abuf[2 * STAGE];
   // prologue tables of three K stages (staged two stages ahead): [stage % 3][image of the tile][scale, shift][ch]
   __shared__ __attribute__((aligned(16))) float tab[3][2][2][64];
 
   const int M = g.M, N = g.N, K = g.K;
-  const int nN = ceil_div(N, BN);
+  // Grouped tile order: consecutive tiles (one XCD, xcd_remap_p) sweep all N tiles for a group of kLGM M
+  // tiles, M fastest, so the group's kLGM blocks of one weight tile run together and fetch it from the
+  // memory side once per group instead of once per M tile (DiT-XL/2 qkv: 16 MB of split weights re-read
+  // for each of 128 M tiles otherwise); the group's A tiles stay in the XCD's L2 during the sweep.
+  const int nN = ceil_div(N, BN), nM = ceil_div(M, BM);
   const int bid = xcd_remap_p(blockIdx.x, gridDim.x);
-  const int mt = bid / nN, nt = bid - (bid / nN) * nN;
+  const int tgrp = bid / (kLGM * nN), gm0 = tgrp * kLGM, gsz = min(kLGM, nM - gm0);
+  const int r = bid - tgrp * (kLGM * nN);
+  const int nt = r / gsz, mt = gm0 + (r - nt * gsz);
   const int m0 = mt * BM, n0 = nt * BN;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / NWN, wn = wave % NWN;
   const int l16 = lane & 15, q = lane >> 4;
   const int lrow = t >> 1, lh = t & 1;  // loader: row, 32-channel half of the stage (= K32 step)
 
@@ -197,7 +209,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
   const f4 bias4 = g.bias ? *reinterpret_cast<const f4*>(g.bias + nc) : zero4;
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < WM / 32; ++h) {
 #pragma unroll
     for (int i = 2 * h; i < 2 * h + 2; ++i)
 #pragma unroll
