@@ -164,7 +164,7 @@ def roofline(prof, workload='c3'):
         np_ = int(dom_name.rstrip('>').split(',')[-1]) if split else 0
         if dom_name.startswith('gemm_kernel') and dom_name.endswith(',true>'):   # <..., B_KN, SPLIT>: fp16x2
             split, np_ = True, 2
-        if dom_name.startswith('conv_k32_kernel'):  # fp16x2 only (v_mfma_f32_16x16x32_f16)
+        if dom_name.startswith('conv_k32_kernel') or dom_name.startswith('linear_k32_kernel'):  # fp16x2 only
             split, np_ = True, 2
         prods = SPLIT_PRODUCTS.get(np_, 0)
         peak = round(BF16_PEAK_TFLOPS / prods, 1) if split else FP32_PEAK_TFLOPS
