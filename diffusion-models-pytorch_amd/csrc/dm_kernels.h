@@ -156,6 +156,12 @@ struct GemmArgs {
   // their inverse row scales; such GEMMs run linear_k32 (linear_k32.hip) and split_eb is unused
   const void* ws;
   const float* ws_rowscale;
+  // linear_k32 only: the attention operand planes instead of C (as ConvArgs::ap_*, the qkv projection
+  // feeding attn_presplit_kernel)
+  _Float16 *ap_q, *ap_k, *ap_v;
+  int ap_L, ap_heads, ap_Dh, ap_legacy;
+  float ap_alpha, ap_bscale;
+  int ap_ea, ap_eb, ap_ev;
   int* range_flag;
 };
 

@@ -32,6 +32,76 @@ constexpr int kLGM = 4;    // M tiles per group of the tile order
 // Wave tiles WM x WN: 128 x 32 (each wave all 128 rows from LDS, its own 32 weight columns: every B
 // fragment fetched once per block, half the L2 traffic of 64 x 64 wave tiles, where each weight fragment is
 // loaded by both row waves) or 64 x 64.
+// One 32 x WN slab (acc * rowscale * 2^-ea, no bias yet) of the qkv projection -> the attention operand
+// planes: q * alpha * 2^ea and k * b_scale * 2^eb as [B][heads][2][L][Dh], v * 2^ev transposed as
+// [B][heads][2][Dh][L] (plane 0 = fp16(x), plane 1 = fp16(x - plane 0)), 16-B stores. The slab's columns
+// lie in one of q / k / v and in one head (3C, C and Dh are multiples of 32).
+template <int WN>
+__device__ __forceinline__ void plane_slab(const GemmArgs& g, const float* st, int EP, int row0, int col0, int lane,
+                                           f4 bias4, bool& bad) {
+  if (col0 >= g.N) return;
+  const int Dh = g.ap_Dh, C = g.ap_heads * Dh;
+  int part, h, d0;
+  if (g.ap_legacy) {
+    h = col0 / (3 * Dh);
+    part = (col0 - h * 3 * Dh) / Dh;
+    d0 = col0 - h * 3 * Dh - part * Dh;
+  } else {
+    part = col0 / C;
+    h = (col0 - part * C) / Dh;
+    d0 = col0 - part * C - h * Dh;
+  }
+  const float scale = part == 0 ? g.ap_alpha : part == 1 ? g.ap_bscale : 1.f;
+  const bool use_scale = part == 0 ? g.ap_alpha != 1.0f : part == 1 && g.ap_bscale != 0.0f && g.ap_bscale != 1.0f;
+  const float pw = ldexpf(1.f, part == 0 ? g.ap_ea : part == 1 ? g.ap_eb : g.ap_ev);
+  const size_t plane = (size_t)g.ap_L * Dh;
+  auto split8 = [&](const float (&x)[8], f16x8& hi, f16x8& lo) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float y = (use_scale ? x[e] * scale : x[e]) * pw;
+      const _Float16 h0 = (_Float16)y;
+      hi[e] = h0;
+      lo[e] = (_Float16)(y - (float)h0);
+      bad |= fabsf(y) > 65504.f;
+    }
+  };
+  const float* bias = g.bias ? g.bias + col0 : nullptr;
+  if (part < 2) {  // q / k: 8 consecutive d of one token per item
+    _Float16* dst = part == 0 ? g.ap_q : g.ap_k;
+    constexpr int G8 = WN / 8;
+    for (int it = lane; it < 32 * G8; it += 64) {
+      const int row = it / G8, c8 = it - row * G8;
+      const int m = row0 + row;
+      if (m >= g.M) continue;
+      float x[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = st[row * EP + 8 * c8 + e] + (bias ? bias[8 * c8 + e] : 0.f);
+      f16x8 hi, lo;
+      split8(x, hi, lo);
+      const int b = m / g.ap_L, tok = m - b * g.ap_L;
+      _Float16* p = dst + ((size_t)b * g.ap_heads + h) * 2 * plane + (size_t)tok * Dh + d0 + 8 * c8;
+      *reinterpret_cast<f16x8*>(p) = hi;
+      *reinterpret_cast<f16x8*>(p + plane) = lo;
+    }
+  } else {  // v: 8 consecutive tokens of one d per item
+    for (int it = lane; it < WN * 4; it += 64) {
+      const int col = it % WN, r8 = it / WN;
+      const int m = row0 + 8 * r8;  // tokens m .. m + 7 lie in one image (L % 8 == 0)
+      if (m >= g.M) continue;
+      float x[8];
+      const float bc = bias ? bias[col] : 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = st[(8 * r8 + e) * EP + col] + bc;
+      f16x8 hi, lo;
+      split8(x, hi, lo);
+      const int b = m / g.ap_L, tok = m - b * g.ap_L;
+      _Float16* p = g.ap_v + ((size_t)b * g.ap_heads + h) * 2 * plane + (size_t)(d0 + col) * g.ap_L + tok;
+      *reinterpret_cast<f16x8*>(p) = hi;
+      *reinterpret_cast<f16x8*>(p + plane) = lo;
+    }
+  }
+}
+
 template <int PRO, int WM = 128, int WN = 32>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) linear_k32_kernel(GemmArgs g) {
   constexpr int BM = kLBM, BN = 128, TM = WM / 16, TN = WN / 16, WD = 2, NWN = BN / WN;
@@ -192,8 +262,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     finish_a((st + 1) & 1, (st + 1) % 3);
     __syncthreads();
   }
-  if (bad && g.range_flag) *g.range_flag = 1;
-
   // ---- epilogue: per 32-row slab of the wave's 64 rows, acc * rowscale * 2^-ea to LDS ([32][68] fp32),
   // then 4 consecutive columns per lane: bias, residual / gated residual, activation, 16-B store
   constexpr int EP = WN + 4, LPR = WN / 4, RPI = 64 / LPR;
@@ -219,6 +287,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's slab is visible to its reads
     __builtin_amdgcn_wave_barrier();
     const int row0 = m0 + wm * WM + 32 * h;
+    if (g.ap_q) {  // attention operand planes (conv_patch3.hip attn_plane_epilogue's expressions)
+      plane_slab<WN>(g, stg, EP, row0, n0 + wn * WN, lane, bias4, bad);
+      __builtin_amdgcn_wave_barrier();
+      continue;
+    }
     f4 rs4[32 / RPI], gt4[32 / RPI];
     if (g.res) {
 #pragma unroll
@@ -244,6 +317,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     }
     __builtin_amdgcn_wave_barrier();  // the next slab reuses the region
   }
+  if (bad && g.range_flag) *g.range_flag = 1;
 }
 
 }  // namespace

@@ -960,7 +960,29 @@ int UNetModel::build_plan(int B, int H, int W) {
         cq.ap_alpha = p.sa; cq.ap_bscale = p.sb;
         cq.ap_ea = 6; cq.ap_eb = 6; cq.ap_ev = 6;
       }
-      if (conv_pw_ok(cq)) {
+      // the qkv projection on linear_k32 (pre-split weights = the MODE 3 conv's split copy, K = 32 MFMA steps,
+      // GroupNorm tables from gn_finalize): the plane or fp32 epilogue of the same values in every attention mode
+      GemmArgs gl{};
+      gl.M = B * hw; gl.N = 3 * C; gl.K = C; gl.Z1 = 1; gl.Z2 = 1;
+      gl.A = xin.p; gl.lda = xin.pitch; gl.Bm = P(p.wqkv); gl.ldb = C; gl.C = qkv; gl.ldc = 3 * C;
+      gl.alpha = 1.f; gl.bias = P(p.bqkv);
+      gl.pro_scale = gsc; gl.pro_shift = gsh; gl.pro_rows = hw;
+      gl.split = 2; gl.split_ea = 0; gl.range_flag = range_flag;
+      gl.ws = cq.ws; gl.ws_rowscale = cq.ws_rowscale;
+      if (presplit) {
+        gl.ap_q = cq.ap_q; gl.ap_k = cq.ap_k; gl.ap_v = cq.ap_v;
+        gl.ap_L = cq.ap_L; gl.ap_heads = cq.ap_heads; gl.ap_Dh = cq.ap_Dh; gl.ap_legacy = cq.ap_legacy;
+        gl.ap_alpha = cq.ap_alpha; gl.ap_bscale = cq.ap_bscale;
+        gl.ap_ea = cq.ap_ea; gl.ap_eb = cq.ap_eb; gl.ap_ev = cq.ap_ev;
+      }
+      const bool qkv_linear = conv_math == 2 && cq.ws && cq.ws_np == 2 && linear_k32_ok(gl) &&
+                              !std::getenv("DM_QKV_NO_LINEAR");
+      if (qkv_linear) {
+        add("gn_finalize", 0, 8.0 * B * C, [=](hipStream_t st) {
+          return gn_finalize(xin, G, sta, 1e-5f, self->P(p.gn.g), self->P(p.gn.b), gsc, gsh, st);
+        });
+        add_gemm(gl);
+      } else if (conv_pw_ok(cq)) {
         gn_prologue(cq, xin, sta, p.gn.g, p.gn.b, nullptr, nullptr, 0);
         add_conv(cq);
       } else {
