@@ -30,7 +30,9 @@ namespace {
 constexpr int kAL = 256;             // tokens
 constexpr int kAK = 32;              // k per staged tile
 constexpr int kAP = 72;              // fp16 pitch of a staged 32-k row (two 16-deep slices + pad: 144 B)
-constexpr int kSP = 8 * kAP / 2;     // fp32 pitch of an S row = one P row of 8 key blocks (1152 B)
+constexpr int kSP = 8 * kAP / 2 + 4;  // fp32 pitch of an S row = one P row of 8 key blocks + 16 B (1168 B = 73
+                                      // 16-B slots, odd: a 32-row P / O fragment read is conflict free; 1152 B
+                                      // put every other row on the same slot, 8-way conflicts)
 
 
 #ifdef DM_K32_STAMPS
@@ -394,10 +396,11 @@ __device__ __forceinline__ void attn_proj(const ConvArgs& c, f16v (&oacc)[2][2],
   if (c.gn_part) epi.emit(m0);
 }
 
-// Pre-split operands (AttnArgs::pq / pk / pv, written by the qkv conv's epilogue, conv_epilogue.h): every
-// MFMA operand fragment is one 16-B load from global (L2) per lane and piece, no LDS staging and no split
-// on the VALU. 64 query rows per block (74 KB of LDS for the S / P rows: two blocks per CU); q, k and
-// v^T slices ride a register ring RD slices ahead of their use. Same MFMA sequence as the unfused GEMMs.
+// Pre-split operands (AttnArgs::pq / pk / pv, written by the qkv projection's epilogue): no split on the
+// VALU. q ([piece][token][d]) is staged once in LDS; k and v^T are fragment images (frag_off, mfma_tile.h),
+// so every k / v operand fragment is one contiguous 1-KiB load per wave and piece from L2, riding a
+// register ring RD slices ahead of its use. 64 query rows per block (75 KB of LDS for the S / P rows: two
+// blocks per CU). Same MFMA sequence as the unfused GEMMs.
 template <int DH>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) attn_presplit_kernel(AttnArgs a) {
   static_assert(DH == 64 || DH == 256, "head dims 64 / 256");
@@ -429,8 +432,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int q = 0; q < 2; ++q)
-        rb[slot][i][q] =
-            *reinterpret_cast<const f16x8*>(K + q * plane + (size_t)(wave * 64 + i * 32 + lr) * DH + 16 * s + 8 * lh);
+        rb[slot][i][q] = *reinterpret_cast<const f16x8*>(K + frag_off(wave * 64 + i * 32, 16 * s, kAL) + q * 512 + lane * 8);
   };
 #pragma unroll
   for (int s = 0; s < RD; ++s) load_k(min(s, NS - 1), s);
@@ -552,8 +554,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int q = 0; q < 2; ++q)
-        rv[slot][j][q] =
-            *reinterpret_cast<const f16x8*>(V + q * plane + (size_t)(ocol0 + j * 32 + lr) * kAL + 16 * s + 8 * lh);
+        rv[slot][j][q] = *reinterpret_cast<const f16x8*>(V + frag_off(ocol0 + j * 32, 16 * s, DH) + q * 512 + lane * 8);
   };
   f16v oacc[TM][TN];
 #pragma unroll
