@@ -397,10 +397,11 @@ __device__ __forceinline__ void attn_proj(const ConvArgs& c, f16v (&oacc)[2][2],
 }
 
 // Pre-split operands (AttnArgs::pq / pk / pv, written by the qkv projection's epilogue): no split on the
-// VALU. q ([piece][token][d]) is staged once in LDS; k and v^T are fragment images (frag_off, mfma_tile.h),
-// so every k / v operand fragment is one contiguous 1-KiB load per wave and piece from L2, riding a
-// register ring RD slices ahead of its use. 64 query rows per block (75 KB of LDS for the S / P rows: two
-// blocks per CU). Same MFMA sequence as the unfused GEMMs.
+// VALU. q is staged once in LDS; k and v^T fragments are 16-B loads per lane from L2 riding a register
+// ring RD slices ahead of their use. (k / v^T as contiguous 1-KiB fragment images cut the block from
+// 125.6 to 110.3 us but measured 1.6 % slower end to end -- every other kernel of the forward then ran at
+// a lower clock -- so the [token][d] / [d][token] planes stay.) 64 query rows per block (75 KB of LDS for
+// the S / P rows: two blocks per CU). Same MFMA sequence as the unfused GEMMs.
 template <int DH>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) attn_presplit_kernel(AttnArgs a) {
   static_assert(DH == 64 || DH == 256, "head dims 64 / 256");
@@ -432,7 +433,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int q = 0; q < 2; ++q)
-        rb[slot][i][q] = *reinterpret_cast<const f16x8*>(K + frag_off(wave * 64 + i * 32, 16 * s, kAL) + q * 512 + lane * 8);
+        rb[slot][i][q] =
+            *reinterpret_cast<const f16x8*>(K + q * plane + (size_t)(wave * 64 + i * 32 + lr) * DH + 16 * s + 8 * lh);
   };
 #pragma unroll
   for (int s = 0; s < RD; ++s) load_k(min(s, NS - 1), s);
@@ -554,7 +556,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int q = 0; q < 2; ++q)
-        rv[slot][j][q] = *reinterpret_cast<const f16x8*>(V + frag_off(ocol0 + j * 32, 16 * s, DH) + q * 512 + lane * 8);
+        rv[slot][j][q] =
+            *reinterpret_cast<const f16x8*>(V + q * plane + (size_t)(ocol0 + j * 32 + lr) * kAL + 16 * s + 8 * lh);
   };
   f16v oacc[TM][TN];
 #pragma unroll

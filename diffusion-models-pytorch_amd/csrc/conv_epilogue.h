@@ -36,14 +36,14 @@ __device__ __forceinline__ void conv_store_attn_planes(const ConvArgs& a, int m,
   const _Float16 h1 = (_Float16)(x - (float)h0);
   if (fabsf(x) > 65504.f && a.range_flag) *a.range_flag = 1;
   const size_t plane = (size_t)a.ap_L * Dh, base = ((size_t)b * a.ap_heads + h) * 2 * plane;
-  if (part == 0) {  // q: [piece][token][d]
-    _Float16* dst = a.ap_q + base + (size_t)tok * Dh + d;
+  if (part < 2) {
+    _Float16* dst = (part == 0 ? a.ap_q : a.ap_k) + base + (size_t)tok * Dh + d;
     dst[0] = h0;
     dst[plane] = h1;
-  } else {  // k ([token][d]) and v^T ([d][token]) as fragment images (frag_off)
-    _Float16* dst = part == 1 ? a.ap_k + base + frag_off(tok, d, a.ap_L) : a.ap_v + base + frag_off(d, tok, Dh);
+  } else {
+    _Float16* dst = a.ap_v + base + (size_t)d * a.ap_L + tok;
     dst[0] = h0;
-    dst[512] = h1;
+    dst[plane] = h1;
   }
 }
 

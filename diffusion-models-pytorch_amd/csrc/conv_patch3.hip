@@ -139,16 +139,9 @@ __device__ __forceinline__ void attn_plane_epilogue(const ConvArgs& a, f16v (&ac
       f16x8 hi, lo;
       split8(x, hi, lo);
       const int b = m / a.ap_L, tok = m - b * a.ap_L;
-      _Float16* base = dst + ((size_t)b * a.ap_heads + h) * 2 * plane;
-      if (part == 0) {  // q: [piece][token][d]
-        _Float16* p = base + (size_t)tok * Dh + d0 + 8 * c8;
-        *reinterpret_cast<f16x8*>(p) = hi;
-        *reinterpret_cast<f16x8*>(p + plane) = lo;
-      } else {  // k: fragment image (frag_off)
-        _Float16* p = base + frag_off(tok, d0 + 8 * c8, a.ap_L);
-        *reinterpret_cast<f16x8*>(p) = hi;
-        *reinterpret_cast<f16x8*>(p + 512) = lo;
-      }
+      _Float16* p = dst + ((size_t)b * a.ap_heads + h) * 2 * plane + (size_t)tok * Dh + d0 + 8 * c8;
+      *reinterpret_cast<f16x8*>(p) = hi;
+      *reinterpret_cast<f16x8*>(p + plane) = lo;
     }
   } else {  // v planes [b][h][piece][d][token]: 8 consecutive tokens of one d per lane
     for (int g = lane; g < WN * (WM / 8); g += 64) {
@@ -161,9 +154,9 @@ __device__ __forceinline__ void attn_plane_epilogue(const ConvArgs& a, f16v (&ac
       f16x8 hi, lo;
       split8(x, hi, lo);
       const int b = m / a.ap_L, tok = m - b * a.ap_L;
-      _Float16* p = a.ap_v + ((size_t)b * a.ap_heads + h) * 2 * plane + frag_off(d0 + col, tok, Dh);
+      _Float16* p = a.ap_v + ((size_t)b * a.ap_heads + h) * 2 * plane + (size_t)(d0 + col) * a.ap_L + tok;
       *reinterpret_cast<f16x8*>(p) = hi;
-      *reinterpret_cast<f16x8*>(p + 512) = lo;
+      *reinterpret_cast<f16x8*>(p + plane) = lo;
     }
   }
   if (bad && a.range_flag) *a.range_flag = 1;

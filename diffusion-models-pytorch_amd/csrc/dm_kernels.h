@@ -74,10 +74,10 @@ struct ConvArgs {
   // optional device flag, set to 1 when an fp16x2 conv meets an activation beyond the fp16 range
   int* range_flag;
   // attention operand planes (MODE 3 qkv conv feeding attn_fused): instead of y, the epilogue writes
-  // q * alpha * 2^ea as fp16x2 planes [B][heads][2][L][Dh] (plane 0 = fp16(x), plane 1 = fp16(x - plane 0)),
-  // k * b_scale * 2^eb ([L][Dh]) and v^T * 2^ev ([Dh][L]) as fp16x2 fragment images per (image, head)
-  // (frag_off, mfma_tile.h): the split the attention GEMMs would do on load, done once by the producer.
-  // Columns: q | k | v blocks of C, or per head [q; k; v] (ap_legacy, QKVAttentionLegacy).
+  // q * alpha * 2^ea and k * b_scale * 2^eb as fp16x2 planes [B][heads][2][L][Dh] and v * 2^ev
+  // transposed, [B][heads][2][Dh][L] (plane 0 = fp16(x), plane 1 = fp16(x - plane 0)): the split the
+  // attention GEMMs would do on load, done once by the producer. Columns: q | k | v blocks of C, or
+  // per head [q; k; v] (ap_legacy, QKVAttentionLegacy).
   _Float16 *ap_q, *ap_k, *ap_v;
   int ap_L, ap_heads, ap_Dh, ap_legacy;
   float ap_alpha, ap_bscale;

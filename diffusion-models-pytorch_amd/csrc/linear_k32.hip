@@ -33,9 +33,8 @@ constexpr int kLGM = 4;    // M tiles per group of the tile order
 // fragment fetched once per block, half the L2 traffic of 64 x 64 wave tiles, where each weight fragment is
 // loaded by both row waves) or 64 x 64.
 // One 32 x WN slab (acc * rowscale * 2^-ea, no bias yet) of the qkv projection -> the attention operand
-// planes: q * alpha * 2^ea as [B][heads][2][L][Dh] (plane 0 = fp16(x), plane 1 = fp16(x - plane 0)), k *
-// b_scale * 2^eb ([L][Dh]) and v^T * 2^ev ([Dh][L]) as fragment images per (image, head) (frag_off), 16-B
-// stores. The slab's columns
+// planes: q * alpha * 2^ea and k * b_scale * 2^eb as [B][heads][2][L][Dh], v * 2^ev transposed as
+// [B][heads][2][Dh][L] (plane 0 = fp16(x), plane 1 = fp16(x - plane 0)), 16-B stores. The slab's columns
 // lie in one of q / k / v and in one head (3C, C and Dh are multiples of 32).
 template <int WN>
 __device__ __forceinline__ void plane_slab(const GemmArgs& g, const float* st, int EP, int row0, int col0, int lane,
@@ -80,16 +79,9 @@ __device__ __forceinline__ void plane_slab(const GemmArgs& g, const float* st, i
       f16x8 hi, lo;
       split8(x, hi, lo);
       const int b = m / g.ap_L, tok = m - b * g.ap_L;
-      _Float16* base = dst + ((size_t)b * g.ap_heads + h) * 2 * plane;
-      if (part == 0) {  // q: [piece][token][d]
-        _Float16* p = base + (size_t)tok * Dh + d0 + 8 * c8;
-        *reinterpret_cast<f16x8*>(p) = hi;
-        *reinterpret_cast<f16x8*>(p + plane) = lo;
-      } else {  // k: fragment image (frag_off)
-        _Float16* p = base + frag_off(tok, d0 + 8 * c8, g.ap_L);
-        *reinterpret_cast<f16x8*>(p) = hi;
-        *reinterpret_cast<f16x8*>(p + 512) = lo;
-      }
+      _Float16* p = dst + ((size_t)b * g.ap_heads + h) * 2 * plane + (size_t)tok * Dh + d0 + 8 * c8;
+      *reinterpret_cast<f16x8*>(p) = hi;
+      *reinterpret_cast<f16x8*>(p + plane) = lo;
     }
   } else {  // v: 8 consecutive tokens of one d per item
     for (int it = lane; it < WN * 4; it += 64) {
@@ -103,9 +95,9 @@ __device__ __forceinline__ void plane_slab(const GemmArgs& g, const float* st, i
       f16x8 hi, lo;
       split8(x, hi, lo);
       const int b = m / g.ap_L, tok = m - b * g.ap_L;
-      _Float16* p = g.ap_v + ((size_t)b * g.ap_heads + h) * 2 * plane + frag_off(d0 + col, tok, Dh);
+      _Float16* p = g.ap_v + ((size_t)b * g.ap_heads + h) * 2 * plane + (size_t)(d0 + col) * g.ap_L + tok;
       *reinterpret_cast<f16x8*>(p) = hi;
-      *reinterpret_cast<f16x8*>(p + 512) = lo;
+      *reinterpret_cast<f16x8*>(p + plane) = lo;
     }
   }
 }

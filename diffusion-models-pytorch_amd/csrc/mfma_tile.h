@@ -105,16 +105,6 @@ __device__ __forceinline__ void mfma_slice(const float* __restrict__ As, const f
   }
 }
 
-// Fragment-image offset (fp16 elements; hi piece, the lo piece at +512) of element (row, k) of a
-// [rows][depth] fp16x2 MFMA operand block laid out [16-deep k slice][32-row group][piece][lane group
-// (k / 8 % 2)][32 rows][8]: one v_mfma_f32_32x32x16_f16 operand fragment (32 rows x 16 k, one piece) is
-// 1 KiB contiguous, one 16-B load per lane. The attention k and v^T operand planes use it (written by the
-// qkv epilogues, read by attn_presplit_kernel): a [row][k] plane made each fragment load touch 32 cache
-// lines.
-__device__ __forceinline__ size_t frag_off(int row, int k, int nrows) {
-  return (size_t)((k >> 4) * (nrows >> 5) + (row >> 5)) * 1024 + (((k >> 3) & 1) * 32 + (row & 31)) * 8 + (k & 7);
-}
-
 // Row (within the wave's 32x32 tile) of accumulator register r for lane half lh.
 __device__ __forceinline__ int acc_row(int r, int lh) { return (r & 3) + 8 * (r >> 2) + 4 * lh; }
 
