@@ -295,8 +295,22 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   }
   if (PRO) {
     if (a.gin_part) {
-      // gn_finalize (gn.hip) for the tile's images, same expressions (conv_patch3.hip's in-kernel finalize)
+      // gn_finalize (gn.hip) for the tile's images, same expressions (conv_patch3.hip's in-kernel finalize).
+      // The per-channel affine (and AdaGN modulation) of this thread's table entries is loaded first, with
+      // the statistics partials, so the prologue waits for one round trip, not two.
       const int G = a.gin_G, cpg = a.Cin1 / G;
+      constexpr int TU = kTab / 2 / 256;  // table entries per thread
+      float gam[TU], bet[TU], fms[TU], fmb[TU];
+#pragma unroll
+      for (int u = 0; u < TU; ++u) {
+        const int i = min(t + 256 * u, tab_n * tab_c - 1);
+        const int bi = i / tab_c, c = tab_c0 + i - (i / tab_c) * tab_c;
+        gam[u] = a.gin_gamma ? a.gin_gamma[c] : 1.0f;
+        bet[u] = a.gin_beta ? a.gin_beta[c] : 0.0f;
+        const size_t mo = (size_t)(tab_img0 + bi) * a.gin_mp + c;
+        fms[u] = a.gin_ms ? a.gin_ms[mo] : 0.0f;
+        fmb[u] = a.gin_mb ? a.gin_mb[mo] : 0.0f;
+      }
       for (int i = t; i < tab_n * G; i += 256) {
         const int b = tab_img0 + i / G, gg = i - (i / G) * G;
         double s1 = 0, s2 = 0;
@@ -313,20 +327,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
         gstat[2 * i + 1] = (float)(1.0 / sqrt(var + (double)a.gin_eps));
       }
       __syncthreads();
-      for (int i = t; i < tab_n * tab_c; i += 256) {
-        const int bi = i / tab_c, c = tab_c0 + i - (i / tab_c) * tab_c;
-        const int si = 2 * (bi * G + c / cpg);
-        const float mu = gstat[si], rs = gstat[si + 1];
-        float sc = rs * (a.gin_gamma ? a.gin_gamma[c] : 1.0f);
-        float sh = -sc * mu + (a.gin_beta ? a.gin_beta[c] : 0.0f);
-        if (a.gin_ms) {
-          const size_t mo = (size_t)(tab_img0 + bi) * a.gin_mp + c;
-          const float f = 1.0f + a.gin_ms[mo];
-          sc = sc * f;
-          sh = sh * f + (a.gin_mb ? a.gin_mb[mo] : 0.0f);
+#pragma unroll
+      for (int u = 0; u < TU; ++u) {
+        const int i = t + 256 * u;
+        if (i < tab_n * tab_c) {
+          const int bi = i / tab_c, c = tab_c0 + i - (i / tab_c) * tab_c;
+          const int si = 2 * (bi * G + c / cpg);
+          const float mu = gstat[si], rs = gstat[si + 1];
+          float sc = rs * gam[u];
+          float sh = -sc * mu + bet[u];
+          if (a.gin_ms) {
+            const float f = 1.0f + fms[u];
+            sc = sc * f;
+            sh = sh * f + fmb[u];
+          }
+          gtab[i] = sc;
+          gtab[tab_n * tab_c + i] = sh;
         }
-        gtab[i] = sc;
-        gtab[tab_n * tab_c + i] = sh;
       }
     } else {
       for (int i = t; i < tab_n * tab_c; i += 256) {
