@@ -138,10 +138,10 @@ struct StagedEpilogue {
       if (m < M && c_ok) *reinterpret_cast<f4*>(dst + (size_t)m * pitch + ncol) = v;
     }
   }
-  // statistics of the 64-row chunk starting at crow0 (all 64 lanes call; resets the sums)
-  __device__ __forceinline__ void emit(int crow0) {
-    const int cpg = a.Cout / a.gn_G;
-    double s = 0.0, q = 0.0;
+  // this lane's 4-channel quad summed over the wave's rows so far (all 64 lanes call; resets the sums)
+  __device__ __forceinline__ void quad_sums(double& s, double& q) {
+    s = 0.0;
+    q = 0.0;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       s += gs[e];
@@ -153,6 +153,16 @@ struct StagedEpilogue {
       s += __shfl_xor(s, o);
       q += __shfl_xor(q, o);
     }
+  }
+  // statistics of the 64-row chunk starting at crow0 (all 64 lanes call; resets the sums)
+  __device__ __forceinline__ void emit(int crow0) {
+    double s, q;
+    quad_sums(s, q);
+    store_quads(s, q, crow0);
+  }
+  // the group sums of per-quad chunk totals s, q (valid in every lane of the quad's column) to gn_part
+  __device__ __forceinline__ void store_quads(double s, double q, int crow0) {
+    const int cpg = a.Cout / a.gn_G;
     for (int o = 1; o < cpg / 4; o <<= 1) {
       s += __shfl_xor(s, o);
       q += __shfl_xor(q, o);

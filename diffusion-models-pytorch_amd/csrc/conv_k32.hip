@@ -105,6 +105,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   const int HWo = Ho * Wo;
   const int b0 = m0 / HWo;
   const int y0 = (m0 - b0 * HWo) / Wo;
+  const int x0 = (m0 - b0 * HWo) - y0 * Wo;  // row-segment tiles (64 pixels of a wider row); 0 otherwise
 
   K32_RSTAMP(5);
   K32_STAMP(0);
@@ -126,7 +127,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     const int rem = p - img * PHW;
     const int pr = rem / g.PW, pc = rem - (rem / g.PW) * g.PW;
     const int b = b0 + img;
-    const int iy = y0 - 1 + pr, ix = pc - 1;
+    const int iy = y0 - 1 + pr, ix = x0 + pc - 1;
     const bool ok = p < g.P && b < a.B && iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
     pok[j] = ok;
     const int bc = min(b, a.B - 1);
@@ -459,6 +460,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     __builtin_amdgcn_wave_barrier();  // the next slab's writes reuse the region
     if (!KSPLIT && a.gn_part && (h & 1)) epi.emit(wrow0 + 32 * (h - 1));
   }
+  if constexpr (!KSPLIT && WM == 32) {
+    if (a.gn_part) {  // 64-row tiles: the block's 64 rows are one chunk, held by the two row waves
+      double s, q;
+      epi.quad_sums(s, q);
+      double* xr = reinterpret_cast<double*>(patch) + 6144;  // past the slabs (48 KiB in)
+      if (wm == 1 && lane < Epi::LPR) {
+        xr[(wn * Epi::LPR + lane) * 2] = s;
+        xr[(wn * Epi::LPR + lane) * 2 + 1] = q;
+      }
+      __syncthreads();
+      if (wm == 0) {
+        s += xr[(wn * Epi::LPR + lane % Epi::LPR) * 2];
+        q += xr[(wn * Epi::LPR + lane % Epi::LPR) * 2 + 1];
+        epi.store_quads(s, q, m0);
+      }
+    }
+  }
   K32_STAMP(4);
   K32_RSTAMP(6);
 }
@@ -472,20 +490,21 @@ extern "C" int dm_debug_k32_stamps(void* host, int nblocks) {
 }
 #endif
 
-// Variants: 1 = 128 x 128 tiles, 2 = 128 x 64 (whole K), 3 = 64 x 64 and 4 = 64 x 128 split-K tiles.
+// Variants: 1 = 128 x 128 tiles, 2 = 128 x 64 (whole K), 3 = 64 x 64 and 4 = 64 x 128 split-K tiles,
+// 5 = 64 x 128 tiles of one image row or 64-pixel row segment (ADM's 64^2 .. 256^2 maps).
 int conv_k32_variant_ok(const ConvArgs& a, int v) {
   const bool sub = a.upsample == 2;  // sub-pixel nearest-2x + 3x3: 4 parity convs of 4 taps
   if (!(a.ws && a.ws_np == 2 && a.ws_rowscale && a.taps == 9 && a.stride == 1 && (a.upsample == 0 || sub))) return 0;
   if (a.Cin1 < kC || a.Cin1 % kC != 0 || a.Cin2 % kC != 0) return 0;
   if (sub ? (a.Cin2 != 0 || a.K != 4 * a.Cin1) : a.K != 9 * a.Cin1 + a.Cin2) return 0;
-  const bool split = v >= 3;
+  const bool split = v == 3 || v == 4, seg = v == 5;
   if (split && sub) return 0;
-  const int bm = split ? 64 : BM_K32;
+  const int bm = (split || seg) ? 64 : BM_K32;
   if (split ? !(a.ksplit > 1 && a.kpart && a.ksplit <= a.Cin1 / kC) : a.ksplit > 1) return 0;
   const int wt = sub ? a.Win : a.Wout;  // tiled width
-  if (wt > bm || bm % wt != 0) return 0;
+  if (seg ? (wt < 64 || wt % 64 != 0) : (wt > bm || bm % wt != 0)) return 0;
   PatchGeom g;
-  if (!conv_patch_geom(a, bm, g) || g.P > kMaxP || g.TB > (split ? 4 : 2)) return 0;
+  if (!conv_patch_geom(a, bm, g) || g.P > kMaxP || g.TB > (split ? 4 : 2) || (seg && g.TB != 1)) return 0;
   const int nch = a.Cin1 / kC, tab_c = split ? ceil_div(nch, a.ksplit) * kC : a.Cin1;
   if (a.pro_scale && 2 * g.TB * tab_c > kTab) return 0;
   if (a.gin_part && g.TB * a.gin_G > kStats) return 0;
@@ -511,12 +530,16 @@ bool conv_k32_enabled() {
 }
 
 int conv_k32_pick(const ConvArgs& a) {
-  if (a.tile >= 10 && a.tile <= 13) return conv_k32_variant_ok(a, a.tile - 9) ? a.tile - 9 : 0;
+  if (a.tile >= 10 && a.tile <= 14) return conv_k32_variant_ok(a, a.tile - 9) ? a.tile - 9 : 0;
   if (a.tile != 0 || !conv_k32_enabled()) return 0;
   // split-K convs of maps of <= 16 pixels: 64 x 128 tiles (4x4 maps at B = 256, K split 2: 32.5 us vs
   // 34.2 us for 64 x 64 and for conv_patch3's 64 x 64 split tiles)
   if (a.ksplit > 1) return conv_k32_variant_ok(a, 4) ? 4 : conv_k32_variant_ok(a, 3) ? 3 : 0;
-  if (!conv_k32_ok(a)) return 0;
+  if (!conv_k32_ok(a)) {
+    // maps whose whole-row 128-row tiles do not fit the patch image (64^2 .. 256^2): 64-pixel rows / segments
+    const int wt = a.upsample == 2 ? a.Win : a.Wout;
+    return (wt >= 64 && conv_k32_variant_ok(a, 5)) ? 5 : 0;
+  }
   const int p = conv_pick(a);
   if (p != 3 && p != 4) return 0;
   // 128 x 128 tiles down to one block per CU (measured on 8^2 maps at B = 256: 256 blocks of 128 x 128 beat
@@ -528,8 +551,9 @@ int conv_k32_pick(const ConvArgs& a) {
 // rocprofv3's name of the instantiation conv2d_k32 launches (spaces removed)
 std::string conv_k32_label(const ConvArgs& a, int v) {
   static const char* names[] = {"", "conv_k32_kernel<128,128,64,64,", "conv_k32_kernel<128,64,64,32,",
-                                "conv_k32_kernel<64,64,32,32,", "conv_k32_kernel<64,128,32,64,"};
-  return std::string(names[v]) + (a.pro_scale ? "true," : "false,") + (v >= 3 ? "true," : "false,") +
+                                "conv_k32_kernel<64,64,32,32,", "conv_k32_kernel<64,128,32,64,",
+                                "conv_k32_kernel<64,128,32,64,"};
+  return std::string(names[v]) + (a.pro_scale ? "true," : "false,") + (v == 3 || v == 4 ? "true," : "false,") +
          (a.upsample == 2 ? "true>" : "false>");
 }
 
@@ -554,17 +578,18 @@ static void launch_k32(const ConvArgs& a, const PatchGeom& g, hipStream_t st) {
 }
 
 int conv2d_k32(const ConvArgs& a, int v, hipStream_t st) {
-  DM_REQUIRE(v >= 1 && v <= 4 && conv_k32_variant_ok(a, v), "conv: shape not supported by the K = 32 split kernel");
+  DM_REQUIRE(v >= 1 && v <= 5 && conv_k32_variant_ok(a, v), "conv: shape not supported by the K = 32 split kernel");
   PatchGeom g;
   conv_patch_geom(a, v >= 3 ? 64 : BM_K32, g);
   switch (v) {
     case 1: launch_k32<128, 128, 64, 64, false>(a, g, st); break;
     case 2: launch_k32<128, 64, 64, 32, false>(a, g, st); break;
     case 3: launch_k32<64, 64, 32, 32, true>(a, g, st); break;
-    default: launch_k32<64, 128, 32, 64, true>(a, g, st); break;
+    case 4: launch_k32<64, 128, 32, 64, true>(a, g, st); break;
+    default: launch_k32<64, 128, 32, 64, false>(a, g, st); break;
   }
   DM_LAUNCH_CHECK();
-  if (v >= 3) return conv_splitk_reduce(a, st);
+  if (v == 3 || v == 4) return conv_splitk_reduce(a, st);
   return DM_OK;
 }
 

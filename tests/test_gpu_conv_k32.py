@@ -160,3 +160,61 @@ def test_k32_subpixel_fp32_accuracy(cuda, B, Cin, Cout, H):
     for k in ('k32', 'k32_64'):
         assert errs[k] < 2.0 * errs['fp32'] + 1e-7 * scale, errs
         assert errs[k] < 4e-6 * scale, (errs, scale)
+
+
+@pytest.mark.parametrize('tile', [14, 0])
+@pytest.mark.parametrize('B,Cin,Cout,H', [(2, 64, 128, 64), (1, 32, 64, 128), (1, 64, 64, 256), (3, 96, 160, 64)])
+def test_k32_row_segments_exact(cuda, B, Cin, Cout, H, tile):
+    """64 x 128 tiles over one 64-pixel row or a 64-pixel segment of a wider row (ADM's 64^2 .. 256^2 maps)."""
+    x = _ints((B, Cin, H, H), -2, 3, seed=50)
+    w = _ints((Cout, Cin, 3, 3), -2, 3, seed=51)
+    b = _ints((Cout, ), seed=52)
+    ref = F.conv2d(x.double(), w.double(), b.double(), padding=1).float()
+    y = _run_conv(cuda, _nhwc(x).to(cuda), _pack(w, cuda), Cout, H, H, 9, 1, 0, b.to(cuda), tile=tile,
+                  split='fp16x2')
+    assert torch.equal(y.cpu(), _nhwc(ref))
+
+
+@pytest.mark.parametrize('tile', [14, 0])
+def test_k32_row_segments_segments_rowvec_residual(cuda, tile):
+    B, C1, C2, Cout, H = 2, 64, 32, 64, 128
+    h = _ints((B, C1, H, H), seed=60)
+    x = _ints((B, C2, H, H), seed=61)
+    w2 = _ints((Cout, C1, 3, 3), -2, 3, seed=62)
+    ws = _ints((Cout, C2, 1, 1), seed=63)
+    b = _ints((Cout, ), seed=64)
+    rv = _ints((B, Cout), seed=65)
+    res = _ints((B, Cout, H, H), seed=66)
+    K = 9 * C1 + C2
+    wp = torch.zeros((Cout, K), device=cuda)
+    _pack(w2, cuda, K, 0, wp)
+    _pack(ws, cuda, K, 9 * C1, wp)
+    ref = (F.conv2d(h.double(), w2.double(), b.double(), padding=1) + rv.double()[:, :, None, None]
+           + F.conv2d(x.double(), ws.double()) + res.double()).float()
+    y = _run_conv(cuda, _nhwc(h).to(cuda), wp, Cout, H, H, 9, bias=b.to(cuda), rowvec=rv.to(cuda),
+                  res=_nhwc(res).to(cuda), x2=_nhwc(x).to(cuda), Cin2=C2, y_pitch=96, tile=tile, split='fp16x2')
+    assert torch.equal(y[..., :Cout].cpu(), _nhwc(ref))
+    assert torch.isnan(y[..., Cout:]).all()
+
+
+@pytest.mark.parametrize('tile', [14, 0])
+@pytest.mark.parametrize('B,Cin,Cout,H', [(1, 64, 64, 64), (1, 32, 64, 128)])
+def test_k32_row_segments_subpixel_exact(cuda, B, Cin, Cout, H, tile):
+    x = _ints((B, Cin, H, H), -2, 3, seed=80)
+    w = _ints((Cout, Cin, 3, 3), -1, 2, seed=81)
+    b = _ints((Cout, ), seed=82)
+    ref = F.conv2d(F.interpolate(x, scale_factor=2, mode='nearest').double(), w.double(), b.double(),
+                   padding=1).float()
+    y = _run_conv(cuda, _nhwc(x).to(cuda), _pack_subpix(w, cuda), Cout, 2 * H, 2 * H, 9, 1, 2, b.to(cuda),
+                  tile=tile, split='fp16x2')
+    assert torch.equal(y.cpu(), _nhwc(ref))
+
+
+@pytest.mark.parametrize('B,Cin,Cout,H', [(2, 256, 256, 64), (1, 256, 128, 128)])
+def test_k32_row_segments_fp32_accuracy(cuda, B, Cin, Cout, H):
+    """(the fp32 kernels have no fused-GroupNorm shape this wide: the bound alone, as for the other tiles)"""
+    xd, wp, b, pro, ref = _rand_case(cuda, B, Cin, Cout, H, 0, seed=94)
+    y = _run_conv(cuda, xd, wp, Cout, H, H, 9, 1, 0, b.to(cuda), pro=pro, split='fp16x2', tile=14)
+    err = (y.cpu().double() - _nhwc(ref)).abs().max().item()
+    scale = ref.abs().max().item()
+    assert err < 4e-6 * scale, (err, scale)
