@@ -24,6 +24,25 @@ namespace dm {
 
 namespace {
 
+#ifdef DM_K32_STAMPS
+// Diagnostic build only (tools/linear_stamps.py): per block of launches with K == g_lin_stamp_k (a device
+// symbol the tool sets), wave 0's s_memtime at the start, after the prologue, after the K loop and at the
+// end, plus s_memrealtime start / end. Written to this buffer only.
+__device__ unsigned long long g_lin_stamps[65536][8];
+__device__ int g_lin_stamp_k;
+#define LIN_STAMP(k)                                                                                         \
+  do {                                                                                                       \
+    if (threadIdx.x == 0 && blockIdx.x < 65536 && g.K == g_lin_stamp_k) g_lin_stamps[blockIdx.x][k] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#define LIN_RSTAMP(k)                                                                                        \
+  do {                                                                                                       \
+    if (threadIdx.x == 0 && blockIdx.x < 65536 && g.K == g_lin_stamp_k) g_lin_stamps[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define LIN_STAMP(k) do {} while (0)
+#define LIN_RSTAMP(k) do {} while (0)
+#endif
+
 constexpr int kLP = 144;   // LDS row pitch in fp16 (288 B) of one 64-channel stage
 constexpr int kLBM = 128;  // block rows
 constexpr int kLGM = 4;    // M tiles per group of the tile order
@@ -111,6 +130,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   // prologue tables of three K stages (staged two stages ahead): [stage % 3][image of the tile][scale, shift][ch]
   __shared__ __attribute__((aligned(16))) float tab[3][2][2][64];
 
+  LIN_RSTAMP(5);
+  LIN_STAMP(0);
   const int M = g.M, N = g.N, K = g.K;
   // Grouped tile order: consecutive tiles (one XCD, xcd_remap_p) sweep all N tiles for a group of kLGM M
   // tiles, M fastest, so the group's kLGM blocks of one weight tile run together and fetch it from the
@@ -243,6 +264,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   __syncthreads();
   finish_a(0, 0);
   __syncthreads();
+  LIN_STAMP(1);
   // One barrier per stage. Stage st: the next stage's A rows and the tables of stage st + 2 are loaded
   // before step 0; after step 1 the tables go to LDS and the next stage is finished into the other
   // buffer (its tables were stored a stage earlier, visible since the last barrier).
@@ -262,6 +284,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     finish_a((st + 1) & 1, (st + 1) % 3);
     __syncthreads();
   }
+  LIN_STAMP(2);
   // ---- epilogue: per 32-row slab of the wave's 64 rows, acc * rowscale * 2^-ea to LDS ([32][68] fp32),
   // then 4 consecutive columns per lane: bias, residual / gated residual, activation, 16-B store
   constexpr int EP = WN + 4, LPR = WN / 4, RPI = 64 / LPR;
@@ -318,9 +341,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     __builtin_amdgcn_wave_barrier();  // the next slab reuses the region
   }
   if (bad && g.range_flag) *g.range_flag = 1;
+  LIN_STAMP(3);
+  LIN_RSTAMP(6);
 }
 
 }  // namespace
+
+#ifdef DM_K32_STAMPS
+extern "C" int dm_debug_lin_stamps(void* host, int nblocks, int k) {
+  if (!host) return hipMemcpyToSymbol(HIP_SYMBOL(g_lin_stamp_k), &k, sizeof(int)) == hipSuccess ? 0 : -2;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_lin_stamps), (size_t)nblocks * 8 * sizeof(unsigned long long)) ==
+                 hipSuccess ? 0 : -2;
+}
+#endif
 
 bool linear_k32_ok(const GemmArgs& g) {
   auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
