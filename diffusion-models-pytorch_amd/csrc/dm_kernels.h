@@ -156,6 +156,10 @@ struct GemmArgs {
   // their inverse row scales; such GEMMs run linear_k32 (linear_k32.hip) and split_eb is unused
   const void* ws;
   const float* ws_rowscale;
+  // linear_k32 only: pre-split A (linear_presplit_a's image of the prologue'd, alpha- and 2^split_ea-scaled
+  // rows, [M][K / 32][piece][4 k-groups][8] fp16); the kernel then stages it into LDS without conversion
+  // (pro_scale / ln_stats must be null: they are applied by the pre-split pass)
+  const _Float16* as;
   // linear_k32 only: the attention operand planes instead of C (as ConvArgs::ap_*, the qkv projection
   // feeding attn_presplit_kernel)
   _Float16 *ap_q, *ap_k, *ap_v;
@@ -246,6 +250,8 @@ std::string conv_k32_label(const ConvArgs& a, int v);
 // static-weight GEMM on pre-split weights with K = 32 MFMA steps (linear_k32.hip)
 bool linear_k32_ok(const GemmArgs& g);
 int linear_k32(const GemmArgs& g, hipStream_t st);
+// the pre-split A image of g (prologue, alpha, 2^split_ea, fp16x2 split; |value| > 65504 sets range_flag)
+int linear_presplit_a(const GemmArgs& g, _Float16* out, hipStream_t st);
 int conv_splitk_reduce(const ConvArgs& a, hipStream_t st);
 // fp32 packed conv weights [nmat][rows][K] -> split slices for conv_patch3_kernel (np 3: bf16x3,
 // np 2: fp16x2 + row scales); split_conv_rowscale gives ConvArgs::ws_rowscale of an fp16x2 copy

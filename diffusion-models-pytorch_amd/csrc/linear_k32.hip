@@ -47,7 +47,9 @@ constexpr int kLP = 144;   // LDS row pitch in fp16 (288 B) of one 64-channel st
 constexpr int kLBM = 128;  // block rows
 constexpr int kLGM = 4;    // M tiles per group of the tile order
 
-// PRO: 0 none, 1 GroupNorm affine (pro_scale / pro_shift [img][K]), 2 LayerNorm + modulate.
+// PRO: 0 none, 1 GroupNorm affine (pro_scale / pro_shift [img][K]), 2 LayerNorm + modulate, 3 pre-split A
+// (GemmArgs::as: no conversion on the way into LDS -- the split of A costs VALU work once per N tile
+// otherwise, which with K = 256 (the UNet's qkv) left the MFMAs idle most of the K loop).
 // Wave tiles WM x WN: 128 x 32 (each wave all 128 rows from LDS, its own 32 weight columns: every B
 // fragment fetched once per block, half the L2 traffic of 64 x 64 wave tiles, where each weight fragment is
 // loaded by both row waves) or 64 x 64.
@@ -121,6 +123,134 @@ __device__ __forceinline__ void plane_slab(const GemmArgs& g, const float* st, i
   }
 }
 
+// The whole 128 x 128 block tile (acc * rowscale * 2^-ea in LDS as [128][TP] fp32) -> the attention operand
+// planes, with every 16 consecutive threads storing 256 contiguous bytes of a plane: q / k rows of 8
+// consecutive d per thread (16 threads per token), v as 4 columns x 8 tokens per thread (16 threads per
+// d row of the tile's 128 tokens) -- instead of the per-wave slabs' 64-B row pieces and 512-B strided v
+// stores. The tile's rows lie in one image (L % 128 == 0); per 8-column group one of q / k / v and one head.
+__device__ __forceinline__ void plane_block(const GemmArgs& g, const float* tile, int TP, int m0, int n0, int t,
+                                            bool& bad) {
+  const int Dh = g.ap_Dh, C = g.ap_heads * Dh;
+  const size_t plane = (size_t)g.ap_L * Dh;
+  auto col_map = [&](int col, int& part, int& h, int& d) {
+    if (g.ap_legacy) {
+      h = col / (3 * Dh);
+      part = (col - h * 3 * Dh) / Dh;
+      d = col - h * 3 * Dh - part * Dh;
+    } else {
+      part = col / C;
+      h = (col - part * C) / Dh;
+      d = col - part * C - h * Dh;
+    }
+  };
+  auto split8 = [&](int part, const float (&x)[8], f16x8& hi, f16x8& lo) {
+    const float scale = part == 0 ? g.ap_alpha : part == 1 ? g.ap_bscale : 1.f;
+    const bool use_scale = part == 0 ? g.ap_alpha != 1.0f : part == 1 && g.ap_bscale != 0.0f && g.ap_bscale != 1.0f;
+    const float pw = ldexpf(1.f, part == 0 ? g.ap_ea : part == 1 ? g.ap_eb : g.ap_ev);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float y = (use_scale ? x[e] * scale : x[e]) * pw;
+      const _Float16 h0 = (_Float16)y;
+      hi[e] = h0;
+      lo[e] = (_Float16)(y - (float)h0);
+      bad |= fabsf(y) > 65504.f;
+    }
+  };
+  const int b = m0 / g.ap_L, tok0 = m0 - b * g.ap_L;
+  const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  {  // q / k: item (row, 8-column group), 16 groups per row; a thread keeps its column group
+    const int c8 = t & 15, col = n0 + 8 * c8;
+    int part, h, d;
+    col_map(min(col, g.N - 1), part, h, d);
+    if (col < g.N && part < 2) {
+      const f4 b0 = g.bias ? *reinterpret_cast<const f4*>(g.bias + col) : zero4;
+      const f4 b1 = g.bias ? *reinterpret_cast<const f4*>(g.bias + col + 4) : zero4;
+      _Float16* base = (part == 0 ? g.ap_q : g.ap_k) + ((size_t)b * g.ap_heads + h) * 2 * plane + (size_t)tok0 * Dh + d;
+#pragma unroll 2
+      for (int row = t >> 4; row < 128; row += 16) {
+        if (m0 + row >= g.M) break;
+        const f4 v0 = *reinterpret_cast<const f4*>(tile + row * TP + 8 * c8) + b0;
+        const f4 v1 = *reinterpret_cast<const f4*>(tile + row * TP + 8 * c8 + 4) + b1;
+        const float x[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+        f16x8 hi, lo;
+        split8(part, x, hi, lo);
+        _Float16* p = base + (size_t)row * Dh;
+        *reinterpret_cast<f16x8*>(p) = hi;
+        *reinterpret_cast<f16x8*>(p + plane) = lo;
+      }
+    }
+  }
+  // v: item (4-column group, 8-token group), 16 token groups per column group
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int it = t + 256 * k;
+    const int r8 = it & 15, cq = it >> 4, col = n0 + 4 * cq;
+    if (col >= g.N || m0 + 8 * r8 >= g.M) continue;  // M % 8 == 0 (L % 128 == 0)
+    int part, h, d;
+    col_map(col, part, h, d);
+    if (part != 2) continue;
+    const f4 bc = g.bias ? *reinterpret_cast<const f4*>(g.bias + col) : zero4;
+    f4 v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = *reinterpret_cast<const f4*>(tile + (8 * r8 + e) * TP + 4 * cq);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      float x[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = v[e][c] + bc[c];
+      f16x8 hi, lo;
+      split8(2, x, hi, lo);
+      _Float16* p = g.ap_v + ((size_t)b * g.ap_heads + h) * 2 * plane + (size_t)(d + c) * g.ap_L + tok0 + 8 * r8;
+      *reinterpret_cast<f16x8*>(p) = hi;
+      *reinterpret_cast<f16x8*>(p + plane) = lo;
+    }
+  }
+}
+
+// linear_presplit_a: one thread per 8 consecutive channels (one k-group of one K = 32 step) of a row:
+// the linear_k32 prologue's expressions (finish_a), the split, piece 0 at [m][kk][0][kg], piece 1 at [m][kk][1][kg].
+template <int PRO>
+__global__ void __launch_bounds__(256) presplit_a_kernel(GemmArgs g, _Float16* out) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const int per_row = g.K / 8;
+  if (i >= (long)g.M * per_row) return;
+  const int m = (int)(i / per_row), c = (int)(i - (long)m * per_row) * 8;
+  const float* a = g.A + (size_t)m * g.lda + c;
+  f4 v0 = *reinterpret_cast<const f4*>(a), v1 = *reinterpret_cast<const f4*>(a + 4);
+  if (PRO == 1) {
+    const size_t o = (size_t)(m / g.pro_rows) * g.K + c;
+    const f4 s0 = *reinterpret_cast<const f4*>(g.pro_scale + o), s1 = *reinterpret_cast<const f4*>(g.pro_scale + o + 4);
+    const f4 h0 = *reinterpret_cast<const f4*>(g.pro_shift + o), h1 = *reinterpret_cast<const f4*>(g.pro_shift + o + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v0[e] = v0[e] * s0[e] + h0[e];
+      v1[e] = v1[e] * s1[e] + h1[e];
+    }
+  } else if (PRO == 2) {
+    const float2 lns = g.ln_stats[m];
+    const size_t o = (size_t)(m / g.ln_rows) * g.ln_pitch + c;
+    const f4 s0 = *reinterpret_cast<const f4*>(g.ln_scale + o), s1 = *reinterpret_cast<const f4*>(g.ln_scale + o + 4);
+    const f4 h0 = *reinterpret_cast<const f4*>(g.ln_shift + o), h1 = *reinterpret_cast<const f4*>(g.ln_shift + o + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v0[e] = ((v0[e] - lns.x) * lns.y) * (1.0f + s0[e]) + h0[e];
+      v1[e] = ((v1[e] - lns.x) * lns.y) * (1.0f + s1[e]) + h1[e];
+    }
+  }
+  if (g.alpha != 1.0f) {
+    v0 = v0 * g.alpha;
+    v1 = v1 * g.alpha;
+  }
+  const float apow = ldexpf(1.f, g.split_ea);
+  bool bad = false;
+  f16x8 pc[2];
+  Split<2>::split(v0 * apow, v1 * apow, pc, bad);
+  _Float16* dst = out + (size_t)m * 2 * g.K + (c / 32) * 64 + ((c % 32) / 8) * 8;
+  *reinterpret_cast<f16x8*>(dst) = pc[0];
+  *reinterpret_cast<f16x8*>(dst + 32) = pc[1];
+  if (bad && g.range_flag) *g.range_flag = 1;
+}
+
 template <int PRO, int WM = 128, int WN = 32>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) linear_k32_kernel(GemmArgs g) {
   constexpr int BM = kLBM, BN = 128, TM = WM / 16, TN = WN / 16, WD = 2, NWN = BN / WN;
@@ -151,21 +281,28 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   // ---- A loader: row lrow of the tile, channels 64 st + 32 lh .. + 31
   const int am = min(m0 + lrow, M - 1);  // rows >= M: clamped, never stored
   const float* asrc = g.A + (size_t)am * g.lda + 32 * lh;
+  constexpr bool TABS = PRO == 1 || PRO == 2;
   const int rows_img = PRO == 1 ? g.pro_rows : PRO == 2 ? g.ln_rows : 1;
-  const int img0 = PRO ? m0 / rows_img : 0;
-  const int aimg = PRO ? am / rows_img - img0 : 0;  // 0 or 1 (rows per image >= 128)
+  const int img0 = TABS ? m0 / rows_img : 0;
+  const int aimg = TABS ? am / rows_img - img0 : 0;  // 0 or 1 (rows per image >= 128)
+  const f4* asp = PRO == 3 ? reinterpret_cast<const f4*>(g.as + (size_t)am * 2 * K) + 8 * lh : nullptr;
   const float2 lns = PRO == 2 ? g.ln_stats[am] : make_float2(0.f, 1.f);
   const float apow = ldexpf(1.f, g.split_ea);
-  f4 ra[8];
+  f4 ra[2][8];  // A rows of two stages in flight (stage s in ra[s & 1])
   f4 rt;  // threads 0 .. 63: one f4 of a stage's tables
   const int ti = t >> 4, tk = (t & 15) * 4;  // table loader: (image, scale | shift) pair ti, channels tk
-  auto load_a = [&](int st) {
+  auto load_a = [&](f4 (&dst)[8], int st) {
+    if (PRO == 3) {  // the step's 64 fp16 (two pieces x 4 k-groups x 8) as 8 x 16 B
+#pragma unroll
+      for (int u = 0; u < 8; ++u) dst[u] = asp[16 * st + u];
+      return;
+    }
     const float* p = asrc + 64 * st;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) ra[u] = *reinterpret_cast<const f4*>(p + 4 * u);
+    for (int u = 0; u < 8; ++u) dst[u] = *reinterpret_cast<const f4*>(p + 4 * u);
   };
   auto load_tab = [&](int st) {
-    if (PRO && t < 64) {
+    if (TABS && t < 64) {
       const int im = min(img0 + (ti >> 1), (M - 1) / rows_img);
       const int kk = 64 * st + tk;
       if (PRO == 1)
@@ -175,16 +312,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     }
   };
   auto store_tab = [&](int buf) {
-    if (PRO && t < 64) *reinterpret_cast<f4*>(&tab[buf][ti >> 1][ti & 1][tk]) = rt;
+    if (TABS && t < 64) *reinterpret_cast<f4*>(&tab[buf][ti >> 1][ti & 1][tk]) = rt;
   };
   bool bad = false;
   // prologue + split + LDS store of this thread's 32 channels (tables of the stage in tab[buf])
-  auto finish_a = [&](int buf, int tb) {
+  auto finish_a = [&](const f4 (&src)[8], int buf, int tb) {
     _Float16* dst = abuf + buf * STAGE + lrow * kLP + lh * 64;
+    if (PRO == 3) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) *reinterpret_cast<f4*>(dst + 8 * u) = src[u];
+      return;
+    }
 #pragma unroll
     for (int u = 0; u < 8; u += 2) {  // k-group u / 2: channels 8 (u / 2) .. + 7 of the step
-      f4 v0 = ra[u], v1 = ra[u + 1];
-      if (PRO) {
+      f4 v0 = src[u], v1 = src[u + 1];
+      if (TABS) {
         const float* sc = &tab[tb][aimg][0][32 * lh + 4 * u];
         const float* sh = &tab[tb][aimg][1][32 * lh + 4 * u];
         const f4 s0 = *reinterpret_cast<const f4*>(sc), s1 = *reinterpret_cast<const f4*>(sc + 4);
@@ -256,21 +398,22 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   const int nst = K / 64, nkk = K / 32;
 #pragma unroll
   for (int d = 0; d < WD; ++d) load_b(bq[d], min(d, nkk - 1));
-  load_a(0);
+  load_a(ra[0], 0);
+  load_a(ra[1], min(1, nst - 1));
   load_tab(0);
   store_tab(0);
   load_tab(min(1, nst - 1));
   store_tab(1);
   __syncthreads();
-  finish_a(0, 0);
+  finish_a(ra[0], 0, 0);
   __syncthreads();
   LIN_STAMP(1);
-  // One barrier per stage. Stage st: the next stage's A rows and the tables of stage st + 2 are loaded
-  // before step 0; after step 1 the tables go to LDS and the next stage is finished into the other
-  // buffer (its tables were stored a stage earlier, visible since the last barrier).
-  for (int st = 0; st < nst; ++st) {
-    const int nx = min(st + 1, nst - 1);
-    load_a(nx);
+  // One barrier per stage. Stage st: the A rows of stage st + 2 (into the registers stage st's rows
+  // left) and the tables of stage st + 2 are loaded before step 0 -- two stages of MFMAs to land (K = 256
+  // GEMMs have 4 stages: one stage did not cover the load latency); after step 1 the tables go to LDS
+  // and stage st + 1 is finished into the other buffer (its tables were stored a stage earlier).
+  auto stage = [&](int st, f4 (&cur)[8], f4 (&nxt)[8]) {
+    load_a(cur, min(st + 2, nst - 1));
     load_tab(min(st + 2, nst - 1));
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -281,8 +424,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
       __builtin_amdgcn_sched_barrier(0);
     }
     store_tab((st + 2) % 3);
-    finish_a((st + 1) & 1, (st + 1) % 3);
+    finish_a(nxt, (st + 1) & 1, (st + 1) % 3);
     __syncthreads();
+  };
+  for (int st = 0; st < nst; st += 2) {
+    stage(st, ra[0], ra[1]);
+    if (st + 1 < nst) stage(st + 1, ra[1], ra[0]);
   }
   LIN_STAMP(2);
   // ---- epilogue: per 32-row slab of the wave's 64 rows, acc * rowscale * 2^-ea to LDS ([32][68] fp32),
@@ -299,6 +446,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   const int nc = c_ok ? ncol : 0;
   const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
   const f4 bias4 = g.bias ? *reinterpret_cast<const f4*>(g.bias + nc) : zero4;
+  if (g.ap_q && g.ap_L % BM == 0) {  // attention planes from the whole block tile (the loop ended on a barrier)
+    constexpr int TP = BN + 4;
+    static_assert(BM * TP * 4 <= 2 * STAGE * 2, "block tile fits the stage buffers");
+    float* tile = reinterpret_cast<float*>(abuf);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) tile[(wm * WM + 16 * i + 4 * q + r) * TP + wn * WN + 16 * j + l16] = acc[i][j][r] * cs[j];
+    __syncthreads();
+    plane_block(g, tile, TP, m0, n0, t, bad);
+    if (bad && g.range_flag) *g.range_flag = 1;
+    LIN_STAMP(3);
+    LIN_RSTAMP(6);
+    return;
+  }
 #pragma unroll
   for (int h = 0; h < WM / 32; ++h) {
 #pragma unroll
@@ -366,13 +530,32 @@ bool linear_k32_ok(const GemmArgs& g) {
   if (g.pro_scale && (g.pro_rows < kLBM || !al16(g.pro_scale) || !al16(g.pro_shift))) return false;
   if (g.ln_stats && (g.ln_rows < kLBM || g.ln_pitch % 4 != 0 || !al16(g.ln_scale) || !al16(g.ln_shift))) return false;
   if (g.pro_scale && g.ln_stats) return false;
+  if (g.as && (g.pro_scale || g.ln_stats || (reinterpret_cast<uintptr_t>(g.as) & 15) != 0)) return false;
   return true;
+}
+
+int linear_presplit_a(const GemmArgs& g, _Float16* out, hipStream_t st) {
+  DM_REQUIRE(g.K % 64 == 0 && g.lda % 4 == 0 && (reinterpret_cast<uintptr_t>(g.A) & 15) == 0 &&
+                 (reinterpret_cast<uintptr_t>(out) & 15) == 0 && !(g.pro_scale && g.ln_stats),
+             "linear_presplit_a: K % 64 == 0 and 16-byte aligned rows");
+  const long n = (long)g.M * (g.K / 8);
+  const int blocks = (int)((n + 255) / 256);
+  if (g.pro_scale)
+    hipLaunchKernelGGL(presplit_a_kernel<1>, dim3(blocks), dim3(256), 0, st, g, out);
+  else if (g.ln_stats)
+    hipLaunchKernelGGL(presplit_a_kernel<2>, dim3(blocks), dim3(256), 0, st, g, out);
+  else
+    hipLaunchKernelGGL(presplit_a_kernel<0>, dim3(blocks), dim3(256), 0, st, g, out);
+  DM_LAUNCH_CHECK();
+  return DM_OK;
 }
 
 int linear_k32(const GemmArgs& g, hipStream_t st) {
   DM_REQUIRE(linear_k32_ok(g), "linear_k32: needs pre-split weights, K % 64 == 0, 16-byte aligned 4-column rows");
   const int blocks = ceil_div(g.M, kLBM) * ceil_div(g.N, 128);
-  if (g.pro_scale)
+  if (g.as)
+    hipLaunchKernelGGL(linear_k32_kernel<3>, dim3(blocks), dim3(256), 0, st, g);
+  else if (g.pro_scale)
     hipLaunchKernelGGL(linear_k32_kernel<1>, dim3(blocks), dim3(256), 0, st, g);
   else if (g.ln_stats)
     hipLaunchKernelGGL(linear_k32_kernel<2>, dim3(blocks), dim3(256), 0, st, g);

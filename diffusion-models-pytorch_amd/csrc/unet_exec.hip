@@ -765,6 +765,8 @@ int UNetModel::build_plan(int B, int H, int W) {
   // A consumer whose input view has them skips its gn_partial pass; every other write to a view
   // drops its entry.
   std::map<const float*, std::pair<double2*, int>> gn_ready;
+  _Float16* qkv_as = nullptr;  // pre-split qkv input (linear_presplit_a), shared by the attention blocks
+  size_t qkv_as_bytes = 0;
   std::map<const float*, double2*> gn_bufs;
   auto gn_buf_for = [&](const View& v) -> double2* {
     auto it = gn_bufs.find(v.p);
@@ -981,7 +983,23 @@ int UNetModel::build_plan(int B, int H, int W) {
         add("gn_finalize", 0, 8.0 * B * C, [=](hipStream_t st) {
           return gn_finalize(xin, G, sta, 1e-5f, self->P(p.gn.g), self->P(p.gn.b), gsc, gsh, st);
         });
-        add_gemm(gl);
+        if (!std::getenv("DM_QKV_NO_PRESPLIT")) {
+          // GroupNorm + split of the input once (linear_presplit_a) instead of once per 128-column tile inside
+          // the GEMM: one buffer shared by the attention blocks (the plan's launches are stream-ordered)
+          const size_t need = (size_t)gl.M * gl.K * 4;
+          if (need > qkv_as_bytes) {
+            qkv_as = reinterpret_cast<_Float16*>(alloc(need));
+            qkv_as_bytes = need;
+          }
+          _Float16* asb = qkv_as;
+          add("linear_presplit_a", 0, 8.0 * gl.M * gl.K, [=](hipStream_t st) { return linear_presplit_a(gl, asb, st); });
+          GemmArgs g2 = gl;
+          g2.as = asb;
+          g2.pro_scale = g2.pro_shift = nullptr;
+          add_gemm(g2);
+        } else {
+          add_gemm(gl);
+        }
       } else if (conv_pw_ok(cq)) {
         gn_prologue(cq, xin, sta, p.gn.g, p.gn.b, nullptr, nullptr, 0);
         add_conv(cq);

@@ -1,7 +1,9 @@
 """Phase timing of linear_k32_kernel (diagnostic build -DDM_K32_STAMPS) on DiT-XL/2's GEMMs: the blocks of
-the last launch with the given K (1152: qkv / proj / fc1 / final, the last of which is recorded; 4608: fc2).
+the last launch with the given K (1152: qkv / proj / fc1 / final, the last of which is recorded; 4608: fc2),
+or (--unet) on the CIFAR-10 UNet's attention qkv projection at B=256 (K 256, N 768, attention-plane epilogue).
 
     DM_HIP_LIB=tools/bin/libdm_stamps.so python tools/linear_stamps.py --k 4608
+    DM_HIP_LIB=tools/bin/libdm_stamps.so python tools/linear_stamps.py --unet
 """
 import argparse
 import ctypes
@@ -23,22 +25,36 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--k', type=int, default=4608)
     ap.add_argument('--n', type=int, default=1152, help='N of the recorded launch (blocks = 128 x N / 128)')
+    ap.add_argument('--unet', action='store_true')
     args = ap.parse_args()
+    if args.unet:
+        args.k, args.n = 256, 768
     L = dmhip.load()
     L.dm_debug_lin_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
     assert L.dm_debug_lin_stamps(None, 0, args.k) == 0
     dev = torch.device('cuda', 0)
-    model = DiT_models['DiT-XL/2'](input_size=32, num_classes=1000, learn_sigma=True).eval()
-    init_synthetic_(model)
-    model = model.to(dev)
-    B = 64
-    x = torch.randn((B, 4, 32, 32), device=dev)
-    t = torch.randint(0, 1000, (B, ), device=dev)
-    y = torch.randint(0, 1000, (B, ), device=dev)
-    for _ in range(3):
-        model(x, t, y)
+    if args.unet:
+        from models.unet import UNet
+        model = UNet().eval()
+        init_synthetic_(model)
+        model = model.to(dev)
+        B, L_tok = 256, 256
+        x = torch.randn((B, 3, 32, 32), device=dev)
+        t = torch.full((B, ), 500, dtype=torch.long, device=dev)
+        for _ in range(4):
+            model(x, t)
+    else:
+        model = DiT_models['DiT-XL/2'](input_size=32, num_classes=1000, learn_sigma=True).eval()
+        init_synthetic_(model)
+        model = model.to(dev)
+        B, L_tok = 64, 256
+        x = torch.randn((B, 4, 32, 32), device=dev)
+        t = torch.randint(0, 1000, (B, ), device=dev)
+        y = torch.randint(0, 1000, (B, ), device=dev)
+        for _ in range(3):
+            model(x, t, y)
     torch.cuda.synchronize()
-    nblk = (B * 256 // 128) * (args.n // 128)
+    nblk = (B * L_tok // 128) * (args.n // 128)
     buf = np.zeros((nblk, 8), dtype=np.uint64)
     assert L.dm_debug_lin_stamps(buf.ctypes.data, nblk, args.k) == 0
     s = buf.astype(np.int64)
