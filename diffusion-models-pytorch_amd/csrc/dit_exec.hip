@@ -221,6 +221,32 @@ int DiTModel::build_plan(int B) {
                       (g.res ? 4.0 * g.M * g.N : 0.0);
     pl.add(gemm_label(g), fl, by, [=](hipStream_t st) { return gemm_batched(g, st); });
   };
+  // token GEMMs on linear_k32: LayerNorm-modulate (or nothing) + fp16x2 split of A once per GEMM
+  // (linear_presplit_a) instead of once per 128-column tile inside it (27 x for qkv, 36 x for fc1);
+  // one buffer shared by all of them (stream-ordered). DM_DIT_PRESPLIT=0: split inside the GEMM.
+  const bool presplit_on = !(std::getenv("DM_DIT_PRESPLIT") && std::getenv("DM_DIT_PRESPLIT")[0] == '0');
+  _Float16* as_buf = nullptr;
+  size_t as_bytes = 0;
+  auto add_token_gemm = [&](GemmArgs g) {
+    if (g.ws && presplit_on && g.M >= 4096) {
+      const size_t need = (size_t)g.M * g.K * 4;
+      if (need > as_bytes) {
+        as_buf = reinterpret_cast<_Float16*>(pl.alloc(need));
+        as_bytes = need;
+      }
+      GemmArgs g2 = g;
+      g2.as = as_buf;
+      g2.pro_scale = g2.pro_shift = nullptr;
+      g2.ln_stats = nullptr;
+      if (as_buf && linear_k32_ok(g2)) {
+        _Float16* buf = as_buf;
+        pl.add("linear_presplit_a", 0, 8.0 * g.M * g.K, [=](hipStream_t st) { return linear_presplit_a(g, buf, st); });
+        add_gemm(g2);
+        return;
+      }
+    }
+    add_gemm(g);
+  };
   // fp16x2 operand exponents (unet_exec.hip split_gemm): weights by max |w|, activations fixed (2^6 for
   // LayerNorm-modulated tokens, q, k, v, attention and MLP outputs; 2^14 for softmax rows)
   auto split = [&](GemmArgs& g, int ea, size_t w, size_t wn, int eb_act) {
@@ -304,7 +330,7 @@ int DiTModel::build_plan(int B) {
       GemmArgs g = linear(x, D, M, bp.qkv_w, bp.qkv_b, 3 * D, D, qkv, 3 * D);
       g.ln_stats = stats; g.ln_shift = mb; g.ln_scale = mb + D; g.ln_pitch = ada_total; g.ln_rows = T;
       split(g, 6, bp.qkv_w, (size_t)3 * D * D, 0);
-      add_gemm(g);
+      add_token_gemm(g);
     }
     {
       // timm Attention: qkv.reshape(B, N, 3, heads, d): q / k / v of head h at columns h*d, D + h*d, 2D + h*d
@@ -332,7 +358,7 @@ int DiTModel::build_plan(int B) {
       GemmArgs g = linear(Ob, D, M, bp.proj_w, bp.proj_b, D, D, x, D);
       g.res = x; g.ld_res = D; g.gate = mb + 2 * D; g.gate_pitch = ada_total; g.gate_rows = T;
       split(g, 6, bp.proj_w, (size_t)D * D, 0);
-      add_gemm(g);
+      add_token_gemm(g);
     }
     // MLP branch
     stats_op();
@@ -341,13 +367,13 @@ int DiTModel::build_plan(int B) {
       g.ln_stats = stats; g.ln_shift = mb + 3 * D; g.ln_scale = mb + 4 * D; g.ln_pitch = ada_total; g.ln_rows = T;
       g.act = 2;
       split(g, 6, bp.fc1_w, (size_t)Hm * D, 0);
-      add_gemm(g);
+      add_token_gemm(g);
     }
     {
       GemmArgs g = linear(hb, Hm, M, bp.fc2_w, bp.fc2_b, D, Hm, x, D);
       g.res = x; g.ld_res = D; g.gate = mb + 5 * D; g.gate_pitch = ada_total; g.gate_rows = T;
       split(g, 6, bp.fc2_w, (size_t)D * Hm, 0);
-      add_gemm(g);
+      add_token_gemm(g);
     }
   }
   // --- final layer (dit/model.py:138-142) + unpatchify
@@ -357,8 +383,9 @@ int DiTModel::build_plan(int B) {
     GemmArgs g = linear(x, D, M, fin_w, fin_b, PP * OC, D, lin, PP * OC);
     g.ln_stats = stats; g.ln_shift = mf; g.ln_scale = mf + D; g.ln_pitch = ada_total; g.ln_rows = T;
     split(g, 6, fin_w, (size_t)PP * OC * D, 0);
-    add_gemm(g);
+    add_token_gemm(g);
   }
+  if (pl.alloc_failed) { set_error("workspace allocation failed"); return DM_ERR_HIP; }
   const int oc = OC;
   pl.add("unpatchify", 0, 8.0 * M * PP * OC,
          [=](hipStream_t st) { return unpatchify(lin, B, oc, S, S, p, P_->out, st); });
