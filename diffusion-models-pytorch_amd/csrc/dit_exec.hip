@@ -367,13 +367,21 @@ int DiTModel::build_plan(int B) {
       g.ln_stats = stats; g.ln_shift = mb + 3 * D; g.ln_scale = mb + 4 * D; g.ln_pitch = ada_total; g.ln_rows = T;
       g.act = 2;
       split(g, 6, bp.fc1_w, (size_t)Hm * D, 0);
-      add_token_gemm(g);
-    }
-    {
-      GemmArgs g = linear(hb, Hm, M, bp.fc2_w, bp.fc2_b, D, Hm, x, D);
-      g.res = x; g.ld_res = D; g.gate = mb + 5 * D; g.gate_pitch = ada_total; g.gate_rows = T;
-      split(g, 6, bp.fc2_w, (size_t)D * Hm, 0);
-      add_token_gemm(g);
+      GemmArgs g2 = linear(hb, Hm, M, bp.fc2_w, bp.fc2_b, D, Hm, x, D);
+      g2.res = x; g2.ld_res = D; g2.gate = mb + 5 * D; g2.gate_pitch = ada_total; g2.gate_rows = T;
+      split(g2, 6, bp.fc2_w, (size_t)D * Hm, 0);
+      // fc1's epilogue writes GELU(h) as fc2's pre-split A image (over hb: same bytes), no split pass for fc2
+      GemmArgs g1s = g, g2s = g2;
+      g1s.c_split = reinterpret_cast<_Float16*>(hb);
+      g1s.c_split_ea = g2.split_ea;
+      g2s.as = reinterpret_cast<const _Float16*>(hb);
+      if (presplit_on && g.ws && g2.ws && linear_k32_ok(g1s) && linear_k32_ok(g2s)) {
+        add_token_gemm(g1s);
+        add_gemm(g2s);
+      } else {
+        add_token_gemm(g);
+        add_token_gemm(g2);
+      }
     }
   }
   // --- final layer (dit/model.py:138-142) + unpatchify

@@ -160,6 +160,10 @@ struct GemmArgs {
   // rows, [M][K / 32][piece][4 k-groups][8] fp16); the kernel then stages it into LDS without conversion
   // (pro_scale / ln_stats must be null: they are applied by the pre-split pass)
   const _Float16* as;
+  // linear_k32 only: the output (after bias / residual / activation) as the next GEMM's pre-split A image
+  // ([M][N / 32][piece][4][8] fp16 of out * 2^c_split_ea, as linear_presplit_a writes it) instead of C
+  _Float16* c_split;
+  int c_split_ea;
   // linear_k32 only: the attention operand planes instead of C (as ConvArgs::ap_*, the qkv projection
   // feeding attn_presplit_kernel)
   _Float16 *ap_q, *ap_k, *ap_v;

@@ -500,7 +500,25 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
         if (g.act == 1) v[e] = silu_f(v[e]);
         else if (g.act == 2) v[e] = gelu_tanh_f(v[e]);
       }
-      if (m < M && c_ok) *reinterpret_cast<f4*>(g.C + (size_t)m * g.ldc + ncol) = v;
+      if (g.c_split) {  // linear_presplit_a's expressions (alpha 1), 4 columns = half a k-group
+        const float cp = ldexpf(1.f, g.c_split_ea);
+        f16x4 h0, h1;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float y = v[e] * cp;
+          const _Float16 a0 = (_Float16)y;
+          h0[e] = a0;
+          h1[e] = (_Float16)(y - (float)a0);
+          bad |= fabsf(y) > 65504.f;
+        }
+        if (m < M && c_ok) {
+          _Float16* d = g.c_split + (size_t)m * 2 * N + (ncol >> 5) * 64 + (ncol & 31);
+          *reinterpret_cast<f16x4*>(d) = h0;
+          *reinterpret_cast<f16x4*>(d + 32) = h1;
+        }
+      } else if (m < M && c_ok) {
+        *reinterpret_cast<f4*>(g.C + (size_t)m * g.ldc + ncol) = v;
+      }
     }
     __builtin_amdgcn_wave_barrier();  // the next slab reuses the region
   }
@@ -531,6 +549,7 @@ bool linear_k32_ok(const GemmArgs& g) {
   if (g.ln_stats && (g.ln_rows < kLBM || g.ln_pitch % 4 != 0 || !al16(g.ln_scale) || !al16(g.ln_shift))) return false;
   if (g.pro_scale && g.ln_stats) return false;
   if (g.as && (g.pro_scale || g.ln_stats || (reinterpret_cast<uintptr_t>(g.as) & 15) != 0)) return false;
+  if (g.c_split && (g.N % 64 != 0 || g.ap_q || (reinterpret_cast<uintptr_t>(g.c_split) & 15) != 0)) return false;
   return true;
 }
 
