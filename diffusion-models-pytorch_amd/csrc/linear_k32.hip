@@ -210,7 +210,8 @@ __device__ __forceinline__ void plane_block(const GemmArgs& g, const float* tile
 // linear_presplit_a: one thread per 8 consecutive channels (one k-group of one K = 32 step) of a row:
 // the linear_k32 prologue's expressions (finish_a), the split, piece 0 at [m][kk][0][kg], piece 1 at [m][kk][1][kg].
 template <int PRO>
-__global__ void __launch_bounds__(256) presplit_a_kernel(GemmArgs g, _Float16* out) {
+__global__ void __launch_bounds__(256) presplit_a_kernel(GemmArgs g, void* out_) {  // (void*: a demangled name)
+  _Float16* out = reinterpret_cast<_Float16*>(out_);
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   const int per_row = g.K / 8;
   if (i >= (long)g.M * per_row) return;
@@ -560,11 +561,11 @@ int linear_presplit_a(const GemmArgs& g, _Float16* out, hipStream_t st) {
   const long n = (long)g.M * (g.K / 8);
   const int blocks = (int)((n + 255) / 256);
   if (g.pro_scale)
-    hipLaunchKernelGGL(presplit_a_kernel<1>, dim3(blocks), dim3(256), 0, st, g, out);
+    hipLaunchKernelGGL(presplit_a_kernel<1>, dim3(blocks), dim3(256), 0, st, g, (void*)out);
   else if (g.ln_stats)
-    hipLaunchKernelGGL(presplit_a_kernel<2>, dim3(blocks), dim3(256), 0, st, g, out);
+    hipLaunchKernelGGL(presplit_a_kernel<2>, dim3(blocks), dim3(256), 0, st, g, (void*)out);
   else
-    hipLaunchKernelGGL(presplit_a_kernel<0>, dim3(blocks), dim3(256), 0, st, g, out);
+    hipLaunchKernelGGL(presplit_a_kernel<0>, dim3(blocks), dim3(256), 0, st, g, (void*)out);
   DM_LAUNCH_CHECK();
   return DM_OK;
 }
