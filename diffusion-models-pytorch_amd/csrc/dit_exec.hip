@@ -227,6 +227,15 @@ int DiTModel::build_plan(int B) {
   const bool presplit_on = !(std::getenv("DM_DIT_PRESPLIT") && std::getenv("DM_DIT_PRESPLIT")[0] == '0');
   _Float16* as_buf = nullptr;
   size_t as_bytes = 0;
+  // LayerNorm statistics for the next GEMM with the LN + modulate prologue: computed by that GEMM's
+  // row_stats_split pass (statistics + prologue + split in one read of the tokens) or by row_stats
+  bool stats_pending = false;
+  const float ln_eps = 1e-6f;
+  auto flush_stats = [&]() {
+    if (!stats_pending) return;
+    stats_pending = false;
+    pl.add("row_stats", 0, 4.0 * M * D, [=](hipStream_t st) { return row_stats(x, M, D, ln_eps, stats, st); });
+  };
   auto add_token_gemm = [&](GemmArgs g) {
     if (g.ws && presplit_on && g.M >= 4096) {
       const size_t need = (size_t)g.M * g.K * 4;
@@ -240,11 +249,22 @@ int DiTModel::build_plan(int B) {
       g2.ln_stats = nullptr;
       if (as_buf && linear_k32_ok(g2)) {
         _Float16* buf = as_buf;
-        pl.add("linear_presplit_a", 0, 8.0 * g.M * g.K, [=](hipStream_t st) { return linear_presplit_a(g, buf, st); });
+        if (g.ln_stats && stats_pending && g.A == x && g.lda == D && g.K == D && g.alpha == 1.0f) {
+          stats_pending = false;
+          float2* sp = stats;
+          pl.add("row_stats_split", 0, 8.0 * g.M * g.K, [=](hipStream_t st) {
+            return row_stats_split(g.A, g.M, g.K, ln_eps, sp, g.ln_shift, g.ln_scale, g.ln_pitch, g.ln_rows, g.split_ea,
+                                   buf, g.range_flag, st);
+          });
+        } else {
+          flush_stats();
+          pl.add("linear_presplit_a", 0, 8.0 * g.M * g.K, [=](hipStream_t st) { return linear_presplit_a(g, buf, st); });
+        }
         add_gemm(g2);
         return;
       }
     }
+    flush_stats();
     add_gemm(g);
   };
   // fp16x2 operand exponents (unet_exec.hip split_gemm): weights by max |w|, activations fixed (2^6 for
@@ -317,10 +337,7 @@ int DiTModel::build_plan(int B) {
     add_gemm(g);
   }
 
-  const float eps = 1e-6f;
-  auto stats_op = [&]() {
-    pl.add("row_stats", 0, 4.0 * M * D, [=](hipStream_t st) { return row_stats(x, M, D, eps, stats, st); });
-  };
+  auto stats_op = [&]() { stats_pending = true; };
   for (int b = 0; b < a.depth; ++b) {
     const BlockP bp = blocks[b];
     const float* mb = mods + (size_t)b * 6 * D;  // shift_msa, scale_msa, gate_msa, shift_mlp, scale_mlp, gate_mlp

@@ -217,6 +217,10 @@ int embed_add_silu(const float* temb, const int64_t* y, const float* table, int 
                    hipStream_t st, int null_row = -1);
 // LayerNorm statistics (no affine): stats[r] = (mean, 1 / sqrt(var + eps)) of each D-wide row
 int row_stats(const float* x, long rows, int D, float eps, float2* stats, hipStream_t st);
+// row_stats + LayerNorm + adaLN modulate + fp16x2 split of each row: the pre-split A image (GemmArgs::as)
+int row_stats_split(const float* x, long rows, int D, float eps, float2* stats, const float* ln_shift,
+                    const float* ln_scale, int ln_pitch, int ln_rows, int split_ea, _Float16* out, int* range_flag,
+                    hipStream_t st);
 // DiT patch embedding input: NCHW [B][C][H][W] -> rows [B * (H/p) * (W/p)][C * p * p] (Conv2d k = s = p order)
 int patchify(const float* x, int B, int C, int H, int W, int p, float* out, hipStream_t st);
 // DiT unpatchify (dit/model.py:219-232): rows [B * T][p * p * C] -> NCHW [B][C][H][W]
