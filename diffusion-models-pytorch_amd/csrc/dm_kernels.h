@@ -203,6 +203,9 @@ struct StepArgs {
 
 int gn_num_chunks(int HW);
 int gn_partial(const View& x, int G, double2* part, hipStream_t st);
+// partials of a concat [h (Ch) | skip (Cs)] from the slices' own G-group partials (group-aligned slices)
+int gn_concat_stats(const double2* ph, int Ch, const double2* ps, int Cs, int B, int HW, int G, double2* out,
+                    hipStream_t st);
 int gn_finalize(const View& x, int G, const double2* part, float eps, const float* gamma, const float* beta,
                 float* scale, float* shift, hipStream_t st, const float* mod_scale = nullptr,
                 const float* mod_shift = nullptr, int mod_pitch = 0);

@@ -185,7 +185,41 @@ inline int gn_block_threads(int C) {
 
 }  // namespace
 
+// GroupNorm partials of a channel concat [h | skip] from its two slices' partials (each emitted with G
+// groups over its own channels by its producer): concat group j is r consecutive groups of one slice
+// (the slices are group-aligned: the caller checks it). Replaces a gn_partial pass over the concat.
+__global__ void gn_concat_stats_kernel(const double2* __restrict__ ph, const double2* __restrict__ ps, long n, int G,
+                                       int jh, int rh, int rs, double2* __restrict__ out) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const long bk = i / G;  // (image, chunk)
+  const int j = (int)(i - bk * G);
+  const double2* src = j < jh ? ph + bk * G + (size_t)j * rh : ps + bk * G + (size_t)(j - jh) * rs;
+  const int r = j < jh ? rh : rs;
+  double s1 = 0.0, s2 = 0.0;
+  for (int u = 0; u < r; ++u) {
+    const double2 v = src[u];
+    s1 += v.x;
+    s2 += v.y;
+  }
+  out[i] = make_double2(s1, s2);
+}
+
 int gn_num_chunks(int HW) { return ceil_div(HW, kGnPixPerChunk); }
+
+int gn_concat_stats(const double2* ph, int Ch, const double2* ps, int Cs, int B, int HW, int G, double2* out,
+                    hipStream_t st) {
+  const int C = Ch + Cs;
+  DM_REQUIRE(C % G == 0 && Ch % G == 0 && Cs % G == 0 && (C / G) % (Ch / G) == 0 && (C / G) % (Cs / G) == 0 &&
+                 Ch % (C / G) == 0,
+             "gn_concat_stats: the slices' groups must tile the concat's groups");
+  const int cpg = C / G;
+  const long n = (long)B * gn_num_chunks(HW) * G;
+  hipLaunchKernelGGL(gn_concat_stats_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, ph, ps, n, G,
+                     Ch / cpg, cpg / (Ch / G), cpg / (Cs / G), out);
+  DM_LAUNCH_CHECK();
+  return DM_OK;
+}
 
 int gn_partial(const View& x, int G, double2* part, hipStream_t st) {
   DM_REQUIRE(x.C % 4 == 0 && x.pitch % 4 == 0, "GroupNorm needs C and pitch multiple of 4");

@@ -802,6 +802,26 @@ int UNetModel::build_plan(int B, int H, int W) {
     add("gn_partial", 0, gn_bytes(v, false), [=](hipStream_t st) { return gn_partial(v, G, part, st); });
     return part;
   };
+  // the concat input [h | skip] of an up-path ResBlock: when both slices' producers emitted their statistics
+  // and the concat's groups do not straddle the slices (512 = 256 + 256, 256 = 128 + 128: all but the
+  // 384-channel concats of the CIFAR UNet), combine the slices' partials instead of a gn_partial pass
+  auto gn_stats_concat = [&](const View& v, const View& sk) -> const double2* {
+    const int Ch = v.C - sk.C;
+    auto ih = gn_ready.find(v.p), is = gn_ready.find(sk.p);
+    const bool aligned = v.C % G == 0 && Ch > 0 && Ch % G == 0 && sk.C % G == 0 && (v.C / G) % (Ch / G) == 0 &&
+                         (v.C / G) % (sk.C / G) == 0 && Ch % (v.C / G) == 0;
+    if (aligned && !std::getenv("DM_GN_NO_CONCAT") && ih != gn_ready.end() && ih->second.second == Ch &&
+        is != gn_ready.end() && is->second.second == sk.C) {
+      const double2* ph = ih->second.first;
+      const double2* ps = is->second.first;
+      const int Cs = sk.C, HW = v.H * v.W;
+      add("gn_concat_stats", 0, 32.0 * B * gn_num_chunks(HW) * G, [=](hipStream_t st) {
+        return gn_concat_stats(ph, Ch, ps, Cs, B, HW, G, part, st);
+      });
+      return part;
+    }
+    return gn_stats(v);
+  };
   // GroupNorm(G) of v feeding conv c's prologue (tables gsc / gsh): either the conv finalizes the
   // statistics itself into its LDS tables (conv_lds_tables: no gn_finalize launch) or gn_finalize runs.
   auto gn_prologue = [&](ConvArgs& c, const View& v, const double2* stp, size_t gamma, size_t beta,
@@ -899,7 +919,7 @@ int UNetModel::build_plan(int B, int H, int W) {
       const float* ms = r.adagn ? projs + r.proj_col : nullptr;
       const float* mb = r.adagn ? projs + r.proj_col + r.cout : nullptr;
       const int mp = r.adagn ? proj_total : 0;
-      const double2* st1 = gn_stats(xin);
+      const double2* st1 = n.pops_skip >= 0 ? gn_stats_concat(xin, skip_view[n.pops_skip]) : gn_stats(xin);
       if (r.updown && !fuse1) {
         // normalise + SiLU + resample into a1, then a plain conv at the output resolution
         add("gn_finalize", 0, 8.0 * B * r.cin, [=](hipStream_t st) {
