@@ -17,6 +17,11 @@ extern "C" int dm_abi_version(void) { return DM_ABI_VERSION; }
 
 extern "C" const char* dm_last_error(void) { return dm::last_error(); }
 
+#ifndef DM_SRC_HASH
+#define DM_SRC_HASH "unknown"
+#endif
+extern "C" const char* dm_build_info(void) { return "src=" DM_SRC_HASH " arch=gfx950"; }
+
 extern "C" int dm_sampler_step(const dm_step_desc* d, void* stream) {
   if (!d) { dm::set_error("null step descriptor"); return DM_ERR_ARG; }
   dm::StepArgs s{};
@@ -40,6 +45,14 @@ extern "C" int dm_sampler_step(const dm_step_desc* d, void* stream) {
   if (s.kind < 0 || s.kind > 1) { dm::set_error("invalid sampler kind"); return DM_ERR_ARG; }
   if (s.B < 0 || s.C <= 0 || s.HW <= 0) { dm::set_error("invalid shape"); return DM_ERR_ARG; }
   return dm::sampler_step(s, (hipStream_t)stream);
+}
+
+extern "C" int dm_lincomb(int mode, const float* a, const float* b, float* out, int64_t n, int64_t row_elems,
+                          const float* c1_rows, const float* c2_rows, float c1, float c2, void* stream) {
+  if (!a || !b || !out) { dm::set_error("null tensor"); return DM_ERR_ARG; }
+  if (mode < 0 || mode > 2) { dm::set_error("lincomb mode must be 0, 1 or 2"); return DM_ERR_ARG; }
+  if (n < 0 || row_elems <= 0) { dm::set_error("invalid shape"); return DM_ERR_ARG; }
+  return dm::lincomb(mode, a, b, out, (long)n, (long)row_elems, c1_rows, c2_rows, c1, c2, (hipStream_t)stream);
 }
 
 extern "C" int64_t dm_groupnorm_scratch_bytes(int B, int HW, int G) {

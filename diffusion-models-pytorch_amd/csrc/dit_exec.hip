@@ -79,17 +79,21 @@ struct DiTModel {
     int64_t* y = nullptr;  // -1 rows select the null class
     float* out = nullptr;
   };
-  std::unique_ptr<Plan> plan;
+  PlanCache<Plan> plans;  // LRU over B, scratch from one pool
+  size_t split_bytes = 0;  // device bytes of the split_w copies
 
   float* P(size_t off) const { return arena + off; }
   ~DiTModel() {
-    plan.reset();
+    plans.clear();
     for (auto& kv : split_w) (void)hipFree(kv.second);
     if (range_flag) (void)hipFree(range_flag);
     if (range_flag_host) (void)hipHostFree(range_flag_host);
     if (arena) (void)hipFree(arena);
   }
-  int build_plan(int B);
+  int build_plan(Plan& pl, int B);
+  int get_plan(int B, Plan** out) {
+    return plans.get([&](const Plan& p) { return p.B == B; }, [&](Plan& p) { return build_plan(p, B); }, out);
+  }
 };
 
 static int dit_create(const dm_dit_arch* arch, const float* const* params, const int64_t* numels, int n_params,
@@ -177,10 +181,7 @@ static int dit_create(const dm_dit_arch* arch, const float* const* params, const
   return DM_OK;
 }
 
-int DiTModel::build_plan(int B) {
-  plan.reset();
-  plan = std::make_unique<Plan>();
-  Plan& pl = *plan;
+int DiTModel::build_plan(Plan& pl, int B) {
   pl.B = B;
   const dm_dit_arch& a = arch;
   const int p = a.patch_size, C = a.in_channels, S = a.input_size, Hm = a.mlp_hidden;
@@ -237,7 +238,9 @@ int DiTModel::build_plan(int B) {
     pl.add("row_stats", 0, 4.0 * M * D, [=](hipStream_t st) { return row_stats(x, M, D, ln_eps, stats, st); });
   };
   auto add_token_gemm = [&](GemmArgs g) {
-    if (g.ws && presplit_on && g.M >= 4096) {
+    // nominal-batch decision (pick_M = T * kPickBatch): the same kernels at every B, so results are
+    // batch-invariant (each image's row block of B * T tokens runs the same code)
+    if (g.ws && presplit_on && g.pick_M >= 4096) {
       const size_t need = (size_t)g.M * g.K * 4;
       if (need > as_bytes) {
         as_buf = reinterpret_cast<_Float16*>(pl.alloc(need));
@@ -291,6 +294,7 @@ int DiTModel::build_plan(int B) {
           return;
         }
         it = split_w.emplace(wp, buf).first;
+        split_bytes += nb;
       }
       g.ws = it->second;
       g.ws_rowscale = split_conv_rowscale(it->second, 1, g.N, g.K);
@@ -454,15 +458,11 @@ extern "C" int dm_dit_forward(dm_dit* h, const float* x, const int64_t* t, const
     return DM_ERR_ARG;
   }
   dm::DiTModel* m = h->m;
-  if (!m->plan || m->plan->B != B) {
-    int rc = m->build_plan(B);
-    if (rc) {
-      m->plan.reset();
-      return rc;
-    }
-  }
+  dm::DiTModel::Plan* plp = nullptr;
+  const int rc0 = m->get_plan(B, &plp);
+  if (rc0) return rc0;
   hipStream_t st = (hipStream_t)stream;
-  auto& pl = *m->plan;
+  auto& pl = *plp;
   const int S = m->arch.input_size;
   const size_t nx = (size_t)B * m->arch.in_channels * S * S, no = (size_t)B * m->OC * S * S;
   DM_CHECK_HIP(hipMemcpyAsync(pl.x, x, nx * sizeof(float), hipMemcpyDeviceToDevice, st));
@@ -480,7 +480,7 @@ extern "C" int dm_dit_forward(dm_dit* h, const float* x, const int64_t* t, const
     if (*m->range_flag_host) {  // an fp16x2 GEMM met an operand beyond the fp16 range: fp32 from here on
       DM_CHECK_HIP(hipMemsetAsync(m->range_flag, 0, sizeof(int), st));
       m->math = 0;
-      m->plan.reset();
+      m->plans.clear();
       return dm_dit_forward(h, x, t, y, B, out, stream);
     }
   }
@@ -506,7 +506,7 @@ extern "C" int dm_dit_range_poll(dm_dit* h, void* stream, int* flagged) {
     *flagged = 1;
     if (m->math == 2) {
       m->math = 0;
-      m->plan.reset();
+      m->plans.clear();
     }
   }
   return DM_OK;
@@ -517,7 +517,7 @@ extern "C" int dm_dit_set_math(dm_dit* h, int kind) {
   if (kind != 0 && kind != DM_SPLIT_FP16X2) { dm::set_error("DiT math must be 0 (fp32) or DM_SPLIT_FP16X2"); return DM_ERR_ARG; }
   if (kind != h->m->math) {
     h->m->math = kind;
-    h->m->plan.reset();
+    h->m->plans.clear();
   }
   return DM_OK;
 }
@@ -532,40 +532,48 @@ extern "C" int dm_dit_set_time_freqs(dm_dit* h, const float* freqs, int n, void*
   if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
   if (!freqs) {
     h->m->freqs_set = false;
-    if (h->m->plan) h->m->plan->invalidate_graph();
+    h->m->plans.invalidate_graphs();
     return DM_OK;
   }
   if (n != 128) { dm::set_error("time frequency table must have 128 entries"); return DM_ERR_ARG; }
   DM_CHECK_HIP(hipMemcpyAsync(h->m->P(h->m->freqs), freqs, 128 * sizeof(float), hipMemcpyDefault,
                               (hipStream_t)stream));
   h->m->freqs_set = true;
-  if (h->m->plan) h->m->plan->invalidate_graph();
+  h->m->plans.invalidate_graphs();
   return DM_OK;
 }
 
 extern "C" int dm_dit_profile(dm_dit* h, int enable) {
   if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
-  if (!h->m->plan) { dm::set_error("no plan yet: run dm_dit_forward once first"); return DM_ERR_STATE; }
-  h->m->plan->profile_enable(enable);
+  if (!h->m->plans.current()) { dm::set_error("no plan yet: run dm_dit_forward once first"); return DM_ERR_STATE; }
+  h->m->plans.current()->profile_enable(enable);
   return DM_OK;
 }
 
 extern "C" int dm_dit_profile_count(dm_dit* h, int* n_ops) {
-  if (!h || !h->m || !h->m->plan || !n_ops) { dm::set_error("null model / no plan"); return DM_ERR_STATE; }
-  *n_ops = (int)h->m->plan->ops.size();
+  if (!h || !h->m || !h->m->plans.current() || !n_ops) { dm::set_error("null model / no plan"); return DM_ERR_STATE; }
+  *n_ops = (int)h->m->plans.current()->ops.size();
   return DM_OK;
 }
 
 extern "C" int dm_dit_profile_get(dm_dit* h, int i, char* label, int label_len, double* flops, double* bytes,
                                   double* ms_total, int64_t* launches) {
-  if (!h || !h->m || !h->m->plan) { dm::set_error("null model / no plan"); return DM_ERR_STATE; }
-  return h->m->plan->profile_get(i, label, label_len, flops, bytes, ms_total, launches);
+  if (!h || !h->m || !h->m->plans.current()) { dm::set_error("null model / no plan"); return DM_ERR_STATE; }
+  return h->m->plans.current()->profile_get(i, label, label_len, flops, bytes, ms_total, launches);
 }
 
 extern "C" int dm_dit_memory(const dm_dit* h, int64_t* weight_bytes, int64_t* workspace_bytes) {
   if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
-  if (weight_bytes) *weight_bytes = (int64_t)(h->m->arena_floats * sizeof(float));
-  if (workspace_bytes) *workspace_bytes = h->m->plan ? (int64_t)h->m->plan->bytes : 0;
+  // the fp32 arena plus the pre-split fp16x2 copies of the token-GEMM weights (as dm_unet_memory counts them)
+  if (weight_bytes) *weight_bytes = (int64_t)(h->m->arena_floats * sizeof(float) + h->m->split_bytes);
+  if (workspace_bytes) *workspace_bytes = (int64_t)h->m->plans.pool->bytes;
+  return DM_OK;
+}
+
+extern "C" int dm_dit_plan_stats(const dm_dit* h, int64_t* builds, int* cached) {
+  if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
+  if (builds) *builds = h->m->plans.builds;
+  if (cached) *cached = (int)h->m->plans.plans.size();
   return DM_OK;
 }
 

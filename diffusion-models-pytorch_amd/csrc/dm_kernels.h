@@ -317,6 +317,9 @@ int small_out_pack(const float* w, int Cout, int Cin, float* wp, hipStream_t st)
 int conv3x3_small_out(const View& x, const float* wp, const float* bias, int Cout, float* y, hipStream_t st,
                       const float* pro_scale = nullptr, const float* pro_shift = nullptr);
 int sampler_step(const StepArgs& s, hipStream_t st);
+// out = c1 a + c2 b (mode 0), c1 a - c2 b (1), (c1 a - b) / c2 (2); per-row coefficients when c*_rows given
+int lincomb(int mode, const float* a, const float* b, float* out, long n, long row_elems, const float* c1_rows,
+            const float* c2_rows, float c1, float c2, hipStream_t st);
 int nchw_to_nhwc(const float* x, int B, int C, int HW, float* y, int y_pitch, hipStream_t st);
 int nhwc_to_nchw(const float* x, int B, int C, int HW, int pitch, float* y, hipStream_t st);
 int repack_conv(const float* w, int Cout, int Cin, int taps, float* out, int ldw, int col0, hipStream_t st);

@@ -325,6 +325,31 @@ __global__ void sampler_step_kernel(StepArgs s) {
   if (s.var_out) s.var_out[e] = var;
 }
 
+// Two-operand combination with scalar or per-row coefficients, each product and the final add / sub / div
+// separately rounded (-ffp-contract=off), i.e. the torch float32 expressions of reference ddpm.py:
+//   mode 0: c1 a + c2 b        diffuse (:164-172), pred_eps_from_v (:117-120)
+//   mode 1: c1 a - c2 b        pred_x0_from_eps (:102-105), pred_x0_from_v (:112-115), get_v (:140-150)
+//   mode 2: (c1 a - b) / c2    pred_eps_from_x0 (:107-110)
+// Row r = e / row_elems selects c1_rows[r] / c2_rows[r] when given (per-image timesteps).
+__global__ void lincomb_kernel(int mode, const float* __restrict__ a, const float* __restrict__ b,
+                               float* __restrict__ out, long n, long row_elems, const float* __restrict__ c1r,
+                               const float* __restrict__ c2r, float c1, float c2) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const long r = e / row_elems;
+  const float k1 = c1r ? c1r[r] : c1, k2 = c2r ? c2r[r] : c2;
+  const float pa = k1 * a[e];
+  float v;
+  if (mode == 0) {
+    v = pa + k2 * b[e];
+  } else if (mode == 1) {
+    v = pa - k2 * b[e];
+  } else {
+    v = (pa - b[e]) / k2;
+  }
+  out[e] = v;
+}
+
 // avg-pool 2x2 / nearest-2x on NHWC views, float4 over channels, optional
 // GroupNorm+SiLU prologue applied to each source pixel before pooling.
 __global__ void resample2x_kernel(View x, View y, int down, const float* __restrict__ pro_scale,
@@ -522,6 +547,17 @@ int sampler_step(const StepArgs& s, hipStream_t st) {
   const long total = (long)s.B * s.C * s.HW;
   if (total == 0) return DM_OK;
   hipLaunchKernelGGL(sampler_step_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, s);
+  DM_LAUNCH_CHECK();
+  return DM_OK;
+}
+
+int lincomb(int mode, const float* a, const float* b, float* out, long n, long row_elems, const float* c1_rows,
+            const float* c2_rows, float c1, float c2, hipStream_t st) {
+  DM_REQUIRE(mode >= 0 && mode <= 2, "lincomb: mode must be 0, 1 or 2");
+  DM_REQUIRE(a && b && out && n >= 0 && row_elems > 0, "lincomb: null tensor or bad shape");
+  if (n == 0) return DM_OK;
+  hipLaunchKernelGGL(lincomb_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, mode, a, b, out, n,
+                     row_elems, c1_rows, c2_rows, c1, c2);
   DM_LAUNCH_CHECK();
   return DM_OK;
 }

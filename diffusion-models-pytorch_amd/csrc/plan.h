@@ -1,16 +1,28 @@
 // Launch plan shared by the native denoiser executors (UNet, DiT).
 //
 // A plan is the flat list of kernel launches of one forward pass for a fixed
-// batch / resolution, built once over a cached workspace and replayed on every
-// call. Every pointer a launch reads is plan-owned (the caller's input and
-// output are staged through plan buffers), so the whole list is captured once
-// into a hipGraph and replayed with one hipGraphLaunch per forward. Profiling
-// records a HIP event pair around each launch on the launch stream (on the
-// observed forwards, which run launch by launch); the per-op totals are read
-// back through the dm_*_profile_* ABI.
+// batch / resolution, built once and replayed on every call. Every pointer a
+// launch reads is plan-owned scratch (the caller's input and output are staged
+// through plan buffers), so the whole list is captured once into a hipGraph and
+// replayed with one hipGraphLaunch per forward. Profiling records a HIP event
+// pair around each launch on the launch stream (on the observed forwards, which
+// run launch by launch); the per-op totals are read back through the
+// dm_*_profile_* ABI.
+//
+// Scratch: a plan does not own device memory. Its builder runs twice: once
+// measuring (alloc hands out placeholder addresses that are never
+// dereferenced, the op list is discarded), then over a ScratchPool slab sized
+// to the measured need. Every plan of a model -- a small LRU cache keyed by
+// the forward's shape -- and of the models that share the pool
+// (dm_unet_share_workspace: UNetCombined's two networks) uses the same slab,
+// since their forwards run one after the other on one stream. A slab that has
+// to grow is reallocated; plans built over the old one are stale (generation)
+// and rebuilt on their next use.
 #include <cstdlib>
 #pragma once
+#include <cstdint>
 #include <functional>
+#include <memory>
 #include <string>
 #include <utility>
 #include <vector>
@@ -26,10 +38,47 @@ struct Op {
   std::function<int(hipStream_t)> fn;
 };
 
-struct PlanBase {
-  std::vector<void*> allocs;
+// One device slab of plan scratch, shared by every plan that runs over it (see above).
+struct ScratchPool {
+  char* base = nullptr;
   size_t bytes = 0;
-  bool alloc_failed = false;
+  uint64_t gen = 0;  // bumped whenever the slab is (re)allocated
+  ScratchPool() = default;
+  ScratchPool(const ScratchPool&) = delete;
+  ScratchPool& operator=(const ScratchPool&) = delete;
+  ~ScratchPool() {
+    if (base) {
+      (void)hipDeviceSynchronize();
+      (void)hipFree(base);
+    }
+  }
+  int ensure(size_t need) {
+    if (base && need <= bytes) return DM_OK;
+    if (base) {
+      (void)hipDeviceSynchronize();  // launches still reading the old slab finish first
+      (void)hipFree(base);
+      base = nullptr;
+      bytes = 0;
+    }
+    ++gen;
+    void* p = nullptr;
+    if (hipMalloc(&p, need ? need : 256) != hipSuccess) {
+      (void)hipGetLastError();
+      set_error("plan scratch allocation of " + std::to_string(need >> 20) + " MiB failed");
+      return DM_ERR_HIP;
+    }
+    base = static_cast<char*>(p);
+    bytes = need;
+    return DM_OK;
+  }
+};
+
+struct PlanBase {
+  size_t bytes = 0;          // scratch this plan uses (offset of the bump allocator)
+  bool alloc_failed = false;  // kept for the builders' checks; never set (the slab is sized beforehand)
+  bool measuring = false;     // first builder pass: placeholder addresses, ops discarded
+  char* scratch = nullptr;    // slab base of the real pass
+  uint64_t gen = 0;           // ScratchPool generation the plan was built over
   std::vector<Op> ops;
   bool profiling = false;
   int profile_every = 1;  // record events on every N-th run only (the others run unobserved)
@@ -45,17 +94,15 @@ struct PlanBase {
   PlanBase() = default;
   PlanBase(const PlanBase&) = delete;
   PlanBase& operator=(const PlanBase&) = delete;
-  ~PlanBase() { release(); }
+  virtual ~PlanBase() { release(); }
 
+  // Bump allocation (256-B aligned) from the slab; while measuring, distinct placeholder addresses that
+  // no host code dereferences (the builders write nothing into plan scratch at build time).
   float* alloc(size_t nbytes) {
-    void* p = nullptr;
-    if (hipMalloc(&p, nbytes ? nbytes : 16) != hipSuccess) {
-      alloc_failed = true;
-      return nullptr;
-    }
-    allocs.push_back(p);
-    bytes += nbytes;
-    return static_cast<float*>(p);
+    const size_t sz = ((nbytes ? nbytes : 1) + 255) & ~size_t(255);
+    char* p = (measuring ? reinterpret_cast<char*>(uintptr_t(1) << 40) : scratch) + bytes;
+    bytes += sz;
+    return reinterpret_cast<float*>(p);
   }
 
   void add(std::string label, double flops, double nbytes, std::function<int(hipStream_t)> fn) {
@@ -86,8 +133,6 @@ struct PlanBase {
     invalidate_graph();
     if (cap_stream) (void)hipStreamDestroy(cap_stream);
     cap_stream = nullptr;
-    for (void* a : allocs) (void)hipFree(a);
-    allocs.clear();
   }
 
   int capture() {
@@ -160,6 +205,68 @@ struct PlanBase {
     if (nbytes) *nbytes = ops[i].bytes;
     if (ms_total) *ms_total = prof_ms[i];
     if (launches) *launches = prof_launches[i];
+    return DM_OK;
+  }
+};
+
+
+// Small LRU of plans keyed by the forward's shape (match), all over one ScratchPool. Rebuilding a plan
+// costs a synchronous build + graph capture, so alternating shapes (sample_cfg's folds, a smaller last
+// fold, batched vs two-call CFG) reuse their plans instead of rebuilding on every switch.
+template <class P>
+struct PlanCache {
+  static constexpr size_t kMaxPlans = 3;
+  std::vector<std::unique_ptr<P>> plans;  // most recently used last
+  std::shared_ptr<ScratchPool> pool = std::make_shared<ScratchPool>();
+  long builds = 0;
+
+  P* current() const { return plans.empty() ? nullptr : plans.back().get(); }
+  void clear() { plans.clear(); }
+  void invalidate_graphs() {
+    for (auto& p : plans) p->invalidate_graph();
+  }
+  void share(const std::shared_ptr<ScratchPool>& other) {
+    plans.clear();
+    pool = other;
+  }
+  // The cached plan for which match(plan) holds, or a new one from build(plan) (called twice: measuring,
+  // then over the slab).
+  template <class Match, class Build>
+  int get(Match match, Build build, P** out) {
+    *out = nullptr;
+    for (size_t i = 0; i < plans.size(); ++i) {
+      if (!match(*plans[i])) continue;
+      std::unique_ptr<P> p = std::move(plans[i]);
+      plans.erase(plans.begin() + i);
+      if (p->gen == pool->gen) {
+        plans.push_back(std::move(p));
+        *out = plans.back().get();
+        return DM_OK;
+      }
+      break;  // built over a slab that has since been reallocated
+    }
+    auto m = std::make_unique<P>();
+    m->measuring = true;
+    int rc = build(*m);
+    if (rc) return rc;
+    const size_t need = m->bytes;
+    m.reset();
+    rc = pool->ensure(need);
+    if (rc) return rc;
+    auto p = std::make_unique<P>();
+    p->scratch = pool->base;
+    p->gen = pool->gen;
+    rc = build(*p);
+    if (rc) return rc;
+    DM_REQUIRE(p->bytes == need, "plan builder is not deterministic (scratch size changed)");
+    ++builds;
+    for (size_t i = 0; i < plans.size();) {  // stale plans (older slab) and the LRU overflow
+      if (plans[i]->gen != pool->gen) plans.erase(plans.begin() + i);
+      else ++i;
+    }
+    plans.push_back(std::move(p));
+    while (plans.size() > kMaxPlans) plans.erase(plans.begin());
+    *out = plans.back().get();
     return DM_OK;
   }
 };

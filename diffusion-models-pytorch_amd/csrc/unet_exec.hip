@@ -153,7 +153,7 @@ struct UNetModel {
   std::vector<int> skip_C, skip_level;  // per skip id
   int n_levels = 0;
 
-  // workspace cache
+  // plan cache (LRU over (B, H, W)), scratch from a pool shared with dm_unet_share_workspace peers
   struct Plan : PlanBase {
     int B = 0, H = 0, W = 0;
     // plan-owned staging of the caller's tensors (every launch reads fixed pointers: graph replay)
@@ -162,7 +162,8 @@ struct UNetModel {
     int64_t* y = nullptr;  // class labels; all -1 when the caller passes none
     float* out = nullptr;
   };
-  std::unique_ptr<Plan> plan;
+  PlanCache<Plan> plans;
+  float* last_packed = nullptr;  // last conv weights as [9][Cin][CO] (small_out_pack), made at the first build
   // Split copies of the halo-patch conv weights (conv_patch3.hip), made at the first plan build.
   // conv_math: 2 fp16x2 (default), 3 bf16x3, 0 fp32 MFMA kernels (DM_CONV_MATH=fp16x2|bf16x3|fp32).
   // fp16x2 convs raise range_flag on an activation beyond the fp16 range; the forward then
@@ -183,11 +184,16 @@ struct UNetModel {
 
   float* P(size_t off) const { return arena + off; }
   ~UNetModel();
-  int build_plan(int B, int H, int W);
+  int build_plan(Plan& pl, int B, int H, int W);
+  int get_plan(int B, int H, int W, Plan** out) {
+    return plans.get([&](const Plan& p) { return p.B == B && p.H == H && p.W == W; },
+                     [&](Plan& p) { return build_plan(p, B, H, W); }, out);
+  }
 };
 
 UNetModel::~UNetModel() {
-  plan.reset();
+  plans.clear();
+  if (last_packed) (void)hipFree(last_packed);
   for (auto& kv : split_w) (void)hipFree(kv.second);
   if (range_flag) (void)hipFree(range_flag);
   if (range_flag_host) (void)hipHostFree(range_flag_host);
@@ -585,10 +591,7 @@ static int unet_create(const dm_unet_arch* arch, const float* const* params, con
 // ---------------------------------------------------------------------------
 // plan (per batch size / resolution)
 // ---------------------------------------------------------------------------
-int UNetModel::build_plan(int B, int H, int W) {
-  plan.reset();
-  plan = std::make_unique<Plan>();
-  Plan& pl = *plan;
+int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
   pl.B = B;
   pl.H = H;
   pl.W = W;
@@ -1144,11 +1147,12 @@ int UNetModel::build_plan(int B, int H, int W) {
     });
     (void)va;
     (void)nchunk;
-    float* lwp = alloc((size_t)9 * C * 8 * sizeof(float));  // packed [9][C][CO] copy of the last conv weight
-    if (!lwp) return DM_ERR_HIP;
-    DM_REQUIRE(small_out_pack(lw, oc, C, lwp, nullptr) == DM_OK, "last conv: weight packing failed");
-    DM_CHECK_HIP(hipDeviceSynchronize());
-    lw = lwp;
+    if (!last_packed) {  // packed [9][C][CO] copy of the last conv weight (model-owned, built once)
+      DM_CHECK_HIP(hipMalloc(&last_packed, (size_t)9 * C * 8 * sizeof(float)));
+      DM_REQUIRE(small_out_pack(lw, oc, C, last_packed, nullptr) == DM_OK, "last conv: weight packing failed");
+      DM_CHECK_HIP(hipDeviceSynchronize());
+    }
+    lw = last_packed;
     add("conv3x3_small_out", 2.0 * B * H * W * oc * 9 * C, 4.0 * B * H * W * (C + oc),
         [=](hipStream_t st) { return conv3x3_small_out(xin, lw, lb, oc, P_->out, st, gsc, gsh); });
   }
@@ -1192,15 +1196,11 @@ extern "C" int dm_unet_forward(dm_unet* h, const float* x, const int64_t* t, con
     return DM_ERR_ARG;
   }
   dm::UNetModel* m = h->m;
-  if (!m->plan || m->plan->B != B || m->plan->H != H || m->plan->W != W) {
-    int rc = m->build_plan(B, H, W);
-    if (rc) {
-      m->plan.reset();
-      return rc;
-    }
-  }
+  dm::UNetModel::Plan* plp = nullptr;
+  int rc0 = m->get_plan(B, H, W, &plp);
+  if (rc0) return rc0;
   hipStream_t st = (hipStream_t)stream;
-  auto& pl = *m->plan;
+  auto& pl = *plp;
   const size_t nx = (size_t)B * m->arch.in_channels * H * W, no = (size_t)B * m->arch.out_channels * H * W;
   DM_CHECK_HIP(hipMemcpyAsync(pl.x, x, nx * sizeof(float), hipMemcpyDeviceToDevice, st));
   DM_CHECK_HIP(hipMemcpyAsync(pl.t, t, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
@@ -1218,7 +1218,7 @@ extern "C" int dm_unet_forward(dm_unet* h, const float* x, const int64_t* t, con
     if (*m->range_flag_host) {
       DM_CHECK_HIP(hipMemsetAsync(m->range_flag, 0, sizeof(int), st));
       m->conv_math = 3;
-      m->plan.reset();
+      m->plans.clear();
       return dm_unet_forward(h, x, t, y, B, H, W, out, stream);
     }
   }
@@ -1244,7 +1244,7 @@ extern "C" int dm_unet_range_poll(dm_unet* h, void* stream, int* flagged) {
     *flagged = 1;
     if (m->conv_math == 2) {  // continue in bf16x3; the caller re-runs what it computed since the last poll
       m->conv_math = 3;
-      m->plan.reset();
+      m->plans.clear();
     }
   }
   return DM_OK;
@@ -1253,7 +1253,20 @@ extern "C" int dm_unet_range_poll(dm_unet* h, void* stream, int* flagged) {
 extern "C" int dm_unet_memory(const dm_unet* h, int64_t* weight_bytes, int64_t* workspace_bytes) {
   if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
   if (weight_bytes) *weight_bytes = (int64_t)(h->m->arena_floats * sizeof(float) + h->m->split_bytes);
-  if (workspace_bytes) *workspace_bytes = h->m->plan ? (int64_t)h->m->plan->bytes : 0;
+  if (workspace_bytes) *workspace_bytes = (int64_t)h->m->plans.pool->bytes;
+  return DM_OK;
+}
+
+extern "C" int dm_unet_share_workspace(dm_unet* a, dm_unet* b) {
+  if (!a || !a->m || !b || !b->m) { dm::set_error("null model"); return DM_ERR_STATE; }
+  if (a->m->plans.pool != b->m->plans.pool) b->m->plans.share(a->m->plans.pool);
+  return DM_OK;
+}
+
+extern "C" int dm_unet_plan_stats(const dm_unet* h, int64_t* builds, int* cached) {
+  if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
+  if (builds) *builds = h->m->plans.builds;
+  if (cached) *cached = (int)h->m->plans.plans.size();
   return DM_OK;
 }
 
@@ -1265,7 +1278,7 @@ extern "C" int dm_unet_set_conv_math(dm_unet* h, int kind) {
   }
   if (kind != h->m->conv_math) {
     h->m->conv_math = kind;
-    h->m->plan.reset();
+    h->m->plans.clear();
   }
   return DM_OK;
 }
@@ -1280,34 +1293,34 @@ extern "C" int dm_unet_set_time_freqs(dm_unet* h, const float* freqs, int n, voi
   if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
   if (!freqs) {
     h->m->te_freqs_set = false;
-    if (h->m->plan) h->m->plan->invalidate_graph();
+    h->m->plans.invalidate_graphs();
     return DM_OK;
   }
   if (n != h->m->arch.dim / 2) { dm::set_error("time frequency table must have dim/2 entries"); return DM_ERR_ARG; }
   DM_CHECK_HIP(hipMemcpyAsync(h->m->P(h->m->te_freqs), freqs, (size_t)n * sizeof(float), hipMemcpyDefault,
                               (hipStream_t)stream));
   h->m->te_freqs_set = true;
-  if (h->m->plan) h->m->plan->invalidate_graph();  // launches read the flag at capture time
+  h->m->plans.invalidate_graphs();  // launches read the flag at capture time
   return DM_OK;
 }
 
 extern "C" int dm_unet_profile(dm_unet* h, int enable) {
   if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
-  if (!h->m->plan) { dm::set_error("no plan yet: run dm_unet_forward once first"); return DM_ERR_STATE; }
-  h->m->plan->profile_enable(enable);
+  if (!h->m->plans.current()) { dm::set_error("no plan yet: run dm_unet_forward once first"); return DM_ERR_STATE; }
+  h->m->plans.current()->profile_enable(enable);
   return DM_OK;
 }
 
 extern "C" int dm_unet_profile_count(dm_unet* h, int* n_ops) {
-  if (!h || !h->m || !h->m->plan || !n_ops) { dm::set_error("null model / no plan"); return DM_ERR_STATE; }
-  *n_ops = (int)h->m->plan->ops.size();
+  if (!h || !h->m || !h->m->plans.current() || !n_ops) { dm::set_error("null model / no plan"); return DM_ERR_STATE; }
+  *n_ops = (int)h->m->plans.current()->ops.size();
   return DM_OK;
 }
 
 extern "C" int dm_unet_profile_get(dm_unet* h, int i, char* label, int label_len, double* flops, double* bytes,
                                    double* ms_total, int64_t* launches) {
-  if (!h || !h->m || !h->m->plan) { dm::set_error("null model / no plan"); return DM_ERR_STATE; }
-  return h->m->plan->profile_get(i, label, label_len, flops, bytes, ms_total, launches);
+  if (!h || !h->m || !h->m->plans.current()) { dm::set_error("null model / no plan"); return DM_ERR_STATE; }
+  return h->m->plans.current()->profile_get(i, label, label_len, flops, bytes, ms_total, launches);
 }
 
 extern "C" void dm_unet_destroy(dm_unet* h) {

@@ -148,6 +148,49 @@ class DDPM:
             self._coef_cache[key] = c
         return c
 
+    # ------------------------------------------------ closed-form conversions
+    # Reference ddpm.py:102-120, 140-172. The coefficients are the reference's torch CPU expressions
+    # (0-dim for an int t, [B] vectors for per-image timesteps), the elementwise arithmetic one
+    # dm_lincomb launch with separately rounded float32 products (bit-identical to the CPU expression).
+    def _row_coefs(self, t, x: Tensor):
+        """sqrt(ac_t), sqrt(1 - ac_t) for t: an int / 0-dim tensor (scalars) or [B] timesteps (one per image)."""
+        if isinstance(t, Tensor) and t.ndim >= 1:
+            tc = t.detach().to('cpu', torch.long).reshape(-1)
+            if tc.numel() != x.shape[0]:
+                raise ValueError(f't must hold one timestep per image ({x.shape[0]}), got {tc.numel()}')
+            a = self._ac_cpu[tc]
+            return (a ** 0.5).to(x.device), ((1. - a) ** 0.5).to(x.device)
+        c = self._predict_coefs(int(t))
+        return c['sqrt_ac'], c['sqrt_one_minus_ac']
+
+    def pred_x0_from_eps(self, xt: Tensor, t: int, eps: Tensor):
+        c = self._predict_coefs(int(t))
+        return dmhip.lincomb(1, xt, eps, c['sqrt_recip_ac'], c['sqrt_recipm1_ac'])
+
+    def pred_eps_from_x0(self, xt: Tensor, t: int, x0: Tensor):
+        c = self._predict_coefs(int(t))
+        return dmhip.lincomb(2, xt, x0, c['sqrt_recip_ac'], c['sqrt_recipm1_ac'])
+
+    def pred_x0_from_v(self, xt: Tensor, t: int, v: Tensor):
+        c = self._predict_coefs(int(t))
+        return dmhip.lincomb(1, xt, v, c['sqrt_ac'], c['sqrt_one_minus_ac'])
+
+    def pred_eps_from_v(self, xt: Tensor, t: int, v: Tensor):
+        c = self._predict_coefs(int(t))
+        return dmhip.lincomb(0, xt, v, c['sqrt_one_minus_ac'], c['sqrt_ac'])
+
+    def get_v(self, x0: Tensor, eps: Tensor, t: Tensor):
+        """v = sqrt(ac_t) eps - sqrt(1 - ac_t) x0 (reference ddpm.py:140-150)."""
+        sa, s1m = self._row_coefs(t, x0)
+        return dmhip.lincomb(1, eps, x0, sa, s1m)
+
+    def diffuse(self, x0: Tensor, t: Tensor, eps: Tensor = None):
+        """Sample from q(x_t | x0) = sqrt(ac_t) x0 + sqrt(1 - ac_t) eps (reference ddpm.py:152-172);
+        t holds one timestep per image (or one int for all), eps defaults to torch.randn_like(x0)."""
+        eps = torch.randn_like(x0) if eps is None else eps
+        sa, s1m = self._row_coefs(t, x0)
+        return dmhip.lincomb(0, x0, eps.contiguous(), sa, s1m)
+
     # ------------------------------------------------------------- the step
     def _draw_noise(self, xt: Tensor, needed: bool) -> Optional[Tensor]:
         if not needed and self.skip_unused_noise:

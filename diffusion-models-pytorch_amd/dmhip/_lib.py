@@ -151,11 +151,38 @@ class deferred_range_check:
         self.flagged = False
         self._outer = None
 
+    @staticmethod
+    def _key(handle) -> int:
+        return int(handle.value if isinstance(handle, ctypes.c_void_p) else handle)
+
     def register(self, handle, abi: str, device):
-        key = int(handle.value if isinstance(handle, ctypes.c_void_p) else handle)
+        key = self._key(handle)
         if key not in self.handles:
             check(getattr(load(), abi + '_set_range_deferred')(handle, 1), abi + '_set_range_deferred')
             self.handles[key] = (handle, abi, device)
+
+    def _poll(self, handle, abi: str, device, poll: bool):
+        L = load()
+        check(getattr(L, abi + '_set_range_deferred')(handle, 0), abi + '_set_range_deferred')
+        if poll:
+            flag = ctypes.c_int()
+            check(getattr(L, abi + '_range_poll')(handle, stream_handle(device), ctypes.byref(flag)),
+                  abi + '_range_poll')
+            self.flagged |= bool(flag.value)
+
+    @classmethod
+    def release(cls, handle):
+        """Called before a native handle is destroyed (NativeDenoiser._release_native): every open scope
+        that registered it polls it now, folding a raised range flag into the scope (the loop is then
+        re-run), and forgets it -- so no scope calls into a freed handle, and a new handle that reuses
+        the address is registered afresh."""
+        key = cls._key(handle)
+        scope = cls.active
+        while scope is not None:
+            entry = scope.handles.pop(key, None)
+            if entry is not None:
+                scope._poll(*entry, poll=True)
+            scope = scope._outer
 
     def __enter__(self):
         self._outer = deferred_range_check.active
@@ -164,14 +191,9 @@ class deferred_range_check:
 
     def __exit__(self, exc_type, *exc):
         deferred_range_check.active = self._outer
-        L = load()
         for handle, abi, device in self.handles.values():
-            flag = ctypes.c_int()
-            check(getattr(L, abi + '_set_range_deferred')(handle, 0), abi + '_set_range_deferred')
-            if exc_type is None:
-                check(getattr(L, abi + '_range_poll')(handle, stream_handle(device), ctypes.byref(flag)),
-                      abi + '_range_poll')
-                self.flagged |= bool(flag.value)
+            self._poll(handle, abi, device, poll=exc_type is None)
+        self.handles.clear()
         if self._outer is not None and self.flagged:
             self._outer.flagged = True
         return False
@@ -180,6 +202,7 @@ class deferred_range_check:
 def _declare(L: ctypes.CDLL):
     L.dm_abi_version.restype = ctypes.c_int
     L.dm_last_error.restype = ctypes.c_char_p
+    L.dm_build_info.restype = ctypes.c_char_p
     L.dm_unet_param_count.argtypes = [ctypes.POINTER(UNetArch), ctypes.POINTER(ctypes.c_int)]
     L.dm_unet_create.argtypes = [ctypes.POINTER(UNetArch), ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_int64),
                                  ctypes.c_int, vp, ctypes.POINTER(vp)]
@@ -232,6 +255,11 @@ def _declare(L: ctypes.CDLL):
     L.dm_dit_memory.argtypes = [vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
     L.dm_dit_destroy.argtypes = [vp]
     L.dm_dit_destroy.restype = None
+    L.dm_unet_share_workspace.argtypes = [vp, vp]
+    L.dm_unet_plan_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int)]
+    L.dm_dit_plan_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int)]
+    L.dm_lincomb.argtypes = [ctypes.c_int, vp, vp, vp, ctypes.c_int64, ctypes.c_int64, vp, vp, ctypes.c_float,
+                             ctypes.c_float, vp]
 
 
 def load() -> ctypes.CDLL:
@@ -423,3 +451,61 @@ def unet_profile_read(handle, abi: str = 'dm_unet'):
         out.append(dict(label=buf.value.decode(), flops=fl.value, bytes=by.value, ms_total=ms.value,
                         launches=nl.value))
     return out
+
+
+def plan_stats(handle, abi: str = 'dm_unet'):
+    """(plans built so far, plans cached) of a native model handle (dm_unet_plan_stats / dm_dit_plan_stats)."""
+    builds, cached = ctypes.c_int64(), ctypes.c_int()
+    check(getattr(load(), abi + '_plan_stats')(handle, ctypes.byref(builds), ctypes.byref(cached)),
+          abi + '_plan_stats')
+    return builds.value, cached.value
+
+
+def share_workspace(a, b):
+    """Let native UNet handle b run over a's plan scratch (forwards of a and b never overlap)."""
+    check(load().dm_unet_share_workspace(a, b), 'dm_unet_share_workspace')
+
+
+def lincomb(mode: int, a: torch.Tensor, b: torch.Tensor, c1, c2, out: torch.Tensor = None) -> torch.Tensor:
+    """out = c1 a + c2 b (mode 0), c1 a - c2 b (1), (c1 a - b) / c2 (2) on device tensors of one shape;
+    c1 / c2 are python floats (rounded to float32) or [B] float32 device tensors (one per image, dim 0)."""
+    for name, t in (('a', a), ('b', b)):
+        require_device_tensor(t, name)
+    if a.shape != b.shape:
+        raise ValueError(f'lincomb: shapes {tuple(a.shape)} and {tuple(b.shape)} differ')
+    out = torch.empty_like(a) if out is None else out
+    B = a.shape[0] if a.ndim else 1
+    row = a.numel() // B if B else 1
+
+    def coef(c):
+        if isinstance(c, torch.Tensor) and c.ndim == 1:
+            require_device_tensor(c, 'coefficient')
+            if c.shape != (B, ):
+                raise ValueError(f'per-row coefficients must have shape ({B},), got {tuple(c.shape)}')
+            return c.data_ptr(), 0.0
+        return None, float(c)
+    p1, s1 = coef(c1)
+    p2, s2 = coef(c2)
+    check(load().dm_lincomb(mode, a.data_ptr(), b.data_ptr(), out.data_ptr(), a.numel(), max(row, 1), p1, p2, s1, s2,
+                            stream_handle(a.device)), 'dm_lincomb')
+    return out
+
+
+def source_hash() -> str:
+    """sha256 (first 16 hex digits) of the library's sources in the Makefile's order: what dm_build_info
+    reports for a library built from this tree."""
+    import hashlib
+    csrc = os.path.join(os.path.dirname(_HERE), 'csrc')
+    with open(os.path.join(csrc, 'Makefile')) as f:
+        mk = f.read()
+    srcs = re.search(r'^SRCS := (.*)$', mk, re.M).group(1).split()
+    hdrs = re.search(r'^HDRS := (.*)$', mk, re.M).group(1).split()
+    h = hashlib.sha256()
+    for name in srcs + hdrs:
+        with open(os.path.join(csrc, name), 'rb') as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def build_info() -> str:
+    return load().dm_build_info().decode()

@@ -6,6 +6,8 @@ classifier-free-guidance samplers run the two branches through the two
 weight sets. State_dict names (``unet_cond.*``, ``unet_uncond.*``) match the
 reference, so combined checkpoints load unchanged.
 """
+import weakref
+
 import torch
 import torch.nn as nn
 
@@ -20,6 +22,9 @@ class UNetCombined(nn.Module):
         kwargs_uncond = kwargs.copy()
         kwargs_uncond.update({'num_classes': None})
         self.unet_uncond = UNetModel(*args, **kwargs_uncond)
+        # the two networks never run concurrently: one plan workspace for both (weak links, not submodules)
+        self.unet_cond.__dict__['_ws_peer'] = weakref.ref(self.unet_uncond)
+        self.unet_uncond.__dict__['_ws_peer'] = weakref.ref(self.unet_cond)
 
     def forward(self, x, timesteps, y=None):
         unet = self.unet_uncond if y is None else self.unet_cond

@@ -111,6 +111,8 @@ class NativeDenoiser(nn.Module):
 
     def _release_native(self):
         if getattr(self, '_native', None) is not None:
+            # an open deferred-range scope polls (and forgets) the handle before it is freed
+            dmhip.deferred_range_check.release(self._native)
             getattr(load(), self._abi + '_destroy')(self._native)
             self._native = None
             self._native_key = None
@@ -146,10 +148,20 @@ class NativeDenoiser(nn.Module):
         freqs = self._time_freqs().to(device)
         check(getattr(L, self._abi + '_set_time_freqs')(handle, freqs.data_ptr(), freqs.numel(), stream_handle(device)),
               self._abi + '_set_time_freqs')
+        self._share_peer_workspace(handle)
         torch.cuda.current_stream(device).synchronize()
         self._native = handle
         self._native_key = key
         return handle
+
+    def _share_peer_workspace(self, handle):
+        """UNetCombined's two networks run one after the other on one stream: the second handle to be
+        created adopts the first one's plan scratch (dm_unet_share_workspace), one workspace for both."""
+        ref = self.__dict__.get('_ws_peer')
+        peer = ref() if ref is not None else None
+        if peer is not None and self._abi == 'dm_unet' and getattr(peer, '_abi', None) == 'dm_unet' \
+                and getattr(peer, '_native', None) is not None:
+            dmhip.share_workspace(peer._native, handle)
 
     def _time_freqs(self) -> Tensor:
         half = self.arch['dim'] // 2

@@ -43,6 +43,9 @@ extern "C" {
 
 /* Library / error handling ------------------------------------------------ */
 int dm_abi_version(void);
+/* "src=<16 hex> arch=gfx950": the first 16 hex digits of sha256 over the library's sources in build order
+ * (csrc/Makefile SRC_HASH), so a caller can tell which sources a prebuilt library came from. */
+const char* dm_build_info(void);
 const char* dm_last_error(void);
 
 /* Denoiser: DDPM UNet ------------------------------------------------------
@@ -110,8 +113,15 @@ int dm_unet_profile(dm_unet* m, int enable);
 int dm_unet_profile_count(dm_unet* m, int* n_ops);
 int dm_unet_profile_get(dm_unet* m, int i, char* label, int label_len, double* flops, double* bytes,
                         double* ms_total, int64_t* launches);
-/* Device bytes held by packed weights and by the cached workspace. */
+/* Device bytes held by packed weights (fp32 arena + split copies) and by the plan scratch slab. */
 int dm_unet_memory(const dm_unet* m, int64_t* weight_bytes, int64_t* workspace_bytes);
+/* Plans are cached per forward shape (B, H, W), up to 3, least recently used evicted; they all run over
+ * one scratch slab sized to the largest. dm_unet_share_workspace(a, b) makes b use a's slab too: for
+ * models whose forwards never overlap (one stream, one after the other) -- UNetCombined's conditional
+ * and unconditional networks (models/adm/unet_combined.py:23-25), which then hold one workspace instead
+ * of two. dm_unet_plan_stats: plans built so far and plans cached. */
+int dm_unet_share_workspace(dm_unet* a, dm_unet* b);
+int dm_unet_plan_stats(const dm_unet* m, int64_t* builds, int* cached);
 /* Arithmetic of the 3x3 halo-patch convs (all fp32-accurate, models/unet.py:16,26 convolve in fp32):
  * DM_SPLIT_FP16X2 (default; env DM_CONV_MATH=fp16x2), DM_SPLIT_BF16X3 (bf16x3), 0 = fp32 MFMA (fp32).
  * An fp16x2 forward that meets an activation beyond the fp16 range (|a| > 65504) is detected on the
@@ -171,6 +181,8 @@ int dm_dit_profile_count(dm_dit* m, int* n_ops);
 int dm_dit_profile_get(dm_dit* m, int i, char* label, int label_len, double* flops, double* bytes,
                        double* ms_total, int64_t* launches);
 int dm_dit_memory(const dm_dit* m, int64_t* weight_bytes, int64_t* workspace_bytes);
+/* As dm_unet_plan_stats (plans keyed by B). */
+int dm_dit_plan_stats(const dm_dit* m, int64_t* builds, int* cached);
 void dm_dit_destroy(dm_dit* m);
 
 /* Sampler update -----------------------------------------------------------
@@ -217,6 +229,17 @@ typedef struct dm_step_desc {
 } dm_step_desc;
 
 int dm_sampler_step(const dm_step_desc* d, void* stream);
+
+/* Closed-form conversions of reference diffusions/ddpm.py, elementwise with separately rounded float32
+ * products (bit-identical to the torch CPU expressions given the same coefficients):
+ *   mode 0: out = c1 a + c2 b       diffuse (:152-172: sqrt(ac_t) x0 + sqrt(1 - ac_t) eps),
+ *                                   pred_eps_from_v (:117-120)
+ *   mode 1: out = c1 a - c2 b       pred_x0_from_eps (:102-105), pred_x0_from_v (:112-115), get_v (:140-150)
+ *   mode 2: out = (c1 a - b) / c2   pred_eps_from_x0 (:107-110)
+ * a, b, out: n floats; c1_rows / c2_rows: per-row coefficients (row = element / row_elems, one row per image
+ * with its own timestep) or NULL for the scalars c1 / c2. */
+int dm_lincomb(int mode, const float* a, const float* b, float* out, int64_t n, int64_t row_elems,
+               const float* c1_rows, const float* c2_rows, float c1, float c2, void* stream);
 
 /* Operator-level entry points (NHWC, channel-pitched views) ----------------
  * Used by the parity tests and to compose other denoisers.

@@ -67,6 +67,46 @@ def predict(ac: Tensor, out: Tensor, xt: Tensor, t: int, objective='pred_eps', c
     return x0, eps, learned_var
 
 
+def pred_x0_from_eps(ac: Tensor, xt: Tensor, t: int, eps: Tensor) -> Tensor:
+    """diffusions/ddpm.py:102-105"""
+    return (1. / ac[t]) ** 0.5 * xt - (1. / ac[t] - 1.) ** 0.5 * eps
+
+
+def pred_eps_from_x0(ac: Tensor, xt: Tensor, t: int, x0: Tensor) -> Tensor:
+    """diffusions/ddpm.py:107-110"""
+    return ((1. / ac[t]) ** 0.5 * xt - x0) / (1. / ac[t] - 1.) ** 0.5
+
+
+def pred_x0_from_v(ac: Tensor, xt: Tensor, t: int, v: Tensor) -> Tensor:
+    """diffusions/ddpm.py:112-115"""
+    return ac[t] ** 0.5 * xt - (1. - ac[t]) ** 0.5 * v
+
+
+def pred_eps_from_v(ac: Tensor, xt: Tensor, t: int, v: Tensor) -> Tensor:
+    """diffusions/ddpm.py:117-120"""
+    return (1. - ac[t]) ** 0.5 * xt + ac[t] ** 0.5 * v
+
+
+def _per_image(c: Tensor, ndim: int) -> Tensor:
+    while c.ndim < ndim:
+        c = c.unsqueeze(-1)
+    return c
+
+
+def get_v(ac: Tensor, x0: Tensor, eps: Tensor, t: Tensor) -> Tensor:
+    """diffusions/ddpm.py:140-150"""
+    sa = _per_image(ac[t] ** 0.5, x0.ndim)
+    s1m = _per_image((1. - ac[t]) ** 0.5, x0.ndim)
+    return sa * eps - s1m * x0
+
+
+def diffuse(ac: Tensor, x0: Tensor, t: Tensor, eps: Tensor) -> Tensor:
+    """diffusions/ddpm.py:152-172"""
+    sa = _per_image(ac[t] ** 0.5, x0.ndim)
+    s1m = _per_image((1. - ac[t]) ** 0.5, x0.ndim)
+    return sa * x0 + s1m * eps
+
+
 def ddpm_denoise(ac, out, xt, t, t_prev, var_type='fixed_large', objective='pred_eps', clip=True,
                  noise_fn: Callable[[Tensor], Tensor] = torch.randn_like) -> Dict[str, Tensor]:
     """diffusions/ddpm.py:205-261"""

@@ -50,3 +50,11 @@ def test_create_rejects_bad_arguments():
     assert L.dm_unet_param_count(ctypes.byref(bad), ctypes.byref(n)) == dmhip._lib.DM_ERR_ARG
     with pytest.raises(ValueError):
         dmhip._lib.check(dmhip._lib.DM_ERR_ARG, 'x')
+
+
+def test_library_built_from_these_sources():
+    """dm_build_info's source fingerprint equals the tree's (csrc/Makefile SRC_HASH): the libdm_hip.so the
+    tests load -- here and, in tests/test_gpu_r3.py, on the GPU box -- was built from these sources."""
+    info = dmhip._lib.build_info()
+    assert info.startswith('src=') and 'arch=gfx950' in info, info
+    assert info.split()[0] == 'src=' + dmhip._lib.source_hash(), (info, dmhip._lib.source_hash())
