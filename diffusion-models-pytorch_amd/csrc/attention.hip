@@ -606,7 +606,240 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
         out[(size_t)(orow0 + i * 32 + acc_row(r, lh)) * a.ldo + ocol0 + j * 32 + lr] = oacc[i][j][r] * ounscale;
 }
 
+// Flash attention on the pre-split operand planes (AttnArgs::pq / pk / pv) for the shapes the kernels above
+// do not take: ADM's 32^2 (L = 1024) and 8^2 (L = 64) blocks with heads of 64 (models/adm/unet.py:347-408)
+// and DiT's 16 heads of 72 over T = 256 tokens (timm Attention, oracle/dit.py:44-51). The L x L score matrix
+// never leaves the CU: per 64-key block, S = (q)(k)^T, an online softmax (running row maximum and sum,
+// exp2 with the log2(e) factor folded into the exact 2^-(ea + eb) unscale) and O += P v.
+//
+// Layout on the matrix cores (v_mfma_f32_32x32x16_f16, fp16x2 products a1 b0 + a0 b1 + a0 b0 as everywhere):
+//  * S^T = K Q^T: the key on the MFMA row, the query on the lane (lane & 31), so a lane holds 32 scores of
+//    ONE query row: the row maximum / sum are register reductions plus one cross-half shuffle, and the
+//    running-softmax correction of the output is lane-local.
+//  * O^T = V^T P^T: the S^T accumulators, exponentiated and split, are directly the B operand (P^T, query on
+//    the lane) -- with the k index of a 16-key step permuted as the accumulator rows lie, (e & 3) + 8 (e >> 2)
+//    + 4 lh for element e of lane half lh, which the V^T tile's LDS image reproduces (two 8-B stores per
+//    16-B load), so a consistent relabelling of the contraction index and no register shuffles.
+// Q stays in registers (its DHP / 16 slices, both pieces); K and V^T blocks are staged through LDS (double
+// buffered, one barrier per 64 keys, loads for the next block in flight during this one's MFMAs), with row
+// pitches of an odd number of 16-B slots times 4 dwords so the 32-row fragment reads are conflict free.
+// Head dims below DHP (72 in an 80-deep contraction) are zero-padded in registers / LDS, never in memory;
+// O^T rows >= Dh read clamped V rows and are not stored. Each wave owns 32 queries; NW waves per block.
+// Not bit-identical to the unfused path (exp2 and the online rescale round differently): within a few ulp of
+// the unfused softmax (tests/test_gpu_r3.py test_flash_attention_vs_unfused).
+template <int DHP, int NW>
+__global__ void __launch_bounds__(NW * 64) attn_flash_kernel(AttnArgs a) {
+  constexpr int KB = 64;                     // keys per block
+  constexpr int NS = DHP / 16;               // 16-deep slices of the S contraction
+  constexpr int KP = DHP == 80 ? 168 : 136;  // fp16 pitch of a K row (2 DHP + pad: 84 / 68 dwords = 4 x odd)
+  constexpr int VP = 136;                    // fp16 pitch of a V^T row (64 keys x 2 pieces + pad: 68 dwords)
+  constexpr int NDT = (DHP + 31) / 32;       // 32-row d tiles of O^T
+  constexpr int KBUF = KB * KP, VBUF = DHP * VP, BUF = KBUF + VBUF;
+  constexpr int NT = NW * 64;
+  __shared__ __attribute__((aligned(16))) _Float16 lds[2 * BUF];
+  static_assert(NW * 32 * (DHP + 1) * 4 <= 2 * BUF * 2, "output staging fits the operand buffers");
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int L = a.L, Dh = a.Dh;
+  const int nqb = L / (32 * NW);
+  const int bid = xcd_remap_p(blockIdx.x, gridDim.x);
+  const int qb = bid % nqb, bh = bid / nqb;
+  const size_t plane = (size_t)L * Dh;
+  const _Float16* Q = a.pq + (size_t)bh * 2 * plane;
+  const _Float16* K = a.pk + (size_t)bh * 2 * plane;
+  const _Float16* V = a.pv + (size_t)bh * 2 * plane;
+  const int q0 = qb * 32 * NW + wave * 32;
+
+  // Q^T fragments (B operand): query q0 + lr, d = 16 s + 8 lh .. + 7 of both pieces; zero beyond Dh
+  f16x8 qf[NS][2];
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int d = 16 * s + 8 * lh;
+      if (d < Dh)
+        qf[s][p] = *reinterpret_cast<const f16x8*>(Q + p * plane + (size_t)(q0 + lr) * Dh + d);
+      else
+        for (int e = 0; e < 8; ++e) qf[s][p][e] = (_Float16)0.f;
+    }
+
+  // loaders: K chunks (row, piece, 8 d) and V^T chunks (d row, piece, 8 keys), 16 B each, into registers
+  const int dh8 = Dh / 8;
+  const int nkc = 2 * KB * dh8, nvc = 2 * Dh * (KB / 8);
+  constexpr int CK = (2 * KB * (DHP / 8) + NT - 1) / NT, CV = (2 * DHP * (KB / 8) + NT - 1) / NT;
+  f4 rk[CK], rv[CV];
+  auto load_blk = [&](int kb) {
+#pragma unroll
+    for (int u = 0; u < CK; ++u) {
+      const int i = min(t + NT * u, nkc - 1);
+      const int p = i / (KB * dh8), r = i - p * (KB * dh8);   // r = row * dh8 + c8: contiguous in the plane
+      rk[u] = *reinterpret_cast<const f4*>(K + p * plane + (size_t)kb * KB * Dh + 8 * r);
+    }
+#pragma unroll
+    for (int u = 0; u < CV; ++u) {
+      const int i = min(t + NT * u, nvc - 1);
+      const int c8 = i & 7, pd = i >> 3, p = pd / Dh, d = pd - p * Dh;
+      rv[u] = *reinterpret_cast<const f4*>(V + p * plane + (size_t)d * L + kb * KB + 8 * c8);
+    }
+  };
+  auto store_blk = [&](int buf) {
+    _Float16* kb_ = lds + buf * BUF;
+    _Float16* vb_ = kb_ + KBUF;
+#pragma unroll
+    for (int u = 0; u < CK; ++u) {
+      const int i = t + NT * u;
+      if (i >= nkc) continue;
+      const int p = i / (KB * dh8), r = i - p * (KB * dh8);
+      const int row = r / dh8, c8 = r - row * dh8;
+      *reinterpret_cast<f4*>(kb_ + row * KP + (c8 >> 1) * 32 + p * 16 + (c8 & 1) * 8) = rk[u];
+    }
+#pragma unroll
+    for (int u = 0; u < CV; ++u) {
+      const int i = t + NT * u;
+      if (i >= nvc) continue;
+      const int c8 = i & 7, pd = i >> 3, p = pd / Dh, d = pd - p * Dh;
+      // keys 8 c8 .. + 3 -> positions 4 (c8 & 1) .. + 3, keys + 4 .. + 7 -> 8 + 4 (c8 & 1) .. of the 16-key group
+      _Float16* dst = vb_ + d * VP + (c8 >> 1) * 32 + p * 16 + (c8 & 1) * 4;
+      const f4 v = rv[u];
+      *reinterpret_cast<float2*>(dst) = make_float2(v[0], v[1]);
+      *reinterpret_cast<float2*>(dst + 8) = make_float2(v[2], v[3]);
+    }
+  };
+  // zero the K rows' head-dim padding (d in [Dh, DHP)) of both buffers: never written by the loader
+  for (int i = t; i < 2 * KB * 2 * (DHP / 8 - dh8); i += NT) {
+    const int per = 2 * (DHP / 8 - dh8);
+    const int rowb = i / per, rem = i - rowb * per;
+    const int buf = rowb / KB, row = rowb - buf * KB, p = rem & 1, c8 = dh8 + (rem >> 1);
+    *reinterpret_cast<f4*>(lds + buf * BUF + row * KP + (c8 >> 1) * 32 + p * 16 + (c8 & 1) * 8) = f4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  const float sl2 = ldexpf(1.f, -(a.ea + a.eb)) * 1.4426950408889634f;   // exact unscale x log2(e)
+  const float pp = ldexpf(1.f, a.ep);
+  f16v oacc[NDT];
+#pragma unroll
+  for (int i = 0; i < NDT; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) oacc[i][r] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;
+
+  const int nkb = L / KB;
+  load_blk(0);
+  store_blk(0);
+  __syncthreads();
+  for (int kb = 0; kb < nkb; ++kb) {
+    if (kb + 1 < nkb) load_blk(kb + 1);
+    const _Float16* Kb = lds + (kb & 1) * BUF;
+    const _Float16* Vb = Kb + KBUF;
+    // S^T [64 keys x 32 queries] = K Q^T
+    f16v sacc[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sacc[j][r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        f16x8 ka[2];
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+          ka[p] = *reinterpret_cast<const f16x8*>(Kb + (j * 32 + lr) * KP + s * 32 + p * 16 + lh * 8);
+        Split<2>::mma(ka, qf[s], sacc[j]);
+      }
+    }
+    // online softmax of this query row (lane) over the block's 64 keys (32 here, 32 in the other half-wave)
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        sacc[j][r] *= sl2;
+        mx = fmaxf(mx, sacc[j][r]);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float m_new = fmaxf(m_run, mx);
+    const float corr = __builtin_amdgcn_exp2f(m_run - m_new);
+    m_run = m_new;
+    l_run *= corr;
+#pragma unroll
+    for (int i = 0; i < NDT; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) oacc[i][r] *= corr;
+    // P^T pieces: k-step ks = 16 keys = accumulator registers 8 (ks & 1) .. + 7 of tile ks >> 1
+    f16x8 pb[4][2];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float pv = __builtin_amdgcn_exp2f(sacc[ks >> 1][8 * (ks & 1) + e] - m_new);
+        l_run += pv;
+        const float x = pv * pp;
+        const _Float16 h0 = (_Float16)x;
+        pb[ks][0][e] = h0;
+        pb[ks][1][e] = (_Float16)(x - (float)h0);
+      }
+    // O^T [d x 32 queries] += V^T P^T
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+      const int drow = min(dt * 32 + lr, Dh - 1);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        f16x8 va[2];
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+          va[p] = *reinterpret_cast<const f16x8*>(Vb + drow * VP + ks * 32 + p * 16 + lh * 8);
+        Split<2>::mma(va, pb[ks], oacc[dt]);
+      }
+    }
+    if (kb + 1 < nkb) store_blk((kb + 1) & 1);
+    __syncthreads();
+  }
+
+  // O = O^T / l (x 2^-(ep + ev)), staged through LDS as [32 queries][Dh + 1] fp32 rows per wave, stored as rows
+  const float l_tot = l_run + __shfl_xor(l_run, 32);
+  const float scale = ldexpf(1.f, -(a.ep + a.ev)) / l_tot;
+  const int OP = Dh + 1;
+  float* st = reinterpret_cast<float*>(lds) + wave * 32 * OP;
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int d = dt * 32 + acc_row(r, lh);
+      if (d < Dh) st[lr * OP + d] = oacc[dt][r] * scale;
+    }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  const int h = bh % a.heads, b = bh / a.heads;
+  float* out = a.out + ((size_t)b * L + q0) * a.ldo + h * Dh;
+  for (int i = lane; i < 32 * Dh; i += 64) {
+    const int q = i / Dh, d = i - q * Dh;
+    out[(size_t)q * a.ldo + d] = st[q * OP + d];
+  }
+}
+
 }  // namespace
+
+bool attn_flash_ok(int L, int Dh) { return L >= 64 && L % 64 == 0 && Dh % 8 == 0 && Dh >= 8 && Dh <= 80; }
+
+int attn_flash(const AttnArgs& a, hipStream_t st) {
+  DM_REQUIRE(attn_flash_ok(a.L, a.Dh), "flash attention: L % 64 == 0 and head dims of 8 .. 80 (multiples of 8)");
+  DM_REQUIRE(a.pq && a.pk && a.pv && a.out && a.B > 0 && a.heads > 0 && a.ldo % 4 == 0,
+             "flash attention: needs the pre-split operand planes and an output");
+  DM_REQUIRE(((reinterpret_cast<uintptr_t>(a.pq) | reinterpret_cast<uintptr_t>(a.pk) |
+               reinterpret_cast<uintptr_t>(a.pv)) & 15) == 0, "flash attention: 16-byte aligned planes");
+  const int nw = a.L % 256 == 0 ? 8 : 2;
+  const unsigned blocks = (unsigned)((long)a.B * a.heads * (a.L / (32 * nw)));
+  if (a.Dh > 64) {
+    if (nw == 8) hipLaunchKernelGGL((attn_flash_kernel<80, 8>), dim3(blocks), dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((attn_flash_kernel<80, 2>), dim3(blocks), dim3(128), 0, st, a);
+  } else {
+    if (nw == 8) hipLaunchKernelGGL((attn_flash_kernel<64, 8>), dim3(blocks), dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((attn_flash_kernel<64, 2>), dim3(blocks), dim3(128), 0, st, a);
+  }
+  DM_LAUNCH_CHECK();
+  return DM_OK;
+}
 
 #ifdef DM_K32_STAMPS
 extern "C" int dm_debug_attn_stamps(void* host, int nblocks) {
@@ -618,6 +851,7 @@ extern "C" int dm_debug_attn_stamps(void* host, int nblocks) {
 bool attn_fused_ok(int L, int Dh) { return L == kAL && (Dh == 64 || Dh == 256); }
 
 int attn_fused(const AttnArgs& args, hipStream_t st) {
+  if (!attn_fused_ok(args.L, args.Dh)) return attn_flash(args, st);
   AttnArgs a = args;
   a.proj_staged = a.fuse_proj && staged_epilogue_ok(a.proj) ? 1 : 0;
   DM_REQUIRE(attn_fused_ok(a.L, a.Dh), "fused attention: L must be 256 and the head dim 64 or 256");

@@ -207,7 +207,7 @@ int DiTModel::build_plan(Plan& pl, int B) {
   float* x = pl.alloc((size_t)M * D * 4);
   float2* stats = (float2*)pl.alloc((size_t)M * sizeof(float2));
   float* qkv = pl.alloc((size_t)M * 3 * D * 4);
-  float* Sb = pl.alloc((size_t)B * heads * T * T * 4);
+  float* Sb = nullptr;  // score matrix of the unfused attention path (allocated on first use)
   float* Ob = pl.alloc((size_t)M * D * 4);
   float* hb = pl.alloc((size_t)M * Hm * 4);
   float* lin = pl.alloc((size_t)M * PP * OC * 4);
@@ -347,13 +347,32 @@ int DiTModel::build_plan(Plan& pl, int B) {
     const float* mb = mods + (size_t)b * 6 * D;  // shift_msa, scale_msa, gate_msa, shift_mlp, scale_mlp, gate_mlp
     // attention branch
     stats_op();
-    {
-      GemmArgs g = linear(x, D, M, bp.qkv_w, bp.qkv_b, 3 * D, D, qkv, 3 * D);
-      g.ln_stats = stats; g.ln_shift = mb; g.ln_scale = mb + D; g.ln_pitch = ada_total; g.ln_rows = T;
-      split(g, 6, bp.qkv_w, (size_t)3 * D * D, 0);
-      add_token_gemm(g);
+    GemmArgs gq = linear(x, D, M, bp.qkv_w, bp.qkv_b, 3 * D, D, qkv, 3 * D);
+    gq.ln_stats = stats; gq.ln_shift = mb; gq.ln_scale = mb + D; gq.ln_pitch = ada_total; gq.ln_rows = T;
+    split(gq, 6, bp.qkv_w, (size_t)3 * D * D, 0);
+    // flash attention (attention.hip attn_flash_kernel): the qkv GEMM's epilogue writes q * d^-1/2, k, v as
+    // the fp16x2 operand planes (over the qkv buffer: same bytes), S never leaves the CU
+    const bool flash = math == 2 && gq.ws && attn_flash_ok(T, Dh) && !std::getenv("DM_DIT_ATTN_UNFUSED");
+    _Float16* planes = reinterpret_cast<_Float16*>(qkv);
+    const size_t plane_n = (size_t)M * D * 2;   // fp16 elements of one operand's two planes
+    if (flash) {
+      gq.ap_q = planes; gq.ap_k = planes + plane_n; gq.ap_v = planes + 2 * plane_n;
+      gq.ap_L = T; gq.ap_heads = heads; gq.ap_Dh = Dh; gq.ap_legacy = 0;
+      gq.ap_alpha = (float)std::pow((double)Dh, -0.5); gq.ap_bscale = 0.f;
+      gq.ap_ea = 6; gq.ap_eb = 6; gq.ap_ev = 6;
     }
-    {
+    add_token_gemm(gq);
+    if (flash) {
+      AttnArgs at{};
+      at.pq = planes; at.pk = planes + plane_n; at.pv = planes + 2 * plane_n;
+      at.L = T; at.Dh = Dh; at.heads = heads; at.B = B;
+      at.out = Ob; at.ldo = D;
+      at.ea = 6; at.eb = 6; at.ep = 14; at.ev = 6;
+      at.range_flag = range_flag;
+      pl.add("attn_flash_kernel<" + std::to_string(Dh) + ">", 4.0 * B * heads * (double)T * T * Dh,
+             4.0 * M * (3.0 * D + D), [=](hipStream_t st) { return attn_flash(at, st); });
+    } else {
+      if (!Sb) Sb = pl.alloc((size_t)B * heads * T * T * 4);
       // timm Attention: qkv.reshape(B, N, 3, heads, d): q / k / v of head h at columns h*d, D + h*d, 2D + h*d
       GemmArgs gs{};
       gs.M = T; gs.N = T; gs.K = Dh; gs.Z1 = B; gs.Z2 = heads; gs.pick_Z = (long)kPickBatch * heads;
@@ -566,7 +585,7 @@ extern "C" int dm_dit_memory(const dm_dit* h, int64_t* weight_bytes, int64_t* wo
   if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
   // the fp32 arena plus the pre-split fp16x2 copies of the token-GEMM weights (as dm_unet_memory counts them)
   if (weight_bytes) *weight_bytes = (int64_t)(h->m->arena_floats * sizeof(float) + h->m->split_bytes);
-  if (workspace_bytes) *workspace_bytes = (int64_t)h->m->plans.pool->bytes;
+  if (workspace_bytes) *workspace_bytes = (int64_t)h->m->plans.pool->bytes();
   return DM_OK;
 }
 

@@ -310,6 +310,10 @@ struct AttnArgs {
 };
 bool attn_fused_ok(int L, int Dh);
 int attn_fused(const AttnArgs& a, hipStream_t st);
+// Flash attention (attention.hip attn_flash_kernel) on pre-split planes for L % 64 == 0, head dims 8 .. 80:
+// ADM's L = 1024 / 64 blocks, DiT's 72-wide heads. attn_fused dispatches there for shapes it does not take.
+bool attn_flash_ok(int L, int Dh);
+int attn_flash(const AttnArgs& a, hipStream_t st);
 int conv3x3_small_in(const float* x, int B, int Cin, int H, int W, const float* w, const float* bias,
                      int Cout, const View& y, hipStream_t st);
 // last conv weights torch [Cout][Cin][3][3] -> [9][Cin][CO], CO = 4 (Cout <= 4) or 8; wp holds 9 * Cin * CO floats

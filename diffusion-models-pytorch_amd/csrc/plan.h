@@ -11,13 +11,13 @@
 //
 // Scratch: a plan does not own device memory. Its builder runs twice: once
 // measuring (alloc hands out placeholder addresses that are never
-// dereferenced, the op list is discarded), then over a ScratchPool slab sized
-// to the measured need. Every plan of a model -- a small LRU cache keyed by
-// the forward's shape -- and of the models that share the pool
-// (dm_unet_share_workspace: UNetCombined's two networks) uses the same slab,
-// since their forwards run one after the other on one stream. A slab that has
-// to grow is reallocated; plans built over the old one are stale (generation)
-// and rebuilt on their next use.
+// dereferenced, the op list is discarded), then over a ScratchPool slab large
+// enough for the measured need. The plans of a model -- a small LRU cache
+// keyed by the forward's shape -- and of the models that share the pool
+// (dm_unet_share_workspace: UNetCombined's two networks) run over the same
+// slab, since their forwards run one after the other on one stream; a plan
+// that needs more than the current slab gets a larger one, and plans built
+// over an older slab keep theirs until they are evicted.
 #include <cstdlib>
 #pragma once
 #include <cstdint>
@@ -38,39 +38,44 @@ struct Op {
   std::function<int(hipStream_t)> fn;
 };
 
-// One device slab of plan scratch, shared by every plan that runs over it (see above).
-struct ScratchPool {
+// One device allocation of plan scratch. Plans hold a reference to the slab they were built over, so a
+// slab lives as long as some cached plan uses it.
+struct Slab {
   char* base = nullptr;
   size_t bytes = 0;
-  uint64_t gen = 0;  // bumped whenever the slab is (re)allocated
-  ScratchPool() = default;
-  ScratchPool(const ScratchPool&) = delete;
-  ScratchPool& operator=(const ScratchPool&) = delete;
-  ~ScratchPool() {
+  Slab() = default;
+  Slab(const Slab&) = delete;
+  Slab& operator=(const Slab&) = delete;
+  ~Slab() {
     if (base) {
-      (void)hipDeviceSynchronize();
+      (void)hipDeviceSynchronize();  // launches still reading the slab finish first
       (void)hipFree(base);
     }
   }
-  int ensure(size_t need) {
-    if (base && need <= bytes) return DM_OK;
-    if (base) {
-      (void)hipDeviceSynchronize();  // launches still reading the old slab finish first
-      (void)hipFree(base);
-      base = nullptr;
-      bytes = 0;
+};
+
+// The scratch of a set of plans that never run concurrently (one model's cached plans, or the models joined
+// by dm_unet_share_workspace): new plans are built over the current slab; one that needs more gets a new,
+// larger slab, while the plans built over the old one keep it (no rebuild) until they are evicted.
+struct ScratchPool {
+  std::shared_ptr<Slab> cur;
+  int ensure(size_t need, std::shared_ptr<Slab>& out) {
+    if (!cur || need > cur->bytes) {
+      auto s = std::make_shared<Slab>();
+      void* p = nullptr;
+      if (hipMalloc(&p, need ? need : 256) != hipSuccess) {
+        (void)hipGetLastError();
+        set_error("plan scratch allocation of " + std::to_string(need >> 20) + " MiB failed");
+        return DM_ERR_HIP;
+      }
+      s->base = static_cast<char*>(p);
+      s->bytes = need;
+      cur = std::move(s);
     }
-    ++gen;
-    void* p = nullptr;
-    if (hipMalloc(&p, need ? need : 256) != hipSuccess) {
-      (void)hipGetLastError();
-      set_error("plan scratch allocation of " + std::to_string(need >> 20) + " MiB failed");
-      return DM_ERR_HIP;
-    }
-    base = static_cast<char*>(p);
-    bytes = need;
+    out = cur;
     return DM_OK;
   }
+  size_t bytes() const { return cur ? cur->bytes : 0; }
 };
 
 struct PlanBase {
@@ -78,7 +83,7 @@ struct PlanBase {
   bool alloc_failed = false;  // kept for the builders' checks; never set (the slab is sized beforehand)
   bool measuring = false;     // first builder pass: placeholder addresses, ops discarded
   char* scratch = nullptr;    // slab base of the real pass
-  uint64_t gen = 0;           // ScratchPool generation the plan was built over
+  std::shared_ptr<Slab> slab;  // the slab this plan runs over (kept alive while the plan is cached)
   std::vector<Op> ops;
   bool profiling = false;
   int profile_every = 1;  // record events on every N-th run only (the others run unobserved)
@@ -238,12 +243,9 @@ struct PlanCache {
       if (!match(*plans[i])) continue;
       std::unique_ptr<P> p = std::move(plans[i]);
       plans.erase(plans.begin() + i);
-      if (p->gen == pool->gen) {
-        plans.push_back(std::move(p));
-        *out = plans.back().get();
-        return DM_OK;
-      }
-      break;  // built over a slab that has since been reallocated
+      plans.push_back(std::move(p));
+      *out = plans.back().get();
+      return DM_OK;
     }
     auto m = std::make_unique<P>();
     m->measuring = true;
@@ -251,19 +253,14 @@ struct PlanCache {
     if (rc) return rc;
     const size_t need = m->bytes;
     m.reset();
-    rc = pool->ensure(need);
-    if (rc) return rc;
     auto p = std::make_unique<P>();
-    p->scratch = pool->base;
-    p->gen = pool->gen;
+    rc = pool->ensure(need, p->slab);
+    if (rc) return rc;
+    p->scratch = p->slab->base;
     rc = build(*p);
     if (rc) return rc;
     DM_REQUIRE(p->bytes == need, "plan builder is not deterministic (scratch size changed)");
     ++builds;
-    for (size_t i = 0; i < plans.size();) {  // stale plans (older slab) and the LRU overflow
-      if (plans[i]->gen != pool->gen) plans.erase(plans.begin() + i);
-      else ++i;
-    }
     plans.push_back(std::move(p));
     while (plans.size() > kMaxPlans) plans.erase(plans.begin());
     *out = plans.back().get();

@@ -975,8 +975,12 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
       split_for(cq);
       // Fused attention (attention.hip) on 16 x 16 maps; with the qkv conv on the split kernel, its epilogue
       // writes q / k / v as the fp16x2 operand planes the fused kernel reads (over the qkv buffer: same bytes)
-      const bool fuse_attn = conv_math == 2 && attn_fused_ok(hw, Dh) && !std::getenv("DM_ATTN_UNFUSED");
+      // other shapes (ADM's 32^2 and 8^2 blocks): flash attention on the pre-split planes (attn_flash)
+      const bool l256 = attn_fused_ok(hw, Dh);
+      const bool flash = !l256 && attn_flash_ok(hw, Dh) && !std::getenv("DM_ATTN_NO_FLASH");
+      bool fuse_attn = conv_math == 2 && (l256 || flash) && !std::getenv("DM_ATTN_UNFUSED");
       const bool presplit = fuse_attn && conv_pw_ok(cq) && !std::getenv("DM_ATTN_NO_PRESPLIT");
+      if (flash && !presplit) fuse_attn = false;   // the flash kernel reads the planes only
       _Float16* planes = reinterpret_cast<_Float16*>(qkv);
       const size_t plane_n = (size_t)B * hw * C * 2;  // fp16 elements of one operand's two planes
       if (presplit) {
@@ -1074,7 +1078,8 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
           fl += 2.0 * B * hw * (double)C * C;
           by += 4.0 * B * hw * C + 4.0 * C * C;
         }
-        add((presplit ? "attn_presplit_kernel<" : "attn_fused_kernel<") + std::to_string(Dh) + (fuse_proj ? ",proj>" : ">"),
+        add((flash ? "attn_flash_kernel<" : presplit ? "attn_presplit_kernel<" : "attn_fused_kernel<") + std::to_string(Dh) +
+                (fuse_proj ? ",proj>" : ">"),
             fl, by, [=](hipStream_t st) { return attn_fused(at, st); });
       } else {
       GemmArgs gs{};
@@ -1253,7 +1258,7 @@ extern "C" int dm_unet_range_poll(dm_unet* h, void* stream, int* flagged) {
 extern "C" int dm_unet_memory(const dm_unet* h, int64_t* weight_bytes, int64_t* workspace_bytes) {
   if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
   if (weight_bytes) *weight_bytes = (int64_t)(h->m->arena_floats * sizeof(float) + h->m->split_bytes);
-  if (workspace_bytes) *workspace_bytes = (int64_t)h->m->plans.pool->bytes;
+  if (workspace_bytes) *workspace_bytes = (int64_t)h->m->plans.pool->bytes();
   return DM_OK;
 }
 

@@ -64,7 +64,7 @@ def dit_forward(sd: Dict[str, Tensor], x: Tensor, t: Tensor, y: Optional[Tensor]
     w = sd['x_embedder.proj.weight']
     h = F.conv2d(x, w, sd['x_embedder.proj.bias'], stride=p).flatten(2).transpose(1, 2)
     h = h + sd['pos_embed']
-    te = _lin(sd, 't_embedder.mlp.2', F.silu(_lin(sd, 't_embedder.mlp.0', timestep_embedding(t, 256))))
+    te = _lin(sd, 't_embedder.mlp.2', F.silu(_lin(sd, 't_embedder.mlp.0', timestep_embedding(t, 256).to(h.dtype))))
     c = te + F.embedding(y, sd['y_embedder.embedding_table.weight'])
     D = h.shape[-1]
     for b in range(depth):
@@ -88,10 +88,12 @@ def dit_forward(sd: Dict[str, Tensor], x: Tensor, t: Tensor, y: Optional[Tensor]
 class OracleDiT:
     """Callable model(x, t, y=None) over a DiT state_dict."""
 
-    def __init__(self, sd: Dict[str, Tensor], **arch):
-        self.sd = {k: v.detach().to('cpu', torch.float32) for k, v in sd.items()}
+    def __init__(self, sd: Dict[str, Tensor], dtype=torch.float32, **arch):
+        # dtype float64: the same restatement in double precision (the drift bound of the trajectory tests)
+        self.sd = {k: v.detach().to('cpu', dtype) for k, v in sd.items()}
+        self.dtype = dtype
         self.arch = arch
 
     @torch.no_grad()
     def __call__(self, x: Tensor, t: Tensor, y: Optional[Tensor] = None) -> Tensor:
-        return dit_forward(self.sd, x, t, y, **self.arch)
+        return dit_forward(self.sd, x.to(self.dtype), t, y, **self.arch)

@@ -172,11 +172,18 @@ def make_dit():
     init = torch.randn((2, 4, 32, 32))
     labels = torch.tensor([207, 360])
     arr = dict(xl2_cfg3_init=init, xl2_cfg3_labels=labels)
-    for i, out in enumerate(od.sample_loop(model, ac, seq, init, sampler='ddim', eta=0.0, guidance_scale=4.0,
-                                           y=labels, clip=False)):
-        arr[f'xl2_cfg3_step{i}_sample'] = out['sample']
-        arr[f'xl2_cfg3_step{i}_pred_eps'] = out['pred_eps']
-        print('dit step', i, flush=True)
+    from oracle.dit import OracleDiT  # noqa: E402
+    m64 = OracleDiT(model.sd, dtype=torch.float64, **model.arch)
+    runs = []
+    for m, x in ((model, init), (m64, init.double())):
+        runs.append([o['sample'] for o in od.sample_loop(m, ac, seq, x, sampler='ddim', eta=0.0, guidance_scale=4.0,
+                                                         y=labels, clip=False)])
+        print('dit run done', flush=True)
+    for i, s32 in enumerate(runs[0]):
+        arr[f'xl2_cfg3_step{i}_sample'] = s32
+    arr['xl2_cfg3_sample64'] = torch.stack(runs[1]).float()
+    arr['xl2_cfg3_drift_sample'] = np.array([float((a.double() - b).abs().max()) for a, b in zip(*runs)])
+    print('drift', arr['xl2_cfg3_drift_sample'], flush=True)
     # clip_denoised false: the DiT-XL/2 YAML (weights/facebookresearch/DiT/DiT-XL-2-256x256.yaml:37)
     meta['xl2_cfg3'] = dict(guidance_scale=4.0, respace_type='uniform', respace_steps=3, eta=0.0,
                             clip_denoised=False)

@@ -11,7 +11,7 @@ import torch
 
 import dmhip
 from diffusions import DDIM, DDIMCFG, DDPM
-from tests.test_gpu_parity import TOL, _model, _ulps
+from tests.test_gpu_parity import TOL, _model
 from utils.synthetic import init_synthetic_
 
 pytestmark = pytest.mark.gpu
@@ -22,7 +22,8 @@ pytestmark = pytest.mark.gpu
 def test_conversions_vs_reference(cuda, golden, case):
     """pred_x0_from_eps / pred_eps_from_x0 / pred_x0_from_v / pred_eps_from_v / get_v / diffuse on the engine
     (dm_lincomb): bit-identical to the oracle's torch CPU expressions on this host, within a few ulp of the
-    reference outputs generated on the build container's CPU (host-dependent 0-dim pow rounding)."""
+    reference outputs generated on the build container's CPU (host-dependent 0-dim pow rounding: a 1-ulp
+    coefficient difference times sqrt(1/ac) ~ 160 at t = 999 is a few 1e-8 relative)."""
     from oracle import diffusion as od
     g, meta = golden('convert')
     c = meta['cases'][case]
@@ -35,7 +36,7 @@ def test_conversions_vs_reference(cuda, golden, case):
     def check(got, ref, gold):
         got = got.cpu().numpy()
         assert np.array_equal(got, ref.numpy()), np.abs(got - ref.numpy()).max()
-        assert _ulps(got, gold) <= 4
+        assert np.allclose(got, gold, rtol=1e-6, atol=1e-7), np.abs(got - gold).max()
     check(d.diffuse(X0, tvec.to(cuda), EPS), od.diffuse(ac, x0, tvec, eps), g[f'{case}_diffuse'])
     check(d.get_v(X0, EPS, tvec.to(cuda)), od.get_v(ac, x0, eps, tvec), g[f'{case}_get_v'])
     for t in c['ts']:
@@ -217,21 +218,26 @@ def test_dit_xl2_cfg_batch64(cuda, golden, report):
 
 def test_dit_xl2_ddimcfg3_trajectory(cuda, golden, report):
     """DiT-XL/2 DDIMCFG-3 (s = 4, clip_denoised false as the DiT-XL/2 YAML sets, batched 2B forward) vs
-    oracle/dit.py (tests/golden/dit_r3.npz; parity unpinned): every step <= 1e-4."""
+    oracle/dit.py (tests/golden/dit_r3.npz; parity unpinned). Unclipped, x0 = sqrt(1/ac_t) x - ... carries
+    the model's rounding times sqrt(1/ac_999) ~ 157 times the CFG gain 2s - 1 = 7 into the sample, so the
+    oracle's own fp32 run sits ~1e-4 from its float64 run after one step: the bound is check_free_running's
+    (tests/conftest.py) against both runs."""
+    from tests.conftest import check_free_running
     g, meta = golden('dit_r3')
     model, _ = _xl2(cuda, golden)
     c = meta['xl2_cfg3']
     d = DDIMCFG(guidance_scale=c['guidance_scale'], respace_type=c['respace_type'], respace_steps=c['respace_steps'],
                 eta=c['eta'], clip_denoised=c['clip_denoised'], device=cuda)
     labels = torch.from_numpy(g['xl2_cfg3_labels']).to(cuda)
-    worst = 0.0
+    worst, worst64 = 0.0, 0.0
     for i, out in enumerate(d.sample_loop(model, torch.from_numpy(g['xl2_cfg3_init']).to(cuda),
                                           model_kwargs=dict(y=labels), tqdm_kwargs=dict(disable=True))):
-        for k in ('sample', 'pred_eps'):
-            err = float(np.abs(out[k].cpu().numpy() - g[f'xl2_cfg3_step{i}_{k}']).max())
-            worst = max(worst, err)
-            assert err <= TOL, (i, k, err)
+        e32, e64 = check_free_running(out['sample'].cpu().numpy(), g[f'xl2_cfg3_step{i}_sample'],
+                                      g['xl2_cfg3_sample64'][i], g['xl2_cfg3_drift_sample'], i)
+        worst, worst64 = max(worst, e32), max(worst64, e64)
     report('dit_xl2_ddimcfg3_maxabs_vs_oracle', worst)
+    report('dit_xl2_ddimcfg3_maxabs_vs_oracle_float64', worst64)
+    report('dit_xl2_ddimcfg3_oracle_fp32_vs_fp64_drift', float(g['xl2_cfg3_drift_sample'].max()))
     del model
     torch.cuda.empty_cache()
 
@@ -310,3 +316,46 @@ def test_step_accuracy_vs_float64(cuda, golden, report, name):
 def test_gpu_library_is_built_from_this_tree(cuda):
     """The library this GPU run loads was built from the sources in the snapshot (not a stale build)."""
     assert dmhip._lib.build_info().split()[0] == 'src=' + dmhip._lib.source_hash()
+
+
+# ------------------------------------------------------------------ flash attention (attention.hip)
+@pytest.mark.parametrize('case', ['adm_tiny', 'dit_s2', 'dit_xl2', 'adm256'])
+def test_flash_attention_vs_unfused(cuda, golden, report, monkeypatch, case):
+    """attn_flash_kernel (online softmax, S never in HBM) against the unfused S GEMM -> softmax_rows -> PV
+    GEMM path it replaces, which stays as the test oracle: ADM's 8^2 blocks (adm_tiny: L = 64, heads of 32,
+    zero-padded to a 64-deep contraction), DiT-S/2 at 16^2 latents (L = 64, heads of 64), DiT-XL/2 (L = 256,
+    16 heads of 72: an 80-deep contraction, 96-row output tiles), the guided-diffusion 256^2 UNet (L = 1024 at
+    32^2 and L = 64 at 8^2, heads of 64). Forwards within 1e-5 of each other (the attention core alone
+    differs by exp2 vs expf and the online rescaling, a few 1e-7 relative)."""
+    from models.adm.unet import UNetModel
+    from models.dit.model import DiT
+    outs = {}
+    for mode in ('flash', 'unfused'):
+        if mode == 'unfused':
+            monkeypatch.setenv('DM_ATTN_NO_FLASH', '1')
+            monkeypatch.setenv('DM_DIT_ATTN_UNFUSED', '1')
+        gen = torch.Generator().manual_seed(21)
+        if case.startswith('adm'):
+            arch = golden('adm')[1]['archs']['adm_tiny' if case == 'adm_tiny' else 'adm256_combined']
+            m = UNetModel(**arch).eval()
+            S, B = arch['image_size'], 2 if case == 'adm_tiny' else 1
+            x = torch.randn((B, 3, S, S), generator=gen)
+            y = torch.tensor([1, 3][:B])
+        else:
+            arch = golden('dit')[1]['archs'][case]
+            m = DiT(**arch).eval()
+            S, B = arch['input_size'], 2
+            x = torch.randn((B, 4, S, S), generator=gen)
+            y = torch.tensor([5, 9])
+        init_synthetic_(m)
+        m = m.to(cuda)
+        t = torch.tensor([999, 40][:B])
+        outs[mode] = m(x.to(cuda), t.to(cuda), y.to(cuda)).cpu()
+        labels = [op['label'] for op in dmhip.unet_profile_read(m.native_handle(torch.device(cuda)), m._abi)]
+        assert any(lb.startswith('attn_flash_kernel') for lb in labels) == (mode == 'flash'), labels
+        del m
+        torch.cuda.empty_cache()
+    err = (outs['flash'] - outs['unfused']).abs().max().item()
+    report(f'flash_attention_{case}_maxabs_vs_unfused', err)
+    assert torch.isfinite(outs['flash']).all()
+    assert err <= 1e-5, err
