@@ -145,6 +145,46 @@ def cpu_baseline(sd, batch, n_steps, timed_steps=3):
                        f'{os.cpu_count()} logical CPUs on the host); {dt:.2f} s per step, extrapolated x{n_steps}')
 
 
+def cpu_baseline_cfg(name, model_sd, arch, batch, n_steps, guidance_scale, timed_steps, clip=True):
+    """Secondary workloads (bounded sample): the oracle of the ADM (c4: oracle/adm.py,
+    UNetCombined routing) or DiT (c5: oracle/dit.py) denoiser on all usable host cores, one warm-up
+    step, then `timed_steps` DDIMCFG steps (cond + uncond forward, predict, combine, update) at `batch`;
+    images/sec = batch / (t_step x n_steps)."""
+    from oracle import diffusion as od
+    threads = usable_cores()
+    prev_threads = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        if name == 'c4':
+            from oracle.adm import OracleADMCombined
+            model = OracleADMCombined(model_sd, **arch)
+            shape = (batch, 3, arch['image_size'], arch['image_size'])
+        else:
+            from oracle.dit import OracleDiT
+            model = OracleDiT(model_sd, **arch)
+            shape = (batch, arch['in_channels'], arch['input_size'], arch['input_size'])
+        ac = od.alphas_cumprod(od.beta_schedule(1000, 'linear'))
+        seq = od.respaced_seq(1000, 'uniform', n_steps)
+        g = torch.Generator().manual_seed(2022)
+        x = torch.randn(shape, generator=g)
+        y = torch.zeros((batch, ), dtype=torch.long)
+        sub = torch.tensor(seq.tolist()[-(timed_steps + 1):])   # the first timed_steps + 1 steps of the loop
+        with torch.no_grad():
+            it = od.sample_loop(model, ac, sub, x, sampler='ddim', eta=0.0, guidance_scale=guidance_scale, y=y,
+                                clip=clip)
+            next(it)   # warm-up step
+            t0 = time.perf_counter()
+            for _ in range(timed_steps):
+                next(it)
+            dt = (time.perf_counter() - t0) / timed_steps
+    finally:
+        torch.set_num_threads(prev_threads)
+    return dict(value=batch / (dt * n_steps), unit='images/sec', cores=threads, kind='port',
+                sample=f'{timed_steps} of {n_steps} DDIMCFG steps (cond + uncond forward + update) timed at B={batch} '
+                       f'after 1 warm-up step, torch CPU on {threads} threads ({cpu_model_name()}, '
+                       f'{os.cpu_count()} logical CPUs on the host); {dt:.2f} s per step, extrapolated x{n_steps}')
+
+
 def roofline(prof, workload='c3'):
     """Roofline of the dominant kernel family (most GPU time in the timed region)."""
     fam = {}
@@ -237,6 +277,7 @@ def build_workload(name, args, dev, rank):
         conf = load_config(os.path.join(cfgdir, 'adm256_combined.yaml'))
         model = instantiate_from_config(conf.model).eval()
         init_synthetic_(model)
+        sd_cpu = {k: v.clone() for k, v in model.state_dict().items()}
         model = model.to(dev)
         B = args.batch or 64
         steps = args.respace_steps or 100
@@ -251,7 +292,8 @@ def build_workload(name, args, dev, rank):
         model(torch.zeros(shape, device=dev), t0, y)
         model(torch.zeros(shape, device=dev), t0, None)
         return dict(metric=f'images/sec at ADM-256 UNetCombined DDIMCFG-{steps} (s=3), bs={B}', fold=fold, images=B,
-                    shape=shape, diffuser=diffuser, sd_cpu=None,
+                    shape=shape, diffuser=diffuser, sd_cpu=sd_cpu, shared_workspace=True,
+                    cpu=dict(arch=dict(conf.model.params), batch=1, timed_steps=1, guidance_scale=3.0),
                     handles=[(model.unet_cond.native_handle(dev), 'dm_unet', len(diffuser.respaced_seq)),
                              (model.unet_uncond.native_handle(dev), 'dm_unet', len(diffuser.respaced_seq))],
                     workload=f'DDIMCFG-{steps} (s=3, eta=0) sampling fold, guided-diffusion 256x256 UNetCombined '
@@ -261,6 +303,11 @@ def build_workload(name, args, dev, rank):
         conf = load_config(os.path.join(cfgdir, 'dit_xl2_256.yaml'))
         model = instantiate_from_config(conf.model).eval()
         init_synthetic_(model.vit)
+        sd_cpu = {k: v.clone() for k, v in model.vit.state_dict().items()}
+        vp = model.vit
+        dit_arch = dict(patch_size=vp.arch['patch_size'], num_heads=vp.arch['num_heads'], depth=vp.arch['depth'],
+                        num_classes=vp.arch['num_classes'], out_channels=vp.arch['out_channels'],
+                        in_channels=vp.arch['in_channels'], input_size=vp.arch['input_size'])
         model = model.to(dev)
         B = args.batch or 32
         steps = args.respace_steps or 250
@@ -278,7 +325,8 @@ def build_workload(name, args, dev, rank):
             model(torch.zeros((2 * B, 4, 32, 32), device=dev), torch.zeros((2 * B, ), dtype=torch.long, device=dev),
                   torch.cat([y, torch.full_like(y, -1)]))
         return dict(metric=f'images/sec at DiT-XL/2 DDIMCFG-{steps} (s=3), latent 4x32x32, bs={B}', fold=fold,
-                    images=B, shape=shape, diffuser=diffuser, sd_cpu=None,
+                    images=B, shape=shape, diffuser=diffuser, sd_cpu=sd_cpu,
+                    cpu=dict(arch=dit_arch, batch=2, timed_steps=3, guidance_scale=3.0, clip=dp.clip_denoised),
                     handles=[(model.vit.native_handle(dev), 'dm_dit', len(diffuser.respaced_seq))],
                     workload=f'DDIMCFG-{steps} (s=3, eta=0, clip_denoised false) sampling fold, DiT-XL/2 (675M '
                              f'params, synthetic weights; cond + null-class rows as one 2B forward), latent 4x32x32, '
@@ -354,7 +402,8 @@ def main():
         wbytes, wsbytes = ctypes.c_int64(), ctypes.c_int64()
         _check(getattr(dmhip.load(), abi + '_memory')(h, ctypes.byref(wbytes), ctypes.byref(wsbytes)), abi + '_memory')
         wbytes_t += wbytes.value
-        wsbytes_t += wsbytes.value
+        # UNetCombined's two networks run over one shared scratch slab (dm_unet_share_workspace): count it once
+        wsbytes_t = max(wsbytes_t, wsbytes.value) if wl.get('shared_workspace') else wsbytes_t + wsbytes.value
         dmhip.unet_profile_enable(h, False, abi=abi)
 
     roof, total_gpu_ms, total_flops, fam = None, 0.0, 0.0, {}
@@ -390,11 +439,16 @@ def main():
         )
         if args.workload != 'c3':
             line['config']['bench_workload'] = args.workload
-        if world == 1 and not args.no_cpu_baseline and wl['sd_cpu'] is not None and args.workload == 'c3':
-            line['cpu_baseline'] = cpu_baseline(wl['sd_cpu'], args.cpu_batch, wl['denoise_steps'])
+        line['cpu_baseline'] = None
+        if world == 1 and not args.no_cpu_baseline and wl['sd_cpu'] is not None:
+            if args.workload in ('c2', 'c3'):
+                line['cpu_baseline'] = cpu_baseline(wl['sd_cpu'], args.cpu_batch, wl['denoise_steps'])
+            else:
+                c = wl['cpu']
+                line['cpu_baseline'] = cpu_baseline_cfg(args.workload, wl['sd_cpu'], c['arch'], c['batch'],
+                                                        wl['denoise_steps'], c['guidance_scale'], c['timed_steps'],
+                                                        clip=c.get('clip', True))
             line['gpu_over_cpu'] = round(line['value'] / line['cpu_baseline']['value'], 1)
-        else:
-            line['cpu_baseline'] = None
         if args.profile_json:
             with open(args.profile_json, 'w') as f:
                 json.dump(dict(families=fam, ops=prof), f, indent=1)

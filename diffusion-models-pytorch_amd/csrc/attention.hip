@@ -811,6 +811,29 @@ __global__ void __launch_bounds__(NW * 64) attn_flash_kernel(AttnArgs a) {
   __builtin_amdgcn_s_waitcnt(0xc07f);
   __builtin_amdgcn_wave_barrier();
   const int h = bh % a.heads, b = bh / a.heads;
+  if (a.o_split) {  // the output projection's pre-split A image: 8 columns (one k-group) per item, 2 x 16 B
+    const float ps = ldexpf(1.f, a.o_split_ea);
+    const int ng = Dh / 8;
+    bool bad = false;
+    for (int i = lane; i < 32 * ng; i += 64) {
+      const int q = i / ng, g8 = i - q * ng;
+      const int c = h * Dh + 8 * g8;
+      f16x8 hi, lo;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float x = st[q * OP + 8 * g8 + e] * ps;
+        const _Float16 h0 = (_Float16)x;
+        hi[e] = h0;
+        lo[e] = (_Float16)(x - (float)h0);
+        bad |= fabsf(x) > 65504.f;
+      }
+      _Float16* dst = a.o_split + ((size_t)b * L + q0 + q) * 2 * a.o_ld + (c >> 5) * 64 + ((c & 31) >> 3) * 8;
+      *reinterpret_cast<f16x8*>(dst) = hi;
+      *reinterpret_cast<f16x8*>(dst + 32) = lo;
+    }
+    if (bad && a.range_flag) *a.range_flag = 1;
+    return;
+  }
   float* out = a.out + ((size_t)b * L + q0) * a.ldo + h * Dh;
   for (int i = lane; i < 32 * Dh; i += 64) {
     const int q = i / Dh, d = i - q * Dh;
@@ -824,8 +847,11 @@ bool attn_flash_ok(int L, int Dh) { return L >= 64 && L % 64 == 0 && Dh % 8 == 0
 
 int attn_flash(const AttnArgs& a, hipStream_t st) {
   DM_REQUIRE(attn_flash_ok(a.L, a.Dh), "flash attention: L % 64 == 0 and head dims of 8 .. 80 (multiples of 8)");
-  DM_REQUIRE(a.pq && a.pk && a.pv && a.out && a.B > 0 && a.heads > 0 && a.ldo % 4 == 0,
+  DM_REQUIRE(a.pq && a.pk && a.pv && (a.out || a.o_split) && a.B > 0 && a.heads > 0 && a.ldo % 4 == 0,
              "flash attention: needs the pre-split operand planes and an output");
+  DM_REQUIRE(!a.o_split || (a.o_ld % 32 == 0 && a.o_ld >= a.heads * a.Dh &&
+                            (reinterpret_cast<uintptr_t>(a.o_split) & 15) == 0),
+             "flash attention: the pre-split output image needs 32-column groups, 16-byte aligned");
   DM_REQUIRE(((reinterpret_cast<uintptr_t>(a.pq) | reinterpret_cast<uintptr_t>(a.pk) |
                reinterpret_cast<uintptr_t>(a.pv)) & 15) == 0, "flash attention: 16-byte aligned planes");
   const int nw = a.L % 256 == 0 ? 8 : 2;

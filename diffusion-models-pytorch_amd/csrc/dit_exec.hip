@@ -298,7 +298,14 @@ int DiTModel::build_plan(Plan& pl, int B) {
       }
       g.ws = it->second;
       g.ws_rowscale = split_conv_rowscale(it->second, 1, g.N, g.K);
-      if (!linear_k32_ok(g)) {
+      // with the pre-split A image (add_token_gemm) the GEMM takes no prologue: check that form
+      GemmArgs probe = g;
+      if (presplit_on && g.pick_M >= 4096 && !probe.c_split) {
+        probe.ln_stats = nullptr;
+        probe.pro_scale = probe.pro_shift = nullptr;
+        probe.as = reinterpret_cast<const _Float16*>(uintptr_t(256));  // only its alignment is checked
+      }
+      if (!linear_k32_ok(probe)) {
         g.ws = nullptr;
         g.ws_rowscale = nullptr;
       }
@@ -369,6 +376,11 @@ int DiTModel::build_plan(Plan& pl, int B) {
       at.out = Ob; at.ldo = D;
       at.ea = 6; at.eb = 6; at.ep = 14; at.ev = 6;
       at.range_flag = range_flag;
+      if (presplit_on && D % 32 == 0) {   // O straight into the proj GEMM's pre-split A image (over Ob)
+        at.o_split = reinterpret_cast<_Float16*>(Ob);
+        at.o_split_ea = 6;
+        at.o_ld = D;
+      }
       pl.add("attn_flash_kernel<" + std::to_string(Dh) + ">", 4.0 * B * heads * (double)T * T * Dh,
              4.0 * M * (3.0 * D + D), [=](hipStream_t st) { return attn_flash(at, st); });
     } else {
@@ -398,7 +410,12 @@ int DiTModel::build_plan(Plan& pl, int B) {
       GemmArgs g = linear(Ob, D, M, bp.proj_w, bp.proj_b, D, D, x, D);
       g.res = x; g.ld_res = D; g.gate = mb + 2 * D; g.gate_pitch = ada_total; g.gate_rows = T;
       split(g, 6, bp.proj_w, (size_t)D * D, 0);
-      add_token_gemm(g);
+      GemmArgs gp = g;
+      gp.as = reinterpret_cast<const _Float16*>(Ob);
+      if (flash && presplit_on && D % 32 == 0 && g.ws && g.split_ea == 6 && linear_k32_ok(gp))
+        add_gemm(gp);   // A = the flash kernel's pre-split O image
+      else
+        add_token_gemm(g);
     }
     // MLP branch
     stats_op();

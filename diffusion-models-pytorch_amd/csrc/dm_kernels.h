@@ -307,6 +307,11 @@ struct AttnArgs {
   int fuse_proj;
   ConvArgs proj;
   int proj_staged;  // set by attn_fused: proj runs the LDS-staged 16-B epilogue (staged_epilogue_ok)
+  // flash kernel only: O written as the next GEMM's pre-split A image instead of fp32 rows (linear_k32 PRO 3:
+  // [B L][o_ld / 32][piece][4][8] fp16 of O * 2^o_split_ea, linear_presplit_a's expressions; head h at
+  // columns h Dh ..): the output projection reads it without a split pass
+  _Float16* o_split;
+  int o_split_ea, o_ld;
 };
 bool attn_fused_ok(int L, int Dh);
 int attn_fused(const AttnArgs& a, hipStream_t st);

@@ -176,6 +176,55 @@ __global__ void gn_finalize_kernel(const double2* __restrict__ part, int B, int 
   shift[idx] = sh;
 }
 
+// Wide maps (more than kGnWideChunks chunk partials per image: ADM's 64^2 .. 256^2 maps, up to 1024): one
+// thread per (image, channel) walking every chunk serially left B * C threads with ~1k dependent fp64
+// loads each (134 us per launch at B = 4, 256^2). Here 32 lanes of a wave reduce one (image, group) --
+// chunk k on lane k % 32, then a fixed shuffle tree -- and the group's channels take the result: the
+// same expressions from the totals on, a different (fixed) fp64 summation order.
+constexpr int kGnWideChunks = 64;
+__global__ void __launch_bounds__(256) gn_finalize_wide_kernel(const double2* __restrict__ part, int B, int nchunk,
+                                                               int G, int C, double n, float eps,
+                                                               const float* __restrict__ gamma,
+                                                               const float* __restrict__ beta,
+                                                               const float* __restrict__ mod_scale,
+                                                               const float* __restrict__ mod_shift, int mod_pitch,
+                                                               float* __restrict__ scale, float* __restrict__ shift) {
+  const int lane = threadIdx.x & 31;
+  const int bg = blockIdx.x * 8 + (threadIdx.x >> 5);   // (image, group)
+  if (bg >= B * G) return;
+  const int b = bg / G, g = bg - b * G;
+  double a = 0, q = 0;
+  for (int k = lane; k < nchunk; k += 32) {
+    const double2 v = part[((size_t)b * nchunk + k) * G + g];
+    a += v.x;
+    q += v.y;
+  }
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 32);
+    q += __shfl_xor(q, o, 32);
+  }
+  const double m = a / n;
+  double var = q / n - m * m;
+  if (var < 0) var = 0;
+  const float mu = (float)m;
+  const float rs = (float)(1.0 / sqrt(var + (double)eps));
+  const int cpg = C / G;
+  for (int j = lane; j < cpg; j += 32) {
+    const int c = g * cpg + j;
+    const size_t idx = (size_t)b * C + c;
+    float sc = rs * (gamma ? gamma[c] : 1.0f);
+    float sh = -sc * mu + (beta ? beta[c] : 0.0f);
+    if (mod_scale) {
+      const float f = 1.0f + mod_scale[(size_t)b * mod_pitch + c];
+      sc = sc * f;
+      sh = sh * f + (mod_shift ? mod_shift[(size_t)b * mod_pitch + c] : 0.0f);
+    }
+    scale[idx] = sc;
+    shift[idx] = sh;
+  }
+}
+
 inline int gn_block_threads(int C) {
   int C4 = C / 4;
   int t = C4 > 256 ? C4 : 256;
@@ -246,6 +295,13 @@ int gn_finalize(const View& x, int G, const double2* part, float eps, const floa
   DM_REQUIRE(x.C % G == 0, "GroupNorm finalize: C must be divisible by groups");
   const int HW = x.H * x.W;
   const int n = x.B * x.C;
+  if (gn_num_chunks(HW) > kGnWideChunks) {
+    hipLaunchKernelGGL(gn_finalize_wide_kernel, dim3(ceil_div(x.B * G, 8)), dim3(256), 0, st, part, x.B,
+                       gn_num_chunks(HW), G, x.C, (double)HW * (x.C / G), eps, gamma, beta, mod_scale, mod_shift,
+                       mod_pitch, scale, shift);
+    DM_LAUNCH_CHECK();
+    return DM_OK;
+  }
   hipLaunchKernelGGL(gn_finalize_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, st, part, x.B, gn_num_chunks(HW), G,
                      x.C, (double)HW * (x.C / G), eps, gamma, beta, mod_scale, mod_shift, mod_pitch, scale, shift);
   DM_LAUNCH_CHECK();

@@ -23,7 +23,8 @@ def test_conversions_vs_reference(cuda, golden, case):
     """pred_x0_from_eps / pred_eps_from_x0 / pred_x0_from_v / pred_eps_from_v / get_v / diffuse on the engine
     (dm_lincomb): bit-identical to the oracle's torch CPU expressions on this host, within a few ulp of the
     reference outputs generated on the build container's CPU (host-dependent 0-dim pow rounding: a 1-ulp
-    coefficient difference times sqrt(1/ac) ~ 160 at t = 999 is a few 1e-8 relative)."""
+    coefficient difference times sqrt(1/ac) ~ 160 at t = 999, or divided by sqrt(1/ac - 1) ~ 0.01 at t = 0, is
+    within 1e-6 of the output's scale)."""
     from oracle import diffusion as od
     g, meta = golden('convert')
     c = meta['cases'][case]
@@ -36,7 +37,7 @@ def test_conversions_vs_reference(cuda, golden, case):
     def check(got, ref, gold):
         got = got.cpu().numpy()
         assert np.array_equal(got, ref.numpy()), np.abs(got - ref.numpy()).max()
-        assert np.allclose(got, gold, rtol=1e-6, atol=1e-7), np.abs(got - gold).max()
+        assert np.abs(got - gold).max() <= 1e-6 * np.abs(gold).max() + 1e-7, np.abs(got - gold).max()
     check(d.diffuse(X0, tvec.to(cuda), EPS), od.diffuse(ac, x0, tvec, eps), g[f'{case}_diffuse'])
     check(d.get_v(X0, EPS, tvec.to(cuda)), od.get_v(ac, x0, eps, tvec), g[f'{case}_get_v'])
     for t in c['ts']:

@@ -80,7 +80,8 @@ if __name__ == '__main__':
     ap = argparse.ArgumentParser()
     ap.add_argument('--which', default='both')
     ap.add_argument('--iters', type=int, default=3)
+    ap.add_argument('--modes', default='flash,unfused')
     a = ap.parse_args()
     for w in (['dit', 'adm'] if a.which == 'both' else [a.which]):
-        for mode in ('flash', 'unfused'):
+        for mode in a.modes.split(','):
             run(w, mode, a.iters)

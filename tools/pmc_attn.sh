@@ -1,0 +1,15 @@
+#!/bin/bash
+# Two SQ PMC passes over the DiT-XL/2 C5 forward (tools/attn_bench.py, flash mode), summarised per kernel
+# into gpurun_out/pmc_attn.json (tools/pmc_summary.py).
+cd "$(dirname "$0")/.." || exit 2
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+A="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE"
+B="SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_VALU_MFMA_COEXEC_CYCLES SQ_BUSY_CU_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"
+D=gpurun_out/pmc_attn
+timeout -s KILL 120 rocprofv3 --pmc $A --kernel-trace -d ${D}_a -o pmc -- \
+    python3 tools/attn_bench.py --which ${WHICH:-dit} --modes flash --iters 1 > ${D}_a.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc $B --kernel-trace -d ${D}_b -o pmc -- \
+    python3 tools/attn_bench.py --which ${WHICH:-dit} --modes flash --iters 1 > ${D}_b.log 2>&1 || exit $?
+python3 tools/pmc_summary.py ${D}.json $(find ${D}_a ${D}_b -name '*.db') > ${D}.txt 2>&1
+grep -A20 "attn_flash" ${D}.txt
