@@ -627,11 +627,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 // O^T rows >= Dh read clamped V rows and are not stored. Each wave owns 32 queries; NW waves per block.
 // Not bit-identical to the unfused path (exp2 and the online rescale round differently): within a few ulp of
 // the unfused softmax (tests/test_gpu_r3.py test_flash_attention_vs_unfused).
-template <int DHP, int NW>
+template <int Dh, int NW>
 __global__ void __launch_bounds__(NW * 64) attn_flash_kernel(AttnArgs a) {
+  constexpr int DHP = (Dh + 15) / 16 * 16;   // contraction depth of S (16-deep slices)
   constexpr int KB = 64;                     // keys per block
   constexpr int NS = DHP / 16;               // 16-deep slices of the S contraction
-  constexpr int KP = DHP == 80 ? 168 : 136;  // fp16 pitch of a K row (2 DHP + pad: 84 / 68 dwords = 4 x odd)
+  constexpr int KP = DHP == 80 ? 168 : DHP == 48 ? 104 : DHP == 32 ? 72 : 136;  // fp16 pitch of a K row:
+                                             // 2 DHP + pad, 4 x an odd number of dwords (conflict-free reads)
   constexpr int VP = 136;                    // fp16 pitch of a V^T row (64 keys x 2 pieces + pad: 68 dwords)
   constexpr int NDT = (DHP + 31) / 32;       // 32-row d tiles of O^T
   constexpr int KBUF = KB * KP, VBUF = DHP * VP, BUF = KBUF + VBUF;
@@ -641,7 +643,7 @@ __global__ void __launch_bounds__(NW * 64) attn_flash_kernel(AttnArgs a) {
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int lr = lane & 31, lh = lane >> 5;
-  const int L = a.L, Dh = a.Dh;
+  const int L = a.L;
   const int nqb = L / (32 * NW);
   const int bid = xcd_remap_p(blockIdx.x, gridDim.x);
   const int qb = bid % nqb, bh = bid / nqb;
@@ -665,8 +667,8 @@ __global__ void __launch_bounds__(NW * 64) attn_flash_kernel(AttnArgs a) {
     }
 
   // loaders: K chunks (row, piece, 8 d) and V^T chunks (d row, piece, 8 keys), 16 B each, into registers
-  const int dh8 = Dh / 8;
-  const int nkc = 2 * KB * dh8, nvc = 2 * Dh * (KB / 8);
+  constexpr int dh8 = Dh / 8;
+  constexpr int nkc = 2 * KB * dh8, nvc = 2 * Dh * (KB / 8);
   constexpr int CK = (2 * KB * (DHP / 8) + NT - 1) / NT, CV = (2 * DHP * (KB / 8) + NT - 1) / NT;
   f4 rk[CK], rv[CV];
   auto load_blk = [&](int kb) {
@@ -799,7 +801,7 @@ __global__ void __launch_bounds__(NW * 64) attn_flash_kernel(AttnArgs a) {
   // O = O^T / l (x 2^-(ep + ev)), staged through LDS as [32 queries][Dh + 1] fp32 rows per wave, stored as rows
   const float l_tot = l_run + __shfl_xor(l_run, 32);
   const float scale = ldexpf(1.f, -(a.ep + a.ev)) / l_tot;
-  const int OP = Dh + 1;
+  constexpr int OP = Dh + 1;
   float* st = reinterpret_cast<float*>(lds) + wave * 32 * OP;
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt)
@@ -813,7 +815,7 @@ __global__ void __launch_bounds__(NW * 64) attn_flash_kernel(AttnArgs a) {
   const int h = bh % a.heads, b = bh / a.heads;
   if (a.o_split) {  // the output projection's pre-split A image: 8 columns (one k-group) per item, 2 x 16 B
     const float ps = ldexpf(1.f, a.o_split_ea);
-    const int ng = Dh / 8;
+    constexpr int ng = Dh / 8;
     bool bad = false;
     for (int i = lane; i < 32 * ng; i += 64) {
       const int q = i / ng, g8 = i - q * ng;
@@ -843,10 +845,18 @@ __global__ void __launch_bounds__(NW * 64) attn_flash_kernel(AttnArgs a) {
 
 }  // namespace
 
-bool attn_flash_ok(int L, int Dh) { return L >= 64 && L % 64 == 0 && Dh % 8 == 0 && Dh >= 8 && Dh <= 80; }
+bool attn_flash_ok(int L, int Dh) {
+  return L >= 64 && L % 64 == 0 && (Dh == 32 || Dh == 64 || Dh == 72 || Dh == 80);
+}
+
+template <int DH>
+static void launch_flash(const AttnArgs& a, unsigned blocks, bool nw8, hipStream_t st) {
+  if (nw8) hipLaunchKernelGGL((attn_flash_kernel<DH, 8>), dim3(blocks), dim3(512), 0, st, a);
+  else hipLaunchKernelGGL((attn_flash_kernel<DH, 2>), dim3(blocks), dim3(128), 0, st, a);
+}
 
 int attn_flash(const AttnArgs& a, hipStream_t st) {
-  DM_REQUIRE(attn_flash_ok(a.L, a.Dh), "flash attention: L % 64 == 0 and head dims of 8 .. 80 (multiples of 8)");
+  DM_REQUIRE(attn_flash_ok(a.L, a.Dh), "flash attention: L % 64 == 0 and head dims 32, 64, 72 or 80");
   DM_REQUIRE(a.pq && a.pk && a.pv && (a.out || a.o_split) && a.B > 0 && a.heads > 0 && a.ldo % 4 == 0,
              "flash attention: needs the pre-split operand planes and an output");
   DM_REQUIRE(!a.o_split || (a.o_ld % 32 == 0 && a.o_ld >= a.heads * a.Dh &&
@@ -854,14 +864,13 @@ int attn_flash(const AttnArgs& a, hipStream_t st) {
              "flash attention: the pre-split output image needs 32-column groups, 16-byte aligned");
   DM_REQUIRE(((reinterpret_cast<uintptr_t>(a.pq) | reinterpret_cast<uintptr_t>(a.pk) |
                reinterpret_cast<uintptr_t>(a.pv)) & 15) == 0, "flash attention: 16-byte aligned planes");
-  const int nw = a.L % 256 == 0 ? 8 : 2;
-  const unsigned blocks = (unsigned)((long)a.B * a.heads * (a.L / (32 * nw)));
-  if (a.Dh > 64) {
-    if (nw == 8) hipLaunchKernelGGL((attn_flash_kernel<80, 8>), dim3(blocks), dim3(512), 0, st, a);
-    else hipLaunchKernelGGL((attn_flash_kernel<80, 2>), dim3(blocks), dim3(128), 0, st, a);
-  } else {
-    if (nw == 8) hipLaunchKernelGGL((attn_flash_kernel<64, 8>), dim3(blocks), dim3(512), 0, st, a);
-    else hipLaunchKernelGGL((attn_flash_kernel<64, 2>), dim3(blocks), dim3(128), 0, st, a);
+  const bool nw8 = a.L % 256 == 0;
+  const unsigned blocks = (unsigned)((long)a.B * a.heads * (a.L / (32 * (nw8 ? 8 : 2))));
+  switch (a.Dh) {
+    case 32: launch_flash<32>(a, blocks, nw8, st); break;
+    case 64: launch_flash<64>(a, blocks, nw8, st); break;
+    case 72: launch_flash<72>(a, blocks, nw8, st); break;
+    default: launch_flash<80>(a, blocks, nw8, st); break;
   }
   DM_LAUNCH_CHECK();
   return DM_OK;
