@@ -49,6 +49,21 @@ def check_free_running(got, ref32, ref64, drift, i):
     return e32, e64
 
 
+def check_chaos_envelope(golden, name, worst64, report, key):
+    """The engine's free-running distance to the float64 trajectory (max over steps) against the spread of
+    the REFERENCE's own fp32 runs with the model output perturbed at the level the engine's forwards differ
+    from the reference's (2^-20 relative, 8 seeds; tests/golden/chaos.npz, make_golden_r3.py make_chaos):
+    it must lie inside that envelope (<= the worst perturbed run). Reports where it lies: the fraction of
+    perturbed reference runs that end further from float64 than the engine does."""
+    import numpy as np
+    g, _ = golden('chaos')
+    runs = g[f'{name}_e64_p20'].max(axis=1)
+    report(f'{key}_chaos_envelope_2^-20_max', float(runs.max()))
+    report(f'{key}_chaos_envelope_2^-22_max', float(g[f'{name}_e64_p22'].max()))
+    report(f'{key}_perturbed_reference_runs_further_than_engine', float(np.mean(runs > worst64)))
+    assert worst64 <= max(TOL, float(runs.max())), (worst64, list(runs))
+
+
 @pytest.fixture(scope='session')
 def golden():
     cache = {}

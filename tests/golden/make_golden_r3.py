@@ -190,7 +190,81 @@ def make_dit():
     mg.save('dit_r3', meta, **arr)
 
 
+class _Perturbed:
+    """The fp32 reference module with its output multiplied by (1 + 2^ex s), s a seeded +-1 pattern: ex = -22
+    is the rounding level of the fp32 forward itself (one ulp is 2^-23 relative), ex = -20 the level at
+    which the engine's forwards differ from the reference's (~1e-6 relative, tests/test_gpu_parity.py)."""
+
+    def __init__(self, model, seed, ex):
+        self.m, self.g, self.ex = model, torch.Generator().manual_seed(1000 + seed), ex
+
+    def __call__(self, *a, **k):
+        out = self.m(*a, **k)
+        s = torch.randint(0, 2, out.shape, generator=self.g).float() * 2 - 1
+        return out * (1 + s * 2.0 ** self.ex)
+
+
+def make_chaos():
+    """chaos.npz -- how far free-running fp32 trajectories of the REFERENCE scatter around its float64 one
+    when only the last bits of the model output change: each drift.npz trajectory (ADM UNetCombined
+    DDIMCFG-6, AdaGN DDIMCFG-10, inversion + reconstruction) re-run by the reference in fp32 with the
+    model output perturbed by 2^-22 and by 2^-20 relative (_Perturbed), 8 seeds each; per seed and step the
+    max-abs distance to the float64 trajectory (drift.npz *_sample64): `<name>_e64_p22`, `<name>_e64_p20`.
+    An engine whose forward differs from the reference's at the 2^-20 level lands inside that spread, not
+    at the unperturbed fp32 run's distance."""
+    torch.set_num_threads(8)
+    schedule, ddpm, ddim, unet = mg.import_reference()
+    import models.unet_categorial_adagn as ua  # noqa: E402
+    import models.adm.unet_combined as admc  # noqa: E402
+    drift, adm = _load('drift'), _load('adm')
+    meta = _common()
+    arr = {}
+    seeds = 8
+
+    def run(name, model, loop_fn, init, traj64):
+        for ex in (-22, -20):
+            e = np.zeros((seeds, len(traj64)))
+            for s in range(seeds):
+                pm = _Perturbed(model, s, ex)
+                with torch.no_grad():
+                    for i, out in enumerate(loop_fn(pm, init)):
+                        e[s, i] = float((out['sample'].double() - torch.from_numpy(traj64[i]).double()).abs().max())
+            arr[f'{name}_e64_p{-ex}'] = e
+            print(name, f'2^{ex}-perturbed fp32 reference vs float64, max over steps per seed',
+                  ['%.2e' % v for v in e.max(1)], flush=True)
+
+    comb = admc.UNetCombined(**mg.ADM_ARCHS['adm_tiny']).eval()
+    meta['combined_tiny_weights_sha256'] = mg.synthetic(comb)
+    d = ddim.DDIMCFG(guidance_scale=2.5, respace_type='uniform', respace_steps=6, eta=0.0)
+    labels = torch.from_numpy(adm['ddpm8_labels'])
+    run('cfg6', comb, lambda m, x: d.sample_loop(m, x, model_kwargs=dict(y=labels), tqdm_kwargs=dict(disable=True)),
+        torch.from_numpy(adm['cfg6_init']), drift['cfg6_sample64'])
+    model = ua.UNetCategorialAdaGN(**mg.ADAGN_ARCHS['tiny_updown']).eval()
+    meta['tiny_updown_weights_sha256'] = mg.synthetic(model)
+    d2 = ddim.DDIMCFG(guidance_scale=3.0, respace_type='uniform', respace_steps=10, eta=0.0)
+    torch.manual_seed(5)
+    init = torch.randn((2, 3, 16, 16))
+    run('adagn_cfg10', model, lambda m, x: d2.sample_loop(m, x, model_kwargs=dict(y=torch.tensor([1, 4])),
+                                                          tqdm_kwargs=dict(disable=True)),
+        init, drift['adagn_cfg10_sample64'])
+    model = unet.UNet(**mg.ARCHS['tiny']).eval()
+    meta['tiny_weights_sha256'] = mg.synthetic(model)
+    d3 = ddim.DDIM(respace_type='uniform', respace_steps=5, eta=0.0)
+    g = torch.Generator().manual_seed(31)
+    img = torch.rand((2, 3, 16, 16), generator=g) * 2 - 1
+
+    def inv_rec(m, x):
+        for out in d3.sample_inversion_loop(m, x, tqdm_kwargs=dict(disable=True)):
+            x = out['sample']
+            yield out
+        yield from d3.sample_loop(m, x, tqdm_kwargs=dict(disable=True))
+    run('invrec', model, inv_rec, img, drift['invrec_sample64'])
+    meta['perturbation'] = 'model output * (1 + 2^ex s), ex in (-22, -20), s = +-1 from torch.Generator(1000 + seed)'
+    meta['seeds'] = seeds
+    mg.save('chaos', meta, **arr)
+
+
 if __name__ == '__main__':
-    which = sys.argv[1:] or ['convert', 'stepacc', 'dit']
+    which = sys.argv[1:] or ['convert', 'stepacc', 'dit', 'chaos']
     for w in which:
-        dict(convert=make_convert, stepacc=make_stepacc, dit=make_dit)[w]()
+        dict(convert=make_convert, stepacc=make_stepacc, dit=make_dit, chaos=make_chaos)[w]()

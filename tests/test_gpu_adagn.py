@@ -82,7 +82,7 @@ def test_ddimcfg_trajectory_vs_reference(cuda, golden, report, batched):
     """DDIMCFG-10 (s = 3). Every step is checked teacher-forced (from the reference's previous
     sample) against the 1e-4 bound, and free-running with tests/conftest.py check_free_running
     (tests/golden/drift.npz adagn_cfg10: the reference's fp32 and float64 runs)."""
-    from tests.conftest import check_free_running
+    from tests.conftest import check_chaos_envelope, check_free_running
     dg = golden('drift')[0]
     drift = dg['adagn_cfg10_drift_sample']
     g, meta = golden('adagn')
@@ -103,12 +103,14 @@ def test_ddimcfg_trajectory_vs_reference(cuda, golden, report, batched):
         err = float(np.abs(out['sample'].cpu().numpy() - g[f'cfg_step{i}_sample']).max())
         worst_step = max(worst_step, err)
         assert err <= TOL, (i, err)
-    worst = 0.0
+    worst, worst64 = 0.0, 0.0
     for i, out in enumerate(d.sample_loop(model, init, model_kwargs=dict(y=labels))):
-        e32, _ = check_free_running(out['sample'].cpu().numpy(), g[f'cfg_step{i}_sample'],
-                                    dg['adagn_cfg10_sample64'][i], drift, i)
-        worst = max(worst, e32)
+        e32, e64 = check_free_running(out['sample'].cpu().numpy(), g[f'cfg_step{i}_sample'],
+                                      dg['adagn_cfg10_sample64'][i], drift, i)
+        worst, worst64 = max(worst, e32), max(worst64, e64)
     tag = 'batched' if batched else 'two_calls'
+    report(f'ddimcfg10_adagn_{tag}_free_running_maxabs_vs_reference_float64', worst64)
+    check_chaos_envelope(golden, 'adagn_cfg10', worst64, report, f'ddimcfg10_adagn_{tag}')
     report(f'ddimcfg10_adagn_{tag}_single_step_maxabs_vs_reference', worst_step)
     report(f'ddimcfg10_adagn_{tag}_free_running_maxabs_vs_reference', worst)
 

@@ -111,7 +111,7 @@ def test_adm_combined_ddimcfg_trajectory(cuda, golden, report):
     sample) <= 1e-4; free-running, tests/conftest.py check_free_running: the reference's own fp32 run
     drifts 1.6e-4 from its float64 run on this trajectory (x0 = sqrt(1/a_t) x - ... with
     sqrt(1/a_t) ~ 160 at t = 996, times the (2s - 1) CFG gain; tests/golden/drift.npz cfg6)."""
-    from tests.conftest import check_free_running
+    from tests.conftest import check_chaos_envelope, check_free_running
     dg = golden('drift')[0]
     drift = dg['cfg6_drift_sample']
     g, meta = golden('adm')
@@ -144,6 +144,7 @@ def test_adm_combined_ddimcfg_trajectory(cuda, golden, report):
     report('adm_combined_ddimcfg6_free_running_maxabs_vs_reference', worst)
     report('adm_combined_ddimcfg6_free_running_maxabs_vs_reference_float64', worst64)
     report('adm_combined_ddimcfg6_reference_fp32_vs_fp64_drift', float(drift.max()))
+    check_chaos_envelope(golden, 'cfg6', worst64, report, 'adm_combined_ddimcfg6')
 
 
 @pytest.mark.gpu

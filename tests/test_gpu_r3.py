@@ -320,23 +320,30 @@ def test_gpu_library_is_built_from_this_tree(cuda):
 
 
 # ------------------------------------------------------------------ flash attention (attention.hip)
-@pytest.mark.parametrize('case', ['adm_tiny', 'dit_s2', 'dit_xl2', 'adm256'])
+@pytest.mark.parametrize('case', ['adm_tiny', 'dit_s2', 'dit_xl2', 'adm256', 'adagn'])
 def test_flash_attention_vs_unfused(cuda, golden, report, monkeypatch, case):
     """attn_flash_kernel (online softmax, S never in HBM) against the unfused S GEMM -> softmax_rows -> PV
     GEMM path it replaces, which stays as the test oracle: ADM's 8^2 blocks (adm_tiny: L = 64, heads of 32,
     zero-padded to a 64-deep contraction), DiT-S/2 at 16^2 latents (L = 64, heads of 64), DiT-XL/2 (L = 256,
     16 heads of 72: an 80-deep contraction, 96-row output tiles), the guided-diffusion 256^2 UNet (L = 1024 at
-    32^2 and L = 64 at 8^2, heads of 64). Forwards within 1e-5 of each other (the attention core alone
-    differs by exp2 vs expf and the online rescaling, a few 1e-7 relative)."""
+    32^2 and L = 64 at 8^2, heads of 64), CFG-CIFAR AdaGN (8^2 blocks, heads of 64). Forwards within 1e-5 of
+    each other (the attention core alone differs by exp2 vs expf and the online rescaling, a few 1e-7
+    relative)."""
     from models.adm.unet import UNetModel
     from models.dit.model import DiT
+    from models.unet_categorial_adagn import UNetCategorialAdaGN
     outs = {}
     for mode in ('flash', 'unfused'):
         if mode == 'unfused':
             monkeypatch.setenv('DM_ATTN_NO_FLASH', '1')
             monkeypatch.setenv('DM_DIT_ATTN_UNFUSED', '1')
         gen = torch.Generator().manual_seed(21)
-        if case.startswith('adm'):
+        if case == 'adagn':
+            m = UNetCategorialAdaGN(**golden('adagn')[1]['archs']['cfg_cifar10']).eval()
+            B = 2
+            x = torch.randn((B, 3, 32, 32), generator=gen)
+            y = torch.tensor([1, 3])
+        elif case.startswith('adm'):
             arch = golden('adm')[1]['archs']['adm_tiny' if case == 'adm_tiny' else 'adm256_combined']
             m = UNetModel(**arch).eval()
             S, B = arch['image_size'], 2 if case == 'adm_tiny' else 1

@@ -86,7 +86,7 @@ def test_ddim_inversion_reconstruction_trajectory(cuda, golden, report):
     check_free_running. x0 = sqrt(1/ac_t) x - ... amplifies a 1e-6 forward difference by up to ~160 at
     t ~ 960 and the reference's own fp32 run drifts 3e-4 from its float64 run here
     (tests/golden/drift.npz invrec, make_golden_r2.py)."""
-    from tests.conftest import check_free_running
+    from tests.conftest import check_chaos_envelope, check_free_running
     dg = golden('drift')[0]
     drift = dg['invrec_drift_sample']
     from diffusions import DDIM
@@ -111,22 +111,24 @@ def test_ddim_inversion_reconstruction_trajectory(cuda, golden, report):
         err = np.abs(out['sample'].cpu().numpy() - arrays[f'rec_step{i}_sample']).max()
         forced = max(forced, err)
         assert err <= TOL, ('rec', i, err)
-    free = 0.0
+    free, free64 = 0.0, 0.0
     x = ref('img')
     for i, out in enumerate(d.sample_inversion_loop(model, x, tqdm_kwargs=dict(disable=True))):
-        err, _ = check_free_running(out['sample'].cpu().numpy(), arrays[f'inv_step{i}_sample'],
-                                    dg['invrec_sample64'][i], drift, i)
-        free = max(free, err)
+        err, e64 = check_free_running(out['sample'].cpu().numpy(), arrays[f'inv_step{i}_sample'],
+                                      dg['invrec_sample64'][i], drift, i)
+        free, free64 = max(free, err), max(free64, e64)
         x = out['sample']
     n_inv = i + 1
     assert n_inv == meta['inv_steps']
     for i, out in enumerate(d.sample_loop(model, x, tqdm_kwargs=dict(disable=True))):
-        err, _ = check_free_running(out['sample'].cpu().numpy(), arrays[f'rec_step{i}_sample'],
-                                    dg['invrec_sample64'][n_inv + i], drift, n_inv + i)
-        free = max(free, err)
+        err, e64 = check_free_running(out['sample'].cpu().numpy(), arrays[f'rec_step{i}_sample'],
+                                      dg['invrec_sample64'][n_inv + i], drift, n_inv + i)
+        free, free64 = max(free, err), max(free64, e64)
     report('ddim_inversion_reconstruction_tiny_teacher_forced_maxabs_vs_reference', forced)
     report('ddim_inversion_reconstruction_tiny_free_running_maxabs_vs_reference', free)
     report('ddim_inversion_reconstruction_tiny_reference_fp32_vs_fp64_drift', float(drift.max()))
+    report('ddim_inversion_reconstruction_tiny_free_running_maxabs_vs_float64', free64)
+    check_chaos_envelope(golden, 'invrec', free64, report, 'ddim_inversion_reconstruction_tiny')
 
 
 def test_sample_uncond_reconstruction(cuda, tmp_path):
