@@ -43,6 +43,10 @@ __device__ int g_lin_stamp_k;
 #define LIN_RSTAMP(k) do {} while (0)
 #endif
 
+#ifndef DM_LIN_ABL
+#define DM_LIN_ABL 0
+#endif
+
 constexpr int kLP = 144;   // LDS row pitch in fp16 (288 B) of one 64-channel stage
 constexpr int kLBM = 128;  // block rows
 constexpr int kLGM = 4;    // M tiles per group of the tile order
@@ -277,25 +281,39 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm = wave / NWN, wn = wave % NWN;
   const int l16 = lane & 15, q = lane >> 4;
-  const int lrow = t >> 1, lh = t & 1;  // loader: row, 32-channel half of the stage (= K32 step)
 
-  // ---- A loader: row lrow of the tile, channels 64 st + 32 lh .. + 31
+  constexpr bool TABS = PRO == 1 || PRO == 2;
+  const int rows_img = PRO == 1 ? g.pro_rows : PRO == 2 ? g.ln_rows : 1;  // rows per image >= 128
+  const int img0 = TABS ? m0 / rows_img : 0;
+  // PRO 3 A loader: 16-B slot a3s = t & 15 (8 fp16 of one piece and k-group) of the stage's 256-B row span
+  // in tile rows a3r + 16 u, u = 0 .. 7 -- every wave instruction reads 4 whole row spans (8 cache lines)
+  // instead of 16 B of 64 different lines, as a row-half per thread did: those A refills cost 25 % of the
+  // DiT GEMMs' time (DM_LIN_ABL=2; fc1 / fc2 at 2B = 64: 663 -> 512 us). The in-GEMM prologues (PRO 0-2,
+  // fp32 A) keep the row-half mapping: the same remap spills them past 256 VGPRs.
+  const int a3s = t & 15, a3r = t >> 4;
+  const f4* asp = PRO == 3 ? reinterpret_cast<const f4*>(g.as) + a3s : nullptr;
+  const size_t a3pitch = (size_t)K / 4;  // f4 per pre-split row
+  const int lrow = t >> 1, lh = t & 1;  // PRO 0-2 loader: row, 32-channel half of the stage (= K32 step)
   const int am = min(m0 + lrow, M - 1);  // rows >= M: clamped, never stored
   const float* asrc = g.A + (size_t)am * g.lda + 32 * lh;
-  constexpr bool TABS = PRO == 1 || PRO == 2;
-  const int rows_img = PRO == 1 ? g.pro_rows : PRO == 2 ? g.ln_rows : 1;
-  const int img0 = TABS ? m0 / rows_img : 0;
-  const int aimg = TABS ? am / rows_img - img0 : 0;  // 0 or 1 (rows per image >= 128)
-  const f4* asp = PRO == 3 ? reinterpret_cast<const f4*>(g.as + (size_t)am * 2 * K) + 8 * lh : nullptr;
+  const int aimg = TABS ? am / rows_img - img0 : 0;  // 0 or 1
   const float2 lns = PRO == 2 ? g.ln_stats[am] : make_float2(0.f, 1.f);
   const float apow = ldexpf(1.f, g.split_ea);
   f4 ra[2][8];  // A rows of two stages in flight (stage s in ra[s & 1])
   f4 rt;  // threads 0 .. 63: one f4 of a stage's tables
   const int ti = t >> 4, tk = (t & 15) * 4;  // table loader: (image, scale | shift) pair ti, channels tk
   auto load_a = [&](f4 (&dst)[8], int st) {
-    if (PRO == 3) {  // the step's 64 fp16 (two pieces x 4 k-groups x 8) as 8 x 16 B
+    // whole tiles (the usual case) address their rows linearly from one per-lane base; the last, partial
+    // tile clamps each row
+    if (PRO == 3) {  // slot a3s of the stage's 256 B in 8 rows
+      if (m0 + kLBM <= M) {
+        const f4* b0 = asp + (size_t)(m0 + a3r) * a3pitch + 16 * st;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) dst[u] = asp[16 * st + u];
+        for (int u = 0; u < 8; ++u) dst[u] = b0[(size_t)(16 * u) * a3pitch];
+      } else {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) dst[u] = asp[(size_t)min(m0 + a3r + 16 * u, M - 1) * a3pitch + 16 * st];
+      }
       return;
     }
     const float* p = asrc + 64 * st;
@@ -318,12 +336,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   bool bad = false;
   // prologue + split + LDS store of this thread's 32 channels (tables of the stage in tab[buf])
   auto finish_a = [&](const f4 (&src)[8], int buf, int tb) {
-    _Float16* dst = abuf + buf * STAGE + lrow * kLP + lh * 64;
     if (PRO == 3) {
+      _Float16* d3 = abuf + buf * STAGE + a3r * kLP + a3s * 8;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) *reinterpret_cast<f4*>(dst + 8 * u) = src[u];
+      for (int u = 0; u < 8; ++u) *reinterpret_cast<f4*>(d3 + 16 * u * kLP) = src[u];
       return;
     }
+    _Float16* dst = abuf + buf * STAGE + lrow * kLP + lh * 64;
 #pragma unroll
     for (int u = 0; u < 8; u += 2) {  // k-group u / 2: channels 8 (u / 2) .. + 7 of the step
       f4 v0 = src[u], v1 = src[u + 1];
@@ -386,6 +405,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int p = 0; p < 2; ++p) av[i][p] = *reinterpret_cast<const f16x8*>(As + i * 16 * kLP + p * 32);
+    // all of the step's A fragment reads issued before its first MFMA (they return in order, so MFMA i waits
+    // for reads 0 .. 2i + 1 only); left to itself the compiler recycles two registers and waits on each read
+    // behind 2-4 MFMAs (SQ_WAIT_INST_ANY 58 % of wave cycles, MFMA busy 40 %). Not with the in-GEMM
+    // prologues (PRO 1 / 2): their tables and split leave no room for 16 fragments (scratch spills).
+    if (PRO == 0 || PRO == 3) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -413,20 +437,27 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   // left) and the tables of stage st + 2 are loaded before step 0 -- two stages of MFMAs to land (K = 256
   // GEMMs have 4 stages: one stage did not cover the load latency); after step 1 the tables go to LDS
   // and stage st + 1 is finished into the other buffer (its tables were stored a stage earlier).
+  // DM_LIN_ABL (diagnostic builds only, wrong results): 1 no B refills, 2 no A refills, 3 no barrier
   auto stage = [&](int st, f4 (&cur)[8], f4 (&nxt)[8]) {
+#if DM_LIN_ABL != 2
     load_a(cur, min(st + 2, nst - 1));
+#endif
     load_tab(min(st + 2, nst - 1));
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int kk = 2 * st + s;
       compute(st & 1, s, bq[s]);
+#if DM_LIN_ABL != 1
       load_b(bq[s], min(kk + WD, nkk - 1));
+#endif
       __builtin_amdgcn_sched_barrier(0);
     }
     store_tab((st + 2) % 3);
     finish_a(nxt, (st + 1) & 1, (st + 1) % 3);
+#if DM_LIN_ABL != 3
     __syncthreads();
+#endif
   };
   for (int st = 0; st < nst; st += 2) {
     stage(st, ra[0], ra[1]);
