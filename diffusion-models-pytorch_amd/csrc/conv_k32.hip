@@ -481,6 +481,385 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   K32_RSTAMP(6);
 }
 
+// ---- Small maps (<= 16 pixels: the 4x4 level at B = 256, M = 4096). The split-K tiles above give each CU a
+// 64 x 128 tile for half of K, 32 x 64 wave tiles (24 MFMAs per 8 B-fragment loads per tap) and a second
+// launch to reduce the partials. Here a block owns a whole 64 x 64 output tile (256 blocks for 4096 x 256)
+// and splits K inside: waves (grp, wn), grp = wave >> 1 takes the input-channel chunks [0, h) or [h, nch)
+// (h = nch / 2; the ResBlock shortcut's chunks likewise), wn = wave & 1 the 32-column half, so each wave has
+// a 64 x 32 tile: 24 MFMAs per 4 B-fragment loads, every weight fragment loaded once per block. Per loop
+// iteration the two groups compute chunks i and h + i from their own double-buffered patch images (4 x 144
+// pixels x 160 B = 90 KiB: one block per CU) while all four waves load and finish the next pair. The two
+// partial tiles meet in LDS as (p0 * s) + (p1 * s) -- the split-K reduction's expression, with its chunk
+// ranges: the same bits as the two-launch path -- and the epilogue emits the consumer's GroupNorm
+// statistics per image (the image is the whole 64-pixel-or-less chunk), as conv_splitk_reduce_gn did.
+constexpr int kSP = 144;      // patch pixels: 4 images of 4 x 4 with their halo (4 x 6 x 6)
+constexpr int kTabS = 4096;   // GroupNorm tables: 4 images x 512 channels x (scale, shift)
+constexpr int kStatsS = 4 * 64;
+
+template <bool PRO>
+__global__ void __launch_bounds__(256) conv_k32s_kernel(ConvArgs a, PatchGeom g) {
+  constexpr int BM = 64, BN = 64, TM = 4, TN = 2, WD = 2, PJ = 5;  // 5 loader passes of 64 (pixel, quarter)
+  constexpr int PATCH = kSP * kRowH;
+  // one LDS array: [group][buffer] patch images, then the GroupNorm tables and statistics
+  __shared__ __attribute__((aligned(16))) _Float16 patch[4 * PATCH];
+  __shared__ __attribute__((aligned(16))) float gtab[PRO ? kTabS : 4];
+  __shared__ float gstat[PRO ? 2 * kStatsS : 2];
+
+  const int Ho = a.Hout, Wo = a.Wout, HWo = Ho * Wo;
+  const int M = a.B * HWo, N = a.Cout;
+  const int nN = ceil_div(N, BN);
+  const int bid = xcd_remap_p(blockIdx.x, gridDim.x);
+  const int mt = bid / nN, nt = bid - (bid / nN) * nN;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int b0 = m0 / HWo;  // tiles hold whole images (HWo divides 64)
+
+  const int t = threadIdx.x;
+  const int lane = t & 63, wave = t >> 6;
+  const int grp = wave >> 1, wn = wave & 1;
+  const int l16 = lane & 15, q = lane >> 4;
+  const int srow = t >> 2, sq = t & 3;
+  const int nch = a.Cin1 / kC, h = nch / 2;
+  const int n2 = a.Cin2 / kC, h2 = n2 / 2;
+
+  // ---- loader: pass j covers item p = srow + 64 j of the pair's 2 x 144 (pixel, quarter) items; p < 144 is
+  // group 0's chunk, the rest group 1's
+  const float* psrc[PJ];
+  bool pok[PJ];
+  int pimg[PJ];
+  const int PHW = g.PH * g.PW;
+#pragma unroll
+  for (int j = 0; j < PJ; ++j) {
+    const int p = srow + 64 * j;
+    const int pg = p >= kSP ? 1 : 0, pp = p - pg * kSP;
+    const int img = pp / PHW;
+    const int rem = pp - img * PHW;
+    const int pr = rem / g.PW, pc = rem - (rem / g.PW) * g.PW;
+    const int b = b0 + img;
+    const int iy = pr - 1, ix = pc - 1;
+    const bool ok = p < 2 * kSP && pp < g.P && b < a.B && iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
+    pok[j] = ok;
+    const int bc = min(b, a.B - 1);
+    pimg[j] = bc;
+    const int iyc = min(max(iy, 0), a.Hin - 1), ixc = min(max(ix, 0), a.Win - 1);
+    psrc[j] = (ok || PRO) ? a.x1 + ((size_t)(bc * a.Hin + iyc) * a.Win + ixc) * a.x1_pitch + 8 * sq + (pg ? h * kC : 0)
+                          : kZeroPage + 8 * sq;
+  }
+
+  // ---- B: fragment images, the wave's 32 columns
+  const int ngrp = ceil_div(N, 32);
+  const size_t sl = (size_t)ngrp * 1024;
+  const _Float16* wbase[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + wn * 32 + j * 16 + l16;
+    const int cg = min(col >> 5, ngrp - 1);
+    wbase[j] = reinterpret_cast<const _Float16*>(a.ws) + (size_t)cg * 1024 + ((q & 1) * 32 + (col & 31)) * 8;
+  }
+  const size_t qoff = (size_t)(q >> 1) * 9 * sl;
+  auto slice_off = [&](int kt) { return (size_t)(kt + (kt / 9) * 9) * sl + qoff; };
+  f16x8 bq[WD][TN][2];
+  auto load_b = [&](f16x8 (&dst)[TN][2], size_t off) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) dst[j][p] = *reinterpret_cast<const f16x8*>(wbase[j] + off + p * 512);
+  };
+
+  // ---- A-fragment patch rows of this lane
+  int fy[TM], fx[TM], fimg[TM];
+  const int tile_rows = g.TH * g.TW;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int ml = i * 16 + l16;
+    fimg[i] = ml / tile_rows;
+    const int rem = ml - fimg[i] * tile_rows;
+    fy[i] = rem / g.TW;
+    fx[i] = rem - fy[i] * g.TW;
+  }
+
+  f4 rp[2][2];
+  auto load_patch = [&](int i, int j0, int j1) {  // passes j0 .. j1 - 1 of pair i
+#pragma unroll
+    for (int j = j0; j < j1; ++j) {
+      rp[j & 1][0] = *reinterpret_cast<const f4*>(psrc[j] + i * kC);
+      rp[j & 1][1] = *reinterpret_cast<const f4*>(psrc[j] + i * kC + 4);
+    }
+  };
+  const bool pro_silu = !a.pro_nosilu;
+  const int tab_n = PRO ? min(b0 + g.TB, a.B) - b0 : 0;
+  const int tab_c = a.Cin1;
+  bool bad = false;
+  auto finish_patch = [&](int i, int j0, int j1, int buf) {
+    const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = j0; j < j1; ++j) {
+      const int p = srow + 64 * j;
+      const int pg = p >= kSP ? 1 : 0, pp = p - pg * kSP;
+      if (PRO) {
+        const float* ts = gtab + min(pimg[j] - b0, tab_n - 1) * tab_c + (pg ? h + i : i) * kC + 8 * sq;
+        f4 sc[2], sh[2];
+#pragma unroll
+        for (int e2 = 0; e2 < 2; ++e2) {
+          sc[e2] = *reinterpret_cast<const f4*>(ts + 4 * e2);
+          sh[e2] = *reinterpret_cast<const f4*>(ts + tab_n * tab_c + 4 * e2);
+        }
+#pragma unroll
+        for (int e2 = 0; e2 < 2; ++e2)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float v = rp[j & 1][e2][e] * sc[e2][e] + sh[e2][e];
+            rp[j & 1][e2][e] = pro_silu ? silu_fast(v) : v;
+          }
+      }
+      if (p < 2 * kSP) {
+        f16x8 pc[2];
+        const bool z = PRO && !pok[j];
+        Split<2>::split(z ? zero4 : rp[j & 1][0], z ? zero4 : rp[j & 1][1], pc, bad);
+        _Float16* dst = patch + (pg * 2 + buf) * PATCH + pp * kRowH;
+        *reinterpret_cast<f16x8*>(dst + sq * 8) = pc[0];
+        *reinterpret_cast<f16x8*>(dst + 32 + sq * 8) = pc[1];
+      }
+    }
+  };
+
+  f4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  auto a_off = [&](int i, int ky, int kx) {
+    return ((fimg[i] * g.PH + fy[i] + ky) * g.PW + fx[i] + kx) * kRowH + q * 8;
+  };
+  auto compute_tap = [&](int tap, int pbuf, const f16x8 (&bv)[TN][2]) {
+    const _Float16* As = patch + pbuf * PATCH;
+    f16x8 av[TM][2];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) av[i][p] = *reinterpret_cast<const f16x8*>(As + a_off(i, tap / 3, tap % 3) + p * 32);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[i][1], bv[j][0], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[i][0], bv[j][1], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[i][0], bv[j][0], acc[i][j], 0, 0, 0);
+      }
+  };
+
+  // ---- prologue: the first pair's patch loads in flight while the GroupNorm tables are built
+  const int c0w = grp ? h : 0;  // this wave's first chunk
+#pragma unroll
+  for (int d = 0; d < WD; ++d) load_b(bq[d], slice_off(c0w * 9 + d));
+  f4 rq[PJ][2];
+#pragma unroll
+  for (int j = 0; j < PJ; ++j) {
+    rq[j][0] = *reinterpret_cast<const f4*>(psrc[j]);
+    rq[j][1] = *reinterpret_cast<const f4*>(psrc[j] + 4);
+  }
+  if (PRO) {
+    if (a.gin_part) {  // gn_finalize for the tile's images (conv_k32_kernel's in-kernel finalize)
+      const int G = a.gin_G, cpg = a.Cin1 / G;
+      for (int i = t; i < tab_n * G; i += 256) {
+        const int b = b0 + i / G, gg = i - (i / G) * G;
+        double s1 = 0, s2 = 0;
+        for (int k = 0; k < a.gin_nchunk; ++k) {
+          const double2 v = a.gin_part[((size_t)b * a.gin_nchunk + k) * G + gg];
+          s1 += v.x;
+          s2 += v.y;
+        }
+        const double mu = s1 / a.gin_n;
+        double var = s2 / a.gin_n - mu * mu;
+        if (var < 0) var = 0;
+        gstat[2 * i] = (float)mu;
+        gstat[2 * i + 1] = (float)(1.0 / sqrt(var + (double)a.gin_eps));
+      }
+      __syncthreads();
+      for (int i = t; i < tab_n * tab_c; i += 256) {
+        const int bi = i / tab_c, c = i - (i / tab_c) * tab_c;
+        const int si = 2 * (bi * G + c / cpg);
+        const float mu = gstat[si], rs = gstat[si + 1];
+        float sc = rs * (a.gin_gamma ? a.gin_gamma[c] : 1.0f);
+        float sh = -sc * mu + (a.gin_beta ? a.gin_beta[c] : 0.0f);
+        if (a.gin_ms) {
+          const size_t mo = (size_t)(b0 + bi) * a.gin_mp + c;
+          const float f = 1.0f + a.gin_ms[mo];
+          sc = sc * f;
+          sh = sh * f + a.gin_mb[mo];
+        }
+        gtab[i] = sc;
+        gtab[tab_n * tab_c + i] = sh;
+      }
+    } else {
+      for (int i = t; i < tab_n * tab_c; i += 256) {
+        const int bi = i / tab_c, c = i - (i / tab_c) * tab_c;
+        gtab[i] = a.pro_scale[(size_t)(b0 + bi) * a.Cin1 + c];
+        gtab[tab_n * tab_c + i] = a.pro_shift[(size_t)(b0 + bi) * a.Cin1 + c];
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int j = 0; j < PJ; j += 2) {
+    rp[0][0] = rq[j][0];
+    rp[0][1] = rq[j][1];
+    if (j + 1 < PJ) {
+      rp[1][0] = rq[j + 1][0];
+      rp[1][1] = rq[j + 1][1];
+    }
+    finish_patch(0, j, min(j + 2, PJ), 0);
+  }
+  __syncthreads();
+
+  // ---- main loop: pair i = chunks i (group 0) and h + i (group 1); the next pair's passes 0-1 loaded at
+  // tap 0 and finished at tap 2, 2-3 at taps 3 / 5, 4 at taps 6 / 8; one barrier per pair
+  for (int i0 = 0; i0 < h; i0 += 2) {
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      const int i = i0 + cc;
+      if (i >= h) break;
+      const int in = min(i + 1, h - 1);
+      const int buf = i & 1;
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int kt = (c0w + i) * 9 + tap;
+        const int slot = (cc * 9 + tap) % WD;
+        if (tap == 0 || tap == 3 || tap == 6) {
+          load_patch(in, tap == 0 ? 0 : tap == 3 ? 2 : 4, tap == 6 ? 5 : tap == 0 ? 2 : 4);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        compute_tap(tap, grp * 2 + buf, bq[slot]);
+        load_b(bq[slot], slice_off(min(kt + WD, (c0w + h) * 9 - 1)));
+        __builtin_amdgcn_sched_barrier(0);
+        if (tap == 2 || tap == 5 || tap == 8)
+          finish_patch(in, tap == 2 ? 0 : tap == 5 ? 2 : 4, tap == 8 ? 5 : tap == 2 ? 2 : 4, (i + 1) & 1);
+      }
+      __syncthreads();
+    }
+  }
+
+  // ---- segment 2: the ResBlock shortcut (1x1 of x2), chunks [0, h2) and [h2, n2) split over the groups,
+  // un-pipelined: per step each group's 64 x 32 row tile into its buffer 0
+  if (n2 > 0) {
+    int abase[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) abase[i] = (i * 16 + l16) * kRowH + q * 8;
+    const size_t s2 = (size_t)(9 * a.Cin1 / 16) * sl + (size_t)(q >> 1) * sl;
+    for (int c2 = 0; c2 < n2 - h2; ++c2) {
+      // loader: item (group j, row srow, quarter sq)
+      f4 r[2][2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int cj = j ? h2 + c2 : min(c2, max(h2 - 1, 0));
+        const float* xs = a.x2 + (size_t)min(m0 + srow, M - 1) * a.x2_pitch + 8 * sq + cj * kC;
+        r[j][0] = *reinterpret_cast<const f4*>(xs);
+        r[j][1] = *reinterpret_cast<const f4*>(xs + 4);
+      }
+      const int cw = grp ? h2 + c2 : c2;
+      const bool active = cw < (grp ? n2 : h2);
+      load_b(bq[0], s2 + (size_t)(2 * min(cw, n2 - 1)) * sl);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        f16x8 pc[2];
+        Split<2>::split(r[j][0], r[j][1], pc, bad);
+        _Float16* dst = patch + (j * 2) * PATCH + srow * kRowH;
+        *reinterpret_cast<f16x8*>(dst + sq * 8) = pc[0];
+        *reinterpret_cast<f16x8*>(dst + 32 + sq * 8) = pc[1];
+      }
+      __syncthreads();
+      if (active) {
+        const _Float16* As = patch + (grp * 2) * PATCH;
+        f16x8 av[TM][2];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int p = 0; p < 2; ++p) av[i][p] = *reinterpret_cast<const f16x8*>(As + abase[i] + p * 32);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[i][1], bq[0][j][0], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[i][0], bq[0][j][1], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[i][0], bq[0][j][0], acc[i][j], 0, 0, 0);
+          }
+      }
+      __syncthreads();
+    }
+  }
+  if (bad && a.range_flag) *a.range_flag = 1;
+
+  // ---- the two partial tiles through LDS ([group][64][68] fp32, raw accumulators), then each wave takes
+  // rows 32 grp .. + 31 of its 32 columns: v = p0 * s + p1 * s, bias, per-image row vector, residual, store,
+  // and the GroupNorm statistics of each of the slab's two 16-row images
+  constexpr int PTP = BN + 4;
+  float* part = reinterpret_cast<float*>(patch);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) part[(grp * 64 + i * 16 + 4 * q + r) * PTP + wn * 32 + j * 16 + l16] = acc[i][j][r];
+  __syncthreads();
+  constexpr int LPR = 8, RPI = 8;  // lanes per row (4 columns each), rows per wave instruction
+  const int c4 = lane % LPR, rsub = lane / LPR;
+  const int ncol = n0 + wn * 32 + 4 * c4;
+  const bool c_ok = ncol < N;
+  const int nc = c_ok ? ncol : 0;
+  const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  const f4 s4 = {a.ws_rowscale[nc], a.ws_rowscale[nc + 1], a.ws_rowscale[nc + 2], a.ws_rowscale[nc + 3]};
+  const f4 bias4 = a.bias ? *reinterpret_cast<const f4*>(a.bias + nc) : zero4;
+  const int row0 = 32 * grp;
+  double gs[2] = {0.0, 0.0}, gq[2] = {0.0, 0.0};
+  f4 rs4[32 / RPI];
+  if (a.res) {
+#pragma unroll
+    for (int it = 0; it < 32 / RPI; ++it) {
+      const int m = min(m0 + row0 + it * RPI + rsub, M - 1);
+      rs4[it] = *reinterpret_cast<const f4*>(a.res + (size_t)m * a.res_pitch + nc);
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < 32 / RPI; ++it) {
+    const int row = row0 + it * RPI + rsub;
+    const int m = m0 + row;
+    const f4 p0 = *reinterpret_cast<const f4*>(part + row * PTP + wn * 32 + 4 * c4);
+    const f4 p1 = *reinterpret_cast<const f4*>(part + (64 + row) * PTP + wn * 32 + 4 * c4);
+    f4 v = p0 * s4 + p1 * s4;
+    if (a.bias) v = v + bias4;
+    if (a.rowvec) v = v + *reinterpret_cast<const f4*>(a.rowvec + (size_t)(min(m, M - 1) / HWo) * a.rowvec_pitch + nc);
+    if (a.res) v = v + rs4[it];
+    if (m < M && c_ok) *reinterpret_cast<f4*>(a.y + (size_t)m * a.y_pitch + ncol) = v;
+    if (a.gn_part && m < M) {
+      const int hh = (it * RPI) / 16;  // the slab's first or second 16-row image (HWo = 16)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        gs[hh] += (double)v[e];
+        gq[hh] += (double)v[e] * v[e];
+      }
+    }
+  }
+  if (a.gn_part) {  // per image of the slab: over the row lanes, then the group's 4-channel quads
+    const int cpg = N / a.gn_G;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      double s = gs[hh], qq = gq[hh];
+#pragma unroll
+      for (int o = LPR; o < 64; o <<= 1) {
+        s += __shfl_xor(s, o);
+        qq += __shfl_xor(qq, o);
+      }
+      for (int o = 1; o < cpg / 4; o <<= 1) {
+        s += __shfl_xor(s, o);
+        qq += __shfl_xor(qq, o);
+      }
+      const int m = m0 + row0 + 16 * hh;
+      if (rsub == 0 && (c4 % (cpg / 4)) == 0 && c_ok && m < M)
+        a.gn_part[(size_t)(m / HWo) * a.gn_G + ncol / cpg] = make_double2(s, qq);
+    }
+  }
+}
+
 }  // namespace
 
 #ifdef DM_K32_STAMPS
@@ -491,8 +870,25 @@ extern "C" int dm_debug_k32_stamps(void* host, int nblocks) {
 #endif
 
 // Variants: 1 = 128 x 128 tiles, 2 = 128 x 64 (whole K), 3 = 64 x 64 and 4 = 64 x 128 split-K tiles,
-// 5 = 64 x 128 tiles of one image row or 64-pixel row segment (ADM's 64^2 .. 256^2 maps).
+// 5 = 64 x 128 tiles of one image row or 64-pixel row segment (ADM's 64^2 .. 256^2 maps), 6 = the small-map
+// kernel (64 x 64 tiles of four 4 x 4 images, K split in two inside the block; the plan's ksplit = 2).
+static bool conv_k32s_ok(const ConvArgs& a) {
+  if (!(a.ws && a.ws_np == 2 && a.ws_rowscale && a.taps == 9 && a.stride == 1 && a.upsample == 0)) return false;
+  if (a.ksplit != 2 || a.Hout * a.Wout != 16 || a.Hin != a.Hout || a.Win != a.Wout) return false;
+  const int nch = a.Cin1 / kC;
+  if (a.Cin1 % kC != 0 || nch < 2 || nch % 2 != 0 || a.Cin2 % kC != 0 || a.K != 9 * a.Cin1 + a.Cin2) return false;
+  if (a.Cout % 64 != 0) return false;
+  PatchGeom g;
+  if (!conv_patch_geom(a, 64, g) || g.P > kSP || g.TB > 4) return false;
+  if ((a.pro_scale || a.gin_part) && 2 * g.TB * a.Cin1 > kTabS) return false;
+  if (a.gin_part && g.TB * a.gin_G > kStatsS) return false;
+  if (a.gn_part && (a.gn_G <= 0 || a.Cout % a.gn_G != 0 || (a.Cout / a.gn_G) % 4 != 0 || a.Cout / a.gn_G > 32))
+    return false;
+  return staged_epilogue_ok(a) || (a.gn_part && a.Cout % 4 == 0);
+}
+
 int conv_k32_variant_ok(const ConvArgs& a, int v) {
+  if (v == 6) return conv_k32s_ok(a) ? 1 : 0;
   const bool sub = a.upsample == 2;  // sub-pixel nearest-2x + 3x3: 4 parity convs of 4 taps
   if (!(a.ws && a.ws_np == 2 && a.ws_rowscale && a.taps == 9 && a.stride == 1 && (a.upsample == 0 || sub))) return 0;
   if (a.Cin1 < kC || a.Cin1 % kC != 0 || a.Cin2 % kC != 0) return 0;
@@ -529,12 +925,22 @@ bool conv_k32_enabled() {
   return on;
 }
 
+// The small-map kernel (variant 6) unless DM_CONV_K32S=0 (the two-launch split-K path, kept as its test oracle;
+// read per call: plans capture their launches once, so this costs nothing per forward)
+static bool conv_k32_small_enabled() {
+  const char* e = std::getenv("DM_CONV_K32S");
+  return !(e && e[0] == '0');
+}
+
 int conv_k32_pick(const ConvArgs& a) {
-  if (a.tile >= 10 && a.tile <= 14) return conv_k32_variant_ok(a, a.tile - 9) ? a.tile - 9 : 0;
+  if (a.tile >= 10 && a.tile <= 15) return conv_k32_variant_ok(a, a.tile - 9) ? a.tile - 9 : 0;
   if (a.tile != 0 || !conv_k32_enabled()) return 0;
   // split-K convs of maps of <= 16 pixels: 64 x 128 tiles (4x4 maps at B = 256, K split 2: 32.5 us vs
   // 34.2 us for 64 x 64 and for conv_patch3's 64 x 64 split tiles)
-  if (a.ksplit > 1) return conv_k32_variant_ok(a, 4) ? 4 : conv_k32_variant_ok(a, 3) ? 3 : 0;
+  if (a.ksplit > 1) {
+    if (conv_k32_small_enabled() && conv_k32_variant_ok(a, 6)) return 6;
+    return conv_k32_variant_ok(a, 4) ? 4 : conv_k32_variant_ok(a, 3) ? 3 : 0;
+  }
   if (!conv_k32_ok(a)) {
     // maps whose whole-row 128-row tiles do not fit the patch image (64^2 .. 256^2): 64-pixel rows / segments
     const int wt = a.upsample == 2 ? a.Win : a.Wout;
@@ -550,6 +956,7 @@ int conv_k32_pick(const ConvArgs& a) {
 
 // rocprofv3's name of the instantiation conv2d_k32 launches (spaces removed)
 std::string conv_k32_label(const ConvArgs& a, int v) {
+  if (v == 6) return std::string("conv_k32s_kernel<") + (a.pro_scale || a.gin_part ? "true>" : "false>");
   static const char* names[] = {"", "conv_k32_kernel<128,128,64,64,", "conv_k32_kernel<128,64,64,32,",
                                 "conv_k32_kernel<64,64,32,32,", "conv_k32_kernel<64,128,32,64,",
                                 "conv_k32_kernel<64,128,32,64,"};
@@ -578,8 +985,18 @@ static void launch_k32(const ConvArgs& a, const PatchGeom& g, hipStream_t st) {
 }
 
 int conv2d_k32(const ConvArgs& a, int v, hipStream_t st) {
-  DM_REQUIRE(v >= 1 && v <= 5 && conv_k32_variant_ok(a, v), "conv: shape not supported by the K = 32 split kernel");
+  DM_REQUIRE(v >= 1 && v <= 6 && conv_k32_variant_ok(a, v), "conv: shape not supported by the K = 32 split kernel");
   PatchGeom g;
+  if (v == 6) {
+    conv_patch_geom(a, 64, g);
+    const int blocks = ceil_div(a.B * a.Hout * a.Wout, 64) * (a.Cout / 64);
+    if (a.pro_scale || a.gin_part)
+      hipLaunchKernelGGL(conv_k32s_kernel<true>, dim3(blocks), dim3(256), 0, st, a, g);
+    else
+      hipLaunchKernelGGL(conv_k32s_kernel<false>, dim3(blocks), dim3(256), 0, st, a, g);
+    DM_LAUNCH_CHECK();
+    return DM_OK;
+  }
   conv_patch_geom(a, v >= 3 ? 64 : BM_K32, g);
   switch (v) {
     case 1: launch_k32<128, 128, 64, 64, false>(a, g, st); break;

@@ -218,3 +218,58 @@ def test_k32_row_segments_fp32_accuracy(cuda, B, Cin, Cout, H):
     err = (y.cpu().double() - _nhwc(ref)).abs().max().item()
     scale = ref.abs().max().item()
     assert err < 4e-6 * scale, (err, scale)
+
+
+# ---- the small-map kernel (conv_k32s_kernel, tile 15 forced / 0 automatic with ksplit = 2): 64 x 64 tiles of
+# four 4 x 4 images, the K reduction split in two inside the block
+@pytest.mark.parametrize('tile', [15, 0])
+@pytest.mark.parametrize('B,Cin,Cout,H', [(5, 256, 256, 4), (3, 128, 64, 4), (8, 512, 256, 4), (1, 64, 128, 4),
+                                          (4, 256, 192, 4)])
+def test_k32_small_exact(cuda, B, Cin, Cout, H, tile):
+    x = _ints((B, Cin, H, H), -2, 3, seed=130)
+    w = _ints((Cout, Cin, 3, 3), -2, 3, seed=131)
+    b = _ints((Cout, ), seed=132)
+    ref = F.conv2d(x.double(), w.double(), b.double(), padding=1).float()
+    y = _run_conv(cuda, _nhwc(x).to(cuda), _pack(w, cuda), Cout, H, H, 9, 1, 0, b.to(cuda), tile=tile,
+                  split='fp16x2', ksplit=2)
+    assert torch.equal(y.cpu(), _nhwc(ref))
+
+
+@pytest.mark.parametrize('C1,C2', [(256, 512), (256, 64), (128, 32), (64, 0)])
+def test_k32_small_segments_rowvec_residual(cuda, C1, C2):
+    """ResBlock conv2 at 4 x 4 (the up path's 512-channel shortcut split over the block's two K groups),
+    temb row vector, residual, pitched output (untouched beyond Cout); B = 6 leaves a partial last tile."""
+    B, Cout, H = 6, 128, 4
+    h = _ints((B, C1, H, H), seed=140)
+    x = _ints((B, max(C2, 32), H, H), seed=141)
+    w2 = _ints((Cout, C1, 3, 3), -2, 3, seed=142)
+    ws = _ints((Cout, max(C2, 32), 1, 1), seed=143)
+    b = _ints((Cout, ), seed=144)
+    rv = _ints((B, Cout), seed=145)
+    res = _ints((B, Cout, H, H), seed=146)
+    K = 9 * C1 + C2
+    wp = torch.zeros((Cout, K), device=cuda)
+    _pack(w2, cuda, K, 0, wp)
+    ref = F.conv2d(h.double(), w2.double(), b.double(), padding=1) + rv.double()[:, :, None, None] + res.double()
+    if C2:
+        _pack(ws, cuda, K, 9 * C1, wp)
+        ref = ref + F.conv2d(x.double(), ws.double())
+    y = _run_conv(cuda, _nhwc(h).to(cuda), wp, Cout, H, H, 9, bias=b.to(cuda), rowvec=rv.to(cuda),
+                  res=_nhwc(res).to(cuda), x2=_nhwc(x).to(cuda) if C2 else None, Cin2=C2, y_pitch=160, tile=15,
+                  split='fp16x2', ksplit=2)
+    assert torch.equal(y[..., :Cout].cpu(), _nhwc(ref.float()))
+    assert torch.isnan(y[..., Cout:]).all()
+
+
+@pytest.mark.parametrize('B,Cin,Cout', [(16, 256, 256), (8, 512, 256)])
+def test_k32_small_fp32_accuracy(cuda, B, Cin, Cout):
+    """fused GroupNorm + SiLU, random data: within 2x of the fp32 MFMA kernel's error vs fp64 (as the split-K
+    tiles it replaces)."""
+    xd, wp, b, pro, ref = _rand_case(cuda, B, Cin, Cout, 4, 0, seed=95)
+    errs = {}
+    for name, split, tile, ks in (('fp32', False, 0, 0), ('k32s', 'fp16x2', 15, 2), ('splitk', 'fp16x2', 13, 2)):
+        y = _run_conv(cuda, xd, wp, Cout, 4, 4, 9, 1, 0, b.to(cuda), pro=pro, split=split, tile=tile, ksplit=ks)
+        errs[name] = (y.cpu().double() - _nhwc(ref)).abs().max().item()
+    scale = ref.abs().max().item()
+    assert errs['k32s'] < 2.0 * errs['fp32'] + 1e-7 * scale, errs
+    assert errs['k32s'] < 4e-6 * scale, (errs, scale)

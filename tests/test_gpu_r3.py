@@ -367,3 +367,37 @@ def test_flash_attention_vs_unfused(cuda, golden, report, monkeypatch, case):
     report(f'flash_attention_{case}_maxabs_vs_unfused', err)
     assert torch.isfinite(outs['flash']).all()
     assert err <= 1e-5, err
+
+
+# ------------------------------------------------------------------ small-map conv kernel (conv_k32.hip)
+@pytest.mark.parametrize('arch', ['cifar10', 'adagn'])
+def test_small_map_conv_vs_splitk(cuda, golden, report, monkeypatch, arch):
+    """The 4 x 4 level's convs on conv_k32s_kernel (one launch, K split inside the block, GroupNorm statistics
+    per image from its epilogue) against the two-launch split-K path with its reduction (DM_CONV_K32S=0):
+    whole forwards within 1e-5 (the ResBlock shortcut's chunks are split over the two K groups, so the
+    partial sums group differently), and the kernel is the one the plan runs."""
+    from models.unet_categorial_adagn import UNetCategorialAdaGN
+    outs = {}
+    for mode in ('small', 'splitk'):
+        if mode == 'splitk':
+            monkeypatch.setenv('DM_CONV_K32S', '0')
+        if arch == 'cifar10':
+            m, _ = _model(golden('forward')[1], 'cifar10', cuda)
+        else:
+            m = UNetCategorialAdaGN(**golden('adagn')[1]['archs']['cfg_cifar10']).eval()
+            init_synthetic_(m)
+            m = m.to(cuda)
+        g = torch.Generator().manual_seed(6)
+        x = torch.randn((8, 3, 32, 32), generator=g).to(cuda)
+        t = torch.tensor([999, 800, 600, 400, 200, 100, 10, 0], device=cuda)
+        outs[mode] = (m(x, t) if arch == 'cifar10' else m(x, t, torch.arange(8, device=cuda) % 10)).cpu()
+        h = m.native_handle(torch.device(cuda))
+        dmhip.unet_profile_enable(h, 1)
+        dmhip.unet_profile_enable(h, 0)
+        labels = [op['label'] for op in dmhip.unet_profile_read(h)]
+        assert any(lb.startswith('conv_k32s_kernel') for lb in labels) == (mode == 'small'), labels
+        del m
+    err = (outs['small'] - outs['splitk']).abs().max().item()
+    report(f'small_map_conv_{arch}_maxabs_vs_splitk', err)
+    assert torch.isfinite(outs['small']).all()
+    assert err <= 1e-5, err
