@@ -54,6 +54,26 @@ __device__ unsigned long long g_attn_stamps[8192][10];
 
 __device__ __forceinline__ int split_off(int k) { return (k >> 4) * 32 + ((k >> 3) & 1) * 16 + (k & 7); }
 
+// Softmax rows of L = 256 scores hold 4 consecutive keys per lane (4 lane .. 4 lane + 3, one 16-B LDS read),
+// as softmax_rows (elementwise.hip) does for L = 256: the max, expf, the lane's sum in key order, then the
+// butterfly -- the same operations in the same order, so P is bit-identical across the three paths. The
+// lane's 4 P values are split and stored as one 8-B piece-0 write and one 8-B piece-1 write (was 8 2-B
+// writes from keys lane + 64 u).
+__device__ __forceinline__ void p_store4(_Float16* prow, int lane, const f4& p, float pp) {
+  f16x4 hi, lo;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float x = p[e] * pp;
+    const _Float16 h0 = (_Float16)x;
+    hi[e] = h0;
+    lo[e] = (_Float16)(x - (float)h0);
+  }
+  const int k = 4 * lane;
+  _Float16* dst = prow + (k >> 5) * kAP + split_off(k & 31);
+  *reinterpret_cast<f16x4*>(dst) = hi;
+  *reinterpret_cast<f16x4*>(dst + 8) = lo;
+}
+
 // QT query rows per block: 32 for DH = 256 (78 KB of LDS: two blocks per CU), 64 for DH = 64 (the PV
 // wave layout needs 64 rows there). Operand tiles are prefetched two k steps ahead into registers.
 template <int DH, int QT>
@@ -170,33 +190,21 @@ __global__ void __launch_bounds__(256) attn_fused_kernel(AttnArgs a) {
   // ---------------------------------------------------------------- 2. softmax rows -> P pieces in place
   for (int row = wave * (kAQ / 4); row < (wave + 1) * (kAQ / 4); ++row) {
     float* srow = sp + row * kSP;
-    float v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = u < 4 ? srow[lane + 64 * u] : -INFINITY;   // softmax_rows' 8 slots
-    float mx = -INFINITY;
-#pragma unroll
-    for (int u = 0; u < 8; ++u) mx = fmaxf(mx, v[u]);
+    f4 v = *reinterpret_cast<const f4*>(srow + 4 * lane);
+    float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
     float sum = 0.f;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      v[u] = expf(v[u] - mx);
-      sum += v[u];
+    for (int e = 0; e < 4; ++e) {
+      v[e] = expf(v[e] - mx);
+      sum += v[e];
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
     const float inv = 1.0f / sum;
-    _Float16* prow = reinterpret_cast<_Float16*>(srow);   // P row: 8 key blocks x kAP fp16 (same bytes)
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int k = lane + 64 * u;
-      const float x = (v[u] * inv) * pp;
-      const _Float16 h0 = (_Float16)x;
-      _Float16* dst = prow + (k >> 5) * kAP + split_off(k & 31);
-      dst[0] = h0;
-      dst[8] = (_Float16)(x - (float)h0);
-    }
+    // P row: 8 key blocks x kAP fp16 over the same bytes (this wave's read of the row came first)
+    p_store4(reinterpret_cast<_Float16*>(srow), lane, v * inv, pp);
   }
   __syncthreads();
 
@@ -402,7 +410,10 @@ __device__ __forceinline__ void attn_proj(const ConvArgs& c, f16v (&oacc)[2][2],
 // 125.6 to 110.3 us but measured 1.6 % slower end to end -- every other kernel of the forward then ran at
 // a lower clock -- so the [token][d] / [d][token] planes stay.) 64 query rows per block (75 KB of LDS for
 // the S / P rows: two blocks per CU). Same MFMA sequence as the unfused GEMMs.
-template <int DH>
+// FRAG: k and v^T are fragment images (frag_off; the qkv projection's ap_frag epilogue): every k / v operand
+// fragment is one contiguous 1-KiB wave instruction instead of 32 rows x 32 B (32 cache lines touched per
+// instruction, each line four times over the 16-deep slices).
+template <int DH, bool FRAG>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) attn_presplit_kernel(AttnArgs a) {
   static_assert(DH == 64 || DH == 256, "head dims 64 / 256");
   constexpr int QT = 64, NS = DH / 16, RD = 6;
@@ -434,7 +445,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 #pragma unroll
       for (int q = 0; q < 2; ++q)
         rb[slot][i][q] =
-            *reinterpret_cast<const f16x8*>(K + q * plane + (size_t)(wave * 64 + i * 32 + lr) * DH + 16 * s + 8 * lh);
+            FRAG ? *reinterpret_cast<const f16x8*>(K + frag_off(wave * 64 + i * 32, 16 * s, kAL) + q * 512 + lane * 8)
+                 : *reinterpret_cast<const f16x8*>(K + q * plane + (size_t)(wave * 64 + i * 32 + lr) * DH + 16 * s + 8 * lh);
   };
 #pragma unroll
   for (int s = 0; s < RD; ++s) load_k(min(s, NS - 1), s);
@@ -497,15 +509,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   // same order as softmax_rows, so P stays bit-identical)
   constexpr int RI = QT / 4;
   for (int row0 = wave * (QT / 4); row0 < (wave + 1) * (QT / 4); row0 += RI) {
-    float v[RI][4], mx[RI], sum[RI];
+    f4 v[RI];
+    float mx[RI], sum[RI];
 #pragma unroll
     for (int ri = 0; ri < RI; ++ri) {
-      const float* srow = sp + (row0 + ri) * kSP;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) v[ri][u] = srow[lane + 64 * u];
-      mx[ri] = -INFINITY;
-#pragma unroll
-      for (int u = 0; u < 8; ++u) mx[ri] = fmaxf(mx[ri], u < 4 ? v[ri][u & 3] : -INFINITY);  // softmax_rows' 8 slots
+      v[ri] = *reinterpret_cast<const f4*>(sp + (row0 + ri) * kSP + 4 * lane);
+      mx[ri] = fmaxf(fmaxf(v[ri][0], v[ri][1]), fmaxf(v[ri][2], v[ri][3]));
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1)
@@ -515,9 +524,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     for (int ri = 0; ri < RI; ++ri) {
       sum[ri] = 0.f;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        v[ri][u] = expf(v[ri][u] - mx[ri]);
-        sum[ri] += v[ri][u];
+      for (int e = 0; e < 4; ++e) {
+        v[ri][e] = expf(v[ri][e] - mx[ri]);
+        sum[ri] += v[ri][e];
       }
     }
 #pragma unroll
@@ -529,16 +538,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 #pragma unroll
     for (int ri = 0; ri < RI; ++ri) {
       const float inv = 1.0f / sum[ri];
-      _Float16* prow = reinterpret_cast<_Float16*>(sp + (row0 + ri) * kSP);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int k = lane + 64 * u;
-        const float x = (v[ri][u] * inv) * pp;
-        const _Float16 h0 = (_Float16)x;
-        _Float16* dst = prow + (k >> 5) * kAP + split_off(k & 31);
-        dst[0] = h0;
-        dst[8] = (_Float16)(x - (float)h0);
-      }
+      p_store4(reinterpret_cast<_Float16*>(sp + (row0 + ri) * kSP), lane, v[ri] * inv, pp);
     }
   }
   __syncthreads();
@@ -557,7 +557,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 #pragma unroll
       for (int q = 0; q < 2; ++q)
         rv[slot][j][q] =
-            *reinterpret_cast<const f16x8*>(V + q * plane + (size_t)(ocol0 + j * 32 + lr) * kAL + 16 * s + 8 * lh);
+            FRAG ? *reinterpret_cast<const f16x8*>(V + frag_off(ocol0 + j * 32, 16 * s, DH) + q * 512 + lane * 8)
+                 : *reinterpret_cast<const f16x8*>(V + q * plane + (size_t)(ocol0 + j * 32 + lr) * kAL + 16 * s + 8 * lh);
   };
   f16v oacc[TM][TN];
 #pragma unroll
@@ -895,10 +896,15 @@ int attn_fused(const AttnArgs& args, hipStream_t st) {
              "fused attention: operands must be float4-aligned rows");
   if (a.pq) {
     DM_REQUIRE(a.pk && a.pv, "fused attention: all three operand planes");
-    if (a.Dh == 256)
-      hipLaunchKernelGGL(attn_presplit_kernel<256>, dim3(a.B * a.heads * (kAL / 64)), dim3(256), 0, st, a);
+    const dim3 grid(a.B * a.heads * (kAL / 64));
+    if (a.Dh == 256 && a.frag)
+      hipLaunchKernelGGL((attn_presplit_kernel<256, true>), grid, dim3(256), 0, st, a);
+    else if (a.Dh == 256)
+      hipLaunchKernelGGL((attn_presplit_kernel<256, false>), grid, dim3(256), 0, st, a);
+    else if (a.frag)
+      hipLaunchKernelGGL((attn_presplit_kernel<64, true>), grid, dim3(256), 0, st, a);
     else
-      hipLaunchKernelGGL(attn_presplit_kernel<64>, dim3(a.B * a.heads * (kAL / 64)), dim3(256), 0, st, a);
+      hipLaunchKernelGGL((attn_presplit_kernel<64, false>), grid, dim3(256), 0, st, a);
     DM_LAUNCH_CHECK();
     return DM_OK;
   }

@@ -339,6 +339,12 @@ bool conv_can_emit_gn(const ConvArgs& a) {
   const int pick = conv_pick(a);
   if (pick != 3 && pick != 4 && pick != 6 && pick != 7 && pick != 8) return false;  // waves own whole 64-row chunks
   if (conv_k32_pick(a) && a.Cout % a.gn_G == 0 && a.Cout / a.gn_G > 16) return false;  // K32: groups within 16 columns
+  // the K32 sub-pixel upsample (128-row tiles, 64-row waves of one parity): chunks of 64 low-res pixels
+  if (a.upsample == 2) {
+    const int v = conv_k32_pick(a);
+    return (v == 1 || v == 2) && !std::getenv("DM_GN_NO_SUB") && (a.Hin * a.Win) % 64 == 0 && a.gn_G > 0 &&
+           a.Cout % a.gn_G == 0 && 32 % (a.Cout / a.gn_G) == 0 && (a.Cout / a.gn_G) % 4 == 0;
+  }
   if (a.upsample || (a.ksplit > 1)) return false;
   if (a.taps == 1 && !conv_pw_ok(a)) return false;
   if ((a.Hout * a.Wout) % 64 != 0 || a.gn_G <= 0 || a.Cout % a.gn_G != 0) return false;

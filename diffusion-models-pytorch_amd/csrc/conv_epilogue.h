@@ -167,8 +167,13 @@ struct StagedEpilogue {
       s += __shfl_xor(s, o);
       q += __shfl_xor(q, o);
     }
-    const int nchunk = (HWo + 63) / 64;
-    const int bb = crow0 / HWo, ch = (crow0 - bb * HWo) / 64;
+    int nchunk = (HWo + 63) / 64;
+    const int bb = crow0 / HWo;
+    int ch = (crow0 - bb * HWo) / 64;
+    if (sub_w) {  // sub-pixel conv: the 64 low-res rows of parity (py, px) are chunk par * HWo / 64 + ch of the
+      ch += (2 * sub_py + sub_px) * nchunk;  // output image (any disjoint cover of its pixels sums the same)
+      nchunk *= 4;
+    }
     if (rsub == 0 && (c4 % (cpg / 4)) == 0 && c_ok && crow0 < M)
       a.gn_part[((size_t)bb * nchunk + ch) * a.gn_G + ncol / cpg] = make_double2(s, q);
   }

@@ -170,6 +170,9 @@ struct GemmArgs {
   int ap_L, ap_heads, ap_Dh, ap_legacy;
   float ap_alpha, ap_bscale;
   int ap_ea, ap_eb, ap_ev;
+  // k ([L][Dh]) and v^T ([Dh][L]) as MFMA fragment images (frag_off, mfma_tile.h) instead of row planes:
+  // attn_presplit_kernel then loads every k / v operand fragment as one contiguous 1-KiB wave instruction
+  int ap_frag;
   int* range_flag;
 };
 
@@ -312,6 +315,7 @@ struct AttnArgs {
   // columns h Dh ..): the output projection reads it without a split pass
   _Float16* o_split;
   int o_split_ea, o_ld;
+  int frag;  // attn_presplit_kernel: pk / pv are fragment images (GemmArgs::ap_frag)
 };
 bool attn_fused_ok(int L, int Dh);
 int attn_fused(const AttnArgs& a, hipStream_t st);

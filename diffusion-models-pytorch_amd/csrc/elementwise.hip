@@ -13,6 +13,7 @@
 // computed with the same torch 0-dim ops as the reference).
 #include "dm_common.h"
 #include "dm_kernels.h"
+#include "mfma_tile.h"
 
 namespace dm {
 
@@ -55,6 +56,25 @@ __global__ void softmax_rows_kernel(float* __restrict__ x, long rows, int L, int
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
   float* r = x + row * ld;
+  if (L == 256 && (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+    // 4 consecutive keys per lane (one 16-B load and store): the order of the fused attention kernels'
+    // softmax (attention.hip), so their P equals this one bit for bit
+    f4 v = *reinterpret_cast<const f4*>(r + 4 * lane);
+    float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    float sum = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[e] = expf(v[e] - mx);
+      sum += v[e];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+    const float inv = 1.0f / sum;
+    *reinterpret_cast<f4*>(r + 4 * lane) = v * inv;
+    return;
+  }
   if (L <= 512) {
     // the row in registers (8 per lane): one read and one write of S instead of five passes; same
     // per-lane order of the max / exp / sum / scale as the loop below, so the same bits

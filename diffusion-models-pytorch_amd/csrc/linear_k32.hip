@@ -162,6 +162,50 @@ __device__ __forceinline__ void plane_block(const GemmArgs& g, const float* tile
   };
   const int b = m0 / g.ap_L, tok0 = m0 - b * g.ap_L;
   const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  if (g.ap_frag) {  // k / v^T as fragment images (frag_off): the tile is one part of whole heads (linear_k32_ok)
+    int part, h, d;
+    col_map(n0, part, h, d);
+    if (part == 1) {  // k: item (token r, 8-column group c8), 32 consecutive tokens per 32 lanes: 512-B runs
+#pragma unroll 2
+      for (int it = 0; it < 8; ++it) {
+        const int r = (t & 31) + 32 * (it & 3), c8 = (t >> 5) + 8 * (it >> 2);
+        const int col = n0 + 8 * c8;
+        if (col >= g.N || m0 + r >= g.M) continue;
+        col_map(col, part, h, d);
+        const f4 b0 = g.bias ? *reinterpret_cast<const f4*>(g.bias + col) : zero4;
+        const f4 b1 = g.bias ? *reinterpret_cast<const f4*>(g.bias + col + 4) : zero4;
+        const f4 v0 = *reinterpret_cast<const f4*>(tile + r * TP + 8 * c8) + b0;
+        const f4 v1 = *reinterpret_cast<const f4*>(tile + r * TP + 8 * c8 + 4) + b1;
+        const float x[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+        f16x8 hi, lo;
+        split8(1, x, hi, lo);
+        _Float16* p = g.ap_k + ((size_t)b * g.ap_heads + h) * 2 * plane + frag_off(tok0 + r, d, g.ap_L);
+        *reinterpret_cast<f16x8*>(p) = hi;
+        *reinterpret_cast<f16x8*>(p + 512) = lo;
+      }
+      return;
+    }
+    if (part == 2) {  // v^T: item (column c, 8-token group r8), 32 consecutive columns (= d) per 32 lanes
+#pragma unroll 2
+      for (int it = 0; it < 8; ++it) {
+        const int c = (t & 31) + 32 * (it & 3), r8 = (t >> 5) + 8 * (it >> 2);
+        const int col = n0 + c;
+        if (col >= g.N || m0 + 8 * r8 >= g.M) continue;
+        col_map(col, part, h, d);
+        const float bc = g.bias ? g.bias[col] : 0.f;
+        float x[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = tile[(8 * r8 + e) * TP + c] + bc;
+        f16x8 hi, lo;
+        split8(2, x, hi, lo);
+        _Float16* p = g.ap_v + ((size_t)b * g.ap_heads + h) * 2 * plane + frag_off(d, tok0 + 8 * r8, Dh);
+        *reinterpret_cast<f16x8*>(p) = hi;
+        *reinterpret_cast<f16x8*>(p + 512) = lo;
+      }
+      return;
+    }
+    // q: the row planes below
+  }
   {  // q / k: item (row, 8-column group), 16 groups per row; a thread keeps its column group
     const int c8 = t & 15, col = n0 + 8 * c8;
     int part, h, d;
@@ -582,6 +626,9 @@ bool linear_k32_ok(const GemmArgs& g) {
   if (g.pro_scale && g.ln_stats) return false;
   if (g.as && (g.pro_scale || g.ln_stats || (reinterpret_cast<uintptr_t>(g.as) & 15) != 0)) return false;
   if (g.c_split && (g.N % 64 != 0 || g.ap_q || (reinterpret_cast<uintptr_t>(g.c_split) & 15) != 0)) return false;
+  if (g.ap_frag && (!g.ap_q || g.ap_legacy || (g.ap_heads * g.ap_Dh) % 128 != 0 || g.ap_L % 128 != 0 ||
+                    g.ap_Dh % 32 != 0))
+    return false;
   return true;
 }
 

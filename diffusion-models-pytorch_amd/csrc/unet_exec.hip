@@ -1006,6 +1006,19 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
       }
       const bool qkv_linear = conv_math == 2 && cq.ws && cq.ws_np == 2 && linear_k32_ok(gl) &&
                               !std::getenv("DM_QKV_NO_LINEAR");
+      // k / v^T as fragment images for attn_presplit_kernel (DM_ATTN_FRAG=1; the L = 256 kernels only). Measured
+      // (tools/attn_stamps.py, same box): the attention block 118.5k -> 89.9k cycles (S 40.9k -> 25.5k, PV 26.4k
+      // -> 14.2k), the qkv epilogue +1.8k; but the forward A/B is -0.6 % (the kernel runs at a lower clock under
+      // the power cap: 2.05 -> 1.90 GHz), so the row planes stay the default.
+      bool frag = false;
+      if (qkv_linear && presplit && l256 && std::getenv("DM_ATTN_FRAG") && std::getenv("DM_ATTN_FRAG")[0] == '1') {
+        GemmArgs gf = gl;
+        gf.ap_frag = 1;
+        gf.as = reinterpret_cast<const _Float16*>(uintptr_t(256));  // as the pre-split GEMM runs it
+        gf.pro_scale = gf.pro_shift = nullptr;
+        frag = linear_k32_ok(gf);
+        gl.ap_frag = frag ? 1 : 0;
+      }
       if (qkv_linear) {
         add("gn_finalize", 0, 8.0 * B * C, [=](hipStream_t st) {
           return gn_finalize(xin, G, sta, 1e-5f, self->P(p.gn.g), self->P(p.gn.b), gsc, gsh, st);
@@ -1065,6 +1078,7 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
         }
         if (presplit) {
           at.pq = planes; at.pk = planes + plane_n; at.pv = planes + 2 * plane_n;
+          at.frag = frag ? 1 : 0;
         }
         at.qkv = qkv; at.ld = 3 * C; at.L = hw; at.Dh = Dh; at.heads = heads; at.B = B;
         at.q0 = 0; at.k0 = k0; at.v0 = v0; at.hs = hs;
@@ -1131,7 +1145,10 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
         split_for(s);
         if (conv_pick(s) >= 3) c = s;
       }
-      gn_ready.erase(y.p);
+      if (c.upsample == 2)
+        emit_conv(c, y);  // the K32 sub-pixel conv's epilogue emits the consumer's GroupNorm partials
+      else
+        gn_ready.erase(y.p);
       add_conv(c);
     }
     x_cur = y;
