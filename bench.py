@@ -76,7 +76,7 @@ def pmc_traffic(label, workload='c3'):
     import re
 
     def order(path):
-        m = re.search(r'r(\d+)_v(\d+)_pmc\.json$', path)
+        m = re.search(r'r(\d+)_v(\d+)(?:_c\d)?_pmc\.json$', path)
         return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
     files = sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*_v*_pmc.json')), key=order)
     for path in reversed(files):
@@ -84,7 +84,10 @@ def pmc_traffic(label, workload='c3'):
             summary = json.load(f)
         if summary.get('workload', 'c3') != workload:
             continue
-        k = summary.get('kernels', {}).get(label)
+        kernels = summary.get('kernels', {})
+        k = kernels.get(label)
+        if k is None and label.endswith('>'):  # family label with fewer template arguments than the trace's
+            k = next((v for n, v in kernels.items() if n.startswith(label[:-1] + ',')), None)
         if k and k.get('hbm_bytes_per_launch'):
             return float(k['hbm_bytes_per_launch']), os.path.relpath(path, ROOT)
     return None, None
