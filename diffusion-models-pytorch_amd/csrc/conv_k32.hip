@@ -44,6 +44,7 @@ constexpr int BM_K32 = 128;   // block rows (output pixels)
 constexpr int kC = 32;          // input channels per chunk = K of one tap's MFMA step
 constexpr int kRowH = 80;       // LDS row pitch in fp16: 160 B; [piece][k-group][8] (piece at +32)
 constexpr int kMaxP = 208;      // patch pixels: 32^2 maps 6 x 34, 16^2 maps 10 x 18, 8^2 maps 2 x 10 x 10
+constexpr int kMaxPW = 392;     // 512-thread wide-map tiles: 3 x 130 (128-pixel row segments), 4 x 66 (64^2 maps)
 constexpr int kTab = 2048;      // GroupNorm table floats (per image of the tile: its channels' scales, then the shifts)
 constexpr int kStats = 128;     // (image, group) pairs of the in-kernel finalize
 
@@ -71,13 +72,18 @@ __device__ unsigned long long g_k32_stamps[65536][8];
 // SUB: the sub-pixel form of nearest-2x + 3x3 (models/modules.py:60-63; conv_patch3 MODE 2): per output
 // parity (py, px) a 2x2-tap conv of the low-res input with pre-combined weights (repack_subpixel), tiles
 // over low-res pixels, the epilogue scattering row (iy, ix) to output pixel (2 iy + py, 2 ix + px).
-template <int BM, int BN, int WM, int WN, bool PRO, bool KSPLIT, bool SUB = false>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) conv_k32_kernel(ConvArgs a, PatchGeom g) {
+// NT threads per block (256, or 512 for the 128-pixel row-segment tiles of the wide maps: 8 waves of 64 x 32
+// in one block per CU, each weight fragment loaded by two waves instead of by four 64 x 128 blocks' waves),
+// MAXP patch pixels per buffer.
+template <int BM, int BN, int WM, int WN, bool PRO, bool KSPLIT, bool SUB = false, int NT = 256, int MAXP = kMaxP>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) conv_k32_kernel(ConvArgs a, PatchGeom g) {
   constexpr int NWN = BN / WN;
-  static_assert((BM / WM) * NWN == 4, "4 waves per block");
+  static_assert((BM / WM) * NWN == NT / 64, "one wave per 64 threads");
   constexpr int TM = WM / 16, TN = WN / 16;
-  constexpr int PJ = (kMaxP + 63) / 64;  // loader passes of 64 pixels (4 threads per pixel)
-  constexpr int PATCH = kMaxP * kRowH;
+  constexpr int SROWS = NT / 4;                       // patch pixels per loader pass (4 threads per pixel)
+  constexpr int PJ = (MAXP + SROWS - 1) / SROWS;      // loader passes
+  static_assert(PJ == 4, "the main loop stages passes 0-1 and 2-3");
+  constexpr int PATCH = MAXP * kRowH;
   constexpr int NTAP = SUB ? 4 : 9, WD = 2, CPI = 2;  // B ring depth; chunks per loop iteration (slot = compile-time)
   __shared__ __attribute__((aligned(16))) _Float16 patch[2 * PATCH];
   __shared__ __attribute__((aligned(16))) float gtab[PRO ? kTab : 4];
@@ -115,14 +121,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   const int l16 = lane & 15, q = lane >> 4;
   const int srow = t >> 2, sq = t & 3;  // loader: pixel slot, 8-channel quarter of the chunk
 
-  // ---- patch loader geometry: pixel p = srow + 64 j of the TB x PH x PW patch
+  // ---- patch loader geometry: pixel p = srow + SROWS j of the TB x PH x PW patch
   const float* psrc[PJ];
   bool pok[PJ];
   int pimg[PJ];
 #pragma unroll
   for (int j = 0; j < PJ; ++j) {
     const int PHW = g.PH * g.PW;
-    const int p = srow + 64 * j;
+    const int p = srow + SROWS * j;
     const int img = p / PHW;
     const int rem = p - img * PHW;
     const int pr = rem / g.PW, pc = rem - (rem / g.PW) * g.PW;
@@ -214,8 +220,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
             rp[j & 1][h][e] = pro_silu ? silu_fast(v) : v;
           }
       }
-      const int p = srow + 64 * j;
-      if (j * 64 < kMaxP && p < kMaxP) {
+      const int p = srow + SROWS * j;
+      if (p < MAXP) {
         f16x8 pc[2];
         const bool z = PRO && !pok[j];
         Split<2>::split(z ? zero4 : rp[j & 1][0], z ? zero4 : rp[j & 1][1], pc, bad);
@@ -300,11 +306,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
       // The per-channel affine (and AdaGN modulation) of this thread's table entries is loaded first, with
       // the statistics partials, so the prologue waits for one round trip, not two.
       const int G = a.gin_G, cpg = a.Cin1 / G;
-      constexpr int TU = kTab / 2 / 256;  // table entries per thread
+      constexpr int TU = kTab / 2 / NT;  // table entries per thread
       float gam[TU], bet[TU], fms[TU], fmb[TU];
 #pragma unroll
       for (int u = 0; u < TU; ++u) {
-        const int i = min(t + 256 * u, tab_n * tab_c - 1);
+        const int i = min(t + NT * u, tab_n * tab_c - 1);
         const int bi = i / tab_c, c = tab_c0 + i - (i / tab_c) * tab_c;
         gam[u] = a.gin_gamma ? a.gin_gamma[c] : 1.0f;
         bet[u] = a.gin_beta ? a.gin_beta[c] : 0.0f;
@@ -312,7 +318,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
         fms[u] = a.gin_ms ? a.gin_ms[mo] : 0.0f;
         fmb[u] = a.gin_mb ? a.gin_mb[mo] : 0.0f;
       }
-      for (int i = t; i < tab_n * G; i += 256) {
+      for (int i = t; i < tab_n * G; i += NT) {
         const int b = tab_img0 + i / G, gg = i - (i / G) * G;
         double s1 = 0, s2 = 0;
 #pragma unroll 4
@@ -330,7 +336,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
       __syncthreads();
 #pragma unroll
       for (int u = 0; u < TU; ++u) {
-        const int i = t + 256 * u;
+        const int i = t + NT * u;
         if (i < tab_n * tab_c) {
           const int bi = i / tab_c, c = tab_c0 + i - (i / tab_c) * tab_c;
           const int si = 2 * (bi * G + c / cpg);
@@ -347,7 +353,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
         }
       }
     } else {
-      for (int i = t; i < tab_n * tab_c; i += 256) {
+      for (int i = t; i < tab_n * tab_c; i += NT) {
         const int bi = i / tab_c, c = tab_c0 + i - (i / tab_c) * tab_c;
         gtab[i] = a.pro_scale[(size_t)(tab_img0 + bi) * a.Cin1 + c];
         gtab[tab_n * tab_c + i] = a.pro_shift[(size_t)(tab_img0 + bi) * a.Cin1 + c];
@@ -396,7 +402,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   K32_STAMP(2);
   // ---- segment 2: 1x1 product of x2 (the ResBlock shortcut), K = Cin2 in 32-channel steps, un-pipelined
   if (a.Cin2 > 0 && (!KSPLIT || split == a.ksplit - 1)) {
-    constexpr int RJ = BM / 64;  // staging passes of 64 rows
+    constexpr int RJ = BM / SROWS;  // staging passes of SROWS rows
     const size_t s2 = (size_t)(NTAP * a.Cin1 / 16) * sl + (size_t)(q >> 1) * sl;  // 16-slices 9 Cin1/16 + 2 c2 + (q>>1)
     int abase[TM];
 #pragma unroll
@@ -404,7 +410,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     const float* xsrc[RJ];
 #pragma unroll
     for (int j = 0; j < RJ; ++j)
-      xsrc[j] = a.x2 + (size_t)min(m0 + srow + 64 * j, M - 1) * a.x2_pitch + 8 * sq;
+      xsrc[j] = a.x2 + (size_t)min(m0 + srow + SROWS * j, M - 1) * a.x2_pitch + 8 * sq;
     for (int c2 = 0; c2 < a.Cin2 / kC; ++c2) {
       f4 r[RJ][2];
 #pragma unroll
@@ -417,7 +423,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
       for (int j = 0; j < RJ; ++j) {  // rows >= M hold clamped data: never stored
         f16x8 pc[2];
         Split<2>::split(r[j][0], r[j][1], pc, bad);
-        const int row = srow + 64 * j;
+        const int row = srow + SROWS * j;
         *reinterpret_cast<f16x8*>(patch + row * kRowH + sq * 8) = pc[0];
         *reinterpret_cast<f16x8*>(patch + row * kRowH + 32 + sq * 8) = pc[1];
       }
@@ -889,6 +895,19 @@ static bool conv_k32s_ok(const ConvArgs& a) {
 
 int conv_k32_variant_ok(const ConvArgs& a, int v) {
   if (v == 6) return conv_k32s_ok(a) ? 1 : 0;
+  if (v == 7) {  // 128-row tiles of 512 threads over one image's 128-pixel row segment or two 64-pixel rows
+    const bool sub = a.upsample == 2;
+    if (!(a.ws && a.ws_np == 2 && a.ws_rowscale && a.taps == 9 && a.stride == 1 && (a.upsample == 0 || sub))) return 0;
+    if (a.Cin1 < kC || a.Cin1 % kC != 0 || a.Cin2 % kC != 0 || a.ksplit > 1) return 0;
+    if (sub ? (a.Cin2 != 0 || a.K != 4 * a.Cin1) : a.K != 9 * a.Cin1 + a.Cin2) return 0;
+    const int wt = sub ? a.Win : a.Wout;
+    if (wt < 64 || (wt > 128 ? wt % 128 != 0 : 128 % wt != 0)) return 0;
+    PatchGeom g;
+    if (!conv_patch_geom(a, 128, g) || g.P > kMaxPW || g.TB != 1) return 0;
+    if (a.pro_scale && 2 * a.Cin1 > kTab) return 0;
+    if (a.gin_part && a.gin_G > kStats) return 0;
+    return staged_epilogue_ok(a) ? 1 : 0;
+  }
   const bool sub = a.upsample == 2;  // sub-pixel nearest-2x + 3x3: 4 parity convs of 4 taps
   if (!(a.ws && a.ws_np == 2 && a.ws_rowscale && a.taps == 9 && a.stride == 1 && (a.upsample == 0 || sub))) return 0;
   if (a.Cin1 < kC || a.Cin1 % kC != 0 || a.Cin2 % kC != 0) return 0;
@@ -925,6 +944,12 @@ bool conv_k32_enabled() {
   return on;
 }
 
+// The 512-thread wide-map tiles (variant 7) unless DM_CONV_K32W=0 (then variant 5, the 64-pixel segments)
+static bool conv_k32_wide_enabled() {
+  const char* e = std::getenv("DM_CONV_K32W");
+  return !(e && e[0] == '0');
+}
+
 // The small-map kernel (variant 6) unless DM_CONV_K32S=0 (the two-launch split-K path, kept as its test oracle;
 // read per call: plans capture their launches once, so this costs nothing per forward)
 static bool conv_k32_small_enabled() {
@@ -933,7 +958,7 @@ static bool conv_k32_small_enabled() {
 }
 
 int conv_k32_pick(const ConvArgs& a) {
-  if (a.tile >= 10 && a.tile <= 15) return conv_k32_variant_ok(a, a.tile - 9) ? a.tile - 9 : 0;
+  if (a.tile >= 10 && a.tile <= 16) return conv_k32_variant_ok(a, a.tile - 9) ? a.tile - 9 : 0;
   if (a.tile != 0 || !conv_k32_enabled()) return 0;
   // split-K convs of maps of <= 16 pixels: 64 x 128 tiles (4x4 maps at B = 256, K split 2: 32.5 us vs
   // 34.2 us for 64 x 64 and for conv_patch3's 64 x 64 split tiles)
@@ -942,8 +967,10 @@ int conv_k32_pick(const ConvArgs& a) {
     return conv_k32_variant_ok(a, 4) ? 4 : conv_k32_variant_ok(a, 3) ? 3 : 0;
   }
   if (!conv_k32_ok(a)) {
-    // maps whose whole-row 128-row tiles do not fit the patch image (64^2 .. 256^2): 64-pixel rows / segments
+    // maps whose whole-row 128-row tiles do not fit the patch image (64^2 .. 256^2): 128-pixel row segments /
+    // two-row tiles of 8 waves, else 64-pixel rows / segments
     const int wt = a.upsample == 2 ? a.Win : a.Wout;
+    if (wt >= 64 && conv_k32_wide_enabled() && conv_k32_variant_ok(a, 7)) return 7;
     return (wt >= 64 && conv_k32_variant_ok(a, 5)) ? 5 : 0;
   }
   const int p = conv_pick(a);
@@ -957,6 +984,9 @@ int conv_k32_pick(const ConvArgs& a) {
 // rocprofv3's name of the instantiation conv2d_k32 launches (spaces removed)
 std::string conv_k32_label(const ConvArgs& a, int v) {
   if (v == 6) return std::string("conv_k32s_kernel<") + (a.pro_scale || a.gin_part ? "true>" : "false>");
+  if (v == 7)
+    return std::string("conv_k32_kernel<128,128,64,32,") + (a.pro_scale ? "true," : "false,") + "false," +
+           (a.upsample == 2 ? "true,512>" : "false,512>");
   static const char* names[] = {"", "conv_k32_kernel<128,128,64,64,", "conv_k32_kernel<128,64,64,32,",
                                 "conv_k32_kernel<64,64,32,32,", "conv_k32_kernel<64,128,32,64,",
                                 "conv_k32_kernel<64,128,32,64,"};
@@ -964,7 +994,7 @@ std::string conv_k32_label(const ConvArgs& a, int v) {
          (a.upsample == 2 ? "true>" : "false>");
 }
 
-template <int BM, int BN, int WM, int WN, bool KSPLIT>
+template <int BM, int BN, int WM, int WN, bool KSPLIT, int NT = 256, int MAXP = kMaxP>
 static void launch_k32(const ConvArgs& a, const PatchGeom& g, hipStream_t st) {
   const bool sub = a.upsample == 2;
   const int M = sub ? a.B * a.Hin * a.Win : a.B * a.Hout * a.Wout;
@@ -972,20 +1002,24 @@ static void launch_k32(const ConvArgs& a, const PatchGeom& g, hipStream_t st) {
   if constexpr (!KSPLIT) {
     if (sub) {
       if (a.pro_scale)
-        hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, true, false, true>), dim3(blocks), dim3(256), 0, st, a, g);
+        hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, true, false, true, NT, MAXP>), dim3(blocks), dim3(NT), 0, st,
+                           a, g);
       else
-        hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, false, false, true>), dim3(blocks), dim3(256), 0, st, a, g);
+        hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, false, false, true, NT, MAXP>), dim3(blocks), dim3(NT), 0,
+                           st, a, g);
       return;
     }
   }
   if (a.pro_scale)
-    hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, true, KSPLIT>), dim3(blocks), dim3(256), 0, st, a, g);
+    hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, true, KSPLIT, false, NT, MAXP>), dim3(blocks), dim3(NT), 0, st,
+                       a, g);
   else
-    hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, false, KSPLIT>), dim3(blocks), dim3(256), 0, st, a, g);
+    hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, false, KSPLIT, false, NT, MAXP>), dim3(blocks), dim3(NT), 0, st,
+                       a, g);
 }
 
 int conv2d_k32(const ConvArgs& a, int v, hipStream_t st) {
-  DM_REQUIRE(v >= 1 && v <= 6 && conv_k32_variant_ok(a, v), "conv: shape not supported by the K = 32 split kernel");
+  DM_REQUIRE(v >= 1 && v <= 7 && conv_k32_variant_ok(a, v), "conv: shape not supported by the K = 32 split kernel");
   PatchGeom g;
   if (v == 6) {
     conv_patch_geom(a, 64, g);
@@ -997,8 +1031,9 @@ int conv2d_k32(const ConvArgs& a, int v, hipStream_t st) {
     DM_LAUNCH_CHECK();
     return DM_OK;
   }
-  conv_patch_geom(a, v >= 3 ? 64 : BM_K32, g);
+  conv_patch_geom(a, v >= 3 && v != 7 ? 64 : BM_K32, g);
   switch (v) {
+    case 7: launch_k32<128, 128, 64, 32, false, 512, kMaxPW>(a, g, st); break;
     case 1: launch_k32<128, 128, 64, 64, false>(a, g, st); break;
     case 2: launch_k32<128, 64, 64, 32, false>(a, g, st); break;
     case 3: launch_k32<64, 64, 32, 32, true>(a, g, st); break;

@@ -162,7 +162,7 @@ def test_k32_subpixel_fp32_accuracy(cuda, B, Cin, Cout, H):
         assert errs[k] < 4e-6 * scale, (errs, scale)
 
 
-@pytest.mark.parametrize('tile', [14, 0])
+@pytest.mark.parametrize('tile', [14, 16, 0])
 @pytest.mark.parametrize('B,Cin,Cout,H', [(2, 64, 128, 64), (1, 32, 64, 128), (1, 64, 64, 256), (3, 96, 160, 64)])
 def test_k32_row_segments_exact(cuda, B, Cin, Cout, H, tile):
     """64 x 128 tiles over one 64-pixel row or a 64-pixel segment of a wider row (ADM's 64^2 .. 256^2 maps)."""
@@ -175,7 +175,7 @@ def test_k32_row_segments_exact(cuda, B, Cin, Cout, H, tile):
     assert torch.equal(y.cpu(), _nhwc(ref))
 
 
-@pytest.mark.parametrize('tile', [14, 0])
+@pytest.mark.parametrize('tile', [14, 16, 0])
 def test_k32_row_segments_segments_rowvec_residual(cuda, tile):
     B, C1, C2, Cout, H = 2, 64, 32, 64, 128
     h = _ints((B, C1, H, H), seed=60)
@@ -197,7 +197,7 @@ def test_k32_row_segments_segments_rowvec_residual(cuda, tile):
     assert torch.isnan(y[..., Cout:]).all()
 
 
-@pytest.mark.parametrize('tile', [14, 0])
+@pytest.mark.parametrize('tile', [14, 16, 0])
 @pytest.mark.parametrize('B,Cin,Cout,H', [(1, 64, 64, 64), (1, 32, 64, 128)])
 def test_k32_row_segments_subpixel_exact(cuda, B, Cin, Cout, H, tile):
     x = _ints((B, Cin, H, H), -2, 3, seed=80)
@@ -210,11 +210,13 @@ def test_k32_row_segments_subpixel_exact(cuda, B, Cin, Cout, H, tile):
     assert torch.equal(y.cpu(), _nhwc(ref))
 
 
-@pytest.mark.parametrize('B,Cin,Cout,H', [(2, 256, 256, 64), (1, 256, 128, 128)])
-def test_k32_row_segments_fp32_accuracy(cuda, B, Cin, Cout, H):
-    """(the fp32 kernels have no fused-GroupNorm shape this wide: the bound alone, as for the other tiles)"""
+@pytest.mark.parametrize('tile', [14, 16])
+@pytest.mark.parametrize('B,Cin,Cout,H', [(2, 256, 256, 64), (1, 256, 128, 128), (1, 128, 128, 256)])
+def test_k32_row_segments_fp32_accuracy(cuda, B, Cin, Cout, H, tile):
+    """(the fp32 kernels have no fused-GroupNorm shape this wide: the bound alone, as for the other tiles;
+    tile 16 = the 512-thread 128-pixel row segments / two-row tiles)"""
     xd, wp, b, pro, ref = _rand_case(cuda, B, Cin, Cout, H, 0, seed=94)
-    y = _run_conv(cuda, xd, wp, Cout, H, H, 9, 1, 0, b.to(cuda), pro=pro, split='fp16x2', tile=14)
+    y = _run_conv(cuda, xd, wp, Cout, H, H, 9, 1, 0, b.to(cuda), pro=pro, split='fp16x2', tile=tile)
     err = (y.cpu().double() - _nhwc(ref)).abs().max().item()
     scale = ref.abs().max().item()
     assert err < 4e-6 * scale, (err, scale)
