@@ -336,8 +336,14 @@ int DiTModel::build_plan(Plan& pl, int B) {
       return embed_add_silu(temb, P_->y, table, B, D, se, st, null_row);
     });
   }
-  // every block's (and the final layer's) adaLN modulation in one GEMM: [B][depth * 6D + 2D]
-  add_gemm(linear(se, D, B, ada_w, ada_b, ada_total, D, mods, ada_total));
+  // every block's (and the final layer's) adaLN modulation in one GEMM: [B][depth * 6D + 2D]. A weight stream
+  // (902 MB for DiT-XL/2 against 2B = 64 rows): on linear_k32 with the weights pre-split once, one block per
+  // 128 columns streaming its K x 128 slice (the fp32 gemm_kernel took 558 us, 1.6 TB/s)
+  {
+    GemmArgs g = linear(se, D, B, ada_w, ada_b, ada_total, D, mods, ada_total);
+    if (!std::getenv("DM_DIT_ADA_FP32")) split(g, 6, ada_w, (size_t)ada_total * D, 6);
+    add_gemm(g);
+  }
 
   // --- patch embedding + pos_embed (dit/model.py:244)
   pl.add("patchify", 0, 8.0 * M * C * p * p,
