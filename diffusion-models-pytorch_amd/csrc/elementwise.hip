@@ -188,80 +188,15 @@ __global__ void __launch_bounds__(256) conv3x3_small_in_kernel(const float* __re
   }
 }
 
-// last conv: NHWC (pitched) input -> NCHW output with few channels (Cout <= 8).
-// Block = TH x TW output pixels of one image, one pixel per thread. Per 32-channel
-// chunk the (TH+2) x (TW+2) halo patch and the chunk's weights ([tap][c][8]) are
-// staged in LDS; each thread accumulates its Cout outputs from the patch.
-constexpr int kSoTW = 32, kSoTH = 8, kSoPP = (kSoTH + 2) * (kSoTW + 2), kSoLD = 36;
-// Last conv (Cout <= 8): one output pixel per thread, CO = Cout rounded up to 4 accumulators. The
-// input patch (GroupNorm + SiLU applied) is staged in LDS per 32-channel chunk; the weights come
-// pre-packed [tap][Cin][CO] (small_out_pack) and are read with wave-uniform addresses, so they are
-// scalar loads (constant cache, SGPR operands) rather than LDS traffic.
-template <int CO>
-__global__ void __launch_bounds__(256) conv3x3_small_out_kernel(const float* __restrict__ x, int B, int H, int W,
-                                                                int Cin, int pitch, const float* __restrict__ wp,
-                                                                const float* __restrict__ bias, int Cout,
-                                                                float* __restrict__ y,
-                                                                const float* __restrict__ pro_scale,
-                                                                const float* __restrict__ pro_shift) {
-  __shared__ __attribute__((aligned(16))) float patch[kSoPP * kSoLD];
-  const int tiles_x = ceil_div(W, kSoTW), tiles_y = ceil_div(H, kSoTH);
-  const int b = blockIdx.x / (tiles_x * tiles_y);
-  const int trem = blockIdx.x - b * tiles_x * tiles_y;
-  const int ty0 = (trem / tiles_x) * kSoTH, tx0 = (trem % tiles_x) * kSoTW;
-  const int t = threadIdx.x;
-  const int py = t / kSoTW, px = t % kSoTW;
-  float acc[CO];
-#pragma unroll
-  for (int c = 0; c < CO; ++c) acc[c] = 0.f;
-  for (int c0 = 0; c0 < Cin; c0 += 32) {
-    __syncthreads();
-    for (int i = t; i < kSoPP * 8; i += blockDim.x) {
-      const int p = i >> 3, c4 = i & 7;
-      const int iy = ty0 + p / (kSoTW + 2) - 1, ix = tx0 + p % (kSoTW + 2) - 1;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (iy >= 0 && iy < H && ix >= 0 && ix < W && c0 + 4 * c4 < Cin) {
-        v = *reinterpret_cast<const float4*>(x + (((size_t)b * H + iy) * W + ix) * pitch + c0 + 4 * c4);
-        if (pro_scale) {  // GroupNorm + SiLU of last_conv (models/unet.py:115-119), padding stays 0
-          const float4 sc = *reinterpret_cast<const float4*>(pro_scale + (size_t)b * Cin + c0 + 4 * c4);
-          const float4 sh = *reinterpret_cast<const float4*>(pro_shift + (size_t)b * Cin + c0 + 4 * c4);
-          v.x = silu_fast(v.x * sc.x + sh.x); v.y = silu_fast(v.y * sc.y + sh.y);
-          v.z = silu_fast(v.z * sc.z + sh.z); v.w = silu_fast(v.w * sc.w + sh.w);
-        }
-      }
-      *reinterpret_cast<float4*>(patch + p * kSoLD + 4 * c4) = v;
-    }
-    __syncthreads();
-#pragma unroll 3
-    for (int tap = 0; tap < 9; ++tap) {
-      const float* pr = patch + ((py + tap / 3) * (kSoTW + 2) + px + tap % 3) * kSoLD;
-      const float* wt = wp + ((size_t)tap * Cin + c0) * CO;  // wave-uniform
-#pragma unroll
-      for (int c4 = 0; c4 < 8; ++c4) {
-        const float4 v = *reinterpret_cast<const float4*>(pr + 4 * c4);
-        const float vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-          for (int co = 0; co < CO; ++co) acc[co] = fmaf(vv[q], wt[(4 * c4 + q) * CO + co], acc[co]);
-      }
-    }
-  }
-  const int oy = ty0 + py, ox = tx0 + px;
-  if (oy < H && ox < W) {
-#pragma unroll
-    for (int c = 0; c < CO; ++c)
-      if (c < Cout) y[(((size_t)b * Cout + c) * H + oy) * W + ox] = acc[c] + bias[c];
-  }
-}
-
+// last conv: NHWC (pitched) input -> NCHW output with few channels (Cout <= 8). Block = TH x TW output
+// pixels of one image, one pixel per thread.
+constexpr int kSoTW = 32, kSoTH = 8, kSoPP = (kSoTH + 2) * (kSoTW + 2);
 // Last conv, pipelined form (the CIFAR / MNIST UNets' 128 -> 3 or 1 channel output conv at 32^2 / 28^2):
 // 16-channel chunks (a 10 x 34 x 16 patch in 27 KB of LDS: five blocks per CU, so the B * 4 tiles of a
 // B = 256 batch run in one wave of blocks instead of 1.33), the next chunk's patch loaded into registers
 // while this chunk's 9 taps run (the previous form loaded, waited, then computed each 32-channel chunk), and
 // exactly CO = Cout accumulators (no padded output). Weights [9][Cin][CO] from wave-uniform scalar loads.
-// Summation per output over (16-channel chunk, tap, channel), fp32 FMAs (conv3x3_small_out_kernel: 32-channel
-// chunks, kept for Cout 5 .. 8).
+// Summation per output over (16-channel chunk, tap, channel), fp32 FMAs.
 constexpr int kSo2C = 16, kSo2LD = 20, kSo2PJ = (kSoPP * (kSo2C / 4) + 255) / 256;
 template <int CO>
 __global__ void __launch_bounds__(256) conv3x3_small_out2_kernel(const float* __restrict__ x, int B, int H, int W,
@@ -626,7 +561,7 @@ int conv3x3_small_in(const float* x, int B, int Cin, int H, int W, const float* 
 
 int small_out_pack(const float* w, int Cout, int Cin, float* wp, hipStream_t st) {
   DM_REQUIRE(Cout >= 1 && Cout <= 8 && Cin > 0, "last conv: Cout out of range");
-  const int CO = Cout <= 4 ? Cout : 8;  // conv3x3_small_out2_kernel<Cout> / conv3x3_small_out_kernel<8>
+  const int CO = Cout;  // conv3x3_small_out2_kernel<Cout>: exactly Cout accumulators
   hipLaunchKernelGGL(small_out_pack_kernel, dim3((9 * Cin * CO + 255) / 256), dim3(256), 0, st, w, Cout, Cin, CO, wp);
   DM_LAUNCH_CHECK();
   return DM_OK;
@@ -636,7 +571,7 @@ int conv3x3_small_out(const View& x, const float* wp, const float* bias, int Cou
                       const float* pro_scale, const float* pro_shift) {
   DM_REQUIRE(Cout >= 1 && Cout <= 8, "last conv: Cout out of range");
   DM_REQUIRE(x.C % 32 == 0 && x.pitch % 4 == 0, "last conv: Cin must be a multiple of 32");
-  // wp: small_out_pack's [9][Cin][CO], CO = Cout (<= 4) or 8
+  // wp: small_out_pack's [9][Cin][Cout]
   DM_REQUIRE((reinterpret_cast<uintptr_t>(x.p) & 15) == 0, "last conv: input must be 16-byte aligned");
   const long tiles = (long)x.B * ceil_div(x.H, kSoTH) * ceil_div(x.W, kSoTW);
 #define DM_SO2(CO)                                                                                            \
@@ -650,10 +585,15 @@ int conv3x3_small_out(const View& x, const float* wp, const float* bias, int Cou
     DM_SO2(3);
   else if (Cout == 4)
     DM_SO2(4);
-#undef DM_SO2
+  else if (Cout == 5)
+    DM_SO2(5);
+  else if (Cout == 6)
+    DM_SO2(6);
+  else if (Cout == 7)
+    DM_SO2(7);
   else
-    hipLaunchKernelGGL(conv3x3_small_out_kernel<8>, dim3((unsigned)tiles), dim3(256), 0, st, x.p, x.B, x.H, x.W, x.C,
-                       x.pitch, wp, bias, Cout, y, pro_scale, pro_shift);
+    DM_SO2(8);
+#undef DM_SO2
   DM_LAUNCH_CHECK();
   return DM_OK;
 }
