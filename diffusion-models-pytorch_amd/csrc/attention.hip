@@ -718,7 +718,6 @@ __global__ void __launch_bounds__(NW * 64) attn_flash_kernel(AttnArgs a) {
   }
 
   const float sl2 = ldexpf(1.f, -(a.ea + a.eb)) * 1.4426950408889634f;   // exact unscale x log2(e)
-  const float pp = ldexpf(1.f, a.ep);
   f16v oacc[NDT];
 #pragma unroll
   for (int i = 0; i < NDT; ++i)
@@ -751,17 +750,17 @@ __global__ void __launch_bounds__(NW * 64) attn_flash_kernel(AttnArgs a) {
         Split<2>::mma(ka, qf[s], sacc[j]);
       }
     }
-    // online softmax of this query row (lane) over the block's 64 keys (32 here, 32 in the other half-wave)
+    // online softmax of this query row (lane) over the block's 64 keys (32 here, 32 in the other half-wave):
+    // the running maximum m_run in the scaled (log2) domain, the max taken over the raw scores and scaled once
+    // (sl2 > 0), each probability exp2(s sl2 - m) as one FMA and one exp2; the P scale 2^ep folded into the
+    // exponent (l_run accumulates 2^ep p, undone at the end)
     float mx = -INFINITY;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        sacc[j][r] *= sl2;
-        mx = fmaxf(mx, sacc[j][r]);
-      }
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[j][r]);
     mx = fmaxf(mx, __shfl_xor(mx, 32));
-    const float m_new = fmaxf(m_run, mx);
+    const float m_new = fmaxf(m_run, mx * sl2);
     const float corr = __builtin_amdgcn_exp2f(m_run - m_new);
     m_run = m_new;
     l_run *= corr;
@@ -769,15 +768,15 @@ __global__ void __launch_bounds__(NW * 64) attn_flash_kernel(AttnArgs a) {
     for (int i = 0; i < NDT; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) oacc[i][r] *= corr;
+    const float mb = (float)a.ep - m_new;
     // P^T pieces: k-step ks = 16 keys = accumulator registers 8 (ks & 1) .. + 7 of tile ks >> 1
     f16x8 pb[4][2];
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float pv = __builtin_amdgcn_exp2f(sacc[ks >> 1][8 * (ks & 1) + e] - m_new);
-        l_run += pv;
-        const float x = pv * pp;
+        const float x = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[ks >> 1][8 * (ks & 1) + e], sl2, mb));
+        l_run += x;
         const _Float16 h0 = (_Float16)x;
         pb[ks][0][e] = h0;
         pb[ks][1][e] = (_Float16)(x - (float)h0);
@@ -800,8 +799,8 @@ __global__ void __launch_bounds__(NW * 64) attn_flash_kernel(AttnArgs a) {
   }
 
   // O = O^T / l (x 2^-(ep + ev)), staged through LDS as [32 queries][Dh + 1] fp32 rows per wave, stored as rows
-  const float l_tot = l_run + __shfl_xor(l_run, 32);
-  const float scale = ldexpf(1.f, -(a.ep + a.ev)) / l_tot;
+  const float l_tot = l_run + __shfl_xor(l_run, 32);   // 2^ep x the softmax denominator
+  const float scale = ldexpf(1.f, -a.ev) / l_tot;
   constexpr int OP = Dh + 1;
   float* st = reinterpret_cast<float*>(lds) + wave * 32 * OP;
 #pragma unroll
