@@ -710,8 +710,8 @@ __global__ void __launch_bounds__(NW * 64) attn_flash_kernel(AttnArgs a) {
     }
   };
   // zero the K rows' head-dim padding (d in [Dh, DHP)) of both buffers: never written by the loader
+  constexpr int per = 2 * (DHP / 8 - dh8 > 0 ? DHP / 8 - dh8 : 1);  // no padding (Dh % 32 == 0): no iterations
   for (int i = t; i < 2 * KB * 2 * (DHP / 8 - dh8); i += NT) {
-    const int per = 2 * (DHP / 8 - dh8);
     const int rowb = i / per, rem = i - rowb * per;
     const int buf = rowb / KB, row = rowb - buf * KB, p = rem & 1, c8 = dh8 + (rem >> 1);
     *reinterpret_cast<f4*>(lds + buf * BUF + row * KP + (c8 >> 1) * 32 + p * 16 + (c8 & 1) * 8) = f4{0.f, 0.f, 0.f, 0.f};

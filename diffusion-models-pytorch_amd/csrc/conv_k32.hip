@@ -900,12 +900,16 @@ int conv_k32_variant_ok(const ConvArgs& a, int v) {
     if (!(a.ws && a.ws_np == 2 && a.ws_rowscale && a.taps == 9 && a.stride == 1 && (a.upsample == 0 || sub))) return 0;
     if (a.Cin1 < kC || a.Cin1 % kC != 0 || a.Cin2 % kC != 0 || a.ksplit > 1) return 0;
     if (sub ? (a.Cin2 != 0 || a.K != 4 * a.Cin1) : a.K != 9 * a.Cin1 + a.Cin2) return 0;
+    // or whole rows of up to two images of a narrower map (8^2 .. 32^2: 8 waves per CU where 256 blocks of 4
+    // waves leave one wave per SIMD)
     const int wt = sub ? a.Win : a.Wout;
-    if (wt < 64 || (wt > 128 ? wt % 128 != 0 : 128 % wt != 0)) return 0;
+    const bool wide = wt >= 64 && (wt > 128 ? wt % 128 == 0 : 128 % wt == 0);
+    const bool narrow = wt < 64 && wt % 8 == 0 && 128 % wt == 0;
+    if (!wide && !narrow) return 0;
     PatchGeom g;
-    if (!conv_patch_geom(a, 128, g) || g.P > kMaxPW || g.TB != 1) return 0;
-    if (a.pro_scale && 2 * a.Cin1 > kTab) return 0;
-    if (a.gin_part && a.gin_G > kStats) return 0;
+    if (!conv_patch_geom(a, 128, g) || g.P > kMaxPW || g.TB > (wide ? 1 : 2)) return 0;
+    if (a.pro_scale && 2 * g.TB * a.Cin1 > kTab) return 0;
+    if (a.gin_part && g.TB * a.gin_G > kStats) return 0;
     return staged_epilogue_ok(a) ? 1 : 0;
   }
   const bool sub = a.upsample == 2;  // sub-pixel nearest-2x + 3x3: 4 parity convs of 4 taps

@@ -207,8 +207,10 @@ struct StepArgs {
 int gn_num_chunks(int HW);
 int gn_partial(const View& x, int G, double2* part, hipStream_t st);
 // partials of a concat [h (Ch) | skip (Cs)] from the slices' own G-group partials (group-aligned slices)
-int gn_concat_stats(const double2* ph, int Ch, const double2* ps, int Cs, int B, int HW, int G, double2* out,
-                    hipStream_t st);
+// slice partials with their own group counts (Gh over Ch, Gs over Cs) -> the concat's G groups
+bool gn_concat_ok(int Ch, int Gh, int Cs, int Gs, int G);
+int gn_concat_stats(const double2* ph, int Ch, int Gh, const double2* ps, int Cs, int Gs, int B, int HW, int G,
+                    double2* out, hipStream_t st);
 int gn_finalize(const View& x, int G, const double2* part, float eps, const float* gamma, const float* beta,
                 float* scale, float* shift, hipStream_t st, const float* mod_scale = nullptr,
                 const float* mod_shift = nullptr, int mod_pitch = 0);
@@ -323,8 +325,10 @@ int attn_fused(const AttnArgs& a, hipStream_t st);
 // ADM's L = 1024 / 64 blocks, DiT's 72-wide heads. attn_fused dispatches there for shapes it does not take.
 bool attn_flash_ok(int L, int Dh);
 int attn_flash(const AttnArgs& a, hipStream_t st);
+// first conv; with gn_part also the GroupNorm(G) chunk partials of its output (conv3x3_small_in_can_emit)
 int conv3x3_small_in(const float* x, int B, int Cin, int H, int W, const float* w, const float* bias,
-                     int Cout, const View& y, hipStream_t st);
+                     int Cout, const View& y, hipStream_t st, double2* gn_part = nullptr, int G = 0);
+bool conv3x3_small_in_can_emit(int H, int W, int Cout, int G);
 // last conv weights torch [Cout][Cin][3][3] -> [9][Cin][CO], CO = 4 (Cout <= 4) or 8; wp holds 9 * Cin * CO floats
 int small_out_pack(const float* w, int Cout, int Cin, float* wp, hipStream_t st);
 int conv3x3_small_out(const View& x, const float* wp, const float* bias, int Cout, float* y, hipStream_t st,

@@ -121,69 +121,135 @@ __global__ void softmax_rows_kernel(float* __restrict__ x, long rows, int L, int
 }
 
 // first conv: NCHW input with few channels -> NHWC (pitched) output.
-// One block per (image, output row). Thread t owns output channel co = t % Cout
-// (its 9*Cin weights live in registers) and every (256/Cout)-th pixel of the row;
-// the three input rows sit in LDS and are read as broadcasts (all lanes of a
-// wave share the pixel). Stores are coalesced over co.
+// One block per R output rows of one image (R = 64 / W for W < 64, so a block is one 64-pixel GroupNorm
+// chunk; else one row). Thread t owns output channel co = t % Cout (its 9*Cin weights, staged through LDS
+// with coalesced loads, in registers) and a run of pixels of the block; the R + 2 input rows sit in LDS and
+// are read as broadcasts (all lanes of a wave share the pixel). Stores are coalesced over co. With gn_part
+// the block also emits the consumer GroupNorm's per-chunk partials (sum, sum of squares in double) -- the
+// layout of gn_partial_kernel -- so the first ResBlock and the last up-path concat skip their gn_partial
+// passes.
+constexpr int kSiMaxChunks = 8, kSiMaxPar = 4, kSiMaxG = 32;
 template <int CIN>
-__global__ void __launch_bounds__(256) conv3x3_small_in_kernel(const float* __restrict__ x, int H, int W,
+__global__ void __launch_bounds__(256) conv3x3_small_in_kernel(const float* __restrict__ x, int H, int W, int R,
                                                                const float* __restrict__ w,
                                                                const float* __restrict__ bias, int Cout,
-                                                               float* __restrict__ y, int y_pitch) {
-  extern __shared__ float rows[];  // [CIN][3][W + 2]
-  const int b = blockIdx.y, oy = blockIdx.x;
+                                                               float* __restrict__ y, int y_pitch,
+                                                               double2* __restrict__ gn_part, int G, int nchunk) {
+  extern __shared__ __attribute__((aligned(16))) float smem_f[];
   const int Wp = W + 2;
-  for (int i = threadIdx.x; i < CIN * 3 * Wp; i += blockDim.x) {
-    const int ci = i / (3 * Wp);
-    const int rr = (i / Wp) % 3;
+  const int nrow = CIN * (R + 2) * Wp;
+  float* rows = smem_f;                                       // [CIN][R + 2][W + 2]
+  float* wl = smem_f + nrow;                                  // [Cout][CIN * 9]
+  double2* st = reinterpret_cast<double2*>(smem_f + ((nrow + Cout * CIN * 9 + 3) & ~3));  // [par][chunk][G]
+  const int b = blockIdx.y, oy0 = blockIdx.x * R;
+  for (int i = threadIdx.x; i < nrow; i += blockDim.x) {
+    const int ci = i / ((R + 2) * Wp);
+    const int rr = (i / Wp) % (R + 2);
     const int xx = i % Wp - 1;
-    const int iy = oy + rr - 1;
+    const int iy = oy0 + rr - 1;
     float v = 0.f;
     if (iy >= 0 && iy < H && xx >= 0 && xx < W) v = x[(((size_t)b * CIN + ci) * H + iy) * W + xx];
     rows[i] = v;
   }
-  __syncthreads();
+  for (int i = threadIdx.x; i < Cout * CIN * 9; i += blockDim.x) wl[i] = w[i];
   const int lanes_per_px = min(Cout, (int)blockDim.x);
   const int px_par = blockDim.x / lanes_per_px;
+  const int cpg = gn_part ? Cout / G : 1;
+  const int bchunks = (R * W) / kGnPixPerChunk;
+  if (gn_part)
+    for (int i = threadIdx.x; i < px_par * kSiMaxChunks * kSiMaxG; i += blockDim.x) st[i] = make_double2(0.0, 0.0);
+  __syncthreads();
+  // this thread's pixels: px_par groups over R rows (whole rows, or row segments when px_par > R)
+  const int gI = threadIdx.x / lanes_per_px;
+  int r0, r1, x0, x1;
+  if (px_par >= R) {
+    const int S = px_par / R, len = (W + S - 1) / S;
+    r0 = gI / S;
+    r1 = min(r0 + 1, R);
+    x0 = (gI % S) * len;
+    x1 = min(x0 + len, W);
+  } else {
+    const int RG = R / px_par;
+    r0 = gI * RG;
+    r1 = r0 + RG;
+    x0 = 0;
+    x1 = W;
+  }
   for (int co = threadIdx.x % lanes_per_px; co < Cout; co += lanes_per_px) {
     float wr[CIN * 9];
 #pragma unroll
-    for (int k = 0; k < CIN * 9; ++k) wr[k] = w[(size_t)co * CIN * 9 + k];
+    for (int k = 0; k < CIN * 9; ++k) wr[k] = wl[co * CIN * 9 + k];
     const float bc = bias[co];
-    // a contiguous run of pixels per thread with a sliding 3x3 window in registers: one new LDS
-    // column (3 CIN broadcasts) per pixel instead of 9 CIN; same products in the same order
-    const int R = (W + px_par - 1) / px_par;
-    const int x0 = (threadIdx.x / lanes_per_px) * R, x1 = min(x0 + R, W);
-    float win[CIN][3][3];
-    if (x0 < x1) {
+    double gs = 0.0, gq = 0.0;
+    int cur = -1;  // chunk the (gs, gq) sums belong to
+    auto flush = [&]() {  // over the group's cpg channel lanes, then one LDS slot per (px group, chunk, group)
+      double s = gs, q = gq;
+      for (int o = 1; o < cpg; o <<= 1) {
+        s += __shfl_xor(s, o);
+        q += __shfl_xor(q, o);
+      }
+      if (co % cpg == 0) st[(gI * kSiMaxChunks + cur) * kSiMaxG + co / cpg] = make_double2(s, q);
+      gs = gq = 0.0;
+    };
+    for (int r = r0; r < r1; ++r) {
+      if (x0 >= x1) break;
+      // a contiguous run of pixels with a sliding 3x3 window in registers: one new LDS column (3 CIN
+      // broadcasts) per pixel instead of 9 CIN; same products in the same order
+      float win[CIN][3][3];
 #pragma unroll
       for (int ci = 0; ci < CIN; ++ci)
 #pragma unroll
         for (int ky = 0; ky < 3; ++ky) {
-          win[ci][ky][0] = rows[(ci * 3 + ky) * Wp + x0];
-          win[ci][ky][1] = rows[(ci * 3 + ky) * Wp + x0 + 1];
+          win[ci][ky][0] = rows[(ci * (R + 2) + r + ky) * Wp + x0];
+          win[ci][ky][1] = rows[(ci * (R + 2) + r + ky) * Wp + x0 + 1];
         }
+      const int oy = oy0 + r;
+      for (int ox = x0; ox < x1; ++ox) {
+#pragma unroll
+        for (int ci = 0; ci < CIN; ++ci)
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky) win[ci][ky][2] = rows[(ci * (R + 2) + r + ky) * Wp + ox + 2];
+        float acc = 0.f;
+#pragma unroll
+        for (int ci = 0; ci < CIN; ++ci)
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) acc += wr[(ci * 3 + ky) * 3 + kx] * win[ci][ky][kx];
+        const float v = acc + bc;
+        y[(((size_t)b * H + oy) * W + ox) * y_pitch + co] = v;
+        if (gn_part) {
+          const int ch = ((oy - oy0) * W + ox) / kGnPixPerChunk;  // block-local chunk
+          if (ch != cur) {
+            if (cur >= 0) flush();
+            cur = ch;
+          }
+          gs += (double)v;
+          gq += (double)v * v;
+        }
+#pragma unroll
+        for (int ci = 0; ci < CIN; ++ci)
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky) {
+            win[ci][ky][0] = win[ci][ky][1];
+            win[ci][ky][1] = win[ci][ky][2];
+          }
+      }
     }
-    for (int ox = x0; ox < x1; ++ox) {
-#pragma unroll
-      for (int ci = 0; ci < CIN; ++ci)
-#pragma unroll
-        for (int ky = 0; ky < 3; ++ky) win[ci][ky][2] = rows[(ci * 3 + ky) * Wp + ox + 2];
-      float acc = 0.f;
-#pragma unroll
-      for (int ci = 0; ci < CIN; ++ci)
-#pragma unroll
-        for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-          for (int kx = 0; kx < 3; ++kx) acc += wr[(ci * 3 + ky) * 3 + kx] * win[ci][ky][kx];
-      y[(((size_t)b * H + oy) * W + ox) * y_pitch + co] = acc + bc;
-#pragma unroll
-      for (int ci = 0; ci < CIN; ++ci)
-#pragma unroll
-        for (int ky = 0; ky < 3; ++ky) {
-          win[ci][ky][0] = win[ci][ky][1];
-          win[ci][ky][1] = win[ci][ky][2];
-        }
+    if (gn_part && cur >= 0) flush();
+  }
+  if (gn_part) {
+    __syncthreads();
+    const size_t c0 = (size_t)blockIdx.x * bchunks;
+    for (int i = threadIdx.x; i < bchunks * G; i += blockDim.x) {
+      const int cl = i / G, g = i - (i / G) * G;
+      double s = 0.0, q = 0.0;
+      for (int p = 0; p < px_par; ++p) {
+        const double2 v = st[(p * kSiMaxChunks + cl) * kSiMaxG + g];
+        s += v.x;
+        q += v.y;
+      }
+      gn_part[((size_t)b * nchunk + c0 + cl) * G + g] = make_double2(s, q);
     }
   }
 }
@@ -542,19 +608,38 @@ int softmax_rows(float* x, long rows, int L, int ld, hipStream_t st) {
   return DM_OK;
 }
 
+// rows per block of the first conv: a whole 64-pixel chunk when W < 64 divides it, else one row
+static int small_in_rows(int H, int W) { return (W < kGnPixPerChunk && kGnPixPerChunk % W == 0 && H % (kGnPixPerChunk / W) == 0) ? kGnPixPerChunk / W : 1; }
+
+bool conv3x3_small_in_can_emit(int H, int W, int Cout, int G) {
+  const int R = small_in_rows(H, W);
+  const int lpp = min(Cout, 256);
+  return G > 0 && G <= kSiMaxG && Cout % G == 0 && (Cout / G) <= 64 && ((Cout / G) & (Cout / G - 1)) == 0 &&
+         Cout >= 64 && 256 % lpp == 0 && Cout % lpp == 0 && (R * W) % kGnPixPerChunk == 0 &&
+         (R * W) / kGnPixPerChunk <= kSiMaxChunks && 256 / lpp <= kSiMaxPar;
+}
+
 int conv3x3_small_in(const float* x, int B, int Cin, int H, int W, const float* w, const float* bias,
-                     int Cout, const View& y, hipStream_t st) {
+                     int Cout, const View& y, hipStream_t st, double2* gn_part, int G) {
   DM_REQUIRE(Cin >= 1 && Cin <= 4, "first conv: Cin out of range (1..4)");
   DM_REQUIRE(y.C == Cout && y.H == H && y.W == W && y.B == B, "first conv: output view mismatch");
-  size_t smem = (size_t)Cin * 3 * (W + 2) * sizeof(float);
+  DM_REQUIRE(!gn_part || conv3x3_small_in_can_emit(H, W, Cout, G), "first conv: GroupNorm statistics shape");
+  const int R = small_in_rows(H, W);
+  const size_t nf = (size_t)Cin * 3 * (W + 2) + (size_t)Cin * (R - 1) * (W + 2) + (size_t)Cout * Cin * 9;
+  size_t smem = ((nf + 3) & ~(size_t)3) * sizeof(float);
+  if (gn_part) smem += (size_t)kSiMaxPar * kSiMaxChunks * kSiMaxG * sizeof(double2);
   DM_REQUIRE(smem <= 64 * 1024, "first conv: image too wide");
-  dim3 grid(H, B);
+  const int nchunk = gn_num_chunks(H * W);
+  dim3 grid(H / R, B);
+#define DM_SI(CI) hipLaunchKernelGGL(conv3x3_small_in_kernel<CI>, grid, dim3(256), smem, st, x, H, W, R, w, bias, \
+                                     Cout, y.p, y.pitch, gn_part, G, nchunk)
   switch (Cin) {
-    case 1: hipLaunchKernelGGL(conv3x3_small_in_kernel<1>, grid, dim3(256), smem, st, x, H, W, w, bias, Cout, y.p, y.pitch); break;
-    case 2: hipLaunchKernelGGL(conv3x3_small_in_kernel<2>, grid, dim3(256), smem, st, x, H, W, w, bias, Cout, y.p, y.pitch); break;
-    case 3: hipLaunchKernelGGL(conv3x3_small_in_kernel<3>, grid, dim3(256), smem, st, x, H, W, w, bias, Cout, y.p, y.pitch); break;
-    default: hipLaunchKernelGGL(conv3x3_small_in_kernel<4>, grid, dim3(256), smem, st, x, H, W, w, bias, Cout, y.p, y.pitch); break;
+    case 1: DM_SI(1); break;
+    case 2: DM_SI(2); break;
+    case 3: DM_SI(3); break;
+    default: DM_SI(4); break;
   }
+#undef DM_SI
   DM_LAUNCH_CHECK();
   return DM_OK;
 }

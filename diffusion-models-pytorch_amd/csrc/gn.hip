@@ -15,6 +15,8 @@
 //                scale-shift norm), optional SiLU, and writes the output view.
 // The partial layout [B][nchunk][G] (double2) is shared with producers that
 // emit GN partials from their epilogue.
+#include <algorithm>
+
 #include "dm_common.h"
 #include "dm_kernels.h"
 
@@ -234,20 +236,27 @@ inline int gn_block_threads(int C) {
 
 }  // namespace
 
-// GroupNorm partials of a channel concat [h | skip] from its two slices' partials (each emitted with G
-// groups over its own channels by its producer): concat group j is r consecutive groups of one slice
-// (the slices are group-aligned: the caller checks it). Replaces a gn_partial pass over the concat.
+// GroupNorm partials of a channel concat [h | skip] from its two slices' partials, each emitted by its producer
+// with its own group count over its own channels (Gh over Ch, Gs over Cs: the consumer's G, or 4-channel units
+// when the concat's groups straddle the slice boundary -- the 384 = 256 + 128 concats of the CIFAR UNet): concat
+// group j sums the slice groups inside its channel range, h's then skip's, in channel order (gn_concat_ok
+// checks that no slice group straddles a concat group). Replaces a gn_partial pass over the concat.
 __global__ void gn_concat_stats_kernel(const double2* __restrict__ ph, const double2* __restrict__ ps, long n, int G,
-                                       int jh, int rh, int rs, double2* __restrict__ out) {
+                                       int cpg, int Ch, int cph, int Gh, int cps, int Gs,
+                                       double2* __restrict__ out) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   const long bk = i / G;  // (image, chunk)
   const int j = (int)(i - bk * G);
-  const double2* src = j < jh ? ph + bk * G + (size_t)j * rh : ps + bk * G + (size_t)(j - jh) * rs;
-  const int r = j < jh ? rh : rs;
+  const int c_lo = j * cpg, c_hi = c_lo + cpg;
   double s1 = 0.0, s2 = 0.0;
-  for (int u = 0; u < r; ++u) {
-    const double2 v = src[u];
+  for (int c = c_lo; c < min(c_hi, Ch); c += cph) {
+    const double2 v = ph[bk * Gh + c / cph];
+    s1 += v.x;
+    s2 += v.y;
+  }
+  for (int c = max(c_lo, Ch); c < c_hi; c += cps) {
+    const double2 v = ps[bk * Gs + (c - Ch) / cps];
     s1 += v.x;
     s2 += v.y;
   }
@@ -256,16 +265,24 @@ __global__ void gn_concat_stats_kernel(const double2* __restrict__ ph, const dou
 
 int gn_num_chunks(int HW) { return ceil_div(HW, kGnPixPerChunk); }
 
-int gn_concat_stats(const double2* ph, int Ch, const double2* ps, int Cs, int B, int HW, int G, double2* out,
-                    hipStream_t st) {
+bool gn_concat_ok(int Ch, int Gh, int Cs, int Gs, int G) {
   const int C = Ch + Cs;
-  DM_REQUIRE(C % G == 0 && Ch % G == 0 && Cs % G == 0 && (C / G) % (Ch / G) == 0 && (C / G) % (Cs / G) == 0 &&
-                 Ch % (C / G) == 0,
-             "gn_concat_stats: the slices' groups must tile the concat's groups");
-  const int cpg = C / G;
+  if (G <= 0 || Gh <= 0 || Gs <= 0 || C % G != 0 || Ch % Gh != 0 || Cs % Gs != 0) return false;
+  const int cpg = C / G, cph = Ch / Gh, cps = Cs / Gs;
+  for (int j = 0; j < G; ++j) {
+    const int lo = j * cpg, hi = lo + cpg;
+    if (lo < Ch && (lo % cph != 0 || std::min(hi, Ch) % cph != 0)) return false;
+    if (hi > Ch && ((std::max(lo, Ch) - Ch) % cps != 0 || (hi - Ch) % cps != 0)) return false;
+  }
+  return true;
+}
+
+int gn_concat_stats(const double2* ph, int Ch, int Gh, const double2* ps, int Cs, int Gs, int B, int HW, int G,
+                    double2* out, hipStream_t st) {
+  DM_REQUIRE(gn_concat_ok(Ch, Gh, Cs, Gs, G), "gn_concat_stats: the slices' groups must tile the concat's groups");
   const long n = (long)B * gn_num_chunks(HW) * G;
   hipLaunchKernelGGL(gn_concat_stats_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, ph, ps, n, G,
-                     Ch / cpg, cpg / (Ch / G), cpg / (Cs / G), out);
+                     (Ch + Cs) / G, Ch, Ch / Gh, Gh, Cs / Gs, Gs, out);
   DM_LAUNCH_CHECK();
   return DM_OK;
 }

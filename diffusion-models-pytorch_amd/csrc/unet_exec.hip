@@ -18,6 +18,7 @@
 #include <functional>
 #include <cmath>
 #include <map>
+#include <set>
 
 #include "dm_common.h"
 #include "dm_kernels.h"
@@ -767,59 +768,73 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
   // GroupNorm statistics emitted by producers (conv / GEMM epilogues): view pointer -> partials.
   // A consumer whose input view has them skips its gn_partial pass; every other write to a view
   // drops its entry.
-  std::map<const float*, std::pair<double2*, int>> gn_ready;
+  struct GnReady {
+    double2* p;
+    int C, G;  // the view's channels, the partials' group count over them
+  };
+  std::map<const float*, GnReady> gn_ready;
   _Float16* qkv_as = nullptr;  // pre-split qkv input (linear_presplit_a), shared by the attention blocks
   size_t qkv_as_bytes = 0;
-  std::map<const float*, double2*> gn_bufs;
-  auto gn_buf_for = [&](const View& v) -> double2* {
+  std::map<const float*, std::pair<double2*, int>> gn_bufs;  // view pointer -> partials buffer, its group capacity
+  auto gn_buf_for = [&](const View& v, int Gv) -> double2* {
     auto it = gn_bufs.find(v.p);
-    if (it != gn_bufs.end()) return it->second;
-    double2* b = (double2*)alloc((size_t)B * gn_num_chunks(v.H * v.W) * G * sizeof(double2));
-    gn_bufs[v.p] = b;
+    if (it != gn_bufs.end() && it->second.second >= Gv) return it->second.first;
+    double2* b = (double2*)alloc((size_t)B * gn_num_chunks(v.H * v.W) * Gv * sizeof(double2));
+    gn_bufs[v.p] = {b, Gv};
     return b;
+  };
+  // the h slice of an up-path concat [h | skip] whose GroupNorm groups straddle the slice boundary (CIFAR's
+  // 384 = 256 + 128): its producer emits 4-channel units, which gn_concat_stats sums into the concat's groups
+  std::set<const float*> concat_base;
+  for (const View& cx : concat_x)
+    if (cx.p) concat_base.insert(cx.p);
+  auto emit_groups = [&](const View& v) -> int {
+    if (std::getenv("DM_GN_NO_UNITS") || !concat_base.count(v.p) || v.pitch == v.C || v.pitch % G != 0) return G;
+    const int cpg = v.pitch / G;
+    return (v.C % cpg != 0 && cpg % 4 == 0 && v.C % 4 == 0) ? v.C / 4 : G;
   };
   auto emit_conv = [&](ConvArgs& c, const View& v) {
     gn_ready.erase(v.p);
-    c.gn_part = gn_buf_for(v);
-    c.gn_G = G;
-    ConvArgs sk = c;
-    maybe_split(sk);  // split-K is shape-determined; its reduction emits the statistics
-    if (!conv_can_emit_gn(sk)) {
-      c.gn_part = nullptr;
+    for (const int Gv : {emit_groups(v), G}) {
+      ConvArgs sk = c;
+      sk.gn_part = reinterpret_cast<double2*>(16);  // placeholder: the shape check only
+      sk.gn_G = Gv;
+      maybe_split(sk);  // split-K is shape-determined; its reduction emits the statistics
+      if (!conv_can_emit_gn(sk)) continue;
+      c.gn_part = gn_buf_for(v, Gv);
+      c.gn_G = Gv;
+      gn_ready[v.p] = {c.gn_part, v.C, Gv};
       return;
     }
-    gn_ready[v.p] = {c.gn_part, v.C};
+    c.gn_part = nullptr;
   };
   auto emit_gemm = [&](GemmArgs& g, const View& v) {
     gn_ready.erase(v.p);
     const int hw = v.H * v.W, cpg = v.C / G;
     if (gemm_pick(g) != 0 || hw % 64 != 0 || v.C % G != 0 || 32 % cpg != 0) return;
-    g.gn_part = gn_buf_for(v);
+    g.gn_part = gn_buf_for(v, G);
     g.gn_G = G;
     g.gn_hw = hw;
-    gn_ready[v.p] = {g.gn_part, v.C};
+    gn_ready[v.p] = {g.gn_part, v.C, G};
   };
   auto gn_stats = [&](const View& v) -> const double2* {
     auto it = gn_ready.find(v.p);
-    if (it != gn_ready.end() && it->second.second == v.C) return it->second.first;
+    if (it != gn_ready.end() && it->second.C == v.C && it->second.G == G) return it->second.p;
     add("gn_partial", 0, gn_bytes(v, false), [=](hipStream_t st) { return gn_partial(v, G, part, st); });
     return part;
   };
   // the concat input [h | skip] of an up-path ResBlock: when both slices' producers emitted their statistics
-  // and the concat's groups do not straddle the slices (512 = 256 + 256, 256 = 128 + 128: all but the
-  // 384-channel concats of the CIFAR UNet), combine the slices' partials instead of a gn_partial pass
+  // in groups that tile the concat's (gn_concat_ok), combine the slices' partials instead of a gn_partial pass
   auto gn_stats_concat = [&](const View& v, const View& sk) -> const double2* {
     const int Ch = v.C - sk.C;
     auto ih = gn_ready.find(v.p), is = gn_ready.find(sk.p);
-    const bool aligned = v.C % G == 0 && Ch > 0 && Ch % G == 0 && sk.C % G == 0 && (v.C / G) % (Ch / G) == 0 &&
-                         (v.C / G) % (sk.C / G) == 0 && Ch % (v.C / G) == 0;
-    if (aligned && !std::getenv("DM_GN_NO_CONCAT") && ih != gn_ready.end() && ih->second.second == Ch &&
-        is != gn_ready.end() && is->second.second == sk.C) {
-      const double2* ph = ih->second.first;
-      const double2* ps = is->second.first;
-      const int Cs = sk.C, HW = v.H * v.W;
+    if (!std::getenv("DM_GN_NO_CONCAT") && ih != gn_ready.end() && ih->second.C == Ch && is != gn_ready.end() &&
+        is->second.C == sk.C && gn_concat_ok(Ch, ih->second.G, sk.C, is->second.G, G)) {
+      const double2* ph = ih->second.p;
+      const double2* ps = is->second.p;
+      const int Cs = sk.C, HW = v.H * v.W, Gh = ih->second.G, Gs = is->second.G;
       add("gn_concat_stats", 0, 32.0 * B * gn_num_chunks(HW) * G, [=](hipStream_t st) {
-        return gn_concat_stats(ph, Ch, ps, Cs, B, HW, G, part, st);
+        return gn_concat_stats(ph, Ch, Gh, ps, Cs, Gs, B, HW, G, part, st);
       });
       return part;
     }
@@ -857,8 +872,15 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
     const float* w = P(first_w);
     const float* bb = P(first_b);
     const int cin = arch.in_channels;
+    // the first ResBlock's GroupNorm statistics (and the last up-path concat's skip slice: skip 0 is never
+    // rewritten) from the conv's epilogue
+    double2* gp = nullptr;
+    if (conv3x3_small_in_can_emit(H, W, C0, G) && !std::getenv("DM_GN_NO_FIRST")) {
+      gp = gn_buf_for(y, G);
+      gn_ready[y.p] = {gp, C0, G};
+    }
     add("conv3x3_small_in", 2.0 * B * H * W * C0 * 9 * cin, 4.0 * B * H * W * (cin + C0),
-        [=](hipStream_t st) { return conv3x3_small_in(P_->x, B, cin, H, W, w, bb, C0, y, st); });
+        [=](hipStream_t st) { return conv3x3_small_in(P_->x, B, cin, H, W, w, bb, C0, y, st, gp, G); });
   }
 
   for (size_t i = 0; i < nodes.size(); ++i) {

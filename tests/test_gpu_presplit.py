@@ -4,9 +4,10 @@ rewrite switched off by its environment toggle (read at plan build):
 * linear_k32 with the A operand pre-split once per GEMM (`linear_presplit_a`, `row_stats_split`, fc1's
   epilogue writing fc2's pre-split A) against the split inside the GEMM: the same fp32 expressions, so
   the outputs are bit-identical (DiT: DM_DIT_PRESPLIT=0; the UNet attention qkv: DM_QKV_NO_PRESPLIT);
-* GroupNorm partials of a concat combined from its slices' emitted partials (`gn_concat_stats`) against a
-  `gn_partial` pass over the concat (DM_GN_NO_CONCAT): the same sums in another fp64 order, so equal
-  to within a few fp32 ulps of the output.
+* GroupNorm partials emitted by producers instead of a `gn_partial` pass over the tensor: a concat's
+  combined from its slices' partials (`gn_concat_stats`; DM_GN_NO_CONCAT), the 4-channel units the h slice
+  of a 384 = 256 + 128 concat emits (DM_GN_NO_UNITS), the first conv's epilogue (DM_GN_NO_FIRST): the same
+  sums in another fp64 order, so equal to within a few fp32 ulps of the output.
 """
 import os
 
@@ -85,9 +86,10 @@ def test_unet_qkv_presplit_bit_identical(cuda, unet_case):
     assert torch.equal(on, off), (on - off).abs().max().item()
 
 
-def test_unet_concat_gn_stats(cuda, unet_case):
+@pytest.mark.parametrize('toggle', ['DM_GN_NO_CONCAT', 'DM_GN_NO_UNITS', 'DM_GN_NO_FIRST'])
+def test_unet_emitted_gn_stats(cuda, unet_case, toggle):
     sd, x, t = unet_case
-    on = _with_env('DM_GN_NO_CONCAT', None, lambda: _unet_out(cuda, sd, x, t))
-    off = _with_env('DM_GN_NO_CONCAT', '1', lambda: _unet_out(cuda, sd, x, t))
+    on = _with_env(toggle, None, lambda: _unet_out(cuda, sd, x, t))
+    off = _with_env(toggle, '1', lambda: _unet_out(cuda, sd, x, t))
     scale = off.abs().max().item()
     assert (on - off).abs().max().item() <= 1e-6 * scale
