@@ -122,13 +122,16 @@ __global__ void softmax_rows_kernel(float* __restrict__ x, long rows, int L, int
 
 // first conv: NCHW input with few channels -> NHWC (pitched) output.
 // One block per R output rows of one image (R = 64 / W for W < 64, so a block is one 64-pixel GroupNorm
-// chunk; else one row). Thread t owns output channel co = t % Cout (its 9*Cin weights, staged through LDS
-// with coalesced loads, in registers) and a run of pixels of the block; the R + 2 input rows sit in LDS and
-// are read as broadcasts (all lanes of a wave share the pixel). Stores are coalesced over co. With gn_part
-// the block also emits the consumer GroupNorm's per-chunk partials (sum, sum of squares in double) -- the
-// layout of gn_partial_kernel -- so the first ResBlock and the last up-path concat skip their gn_partial
-// passes.
+// chunk; else one row). The R + 2 input rows and the weights sit in LDS (coalesced loads). Thread t owns the
+// output channel pair 2 cp, 2 cp + 1 (cp = t % (Cout / 2); its 2 x 9 Cin weights in registers) and a run of
+// pixels of the block: per pixel 9 Cin packed FMAs (v_pk_fma_f32, both channels from one broadcast input
+// value) over a 3-column window whose column slots rotate (no register moves), then + bias; a float2 store
+// per lane, coalesced over the channel pairs. Per output: fma chain over (ci, ky, kx), acc from 0, + bias.
+// With gn_part the block also emits the consumer GroupNorm's per-chunk partials (sum, sum of squares in
+// double) -- the layout of gn_partial_kernel -- so the first ResBlock and the last up-path concat skip their
+// gn_partial passes.
 constexpr int kSiMaxChunks = 8, kSiMaxPar = 4, kSiMaxG = 32;
+typedef float fl2 __attribute__((ext_vector_type(2)));
 template <int CIN>
 __global__ void __launch_bounds__(256) conv3x3_small_in_kernel(const float* __restrict__ x, int H, int W, int R,
                                                                const float* __restrict__ w,
@@ -136,11 +139,12 @@ __global__ void __launch_bounds__(256) conv3x3_small_in_kernel(const float* __re
                                                                float* __restrict__ y, int y_pitch,
                                                                double2* __restrict__ gn_part, int G, int nchunk) {
   extern __shared__ __attribute__((aligned(16))) float smem_f[];
+  constexpr int KW = CIN * 9;
   const int Wp = W + 2;
   const int nrow = CIN * (R + 2) * Wp;
   float* rows = smem_f;                                       // [CIN][R + 2][W + 2]
   float* wl = smem_f + nrow;                                  // [Cout][CIN * 9]
-  double2* st = reinterpret_cast<double2*>(smem_f + ((nrow + Cout * CIN * 9 + 3) & ~3));  // [par][chunk][G]
+  double2* st = reinterpret_cast<double2*>(smem_f + ((nrow + Cout * KW + 3) & ~3));  // [par][chunk][G]
   const int b = blockIdx.y, oy0 = blockIdx.x * R;
   for (int i = threadIdx.x; i < nrow; i += blockDim.x) {
     const int ci = i / ((R + 2) * Wp);
@@ -151,10 +155,11 @@ __global__ void __launch_bounds__(256) conv3x3_small_in_kernel(const float* __re
     if (iy >= 0 && iy < H && xx >= 0 && xx < W) v = x[(((size_t)b * CIN + ci) * H + iy) * W + xx];
     rows[i] = v;
   }
-  for (int i = threadIdx.x; i < Cout * CIN * 9; i += blockDim.x) wl[i] = w[i];
-  const int lanes_per_px = min(Cout, (int)blockDim.x);
+  for (int i = threadIdx.x; i < Cout * KW; i += blockDim.x) wl[i] = w[i];
+  const int npair = Cout / 2;
+  const int lanes_per_px = min(npair, (int)blockDim.x);
   const int px_par = blockDim.x / lanes_per_px;
-  const int cpg = gn_part ? Cout / G : 1;
+  const int cpg = gn_part ? Cout / G : 2;  // channels per group; cpg / 2 lanes hold one group
   const int bchunks = (R * W) / kGnPixPerChunk;
   if (gn_part)
     for (int i = threadIdx.x; i < px_par * kSiMaxChunks * kSiMaxG; i += blockDim.x) st[i] = make_double2(0.0, 0.0);
@@ -175,16 +180,17 @@ __global__ void __launch_bounds__(256) conv3x3_small_in_kernel(const float* __re
     x0 = 0;
     x1 = W;
   }
-  for (int co = threadIdx.x % lanes_per_px; co < Cout; co += lanes_per_px) {
-    float wr[CIN * 9];
+  for (int cp = threadIdx.x % lanes_per_px; cp < npair; cp += lanes_per_px) {
+    const int co = 2 * cp;
+    fl2 wr[KW];
 #pragma unroll
-    for (int k = 0; k < CIN * 9; ++k) wr[k] = wl[co * CIN * 9 + k];
-    const float bc = bias[co];
+    for (int k = 0; k < KW; ++k) wr[k] = fl2{wl[co * KW + k], wl[(co + 1) * KW + k]};
+    const fl2 bc = {bias[co], bias[co + 1]};
     double gs = 0.0, gq = 0.0;
     int cur = -1;  // chunk the (gs, gq) sums belong to
-    auto flush = [&]() {  // over the group's cpg channel lanes, then one LDS slot per (px group, chunk, group)
+    auto flush = [&]() {  // over the group's cpg / 2 lanes, then one LDS slot per (px group, chunk, group)
       double s = gs, q = gq;
-      for (int o = 1; o < cpg; o <<= 1) {
+      for (int o = 1; o < cpg / 2; o <<= 1) {
         s += __shfl_xor(s, o);
         q += __shfl_xor(q, o);
       }
@@ -193,48 +199,52 @@ __global__ void __launch_bounds__(256) conv3x3_small_in_kernel(const float* __re
     };
     for (int r = r0; r < r1; ++r) {
       if (x0 >= x1) break;
-      // a contiguous run of pixels with a sliding 3x3 window in registers: one new LDS column (3 CIN
-      // broadcasts) per pixel instead of 9 CIN; same products in the same order
-      float win[CIN][3][3];
-#pragma unroll
-      for (int ci = 0; ci < CIN; ++ci)
-#pragma unroll
-        for (int ky = 0; ky < 3; ++ky) {
-          win[ci][ky][0] = rows[(ci * (R + 2) + r + ky) * Wp + x0];
-          win[ci][ky][1] = rows[(ci * (R + 2) + r + ky) * Wp + x0 + 1];
-        }
       const int oy = oy0 + r;
-      for (int ox = x0; ox < x1; ++ox) {
+      const float* rrow = rows + r * Wp;  // + (ci (R + 2) + ky) Wp + input column
+      float col[3][CIN][3];               // column slots of the window, [slot][ci][ky]
+      auto load_col = [&](int slot, int xx) {
 #pragma unroll
         for (int ci = 0; ci < CIN; ++ci)
 #pragma unroll
-          for (int ky = 0; ky < 3; ++ky) win[ci][ky][2] = rows[(ci * (R + 2) + r + ky) * Wp + ox + 2];
-        float acc = 0.f;
+          for (int ky = 0; ky < 3; ++ky) col[slot][ci][ky] = rrow[(ci * (R + 2) + ky) * Wp + xx];
+      };
+      // output pixel ox with the window's left column in slot u % 3 (u = phase, compile-time after unrolling)
+      auto pixel = [&](int ox, int u) {
+        load_col((u + 2) % 3, ox + 2);
+        fl2 acc = {0.f, 0.f};
 #pragma unroll
         for (int ci = 0; ci < CIN; ++ci)
 #pragma unroll
           for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-            for (int kx = 0; kx < 3; ++kx) acc += wr[(ci * 3 + ky) * 3 + kx] * win[ci][ky][kx];
-        const float v = acc + bc;
-        y[(((size_t)b * H + oy) * W + ox) * y_pitch + co] = v;
+            for (int kx = 0; kx < 3; ++kx) {
+              const float xv = col[(u + kx) % 3][ci][ky];
+              acc = __builtin_elementwise_fma(wr[(ci * 3 + ky) * 3 + kx], fl2{xv, xv}, acc);
+            }
+        const fl2 v = acc + bc;
+        *reinterpret_cast<fl2*>(y + (((size_t)b * H + oy) * W + ox) * y_pitch + co) = v;
         if (gn_part) {
           const int ch = ((oy - oy0) * W + ox) / kGnPixPerChunk;  // block-local chunk
           if (ch != cur) {
             if (cur >= 0) flush();
             cur = ch;
           }
-          gs += (double)v;
-          gq += (double)v * v;
+          gs += (double)v.x;
+          gs += (double)v.y;
+          gq += (double)v.x * v.x;
+          gq += (double)v.y * v.y;
         }
+      };
+      load_col(0, x0);
+      load_col(1, x0 + 1);
+      int ox = x0;
+      for (; ox + 3 <= x1; ox += 3) {
 #pragma unroll
-        for (int ci = 0; ci < CIN; ++ci)
-#pragma unroll
-          for (int ky = 0; ky < 3; ++ky) {
-            win[ci][ky][0] = win[ci][ky][1];
-            win[ci][ky][1] = win[ci][ky][2];
-          }
+        for (int u = 0; u < 3; ++u) pixel(ox + u, u);
       }
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        if (ox + u < x1) pixel(ox + u, u);
     }
     if (gn_part && cur >= 0) flush();
   }
@@ -262,7 +272,9 @@ constexpr int kSoTW = 32, kSoTH = 8, kSoPP = (kSoTH + 2) * (kSoTW + 2);
 // B = 256 batch run in one wave of blocks instead of 1.33), the next chunk's patch loaded into registers
 // while this chunk's 9 taps run (the previous form loaded, waited, then computed each 32-channel chunk), and
 // exactly CO = Cout accumulators (no padded output). Weights [9][Cin][CO] from wave-uniform scalar loads.
-// Summation per output over (16-channel chunk, tap, channel), fp32 FMAs.
+// Summation per output over (16-channel chunk, tap, channel), fp32 FMAs. The patch registers are double
+// buffered: chunk c + 2's loads are issued right after chunk c's patch is stored, so each load has two
+// chunks' taps to land (one chunk's 432 FMAs per thread did not cover the load latency).
 constexpr int kSo2C = 16, kSo2LD = 20, kSo2PJ = (kSoPP * (kSo2C / 4) + 255) / 256;
 template <int CO>
 __global__ void __launch_bounds__(256) conv3x3_small_out2_kernel(const float* __restrict__ x, int B, int H, int W,
@@ -289,12 +301,12 @@ __global__ void __launch_bounds__(256) conv3x3_small_out2_kernel(const float* __
     ok[j] = t + 256 * j < kSoPP * 4 && iy >= 0 && iy < H && ix >= 0 && ix < W;
     src[j] = x + (((size_t)b * H + min(max(iy, 0), H - 1)) * W + min(max(ix, 0), W - 1)) * pitch + 4 * c4;
   }
-  f4 rv[kSo2PJ];
-  auto load = [&](int c0) {
+  f4 rva[kSo2PJ], rvb[kSo2PJ];
+  auto load = [&](f4 (&rv)[kSo2PJ], int c0) {
 #pragma unroll
     for (int j = 0; j < kSo2PJ; ++j) rv[j] = *reinterpret_cast<const f4*>(src[j] + c0);
   };
-  auto store = [&](int c0) {
+  auto store = [&](const f4 (&rv)[kSo2PJ], int c0) {
 #pragma unroll
     for (int j = 0; j < kSo2PJ; ++j) {
       const int i = t + 256 * j;
@@ -316,11 +328,10 @@ __global__ void __launch_bounds__(256) conv3x3_small_out2_kernel(const float* __
   float acc[CO];
 #pragma unroll
   for (int c = 0; c < CO; ++c) acc[c] = 0.f;
-  load(0);
-  for (int c0 = 0; c0 < Cin; c0 += kSo2C) {
-    store(c0);
+  auto chunk = [&](f4 (&rv)[kSo2PJ], int c0) {
+    store(rv, c0);
     __syncthreads();
-    if (c0 + kSo2C < Cin) load(c0 + kSo2C);  // in flight during this chunk's taps
+    if (c0 + 2 * kSo2C < Cin) load(rv, c0 + 2 * kSo2C);  // in flight during this and the next chunk's taps
 #pragma unroll 3
     for (int tap = 0; tap < 9; ++tap) {
       const float* pr = patch + ((py + tap / 3) * (kSoTW + 2) + px + tap % 3) * kSo2LD;
@@ -336,6 +347,12 @@ __global__ void __launch_bounds__(256) conv3x3_small_out2_kernel(const float* __
       }
     }
     __syncthreads();  // every thread is done with the patch before the next chunk overwrites it
+  };
+  load(rva, 0);
+  if (kSo2C < Cin) load(rvb, kSo2C);
+  for (int c0 = 0; c0 < Cin; c0 += 2 * kSo2C) {
+    chunk(rva, c0);
+    if (c0 + kSo2C < Cin) chunk(rvb, c0 + kSo2C);
   }
   const int oy = ty0 + py, ox = tx0 + px;
   if (oy < H && ox < W) {
@@ -613,15 +630,17 @@ static int small_in_rows(int H, int W) { return (W < kGnPixPerChunk && kGnPixPer
 
 bool conv3x3_small_in_can_emit(int H, int W, int Cout, int G) {
   const int R = small_in_rows(H, W);
-  const int lpp = min(Cout, 256);
-  return G > 0 && G <= kSiMaxG && Cout % G == 0 && (Cout / G) <= 64 && ((Cout / G) & (Cout / G - 1)) == 0 &&
-         Cout >= 64 && 256 % lpp == 0 && Cout % lpp == 0 && (R * W) % kGnPixPerChunk == 0 &&
+  const int lpp = min(Cout / 2, 256);  // lanes per pixel (channel pairs); a wave's lanes share one pixel run
+  const int cpg = G > 0 ? Cout / G : 0;
+  return G > 0 && G <= kSiMaxG && Cout % G == 0 && cpg % 2 == 0 && cpg <= 64 && (cpg & (cpg - 1)) == 0 &&
+         lpp >= 64 && 256 % lpp == 0 && (Cout / 2) % lpp == 0 && (R * W) % kGnPixPerChunk == 0 &&
          (R * W) / kGnPixPerChunk <= kSiMaxChunks && 256 / lpp <= kSiMaxPar;
 }
 
 int conv3x3_small_in(const float* x, int B, int Cin, int H, int W, const float* w, const float* bias,
                      int Cout, const View& y, hipStream_t st, double2* gn_part, int G) {
   DM_REQUIRE(Cin >= 1 && Cin <= 4, "first conv: Cin out of range (1..4)");
+  DM_REQUIRE(Cout % 2 == 0 && y.pitch % 2 == 0, "first conv: Cout and the output pitch must be even");
   DM_REQUIRE(y.C == Cout && y.H == H && y.W == W && y.B == B, "first conv: output view mismatch");
   DM_REQUIRE(!gn_part || conv3x3_small_in_can_emit(H, W, Cout, G), "first conv: GroupNorm statistics shape");
   const int R = small_in_rows(H, W);

@@ -24,10 +24,10 @@ def main():
     ap.add_argument('--tile', type=int, default=10)
     args = ap.parse_args()
     dmhip.load()
-    conv_bench.run(args.shape, 5, 'fp16x2', args.tile)
+    conv_bench.run(args.shape, 5, 'fp16x2', args.tile, 2 if args.tile == 15 else 0)
     B, Cin, Cout, H, pro, up = conv_bench.SHAPES[args.shape]
-    bn = 128 if args.tile == 10 else 64
-    nblk = (B * H * H // 128) * ((Cout + bn - 1) // bn)
+    bm, bn = (64, 64) if args.tile == 15 else (128, 128 if args.tile == 10 else 64)
+    nblk = (B * H * H // bm) * ((Cout + bn - 1) // bn)
     buf = np.zeros((nblk, 8), dtype=np.uint64)
     L = dmhip.load()
     L.dm_debug_k32_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
