@@ -124,9 +124,12 @@ __global__ void softmax_rows_kernel(float* __restrict__ x, long rows, int L, int
 // One block per R output rows of one image (R = 64 / W for W < 64, so a block is one 64-pixel GroupNorm
 // chunk; else one row). The R + 2 input rows and the weights sit in LDS (coalesced loads). Thread t owns the
 // output channel pair 2 cp, 2 cp + 1 (cp = t % (Cout / 2); its 2 x 9 Cin weights in registers) and a run of
-// pixels of the block: per pixel 9 Cin packed FMAs (v_pk_fma_f32, both channels from one broadcast input
-// value) over a 3-column window whose column slots rotate (no register moves), then + bias; a float2 store
-// per lane, coalesced over the channel pairs. Per output: fma chain over (ci, ky, kx), acc from 0, + bias.
+// pixels of the block: per pixel 9 Cin packed multiply + packed add pairs (v_pk_mul_f32 / v_pk_add_f32, both
+// channels from one broadcast input value) over a 3-column window whose column slots rotate (no register
+// moves), then + bias; a float2 store per lane, coalesced over the channel pairs. Per output: acc from 0,
+// acc + w x over (ci, ky, kx) with separately rounded products -- the reference CPU conv's arithmetic for
+// this layer (a fused-multiply-add chain measured 2.6x further from the float64 trajectory on the ADM CFG
+// test, whose free-running steps amplify a first-layer ulp ~10^3-fold).
 // With gn_part the block also emits the consumer GroupNorm's per-chunk partials (sum, sum of squares in
 // double) -- the layout of gn_partial_kernel -- so the first ResBlock and the last up-path concat skip their
 // gn_partial passes.
@@ -219,7 +222,7 @@ __global__ void __launch_bounds__(256) conv3x3_small_in_kernel(const float* __re
 #pragma unroll
             for (int kx = 0; kx < 3; ++kx) {
               const float xv = col[(u + kx) % 3][ci][ky];
-              acc = __builtin_elementwise_fma(wr[(ci * 3 + ky) * 3 + kx], fl2{xv, xv}, acc);
+              acc = acc + wr[(ci * 3 + ky) * 3 + kx] * fl2{xv, xv};  // separately rounded (no contraction)
             }
         const fl2 v = acc + bc;
         *reinterpret_cast<fl2*>(y + (((size_t)b * H + oy) * W + ox) * y_pitch + co) = v;
