@@ -46,6 +46,7 @@ constexpr int kRowH = 80;       // LDS row pitch in fp16: 160 B; [piece][k-group
 constexpr int kMaxP = 208;      // patch pixels: 32^2 maps 6 x 34, 16^2 maps 10 x 18, 8^2 maps 2 x 10 x 10
 constexpr int kMaxPW = 392;     // 512-thread wide-map tiles: 3 x 130 (128-pixel row segments), 4 x 66 (64^2 maps)
 constexpr int kTab = 2048;      // GroupNorm table floats (per image of the tile: its channels' scales, then the shifts)
+constexpr int kTabBig = 8192;   // variant 8: up to 2048 input channels of two images (one block per CU)
 constexpr int kStats = 128;     // (image, group) pairs of the in-kernel finalize
 
 
@@ -75,7 +76,8 @@ __device__ unsigned long long g_k32_stamps[65536][8];
 // NT threads per block (256, or 512 for the 128-pixel row-segment tiles of the wide maps: 8 waves of 64 x 32
 // in one block per CU, each weight fragment loaded by two waves instead of by four 64 x 128 blocks' waves),
 // MAXP patch pixels per buffer.
-template <int BM, int BN, int WM, int WN, bool PRO, bool KSPLIT, bool SUB = false, int NT = 256, int MAXP = kMaxP>
+template <int BM, int BN, int WM, int WN, bool PRO, bool KSPLIT, bool SUB = false, int NT = 256, int MAXP = kMaxP,
+          int TABF = kTab>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) conv_k32_kernel(ConvArgs a, PatchGeom g) {
   constexpr int NWN = BN / WN;
   static_assert((BM / WM) * NWN == NT / 64, "one wave per 64 threads");
@@ -86,7 +88,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
   constexpr int PATCH = MAXP * kRowH;
   constexpr int NTAP = SUB ? 4 : 9, WD = 2, CPI = 2;  // B ring depth; chunks per loop iteration (slot = compile-time)
   __shared__ __attribute__((aligned(16))) _Float16 patch[2 * PATCH];
-  __shared__ __attribute__((aligned(16))) float gtab[PRO ? kTab : 4];
+  __shared__ __attribute__((aligned(16))) float gtab[PRO ? TABF : 4];
   __shared__ float gstat[PRO ? 2 * kStats : 2];
 
   const int Ho = SUB ? a.Hin : a.Hout, Wo = SUB ? a.Win : a.Wout;  // the tiled (GEMM-row) resolution
@@ -306,7 +308,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
       // The per-channel affine (and AdaGN modulation) of this thread's table entries is loaded first, with
       // the statistics partials, so the prologue waits for one round trip, not two.
       const int G = a.gin_G, cpg = a.Cin1 / G;
-      constexpr int TU = kTab / 2 / NT;  // table entries per thread
+      constexpr int TU = TABF / 2 / NT;  // table entries per thread
       float gam[TU], bet[TU], fms[TU], fmb[TU];
 #pragma unroll
       for (int u = 0; u < TU; ++u) {
@@ -877,7 +879,9 @@ extern "C" int dm_debug_k32_stamps(void* host, int nblocks) {
 
 // Variants: 1 = 128 x 128 tiles, 2 = 128 x 64 (whole K), 3 = 64 x 64 and 4 = 64 x 128 split-K tiles,
 // 5 = 64 x 128 tiles of one image row or 64-pixel row segment (ADM's 64^2 .. 256^2 maps), 6 = the small-map
-// kernel (64 x 64 tiles of four 4 x 4 images, K split in two inside the block; the plan's ksplit = 2).
+// kernel (64 x 64 tiles of four 4 x 4 images, K split in two inside the block; the plan's ksplit = 2),
+// 7 = 512-thread 128 x 128 tiles of 64 x 32 wave tiles (wide maps), 8 = variant 1 / its sub-pixel form with a
+// 32 KB GroupNorm table (inputs of up to 2048 channels at two images per tile; one block per CU).
 static bool conv_k32s_ok(const ConvArgs& a) {
   if (!(a.ws && a.ws_np == 2 && a.ws_rowscale && a.taps == 9 && a.stride == 1 && a.upsample == 0)) return false;
   if (a.ksplit != 2 || a.Hout * a.Wout != 16 || a.Hin != a.Hout || a.Win != a.Wout) return false;
@@ -916,7 +920,7 @@ int conv_k32_variant_ok(const ConvArgs& a, int v) {
   if (!(a.ws && a.ws_np == 2 && a.ws_rowscale && a.taps == 9 && a.stride == 1 && (a.upsample == 0 || sub))) return 0;
   if (a.Cin1 < kC || a.Cin1 % kC != 0 || a.Cin2 % kC != 0) return 0;
   if (sub ? (a.Cin2 != 0 || a.K != 4 * a.Cin1) : a.K != 9 * a.Cin1 + a.Cin2) return 0;
-  const bool split = v == 3 || v == 4, seg = v == 5;
+  const bool split = v == 3 || v == 4, seg = v == 5, big = v == 8;
   if (split && sub) return 0;
   const int bm = (split || seg) ? 64 : BM_K32;
   if (split ? !(a.ksplit > 1 && a.kpart && a.ksplit <= a.Cin1 / kC) : a.ksplit > 1) return 0;
@@ -925,7 +929,7 @@ int conv_k32_variant_ok(const ConvArgs& a, int v) {
   PatchGeom g;
   if (!conv_patch_geom(a, bm, g) || g.P > kMaxP || g.TB > (split ? 4 : 2) || (seg && g.TB != 1)) return 0;
   const int nch = a.Cin1 / kC, tab_c = split ? ceil_div(nch, a.ksplit) * kC : a.Cin1;
-  if (a.pro_scale && 2 * g.TB * tab_c > kTab) return 0;
+  if (a.pro_scale && 2 * g.TB * tab_c > (big ? kTabBig : kTab)) return 0;
   if (a.gin_part && g.TB * a.gin_G > kStats) return 0;
   if (split) {  // raw partial sums with 16-byte stores
     if (a.Cout % 4 != 0 || (reinterpret_cast<uintptr_t>(a.kpart) & 15) != 0) return 0;
@@ -954,6 +958,13 @@ static bool conv_k32_wide_enabled() {
   return !(e && e[0] == '0');
 }
 
+// The big-table 128 x 128 tiles (variant 8) for convs whose GroupNorm tables exceed kTab (ADM's 8^2 / 16^2 levels:
+// 1024-2048 input channels) unless DM_CONV_K32B=0 (then conv_patch3)
+static bool conv_k32_bigtab_enabled() {
+  const char* e = std::getenv("DM_CONV_K32B");
+  return !(e && e[0] == '0');
+}
+
 // The small-map kernel (variant 6) unless DM_CONV_K32S=0 (the two-launch split-K path, kept as its test oracle;
 // read per call: plans capture their launches once, so this costs nothing per forward)
 static bool conv_k32_small_enabled() {
@@ -962,7 +973,7 @@ static bool conv_k32_small_enabled() {
 }
 
 int conv_k32_pick(const ConvArgs& a) {
-  if (a.tile >= 10 && a.tile <= 16) return conv_k32_variant_ok(a, a.tile - 9) ? a.tile - 9 : 0;
+  if (a.tile >= 10 && a.tile <= 17) return conv_k32_variant_ok(a, a.tile - 9) ? a.tile - 9 : 0;
   if (a.tile != 0 || !conv_k32_enabled()) return 0;
   // split-K convs of maps of <= 16 pixels: 64 x 128 tiles (4x4 maps at B = 256, K split 2: 32.5 us vs
   // 34.2 us for 64 x 64 and for conv_patch3's 64 x 64 split tiles)
@@ -975,7 +986,10 @@ int conv_k32_pick(const ConvArgs& a) {
     // two-row tiles of 8 waves, else 64-pixel rows / segments
     const int wt = a.upsample == 2 ? a.Win : a.Wout;
     if (wt >= 64 && conv_k32_wide_enabled() && conv_k32_variant_ok(a, 7)) return 7;
-    return (wt >= 64 && conv_k32_variant_ok(a, 5)) ? 5 : 0;
+    if (wt >= 64) return conv_k32_variant_ok(a, 5) ? 5 : 0;
+    // 128-row tiles whose GroupNorm tables do not fit kTab: the big-table instantiation (one block per CU)
+    const int p = conv_pick(a);
+    return ((p == 3 || p == 4) && conv_k32_bigtab_enabled() && conv_k32_variant_ok(a, 8)) ? 8 : 0;
   }
   const int p = conv_pick(a);
   if (p != 3 && p != 4) return 0;
@@ -991,6 +1005,9 @@ std::string conv_k32_label(const ConvArgs& a, int v) {
   if (v == 7)
     return std::string("conv_k32_kernel<128,128,64,32,") + (a.pro_scale ? "true," : "false,") + "false," +
            (a.upsample == 2 ? "true,512>" : "false,512>");
+  if (v == 8)
+    return std::string("conv_k32_kernel<128,128,64,64,") + (a.pro_scale ? "true," : "false,") + "false," +
+           (a.upsample == 2 ? "true,256,208,8192>" : "false,256,208,8192>");
   static const char* names[] = {"", "conv_k32_kernel<128,128,64,64,", "conv_k32_kernel<128,64,64,32,",
                                 "conv_k32_kernel<64,64,32,32,", "conv_k32_kernel<64,128,32,64,",
                                 "conv_k32_kernel<64,128,32,64,"};
@@ -998,7 +1015,7 @@ std::string conv_k32_label(const ConvArgs& a, int v) {
          (a.upsample == 2 ? "true>" : "false>");
 }
 
-template <int BM, int BN, int WM, int WN, bool KSPLIT, int NT = 256, int MAXP = kMaxP>
+template <int BM, int BN, int WM, int WN, bool KSPLIT, int NT = 256, int MAXP = kMaxP, int TABF = kTab>
 static void launch_k32(const ConvArgs& a, const PatchGeom& g, hipStream_t st) {
   const bool sub = a.upsample == 2;
   const int M = sub ? a.B * a.Hin * a.Win : a.B * a.Hout * a.Wout;
@@ -1006,24 +1023,24 @@ static void launch_k32(const ConvArgs& a, const PatchGeom& g, hipStream_t st) {
   if constexpr (!KSPLIT) {
     if (sub) {
       if (a.pro_scale)
-        hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, true, false, true, NT, MAXP>), dim3(blocks), dim3(NT), 0, st,
-                           a, g);
+        hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, true, false, true, NT, MAXP, TABF>), dim3(blocks), dim3(NT),
+                           0, st, a, g);
       else
-        hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, false, false, true, NT, MAXP>), dim3(blocks), dim3(NT), 0,
-                           st, a, g);
+        hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, false, false, true, NT, MAXP, TABF>), dim3(blocks),
+                           dim3(NT), 0, st, a, g);
       return;
     }
   }
   if (a.pro_scale)
-    hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, true, KSPLIT, false, NT, MAXP>), dim3(blocks), dim3(NT), 0, st,
-                       a, g);
+    hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, true, KSPLIT, false, NT, MAXP, TABF>), dim3(blocks), dim3(NT), 0,
+                       st, a, g);
   else
-    hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, false, KSPLIT, false, NT, MAXP>), dim3(blocks), dim3(NT), 0, st,
-                       a, g);
+    hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, false, KSPLIT, false, NT, MAXP, TABF>), dim3(blocks), dim3(NT),
+                       0, st, a, g);
 }
 
 int conv2d_k32(const ConvArgs& a, int v, hipStream_t st) {
-  DM_REQUIRE(v >= 1 && v <= 7 && conv_k32_variant_ok(a, v), "conv: shape not supported by the K = 32 split kernel");
+  DM_REQUIRE(v >= 1 && v <= 8 && conv_k32_variant_ok(a, v), "conv: shape not supported by the K = 32 split kernel");
   PatchGeom g;
   if (v == 6) {
     conv_patch_geom(a, 64, g);
@@ -1035,8 +1052,9 @@ int conv2d_k32(const ConvArgs& a, int v, hipStream_t st) {
     DM_LAUNCH_CHECK();
     return DM_OK;
   }
-  conv_patch_geom(a, v >= 3 && v != 7 ? 64 : BM_K32, g);
+  conv_patch_geom(a, v >= 3 && v <= 6 ? 64 : BM_K32, g);
   switch (v) {
+    case 8: launch_k32<128, 128, 64, 64, false, 256, kMaxP, kTabBig>(a, g, st); break;
     case 7: launch_k32<128, 128, 64, 32, false, 512, kMaxPW>(a, g, st); break;
     case 1: launch_k32<128, 128, 64, 64, false>(a, g, st); break;
     case 2: launch_k32<128, 64, 64, 32, false>(a, g, st); break;

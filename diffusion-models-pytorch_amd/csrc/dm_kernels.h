@@ -329,7 +329,7 @@ int attn_flash(const AttnArgs& a, hipStream_t st);
 int conv3x3_small_in(const float* x, int B, int Cin, int H, int W, const float* w, const float* bias,
                      int Cout, const View& y, hipStream_t st, double2* gn_part = nullptr, int G = 0);
 bool conv3x3_small_in_can_emit(int H, int W, int Cout, int G);
-// last conv weights torch [Cout][Cin][3][3] -> [9][Cin][CO], CO = 4 (Cout <= 4) or 8; wp holds 9 * Cin * CO floats
+// last conv weights torch [Cout][Cin][3][3] -> [9][Cin][CO], CO = Cout rounded up to even (<= 8; zero-padded)
 int small_out_pack(const float* w, int Cout, int Cin, float* wp, hipStream_t st);
 int conv3x3_small_out(const View& x, const float* wp, const float* bias, int Cout, float* y, hipStream_t st,
                       const float* pro_scale = nullptr, const float* pro_shift = nullptr);

@@ -274,8 +274,10 @@ constexpr int kSoTW = 32, kSoTH = 8, kSoPP = (kSoTH + 2) * (kSoTW + 2);
 // 16-channel chunks (a 10 x 34 x 16 patch in 27 KB of LDS: five blocks per CU, so the B * 4 tiles of a
 // B = 256 batch run in one wave of blocks instead of 1.33), the next chunk's patch loaded into registers
 // while this chunk's 9 taps run (the previous form loaded, waited, then computed each 32-channel chunk), and
-// exactly CO = Cout accumulators (no padded output). Weights [9][Cin][CO] from wave-uniform scalar loads.
-// Summation per output over (16-channel chunk, tap, channel), fp32 FMAs. The patch registers are double
+// output channels in pairs on packed FMAs (v_pk_fma_f32: one broadcast input value times a channel pair's
+// weights; COP = Cout rounded up to even accumulators). Weights [9][Cin][COP] (zero-padded), wave-uniform
+// 8-B pair loads. Summation per output over (16-channel chunk, tap, channel), one fused chain per channel as
+// before (a packed FMA rounds each lane as v_fma_f32 does). The patch registers are double
 // buffered: chunk c + 2's loads are issued right after chunk c's patch is stored, so each load has two
 // chunks' taps to land (one chunk's 432 FMAs per thread did not cover the load latency).
 constexpr int kSo2C = 16, kSo2LD = 20, kSo2PJ = (kSoPP * (kSo2C / 4) + 255) / 256;
@@ -328,9 +330,10 @@ __global__ void __launch_bounds__(256) conv3x3_small_out2_kernel(const float* __
       *reinterpret_cast<f4*>(patch + p * kSo2LD + 4 * c4) = v;
     }
   };
-  float acc[CO];
+  constexpr int COP = (CO + 1) & ~1;
+  fl2 acc[COP / 2];
 #pragma unroll
-  for (int c = 0; c < CO; ++c) acc[c] = 0.f;
+  for (int c = 0; c < COP / 2; ++c) acc[c] = fl2{0.f, 0.f};
   auto chunk = [&](f4 (&rv)[kSo2PJ], int c0) {
     store(rv, c0);
     __syncthreads();
@@ -338,7 +341,7 @@ __global__ void __launch_bounds__(256) conv3x3_small_out2_kernel(const float* __
 #pragma unroll 3
     for (int tap = 0; tap < 9; ++tap) {
       const float* pr = patch + ((py + tap / 3) * (kSoTW + 2) + px + tap % 3) * kSo2LD;
-      const float* wt = wp + ((size_t)tap * Cin + c0) * CO;  // wave-uniform
+      const float* wt = wp + ((size_t)tap * Cin + c0) * COP;  // wave-uniform
 #pragma unroll
       for (int c4 = 0; c4 < kSo2C / 4; ++c4) {
         const f4 v = *reinterpret_cast<const f4*>(pr + 4 * c4);
@@ -346,7 +349,9 @@ __global__ void __launch_bounds__(256) conv3x3_small_out2_kernel(const float* __
 #pragma unroll
         for (int q = 0; q < 4; ++q)
 #pragma unroll
-          for (int co = 0; co < CO; ++co) acc[co] = fmaf(vv[q], wt[(4 * c4 + q) * CO + co], acc[co]);
+          for (int cp = 0; cp < COP / 2; ++cp)
+            acc[cp] = __builtin_elementwise_fma(fl2{vv[q], vv[q]},
+                                                *reinterpret_cast<const fl2*>(wt + (4 * c4 + q) * COP + 2 * cp), acc[cp]);
       }
     }
     __syncthreads();  // every thread is done with the patch before the next chunk overwrites it
@@ -360,7 +365,7 @@ __global__ void __launch_bounds__(256) conv3x3_small_out2_kernel(const float* __
   const int oy = ty0 + py, ox = tx0 + px;
   if (oy < H && ox < W) {
 #pragma unroll
-    for (int c = 0; c < CO; ++c) y[(((size_t)b * CO + c) * H + oy) * W + ox] = acc[c] + bias[c];
+    for (int c = 0; c < CO; ++c) y[(((size_t)b * CO + c) * H + oy) * W + ox] = acc[c / 2][c % 2] + bias[c];
   }
 }
 
@@ -668,7 +673,7 @@ int conv3x3_small_in(const float* x, int B, int Cin, int H, int W, const float* 
 
 int small_out_pack(const float* w, int Cout, int Cin, float* wp, hipStream_t st) {
   DM_REQUIRE(Cout >= 1 && Cout <= 8 && Cin > 0, "last conv: Cout out of range");
-  const int CO = Cout;  // conv3x3_small_out2_kernel<Cout>: exactly Cout accumulators
+  const int CO = (Cout + 1) & ~1;  // conv3x3_small_out2_kernel<Cout>: channel pairs, zero-padded to even
   hipLaunchKernelGGL(small_out_pack_kernel, dim3((9 * Cin * CO + 255) / 256), dim3(256), 0, st, w, Cout, Cin, CO, wp);
   DM_LAUNCH_CHECK();
   return DM_OK;
@@ -678,7 +683,7 @@ int conv3x3_small_out(const View& x, const float* wp, const float* bias, int Cou
                       const float* pro_scale, const float* pro_shift) {
   DM_REQUIRE(Cout >= 1 && Cout <= 8, "last conv: Cout out of range");
   DM_REQUIRE(x.C % 32 == 0 && x.pitch % 4 == 0, "last conv: Cin must be a multiple of 32");
-  // wp: small_out_pack's [9][Cin][Cout]
+  // wp: small_out_pack's [9][Cin][Cout rounded up to even]
   DM_REQUIRE((reinterpret_cast<uintptr_t>(x.p) & 15) == 0, "last conv: input must be 16-byte aligned");
   const long tiles = (long)x.B * ceil_div(x.H, kSoTH) * ceil_div(x.W, kSoTW);
 #define DM_SO2(CO)                                                                                            \

@@ -275,3 +275,30 @@ def test_k32_small_fp32_accuracy(cuda, B, Cin, Cout):
     scale = ref.abs().max().item()
     assert errs['k32s'] < 2.0 * errs['fp32'] + 1e-7 * scale, errs
     assert errs['k32s'] < 4e-6 * scale, (errs, scale)
+
+
+# ---- big-table 128 x 128 tiles (tile 17; automatic where the GroupNorm tables of two images exceed the
+# 8 KB table: ADM's 8^2 / 16^2 levels with 1024-2048 input channels, formerly on conv_patch3)
+@pytest.mark.parametrize('B,Cin,Cout,H,up', [(4, 256, 128, 8, 0), (3, 128, 64, 16, 0), (2, 128, 64, 8, 2)])
+def test_k32_bigtab_equals_v1(cuda, B, Cin, Cout, H, up):
+    """Same kernel, larger LDS table: bit-identical to the 128 x 128 tiles where those fit."""
+    xd, wp, b, pro, ref = _rand_case(cuda, B, Cin, Cout, H, up, seed=97)
+    Ho = ref.shape[-1]
+    y17 = _run_conv(cuda, xd, wp, Cout, Ho, Ho, 9, 1, up, b.to(cuda), pro=pro, split='fp16x2', tile=17)
+    y10 = _run_conv(cuda, xd, wp, Cout, Ho, Ho, 9, 1, up, b.to(cuda), pro=pro, split='fp16x2', tile=10)
+    assert torch.equal(y17.cpu(), y10.cpu())
+
+
+@pytest.mark.parametrize('B,Cin,Cout,H,up', [(4, 1024, 128, 8, 0), (2, 2048, 128, 8, 0), (2, 1536, 256, 16, 0),
+                                             (2, 1024, 128, 8, 2)])
+def test_k32_bigtab_fp32_accuracy(cuda, B, Cin, Cout, H, up):
+    """fused GroupNorm + SiLU with up to 2048 input channels, random data: within 2x of the fp32 MFMA kernel's
+    error vs fp64 (the plans pick tile 17 for these shapes at their nominal batch)."""
+    xd, wp, b, pro, ref = _rand_case(cuda, B, Cin, Cout, H, up, seed=98)
+    Ho = ref.shape[-1]
+    errs = {}
+    for name, split, tile in (('fp32', False, 0), ('big', 'fp16x2', 17)):
+        y = _run_conv(cuda, xd, wp, Cout, Ho, Ho, 9, 1, up, b.to(cuda), pro=pro, split=split, tile=tile)
+        errs[name] = (y.cpu().double() - _nhwc(ref)).abs().max().item()
+    scale = ref.abs().max().item()
+    assert errs['big'] < 2.0 * errs['fp32'] + 1e-7 * scale, errs

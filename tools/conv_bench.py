@@ -25,6 +25,9 @@ SHAPES = {
     'res16_256': (256, 256, 256, 16, True, 0),
     'res8_256': (256, 256, 256, 8, True, 0),
     'res8_512': (256, 512, 256, 8, True, 0),       # up-path conv1 at 8x8 with concat input
+    'adm8_1024': (64, 1024, 1024, 8, True, 0),    # ADM-256 8x8 level ResBlock conv (C4, B = 64)
+    'adm8_2048': (64, 2048, 1024, 8, True, 0),    # ADM-256 8x8 up-path conv1 with concat input
+    'adm16_2048': (64, 2048, 1024, 16, True, 0),  # ADM-256 16x16 up-path conv1 with concat input
     'res4_256': (256, 256, 256, 4, True, 0),
     'res4_512': (256, 512, 256, 4, True, 0),      # up-path conv1 at 4x4 with concat input
     'up16_256': (256, 256, 256, 16, False, 2),     # sub-pixel upsample 16 -> 32
