@@ -340,7 +340,7 @@ bool conv_can_emit_gn(const ConvArgs& a) {
            a.Cout <= 1024;
   const int pick = conv_pick(a);
   if (pick != 3 && pick != 4 && pick != 6 && pick != 7 && pick != 8) return false;  // waves own whole 64-row chunks
-  if (conv_k32_pick(a) && a.Cout % a.gn_G == 0 && a.Cout / a.gn_G > 16) return false;  // K32: groups within 16 columns
+  if (conv_k32_pick(a) && a.Cout % a.gn_G == 0 && a.Cout / a.gn_G > 32) return false;  // K32: groups within 32 columns
   // the K32 sub-pixel upsample (128-row tiles, 64-row waves of one parity): chunks of 64 low-res pixels
   if (a.upsample == 2) {
     const int v = conv_k32_pick(a);

@@ -54,11 +54,13 @@ __device__ __forceinline__ void conv_store_attn_planes(const ConvArgs& a, int m,
 // vector and residual with 16-B loads and stores 16 B -- instead of one 4-B store per accumulator
 // register (store-issue bound: 27k -> 8.5k cycles per K32 block). GroupNorm statistics of the stored
 // values per 64-row chunk: per channel over the lane's rows, then across the wave's row lanes, then
-// across the group's 4-channel quads (cpg = Cout / gn_G in {4, 8, 16}).
+// across the group's 4-channel quads (cpg = Cout / gn_G in {4, 8, 16, 32}: at most 8 quad lanes, within the
+// LPR >= 8 lanes of a row for every wave width WN >= 32).
 template <int WN>
 struct StagedEpilogue {
   static constexpr int EP = WN + 4;     // slab pitch (floats)
   static constexpr int LPR = WN / 4;    // lanes per row
+  static_assert(WN >= 32, "GroupNorm groups of up to 32 channels need >= 8 quad lanes per row");
   static constexpr int RPI = 64 / LPR;  // rows per wave instruction
   const ConvArgs& a;
   int M, HWo, b0, c4, rsub, ncol, nc;
@@ -179,13 +181,13 @@ struct StagedEpilogue {
   }
 };
 
-// whether StagedEpilogue takes this conv's output (16-B columns, GroupNorm groups of 4, 8 or 16 channels)
+// whether StagedEpilogue takes this conv's output (16-B columns, GroupNorm groups of 4, 8, 16 or 32 channels)
 inline bool staged_epilogue_ok(const ConvArgs& a) {
   auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   if (a.Cout % 4 != 0 || a.y_pitch % 4 != 0 || !al16(a.y) || (a.bias && !al16(a.bias)) ||
       (a.res && (a.res_pitch % 4 != 0 || !al16(a.res))) || (a.rowvec && (a.rowvec_pitch % 4 != 0 || !al16(a.rowvec))))
     return false;
-  if (a.gn_part && (a.gn_G <= 0 || a.Cout % a.gn_G != 0 || a.Cout / a.gn_G > 16 || (a.Cout / a.gn_G) % 4 != 0 ||
+  if (a.gn_part && (a.gn_G <= 0 || a.Cout % a.gn_G != 0 || a.Cout / a.gn_G > 32 || (a.Cout / a.gn_G) % 4 != 0 ||
                     (a.Hout * a.Wout) % 64 != 0))
     return false;
   return true;
