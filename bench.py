@@ -56,7 +56,7 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=3, help='timed folds')
     ap.add_argument('--warmup', type=int, default=1, help='untimed folds')
-    ap.add_argument('--workload', default='c3', choices=sorted(WORKLOADS),
+    ap.add_argument('--workload', default='c3', choices=sorted(WORKLOADS) + ['stub'],
                     help='; '.join(f'{k}: {v}' for k, v in sorted(WORKLOADS.items())))
     ap.add_argument('--batch', type=int, default=None, help='images per GPU per fold (default: the workload\'s)')
     ap.add_argument('--respace-steps', type=int, default=None, help='denoising steps (default: the workload\'s)')
@@ -337,28 +337,96 @@ def build_workload(name, args, dev, rank):
     raise ValueError(f'unknown workload {name}')
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` without a launcher: start N fresh child processes of this script, one per GPU, with
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set (the process-per-GPU layout of accelerate's launch that the
+    reference's harness runs under, scripts/sample_uncond.py:119,131,190), wait for all of them and forward
+    rank 0's JSON line. Runs before this process makes any HIP call (torch.cuda.device_count() does not
+    initialise the GPU), and never execs: the children are new processes. Returns the exit code."""
+    import subprocess
+    backend = os.environ.get('DM_DIST_BACKEND', 'nccl')
+    if backend == 'nccl' and torch.cuda.device_count() < n:
+        print(f'bench.py: --gpus {n} but only {torch.cuda.device_count()} GPU(s) visible', file=sys.stderr)
+        return 2
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR='127.0.0.1', MASTER_PORT=port)
+        env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')   # RCCL over dmabuf IPC on this pool
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else None, text=True))
+    out0 = procs[0].communicate()[0]
+    codes = [procs[0].returncode] + [p.wait() for p in procs[1:]]
+    if out0:
+        sys.stdout.write(out0)
+        sys.stdout.flush()
+    bad = [(r, c) for r, c in enumerate(codes) if c != 0]
+    if bad:
+        print(f'bench.py: rank(s) failed: {bad}', file=sys.stderr)
+        return 1
+    return 0
+
+
+def build_stub(args, dev, rank):
+    """Harness-only workload (`--workload stub`, CPU, no HIP library): exercises the launch, barrier,
+    max-over-ranks timing and gather of the bench without a GPU (tests/test_distributed.py)."""
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(2022 + rank)
+    B = args.batch or 4
+    shape = (B, 3, 8, 8)
+
+    def fold():
+        return torch.randn(shape, generator=gen, device=dev).clamp(-1, 1)
+    return dict(metric='harness stub', fold=fold, images=B, shape=shape, handles=[], sd_cpu=None,
+                workload='stub fold (harness test, no model)', denoise_steps=0, diffuser=None)
+
+
 def main():
     args = parse()
+    if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != args.gpus:
+        print(f'bench.py: --gpus {args.gpus} but WORLD_SIZE={world}', file=sys.stderr)
+        sys.exit(2)
     # DM_DIST_BACKEND=gloo rehearses the N > 1 path with several ranks on one GPU (host-side gather);
     # the measured configuration is nccl (RCCL over xGMI), one rank per GPU.
     backend = os.environ.get('DM_DIST_BACKEND', 'nccl')
+    stub = args.workload == 'stub'
+    if stub:
+        backend = 'gloo'
     gpu = local_rank % max(1, torch.cuda.device_count())
     if world > 1:
-        torch.cuda.set_device(gpu)
+        if not stub:
+            torch.cuda.set_device(gpu)
         if backend == 'nccl':
             dist.init_process_group('nccl', device_id=torch.device('cuda', gpu))
         else:
             dist.init_process_group(backend)
-    dev = torch.device('cuda', gpu)
+        if dist.get_world_size() != args.gpus:
+            print(f'bench.py: --gpus {args.gpus} but the process group has {dist.get_world_size()} ranks',
+                  file=sys.stderr)
+            sys.exit(2)
+    dev = torch.device('cpu') if stub else torch.device('cuda', gpu)
+    sync = (lambda: None) if stub else torch.cuda.synchronize
 
-    import dmhip
-    from dmhip._lib import check as _check
-
-    dmhip.load()
-    wl = build_workload(args.workload, args, dev, rank)
+    if stub:
+        wl = build_stub(args, dev, rank)
+    else:
+        import dmhip
+        from dmhip._lib import check as _check
+        dmhip.load()
+        wl = build_workload(args.workload, args, dev, rank)
     B, shape = wl['images'], wl['shape']
     gathered = torch.empty((world * B, *shape[1:]), device=dev) if world > 1 else None
 
@@ -384,11 +452,11 @@ def main():
     for h, abi, _ in wl['handles']:
         dmhip.unet_profile_enable(h, 0 if args.no_profile else PROFILE_EVERY, abi=abi)
     barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         fold()
-    torch.cuda.synchronize()
+    sync()
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -410,13 +478,16 @@ def main():
         dmhip.unet_profile_enable(h, False, abi=abi)
 
     roof, total_gpu_ms, total_flops, fam = None, 0.0, 0.0, {}
-    if not args.no_profile:
+    if not args.no_profile and prof:
         roof, total_gpu_ms, total_flops, fam = roofline(prof, args.workload)
 
     if rank == 0:
         images = world * B * args.steps
-        h0, abi0, _ = wl['handles'][0]
-        math = dmhip.unet_conv_math(h0) if abi0 == 'dm_unet' else dmhip.dit_math(h0)
+        if stub:
+            math = 'fp32'
+        else:
+            h0, abi0, _ = wl['handles'][0]
+            math = dmhip.unet_conv_math(h0) if abi0 == 'dm_unet' else dmhip.dit_math(h0)
         line = dict(
             metric=wl['metric'],
             value=round(images / elapsed, 4),
@@ -434,7 +505,7 @@ def main():
                         denoise_steps=wl['denoise_steps'], weights_gb=round(wbytes_t / 1e9, 3),
                         workspace_gb=round(wsbytes_t / 1e9, 3), conv_math=math,
                         # the reference draws randn_like every step even at eta=0 (ddim.py:76): so does the bench
-                        skip_unused_noise=wl['diffuser'].skip_unused_noise),
+                        skip_unused_noise=wl['diffuser'].skip_unused_noise if wl['diffuser'] else None),
             roofline=roof,
             step_level=dict(model_tflops=round(total_flops / (total_gpu_ms * 1e-3) / 1e12, 2) if total_gpu_ms else None,
                             # observed forwards are 1 in PROFILE_EVERY: their kernel time scaled to all forwards

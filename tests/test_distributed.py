@@ -58,3 +58,32 @@ def test_gloo_world2_fold_gather(tmp_path, n_samples, batch_size):
         parts = [torch.tanh(torch.randn((bspp, 1, 2, 2), generator=gens[r])) * 0.5 + 0.25 * r for r in range(world)]
         expect = torch.cat(parts)[:bs].clamp(-1, 1)
         assert torch.equal(imgs, expect)
+
+
+def _bench(args, env_extra):
+    import json
+    import subprocess
+    env = dict(os.environ, DM_DIST_BACKEND='gloo', MASTER_ADDR='127.0.0.1')
+    for k in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_PORT'):
+        env.pop(k, None)
+    env.update(env_extra)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py')] + args, env=env, capture_output=True,
+                       text=True, timeout=240)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{')]
+    return p.returncode, [json.loads(ln) for ln in lines], p.stderr
+
+
+def test_bench_gpus2_launches_two_ranks():
+    """`bench.py --gpus 2` with no launcher starts the two ranks itself (fresh child processes, before any GPU
+    call) and forwards rank 0's line: n_gpus 2, the global batch of both ranks, barrier + max-over-ranks timing."""
+    rc, lines, err = _bench(['--gpus', '2', '--workload', 'stub', '--steps', '2', '--warmup', '1'], {})
+    assert rc == 0, err
+    assert len(lines) == 1, (lines, err)
+    line = lines[0]
+    assert line['n_gpus'] == 2 and line['config']['global_batch'] == 8 and line['config']['parallelism'] == 'dp2'
+    assert line['value'] > 0 and line['steps'] == 2
+
+
+def test_bench_rejects_gpus_world_mismatch():
+    rc, lines, err = _bench(['--gpus', '1', '--workload', 'stub'], {'WORLD_SIZE': '2', 'RANK': '0'})
+    assert rc == 2 and not lines and 'WORLD_SIZE=2' in err
