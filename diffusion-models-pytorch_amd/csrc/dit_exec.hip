@@ -59,8 +59,14 @@ struct DiTModel {
   std::vector<BlockP> blocks;
   // Arithmetic of the token GEMMs (qkv, attention, proj, fc1, fc2, final): 2 = fp16x2 split (gemm.hip
   // SPLIT; default unless DM_CONV_MATH=fp32|bf16x3), 0 = fp32 MFMA. A forward that raises range_flag
-  // (an operand beyond the fp16 range) runs again in fp32 and the model stays there.
-  int math = conv_math_from_env() == 2 ? 2 : 0;
+  // (an operand beyond the fp16 range) runs again in fp32; the next forward is fp16x2 again (plans cached
+  // per (B, arithmetic)). Deferred mode: dm_dit_range_poll sets `fallback` for the caller's re-run,
+  // dm_dit_range_fallback clears it. `math` is the arithmetic of the plan being built (set by get_plan).
+  int base_math = conv_math_from_env() == 2 ? 2 : 0;
+  bool fallback = false;
+  long range_fallbacks = 0;
+  int math = base_math;
+  int run_math() const { return base_math == 2 && fallback ? 0 : base_math; }
   bool range_check = !(std::getenv("DM_RANGE_CHECK") && std::string(std::getenv("DM_RANGE_CHECK")) == "0");
   int* range_flag = nullptr;
   int* range_flag_host = nullptr;
@@ -73,6 +79,7 @@ struct DiTModel {
 
   struct Plan : PlanBase {
     int B = 0;
+    int math = 0;   // the arithmetic the plan was built with
     // plan-owned staging of the caller's tensors (graph replay reads fixed pointers)
     float* x = nullptr;
     int64_t* t = nullptr;
@@ -91,8 +98,10 @@ struct DiTModel {
     if (arena) (void)hipFree(arena);
   }
   int build_plan(Plan& pl, int B);
-  int get_plan(int B, Plan** out) {
-    return plans.get([&](const Plan& p) { return p.B == B; }, [&](Plan& p) { return build_plan(p, B); }, out);
+  int get_plan(int B, int m, Plan** out) {
+    math = m;
+    return plans.get([&](const Plan& p) { return p.B == B && p.math == m; }, [&](Plan& p) { return build_plan(p, B); },
+                     out);
   }
 };
 
@@ -183,6 +192,7 @@ static int dit_create(const dm_dit_arch* arch, const float* const* params, const
 
 int DiTModel::build_plan(Plan& pl, int B) {
   pl.B = B;
+  pl.math = math;
   const dm_dit_arch& a = arch;
   const int p = a.patch_size, C = a.in_channels, S = a.input_size, Hm = a.mlp_hidden;
   const int heads = a.num_heads, Dh = D / heads;
@@ -375,6 +385,14 @@ int DiTModel::build_plan(Plan& pl, int B) {
       gq.ap_ea = 6; gq.ap_eb = 6; gq.ap_ev = 6;
     }
     add_token_gemm(gq);
+    // the proj GEMM, built before the attention op: the flash kernel writes O as the proj's pre-split A image
+    // only when this GEMM is the one that will read it (same predicate), else O as fp32 rows
+    GemmArgs gpj = linear(Ob, D, M, bp.proj_w, bp.proj_b, D, D, x, D);
+    gpj.res = x; gpj.ld_res = D; gpj.gate = mb + 2 * D; gpj.gate_pitch = ada_total; gpj.gate_rows = T;
+    split(gpj, 6, bp.proj_w, (size_t)D * D, 0);
+    GemmArgs gpj_as = gpj;
+    gpj_as.as = reinterpret_cast<const _Float16*>(Ob);
+    const bool o_presplit = flash && presplit_on && D % 32 == 0 && gpj.ws && gpj.split_ea == 6 && linear_k32_ok(gpj_as);
     if (flash) {
       AttnArgs at{};
       at.pq = planes; at.pk = planes + plane_n; at.pv = planes + 2 * plane_n;
@@ -382,7 +400,7 @@ int DiTModel::build_plan(Plan& pl, int B) {
       at.out = Ob; at.ldo = D;
       at.ea = 6; at.eb = 6; at.ep = 14; at.ev = 6;
       at.range_flag = range_flag;
-      if (presplit_on && D % 32 == 0) {   // O straight into the proj GEMM's pre-split A image (over Ob)
+      if (o_presplit) {   // O straight into the proj GEMM's pre-split A image (over Ob)
         at.o_split = reinterpret_cast<_Float16*>(Ob);
         at.o_split_ea = 6;
         at.o_ld = D;
@@ -412,17 +430,10 @@ int DiTModel::build_plan(Plan& pl, int B) {
       split(go, 14, 0, 0, 6);
       add_gemm(go);
     }
-    {
-      GemmArgs g = linear(Ob, D, M, bp.proj_w, bp.proj_b, D, D, x, D);
-      g.res = x; g.ld_res = D; g.gate = mb + 2 * D; g.gate_pitch = ada_total; g.gate_rows = T;
-      split(g, 6, bp.proj_w, (size_t)D * D, 0);
-      GemmArgs gp = g;
-      gp.as = reinterpret_cast<const _Float16*>(Ob);
-      if (flash && presplit_on && D % 32 == 0 && g.ws && g.split_ea == 6 && linear_k32_ok(gp))
-        add_gemm(gp);   // A = the flash kernel's pre-split O image
-      else
-        add_token_gemm(g);
-    }
+    if (o_presplit)
+      add_gemm(gpj_as);   // A = the flash kernel's pre-split O image
+    else
+      add_token_gemm(gpj);
     // MLP branch
     stats_op();
     {
@@ -500,33 +511,34 @@ extern "C" int dm_dit_forward(dm_dit* h, const float* x, const int64_t* t, const
     return DM_ERR_ARG;
   }
   dm::DiTModel* m = h->m;
-  dm::DiTModel::Plan* plp = nullptr;
-  const int rc0 = m->get_plan(B, &plp);
-  if (rc0) return rc0;
   hipStream_t st = (hipStream_t)stream;
-  auto& pl = *plp;
   const int S = m->arch.input_size;
   const size_t nx = (size_t)B * m->arch.in_channels * S * S, no = (size_t)B * m->OC * S * S;
-  DM_CHECK_HIP(hipMemcpyAsync(pl.x, x, nx * sizeof(float), hipMemcpyDeviceToDevice, st));
-  DM_CHECK_HIP(hipMemcpyAsync(pl.t, t, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
-  if (y)
-    DM_CHECK_HIP(hipMemcpyAsync(pl.y, y, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
-  else
-    DM_CHECK_HIP(hipMemsetAsync(pl.y, 0xff, (size_t)B * sizeof(int64_t), st));  // -1: the null class
-  const int rc = pl.run(st);
-  if (rc) return rc;
-  DM_CHECK_HIP(hipMemcpyAsync(out, pl.out, no * sizeof(float), hipMemcpyDeviceToDevice, st));
-  if (m->math == 2 && m->range_check && !m->range_deferred) {
+  // at most two passes: the caller's arithmetic, then (an fp16x2 operand beyond the fp16 range) fp32
+  if (const int rco = m->plans.pool->order(st)) return rco;
+  for (int math = m->run_math();;) {
+    dm::DiTModel::Plan* plp = nullptr;
+    const int rc0 = m->get_plan(B, math, &plp);
+    if (rc0) return rc0;
+    auto& pl = *plp;
+    DM_CHECK_HIP(hipMemcpyAsync(pl.x, x, nx * sizeof(float), hipMemcpyDeviceToDevice, st));
+    DM_CHECK_HIP(hipMemcpyAsync(pl.t, t, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+    if (y)
+      DM_CHECK_HIP(hipMemcpyAsync(pl.y, y, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+    else
+      DM_CHECK_HIP(hipMemsetAsync(pl.y, 0xff, (size_t)B * sizeof(int64_t), st));  // -1: the null class
+    const int rc = pl.run(st);
+    if (rc) return rc;
+    DM_CHECK_HIP(hipMemcpyAsync(out, pl.out, no * sizeof(float), hipMemcpyDeviceToDevice, st));
+    if (math != 2 || !m->range_check || m->range_deferred) break;
     DM_CHECK_HIP(hipMemcpyAsync(m->range_flag_host, m->range_flag, sizeof(int), hipMemcpyDeviceToHost, st));
     DM_CHECK_HIP(hipStreamSynchronize(st));
-    if (*m->range_flag_host) {  // an fp16x2 GEMM met an operand beyond the fp16 range: fp32 from here on
-      DM_CHECK_HIP(hipMemsetAsync(m->range_flag, 0, sizeof(int), st));
-      m->math = 0;
-      m->plans.clear();
-      return dm_dit_forward(h, x, t, y, B, out, stream);
-    }
+    if (!*m->range_flag_host) break;
+    DM_CHECK_HIP(hipMemsetAsync(m->range_flag, 0, sizeof(int), st));
+    m->range_fallbacks++;
+    math = 0;
   }
-  return DM_OK;
+  return m->plans.pool->mark(st);
 }
 
 extern "C" int dm_dit_set_range_deferred(dm_dit* h, int deferred) {
@@ -546,19 +558,33 @@ extern "C" int dm_dit_range_poll(dm_dit* h, void* stream, int* flagged) {
   if (*m->range_flag_host) {
     DM_CHECK_HIP(hipMemsetAsync(m->range_flag, 0, sizeof(int), st));
     *flagged = 1;
-    if (m->math == 2) {
-      m->math = 0;
-      m->plans.clear();
+    if (m->base_math == 2) {  // the caller re-runs what it computed since the last poll: in fp32
+      m->fallback = true;
+      m->range_fallbacks++;
     }
   }
+  return DM_OK;
+}
+
+extern "C" int dm_dit_range_fallback(dm_dit* h, int on) {
+  if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
+  h->m->fallback = on != 0;
+  return DM_OK;
+}
+
+extern "C" int dm_dit_range_stats(const dm_dit* h, int64_t* fallbacks, int* active) {
+  if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
+  if (fallbacks) *fallbacks = h->m->range_fallbacks;
+  if (active) *active = h->m->run_math();
   return DM_OK;
 }
 
 extern "C" int dm_dit_set_math(dm_dit* h, int kind) {
   if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
   if (kind != 0 && kind != DM_SPLIT_FP16X2) { dm::set_error("DiT math must be 0 (fp32) or DM_SPLIT_FP16X2"); return DM_ERR_ARG; }
-  if (kind != h->m->math) {
-    h->m->math = kind;
+  h->m->fallback = false;
+  if (kind != h->m->base_math) {
+    h->m->base_math = kind;
     h->m->plans.clear();
   }
   return DM_OK;
@@ -566,7 +592,7 @@ extern "C" int dm_dit_set_math(dm_dit* h, int kind) {
 
 extern "C" int dm_dit_get_math(const dm_dit* h, int* kind) {
   if (!h || !h->m || !kind) { dm::set_error("null model"); return DM_ERR_STATE; }
-  *kind = h->m->math;
+  *kind = h->m->base_math;
   return DM_OK;
 }
 

@@ -177,9 +177,11 @@ __global__ void __launch_bounds__(256) conv3x3_small_in_kernel(const float* __re
     x0 = (gI % S) * len;
     x1 = min(x0 + len, W);
   } else {
-    const int RG = R / px_par;
-    r0 = gI * RG;
-    r1 = r0 + RG;
+    // px_par groups over R rows, ceil(R / px_par) rows each (the last group may hold fewer); the leftover
+    // threads of a block whose size the channel pairs do not divide (gI == px_par) get no rows
+    const int RG = (R + px_par - 1) / px_par;
+    r0 = min(gI * RG, R);
+    r1 = min(r0 + RG, R);
     x0 = 0;
     x1 = W;
   }

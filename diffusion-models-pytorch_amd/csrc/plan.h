@@ -59,6 +59,30 @@ struct Slab {
 // larger slab, while the plans built over the old one keep it (no rebuild) until they are evicted.
 struct ScratchPool {
   std::shared_ptr<Slab> cur;
+  // Stream order of the forwards over this pool's slabs: a forward on a stream other than the previous
+  // forward's waits for that forward's completion event first (the slabs are shared by the cached plans and
+  // by the models joined with dm_unet_share_workspace; two forwards in flight on two streams would race on
+  // the scratch). Same stream: no wait, one event record per forward.
+  hipEvent_t done = nullptr;
+  hipStream_t last = nullptr;
+  bool used = false;
+  ScratchPool() = default;
+  ScratchPool(const ScratchPool&) = delete;
+  ScratchPool& operator=(const ScratchPool&) = delete;
+  ~ScratchPool() {
+    if (done) (void)hipEventDestroy(done);
+  }
+  int order(hipStream_t st) {
+    if (used && last != st) DM_CHECK_HIP(hipStreamWaitEvent(st, done, 0));
+    return DM_OK;
+  }
+  int mark(hipStream_t st) {
+    if (!done) DM_CHECK_HIP(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+    DM_CHECK_HIP(hipEventRecord(done, st));
+    last = st;
+    used = true;
+    return DM_OK;
+  }
   int ensure(size_t need, std::shared_ptr<Slab>& out) {
     if (!cur || need > cur->bytes) {
       auto s = std::make_shared<Slab>();
@@ -255,6 +279,14 @@ struct PlanCache {
     m.reset();
     auto p = std::make_unique<P>();
     rc = pool->ensure(need, p->slab);
+    if (rc == DM_ERR_HIP) {
+      // out of device memory: drop this model's cached plans (they pin older, smaller slabs) and the pool's
+      // current slab if nothing else holds it, then try once more
+      plans.clear();
+      if (pool->cur && pool->cur.use_count() == 1) pool->cur.reset();
+      (void)hipDeviceSynchronize();
+      rc = pool->ensure(need, p->slab);
+    }
     if (rc) return rc;
     p->scratch = p->slab->base;
     rc = build(*p);

@@ -157,6 +157,7 @@ struct UNetModel {
   // plan cache (LRU over (B, H, W)), scratch from a pool shared with dm_unet_share_workspace peers
   struct Plan : PlanBase {
     int B = 0, H = 0, W = 0;
+    int math = 0;   // the arithmetic the plan was built with (conv_math at build time)
     // plan-owned staging of the caller's tensors (every launch reads fixed pointers: graph replay)
     float* x = nullptr;
     int64_t* t = nullptr;
@@ -166,16 +167,23 @@ struct UNetModel {
   PlanCache<Plan> plans;
   float* last_packed = nullptr;  // last conv weights as [9][Cin][CO] (small_out_pack), made at the first build
   // Split copies of the halo-patch conv weights (conv_patch3.hip), made at the first plan build.
-  // conv_math: 2 fp16x2 (default), 3 bf16x3, 0 fp32 MFMA kernels (DM_CONV_MATH=fp16x2|bf16x3|fp32).
-  // fp16x2 convs raise range_flag on an activation beyond the fp16 range; the forward then
-  // switches this model to bf16x3 and runs again (DM_RANGE_CHECK=0 skips the check and its sync).
-  int conv_math = conv_math_from_env();
+  // base_math: the arithmetic the caller chose -- 2 fp16x2 (default), 3 bf16x3, 0 fp32 MFMA kernels
+  // (DM_CONV_MATH=fp16x2|bf16x3|fp32). fp16x2 convs raise range_flag on an activation beyond the fp16 range;
+  // that forward then runs again in bf16x3 and the next one is fp16x2 again (not sticky: plans are cached
+  // per (shape, arithmetic)). In deferred mode the caller's re-run of a flagged loop runs in bf16x3 while
+  // `fallback` is set (dm_unet_range_poll sets it, dm_unet_range_fallback clears it). DM_RANGE_CHECK=0
+  // skips the check and its sync. conv_math is the arithmetic of the plan being built (set by get_plan).
+  int base_math = conv_math_from_env();
+  bool fallback = false;
+  int conv_math = base_math;
+  int run_math() const { return base_math == 2 && fallback ? 3 : base_math; }
   bool range_check = !(std::getenv("DM_RANGE_CHECK") && std::string(std::getenv("DM_RANGE_CHECK")) == "0");
   int* range_flag = nullptr;       // device
   int* range_flag_host = nullptr;  // pinned
   // Deferred mode (dm_unet_set_range_deferred): forwards neither read the flag nor sync; the caller
   // polls it once per sampling loop (dm_unet_range_poll) and re-runs the loop if it was raised.
   bool range_deferred = false;
+  long range_fallbacks = 0;   // forwards / loops re-run in bf16x3 (dm_unet_range_stats)
   std::map<std::pair<const float*, int>, void*> split_w;
   size_t split_bytes = 0;
   void split_for(ConvArgs& c);
@@ -186,8 +194,9 @@ struct UNetModel {
   float* P(size_t off) const { return arena + off; }
   ~UNetModel();
   int build_plan(Plan& pl, int B, int H, int W);
-  int get_plan(int B, int H, int W, Plan** out) {
-    return plans.get([&](const Plan& p) { return p.B == B && p.H == H && p.W == W; },
+  int get_plan(int B, int H, int W, int math, Plan** out) {
+    conv_math = math;
+    return plans.get([&](const Plan& p) { return p.B == B && p.H == H && p.W == W && p.math == math; },
                      [&](Plan& p) { return build_plan(p, B, H, W); }, out);
   }
 };
@@ -594,6 +603,7 @@ static int unet_create(const dm_unet_arch* arch, const float* const* params, con
 // ---------------------------------------------------------------------------
 int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
   pl.B = B;
+  pl.math = conv_math;
   pl.H = H;
   pl.W = W;
   if (!range_flag) {
@@ -1240,33 +1250,34 @@ extern "C" int dm_unet_forward(dm_unet* h, const float* x, const int64_t* t, con
     return DM_ERR_ARG;
   }
   dm::UNetModel* m = h->m;
-  dm::UNetModel::Plan* plp = nullptr;
-  int rc0 = m->get_plan(B, H, W, &plp);
-  if (rc0) return rc0;
   hipStream_t st = (hipStream_t)stream;
-  auto& pl = *plp;
   const size_t nx = (size_t)B * m->arch.in_channels * H * W, no = (size_t)B * m->arch.out_channels * H * W;
-  DM_CHECK_HIP(hipMemcpyAsync(pl.x, x, nx * sizeof(float), hipMemcpyDeviceToDevice, st));
-  DM_CHECK_HIP(hipMemcpyAsync(pl.t, t, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
-  if (y)
-    DM_CHECK_HIP(hipMemcpyAsync(pl.y, y, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
-  else
-    DM_CHECK_HIP(hipMemsetAsync(pl.y, 0xff, (size_t)B * sizeof(int64_t), st));  // -1: no label
-  const int rc = pl.run(st);
-  if (rc) return rc;
-  DM_CHECK_HIP(hipMemcpyAsync(out, pl.out, no * sizeof(float), hipMemcpyDeviceToDevice, st));
-  if (m->conv_math == 2 && m->range_check && !m->range_deferred) {
-    // an fp16x2 conv met an activation beyond 65504: this model continues in bf16x3, from this call
+  // at most two passes: the caller's arithmetic, then (fp16x2 met an activation beyond the fp16 range) the
+  // same forward in bf16x3; the model's next forward is fp16x2 again
+  if (const int rco = m->plans.pool->order(st)) return rco;
+  for (int math = m->run_math();;) {
+    dm::UNetModel::Plan* plp = nullptr;
+    const int rc0 = m->get_plan(B, H, W, math, &plp);
+    if (rc0) return rc0;
+    auto& pl = *plp;
+    DM_CHECK_HIP(hipMemcpyAsync(pl.x, x, nx * sizeof(float), hipMemcpyDeviceToDevice, st));
+    DM_CHECK_HIP(hipMemcpyAsync(pl.t, t, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+    if (y)
+      DM_CHECK_HIP(hipMemcpyAsync(pl.y, y, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+    else
+      DM_CHECK_HIP(hipMemsetAsync(pl.y, 0xff, (size_t)B * sizeof(int64_t), st));  // -1: no label
+    const int rc = pl.run(st);
+    if (rc) return rc;
+    DM_CHECK_HIP(hipMemcpyAsync(out, pl.out, no * sizeof(float), hipMemcpyDeviceToDevice, st));
+    if (math != 2 || !m->range_check || m->range_deferred) break;
     DM_CHECK_HIP(hipMemcpyAsync(m->range_flag_host, m->range_flag, sizeof(int), hipMemcpyDeviceToHost, st));
     DM_CHECK_HIP(hipStreamSynchronize(st));
-    if (*m->range_flag_host) {
-      DM_CHECK_HIP(hipMemsetAsync(m->range_flag, 0, sizeof(int), st));
-      m->conv_math = 3;
-      m->plans.clear();
-      return dm_unet_forward(h, x, t, y, B, H, W, out, stream);
-    }
+    if (!*m->range_flag_host) break;
+    DM_CHECK_HIP(hipMemsetAsync(m->range_flag, 0, sizeof(int), st));
+    m->range_fallbacks++;
+    math = 3;
   }
-  return DM_OK;
+  return m->plans.pool->mark(st);
 }
 
 extern "C" int dm_unet_set_range_deferred(dm_unet* h, int deferred) {
@@ -1286,11 +1297,24 @@ extern "C" int dm_unet_range_poll(dm_unet* h, void* stream, int* flagged) {
   if (*m->range_flag_host) {
     DM_CHECK_HIP(hipMemsetAsync(m->range_flag, 0, sizeof(int), st));
     *flagged = 1;
-    if (m->conv_math == 2) {  // continue in bf16x3; the caller re-runs what it computed since the last poll
-      m->conv_math = 3;
-      m->plans.clear();
+    if (m->base_math == 2) {  // the caller re-runs what it computed since the last poll: in bf16x3
+      m->fallback = true;
+      m->range_fallbacks++;
     }
   }
+  return DM_OK;
+}
+
+extern "C" int dm_unet_range_fallback(dm_unet* h, int on) {
+  if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
+  h->m->fallback = on != 0;
+  return DM_OK;
+}
+
+extern "C" int dm_unet_range_stats(const dm_unet* h, int64_t* fallbacks, int* active) {
+  if (!h || !h->m) { dm::set_error("null model"); return DM_ERR_STATE; }
+  if (fallbacks) *fallbacks = h->m->range_fallbacks;
+  if (active) *active = h->m->run_math();
   return DM_OK;
 }
 
@@ -1320,8 +1344,9 @@ extern "C" int dm_unet_set_conv_math(dm_unet* h, int kind) {
     dm::set_error("conv math must be 0 (fp32), DM_SPLIT_BF16X3 or DM_SPLIT_FP16X2");
     return DM_ERR_ARG;
   }
-  if (kind != h->m->conv_math) {
-    h->m->conv_math = kind;
+  h->m->fallback = false;
+  if (kind != h->m->base_math) {
+    h->m->base_math = kind;
     h->m->plans.clear();
   }
   return DM_OK;
@@ -1329,7 +1354,7 @@ extern "C" int dm_unet_set_conv_math(dm_unet* h, int kind) {
 
 extern "C" int dm_unet_get_conv_math(const dm_unet* h, int* kind) {
   if (!h || !h->m || !kind) { dm::set_error("null model"); return DM_ERR_STATE; }
-  *kind = h->m->conv_math;
+  *kind = h->m->base_math;
   return DM_OK;
 }
 

@@ -152,6 +152,7 @@ class DDPM:
     # Reference ddpm.py:102-120, 140-172. The coefficients are the reference's torch CPU expressions
     # (0-dim for an int t, [B] vectors for per-image timesteps), the elementwise arithmetic one
     # dm_lincomb launch with separately rounded float32 products (bit-identical to the CPU expression).
+    # Non-contiguous tensor arguments are accepted, as by the reference's torch expressions.
     def _row_coefs(self, t, x: Tensor):
         """sqrt(ac_t), sqrt(1 - ac_t) for t: an int / 0-dim tensor (scalars) or [B] timesteps (one per image)."""
         if isinstance(t, Tensor) and t.ndim >= 1:
@@ -165,31 +166,31 @@ class DDPM:
 
     def pred_x0_from_eps(self, xt: Tensor, t: int, eps: Tensor):
         c = self._predict_coefs(int(t))
-        return dmhip.lincomb(1, xt, eps, c['sqrt_recip_ac'], c['sqrt_recipm1_ac'])
+        return dmhip.lincomb(1, xt.contiguous(), eps.contiguous(), c['sqrt_recip_ac'], c['sqrt_recipm1_ac'])
 
     def pred_eps_from_x0(self, xt: Tensor, t: int, x0: Tensor):
         c = self._predict_coefs(int(t))
-        return dmhip.lincomb(2, xt, x0, c['sqrt_recip_ac'], c['sqrt_recipm1_ac'])
+        return dmhip.lincomb(2, xt.contiguous(), x0.contiguous(), c['sqrt_recip_ac'], c['sqrt_recipm1_ac'])
 
     def pred_x0_from_v(self, xt: Tensor, t: int, v: Tensor):
         c = self._predict_coefs(int(t))
-        return dmhip.lincomb(1, xt, v, c['sqrt_ac'], c['sqrt_one_minus_ac'])
+        return dmhip.lincomb(1, xt.contiguous(), v.contiguous(), c['sqrt_ac'], c['sqrt_one_minus_ac'])
 
     def pred_eps_from_v(self, xt: Tensor, t: int, v: Tensor):
         c = self._predict_coefs(int(t))
-        return dmhip.lincomb(0, xt, v, c['sqrt_one_minus_ac'], c['sqrt_ac'])
+        return dmhip.lincomb(0, xt.contiguous(), v.contiguous(), c['sqrt_one_minus_ac'], c['sqrt_ac'])
 
     def get_v(self, x0: Tensor, eps: Tensor, t: Tensor):
         """v = sqrt(ac_t) eps - sqrt(1 - ac_t) x0 (reference ddpm.py:140-150)."""
         sa, s1m = self._row_coefs(t, x0)
-        return dmhip.lincomb(1, eps, x0, sa, s1m)
+        return dmhip.lincomb(1, eps.contiguous(), x0.contiguous(), sa, s1m)
 
     def diffuse(self, x0: Tensor, t: Tensor, eps: Tensor = None):
         """Sample from q(x_t | x0) = sqrt(ac_t) x0 + sqrt(1 - ac_t) eps (reference ddpm.py:152-172);
         t holds one timestep per image (or one int for all), eps defaults to torch.randn_like(x0)."""
         eps = torch.randn_like(x0) if eps is None else eps
         sa, s1m = self._row_coefs(t, x0)
-        return dmhip.lincomb(0, x0, eps.contiguous(), sa, s1m)
+        return dmhip.lincomb(0, x0.contiguous(), eps.contiguous(), sa, s1m)
 
     # ------------------------------------------------------------- the step
     def _draw_noise(self, xt: Tensor, needed: bool) -> Optional[Tensor]:
@@ -318,8 +319,9 @@ class DDPM:
     def _range_guarded(self, run: Callable[[], Tensor], init_noise: Tensor) -> Tensor:
         """Run a whole sampling loop with the fp16x2 range check of the native models deferred to its
         end: one host sync per loop instead of one per forward. If any forward met an activation
-        beyond the fp16 range, those models have switched to their exact fallback arithmetic and the
-        loop runs again from the same device RNG state, so the result is what the fallback gives.
+        beyond the fp16 range, the loop runs again from the same device RNG state with those models in
+        their exact fallback arithmetic, so the result is what the fallback gives; afterwards they run
+        fp16x2 again (the fallback is not sticky).
         A caller-installed noise source cannot be rewound: then every forward checks as it goes."""
         if self.noise_fn is not None or not isinstance(init_noise, Tensor) or init_noise.device.type != 'cuda':
             return run()
@@ -329,7 +331,10 @@ class DDPM:
             result = run()
         if scope.flagged:
             torch.cuda.set_rng_state(rng, dev)
-            result = run()
+            try:
+                result = run()
+            finally:
+                scope.end_fallback()
         return result
 
 

@@ -142,13 +142,15 @@ def null_labels_allowed() -> bool:
 class deferred_range_check:
     """Context manager over one sampling loop: native forwards inside it do not sync on the fp16x2
     range flag; on exit every model handle used inside is polled once (dm_*_range_poll) and
-    ``flagged`` tells whether any forward met an activation beyond the fp16 range (those models
-    have then switched to their exact fallback arithmetic and the loop must be re-run)."""
+    ``flagged`` tells whether any forward met an activation beyond the fp16 range. Those models
+    (``flagged_handles``) are then in fallback: their forwards run in the exact fallback arithmetic
+    while the caller re-runs the loop, and ``end_fallback()`` returns them to fp16x2."""
     active = None
 
     def __init__(self):
         self.handles = {}
         self.flagged = False
+        self.flagged_handles = []
         self._outer = None
 
     @staticmethod
@@ -168,7 +170,9 @@ class deferred_range_check:
             flag = ctypes.c_int()
             check(getattr(L, abi + '_range_poll')(handle, stream_handle(device), ctypes.byref(flag)),
                   abi + '_range_poll')
-            self.flagged |= bool(flag.value)
+            if flag.value:
+                self.flagged = True
+                self.flagged_handles.append((handle, abi))
 
     @classmethod
     def release(cls, handle):
@@ -196,7 +200,15 @@ class deferred_range_check:
         self.handles.clear()
         if self._outer is not None and self.flagged:
             self._outer.flagged = True
+            self._outer.flagged_handles.extend(self.flagged_handles)
+            self.flagged_handles = []
         return False
+
+    def end_fallback(self):
+        """The re-run is done: the flagged models run fp16x2 again from their next forward."""
+        for handle, abi in self.flagged_handles:
+            check(getattr(load(), abi + '_range_fallback')(handle, 0), abi + '_range_fallback')
+        self.flagged_handles = []
 
 
 def _declare(L: ctypes.CDLL):
@@ -234,6 +246,10 @@ def _declare(L: ctypes.CDLL):
     L.dm_unet_get_conv_math.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
     L.dm_unet_set_range_deferred.argtypes = [vp, ctypes.c_int]
     L.dm_unet_range_poll.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_int)]
+    L.dm_unet_range_fallback.argtypes = [vp, ctypes.c_int]
+    L.dm_unet_range_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int)]
+    L.dm_dit_range_fallback.argtypes = [vp, ctypes.c_int]
+    L.dm_dit_range_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int)]
     L.dm_dit_set_range_deferred.argtypes = [vp, ctypes.c_int]
     L.dm_dit_range_poll.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_int)]
     L.dm_dit_set_math.argtypes = [vp, ctypes.c_int]
@@ -453,6 +469,14 @@ def unet_profile_read(handle, abi: str = 'dm_unet'):
     return out
 
 
+def range_stats(handle, abi: str = 'dm_unet'):
+    """(forwards / loops re-run in the fallback arithmetic so far, arithmetic of the next forward) of a native
+    model handle (dm_unet_range_stats / dm_dit_range_stats)."""
+    n, active = ctypes.c_int64(), ctypes.c_int()
+    check(getattr(load(), abi + '_range_stats')(handle, ctypes.byref(n), ctypes.byref(active)), abi + '_range_stats')
+    return n.value, {v: k for k, v in CONV_MATH.items()}[active.value]
+
+
 def plan_stats(handle, abi: str = 'dm_unet'):
     """(plans built so far, plans cached) of a native model handle (dm_unet_plan_stats / dm_dit_plan_stats)."""
     builds, cached = ctypes.c_int64(), ctypes.c_int()
@@ -473,7 +497,12 @@ def lincomb(mode: int, a: torch.Tensor, b: torch.Tensor, c1, c2, out: torch.Tens
         require_device_tensor(t, name)
     if a.shape != b.shape:
         raise ValueError(f'lincomb: shapes {tuple(a.shape)} and {tuple(b.shape)} differ')
-    out = torch.empty_like(a) if out is None else out
+    if out is None:
+        out = torch.empty_like(a)
+    else:
+        require_device_tensor(out, 'out')
+        if out.shape != a.shape:
+            raise ValueError(f'lincomb: out has shape {tuple(out.shape)}, the operands {tuple(a.shape)}')
     B = a.shape[0] if a.ndim else 1
     row = a.numel() // B if B else 1
 

@@ -22,7 +22,8 @@ class UNetCombined(nn.Module):
         kwargs_uncond = kwargs.copy()
         kwargs_uncond.update({'num_classes': None})
         self.unet_uncond = UNetModel(*args, **kwargs_uncond)
-        # the two networks never run concurrently: one plan workspace for both (weak links, not submodules)
+        # one plan workspace for both networks (weak links, not submodules); forwards of the two on different
+        # streams are serialised by the engine over that workspace (dm_unet_share_workspace)
         self.unet_cond.__dict__['_ws_peer'] = weakref.ref(self.unet_uncond)
         self.unet_uncond.__dict__['_ws_peer'] = weakref.ref(self.unet_cond)
 

@@ -155,8 +155,10 @@ class NativeDenoiser(nn.Module):
         return handle
 
     def _share_peer_workspace(self, handle):
-        """UNetCombined's two networks run one after the other on one stream: the second handle to be
-        created adopts the first one's plan scratch (dm_unet_share_workspace), one workspace for both."""
+        """UNetCombined's two networks never need to run at the same time: the second handle to be created
+        adopts the first one's plan scratch (dm_unet_share_workspace), one workspace for both. Forwards issued
+        on different streams stay correct: the engine makes a forward on a new stream wait for the previous
+        forward over the shared scratch (an event wait), so they serialise instead of racing."""
         ref = self.__dict__.get('_ws_peer')
         peer = ref() if ref is not None else None
         if peer is not None and self._abi == 'dm_unet' and getattr(peer, '_abi', None) == 'dm_unet' \

@@ -119,22 +119,29 @@ int dm_unet_memory(const dm_unet* m, int64_t* weight_bytes, int64_t* workspace_b
  * one scratch slab sized to the largest. dm_unet_share_workspace(a, b) makes b use a's slab too: for
  * models whose forwards never overlap (one stream, one after the other) -- UNetCombined's conditional
  * and unconditional networks (models/adm/unet_combined.py:23-25), which then hold one workspace instead
- * of two. dm_unet_plan_stats: plans built so far and plans cached. */
+ * of two. A forward on a stream other than the previous forward's over the same scratch waits for that
+ * forward first (an event wait), so forwards issued on several streams serialise instead of racing.
+ * dm_unet_plan_stats: plans built so far and plans cached. */
 int dm_unet_share_workspace(dm_unet* a, dm_unet* b);
 int dm_unet_plan_stats(const dm_unet* m, int64_t* builds, int* cached);
 /* Arithmetic of the 3x3 halo-patch convs (all fp32-accurate, models/unet.py:16,26 convolve in fp32):
  * DM_SPLIT_FP16X2 (default; env DM_CONV_MATH=fp16x2), DM_SPLIT_BF16X3 (bf16x3), 0 = fp32 MFMA (fp32).
  * An fp16x2 forward that meets an activation beyond the fp16 range (|a| > 65504) is detected on the
- * device and run again in bf16x3, which the model then keeps; get reports the current kind. */
+ * device and that forward is run again in bf16x3; the next forward is fp16x2 again (plans are cached per
+ * shape and arithmetic). get reports the caller's kind. */
 int dm_unet_set_conv_math(dm_unet* m, int kind);
 int dm_unet_get_conv_math(const dm_unet* m, int* kind);
 /* Deferred range check: with deferred != 0 a forward does not read the fp16x2 range flag (no host
  * sync per forward); the caller polls it once per sampling loop. dm_unet_range_poll synchronises
  * `stream`, reports whether any forward since the last poll met an activation beyond the fp16 range,
- * clears the flag and, if it was set, switches the model to bf16x3: the caller then re-runs what it
- * computed since the last poll (diffusions.DDPM.sample re-runs the loop from the same RNG state). */
+ * clears the flag and, if it was set, puts the model in fallback (bf16x3 forwards): the caller then re-runs
+ * what it computed since the last poll (diffusions.DDPM.sample re-runs the loop from the same RNG state) and
+ * ends the fallback with dm_unet_range_fallback(m, 0). dm_unet_range_stats: forwards / loops re-run in
+ * bf16x3 so far, and the arithmetic the next forward runs in. */
 int dm_unet_set_range_deferred(dm_unet* m, int deferred);
 int dm_unet_range_poll(dm_unet* m, void* stream, int* flagged);
+int dm_unet_range_fallback(dm_unet* m, int on);
+int dm_unet_range_stats(const dm_unet* m, int64_t* fallbacks, int* active_math);
 void dm_unet_destroy(dm_unet* m);
 
 /* Denoiser: DiT ------------------------------------------------------------
@@ -168,12 +175,15 @@ int dm_dit_create(const dm_dit_arch* arch, const float* const* params, const int
 int dm_dit_forward(dm_dit* m, const float* x, const int64_t* t, const int64_t* y, int B, float* out, void* stream);
 /* Arithmetic of the DiT token GEMMs: DM_SPLIT_FP16X2 (default, fp32-accurate products from an fp16 split
  * on the matrix cores) or 0 (fp32 MFMA; also DM_CONV_MATH=fp32|bf16x3). A forward whose operands leave
- * the fp16 range is re-run in fp32, which the model then keeps. */
+ * the fp16 range is re-run in fp32; the next forward is fp16x2 again. */
 int dm_dit_set_math(dm_dit* m, int kind);
 int dm_dit_get_math(const dm_dit* m, int* kind);
-/* As dm_unet_set_range_deferred / dm_unet_range_poll (a raised flag switches the DiT to fp32). */
+/* As dm_unet_set_range_deferred / dm_unet_range_poll / _range_fallback / _range_stats (the DiT's fallback
+ * arithmetic is fp32). */
 int dm_dit_set_range_deferred(dm_dit* m, int deferred);
 int dm_dit_range_poll(dm_dit* m, void* stream, int* flagged);
+int dm_dit_range_fallback(dm_dit* m, int on);
+int dm_dit_range_stats(const dm_dit* m, int64_t* fallbacks, int* active_math);
 /* 128-entry table exp(-ln(1e4) * i / 128) of the 256-wide frequency embedding (dit/model.py:51-54). */
 int dm_dit_set_time_freqs(dm_dit* m, const float* freqs, int n, void* stream);
 int dm_dit_profile(dm_dit* m, int enable);

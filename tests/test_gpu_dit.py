@@ -129,7 +129,7 @@ def test_dit_math_vs_oracle(cuda, golden, report, math):
 @pytest.mark.gpu
 def test_dit_range_fallback(cuda, golden):
     """fc1 weights x 1e5 push the GELU output (fc2's input, x 2^6) beyond fp16: the fp16x2 forward is
-    re-run in fp32 and equals a forward forced to fp32."""
+    re-run in fp32 and equals a forward forced to fp32; the model's arithmetic stays fp16x2 (not sticky)."""
     import dmhip
     g, meta = golden('dit')
     x, t, y = (torch.from_numpy(g[f'dit_tiny_{k}']).to(cuda) for k in ('x', 't', 'labels'))
@@ -144,5 +144,6 @@ def test_dit_range_fallback(cuda, golden):
         h = model.native_handle(torch.device(cuda))
         dmhip.dit_math(h, math)
         outs[math] = model(x, t, y).cpu()
-        assert dmhip.dit_math(h) == 'fp32'
+        assert dmhip.dit_math(h) == math
+        assert dmhip.range_stats(h, abi='dm_dit') == ((1, 'fp16x2') if math == 'fp16x2' else (0, 'fp32'))
     assert torch.equal(outs['fp16x2'], outs['fp32'])

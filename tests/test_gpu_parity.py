@@ -277,7 +277,7 @@ def test_conv_math_vs_reference(cuda, golden, report, math):
 def test_fp16x2_range_fallback(cuda, golden):
     """An activation beyond the fp16 range (first conv scaled by 1e5: the skip / shortcut inputs of
     the up path carry ~1e5) makes the fp16x2 forward re-run in bf16x3: the result equals a forward
-    forced to bf16x3, and the model keeps bf16x3."""
+    forced to bf16x3; the model's arithmetic stays fp16x2 (the fallback is per forward)."""
     import dmhip
     _, meta = golden('forward')
     g = torch.Generator().manual_seed(5)
@@ -291,7 +291,8 @@ def test_fp16x2_range_fallback(cuda, golden):
         h = model.native_handle(torch.device(cuda))
         dmhip.unet_conv_math(h, math)
         outs[math] = model(x, t).cpu()
-        assert dmhip.unet_conv_math(h) == 'bf16x3'
+        assert dmhip.unet_conv_math(h) == math
+        assert dmhip.range_stats(h) == ((1, 'fp16x2') if math == 'fp16x2' else (0, 'bf16x3'))
     assert torch.isfinite(outs['bf16x3']).all()
     assert torch.equal(outs['fp16x2'], outs['bf16x3'])
 
@@ -299,7 +300,8 @@ def test_fp16x2_range_fallback(cuda, golden):
 def test_fp16x2_range_fallback_deferred(cuda, golden):
     """Inside DDPM.sample the range flag is polled once per loop (no per-forward host sync): a loop
     whose forwards leave the fp16 range is re-run from the same RNG state in bf16x3, so sample()
-    returns exactly what a model forced to bf16x3 gives (eta > 0: the re-run must replay the noise)."""
+    returns exactly what a model forced to bf16x3 gives (eta > 0: the re-run must replay the noise); after
+    the loop the model runs fp16x2 again."""
     import dmhip
     _, meta = golden('forward')
     outs = {}
@@ -313,9 +315,39 @@ def test_fp16x2_range_fallback_deferred(cuda, golden):
         torch.manual_seed(9)
         init = torch.randn((2, 3, 16, 16), device=cuda)
         outs[math] = d.sample(model, init, tqdm_kwargs=dict(disable=True)).cpu()
-        assert dmhip.unet_conv_math(model.native_handle(torch.device(cuda))) == 'bf16x3'
+        h = model.native_handle(torch.device(cuda))
+        assert dmhip.unet_conv_math(h) == math
+        assert dmhip.range_stats(h) == ((1, 'fp16x2') if math == 'fp16x2' else (0, 'bf16x3'))
     assert torch.isfinite(outs['bf16x3']).all()
     assert torch.equal(outs['fp16x2'], outs['bf16x3'])
+
+
+def test_range_fallback_not_sticky(cuda, golden):
+    """One forward whose input leaves the fp16 range (x * 1e6: the first conv's output ~1e6) runs again in
+    bf16x3 and equals a bf16x3 model's forward bit for bit; the forwards after it run fp16x2 again and equal
+    a fresh fp16x2 model's bit for bit (ref VERDICT r3 item 7: the fallback no longer holds the model at half
+    throughput for the rest of its life). Plans are cached per (shape, arithmetic): one bf16x3 build."""
+    import dmhip
+    _, meta = golden('forward')
+    g = torch.Generator().manual_seed(6)
+    xs = [torch.randn((2, 3, 16, 16), generator=g).to(cuda) for _ in range(3)]
+    t = torch.tensor([30, 800], device=cuda)
+    big = xs[0] * 1e6
+    model, _ = _model(meta, 'tiny', cuda)
+    fresh, _ = _model(meta, 'tiny', cuda)
+    slow, _ = _model(meta, 'tiny', cuda)
+    h = model.native_handle(torch.device(cuda))
+    dmhip.unet_conv_math(slow.native_handle(torch.device(cuda)), 'bf16x3')
+    assert torch.equal(model(xs[1], t), fresh(xs[1], t))
+    out_big = model(big, t)
+    assert torch.isfinite(out_big).all()
+    assert torch.equal(out_big, slow(big, t))
+    assert dmhip.range_stats(h) == (1, 'fp16x2')
+    for x in (xs[1], xs[2], xs[0]):
+        assert torch.equal(model(x, t), fresh(x, t))
+    assert not torch.equal(model(xs[2], t), slow(xs[2], t))   # fp16x2 and bf16x3 differ in the last bits
+    assert dmhip.plan_stats(h) == (2, 2)                       # fp16x2 + bf16x3 plans, both cached
+    assert dmhip.range_stats(h) == (1, 'fp16x2')
 
 
 def test_public_forward_rejects_negative_labels(cuda, golden):

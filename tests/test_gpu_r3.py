@@ -169,7 +169,9 @@ def test_dit_deferred_range_fallback(cuda):
         init = torch.randn((16, 4, 32, 32), device=cuda)
         y = torch.arange(16, device=cuda)
         outs[math] = d.sample(m, init, model_kwargs=dict(y=y), tqdm_kwargs=dict(disable=True)).cpu()
-        assert dmhip.dit_math(m.native_handle(torch.device(cuda))) == 'fp32'
+        h = m.native_handle(torch.device(cuda))
+        assert dmhip.dit_math(h) == math
+        assert dmhip.range_stats(h, abi='dm_dit') == ((1, 'fp16x2') if math == 'fp16x2' else (0, 'fp32'))
     assert torch.isfinite(outs['fp32']).all()
     assert torch.equal(outs['fp16x2'], outs['fp32'])
 
@@ -401,3 +403,60 @@ def test_small_map_conv_vs_splitk(cuda, golden, report, monkeypatch, arch):
     report(f'small_map_conv_{arch}_maxabs_vs_splitk', err)
     assert torch.isfinite(outs['small']).all()
     assert err <= 1e-5, err
+
+
+# ------------------------------------------------------------------ first conv row split
+@pytest.mark.parametrize('dim,size', [(320, 32), (192, 16), (96, 8)])
+def test_first_conv_wide_channels(cuda, dim, size):
+    """The first conv's block covers R = 64 / W rows; with dim / 2 channel pairs not dividing 256 its pixel
+    groups split those rows unevenly (dim 320 at 32^2: one group of 160 lanes, 96 leftover threads; dim 192 at
+    16^2: two groups, 64 leftover). Every row is computed once and no thread writes past its block: a UNet
+    with that first layer matches the oracle (reference models/unet.py:72, 121-152)."""
+    from models.unet import UNet
+    from oracle.unet import OracleUNet
+    arch = dict(dim=dim, dim_mults=[1], use_attn=[False], num_res_blocks=1, n_heads=1, dropout=0.0)
+    m = UNet(**arch).eval()
+    init_synthetic_(m)
+    oracle = OracleUNet(m.state_dict(), **arch)
+    m = m.to(cuda)
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn((2, 3, size, size), generator=g)
+    t = torch.tensor([5, 640])
+    # the output buffer is followed by other plan scratch: a write past the last block would land there
+    out = m(x.to(cuda), t.to(cuda)).cpu()
+    ref = oracle(x, t)
+    err = (out - ref).abs().max().item()
+    assert err <= TOL, err
+    assert torch.equal(m(x.to(cuda), t.to(cuda)).cpu(), out)
+
+
+def test_combined_shared_workspace_two_streams(cuda, golden):
+    """The cond and uncond networks of a UNetCombined share one scratch slab; forwards issued on two different
+    streams without any host sync are ordered by the engine (a forward on a new stream waits for the previous
+    forward over the slab) and equal separate networks' forwards bit for bit."""
+    from models.adm.unet import UNetModel
+    from models.adm.unet_combined import UNetCombined
+    _, meta = golden('adm')
+    arch = meta['archs']['adm_tiny']
+    comb = UNetCombined(**arch).eval()
+    init_synthetic_(comb)
+    sep_c = UNetModel(**arch).eval()
+    sep_u = UNetModel(**dict(arch, num_classes=None)).eval()
+    sep_c.load_state_dict(comb.unet_cond.state_dict())
+    sep_u.load_state_dict(comb.unet_uncond.state_dict())
+    comb, sep_c, sep_u = comb.to(cuda), sep_c.to(cuda), sep_u.to(cuda)
+    gen = torch.Generator().manual_seed(21)
+    y = torch.tensor([1, 4], device=cuda)
+    xs = [torch.randn((2, 3, 16, 16), generator=gen).to(cuda) for _ in range(4)]
+    t = torch.tensor([700, 90], device=cuda)
+    comb(xs[0], t, y), comb(xs[0], t, None)   # plans
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = []
+    for i, x in enumerate(xs):
+        with torch.cuda.stream(s1 if i % 2 == 0 else s2):
+            outs.append((comb(x, t, y), comb(x, t, None)))
+    torch.cuda.synchronize()
+    for x, (oc, ou) in zip(xs, outs):
+        assert torch.equal(oc, sep_c(x, t, y))
+        assert torch.equal(ou, sep_u(x, t, None))
