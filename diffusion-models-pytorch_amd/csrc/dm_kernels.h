@@ -167,6 +167,7 @@ struct GemmArgs {
   // linear_k32 only: the attention operand planes instead of C (as ConvArgs::ap_*, the qkv projection
   // feeding attn_presplit_kernel)
   _Float16 *ap_q, *ap_k, *ap_v;
+  int ap_vonly;   // every column is a v column (the folded attention's g^T plane; ap_q = ap_k = ap_v)
   int ap_L, ap_heads, ap_Dh, ap_legacy;
   float ap_alpha, ap_bscale;
   int ap_ea, ap_eb, ap_ev;
@@ -321,6 +322,28 @@ struct AttnArgs {
 };
 bool attn_fused_ok(int L, int Dh);
 int attn_fused(const AttnArgs& a, hipStream_t st);
+// Folded single-head attention block (attn_block.hip): T = xn At^T + w, S = T xn^T, P = softmax(S),
+// y = x + P g (g^T from a linear_k32 GEMM with the folded Wg = Wp Wv as the v-plane), GroupNorm statistics of y.
+struct AttnBlockArgs {
+  const float* x;               // [B][256][x_pitch] block input (NHWC rows)
+  int x_pitch;
+  const float *gsc, *gsh;       // [B][256] GroupNorm affine of x (gn_finalize)
+  const _Float16* at_img;       // split_conv_weights image of At [256][256] (fp16x2)
+  const float* at_rowscale;     // its row-scale undo (split_conv_rowscale)
+  const float* w;               // [256] T bias
+  const _Float16* g_plane;      // [B][2][256][256] g^T pieces x 2^eg (GemmArgs::ap_v with ap_vonly)
+  float* y;                     // [B][256][y_pitch]
+  int y_pitch;
+  double2* gn_part;             // optional GroupNorm(gn_G) chunk partials of y
+  int gn_G;
+  int B, ex, eg;
+  int* range_flag;
+};
+bool attn_block_ok(int L, int C, int heads);
+// at = s Wk^T Wq, w = s Wk^T bq, wg = Wp Wv, cb = Wp bv + bp (float64 sums, fp32 results)
+int attn_fold(const float* wqkv, const float* bqkv, const float* wproj, const float* bproj, int C, double scale,
+              float* at, float* w, float* wg, float* cb, hipStream_t st);
+int attn_block(const AttnBlockArgs& a, hipStream_t st);
 // Flash attention (attention.hip attn_flash_kernel) on pre-split planes for L % 64 == 0, head dims 8 .. 80:
 // ADM's L = 1024 / 64 blocks, DiT's 72-wide heads. attn_fused dispatches there for shapes it does not take.
 bool attn_flash_ok(int L, int Dh);

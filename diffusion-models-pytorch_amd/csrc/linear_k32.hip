@@ -67,7 +67,11 @@ __device__ __forceinline__ void plane_slab(const GemmArgs& g, const float* st, i
   if (col0 >= g.N) return;
   const int Dh = g.ap_Dh, C = g.ap_heads * Dh;
   int part, h, d0;
-  if (g.ap_legacy) {
+  if (g.ap_vonly) {
+    part = 2;
+    h = col0 / Dh;
+    d0 = col0 - h * Dh;
+  } else if (g.ap_legacy) {
     h = col0 / (3 * Dh);
     part = (col0 - h * 3 * Dh) / Dh;
     d0 = col0 - h * 3 * Dh - part * Dh;
@@ -137,7 +141,11 @@ __device__ __forceinline__ void plane_block(const GemmArgs& g, const float* tile
   const int Dh = g.ap_Dh, C = g.ap_heads * Dh;
   const size_t plane = (size_t)g.ap_L * Dh;
   auto col_map = [&](int col, int& part, int& h, int& d) {
-    if (g.ap_legacy) {
+    if (g.ap_vonly) {
+      part = 2;
+      h = col / Dh;
+      d = col - h * Dh;
+    } else if (g.ap_legacy) {
       h = col / (3 * Dh);
       part = (col - h * 3 * Dh) / Dh;
       d = col - h * 3 * Dh - part * Dh;
@@ -626,6 +634,7 @@ bool linear_k32_ok(const GemmArgs& g) {
   if (g.pro_scale && g.ln_stats) return false;
   if (g.as && (g.pro_scale || g.ln_stats || (reinterpret_cast<uintptr_t>(g.as) & 15) != 0)) return false;
   if (g.c_split && (g.N % 64 != 0 || g.ap_q || (reinterpret_cast<uintptr_t>(g.c_split) & 15) != 0)) return false;
+  if (g.ap_vonly && (!g.ap_q || g.ap_frag || g.ap_legacy)) return false;
   if (g.ap_frag && (!g.ap_q || g.ap_legacy || (g.ap_heads * g.ap_Dh) % 128 != 0 || g.ap_L % 128 != 0 ||
                     g.ap_Dh % 32 != 0))
     return false;

@@ -187,6 +187,16 @@ struct UNetModel {
   std::map<std::pair<const float*, int>, void*> split_w;
   size_t split_bytes = 0;
   void split_for(ConvArgs& c);
+  // folded single-head attention blocks (attn_block.hip): per block's qkv weights, the fp32 products At, w,
+  // Wg, cb and the fp16x2 fragment images of At and Wg, made at the first fp16x2 plan build
+  struct FoldW {
+    float *at = nullptr, *w = nullptr, *wg = nullptr, *cb = nullptr;
+    void *at_img = nullptr, *wg_img = nullptr;
+    const float *at_rs = nullptr, *wg_rs = nullptr;
+  };
+  std::map<size_t, FoldW> folds;
+  std::vector<void*> fold_mem;
+  const FoldW* fold_for(const AttnP& p);
   // fp16x2 GEMMs (attention): operand exponents; weights by max |w| (cached), activations fixed
   std::map<const float*, int> w_exp;
   void split_gemm(GemmArgs& g, int ea, const float* weight, size_t weight_n, int eb_act = 0);
@@ -203,6 +213,7 @@ struct UNetModel {
 
 UNetModel::~UNetModel() {
   plans.clear();
+  for (void* q : fold_mem) (void)hipFree(q);
   if (last_packed) (void)hipFree(last_packed);
   for (auto& kv : split_w) (void)hipFree(kv.second);
   if (range_flag) (void)hipFree(range_flag);
@@ -244,6 +255,43 @@ void UNetModel::split_for(ConvArgs& c) {
     c.ws_rowscale = split_conv_rowscale(p, nmat, c.Cout, c.K);
     c.range_flag = range_flag;
   }
+}
+
+// The folded weights of a single-head attention block (attn_fold, float64 products of the block's own
+// weights) and their fp16x2 images; null if an allocation or launch fails (the block then runs unfolded).
+const UNetModel::FoldW* UNetModel::fold_for(const AttnP& p) {
+  auto it = folds.find(p.wqkv);
+  if (it != folds.end()) return it->second.at ? &it->second : nullptr;  // a failed fold stays failed
+  const int C = p.C;
+  const size_t CC = (size_t)C * C;
+  FoldW f;
+  void* mem = nullptr;
+  const size_t nimg = split_conv_weights_bytes(1, C, C, 2);
+  const size_t nf = (2 * CC + 2 * (size_t)C) * sizeof(float);
+  if (hipMalloc(&mem, nf + 2 * nimg + 64) != hipSuccess) {
+    (void)hipGetLastError();
+    folds[p.wqkv] = FoldW{};  // plan builds stay deterministic: every later build sees the same failure
+    return nullptr;
+  }
+  fold_mem.push_back(mem);
+  char* base = static_cast<char*>(mem);
+  f.at = reinterpret_cast<float*>(base);
+  f.wg = f.at + CC;
+  f.w = f.wg + CC;
+  f.cb = f.w + C;
+  f.at_img = base + ((nf + 15) & ~size_t(15));
+  f.wg_img = static_cast<char*>(f.at_img) + nimg;
+  const double s = (double)p.sa * (p.sb != 0.f ? (double)p.sb : 1.0);
+  if (attn_fold(P(p.wqkv), P(p.bqkv), P(p.wproj), P(p.bproj), C, s, f.at, f.w, f.wg, f.cb, nullptr) != DM_OK ||
+      split_conv_weights(f.at, 1, C, C, C, 1, 2, f.at_img, nullptr) != DM_OK ||
+      split_conv_weights(f.wg, 1, C, C, C, 1, 2, f.wg_img, nullptr) != DM_OK || hipDeviceSynchronize() != hipSuccess) {
+    folds[p.wqkv] = FoldW{};
+    return nullptr;
+  }
+  f.at_rs = split_conv_rowscale(f.at_img, 1, C, C);
+  f.wg_rs = split_conv_rowscale(f.wg_img, 1, C, C);
+  split_bytes += nf + 2 * nimg;
+  return &(folds[p.wqkv] = f);
 }
 
 // fp16x2 attention GEMMs (gemm.hip SPLIT): A scaled by 2^ea, B by the weight's exponent (max |w| *
@@ -994,6 +1042,51 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
       const int C = p.C, heads = p.heads, Dh = C / heads;
       // GroupNorm folded into the QKV projection's A load (modules.py:91-94): one pass over x
       const double2* sta = gn_stats(xin);
+      // One head of 256 channels on a 16 x 16 map (the CIFAR UNet's stage-1 blocks): the folded block
+      // (attn_block.hip): g = GroupNorm(x) Wg^T + cb as the fp16x2 g^T plane (linear_k32, GroupNorm prologue),
+      // then T, S, softmax, P g and the residual in one kernel. DM_ATTN_FOLD=0: the unfolded path below.
+      const FoldW* fw = nullptr;
+      if (conv_math == 2 && arch.variant != 2 && attn_block_ok(hw, C, heads) && y.p != xin.p &&
+          !(std::getenv("DM_ATTN_FOLD") && std::getenv("DM_ATTN_FOLD")[0] == '0'))
+        fw = fold_for(p);
+      if (fw) {
+        GemmArgs gg{};
+        gg.M = B * hw; gg.N = C; gg.K = C; gg.Z1 = 1; gg.Z2 = 1;
+        gg.A = xin.p; gg.lda = xin.pitch; gg.ldc = C; gg.alpha = 1.f;
+        gg.pro_scale = gsc; gg.pro_shift = gsh; gg.pro_rows = hw;
+        gg.split = 2; gg.split_ea = 0; gg.range_flag = range_flag;
+        _Float16* gplane = reinterpret_cast<_Float16*>(qkv);
+        gg.C = qkv;   // unused by the plane epilogue (alignment check only)
+        gg.ap_q = gg.ap_k = gg.ap_v = gplane; gg.ap_vonly = 1;
+        gg.ap_L = hw; gg.ap_heads = 1; gg.ap_Dh = C; gg.ap_ev = 6;
+        gg.Bm = fw->wg; gg.ldb = C; gg.bias = fw->cb;
+        gg.ws = fw->wg_img; gg.ws_rowscale = fw->wg_rs;
+        AttnBlockArgs ab{};
+        ab.x = xin.p; ab.x_pitch = xin.pitch; ab.gsc = gsc; ab.gsh = gsh;
+        ab.at_img = static_cast<const _Float16*>(fw->at_img); ab.at_rowscale = fw->at_rs; ab.w = fw->w;
+        ab.g_plane = gplane; ab.y = y.p; ab.y_pitch = y.pitch; ab.B = B; ab.ex = 6; ab.eg = 6;
+        ab.range_flag = range_flag;
+        if (linear_k32_ok(gg)) {
+          add("gn_finalize", 0, 8.0 * B * C, [=](hipStream_t st) {
+            return gn_finalize(xin, G, sta, 1e-5f, self->P(p.gn.g), self->P(p.gn.b), gsc, gsh, st);
+          });
+          add_gemm(gg);
+          gn_ready.erase(y.p);
+          const int cpg = C / G;
+          if (C % G == 0 && cpg >= 4 && cpg <= 32 && (cpg & (cpg - 1)) == 0) {
+            ab.gn_part = gn_buf_for(y, G);
+            ab.gn_G = G;
+            gn_ready[y.p] = {ab.gn_part, y.C, G};
+          }
+          // T (2 L C^2), S (2 L^2 C), P g (2 L^2 C) per image; x read once for the keys and the queries, y
+          // written, the g^T plane (fp16x2, 4 B per element) read
+          const double fl = 2.0 * B * ((double)hw * C * C + 2.0 * hw * hw * C);
+          const double by = 4.0 * B * hw * C * 3.0;
+          add("attn_block_kernel", fl, by, [=](hipStream_t st) { return attn_block(ab, st); });
+          x_cur = y;
+          continue;
+        }
+      }
       GemmArgs gq{};
       gq.M = B * hw; gq.N = 3 * C; gq.K = C; gq.Z1 = 1; gq.Z2 = 1; gq.pick_M = (long)kPickBatch * hw;
       gq.A = xin.p; gq.lda = xin.pitch; gq.Bm = P(p.wqkv); gq.ldb = C; gq.C = qkv; gq.ldc = 3 * C;

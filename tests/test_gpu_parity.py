@@ -388,6 +388,8 @@ def test_fused_attention_bit_identical(cuda, golden, arch, monkeypatch):
         # the other shapes' flash kernel (AdaGN's 8^2 blocks) is not bit-identical by design: it has its
         # own test against the unfused path (test_gpu_r3.py test_flash_attention_vs_unfused)
         monkeypatch.setenv('DM_ATTN_NO_FLASH', '1')
+        # the unfolded kernels (q / k / v planes); the folded block has its own tests (test_gpu_r4.py)
+        monkeypatch.setenv('DM_ATTN_FOLD', '0')
         if mode == 'unfused':
             monkeypatch.setenv('DM_ATTN_UNFUSED', '1')
         elif mode == 'fused':
