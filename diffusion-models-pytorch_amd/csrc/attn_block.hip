@@ -43,6 +43,30 @@ constexpr int kOP = kBC + 4;        // fp32 pitch of the epilogue staging rows
 
 typedef float fq __attribute__((ext_vector_type(4)));
 
+#ifdef DM_K32_STAMPS
+// Diagnostic build only (tools/ab_stamps.py): per work-group, wave 0's s_memtime at the phase boundaries and
+// s_memrealtime at start / end. Written to this buffer only.
+__device__ unsigned long long g_ab_stamps[4096][10];
+#define AB_STAMP(k)                                                                                      \
+  do {                                                                                                   \
+    __builtin_amdgcn_sched_barrier(0);                                                                   \
+    if (threadIdx.x == 0 && blockIdx.x < 4096) g_ab_stamps[blockIdx.x][k] = __builtin_amdgcn_s_memtime();  \
+    __builtin_amdgcn_sched_barrier(0);                                                                   \
+  } while (0)
+#define AB_RSTAMP(k)                                                                                     \
+  do {                                                                                                   \
+    if (threadIdx.x == 0 && blockIdx.x < 4096) g_ab_stamps[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define AB_STAMP(k) do {} while (0)
+#define AB_RSTAMP(k) do {} while (0)
+#endif
+// DM_AB_ABL (diagnostic builds only, wrong results): 1 no staging refills after the first two k-steps of a
+// phase, 2 no residual loads in the epilogue
+#ifndef DM_AB_ABL
+#define DM_AB_ABL 0
+#endif
+
 // fragment-image offset (fp16 elements) of (row, lane group q, piece p) in a staged k-step, + e0
 __device__ __forceinline__ int img_off(int row, int q, int p) {
   return (q >> 1) * 8192 + (row >> 5) * 1024 + p * 512 + (q & 1) * 256 + (row & 31) * 8;
@@ -73,8 +97,12 @@ __device__ __forceinline__ void mma3(const f16x8 (&a)[2], const f16x8 (&b)[2], f
 }
 
 // One k-step of a 256-row x 32-column contraction: acc[t][qt] += A(tile t) B[qt] over 16 row tiles, the
-// A fragments read from the staged image `img`, one tile ahead of its MFMAs.
-__device__ __forceinline__ void kstep(const _Float16* img, int l16, int q, const f16x8 (&b)[2][2], fq (&acc)[16][2]) {
+// A fragments read from the staged image `img`, one tile ahead of its MFMAs. mid(t) runs after tile t's
+// MFMAs are issued: the staging of later k-steps (global loads, LDS stores into the other image, the
+// GroupNorm + split VALU work) placed between MFMAs, so one wave per SIMD keeps its matrix pipe fed.
+template <class MID>
+__device__ __forceinline__ void kstep(const _Float16* img, int l16, int q, const f16x8 (&b)[2][2], fq (&acc)[16][2],
+                                      MID&& mid) {
   const int base = (q >> 1) * 8192 + (q & 1) * 256 + l16 * 8;
   f16x8 a[2][2];
   auto rd = [&](int t, f16x8 (&dst)[2]) {
@@ -88,6 +116,7 @@ __device__ __forceinline__ void kstep(const _Float16* img, int l16, int q, const
     if (t + 1 < 16) rd(t + 1, a[(t + 1) & 1]);
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) mma3(a[t & 1], b[qt], acc[t][qt]);
+    mid(t);
   }
 }
 
@@ -137,6 +166,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
   __shared__ __attribute__((aligned(16))) float tab[2][kBC];   // GroupNorm scale / shift of the image
   static_assert(2 * kStepH * 2 <= kBQ * kOP * 4, "two k-step images fit the epilogue region");
   _Float16* stg = reinterpret_cast<_Float16*>(lds);
+  AB_RSTAMP(8);
+  AB_STAMP(0);
+#ifdef DM_K32_STAMPS
+  if (threadIdx.x == 0 && blockIdx.x < 4096) g_ab_stamps[blockIdx.x][7] = __smid();
+#endif
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int l16 = lane & 15, q = lane >> 4;
@@ -153,65 +187,46 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
   }
 
   // ------------------------------------------------------------------ staging (8 x 16 B per thread per k-step)
+  // A k-step image is 8 slots of one 16-B load + LDS store per thread; during k-step kk the slots of k-step
+  // kk + 2 are loaded (after tiles 0 .. 7) and those of k-step kk + 1 stored (after tiles 8 .. 15).
   f4 rg[2][8];
   // At image rows (a verbatim copy of the k-step's two 16-slices of split_conv_weights' image)
-  auto load_at = [&](int kk, f4 (&r)[8]) {
-    const f4* src = reinterpret_cast<const f4*>(a.at_img + (size_t)kk * kStepH);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) r[u] = src[t + 256 * u];
+  auto load_at = [&](int kk, int s, f4& r) {
+    r = reinterpret_cast<const f4*>(a.at_img + (size_t)kk * kStepH)[t + 256 * s];
   };
-  auto store_at = [&](int buf, const f4 (&r)[8]) {
-    f4* dst = reinterpret_cast<f4*>(stg + buf * kStepH);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) dst[t + 256 * u] = r[u];
-  };
+  auto store_at = [&](int buf, int s, const f4& r) { reinterpret_cast<f4*>(stg + buf * kStepH)[t + 256 * s] = r; };
   // the keys' x rows, channels 32 ks + 4 u .. + 3 (u = g + 4 hi): lane group g, lanes 8 hi .. + 7 hold 8
-  // consecutive keys; slot s = 0 .. 7 of this wave covers keys 64 wave + 8 s ..
+  // consecutive keys; slot s of this wave covers keys 64 wave + 8 s ..
   const int kg = lane >> 4, khi = (lane >> 3) & 1, kkey = lane & 7;
-  auto load_keys = [&](int ks, f4 (&r)[8]) {
-    const int u = kg + 4 * khi;
-#pragma unroll
-    for (int s = 0; s < 8; ++s)
-      r[s] = *reinterpret_cast<const f4*>(xb + (size_t)(64 * wave + 8 * s + kkey) * a.x_pitch + 32 * ks + 4 * u);
+  const int ku = kg + 4 * khi;
+  auto load_keys = [&](int ks, int s, f4& r) {
+    r = *reinterpret_cast<const f4*>(xb + (size_t)(64 * wave + 8 * s + kkey) * a.x_pitch + 32 * ks + 4 * ku);
   };
-  auto store_keys = [&](int ks, int buf, const f4 (&r)[8]) {
-    const int u = kg + 4 * khi;
-    const int c = 32 * ks + 4 * u;
+  auto store_keys = [&](int ks, int buf, int s, const f4& r) {
+    const int c = 32 * ks + 4 * ku;
     const f4 sc = *reinterpret_cast<const f4*>(&tab[0][c]), sh = *reinterpret_cast<const f4*>(&tab[1][c]);
-    _Float16* img = stg + buf * kStepH;
+    f4 v = r;
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      f4 v = r[s];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = (v[e] * sc[e] + sh[e]) * xs;
-      bad |= fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))) > 65504.f;
-      f16x4 hi, lo;
-      split4(v, hi, lo);
-      const int key = 64 * wave + 8 * s + kkey;
-      const int o = img_off(key, kg, 0) + 4 * khi;
-      *reinterpret_cast<f16x4*>(img + o) = hi;
-      *reinterpret_cast<f16x4*>(img + o + 512) = lo;
-    }
+    for (int e = 0; e < 4; ++e) v[e] = (v[e] * sc[e] + sh[e]) * xs;
+    bad |= fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))) > 65504.f;
+    f16x4 hi, lo;
+    split4(v, hi, lo);
+    _Float16* dst = stg + buf * kStepH + img_off(64 * wave + 8 * s + kkey, kg, 0) + 4 * khi;
+    *reinterpret_cast<f16x4*>(dst) = hi;
+    *reinterpret_cast<f16x4*>(dst + 512) = lo;
   };
   // g^T rows d (the v-plane [2][C][L] of this image), keys 32 ks + 8 u' .. + 7 (u' = 2 hi + g1, piece g0)
   const _Float16* gb = a.g_plane + (size_t)b * 2 * kBC * kBL;
   const int gu = 2 * khi + (kg & 1), gp = kg >> 1;
-  auto load_g = [&](int ks, f4 (&r)[8]) {
-#pragma unroll
-    for (int s = 0; s < 8; ++s)
-      r[s] = *reinterpret_cast<const f4*>(gb + ((size_t)gp * kBC + 64 * wave + 8 * s + kkey) * kBL + 32 * ks + 8 * gu);
+  auto load_g = [&](int ks, int s, f4& r) {
+    r = *reinterpret_cast<const f4*>(gb + ((size_t)gp * kBC + 64 * wave + 8 * s + kkey) * kBL + 32 * ks + 8 * gu);
   };
-  auto store_g = [&](int buf, const f4 (&r)[8]) {
+  auto store_g = [&](int buf, int s, const f4& r) {
     // keys 8 u' .. + 3 -> lane group 2 (u' & 1), e0 = 4 (u' >> 1); keys 8 u' + 4 .. + 7 -> lane group + 1
     _Float16* img = stg + buf * kStepH;
-    const int q0 = 2 * (gu & 1), e0 = 4 * (gu >> 1);
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const int d = 64 * wave + 8 * s + kkey;
-      const f4 v = r[s];
-      *reinterpret_cast<float2*>(img + img_off(d, q0, gp) + e0) = make_float2(v[0], v[1]);
-      *reinterpret_cast<float2*>(img + img_off(d, q0 + 1, gp) + e0) = make_float2(v[2], v[3]);
-    }
+    const int q0 = 2 * (gu & 1), e0 = 4 * (gu >> 1), d = 64 * wave + 8 * s + kkey;
+    *reinterpret_cast<float2*>(img + img_off(d, q0, gp) + e0) = make_float2(r[0], r[1]);
+    *reinterpret_cast<float2*>(img + img_off(d, q0 + 1, gp) + e0) = make_float2(r[2], r[3]);
   };
 
   fq acc[16][2];
@@ -254,25 +269,37 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
   };
 
   zero_acc();
-  load_at(0, rg[0]);
-  load_at(1, rg[1]);
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    load_at(0, u, rg[0][u]);
+    load_at(1, u, rg[1][u]);
+  }
   load_xq(0, rx[0]);
   load_xq(1, rx[1]);
-  store_at(0, rg[0]);
+#pragma unroll
+  for (int u = 0; u < 8; ++u) store_at(0, u, rg[0][u]);
   __syncthreads();   // tab and the first image
 #pragma unroll
   for (int kk = 0; kk < 8; ++kk) {
-    if (kk + 2 < 8) load_at(kk + 2, rg[kk & 1]);
     f16x8 bf[2][2];
     xq_frag(kk, rx[kk & 1], bf);
-    if (kk + 2 < 8) load_xq(kk + 2, rx[kk & 1]);
-    kstep(stg + (kk & 1) * kStepH, l16, q, bf, acc);
-    if (kk + 1 < 8) store_at((kk + 1) & 1, rg[(kk + 1) & 1]);
+    if (kk + 2 < 8 && DM_AB_ABL != 1) load_xq(kk + 2, rx[kk & 1]);
+    kstep(stg + (kk & 1) * kStepH, l16, q, bf, acc, [&](int tt) {
+      if (tt < 8) {
+        if (kk + 2 < 8 && DM_AB_ABL != 1) load_at(kk + 2, tt, rg[kk & 1][tt]);
+      } else if (kk + 1 < 8) {
+        store_at((kk + 1) & 1, tt - 8, rg[(kk + 1) & 1][tt - 8]);
+      }
+    });
     __syncthreads();
   }
+  AB_STAMP(1);
   // keys' rows for the S contraction: first two k-steps in flight during the T epilogue
-  load_keys(0, rg[0]);
-  load_keys(1, rg[1]);
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    load_keys(0, u, rg[0][u]);
+    load_keys(1, u, rg[1][u]);
+  }
 
   // T = acc * rowscale * 2^-ex + w; per query the exponent eT with max |T| 2^eT in [2^13, 2^14)
   f16x8 tp[8][2][2];   // [k-step][qt][piece]: T's split pieces as the S contraction's B operand
@@ -315,19 +342,29 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     }
   }
 
+  AB_STAMP(2);
   // ------------------------------------------------------------------ 2. S^T = xn_keys T^T
-  store_keys(0, 0, rg[0]);
+#pragma unroll
+  for (int u = 0; u < 8; ++u) store_keys(0, 0, u, rg[0][u]);
   __syncthreads();
   zero_acc();
 #pragma unroll
   for (int ks = 0; ks < 8; ++ks) {
-    if (ks + 2 < 8) load_keys(ks + 2, rg[ks & 1]);
-    kstep(stg + (ks & 1) * kStepH, l16, q, tp[ks], acc);
-    if (ks + 1 < 8) store_keys(ks + 1, (ks + 1) & 1, rg[(ks + 1) & 1]);
+    kstep(stg + (ks & 1) * kStepH, l16, q, tp[ks], acc, [&](int tt) {
+      if (tt < 8) {
+        if (ks + 2 < 8 && DM_AB_ABL != 1) load_keys(ks + 2, tt, rg[ks & 1][tt]);
+      } else if (ks + 1 < 8) {
+        store_keys(ks + 1, (ks + 1) & 1, tt - 8, rg[(ks + 1) & 1][tt - 8]);
+      }
+    });
     __syncthreads();
   }
-  load_g(0, rg[0]);
-  load_g(1, rg[1]);
+  AB_STAMP(3);
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    load_g(0, u, rg[0][u]);
+    load_g(1, u, rg[1][u]);
+  }
 
   // ------------------------------------------------------------------ 3. softmax over the keys (per query lane)
   // S = acc 2^-(ex + eT); p = exp2(S log2 e - max) on the hardware exp2 (scale folded into one FMA), P = p / sum
@@ -367,18 +404,42 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     }
   }
 
+  AB_STAMP(4);
   // ------------------------------------------------------------------ 4. O^T = g^T P^T
-  store_g(0, rg[0]);
+#pragma unroll
+  for (int u = 0; u < 8; ++u) store_g(0, u, rg[0][u]);
   __syncthreads();
   zero_acc();
+  // epilogue slice of this wave: 64-row chunk ch, 128-column half chalf; lane = 4 channels of rows 2 i + rsub.
+  // The residual rows are loaded during the last two k-steps (slots free there) and right after the loop.
+  const int ch = wave >> 1, chalf = wave & 1;
+  const int c4 = lane & 31, rsub = lane >> 5;
+  const int col = 128 * chalf + 4 * c4;
+  const int tok0 = qh * kBQ + 64 * ch;
+  auto load_res = [&](int i, f4& r) {
+    r = DM_AB_ABL == 2 ? f4{0.f, 0.f, 0.f, 0.f}
+                       : *reinterpret_cast<const f4*>(xb + (size_t)(tok0 + 2 * i + rsub) * a.x_pitch + col);
+  };
 #pragma unroll
   for (int ks = 0; ks < 8; ++ks) {
-    if (ks + 2 < 8) load_g(ks + 2, rg[ks & 1]);
-    kstep(stg + (ks & 1) * kStepH, l16, q, pp[ks], acc);
-    if (ks + 1 < 8) store_g((ks + 1) & 1, rg[(ks + 1) & 1]);
+    kstep(stg + (ks & 1) * kStepH, l16, q, pp[ks], acc, [&](int tt) {
+      if (tt < 8) {
+        if (ks + 2 < 8) {
+          if (DM_AB_ABL != 1) load_g(ks + 2, tt, rg[ks & 1][tt]);
+        } else {
+          load_res(8 * (ks - 6) + tt, rg[ks & 1][tt]);   // residual rows 0 .. 15
+        }
+      } else if (ks + 1 < 8) {
+        store_g((ks + 1) & 1, tt - 8, rg[(ks + 1) & 1][tt - 8]);
+      }
+    });
     __syncthreads();
   }
+  f4 xr2[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) load_res(16 + i, xr2[i]);
   if (bad && a.range_flag) *a.range_flag = 1;
+  AB_STAMP(5);
 
   // ------------------------------------------------------------------ 5. y = x + O, GroupNorm statistics
   // O rows to LDS ([128 queries][C] fp32): lane (l16, q) holds d = 16 dt + 4 q .. + 3 of query 16 qt + l16
@@ -389,18 +450,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     for (int qt = 0; qt < 2; ++qt)
       *reinterpret_cast<fq*>(lds + (wave * 32 + 16 * qt + l16) * kOP + 16 * dt + 4 * q) = acc[dt][qt] * oun;
   __syncthreads();
-  // wave (chunk c = 64 rows, column half h): lane = 4 channels of one row, two rows per pass
-  const int ch = wave >> 1, chalf = wave & 1;
-  const int c4 = lane & 31, rsub = lane >> 5;
-  const int col = 128 * chalf + 4 * c4;
-  const int tok0 = qh * kBQ + 64 * ch;
   double gs[4] = {0.0, 0.0, 0.0, 0.0}, gq[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll 4
+#pragma unroll
   for (int i = 0; i < 32; ++i) {
-    const int row = 64 * ch + 2 * i + rsub;          // work-group-local query row
     const int tok = tok0 + 2 * i + rsub;
-    const f4 o = *reinterpret_cast<const f4*>(lds + row * kOP + col);
-    const f4 xr = *reinterpret_cast<const f4*>(xb + (size_t)tok * a.x_pitch + col);
+    const f4 o = *reinterpret_cast<const f4*>(lds + (64 * ch + 2 * i + rsub) * kOP + col);
+    const f4 xr = i < 8 ? rg[0][i & 7] : i < 16 ? rg[1][i & 7] : xr2[i & 15];
     const f4 yv = xr + o;
     *reinterpret_cast<f4*>(a.y + ((size_t)b * kBL + tok) * a.y_pitch + col) = yv;
 #pragma unroll
@@ -421,9 +476,396 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     if (rsub == 0 && (c4 % (cpg / 4)) == 0)
       a.gn_part[((size_t)b * (kBL / 64) + (tok0 >> 6)) * a.gn_G + col / cpg] = make_double2(s, qq);
   }
+  AB_STAMP(6);
+  AB_RSTAMP(9);
+}
+
+// ======================================================================================================
+// Variant 3 (default): no g GEMM. The values are xn itself and the folded projection comes after:
+//   y_i = x_i + Wg (sum_j P_ij xn_j) + cb        (sum_j P_ij = 1)
+// so per work-group: T (At xn_q^T), then ONE pass over the keys in chunks of 32 -- S^T for the chunk, an
+// online softmax update (running maximum / sum per query, the O accumulators rescaled), O^T += xn_K^T P^T --
+// then Y^T = Wg' O^T and the residual. Per image and query half 4 GEMMs of 128 x 256 x 256 (T, S, P xn, Wg O):
+// the g GEMM kernel and its fp16x2 plane (67 MB written, read twice at B = 256) are gone, and the keys' x rows
+// are staged once for S and P xn together.
+//
+// The keys' chunk image holds 32 keys x 256 channels (two fp16 pieces, 544-B rows: conflict-free for both
+// the 16x16x32 A-operand row reads of S and the ds_read_b64_tr_b16 transposed reads of P xn). Its channel
+// order is the accumulator permutation pi within every 32 channels (storage position 32 g + 8 q + e holds
+// channel 32 g + 4 q + (e & 3) + 16 (e >> 2)), so T's accumulators are S's B operand as they lie; O^T's rows
+// come out in storage order, and Wg' = Wg with its columns permuted by pi o pi within 32-groups (made at the
+// fold) takes them as they lie as the B operand of the projection.
+constexpr int kKP = 272;            // fp16 pitch of a key row of one piece (544 B = 136 dwords: 8 mod 64)
+constexpr int kKPiece = 32 * kKP;   // one piece of a key-chunk image
+constexpr int kKImg = 2 * kKPiece;  // fp16 elements of a key-chunk image (34 KB)
+
+typedef _Float16 f16x4_t __attribute__((ext_vector_type(4)));
+
+// ds_read_b64_tr_b16 (gfx950): lane 4 q' + p of each 16-lane group addresses row q' of a 4-row block, columns
+// 4 p .. 4 p + 3; lane i of the group receives column i of the 4 rows (cdna_hip_programming.md T10)
+__device__ __forceinline__ f16x4_t lds_tr16(const _Float16* p) {
+  typedef __fp16 hv4 __attribute__((__vector_size__(4 * sizeof(__fp16))));
+  typedef __attribute__((address_space(3))) hv4 lds_hv4;
+  const hv4 r = __builtin_amdgcn_ds_read_tr16_b64_v4f16((lds_hv4*)(p));
+  return __builtin_bit_cast(f16x4_t, r);
+}
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) attn_block3_kernel(AttnBlockArgs a) {
+  __shared__ __attribute__((aligned(16))) float lds[kBQ * kOP];
+  __shared__ __attribute__((aligned(16))) float tab[2][kBC];
+  static_assert(2 * kKImg * 2 <= kBQ * kOP * 4, "two key-chunk images fit the epilogue region");
+  _Float16* stg = reinterpret_cast<_Float16*>(lds);
+  AB_RSTAMP(8);
+  AB_STAMP(0);
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int l16 = lane & 15, q = lane >> 4;
+  const int bid = xcd_remap_p(blockIdx.x, gridDim.x);
+  const int b = bid >> 1, qh = bid & 1;
+  const float* xb = a.x + (size_t)b * kBL * a.x_pitch;
+  const int qrow0 = qh * kBQ + wave * 32;
+  const float xs = ldexpf(1.f, a.ex);
+  bool bad = false;
+  for (int i = t; i < kBC; i += 256) {
+    tab[0][i] = a.gsc[(size_t)b * kBC + i];
+    tab[1][i] = a.gsh[(size_t)b * kBC + i];
+  }
+
+  f4 rg[2][8];
+  // weight images (At, Wg'): verbatim copies of split_conv_weights' k-step regions
+  auto load_w = [&](const _Float16* img, int kk, int s, f4& r) {
+    r = reinterpret_cast<const f4*>(img + (size_t)kk * kStepH)[t + 256 * s];
+  };
+  auto store_w = [&](int buf, int s, const f4& r) { reinterpret_cast<f4*>(stg + buf * kStepH)[t + 256 * s] = r; };
+  // key chunk kc = keys 32 kc .. + 31, all channels. Slot s = 32-channel group s; lane: run krun of 4 channels,
+  // key kkey3 (a 16-lane group covers keys {k0, k0 + 2} x 8 runs: conflict-free 8-B LDS stores; a wave
+  // instruction reads 8 whole 128-B row pieces)
+  const int krun = lane & 7, kk2 = (lane >> 3) & 1, kgrp = lane >> 4;
+  const int kkey3 = 8 * wave + 4 * (kgrp >> 1) + 2 * kk2 + (kgrp & 1);   // 0 .. 31 within the chunk
+  auto load_k = [&](int kc, int s, f4& r) {
+    r = *reinterpret_cast<const f4*>(xb + (size_t)(32 * kc + kkey3) * a.x_pitch + 32 * s + 4 * krun);
+  };
+  auto store_k = [&](int buf, int s, const f4& r) {
+    const int c = 32 * s + 4 * krun;
+    const f4 sc = *reinterpret_cast<const f4*>(&tab[0][c]), sh = *reinterpret_cast<const f4*>(&tab[1][c]);
+    f4 v = r;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = (v[e] * sc[e] + sh[e]) * xs;
+    bad |= fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))) > 65504.f;
+    f16x4 hi, lo;
+    split4(v, hi, lo);
+    // channels 4 krun .. + 3 of the 32-group -> storage positions 8 (krun & 3) + 4 (krun >> 2) ..
+    _Float16* dst = stg + buf * kKImg + kkey3 * kKP + 32 * s + 8 * (krun & 3) + 4 * (krun >> 2);
+    *reinterpret_cast<f16x4*>(dst) = hi;
+    *reinterpret_cast<f16x4*>(dst + kKPiece) = lo;
+  };
+
+  fq acc[16][2];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = fq{0.f, 0.f, 0.f, 0.f};
+  };
+
+  // ------------------------------------------------------------------ 1. T^T = At xn_q^T (+ w)
+  f4 rx[2][2][2];
+  auto load_xq = [&](int kk, f4 (&r)[2][2]) {
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const float* p = xb + (size_t)(qrow0 + 16 * qt + l16) * a.x_pitch + 32 * kk + 8 * q;
+      r[qt][0] = *reinterpret_cast<const f4*>(p);
+      r[qt][1] = *reinterpret_cast<const f4*>(p + 4);
+    }
+  };
+  auto xq_frag = [&](int kk, const f4 (&r)[2][2], f16x8 (&bf)[2][2]) {
+    const int c = 32 * kk + 8 * q;
+    const f4 s0 = *reinterpret_cast<const f4*>(&tab[0][c]), s1 = *reinterpret_cast<const f4*>(&tab[0][c + 4]);
+    const f4 h0 = *reinterpret_cast<const f4*>(&tab[1][c]), h1 = *reinterpret_cast<const f4*>(&tab[1][c + 4]);
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = (r[qt][0][e] * s0[e] + h0[e]) * xs;
+        v[4 + e] = (r[qt][1][e] * s1[e] + h1[e]) * xs;
+      }
+      float m = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(v[e]));
+      bad |= m > 65504.f;
+      split8(v, bf[qt][0], bf[qt][1]);
+    }
+  };
+  zero_acc();
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    load_w(a.at_img, 0, u, rg[0][u]);
+    load_w(a.at_img, 1, u, rg[1][u]);
+  }
+  load_xq(0, rx[0]);
+  load_xq(1, rx[1]);
+#pragma unroll
+  for (int u = 0; u < 8; ++u) store_w(0, u, rg[0][u]);
+  __syncthreads();
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) {
+    f16x8 bf[2][2];
+    xq_frag(kk, rx[kk & 1], bf);
+    if (kk + 2 < 8) load_xq(kk + 2, rx[kk & 1]);
+    kstep(stg + (kk & 1) * kStepH, l16, q, bf, acc, [&](int tt) {
+      if (tt < 8) {
+        if (kk + 2 < 8) load_w(a.at_img, kk + 2, tt, rg[kk & 1][tt]);
+      } else if (kk + 1 < 8) {
+        store_w((kk + 1) & 1, tt - 8, rg[(kk + 1) & 1][tt - 8]);
+      }
+    });
+    __syncthreads();
+  }
+  AB_STAMP(1);
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    load_k(0, u, rg[0][u]);
+    load_k(1, u, rg[1][u]);
+  }
+  f16x8 tp[8][2][2];
+  float tun[2];
+  {
+    const float xun = ldexpf(1.f, -a.ex);
+    float mx[2] = {0.f, 0.f};
+#pragma unroll
+    for (int ct = 0; ct < 16; ++ct) {
+      const f4 rs = *reinterpret_cast<const f4*>(a.at_rowscale + 16 * ct + 4 * q);
+      const f4 wv = *reinterpret_cast<const f4*>(a.w + 16 * ct + 4 * q);
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = acc[ct][qt][r] * (rs[r] * xun) + wv[r];
+          acc[ct][qt][r] = v;
+          mx[qt] = fmaxf(mx[qt], fabsf(v));
+        }
+    }
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      float m = fmaxf(mx[qt], __shfl_xor(mx[qt], 16));
+      m = fmaxf(m, __shfl_xor(m, 32));
+      int E = 0;
+      (void)frexpf(m, &E);
+      const int eT = m > 0.f ? 14 - E : 0;
+      const float sc = ldexpf(1.f, eT);
+      tun[qt] = ldexpf(1.f, -(a.ex + eT));
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = acc[2 * ks][qt][e] * sc;
+          v[4 + e] = acc[2 * ks + 1][qt][e] * sc;
+        }
+        split8(v, tp[ks][qt][0], tp[ks][qt][1]);
+      }
+    }
+  }
+  AB_STAMP(2);
+
+  // ------------------------------------------------------------------ 2. one pass over the keys (chunks of 32)
+  // S^T chunk [2 key tiles][qt] = xn_chunk T^T; online softmax; O^T [16 storage tiles][qt] += xn_chunk^T P^T
+#pragma unroll
+  for (int u = 0; u < 8; ++u) store_k(0, u, rg[0][u]);
+  __syncthreads();
+  zero_acc();   // O^T accumulators
+  float m_run[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
+  const float sl2[2] = {tun[0] * 1.4426950408889634f, tun[1] * 1.4426950408889634f};
+#pragma unroll
+  for (int kc = 0; kc < 8; ++kc) {
+    const _Float16* img = stg + (kc & 1) * kKImg;
+    // S^T: A = the chunk's key rows (tile kt: keys 16 kt + l16), k = storage positions 32 ks + 8 q ..
+    fq sacc[2][2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) sacc[kt][qt] = fq{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        const _Float16* pr = img + (16 * kt + l16) * kKP + 32 * ks + 8 * q;
+        f16x8 av[2];
+        av[0] = *reinterpret_cast<const f16x8*>(pr);
+        av[1] = *reinterpret_cast<const f16x8*>(pr + kKPiece);
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) mma3(av, tp[ks][qt], sacc[kt][qt]);
+      }
+      // staging between the S MFMAs: the loads of chunk kc + 2 (this thread's slots)
+      if (kc + 2 < 8) load_k(kc + 2, ks, rg[kc & 1][ks]);
+    }
+    // online softmax of the chunk (per query lane; the 4 lane groups q hold 8 of its 32 keys each)
+    f16x8 pp[2][2];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      float mx = fmaxf(fmaxf(fmaxf(sacc[0][qt][0], sacc[0][qt][1]), fmaxf(sacc[0][qt][2], sacc[0][qt][3])),
+                       fmaxf(fmaxf(sacc[1][qt][0], sacc[1][qt][1]), fmaxf(sacc[1][qt][2], sacc[1][qt][3])));
+      mx = fmaxf(mx, __shfl_xor(mx, 16));
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      const float m_new = fmaxf(m_run[qt], mx * sl2[qt]);
+      const float corr = __builtin_amdgcn_exp2f(m_run[qt] - m_new);
+      m_run[qt] = m_new;
+      float ls = 0.f, v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[0][qt][e], sl2[qt], -m_new));
+        v[4 + e] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[1][qt][e], sl2[qt], -m_new));
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        ls += v[e];
+        v[e] *= 16384.f;
+      }
+      l_run[qt] = l_run[qt] * corr + ls;
+      split8(v, pp[qt][0], pp[qt][1]);
+      if (kc > 0) {
+#pragma unroll
+        for (int ot = 0; ot < 16; ++ot) acc[ot][qt] *= corr;
+      }
+    }
+    // O^T += xn_chunk^T P^T: A rows = storage positions 16 ot + l16 (transposed reads of the key rows), k = the
+    // chunk's keys in P's accumulator permutation (lane group q: keys 4 q .. + 3, then 16 + 4 q .. + 3)
+    {
+      const _Float16* pt = img + (4 * q + (l16 >> 2)) * kKP + 4 * (l16 & 3);
+#pragma unroll
+      for (int ot = 0; ot < 16; ++ot) {
+        f16x8 av[2];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const f16x4_t lo4 = lds_tr16(pt + p * kKPiece + 16 * ot);
+          const f16x4_t hi4 = lds_tr16(pt + p * kKPiece + 16 * kKP + 16 * ot);
+          av[p] = f16x8{lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+        }
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) mma3(av, pp[qt], acc[ot][qt]);
+        // the stores of chunk kc + 1 (into the other image) between the P xn MFMAs
+        if (ot >= 8 && kc + 1 < 8) store_k((kc + 1) & 1, ot - 8, rg[(kc + 1) & 1][ot - 8]);
+      }
+    }
+    __syncthreads();
+  }
+  AB_STAMP(3);
+  // Wg' images of the projection: the first two k-steps in flight during the O finalize
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    load_w(a.wg_img, 0, u, rg[0][u]);
+    load_w(a.wg_img, 1, u, rg[1][u]);
+  }
+  // O = acc / (2^14 l) (rows in storage order) -> split pieces x 2^ex as the projection's B operand
+  f16x8 op[8][2][2];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    float l = l_run[qt] + __shfl_xor(l_run[qt], 16);
+    l += __shfl_xor(l, 32);
+    const float sc = xs / (16384.f * l);
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = acc[2 * ks][qt][e] * sc;
+        v[4 + e] = acc[2 * ks + 1][qt][e] * sc;
+      }
+      split8(v, op[ks][qt][0], op[ks][qt][1]);
+    }
+  }
+  AB_STAMP(4);
+
+  // ------------------------------------------------------------------ 3. Y^T = Wg' O^T
+#pragma unroll
+  for (int u = 0; u < 8; ++u) store_w(0, u, rg[0][u]);
+  __syncthreads();
+  zero_acc();
+  const int ch = wave >> 1, chalf = wave & 1;
+  const int c4 = lane & 31, rsub = lane >> 5;
+  const int col = 128 * chalf + 4 * c4;
+  const int tok0 = qh * kBQ + 64 * ch;
+  auto load_res = [&](int i, f4& r) {
+    r = *reinterpret_cast<const f4*>(xb + (size_t)(tok0 + 2 * i + rsub) * a.x_pitch + col);
+  };
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) {
+    kstep(stg + (kk & 1) * kStepH, l16, q, op[kk], acc, [&](int tt) {
+      if (tt < 8) {
+        if (kk + 2 < 8) load_w(a.wg_img, kk + 2, tt, rg[kk & 1][tt]);
+        else load_res(8 * (kk - 6) + tt, rg[kk & 1][tt]);   // residual rows 0 .. 15
+      } else if (kk + 1 < 8) {
+        store_w((kk + 1) & 1, tt - 8, rg[(kk + 1) & 1][tt - 8]);
+      }
+    });
+    __syncthreads();
+  }
+  f4 xr2[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) load_res(16 + i, xr2[i]);
+  if (bad && a.range_flag) *a.range_flag = 1;
+  AB_STAMP(5);
+
+  // ------------------------------------------------------------------ 4. y = x + Y + cb, GroupNorm statistics
+  const float yun = ldexpf(1.f, -a.ex);
+#pragma unroll
+  for (int dt = 0; dt < 16; ++dt) {
+    const f4 rs = *reinterpret_cast<const f4*>(a.wg_rowscale + 16 * dt + 4 * q);
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+      *reinterpret_cast<fq*>(lds + (wave * 32 + 16 * qt + l16) * kOP + 16 * dt + 4 * q) = acc[dt][qt] * (rs * yun);
+  }
+  __syncthreads();
+  const f4 cb4 = *reinterpret_cast<const f4*>(a.cb + col);
+  double gs[4] = {0.0, 0.0, 0.0, 0.0}, gq[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    const int tok = tok0 + 2 * i + rsub;
+    const f4 o = *reinterpret_cast<const f4*>(lds + (64 * ch + 2 * i + rsub) * kOP + col);
+    const f4 xr = i < 8 ? rg[0][i & 7] : i < 16 ? rg[1][i & 7] : xr2[i & 15];
+    const f4 yv = xr + (o + cb4);
+    *reinterpret_cast<f4*>(a.y + ((size_t)b * kBL + tok) * a.y_pitch + col) = yv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      gs[e] += (double)yv[e];
+      gq[e] += (double)yv[e] * yv[e];
+    }
+  }
+  if (a.gn_part) {
+    double s = gs[0] + gs[1] + gs[2] + gs[3], qq = gq[0] + gq[1] + gq[2] + gq[3];
+    s += __shfl_xor(s, 32);
+    qq += __shfl_xor(qq, 32);
+    const int cpg = kBC / a.gn_G;
+    for (int o = 1; o < cpg / 4; o <<= 1) {
+      s += __shfl_xor(s, o);
+      qq += __shfl_xor(qq, o);
+    }
+    if (rsub == 0 && (c4 % (cpg / 4)) == 0)
+      a.gn_part[((size_t)b * (kBL / 64) + (tok0 >> 6)) * a.gn_G + col / cpg] = make_double2(s, qq);
+  }
+  AB_STAMP(6);
+  AB_RSTAMP(9);
+}
+
+__device__ __forceinline__ int pi32(int m) { return 4 * (m >> 3) + (m & 3) + 16 * ((m >> 2) & 1); }
+
+// Wg' = Wg with its columns permuted by pi o pi within every 32 columns (attn_block3_kernel's projection)
+__global__ void attn_perm_cols_kernel(const float* __restrict__ wg, float* __restrict__ wgp, int C) {
+  const long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= (long)C * C) return;
+  const int d = (int)(id / C), k = (int)(id % C);
+  wgp[id] = wg[(size_t)d * C + (k & ~31) + pi32(pi32(k & 31))];
 }
 
 }  // namespace
+
+#ifdef DM_K32_STAMPS
+extern "C" int dm_debug_ab_stamps(void* host, int nblocks) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ab_stamps), (size_t)nblocks * 10 * sizeof(unsigned long long)) ==
+                 hipSuccess ? 0 : -2;
+}
+#endif
 
 bool attn_block_ok(int L, int C, int heads) { return L == kBL && C == kBC && heads == 1; }
 
@@ -437,17 +879,31 @@ int attn_fold(const float* wqkv, const float* bqkv, const float* wproj, const fl
   return DM_OK;
 }
 
+int attn_perm_cols(const float* wg, float* wgp, int C, hipStream_t st) {
+  DM_REQUIRE(wg && wgp && C % 32 == 0, "attention fold: column permutation needs C % 32 == 0");
+  const long n = (long)C * C;
+  hipLaunchKernelGGL(attn_perm_cols_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, wg, wgp, C);
+  DM_LAUNCH_CHECK();
+  return DM_OK;
+}
+
 int attn_block(const AttnBlockArgs& a, hipStream_t st) {
   auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-  DM_REQUIRE(a.B > 0 && a.x && a.y && a.gsc && a.gsh && a.at_img && a.at_rowscale && a.w && a.g_plane,
+  DM_REQUIRE(a.variant == 2 || a.variant == 3, "attention block: variant 2 or 3");
+  DM_REQUIRE(a.B > 0 && a.x && a.y && a.gsc && a.gsh && a.at_img && a.at_rowscale && a.w &&
+                 (a.variant == 2 ? a.g_plane != nullptr : (a.wg_img && a.wg_rowscale && a.cb)),
              "attention block: null argument");
   DM_REQUIRE(a.x_pitch % 4 == 0 && a.y_pitch % 4 == 0 && al16(a.x) && al16(a.y) && al16(a.gsc) && al16(a.gsh) &&
-                 al16(a.at_img) && al16(a.at_rowscale) && al16(a.w) && al16(a.g_plane),
+                 al16(a.at_img) && al16(a.at_rowscale) && al16(a.w) &&
+                 (a.variant == 2 ? al16(a.g_plane) : (al16(a.wg_img) && al16(a.wg_rowscale) && al16(a.cb))),
              "attention block: 16-byte aligned rows");
   DM_REQUIRE(!a.gn_part || (a.gn_G > 0 && kBC % a.gn_G == 0 && kBC / a.gn_G >= 4 && kBC / a.gn_G <= 32 &&
                             ((kBC / a.gn_G) & (kBC / a.gn_G - 1)) == 0),
              "attention block: GroupNorm statistics need groups of 4, 8, 16 or 32 channels");
-  hipLaunchKernelGGL(attn_block_kernel, dim3(a.B * (kBL / kBQ)), dim3(256), 0, st, a);
+  if (a.variant == 3)
+    hipLaunchKernelGGL(attn_block3_kernel, dim3(a.B * (kBL / kBQ)), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL(attn_block_kernel, dim3(a.B * (kBL / kBQ)), dim3(256), 0, st, a);
   DM_LAUNCH_CHECK();
   return DM_OK;
 }

@@ -331,7 +331,11 @@ struct AttnBlockArgs {
   const _Float16* at_img;       // split_conv_weights image of At [256][256] (fp16x2)
   const float* at_rowscale;     // its row-scale undo (split_conv_rowscale)
   const float* w;               // [256] T bias
-  const _Float16* g_plane;      // [B][2][256][256] g^T pieces x 2^eg (GemmArgs::ap_v with ap_vonly)
+  const _Float16* g_plane;      // variant 2: [B][2][256][256] g^T pieces x 2^eg (GemmArgs::ap_v with ap_vonly)
+  const _Float16* wg_img;       // variant 3: split_conv_weights image of Wg' (Wg, columns permuted: attn_perm_cols)
+  const float* wg_rowscale;
+  const float* cb;              // variant 3: [256] output bias Wp bv + bp
+  int variant;                  // 2: g from the linear_k32 plane; 3 (default): values = xn, Wg' after
   float* y;                     // [B][256][y_pitch]
   int y_pitch;
   double2* gn_part;             // optional GroupNorm(gn_G) chunk partials of y
@@ -344,6 +348,8 @@ bool attn_block_ok(int L, int C, int heads);
 int attn_fold(const float* wqkv, const float* bqkv, const float* wproj, const float* bproj, int C, double scale,
               float* at, float* w, float* wg, float* cb, hipStream_t st);
 int attn_block(const AttnBlockArgs& a, hipStream_t st);
+// wgp = wg with its columns permuted within 32-groups as attn_block variant 3 reads its projection operand
+int attn_perm_cols(const float* wg, float* wgp, int C, hipStream_t st);
 // Flash attention (attention.hip attn_flash_kernel) on pre-split planes for L % 64 == 0, head dims 8 .. 80:
 // ADM's L = 1024 / 64 blocks, DiT's 72-wide heads. attn_fused dispatches there for shapes it does not take.
 bool attn_flash_ok(int L, int Dh);

@@ -190,9 +190,9 @@ struct UNetModel {
   // folded single-head attention blocks (attn_block.hip): per block's qkv weights, the fp32 products At, w,
   // Wg, cb and the fp16x2 fragment images of At and Wg, made at the first fp16x2 plan build
   struct FoldW {
-    float *at = nullptr, *w = nullptr, *wg = nullptr, *cb = nullptr;
-    void *at_img = nullptr, *wg_img = nullptr;
-    const float *at_rs = nullptr, *wg_rs = nullptr;
+    float *at = nullptr, *w = nullptr, *wg = nullptr, *cb = nullptr, *wgp = nullptr;
+    void *at_img = nullptr, *wg_img = nullptr, *wgp_img = nullptr;
+    const float *at_rs = nullptr, *wg_rs = nullptr, *wgp_rs = nullptr;
   };
   std::map<size_t, FoldW> folds;
   std::vector<void*> fold_mem;
@@ -267,8 +267,8 @@ const UNetModel::FoldW* UNetModel::fold_for(const AttnP& p) {
   FoldW f;
   void* mem = nullptr;
   const size_t nimg = split_conv_weights_bytes(1, C, C, 2);
-  const size_t nf = (2 * CC + 2 * (size_t)C) * sizeof(float);
-  if (hipMalloc(&mem, nf + 2 * nimg + 64) != hipSuccess) {
+  const size_t nf = (3 * CC + 2 * (size_t)C) * sizeof(float);
+  if (hipMalloc(&mem, nf + 3 * nimg + 64) != hipSuccess) {
     (void)hipGetLastError();
     folds[p.wqkv] = FoldW{};  // plan builds stay deterministic: every later build sees the same failure
     return nullptr;
@@ -279,18 +279,23 @@ const UNetModel::FoldW* UNetModel::fold_for(const AttnP& p) {
   f.wg = f.at + CC;
   f.w = f.wg + CC;
   f.cb = f.w + C;
+  f.wgp = f.cb + C;
   f.at_img = base + ((nf + 15) & ~size_t(15));
   f.wg_img = static_cast<char*>(f.at_img) + nimg;
+  f.wgp_img = static_cast<char*>(f.wg_img) + nimg;
   const double s = (double)p.sa * (p.sb != 0.f ? (double)p.sb : 1.0);
   if (attn_fold(P(p.wqkv), P(p.bqkv), P(p.wproj), P(p.bproj), C, s, f.at, f.w, f.wg, f.cb, nullptr) != DM_OK ||
       split_conv_weights(f.at, 1, C, C, C, 1, 2, f.at_img, nullptr) != DM_OK ||
-      split_conv_weights(f.wg, 1, C, C, C, 1, 2, f.wg_img, nullptr) != DM_OK || hipDeviceSynchronize() != hipSuccess) {
+      split_conv_weights(f.wg, 1, C, C, C, 1, 2, f.wg_img, nullptr) != DM_OK ||
+      attn_perm_cols(f.wg, f.wgp, C, nullptr) != DM_OK ||
+      split_conv_weights(f.wgp, 1, C, C, C, 1, 2, f.wgp_img, nullptr) != DM_OK || hipDeviceSynchronize() != hipSuccess) {
     folds[p.wqkv] = FoldW{};
     return nullptr;
   }
   f.at_rs = split_conv_rowscale(f.at_img, 1, C, C);
   f.wg_rs = split_conv_rowscale(f.wg_img, 1, C, C);
-  split_bytes += nf + 2 * nimg;
+  f.wgp_rs = split_conv_rowscale(f.wgp_img, 1, C, C);
+  split_bytes += nf + 3 * nimg;
   return &(folds[p.wqkv] = f);
 }
 
@@ -1066,11 +1071,19 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
         ab.at_img = static_cast<const _Float16*>(fw->at_img); ab.at_rowscale = fw->at_rs; ab.w = fw->w;
         ab.g_plane = gplane; ab.y = y.p; ab.y_pitch = y.pitch; ab.B = B; ab.ex = 6; ab.eg = 6;
         ab.range_flag = range_flag;
-        if (linear_k32_ok(gg)) {
+        // variant 3 (default): values = xn and the folded projection Wg' inside the kernel, no g GEMM;
+        // DM_ATTN_BLOCK=2: g = xn Wg^T + cb from linear_k32 as the fp16x2 plane
+        const bool v3 = !(std::getenv("DM_ATTN_BLOCK") && std::getenv("DM_ATTN_BLOCK")[0] == '2');
+        ab.variant = v3 ? 3 : 2;
+        if (v3) {
+          ab.g_plane = nullptr;
+          ab.wg_img = static_cast<const _Float16*>(fw->wgp_img); ab.wg_rowscale = fw->wgp_rs; ab.cb = fw->cb;
+        }
+        if (v3 || linear_k32_ok(gg)) {
           add("gn_finalize", 0, 8.0 * B * C, [=](hipStream_t st) {
             return gn_finalize(xin, G, sta, 1e-5f, self->P(p.gn.g), self->P(p.gn.b), gsc, gsh, st);
           });
-          add_gemm(gg);
+          if (!v3) add_gemm(gg);
           gn_ready.erase(y.p);
           const int cpg = C / G;
           if (C % G == 0 && cpg >= 4 && cpg <= 32 && (cpg & (cpg - 1)) == 0) {
@@ -1078,11 +1091,11 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
             ab.gn_G = G;
             gn_ready[y.p] = {ab.gn_part, y.C, G};
           }
-          // T (2 L C^2), S (2 L^2 C), P g (2 L^2 C) per image; x read once for the keys and the queries, y
-          // written, the g^T plane (fp16x2, 4 B per element) read
-          const double fl = 2.0 * B * ((double)hw * C * C + 2.0 * hw * hw * C);
-          const double by = 4.0 * B * hw * C * 3.0;
-          add("attn_block_kernel", fl, by, [=](hipStream_t st) { return attn_block(ab, st); });
+          // v3: T (2 L C^2), S (2 L^2 C), P xn (2 L^2 C), Wg' O (2 L C^2) per image; x read, y written.
+          // v2: T, S, P g; x read, y written, the g^T plane (fp16x2, 4 B per element) read
+          const double fl = 2.0 * B * ((v3 ? 2.0 : 1.0) * hw * C * C + 2.0 * hw * hw * C);
+          const double by = 4.0 * B * hw * C * (v3 ? 2.0 : 3.0);
+          add(v3 ? "attn_block3_kernel" : "attn_block_kernel", fl, by, [=](hipStream_t st) { return attn_block(ab, st); });
           x_cur = y;
           continue;
         }

@@ -24,11 +24,13 @@ def _labels(h):
     return [op['label'] for op in dmhip.unet_profile_read(h)]
 
 
-@pytest.mark.parametrize('B', [2, 7])
-def test_folded_attention_vs_unfolded(cuda, golden, monkeypatch, B):
-    """The CIFAR-10 UNet's five 16 x 16 attention blocks run folded (g GEMM + attn_block_kernel, no q / k / v
-    planes): whole forwards within 1e-5 of the unfolded path (same weights, same inputs), and the folded
-    kernels are the ones in the plan."""
+@pytest.mark.parametrize('B,variant', [(2, '3'), (7, '3'), (3, '2')])
+def test_folded_attention_vs_unfolded(cuda, golden, monkeypatch, B, variant):
+    """The CIFAR-10 UNet's five 16 x 16 attention blocks run folded (variant 3, the default: attn_block3_kernel
+    alone; variant 2: g GEMM + attn_block_kernel; no q / k / v planes in either): whole forwards within 1e-5 of
+    the unfolded path (same weights, same inputs), and the folded kernels are the ones in the plan."""
+    monkeypatch.setenv('DM_ATTN_BLOCK', variant)
+    kname = 'attn_block3_kernel' if variant == '3' else 'attn_block_kernel'
     _, meta = golden('forward')
     g = torch.Generator().manual_seed(31)
     x = torch.randn((B, 3, 32, 32), generator=g).to(cuda)
@@ -40,7 +42,8 @@ def test_folded_attention_vs_unfolded(cuda, golden, monkeypatch, B):
     folded(x, t)
     labels = _labels(h)
     dmhip.unet_profile_enable(h, 0)
-    assert labels.count('attn_block_kernel') == 5, labels
+    assert labels.count(kname) == 5, labels
+    assert any(lb.startswith('linear_k32_kernel') for lb in labels) == (variant == '2')
     assert not any(lb.startswith('attn_presplit_kernel') for lb in labels)
     monkeypatch.setenv('DM_ATTN_FOLD', '0')
     unfolded, _ = _model(meta, 'cifar10', cuda)
@@ -73,3 +76,68 @@ def test_folded_attention_batch_invariance(cuda, golden):
     idx = [0, 129, 255]
     small = model(x[idx].contiguous(), t[idx].contiguous())
     assert torch.equal(big[idx], small)
+
+
+# ------------------------------------------------------------------ DiT accuracy evidence
+def _dit_xl2(cuda, golden):
+    from models.dit.model import DiT
+    _, meta = golden('dit')
+    g, ameta = golden('dit_acc')
+    m = DiT(**meta['archs']['dit_xl2']).eval()
+    assert init_synthetic_(m) == ameta['dit_xl2_weights_sha256']
+    return m.to(cuda), g, ameta
+
+
+def test_dit_step_accuracy_vs_float64(cuda, golden, report):
+    """DiT-XL/2 DDIMCFG-3 (s = 4, clip_denoised false: the C5 config), per step from the same input (the
+    oracle's float64 trajectory state rounded to float32; tests/golden/dit_acc.npz, make_golden_r4.py): the
+    engine's distance to the float64 step against the fp32 oracle's. Asserted: every step's rms error at most
+    2x the fp32 oracle's (parity unpinned: oracle/dit.py restates the reference, timm absent)."""
+    from diffusions import DDIMCFG
+    model, g, meta = _dit_xl2(cuda, golden)
+    s = meta['guidance_scale']
+    d = DDIMCFG(guidance_scale=s, respace_type='uniform', respace_steps=meta['respace_steps'], eta=0.0,
+                clip_denoised=meta['clip_denoised'], device=cuda)
+    y = torch.tensor(meta['labels'], device=cuda)
+    ratios, e_max = [], []
+    for i, (t, tn) in enumerate(meta['steps']):
+        x = torch.from_numpy(g['x'][i]).to(cuda)
+        tb = torch.full((x.shape[0], ), t, dtype=torch.long, device=cuda)
+        got = d._step(model(x, tb, y), x, t, tn, model_output_uncond=model(x, tb, None),
+                      guidance_scale=s)['sample'].cpu().double().numpy()
+        diff = np.abs(got - g['ref64'][i])
+        rms = float(np.sqrt((diff ** 2).mean()))
+        e_max.append(float(diff.max()))
+        ratios.append(rms / meta['ref32_rms'][i])
+    report('dit_xl2_stepacc_max_err_vs_float64', max(e_max))
+    report('dit_xl2_stepacc_fp32_oracle_max_err_vs_float64', max(meta['ref32_max']))
+    report('dit_xl2_stepacc_worst_step_rms_ratio_to_fp32_oracle', max(ratios))
+    report('dit_xl2_stepacc_mean_rms_ratio_to_fp32_oracle', float(np.mean(ratios)))
+    assert max(ratios) <= 2.0, ratios
+    del model
+    torch.cuda.empty_cache()
+
+
+def test_dit_trajectory_chaos_envelope(cuda, golden, report):
+    """The DiT-XL/2 DDIMCFG-3 free-running trajectory (batched 2B CFG forward, as the sampler runs it)
+    against the oracle's float64 run: its worst distance must lie inside the envelope of the fp32 oracle's own
+    runs with the model output perturbed by 2^-20 relative (8 seeds, the level at which the engine's forwards
+    differ from the oracle's) -- the check_chaos_envelope criterion of the UNet CFG trajectories."""
+    from diffusions import DDIMCFG
+    model, g, meta = _dit_xl2(cuda, golden)
+    d = DDIMCFG(guidance_scale=meta['guidance_scale'], respace_type='uniform', respace_steps=meta['respace_steps'],
+                eta=0.0, clip_denoised=meta['clip_denoised'], device=cuda)
+    y = torch.tensor(meta['labels'], device=cuda)
+    worst = 0.0
+    for i, out in enumerate(d.sample_loop(model, torch.from_numpy(g['init']).to(cuda), model_kwargs=dict(y=y),
+                                          tqdm_kwargs=dict(disable=True))):
+        worst = max(worst, float(np.abs(out['sample'].cpu().double().numpy() - g['traj64'][i]).max()))
+    env20 = g['e64_p20'].max(axis=1)
+    report('dit_xl2_free_running_maxabs_vs_oracle_float64', worst)
+    report('dit_xl2_fp32_oracle_unperturbed_vs_float64', float(g['e64_p0'].max()))
+    report('dit_xl2_chaos_envelope_2^-20_max', float(env20.max()))
+    report('dit_xl2_chaos_envelope_2^-22_max', float(g['e64_p22'].max()))
+    report('dit_xl2_perturbed_oracle_runs_further_than_engine', float(np.mean(env20 > worst)))
+    assert worst <= max(TOL, float(env20.max())), (worst, list(env20))
+    del model
+    torch.cuda.empty_cache()
