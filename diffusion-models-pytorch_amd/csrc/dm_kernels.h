@@ -167,6 +167,7 @@ struct GemmArgs {
   // linear_k32 only: the attention operand planes instead of C (as ConvArgs::ap_*, the qkv projection
   // feeding attn_presplit_kernel)
   _Float16 *ap_q, *ap_k, *ap_v;
+  int lin_gm;     // linear_k32 tile order: M tiles per group (0: kLGM = 4)
   int ap_vonly;   // every column is a v column (the folded attention's g^T plane; ap_q = ap_k = ap_v)
   int ap_L, ap_heads, ap_Dh, ap_legacy;
   float ap_alpha, ap_bscale;

@@ -326,8 +326,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   // for each of 128 M tiles otherwise); the group's A tiles stay in the XCD's L2 during the sweep.
   const int nN = ceil_div(N, BN), nM = ceil_div(M, BM);
   const int bid = xcd_remap_p(blockIdx.x, gridDim.x);
-  const int tgrp = bid / (kLGM * nN), gm0 = tgrp * kLGM, gsz = min(kLGM, nM - gm0);
-  const int r = bid - tgrp * (kLGM * nN);
+  const int LGM = g.lin_gm > 0 ? g.lin_gm : kLGM;
+  const int tgrp = bid / (LGM * nN), gm0 = tgrp * LGM, gsz = min(LGM, nM - gm0);
+  const int r = bid - tgrp * (LGM * nN);
   const int nt = r / gsz, mt = gm0 + (r - nt * gsz);
   const int m0 = mt * BM, n0 = nt * BN;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -657,8 +658,11 @@ int linear_presplit_a(const GemmArgs& g, _Float16* out, hipStream_t st) {
   return DM_OK;
 }
 
-int linear_k32(const GemmArgs& g, hipStream_t st) {
-  DM_REQUIRE(linear_k32_ok(g), "linear_k32: needs pre-split weights, K % 64 == 0, 16-byte aligned 4-column rows");
+int linear_k32(const GemmArgs& g0, hipStream_t st) {
+  DM_REQUIRE(linear_k32_ok(g0), "linear_k32: needs pre-split weights, K % 64 == 0, 16-byte aligned 4-column rows");
+  static const int env_gm = std::getenv("DM_LIN_GM") ? std::atoi(std::getenv("DM_LIN_GM")) : 0;  // tile-order A/B
+  GemmArgs g = g0;
+  if (env_gm > 0 && g.lin_gm == 0) g.lin_gm = env_gm;
   const int blocks = ceil_div(g.M, kLBM) * ceil_div(g.N, 128);
   if (g.as)
     hipLaunchKernelGGL(linear_k32_kernel<3>, dim3(blocks), dim3(256), 0, st, g);
