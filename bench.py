@@ -23,8 +23,9 @@ bf16x3: P = 6, 416.7 TF).
 
 CPU baseline: the oracle (a torch-CPU restatement of the reference path,
 bit-equal to it at equal thread count) timed on all usable host cores, rank 0 /
-N=1 only: one warm-up step and 3 timed denoising steps of the same B=256 fold,
-extrapolated x50.
+N=1 only: one warm-up step and 8 timed denoising steps of the same B=256 fold
+(about 10 s of CPU work: the 3-step sample of round 3 scattered 0.79-0.88 img/s
+between boxes), extrapolated x50.
 """
 import argparse
 import ctypes
@@ -117,7 +118,7 @@ def usable_cores():
     return n
 
 
-def cpu_baseline(sd, batch, n_steps, timed_steps=3):
+def cpu_baseline(sd, batch, n_steps, timed_steps=8):
     """Oracle (reference op sequence on torch CPU) per BASELINE.md §4: all usable host cores, one warm-up
     step at the config's batch, then `timed_steps` denoising steps (forward + DDIM update) timed at that
     batch; images/sec = batch / (t_step x n_steps) (the per-step cost does not depend on t)."""

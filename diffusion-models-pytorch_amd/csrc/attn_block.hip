@@ -724,7 +724,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
       }
       l_run[qt] = l_run[qt] * corr + ls;
       split8(v, pp[qt][0], pp[qt][1]);
-      if (kc > 0) {
+      // rescale O only when some query's running maximum moved (after the first chunks it mostly does not)
+      if (kc > 0 && __any(corr != 1.0f)) {
 #pragma unroll
         for (int ot = 0; ot < 16; ++ot) acc[ot][qt] *= corr;
       }
@@ -757,13 +758,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     load_w(a.wg_img, 0, u, rg[0][u]);
     load_w(a.wg_img, 1, u, rg[1][u]);
   }
-  // O = acc / (2^14 l) (rows in storage order) -> split pieces x 2^ex as the projection's B operand
+  // O x 2^ex = acc / (2^14 l) (the staged keys carry xn x 2^ex; rows in storage order) -> split pieces as the
+  // projection's B operand
   f16x8 op[8][2][2];
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     float l = l_run[qt] + __shfl_xor(l_run[qt], 16);
     l += __shfl_xor(l, 32);
-    const float sc = xs / (16384.f * l);
+    const float sc = 1.f / (16384.f * l);
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {
       float v[8];

@@ -504,9 +504,14 @@ constexpr int kSP = 144;      // patch pixels: 4 images of 4 x 4 with their halo
 constexpr int kTabS = 4096;   // GroupNorm tables: 4 images x 512 channels x (scale, shift)
 constexpr int kStatsS = 4 * 64;
 
-template <bool PRO>
-__global__ void __launch_bounds__(256) conv_k32s_kernel(ConvArgs a, PatchGeom g) {
-  constexpr int BM = 64, BN = 64, TM = 4, TN = 2, WD = 2, PJ = 5;  // 5 loader passes of 64 (pixel, quarter)
+// NW = 8 (default): 8 waves, (grp, wn, wm): each wave a 32 x 32 tile (TM = 2), two waves per SIMD, so one wave's
+// LDS / L2 waits overlap the other's MFMAs (the 4-wave form waited on each tap's fragment reads with its matrix
+// pipe idle). Every output element's MFMA sequence and K split are those of NW = 4: bit-identical results.
+template <bool PRO, int NW>
+__global__ void __launch_bounds__(NW * 64) conv_k32s_kernel(ConvArgs a, PatchGeom g) {
+  constexpr int NT = NW * 64, SR = NT / 4;   // threads; loader rows per pass ((pixel, quarter) items)
+  constexpr int BM = 64, BN = 64, TM = NW == 8 ? 2 : 4, TN = 2, WD = 2;
+  constexpr int PJ = (2 * kSP + SR - 1) / SR;  // loader passes over the pair's 2 x 144 items: 5 (NW 4) / 3 (NW 8)
   constexpr int PATCH = kSP * kRowH;
   // one LDS array: [group][buffer] patch images, then the GroupNorm tables and statistics
   __shared__ __attribute__((aligned(16))) _Float16 patch[4 * PATCH];
@@ -523,13 +528,14 @@ __global__ void __launch_bounds__(256) conv_k32s_kernel(ConvArgs a, PatchGeom g)
 
   const int t = threadIdx.x;
   const int lane = t & 63, wave = t >> 6;
-  const int grp = wave >> 1, wn = wave & 1;
+  const int grp = NW == 8 ? wave >> 2 : wave >> 1, wn = NW == 8 ? (wave >> 1) & 1 : wave & 1;
+  const int wm = NW == 8 ? wave & 1 : 0;   // row half (NW 8)
   const int l16 = lane & 15, q = lane >> 4;
   const int srow = t >> 2, sq = t & 3;
   const int nch = a.Cin1 / kC, h = nch / 2;
   const int n2 = a.Cin2 / kC, h2 = n2 / 2;
 
-  // ---- loader: pass j covers item p = srow + 64 j of the pair's 2 x 144 (pixel, quarter) items; p < 144 is
+  // ---- loader: pass j covers item p = srow + SR j of the pair's 2 x 144 (pixel, quarter) items; p < 144 is
   // group 0's chunk, the rest group 1's
   const float* psrc[PJ];
   bool pok[PJ];
@@ -537,7 +543,7 @@ __global__ void __launch_bounds__(256) conv_k32s_kernel(ConvArgs a, PatchGeom g)
   const int PHW = g.PH * g.PW;
 #pragma unroll
   for (int j = 0; j < PJ; ++j) {
-    const int p = srow + 64 * j;
+    const int p = srow + SR * j;
     const int pg = p >= kSP ? 1 : 0, pp = p - pg * kSP;
     const int img = pp / PHW;
     const int rem = pp - img * PHW;
@@ -578,7 +584,7 @@ __global__ void __launch_bounds__(256) conv_k32s_kernel(ConvArgs a, PatchGeom g)
   const int tile_rows = g.TH * g.TW;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    const int ml = i * 16 + l16;
+    const int ml = (wm * TM + i) * 16 + l16;
     fimg[i] = ml / tile_rows;
     const int rem = ml - fimg[i] * tile_rows;
     fy[i] = rem / g.TW;
@@ -601,7 +607,7 @@ __global__ void __launch_bounds__(256) conv_k32s_kernel(ConvArgs a, PatchGeom g)
     const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int j = j0; j < j1; ++j) {
-      const int p = srow + 64 * j;
+      const int p = srow + SR * j;
       const int pg = p >= kSP ? 1 : 0, pp = p - pg * kSP;
       if (PRO) {
         const float* ts = gtab + min(pimg[j] - b0, tab_n - 1) * tab_c + (pg ? h + i : i) * kC + 8 * sq;
@@ -669,7 +675,7 @@ __global__ void __launch_bounds__(256) conv_k32s_kernel(ConvArgs a, PatchGeom g)
   if (PRO) {
     if (a.gin_part) {  // gn_finalize for the tile's images (conv_k32_kernel's in-kernel finalize)
       const int G = a.gin_G, cpg = a.Cin1 / G;
-      for (int i = t; i < tab_n * G; i += 256) {
+      for (int i = t; i < tab_n * G; i += NT) {
         const int b = b0 + i / G, gg = i - (i / G) * G;
         double s1 = 0, s2 = 0;
         for (int k = 0; k < a.gin_nchunk; ++k) {
@@ -684,7 +690,7 @@ __global__ void __launch_bounds__(256) conv_k32s_kernel(ConvArgs a, PatchGeom g)
         gstat[2 * i + 1] = (float)(1.0 / sqrt(var + (double)a.gin_eps));
       }
       __syncthreads();
-      for (int i = t; i < tab_n * tab_c; i += 256) {
+      for (int i = t; i < tab_n * tab_c; i += NT) {
         const int bi = i / tab_c, c = i - (i / tab_c) * tab_c;
         const int si = 2 * (bi * G + c / cpg);
         const float mu = gstat[si], rs = gstat[si + 1];
@@ -700,7 +706,7 @@ __global__ void __launch_bounds__(256) conv_k32s_kernel(ConvArgs a, PatchGeom g)
         gtab[tab_n * tab_c + i] = sh;
       }
     } else {
-      for (int i = t; i < tab_n * tab_c; i += 256) {
+      for (int i = t; i < tab_n * tab_c; i += NT) {
         const int bi = i / tab_c, c = i - (i / tab_c) * tab_c;
         gtab[i] = a.pro_scale[(size_t)(b0 + bi) * a.Cin1 + c];
         gtab[tab_n * tab_c + i] = a.pro_shift[(size_t)(b0 + bi) * a.Cin1 + c];
@@ -733,15 +739,17 @@ __global__ void __launch_bounds__(256) conv_k32s_kernel(ConvArgs a, PatchGeom g)
       for (int tap = 0; tap < 9; ++tap) {
         const int kt = (c0w + i) * 9 + tap;
         const int slot = (cc * 9 + tap) % WD;
+        // the pair's loader passes in three phases (taps 0 / 3 / 6 load, 2 / 5 / 8 finish): passes 0-1, 2-3, 4
+        // (NW 4) or 0, 1, 2 (NW 8)
+        constexpr int P0[3] = {0, NW == 8 ? 1 : 2, NW == 8 ? 2 : 4}, P1[3] = {NW == 8 ? 1 : 2, NW == 8 ? 2 : 4, PJ};
         if (tap == 0 || tap == 3 || tap == 6) {
-          load_patch(in, tap == 0 ? 0 : tap == 3 ? 2 : 4, tap == 6 ? 5 : tap == 0 ? 2 : 4);
+          load_patch(in, P0[tap / 3], P1[tap / 3]);
           __builtin_amdgcn_sched_barrier(0);
         }
         compute_tap(tap, grp * 2 + buf, bq[slot]);
         load_b(bq[slot], slice_off(min(kt + WD, (c0w + h) * 9 - 1)));
         __builtin_amdgcn_sched_barrier(0);
-        if (tap == 2 || tap == 5 || tap == 8)
-          finish_patch(in, tap == 2 ? 0 : tap == 5 ? 2 : 4, tap == 8 ? 5 : tap == 2 ? 2 : 4, (i + 1) & 1);
+        if (tap == 2 || tap == 5 || tap == 8) finish_patch(in, P0[tap / 3], P1[tap / 3], (i + 1) & 1);
       }
       __syncthreads();
     }
@@ -752,15 +760,18 @@ __global__ void __launch_bounds__(256) conv_k32s_kernel(ConvArgs a, PatchGeom g)
   if (n2 > 0) {
     int abase[TM];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) abase[i] = (i * 16 + l16) * kRowH + q * 8;
+    for (int i = 0; i < TM; ++i) abase[i] = ((wm * TM + i) * 16 + l16) * kRowH + q * 8;
     const size_t s2 = (size_t)(9 * a.Cin1 / 16) * sl + (size_t)(q >> 1) * sl;
     for (int c2 = 0; c2 < n2 - h2; ++c2) {
-      // loader: item (group j, row srow, quarter sq)
-      f4 r[2][2];
+      // loader: item (group jg, row, quarter sq): NW 4 -- both groups per thread; NW 8 -- group srow >> 6
+      constexpr int SJ = NW == 8 ? 1 : 2;
+      const int lrow = srow & 63;
+      f4 r[SJ][2];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int cj = j ? h2 + c2 : min(c2, max(h2 - 1, 0));
-        const float* xs = a.x2 + (size_t)min(m0 + srow, M - 1) * a.x2_pitch + 8 * sq + cj * kC;
+      for (int j = 0; j < SJ; ++j) {
+        const int jg = NW == 8 ? (srow >> 6) : j;
+        const int cj = jg ? h2 + c2 : min(c2, max(h2 - 1, 0));
+        const float* xs = a.x2 + (size_t)min(m0 + lrow, M - 1) * a.x2_pitch + 8 * sq + cj * kC;
         r[j][0] = *reinterpret_cast<const f4*>(xs);
         r[j][1] = *reinterpret_cast<const f4*>(xs + 4);
       }
@@ -768,10 +779,11 @@ __global__ void __launch_bounds__(256) conv_k32s_kernel(ConvArgs a, PatchGeom g)
       const bool active = cw < (grp ? n2 : h2);
       load_b(bq[0], s2 + (size_t)(2 * min(cw, n2 - 1)) * sl);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < SJ; ++j) {
+        const int jg = NW == 8 ? (srow >> 6) : j;
         f16x8 pc[2];
         Split<2>::split(r[j][0], r[j][1], pc, bad);
-        _Float16* dst = patch + (j * 2) * PATCH + srow * kRowH;
+        _Float16* dst = patch + (jg * 2) * PATCH + lrow * kRowH;
         *reinterpret_cast<f16x8*>(dst + sq * 8) = pc[0];
         *reinterpret_cast<f16x8*>(dst + 32 + sq * 8) = pc[1];
       }
@@ -807,7 +819,8 @@ __global__ void __launch_bounds__(256) conv_k32s_kernel(ConvArgs a, PatchGeom g)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) part[(grp * 64 + i * 16 + 4 * q + r) * PTP + wn * 32 + j * 16 + l16] = acc[i][j][r];
+      for (int r = 0; r < 4; ++r)
+        part[(grp * 64 + (wm * TM + i) * 16 + 4 * q + r) * PTP + wn * 32 + j * 16 + l16] = acc[i][j][r];
   __syncthreads();
   constexpr int LPR = 8, RPI = 8;  // lanes per row (4 columns each), rows per wave instruction
   const int c4 = lane % LPR, rsub = lane / LPR;
@@ -817,18 +830,20 @@ __global__ void __launch_bounds__(256) conv_k32s_kernel(ConvArgs a, PatchGeom g)
   const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
   const f4 s4 = {a.ws_rowscale[nc], a.ws_rowscale[nc + 1], a.ws_rowscale[nc + 2], a.ws_rowscale[nc + 3]};
   const f4 bias4 = a.bias ? *reinterpret_cast<const f4*>(a.bias + nc) : zero4;
-  const int row0 = 32 * grp;
+  // rows of this wave: 32 (NW 4: slab grp) or 16 (NW 8: slab 2 grp + wm)
+  constexpr int WR = 128 / NW;
+  const int row0 = NW == 8 ? 16 * (2 * grp + wm) : 32 * grp;
   double gs[2] = {0.0, 0.0}, gq[2] = {0.0, 0.0};
-  f4 rs4[32 / RPI];
+  f4 rs4[WR / RPI];
   if (a.res) {
 #pragma unroll
-    for (int it = 0; it < 32 / RPI; ++it) {
+    for (int it = 0; it < WR / RPI; ++it) {
       const int m = min(m0 + row0 + it * RPI + rsub, M - 1);
       rs4[it] = *reinterpret_cast<const f4*>(a.res + (size_t)m * a.res_pitch + nc);
     }
   }
 #pragma unroll
-  for (int it = 0; it < 32 / RPI; ++it) {
+  for (int it = 0; it < WR / RPI; ++it) {
     const int row = row0 + it * RPI + rsub;
     const int m = m0 + row;
     const f4 p0 = *reinterpret_cast<const f4*>(part + row * PTP + wn * 32 + 4 * c4);
@@ -850,7 +865,7 @@ __global__ void __launch_bounds__(256) conv_k32s_kernel(ConvArgs a, PatchGeom g)
   if (a.gn_part) {  // per image of the slab: over the row lanes, then the group's 4-channel quads
     const int cpg = N / a.gn_G;
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
+    for (int hh = 0; hh < WR / 16; ++hh) {
       double s = gs[hh], qq = gq[hh];
 #pragma unroll
       for (int o = LPR; o < 64; o <<= 1) {
@@ -1001,7 +1016,10 @@ int conv_k32_pick(const ConvArgs& a) {
 
 // rocprofv3's name of the instantiation conv2d_k32 launches (spaces removed)
 std::string conv_k32_label(const ConvArgs& a, int v) {
-  if (v == 6) return std::string("conv_k32s_kernel<") + (a.pro_scale || a.gin_part ? "true>" : "false>");
+  if (v == 6) {
+    const bool w4 = std::getenv("DM_K32S_W4") && std::getenv("DM_K32S_W4")[0] == '1';
+    return std::string("conv_k32s_kernel<") + (a.pro_scale || a.gin_part ? "true," : "false,") + (w4 ? "4>" : "8>");
+  }
   if (v == 7)
     return std::string("conv_k32_kernel<128,128,64,32,") + (a.pro_scale ? "true," : "false,") + "false," +
            (a.upsample == 2 ? "true,512>" : "false,512>");
@@ -1045,10 +1063,16 @@ int conv2d_k32(const ConvArgs& a, int v, hipStream_t st) {
   if (v == 6) {
     conv_patch_geom(a, 64, g);
     const int blocks = ceil_div(a.B * a.Hout * a.Wout, 64) * (a.Cout / 64);
-    if (a.pro_scale || a.gin_part)
-      hipLaunchKernelGGL(conv_k32s_kernel<true>, dim3(blocks), dim3(256), 0, st, a, g);
-    else
-      hipLaunchKernelGGL(conv_k32s_kernel<false>, dim3(blocks), dim3(256), 0, st, a, g);
+    // DM_K32S_W4=1: the 4-wave form (one wave per SIMD)
+    static const bool w4 = std::getenv("DM_K32S_W4") && std::getenv("DM_K32S_W4")[0] == '1';
+    const bool pro = a.pro_scale || a.gin_part;
+    if (w4) {
+      if (pro) hipLaunchKernelGGL((conv_k32s_kernel<true, 4>), dim3(blocks), dim3(256), 0, st, a, g);
+      else hipLaunchKernelGGL((conv_k32s_kernel<false, 4>), dim3(blocks), dim3(256), 0, st, a, g);
+    } else {
+      if (pro) hipLaunchKernelGGL((conv_k32s_kernel<true, 8>), dim3(blocks), dim3(512), 0, st, a, g);
+      else hipLaunchKernelGGL((conv_k32s_kernel<false, 8>), dim3(blocks), dim3(512), 0, st, a, g);
+    }
     DM_LAUNCH_CHECK();
     return DM_OK;
   }

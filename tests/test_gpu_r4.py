@@ -141,3 +141,27 @@ def test_dit_trajectory_chaos_envelope(cuda, golden, report):
     assert worst <= max(TOL, float(env20.max())), (worst, list(env20))
     del model
     torch.cuda.empty_cache()
+
+
+# ------------------------------------------------------------------ small-map conv, 8 waves (conv_k32.hip)
+def test_small_map_conv_8_waves_bit_identical(cuda, golden, monkeypatch):
+    """The 4x4-level convs (conv_k32s_kernel) with 8 waves (two per SIMD, 32 x 32 wave tiles) give the same bits
+    as the 4-wave form (same K split, same MFMA sequence per output element): whole CIFAR forwards equal, and the
+    8-wave kernel is the one in the plan."""
+    _, meta = golden('forward')
+    g = torch.Generator().manual_seed(33)
+    x = torch.randn((5, 3, 32, 32), generator=g).to(cuda)
+    t = torch.randint(0, 1000, (5, ), generator=g).to(cuda)
+    outs, labels = {}, {}
+    for w4 in ('0', '1'):
+        monkeypatch.setenv('DM_K32S_W4', w4)
+        model, _ = _model(meta, 'cifar10', cuda)
+        outs[w4] = model(x, t)
+        h = model.native_handle(torch.device(cuda))
+        dmhip.unet_profile_enable(h, 1)
+        model(x, t)
+        labels[w4] = _labels(h)
+        dmhip.unet_profile_enable(h, 0)
+        del model
+    assert any(lb.startswith('conv_k32s_kernel<') and lb.endswith(',8>') for lb in labels['0']), labels['0']
+    assert torch.equal(outs['0'], outs['1'])
