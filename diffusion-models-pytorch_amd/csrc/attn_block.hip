@@ -724,8 +724,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
       }
       l_run[qt] = l_run[qt] * corr + ls;
       split8(v, pp[qt][0], pp[qt][1]);
-      // rescale O only when some query's running maximum moved (after the first chunks it mostly does not)
-      if (kc > 0 && __any(corr != 1.0f)) {
+      // (a wave-uniform skip of this rescale when no running maximum moved made the compiler spill 2.2 KB
+      // per lane: the accumulators live in AGPRs, and the branch forced copies of all of them)
+      if (kc > 0) {
 #pragma unroll
         for (int ot = 0; ot < 16; ++ot) acc[ot][qt] *= corr;
       }

@@ -76,8 +76,12 @@ __device__ unsigned long long g_k32_stamps[65536][8];
 // NT threads per block (256, or 512 for the 128-pixel row-segment tiles of the wide maps: 8 waves of 64 x 32
 // in one block per CU, each weight fragment loaded by two waves instead of by four 64 x 128 blocks' waves),
 // MAXP patch pixels per buffer.
+// S2: the stride-2 3x3 (Downsample, models/modules.py:70-72): 64-pixel output tiles of whole output rows, a
+// (2 TH + 1) x (2 Wo + 2) input patch whose columns are stored parity-split (even input columns -1 + 2 u' at
+// u', odd ones after them), so the 16 lanes of a fragment -- consecutive output columns -- read consecutive
+// patch pixels for every tap, as in the stride-1 patch (conflict-free ds_read_b128).
 template <int BM, int BN, int WM, int WN, bool PRO, bool KSPLIT, bool SUB = false, int NT = 256, int MAXP = kMaxP,
-          int TABF = kTab>
+          int TABF = kTab, bool S2 = false>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) conv_k32_kernel(ConvArgs a, PatchGeom g) {
   constexpr int NWN = BN / WN;
   static_assert((BM / WM) * NWN == NT / 64, "one wave per 64 threads");
@@ -135,7 +139,9 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const int rem = p - img * PHW;
     const int pr = rem / g.PW, pc = rem - (rem / g.PW) * g.PW;
     const int b = b0 + img;
-    const int iy = y0 - 1 + pr, ix = x0 + pc - 1;
+    // S2: patch row pr = input row 2 y0 - 1 + pr; patch column pc = parity-split input column
+    const int u2 = pc <= g.TW ? 2 * pc : 2 * (pc - g.TW - 1) + 1;
+    const int iy = S2 ? 2 * y0 - 1 + pr : y0 - 1 + pr, ix = S2 ? u2 - 1 : x0 + pc - 1;
     const bool ok = p < g.P && b < a.B && iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
     pok[j] = ok;
     const int bc = min(b, a.B - 1);
@@ -257,6 +263,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
   };
   // A row offsets of tap (ky, kx) for the lane's row of tile i
   auto a_off = [&](int i, int ky, int kx) {
+    if (S2) return ((fimg[i] * g.PH + 2 * fy[i] + ky) * g.PW + (kx & 1) * (g.TW + 1) + fx[i] + (kx >> 1)) * kRowH + q * 8;
     return ((fimg[i] * g.PH + fy[i] + ky) * g.PW + fx[i] + kx) * kRowH + q * 8;
   };
   // One tap of the main loop. a0 holds tile 0's fragment of this tap on entry (read ahead) and, for
@@ -403,6 +410,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
 
   K32_STAMP(2);
   // ---- segment 2: 1x1 product of x2 (the ResBlock shortcut), K = Cin2 in 32-channel steps, un-pipelined
+  if constexpr (BM >= SROWS) {  // (the stride-2 tiles take no second segment)
   if (a.Cin2 > 0 && (!KSPLIT || split == a.ksplit - 1)) {
     constexpr int RJ = BM / SROWS;  // staging passes of SROWS rows
     const size_t s2 = (size_t)(NTAP * a.Cin1 / 16) * sl + (size_t)(q >> 1) * sl;  // 16-slices 9 Cin1/16 + 2 c2 + (q>>1)
@@ -433,6 +441,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
       compute(patch, abase, bq[0]);
       __syncthreads();
     }
+  }
   }
   if (bad && a.range_flag) *a.range_flag = 1;
   K32_STAMP(3);
@@ -896,7 +905,8 @@ extern "C" int dm_debug_k32_stamps(void* host, int nblocks) {
 // 5 = 64 x 128 tiles of one image row or 64-pixel row segment (ADM's 64^2 .. 256^2 maps), 6 = the small-map
 // kernel (64 x 64 tiles of four 4 x 4 images, K split in two inside the block; the plan's ksplit = 2),
 // 7 = 512-thread 128 x 128 tiles of 64 x 32 wave tiles (wide maps), 8 = variant 1 / its sub-pixel form with a
-// 32 KB GroupNorm table (inputs of up to 2048 channels at two images per tile; one block per CU).
+// 32 KB GroupNorm table (inputs of up to 2048 channels at two images per tile; one block per CU), 9 = the
+// stride-2 downsample (64 x 128 tiles of 8 waves of 32 x 32 over whole output rows, one block per CU).
 static bool conv_k32s_ok(const ConvArgs& a) {
   if (!(a.ws && a.ws_np == 2 && a.ws_rowscale && a.taps == 9 && a.stride == 1 && a.upsample == 0)) return false;
   if (a.ksplit != 2 || a.Hout * a.Wout != 16 || a.Hin != a.Hout || a.Win != a.Wout) return false;
@@ -914,6 +924,16 @@ static bool conv_k32s_ok(const ConvArgs& a) {
 
 int conv_k32_variant_ok(const ConvArgs& a, int v) {
   if (v == 6) return conv_k32s_ok(a) ? 1 : 0;
+  if (v == 9) {
+    if (!(a.ws && a.ws_np == 2 && a.ws_rowscale && a.taps == 9 && a.stride == 2 && a.upsample == 0)) return 0;
+    if (a.Cin1 < kC || a.Cin1 % kC != 0 || a.Cin2 != 0 || a.ksplit > 1 || a.K != 9 * a.Cin1) return 0;
+    if (a.Wout % 8 != 0) return 0;
+    PatchGeom g;
+    if (!conv_patch_geom(a, 64, g) || g.P > kMaxPW || g.TB > 2) return 0;
+    if (a.pro_scale && 2 * g.TB * a.Cin1 > kTab) return 0;
+    if (a.gin_part && g.TB * a.gin_G > kStats) return 0;
+    return staged_epilogue_ok(a) ? 1 : 0;
+  }
   if (v == 7) {  // 128-row tiles of 512 threads over one image's 128-pixel row segment or two 64-pixel rows
     const bool sub = a.upsample == 2;
     if (!(a.ws && a.ws_np == 2 && a.ws_rowscale && a.taps == 9 && a.stride == 1 && (a.upsample == 0 || sub))) return 0;
@@ -980,6 +1000,12 @@ static bool conv_k32_bigtab_enabled() {
   return !(e && e[0] == '0');
 }
 
+// The stride-2 tiles (variant 9) unless DM_CONV_K32S2=0 (then conv_patch3 MODE 4, kept as their test oracle)
+static bool conv_k32_s2_enabled() {
+  const char* e = std::getenv("DM_CONV_K32S2");
+  return !(e && e[0] == '0');
+}
+
 // The small-map kernel (variant 6) unless DM_CONV_K32S=0 (the two-launch split-K path, kept as its test oracle;
 // read per call: plans capture their launches once, so this costs nothing per forward)
 static bool conv_k32_small_enabled() {
@@ -988,8 +1014,12 @@ static bool conv_k32_small_enabled() {
 }
 
 int conv_k32_pick(const ConvArgs& a) {
-  if (a.tile >= 10 && a.tile <= 17) return conv_k32_variant_ok(a, a.tile - 9) ? a.tile - 9 : 0;
+  if (a.tile >= 10 && a.tile <= 18) return conv_k32_variant_ok(a, a.tile - 9) ? a.tile - 9 : 0;
   if (a.tile != 0 || !conv_k32_enabled()) return 0;
+  if (a.stride == 2) {  // at least one block per CU (the nominal batch keeps the choice batch-invariant)
+    const long M = (long)(a.pick_B > 0 ? a.pick_B : a.B) * a.Hout * a.Wout;
+    return conv_k32_s2_enabled() && conv_k32_variant_ok(a, 9) && (M / 64) * ((a.Cout + 127) / 128) >= 256 ? 9 : 0;
+  }
   // split-K convs of maps of <= 16 pixels: 64 x 128 tiles (4x4 maps at B = 256, K split 2: 32.5 us vs
   // 34.2 us for 64 x 64 and for conv_patch3's 64 x 64 split tiles)
   if (a.ksplit > 1) {
@@ -1026,6 +1056,8 @@ std::string conv_k32_label(const ConvArgs& a, int v) {
   if (v == 8)
     return std::string("conv_k32_kernel<128,128,64,64,") + (a.pro_scale ? "true," : "false,") + "false," +
            (a.upsample == 2 ? "true,256,208,8192>" : "false,256,208,8192>");
+  if (v == 9)
+    return std::string("conv_k32_kernel<64,128,32,32,") + (a.pro_scale ? "true," : "false,") + "false,false,512,392,2048,true>";
   static const char* names[] = {"", "conv_k32_kernel<128,128,64,64,", "conv_k32_kernel<128,64,64,32,",
                                 "conv_k32_kernel<64,64,32,32,", "conv_k32_kernel<64,128,32,64,",
                                 "conv_k32_kernel<64,128,32,64,"};
@@ -1033,7 +1065,7 @@ std::string conv_k32_label(const ConvArgs& a, int v) {
          (a.upsample == 2 ? "true>" : "false>");
 }
 
-template <int BM, int BN, int WM, int WN, bool KSPLIT, int NT = 256, int MAXP = kMaxP, int TABF = kTab>
+template <int BM, int BN, int WM, int WN, bool KSPLIT, int NT = 256, int MAXP = kMaxP, int TABF = kTab, bool S2 = false>
 static void launch_k32(const ConvArgs& a, const PatchGeom& g, hipStream_t st) {
   const bool sub = a.upsample == 2;
   const int M = sub ? a.B * a.Hin * a.Win : a.B * a.Hout * a.Wout;
@@ -1050,15 +1082,15 @@ static void launch_k32(const ConvArgs& a, const PatchGeom& g, hipStream_t st) {
     }
   }
   if (a.pro_scale)
-    hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, true, KSPLIT, false, NT, MAXP, TABF>), dim3(blocks), dim3(NT), 0,
-                       st, a, g);
-  else
-    hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, false, KSPLIT, false, NT, MAXP, TABF>), dim3(blocks), dim3(NT),
+    hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, true, KSPLIT, false, NT, MAXP, TABF, S2>), dim3(blocks), dim3(NT),
                        0, st, a, g);
+  else
+    hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, false, KSPLIT, false, NT, MAXP, TABF, S2>), dim3(blocks),
+                       dim3(NT), 0, st, a, g);
 }
 
 int conv2d_k32(const ConvArgs& a, int v, hipStream_t st) {
-  DM_REQUIRE(v >= 1 && v <= 8 && conv_k32_variant_ok(a, v), "conv: shape not supported by the K = 32 split kernel");
+  DM_REQUIRE(v >= 1 && v <= 9 && conv_k32_variant_ok(a, v), "conv: shape not supported by the K = 32 split kernel");
   PatchGeom g;
   if (v == 6) {
     conv_patch_geom(a, 64, g);
@@ -1076,8 +1108,9 @@ int conv2d_k32(const ConvArgs& a, int v, hipStream_t st) {
     DM_LAUNCH_CHECK();
     return DM_OK;
   }
-  conv_patch_geom(a, v >= 3 && v <= 6 ? 64 : BM_K32, g);
+  conv_patch_geom(a, (v >= 3 && v <= 6) || v == 9 ? 64 : BM_K32, g);
   switch (v) {
+    case 9: launch_k32<64, 128, 32, 32, false, 512, kMaxPW, kTab, true>(a, g, st); break;
     case 8: launch_k32<128, 128, 64, 64, false, 256, kMaxP, kTabBig>(a, g, st); break;
     case 7: launch_k32<128, 128, 64, 32, false, 512, kMaxPW>(a, g, st); break;
     case 1: launch_k32<128, 128, 64, 64, false>(a, g, st); break;

@@ -64,9 +64,11 @@ def test_folded_attention_vs_reference(cuda, golden, report):
     assert err <= TOL, err
 
 
-def test_folded_attention_batch_invariance(cuda, golden):
+@pytest.mark.parametrize('variant', ['2', '3'])
+def test_folded_attention_batch_invariance(cuda, golden, monkeypatch, variant):
     """B = 256 (the benchmark batch) rows equal the B = 3 forward's rows bit for bit: every work-group is one
     (image, query half) and reads only its image."""
+    monkeypatch.setenv('DM_ATTN_BLOCK', variant)
     _, meta = golden('forward')
     model, _ = _model(meta, 'cifar10', cuda)
     g = torch.Generator().manual_seed(32)
@@ -165,3 +167,65 @@ def test_small_map_conv_8_waves_bit_identical(cuda, golden, monkeypatch):
         del model
     assert any(lb.startswith('conv_k32s_kernel<') and lb.endswith(',8>') for lb in labels['0']), labels['0']
     assert torch.equal(outs['0'], outs['1'])
+
+
+# ------------------------------------------------------------------ stride-2 downsample on K32 (conv_k32.hip S2)
+S2_LABEL = 'conv_k32_kernel<64,128,32,32,false,false,false,512,392,2048,true>'
+
+
+@pytest.mark.parametrize('B,Cin,Cout,H', [(2, 32, 64, 32), (3, 64, 128, 16), (2, 128, 256, 16), (1, 96, 160, 32),
+                                          (3, 128, 128, 32)])
+def test_stride2_k32_exact(cuda, B, Cin, Cout, H):
+    """The stride-2 3x3 (models/modules.py:70-72) on the K32 tiles (tile 18: 64-pixel output tiles of whole
+    rows, parity-split patch columns, 8 waves of 32 x 32, ragged Cout tails): bit-exact on integer operands."""
+    from tests.test_gpu_ops import _ints, _nhwc, _pack, _run_conv
+    import torch.nn.functional as F
+    x = _ints((B, Cin, H, H), -2, 3, seed=44)
+    w = _ints((Cout, Cin, 3, 3), -2, 3, seed=45)
+    b = _ints((Cout, ), seed=46)
+    ref = F.conv2d(x.double(), w.double(), b.double(), stride=2, padding=1).float()
+    Ho = ref.shape[-1]
+    y = _run_conv(cuda, _nhwc(x).to(cuda), _pack(w, cuda), Cout, Ho, Ho, 9, 2, 0, b.to(cuda), split='fp16x2', tile=18)
+    assert torch.equal(y.cpu(), _nhwc(ref))
+
+
+def test_stride2_k32_fp32_accuracy(cuda):
+    """Random stride-2 conv on the K32 tiles: error vs fp64 within 2x the fp32 kernel's."""
+    from tests.test_gpu_ops import _nhwc, _pack, _run_conv
+    import torch.nn.functional as F
+    g = torch.Generator().manual_seed(47)
+    B, Cin, Cout, H = 8, 256, 256, 16
+    x = torch.randn((B, Cin, H, H), generator=g) * 3
+    w = torch.randn((Cout, Cin, 3, 3), generator=g) * (1.0 / (9 * Cin) ** 0.5)
+    ref = _nhwc(F.conv2d(x.double(), w.double(), stride=2, padding=1))
+    errs = []
+    for split, tile in ((False, 0), ('fp16x2', 18)):
+        y = _run_conv(cuda, _nhwc(x).to(cuda), _pack(w, cuda), Cout, H // 2, H // 2, 9, 2, split=split, tile=tile)
+        errs.append((y.cpu().double() - ref).abs().max().item())
+    assert errs[1] < 2.0 * errs[0] + 1e-7 * ref.abs().max().item(), errs
+
+
+def test_downsample_k32_vs_patch3(cuda, golden, report, monkeypatch):
+    """The CIFAR UNet's 32->16 and 16->8 Downsample convs on the K32 stride-2 tiles (with the consumer's
+    GroupNorm statistics from their epilogue) against conv_patch3 MODE 4 + gn_partial (DM_CONV_K32S2=0): whole
+    forwards within 1e-5, and the K32 kernel is the one in the plan."""
+    _, meta = golden('forward')
+    g = torch.Generator().manual_seed(48)
+    x = torch.randn((6, 3, 32, 32), generator=g).to(cuda)
+    t = torch.randint(0, 1000, (6, ), generator=g).to(cuda)
+    outs = {}
+    for mode in ('k32', 'patch3'):
+        if mode == 'patch3':
+            monkeypatch.setenv('DM_CONV_K32S2', '0')
+        model, _ = _model(meta, 'cifar10', cuda)
+        outs[mode] = model(x, t)
+        h = _profile_labels(model, cuda)
+        model(x, t)
+        labels = _labels(h)
+        dmhip.unet_profile_enable(h, 0)
+        assert labels.count(S2_LABEL) == (2 if mode == 'k32' else 0), labels
+        del model
+    err = (outs['k32'] - outs['patch3']).abs().max().item()
+    report('downsample_k32_maxabs_vs_patch3', err)
+    assert torch.isfinite(outs['k32']).all()
+    assert err <= 1e-5, err

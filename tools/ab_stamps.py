@@ -37,7 +37,7 @@ def main():
     L.dm_debug_ab_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
     assert L.dm_debug_ab_stamps(buf.ctypes.data, nblk) == 0
     s = buf.astype(np.int64)
-    if os.environ.get('DM_ATTN_BLOCK', '3') == '2':
+    if os.environ.get("DM_ATTN_BLOCK", "3") == "2":
         names = ['T (At xn^T)', 'T finalize + split', 'S (xn T^T)', 'softmax', 'P g', 'epilogue']
     else:
         names = ['T (At xn^T)', 'T finalize + split', 'keys: S + softmax + P xn', 'O finalize', 'Y = Wg O',
