@@ -851,6 +851,335 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
   AB_RSTAMP(9);
 }
 
+// ---- variant 4: attn_block3_kernel's algorithm with 8 waves of 16 queries (512 threads, 128 queries per
+// work-group, one work-group per CU, two waves per SIMD). Per wave half the state of variant 3 (T pieces 64,
+// O / Y accumulators 64 registers, 4 staging slots per thread instead of 8), so two waves fit a SIMD and one
+// wave's LDS / L2 waits, softmax and staging overlap the other's MFMAs, where variant 3's single wave per SIMD
+// left its matrix pipe idle through them (0.27 of the fp16x2 issue peak). The A operands (At / Wg' rows, the
+// keys' xn) are read once per 16 queries instead of per 32: 171 B/clk/CU of ds_read_b128 at the full MFMA rate,
+// within the LDS's 256. Same fragment images, staging layouts, accumulator permutations and scales as variant
+// 3; every output element's MFMA sequence is variant 3's, so the two give the same bits.
+template <class MID>
+__device__ __forceinline__ void kstep1(const _Float16* img, int l16, int q, const f16x8 (&b)[2], fq (&acc)[16],
+                                       MID&& mid) {
+  const int base = (q >> 1) * 8192 + (q & 1) * 256 + l16 * 8;
+  f16x8 a[3][2];
+  auto rd = [&](int t, f16x8 (&dst)[2]) {
+    const int o = base + (t >> 1) * 1024 + (t & 1) * 128;
+    dst[0] = *reinterpret_cast<const f16x8*>(img + o);
+    dst[1] = *reinterpret_cast<const f16x8*>(img + o + 512);
+  };
+  rd(0, a[0]);
+  rd(1, a[1]);
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    if (t + 2 < 16) rd(t + 2, a[(t + 2) % 3]);
+    mma3(a[t % 3], b, acc[t]);
+    mid(t);
+  }
+}
+
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) attn_block4_kernel(AttnBlockArgs a) {
+  __shared__ __attribute__((aligned(16))) float lds[kBQ * kOP];
+  __shared__ __attribute__((aligned(16))) float tab[2][kBC];
+  _Float16* stg = reinterpret_cast<_Float16*>(lds);
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int l16 = lane & 15, q = lane >> 4;
+  const int bid = xcd_remap_p(blockIdx.x, gridDim.x);
+  const int b = bid >> 1, qh = bid & 1;
+  const float* xb = a.x + (size_t)b * kBL * a.x_pitch;
+  const int qrow0 = qh * kBQ + wave * 16;   // this wave's 16 queries
+  const float xs = ldexpf(1.f, a.ex);
+  bool bad = false;
+  for (int i = t; i < kBC; i += 512) {
+    tab[0][i] = a.gsc[(size_t)b * kBC + i];
+    tab[1][i] = a.gsh[(size_t)b * kBC + i];
+  }
+
+  f4 rg[2][4];
+  // weight images (At, Wg'): verbatim copies of split_conv_weights' k-step regions, 4 x 16 B per thread
+  auto load_w = [&](const _Float16* img, int kk, int s, f4& r) {
+    r = reinterpret_cast<const f4*>(img + (size_t)kk * kStepH)[t + 512 * s];
+  };
+  auto store_w = [&](int buf, int s, const f4& r) { reinterpret_cast<f4*>(stg + buf * kStepH)[t + 512 * s] = r; };
+  // key chunk kc: variant 3's key / run mapping on wave & 3; waves 0-3 take the 32-channel groups 0-3, waves
+  // 4-7 groups 4-7 (slot u = group 4 (wave >> 2) + u)
+  const int krun = lane & 7, kk2 = (lane >> 3) & 1, kgrp = lane >> 4;
+  const int kkey3 = 8 * (wave & 3) + 4 * (kgrp >> 1) + 2 * kk2 + (kgrp & 1);
+  const int sg0 = 4 * (wave >> 2);
+  auto load_k = [&](int kc, int u, f4& r) {
+    r = *reinterpret_cast<const f4*>(xb + (size_t)(32 * kc + kkey3) * a.x_pitch + 32 * (sg0 + u) + 4 * krun);
+  };
+  auto store_k = [&](int buf, int u, const f4& r) {
+    const int s = sg0 + u, c = 32 * s + 4 * krun;
+    const f4 sc = *reinterpret_cast<const f4*>(&tab[0][c]), sh = *reinterpret_cast<const f4*>(&tab[1][c]);
+    f4 v = r;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = (v[e] * sc[e] + sh[e]) * xs;
+    bad |= fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))) > 65504.f;
+    f16x4 hi, lo;
+    split4(v, hi, lo);
+    _Float16* dst = stg + buf * kKImg + kkey3 * kKP + 32 * s + 8 * (krun & 3) + 4 * (krun >> 2);
+    *reinterpret_cast<f16x4*>(dst) = hi;
+    *reinterpret_cast<f16x4*>(dst + kKPiece) = lo;
+  };
+
+  fq acc[16];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = fq{0.f, 0.f, 0.f, 0.f};
+  };
+
+  // ------------------------------------------------------------------ 1. T^T = At xn_q^T (+ w)
+  f4 rx[2][2];
+  auto load_xq = [&](int kk, f4 (&r)[2]) {
+    const float* p = xb + (size_t)(qrow0 + l16) * a.x_pitch + 32 * kk + 8 * q;
+    r[0] = *reinterpret_cast<const f4*>(p);
+    r[1] = *reinterpret_cast<const f4*>(p + 4);
+  };
+  auto xq_frag = [&](int kk, const f4 (&r)[2], f16x8 (&bf)[2]) {
+    const int c = 32 * kk + 8 * q;
+    const f4 s0 = *reinterpret_cast<const f4*>(&tab[0][c]), s1 = *reinterpret_cast<const f4*>(&tab[0][c + 4]);
+    const f4 h0 = *reinterpret_cast<const f4*>(&tab[1][c]), h1 = *reinterpret_cast<const f4*>(&tab[1][c + 4]);
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[e] = (r[0][e] * s0[e] + h0[e]) * xs;
+      v[4 + e] = (r[1][e] * s1[e] + h1[e]) * xs;
+    }
+    float m = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(v[e]));
+    bad |= m > 65504.f;
+    split8(v, bf[0], bf[1]);
+  };
+  zero_acc();
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    load_w(a.at_img, 0, u, rg[0][u]);
+    load_w(a.at_img, 1, u, rg[1][u]);
+  }
+  load_xq(0, rx[0]);
+  load_xq(1, rx[1]);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) store_w(0, u, rg[0][u]);
+  __syncthreads();
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) {
+    f16x8 bf[2];
+    xq_frag(kk, rx[kk & 1], bf);
+    if (kk + 2 < 8) load_xq(kk + 2, rx[kk & 1]);
+    kstep1(stg + (kk & 1) * kStepH, l16, q, bf, acc, [&](int tt) {
+      if (tt & 1) return;
+      if (tt < 8) {
+        if (kk + 2 < 8) load_w(a.at_img, kk + 2, tt >> 1, rg[kk & 1][tt >> 1]);
+      } else if (kk + 1 < 8) {
+        store_w((kk + 1) & 1, (tt - 8) >> 1, rg[(kk + 1) & 1][(tt - 8) >> 1]);
+      }
+    });
+    __syncthreads();
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    load_k(0, u, rg[0][u]);
+    load_k(1, u, rg[1][u]);
+  }
+  f16x8 tp[8][2];
+  float tun;
+  {
+    const float xun = ldexpf(1.f, -a.ex);
+    float mx = 0.f;
+#pragma unroll
+    for (int ct = 0; ct < 16; ++ct) {
+      const f4 rs = *reinterpret_cast<const f4*>(a.at_rowscale + 16 * ct + 4 * q);
+      const f4 wv = *reinterpret_cast<const f4*>(a.w + 16 * ct + 4 * q);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = acc[ct][r] * (rs[r] * xun) + wv[r];
+        acc[ct][r] = v;
+        mx = fmaxf(mx, fabsf(v));
+      }
+    }
+    float m = fmaxf(mx, __shfl_xor(mx, 16));
+    m = fmaxf(m, __shfl_xor(m, 32));
+    int E = 0;
+    (void)frexpf(m, &E);
+    const int eT = m > 0.f ? 14 - E : 0;
+    const float sc = ldexpf(1.f, eT);
+    tun = ldexpf(1.f, -(a.ex + eT));
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = acc[2 * ks][e] * sc;
+        v[4 + e] = acc[2 * ks + 1][e] * sc;
+      }
+      split8(v, tp[ks][0], tp[ks][1]);
+    }
+  }
+
+  // ------------------------------------------------------------------ 2. one pass over the keys (chunks of 32)
+#pragma unroll
+  for (int u = 0; u < 4; ++u) store_k(0, u, rg[0][u]);
+  __syncthreads();
+  zero_acc();   // O^T accumulators
+  float m_run = -INFINITY, l_run = 0.f;
+  const float sl2 = tun * 1.4426950408889634f;
+#pragma unroll
+  for (int kc = 0; kc < 8; ++kc) {
+    const _Float16* img = stg + (kc & 1) * kKImg;
+    fq sacc[2] = {fq{0.f, 0.f, 0.f, 0.f}, fq{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        const _Float16* pr = img + (16 * kt + l16) * kKP + 32 * ks + 8 * q;
+        f16x8 av[2];
+        av[0] = *reinterpret_cast<const f16x8*>(pr);
+        av[1] = *reinterpret_cast<const f16x8*>(pr + kKPiece);
+        mma3(av, tp[ks], sacc[kt]);
+      }
+      if (kc + 2 < 8 && !(ks & 1)) load_k(kc + 2, ks >> 1, rg[kc & 1][ks >> 1]);
+    }
+    f16x8 pp[2];
+    {
+      float mx = fmaxf(fmaxf(fmaxf(sacc[0][0], sacc[0][1]), fmaxf(sacc[0][2], sacc[0][3])),
+                       fmaxf(fmaxf(sacc[1][0], sacc[1][1]), fmaxf(sacc[1][2], sacc[1][3])));
+      mx = fmaxf(mx, __shfl_xor(mx, 16));
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      const float m_new = fmaxf(m_run, mx * sl2);
+      const float corr = __builtin_amdgcn_exp2f(m_run - m_new);
+      m_run = m_new;
+      float ls = 0.f, v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[0][e], sl2, -m_new));
+        v[4 + e] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[1][e], sl2, -m_new));
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        ls += v[e];
+        v[e] *= 16384.f;
+      }
+      l_run = l_run * corr + ls;
+      split8(v, pp[0], pp[1]);
+      if (kc > 0) {
+#pragma unroll
+        for (int ot = 0; ot < 16; ++ot) acc[ot] *= corr;
+      }
+    }
+    {
+      const _Float16* pt = img + (4 * q + (l16 >> 2)) * kKP + 4 * (l16 & 3);
+#pragma unroll
+      for (int ot = 0; ot < 16; ++ot) {
+        f16x8 av[2];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const f16x4_t lo4 = lds_tr16(pt + p * kKPiece + 16 * ot);
+          const f16x4_t hi4 = lds_tr16(pt + p * kKPiece + 16 * kKP + 16 * ot);
+          av[p] = f16x8{lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+        }
+        mma3(av, pp, acc[ot]);
+        if (ot >= 8 && !(ot & 1) && kc + 1 < 8) store_k((kc + 1) & 1, (ot - 8) >> 1, rg[(kc + 1) & 1][(ot - 8) >> 1]);
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    load_w(a.wg_img, 0, u, rg[0][u]);
+    load_w(a.wg_img, 1, u, rg[1][u]);
+  }
+  // O x 2^ex = acc / (2^14 l) (the staged keys carry xn x 2^ex), rows in storage order -> the projection's B
+  f16x8 op[8][2];
+  {
+    float l = l_run + __shfl_xor(l_run, 16);
+    l += __shfl_xor(l, 32);
+    const float sc = 1.f / (16384.f * l);
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = acc[2 * ks][e] * sc;
+        v[4 + e] = acc[2 * ks + 1][e] * sc;
+      }
+      split8(v, op[ks][0], op[ks][1]);
+    }
+  }
+
+  // ------------------------------------------------------------------ 3. Y^T = Wg' O^T
+#pragma unroll
+  for (int u = 0; u < 4; ++u) store_w(0, u, rg[0][u]);
+  __syncthreads();
+  zero_acc();
+  // output pass mapping: wave -> (64-token chunk ch, 64-column quarter cq); lane -> 4 columns, row of 4
+  const int ch = wave >> 2, cq = wave & 3;
+  const int c4 = lane & 15, rsub = lane >> 4;
+  const int col = 64 * cq + 4 * c4;
+  const int tok0 = qh * kBQ + 64 * ch;
+  auto load_res = [&](int i, f4& r) {
+    r = *reinterpret_cast<const f4*>(xb + (size_t)(tok0 + 4 * i + rsub) * a.x_pitch + col);
+  };
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) {
+    kstep1(stg + (kk & 1) * kStepH, l16, q, op[kk], acc, [&](int tt) {
+      if (tt & 1) return;
+      if (tt < 8) {
+        if (kk + 2 < 8) load_w(a.wg_img, kk + 2, tt >> 1, rg[kk & 1][tt >> 1]);
+        else load_res(4 * (kk - 6) + (tt >> 1), rg[kk & 1][tt >> 1]);   // residual rows 0 .. 7
+      } else if (kk + 1 < 8) {
+        store_w((kk + 1) & 1, (tt - 8) >> 1, rg[(kk + 1) & 1][(tt - 8) >> 1]);
+      }
+    });
+    __syncthreads();
+  }
+  f4 xr2[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) load_res(8 + i, xr2[i]);
+  if (bad && a.range_flag) *a.range_flag = 1;
+
+  // ------------------------------------------------------------------ 4. y = x + Y + cb, GroupNorm statistics
+  const float yun = ldexpf(1.f, -a.ex);
+#pragma unroll
+  for (int dt = 0; dt < 16; ++dt) {
+    const f4 rs = *reinterpret_cast<const f4*>(a.wg_rowscale + 16 * dt + 4 * q);
+    *reinterpret_cast<fq*>(lds + (wave * 16 + l16) * kOP + 16 * dt + 4 * q) = acc[dt] * (rs * yun);
+  }
+  __syncthreads();
+  const f4 cb4 = *reinterpret_cast<const f4*>(a.cb + col);
+  double gs[4] = {0.0, 0.0, 0.0, 0.0}, gq[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int tok = tok0 + 4 * i + rsub;
+    const f4 o = *reinterpret_cast<const f4*>(lds + (64 * ch + 4 * i + rsub) * kOP + col);
+    const f4 xr = i < 4 ? rg[0][i & 3] : i < 8 ? rg[1][i & 3] : xr2[i & 7];
+    const f4 yv = xr + (o + cb4);
+    *reinterpret_cast<f4*>(a.y + ((size_t)b * kBL + tok) * a.y_pitch + col) = yv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      gs[e] += (double)yv[e];
+      gq[e] += (double)yv[e] * yv[e];
+    }
+  }
+  if (a.gn_part) {
+    double s = gs[0] + gs[1] + gs[2] + gs[3], qq = gq[0] + gq[1] + gq[2] + gq[3];
+    s += __shfl_xor(s, 16);
+    qq += __shfl_xor(qq, 16);
+    s += __shfl_xor(s, 32);
+    qq += __shfl_xor(qq, 32);
+    const int cpg = kBC / a.gn_G;
+    for (int o = 1; o < cpg / 4; o <<= 1) {
+      s += __shfl_xor(s, o);
+      qq += __shfl_xor(qq, o);
+    }
+    if (rsub == 0 && (c4 % (cpg / 4)) == 0)
+      a.gn_part[((size_t)b * (kBL / 64) + (tok0 >> 6)) * a.gn_G + col / cpg] = make_double2(s, qq);
+  }
+}
+
 __device__ __forceinline__ int pi32(int m) { return 4 * (m >> 3) + (m & 3) + 16 * ((m >> 2) & 1); }
 
 // Wg' = Wg with its columns permuted by pi o pi within every 32 columns (attn_block3_kernel's projection)
@@ -892,7 +1221,7 @@ int attn_perm_cols(const float* wg, float* wgp, int C, hipStream_t st) {
 
 int attn_block(const AttnBlockArgs& a, hipStream_t st) {
   auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-  DM_REQUIRE(a.variant == 2 || a.variant == 3, "attention block: variant 2 or 3");
+  DM_REQUIRE(a.variant >= 2 && a.variant <= 4, "attention block: variant 2, 3 or 4");
   DM_REQUIRE(a.B > 0 && a.x && a.y && a.gsc && a.gsh && a.at_img && a.at_rowscale && a.w &&
                  (a.variant == 2 ? a.g_plane != nullptr : (a.wg_img && a.wg_rowscale && a.cb)),
              "attention block: null argument");
@@ -903,7 +1232,9 @@ int attn_block(const AttnBlockArgs& a, hipStream_t st) {
   DM_REQUIRE(!a.gn_part || (a.gn_G > 0 && kBC % a.gn_G == 0 && kBC / a.gn_G >= 4 && kBC / a.gn_G <= 32 &&
                             ((kBC / a.gn_G) & (kBC / a.gn_G - 1)) == 0),
              "attention block: GroupNorm statistics need groups of 4, 8, 16 or 32 channels");
-  if (a.variant == 3)
+  if (a.variant == 4)
+    hipLaunchKernelGGL(attn_block4_kernel, dim3(a.B * (kBL / kBQ)), dim3(512), 0, st, a);
+  else if (a.variant == 3)
     hipLaunchKernelGGL(attn_block3_kernel, dim3(a.B * (kBL / kBQ)), dim3(256), 0, st, a);
   else
     hipLaunchKernelGGL(attn_block_kernel, dim3(a.B * (kBL / kBQ)), dim3(256), 0, st, a);

@@ -754,7 +754,7 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
   float* kpart_ws = nullptr;
   size_t kpart_floats = 0;
   auto maybe_split = [&](ConvArgs& c) {
-    if (c.upsample == 2 || c.taps != 9 || c.Hout * c.Wout > 16 || conv_pick(c) < 3) return;
+    if (c.upsample == 2 || c.taps != 9 || c.stride != 1 || c.Hout * c.Wout > 16 || conv_pick(c) < 3) return;
     // K32 split tiles (conv_k32.hip): 2 splits (4x4 maps, B = 256: 32.5 us vs 37.8 us with 4, the
     // reduction included); conv_patch3's 16-channel chunks: 4
     const int ks = std::min(conv_k32_enabled() ? 2 : 4, c.Cin1 / 32);
@@ -1074,8 +1074,11 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
         // variant 3 (default): values = xn and the folded projection Wg' inside the kernel, no g GEMM (C3 A/B
         // +2.3 % over variant 2: 153 us per block vs 113 + 67 us); DM_ATTN_BLOCK=2: g = xn Wg^T + cb from
         // linear_k32 as the fp16x2 plane, then attn_block_kernel
-        const bool v3 = !(std::getenv("DM_ATTN_BLOCK") && std::getenv("DM_ATTN_BLOCK")[0] == '2');
-        ab.variant = v3 ? 3 : 2;
+        // DM_ATTN_BLOCK=4: variant 3's algorithm on 8 waves of 16 queries (attn_block4_kernel)
+        const char* avs = std::getenv("DM_ATTN_BLOCK");
+        const int av = avs && avs[0] == '2' ? 2 : avs && avs[0] == '4' ? 4 : 3;
+        const bool v3 = av != 2;
+        ab.variant = av;
         if (v3) {
           ab.g_plane = nullptr;
           ab.wg_img = static_cast<const _Float16*>(fw->wgp_img); ab.wg_rowscale = fw->wgp_rs; ab.cb = fw->cb;
@@ -1096,7 +1099,8 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
           // v2: T, S, P g; x read, y written, the g^T plane (fp16x2, 4 B per element) read
           const double fl = 2.0 * B * ((v3 ? 2.0 : 1.0) * hw * C * C + 2.0 * hw * hw * C);
           const double by = 4.0 * B * hw * C * (v3 ? 2.0 : 3.0);
-          add(v3 ? "attn_block3_kernel" : "attn_block_kernel", fl, by, [=](hipStream_t st) { return attn_block(ab, st); });
+          add(av == 4 ? "attn_block4_kernel" : v3 ? "attn_block3_kernel" : "attn_block_kernel", fl, by,
+              [=](hipStream_t st) { return attn_block(ab, st); });
           x_cur = y;
           continue;
         }
@@ -1287,9 +1291,17 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
       if (c.upsample == 2) {
         emit_conv(c, y);  // the K32 sub-pixel conv's epilogue emits the consumer's GroupNorm partials
       } else if (c.stride == 2) {
-        split_for(c);  // the K32 stride-2 tiles emit them too
-        if (conv_k32_pick(c) == 9) emit_conv(c, y);
-        else gn_ready.erase(y.p);
+        // the K32 stride-2 tiles emit them too. Only those take the split weights here: attached earlier to a
+        // 4x4-output downsample they made maybe_split() put it on conv_patch3 MODE 4 with split-K, a path the
+        // plan never takes otherwise (reference-fixture forwards off by 0.14)
+        ConvArgs s = c;
+        split_for(s);
+        if (conv_k32_pick(s) == 9) {
+          c = s;
+          emit_conv(c, y);
+        } else {
+          gn_ready.erase(y.p);
+        }
       } else {
         gn_ready.erase(y.p);
       }

@@ -178,14 +178,16 @@ class deferred_range_check:
     def release(cls, handle):
         """Called before a native handle is destroyed (NativeDenoiser._release_native): every open scope
         that registered it polls it now, folding a raised range flag into the scope (the loop is then
-        re-run), and forgets it -- so no scope calls into a freed handle, and a new handle that reuses
-        the address is registered afresh."""
+        re-run), and forgets it (also from the handles end_fallback returns to fp16x2) -- so no scope calls
+        into a freed handle, and a new handle that reuses the address is registered afresh."""
         key = cls._key(handle)
         scope = cls.active
         while scope is not None:
             entry = scope.handles.pop(key, None)
             if entry is not None:
                 scope._poll(*entry, poll=True)
+            # the scope stays flagged (its loop re-runs), but end_fallback must not reach the freed handle
+            scope.flagged_handles = [(h, a) for h, a in scope.flagged_handles if cls._key(h) != key]
             scope = scope._outer
 
     def __enter__(self):

@@ -24,13 +24,13 @@ def _labels(h):
     return [op['label'] for op in dmhip.unet_profile_read(h)]
 
 
-@pytest.mark.parametrize('B,variant', [(2, '3'), (7, '3'), (3, '2')])
+@pytest.mark.parametrize('B,variant', [(2, '3'), (7, '3'), (3, '2'), (5, '4')])
 def test_folded_attention_vs_unfolded(cuda, golden, monkeypatch, B, variant):
     """The CIFAR-10 UNet's five 16 x 16 attention blocks run folded (variant 3, the default: attn_block3_kernel
     alone; variant 2: g GEMM + attn_block_kernel; no q / k / v planes in either): whole forwards within 1e-5 of
     the unfolded path (same weights, same inputs), and the folded kernels are the ones in the plan."""
     monkeypatch.setenv('DM_ATTN_BLOCK', variant)
-    kname = 'attn_block3_kernel' if variant == '3' else 'attn_block_kernel'
+    kname = {'2': 'attn_block_kernel', '3': 'attn_block3_kernel', '4': 'attn_block4_kernel'}[variant]
     _, meta = golden('forward')
     g = torch.Generator().manual_seed(31)
     x = torch.randn((B, 3, 32, 32), generator=g).to(cuda)
@@ -64,7 +64,7 @@ def test_folded_attention_vs_reference(cuda, golden, report):
     assert err <= TOL, err
 
 
-@pytest.mark.parametrize('variant', ['2', '3'])
+@pytest.mark.parametrize('variant', ['2', '3', '4'])
 def test_folded_attention_batch_invariance(cuda, golden, monkeypatch, variant):
     """B = 256 (the benchmark batch) rows equal the B = 3 forward's rows bit for bit: every work-group is one
     (image, query half) and reads only its image."""
@@ -78,6 +78,22 @@ def test_folded_attention_batch_invariance(cuda, golden, monkeypatch, variant):
     idx = [0, 129, 255]
     small = model(x[idx].contiguous(), t[idx].contiguous())
     assert torch.equal(big[idx], small)
+
+
+def test_folded_attention_8_waves_bit_identical(cuda, golden, monkeypatch):
+    """Variant 4 (8 waves of 16 queries) runs variant 3's MFMA sequence per output element with the same
+    staging layouts and scales: whole forwards equal bit for bit."""
+    _, meta = golden('forward')
+    g = torch.Generator().manual_seed(34)
+    x = torch.randn((4, 3, 32, 32), generator=g).to(cuda)
+    t = torch.randint(0, 1000, (4, ), generator=g).to(cuda)
+    outs = {}
+    for v in ('3', '4'):
+        monkeypatch.setenv('DM_ATTN_BLOCK', v)
+        model, _ = _model(meta, 'cifar10', cuda)
+        outs[v] = model(x, t)
+        del model
+    assert torch.equal(outs['3'], outs['4'])
 
 
 # ------------------------------------------------------------------ DiT accuracy evidence (VERDICT r3 item 3)
