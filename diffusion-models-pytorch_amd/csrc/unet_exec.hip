@@ -1071,12 +1071,13 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
         ab.at_img = static_cast<const _Float16*>(fw->at_img); ab.at_rowscale = fw->at_rs; ab.w = fw->w;
         ab.g_plane = gplane; ab.y = y.p; ab.y_pitch = y.pitch; ab.B = B; ab.ex = 6; ab.eg = 6;
         ab.range_flag = range_flag;
-        // variant 3 (default): values = xn and the folded projection Wg' inside the kernel, no g GEMM (C3 A/B
-        // +2.3 % over variant 2: 153 us per block vs 113 + 67 us); DM_ATTN_BLOCK=2: g = xn Wg^T + cb from
-        // linear_k32 as the fp16x2 plane, then attn_block_kernel
-        // DM_ATTN_BLOCK=4: variant 3's algorithm on 8 waves of 16 queries (attn_block4_kernel)
+        // variant 4 (default): values = xn and the folded projection Wg' inside the kernel, no g GEMM, on 8
+        // waves of 16 queries (attn_block4_kernel: 129 us per block; C3 A/B +0.9 % over variant 3, its 4-wave
+        // form at 156 us, bit-identical); DM_ATTN_BLOCK=3: that 4-wave kernel (C3 A/B +2.3 % over variant 2);
+        // DM_ATTN_BLOCK=2: g = xn Wg^T + cb from linear_k32 as the fp16x2 plane, then attn_block_kernel
+        // (113 + 67 us)
         const char* avs = std::getenv("DM_ATTN_BLOCK");
-        const int av = avs && avs[0] == '2' ? 2 : avs && avs[0] == '4' ? 4 : 3;
+        const int av = avs && avs[0] == '2' ? 2 : avs && avs[0] == '3' ? 3 : 4;
         const bool v3 = av != 2;
         ab.variant = av;
         if (v3) {

@@ -26,9 +26,10 @@ def _labels(h):
 
 @pytest.mark.parametrize('B,variant', [(2, '3'), (7, '3'), (3, '2'), (5, '4')])
 def test_folded_attention_vs_unfolded(cuda, golden, monkeypatch, B, variant):
-    """The CIFAR-10 UNet's five 16 x 16 attention blocks run folded (variant 3, the default: attn_block3_kernel
-    alone; variant 2: g GEMM + attn_block_kernel; no q / k / v planes in either): whole forwards within 1e-5 of
-    the unfolded path (same weights, same inputs), and the folded kernels are the ones in the plan."""
+    """The CIFAR-10 UNet's five 16 x 16 attention blocks run folded (variant 4, the default, and 3:
+    attn_block4_kernel / attn_block3_kernel alone; variant 2: g GEMM + attn_block_kernel; no q / k / v planes in
+    any): whole forwards within 1e-5 of the unfolded path (same weights, same inputs), and the folded kernels
+    are the ones in the plan."""
     monkeypatch.setenv('DM_ATTN_BLOCK', variant)
     kname = {'2': 'attn_block_kernel', '3': 'attn_block3_kernel', '4': 'attn_block4_kernel'}[variant]
     _, meta = golden('forward')

@@ -37,14 +37,14 @@ def main():
     L.dm_debug_ab_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
     assert L.dm_debug_ab_stamps(buf.ctypes.data, nblk) == 0
     s = buf.astype(np.int64)
-    if os.environ.get("DM_ATTN_BLOCK", "3") == "2":
+    if os.environ.get("DM_ATTN_BLOCK", "4") == "2":
         names = ['T (At xn^T)', 'T finalize + split', 'S (xn T^T)', 'softmax', 'P g', 'epilogue']
     else:
         names = ['T (At xn^T)', 'T finalize + split', 'keys: S + softmax + P xn', 'O finalize', 'Y = Wg O',
                  'epilogue']
     tot = s[:, 6] - s[:, 0]
     wall = s[:, 9] - s[:, 8]
-    print(f'attn_block kernel (variant {os.environ.get("DM_ATTN_BLOCK", "3")}): {nblk} work-groups, wall (stamps) {(s[:, 9].max() - s[:, 8].min()) / 100.0:.1f} us, '
+    print(f'attn_block kernel (variant {os.environ.get("DM_ATTN_BLOCK", "4")}): {nblk} work-groups, wall (stamps) {(s[:, 9].max() - s[:, 8].min()) / 100.0:.1f} us, '
           f'work-group cycles mean {tot.mean():.0f}, clock {np.mean(tot / np.maximum(wall, 1)) / 100:.3f} GHz')
     for i, n in enumerate(names):
         v = s[:, i + 1] - s[:, i]
