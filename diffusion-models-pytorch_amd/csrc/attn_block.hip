@@ -879,35 +879,46 @@ __device__ __forceinline__ void kstep1(const _Float16* img, int l16, int q, cons
   }
 }
 
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) attn_block4_kernel(AttnBlockArgs a) {
-  __shared__ __attribute__((aligned(16))) float lds[kBQ * kOP];
+// NWV waves of 16 queries per work-group: 8 (variant 4: 128 queries, one work-group per CU) or 4 (variant 5:
+// 64 queries, two independent work-groups per CU -- the two waves of a SIMD no longer meet at the same barriers
+// -- at twice the L2 -> LDS staging of the weight images per query).
+template <int NWV>
+__global__ void __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) attn_block4_kernel(AttnBlockArgs a) {
+  constexpr int NT = NWV * 64, QB = 16 * NWV, NS = 2048 / NT;   // threads, queries, staging slots per thread
+  // staging register sets: 2 (loads two k-steps / key chunks ahead) with 4 slots per thread, 1 (one ahead) with 8
+  constexpr int RD = NS == 4 ? 2 : 1;
+  constexpr int LDSF = QB * kOP > kKImg ? QB * kOP : kKImg;     // floats: epilogue rows / two key-chunk images
+  static_assert(2 * kStepH <= 2 * LDSF && 2 * kKImg <= 2 * LDSF, "staging fits");
+  __shared__ __attribute__((aligned(16))) float lds[LDSF];
   __shared__ __attribute__((aligned(16))) float tab[2][kBC];
   _Float16* stg = reinterpret_cast<_Float16*>(lds);
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int l16 = lane & 15, q = lane >> 4;
   const int bid = xcd_remap_p(blockIdx.x, gridDim.x);
-  const int b = bid >> 1, qh = bid & 1;
+  const int b = bid / (kBL / QB), qh = bid - b * (kBL / QB);
   const float* xb = a.x + (size_t)b * kBL * a.x_pitch;
-  const int qrow0 = qh * kBQ + wave * 16;   // this wave's 16 queries
+  const int qrow0 = qh * QB + wave * 16;   // this wave's 16 queries
   const float xs = ldexpf(1.f, a.ex);
   bool bad = false;
-  for (int i = t; i < kBC; i += 512) {
+  for (int i = t; i < kBC; i += NT) {
     tab[0][i] = a.gsc[(size_t)b * kBC + i];
     tab[1][i] = a.gsh[(size_t)b * kBC + i];
   }
 
-  f4 rg[2][4];
-  // weight images (At, Wg'): verbatim copies of split_conv_weights' k-step regions, 4 x 16 B per thread
+  f4 rg[RD][NS];
+  // weight images (At, Wg'): verbatim copies of split_conv_weights' k-step regions, NS x 16 B per thread
   auto load_w = [&](const _Float16* img, int kk, int s, f4& r) {
-    r = reinterpret_cast<const f4*>(img + (size_t)kk * kStepH)[t + 512 * s];
+    r = reinterpret_cast<const f4*>(img + (size_t)kk * kStepH)[t + NT * s];
   };
-  auto store_w = [&](int buf, int s, const f4& r) { reinterpret_cast<f4*>(stg + buf * kStepH)[t + 512 * s] = r; };
-  // key chunk kc: variant 3's key / run mapping on wave & 3; waves 0-3 take the 32-channel groups 0-3, waves
-  // 4-7 groups 4-7 (slot u = group 4 (wave >> 2) + u)
+  auto store_w = [&](int buf, int s, const f4& r) { reinterpret_cast<f4*>(stg + buf * kStepH)[t + NT * s] = r; };
+  // key chunk kc: variant 3's key / run mapping on wave & 3; with 8 waves, waves 0-3 take the 32-channel
+  // groups 0-3 and waves 4-7 groups 4-7 (slot u = group 4 (wave >> 2) + u); with 4 waves every thread all 8
   const int krun = lane & 7, kk2 = (lane >> 3) & 1, kgrp = lane >> 4;
   const int kkey3 = 8 * (wave & 3) + 4 * (kgrp >> 1) + 2 * kk2 + (kgrp & 1);
-  const int sg0 = 4 * (wave >> 2);
+  const int sg0 = NWV == 8 ? 4 * (wave >> 2) : 0;
+  // staging slot of the mid-step callbacks: NS = 4 at even tiles / key steps, NS = 8 at every one
+  constexpr int SD = 8 / NS;
   auto load_k = [&](int kc, int u, f4& r) {
     r = *reinterpret_cast<const f4*>(xb + (size_t)(32 * kc + kkey3) * a.x_pitch + 32 * (sg0 + u) + 4 * krun);
   };
@@ -956,14 +967,14 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   };
   zero_acc();
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
+  for (int u = 0; u < NS; ++u) {
     load_w(a.at_img, 0, u, rg[0][u]);
-    load_w(a.at_img, 1, u, rg[1][u]);
+    if (RD == 2) load_w(a.at_img, 1, u, rg[RD - 1][u]);
   }
   load_xq(0, rx[0]);
   load_xq(1, rx[1]);
 #pragma unroll
-  for (int u = 0; u < 4; ++u) store_w(0, u, rg[0][u]);
+  for (int u = 0; u < NS; ++u) store_w(0, u, rg[0][u]);
   __syncthreads();
 #pragma unroll
   for (int kk = 0; kk < 8; ++kk) {
@@ -971,19 +982,19 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     xq_frag(kk, rx[kk & 1], bf);
     if (kk + 2 < 8) load_xq(kk + 2, rx[kk & 1]);
     kstep1(stg + (kk & 1) * kStepH, l16, q, bf, acc, [&](int tt) {
-      if (tt & 1) return;
+      if (tt % SD) return;
       if (tt < 8) {
-        if (kk + 2 < 8) load_w(a.at_img, kk + 2, tt >> 1, rg[kk & 1][tt >> 1]);
+        if (kk + RD < 8) load_w(a.at_img, kk + RD, tt / SD, rg[(kk + RD) % RD][tt / SD]);
       } else if (kk + 1 < 8) {
-        store_w((kk + 1) & 1, (tt - 8) >> 1, rg[(kk + 1) & 1][(tt - 8) >> 1]);
+        store_w((kk + 1) & 1, (tt - 8) / SD, rg[(kk + 1) % RD][(tt - 8) / SD]);
       }
     });
     __syncthreads();
   }
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
+  for (int u = 0; u < NS; ++u) {
     load_k(0, u, rg[0][u]);
-    load_k(1, u, rg[1][u]);
+    if (RD == 2) load_k(1, u, rg[RD - 1][u]);
   }
   f16x8 tp[8][2];
   float tun;
@@ -1022,7 +1033,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
 
   // ------------------------------------------------------------------ 2. one pass over the keys (chunks of 32)
 #pragma unroll
-  for (int u = 0; u < 4; ++u) store_k(0, u, rg[0][u]);
+  for (int u = 0; u < NS; ++u) store_k(0, u, rg[0][u]);
   __syncthreads();
   zero_acc();   // O^T accumulators
   float m_run = -INFINITY, l_run = 0.f;
@@ -1041,7 +1052,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
         av[1] = *reinterpret_cast<const f16x8*>(pr + kKPiece);
         mma3(av, tp[ks], sacc[kt]);
       }
-      if (kc + 2 < 8 && !(ks & 1)) load_k(kc + 2, ks >> 1, rg[kc & 1][ks >> 1]);
+      if (kc + RD < 8 && ks % SD == 0) load_k(kc + RD, ks / SD, rg[(kc + RD) % RD][ks / SD]);
     }
     f16x8 pp[2];
     {
@@ -1082,15 +1093,15 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
           av[p] = f16x8{lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
         }
         mma3(av, pp, acc[ot]);
-        if (ot >= 8 && !(ot & 1) && kc + 1 < 8) store_k((kc + 1) & 1, (ot - 8) >> 1, rg[(kc + 1) & 1][(ot - 8) >> 1]);
+        if (ot >= 8 && ot % SD == 0 && kc + 1 < 8) store_k((kc + 1) & 1, (ot - 8) / SD, rg[(kc + 1) % RD][(ot - 8) / SD]);
       }
     }
     __syncthreads();
   }
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
+  for (int u = 0; u < NS; ++u) {
     load_w(a.wg_img, 0, u, rg[0][u]);
-    load_w(a.wg_img, 1, u, rg[1][u]);
+    if (RD == 2) load_w(a.wg_img, 1, u, rg[RD - 1][u]);
   }
   // O x 2^ex = acc / (2^14 l) (the staged keys carry xn x 2^ex), rows in storage order -> the projection's B
   f16x8 op[8][2];
@@ -1112,33 +1123,34 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
 
   // ------------------------------------------------------------------ 3. Y^T = Wg' O^T
 #pragma unroll
-  for (int u = 0; u < 4; ++u) store_w(0, u, rg[0][u]);
+  for (int u = 0; u < NS; ++u) store_w(0, u, rg[0][u]);
   __syncthreads();
   zero_acc();
   // output pass mapping: wave -> (64-token chunk ch, 64-column quarter cq); lane -> 4 columns, row of 4
   const int ch = wave >> 2, cq = wave & 3;
   const int c4 = lane & 15, rsub = lane >> 4;
   const int col = 64 * cq + 4 * c4;
-  const int tok0 = qh * kBQ + 64 * ch;
+  const int tok0 = qh * QB + 64 * ch;
   auto load_res = [&](int i, f4& r) {
     r = *reinterpret_cast<const f4*>(xb + (size_t)(tok0 + 4 * i + rsub) * a.x_pitch + col);
   };
 #pragma unroll
   for (int kk = 0; kk < 8; ++kk) {
     kstep1(stg + (kk & 1) * kStepH, l16, q, op[kk], acc, [&](int tt) {
-      if (tt & 1) return;
+      if (tt % SD) return;
       if (tt < 8) {
-        if (kk + 2 < 8) load_w(a.wg_img, kk + 2, tt >> 1, rg[kk & 1][tt >> 1]);
-        else load_res(4 * (kk - 6) + (tt >> 1), rg[kk & 1][tt >> 1]);   // residual rows 0 .. 7
+        if (kk + RD < 8) load_w(a.wg_img, kk + RD, tt / SD, rg[(kk + RD) % RD][tt / SD]);
+        else load_res(NS * (kk + RD - 8) + tt / SD, rg[(kk + RD) % RD][tt / SD]);   // residual rows 0 .. RD NS - 1
       } else if (kk + 1 < 8) {
-        store_w((kk + 1) & 1, (tt - 8) >> 1, rg[(kk + 1) & 1][(tt - 8) >> 1]);
+        store_w((kk + 1) & 1, (tt - 8) / SD, rg[(kk + 1) % RD][(tt - 8) / SD]);
       }
     });
     __syncthreads();
   }
-  f4 xr2[8];
+  constexpr int NX = 16 - RD * NS;   // residual rows loaded after the loop
+  f4 xr2[NX > 0 ? NX : 1];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) load_res(8 + i, xr2[i]);
+  for (int i = 0; i < NX; ++i) load_res(RD * NS + i, xr2[i]);
   if (bad && a.range_flag) *a.range_flag = 1;
 
   // ------------------------------------------------------------------ 4. y = x + Y + cb, GroupNorm statistics
@@ -1155,7 +1167,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   for (int i = 0; i < 16; ++i) {
     const int tok = tok0 + 4 * i + rsub;
     const f4 o = *reinterpret_cast<const f4*>(lds + (64 * ch + 4 * i + rsub) * kOP + col);
-    const f4 xr = i < 4 ? rg[0][i & 3] : i < 8 ? rg[1][i & 3] : xr2[i & 7];
+    const f4 xr = i < NS ? rg[0][i % NS] : i < RD * NS ? rg[RD - 1][i % NS] : xr2[(i - RD * NS) % (NX > 0 ? NX : 1)];
     const f4 yv = xr + (o + cb4);
     *reinterpret_cast<f4*>(a.y + ((size_t)b * kBL + tok) * a.y_pitch + col) = yv;
 #pragma unroll
@@ -1221,7 +1233,7 @@ int attn_perm_cols(const float* wg, float* wgp, int C, hipStream_t st) {
 
 int attn_block(const AttnBlockArgs& a, hipStream_t st) {
   auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-  DM_REQUIRE(a.variant >= 2 && a.variant <= 4, "attention block: variant 2, 3 or 4");
+  DM_REQUIRE(a.variant >= 2 && a.variant <= 5, "attention block: variant 2 .. 5");
   DM_REQUIRE(a.B > 0 && a.x && a.y && a.gsc && a.gsh && a.at_img && a.at_rowscale && a.w &&
                  (a.variant == 2 ? a.g_plane != nullptr : (a.wg_img && a.wg_rowscale && a.cb)),
              "attention block: null argument");
@@ -1232,8 +1244,10 @@ int attn_block(const AttnBlockArgs& a, hipStream_t st) {
   DM_REQUIRE(!a.gn_part || (a.gn_G > 0 && kBC % a.gn_G == 0 && kBC / a.gn_G >= 4 && kBC / a.gn_G <= 32 &&
                             ((kBC / a.gn_G) & (kBC / a.gn_G - 1)) == 0),
              "attention block: GroupNorm statistics need groups of 4, 8, 16 or 32 channels");
-  if (a.variant == 4)
-    hipLaunchKernelGGL(attn_block4_kernel, dim3(a.B * (kBL / kBQ)), dim3(512), 0, st, a);
+  if (a.variant == 5)
+    hipLaunchKernelGGL(attn_block4_kernel<4>, dim3(a.B * (kBL / 64)), dim3(256), 0, st, a);
+  else if (a.variant == 4)
+    hipLaunchKernelGGL(attn_block4_kernel<8>, dim3(a.B * (kBL / 128)), dim3(512), 0, st, a);
   else if (a.variant == 3)
     hipLaunchKernelGGL(attn_block3_kernel, dim3(a.B * (kBL / kBQ)), dim3(256), 0, st, a);
   else

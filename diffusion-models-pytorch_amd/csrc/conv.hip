@@ -278,7 +278,7 @@ int conv2d_igemm(const ConvArgs& a, hipStream_t st) {
   }
   const long M = (long)a.B * a.Hout * a.Wout;
   DM_REQUIRE(M > 0 && M < (1L << 31), "conv: M out of range");
-  DM_REQUIRE(a.tile >= 0 && a.tile <= 18, "conv: tile must be 0..18");
+  DM_REQUIRE(a.tile >= 0 && a.tile <= 19, "conv: tile must be 0..19");
   const int mode = conv_mode(a);
   const int pick = conv_pick(a);
   DM_REQUIRE(!a.gn_part || conv_can_emit_gn(a), "conv: GroupNorm statistics need a 128-row halo-patch tile, "
@@ -318,6 +318,7 @@ int conv_pick(const ConvArgs& a) {
   if (a.tile == 16 && conv_k32_variant_ok(a, 7)) return 8;  // forced K32 512-thread wide-map tiles
   if (a.tile == 17 && conv_k32_variant_ok(a, 8)) return 3;  // forced K32 big-table 128 x 128 tiles
   if (a.tile == 18 && conv_k32_variant_ok(a, 9)) return 5;  // forced K32 stride-2 tiles
+  if (a.tile == 19 && conv_k32_variant_ok(a, 10)) return 3;  // forced K32 2-D tiles of wide maps
   if (conv_pw_ok(a)) {  // split 1x1: 128x128 tiles when they still give >= 2 blocks per CU, else 128x64
     const long M = (long)(a.pick_B > 0 ? a.pick_B : a.B) * a.Hout * a.Wout;
     return (a.Cout >= 128 && ((M + 127) / 128) * ((a.Cout + 127) / 128) >= 512) ? 3 : 4;
@@ -342,6 +343,9 @@ bool conv_can_emit_gn(const ConvArgs& a) {
   // the K32 stride-2 tiles: a block's 64 rows are one 64-pixel chunk (two 32-row waves per column slice)
   if (a.stride == 2 && conv_k32_pick(a) == 9)
     return (a.Hout * a.Wout) % 64 == 0 && a.gn_G > 0 && a.Cout % a.gn_G == 0 && 32 % (a.Cout / a.gn_G) == 0;
+  // the K32 2-D tiles of wide maps: each wave's 64 rows are one tile's 64 pixels (a disjoint cover of the image)
+  if (conv_k32_pick(a) == 10)
+    return a.gn_G > 0 && a.Cout % a.gn_G == 0 && 32 % (a.Cout / a.gn_G) == 0;
   const int pick = conv_pick(a);
   if (pick != 3 && pick != 4 && pick != 6 && pick != 7 && pick != 8) return false;  // waves own whole 64-row chunks
   if (conv_k32_pick(a) && a.Cout % a.gn_G == 0 && a.Cout / a.gn_G > 32) return false;  // K32: groups within 32 columns

@@ -66,6 +66,7 @@ struct StagedEpilogue {
   int M, HWo, b0, c4, rsub, ncol, nc;
   bool c_ok, one_image;
   int sub_w = 0, sub_ho = 0, sub_wo = 0, sub_py = 0, sub_px = 0;  // sub-pixel scatter (sub())
+  int t2_wo = 0, t2_th = 0, t2_tw = 0;                             // 2-D tiles (t2d())
   f4 bias4, rv4;
   double gs[4], gq[4];
 
@@ -94,7 +95,20 @@ struct StagedEpilogue {
     sub_py = py;
     sub_px = px;
   }
+  // 2-D tiles of wide maps: tile row m enumerates the image's TH x TW tiles in row-major order, row-major inside
+  // the tile (conv_k32.hip T2D)
+  __device__ __forceinline__ void t2d(int wo, int th, int tw) {
+    t2_wo = wo;
+    t2_th = th;
+    t2_tw = tw;
+  }
   __device__ __forceinline__ size_t out_row(int m) const {
+    if (t2_wo) {
+      const int bb = m / HWo, rr = m - bb * HWo, tsz = t2_th * t2_tw;
+      const int tl = rr / tsz, r = rr - tl * tsz, ntx = t2_wo / t2_tw;
+      const int ty = tl / ntx, tx = tl - ty * ntx, iy = r / t2_tw;
+      return (size_t)bb * HWo + (size_t)(ty * t2_th + iy) * t2_wo + tx * t2_tw + (r - iy * t2_tw);
+    }
     if (!sub_w) return (size_t)m;
     const int bb = m / HWo, rr = m - bb * HWo;
     const int iy = rr / sub_w, ix = rr - iy * sub_w;

@@ -68,6 +68,16 @@ __device__ unsigned long long g_k32_stamps[65536][8];
 #define K32_RSTAMP(k) do {} while (0)
 #endif
 
+// T2D tiles: GEMM row m -> pixel row of the NHWC tensor (image m / HWo, tile (m % HWo) / (TH TW) in row-major
+// tile order, row-major inside the tile)
+__device__ __forceinline__ size_t t2d_pixel(int m, int HWo, int Wo, int TH, int TW) {
+  const int bb = m / HWo, rr = m - bb * HWo, tsz = TH * TW;
+  const int tl = rr / tsz, r = rr - tl * tsz, ntx = Wo / TW;
+  const int ty = tl / ntx, tx = tl - ty * ntx;
+  const int iy = r / TW;
+  return ((size_t)bb * HWo + (size_t)(ty * TH + iy) * Wo) + tx * TW + (r - iy * TW);
+}
+
 // KSPLIT: split-K over 32-channel chunks for maps of <= 16 pixels (64-row tiles of 4 images): raw partial
 // sums to kpart [ksplit][M][Cout], the epilogue in conv_splitk_reduce (conv_patch.hip), as conv_patch3.
 // SUB: the sub-pixel form of nearest-2x + 3x3 (models/modules.py:60-63; conv_patch3 MODE 2): per output
@@ -80,8 +90,12 @@ __device__ unsigned long long g_k32_stamps[65536][8];
 // (2 TH + 1) x (2 Wo + 2) input patch whose columns are stored parity-split (even input columns -1 + 2 u' at
 // u', odd ones after them), so the 16 lanes of a fragment -- consecutive output columns -- read consecutive
 // patch pixels for every tap, as in the stride-1 patch (conflict-free ds_read_b128).
+// T2D: 2-D tiles of wide maps (ADM's 64^2 .. 256^2): a 128-row tile is TH = 4 output rows x TW = 32 columns,
+// the GEMM row index m enumerating pixels tile by tile (t2d_pixel), so the patch is the 32^2 maps' 6 x 34 and the
+// kernel runs as variant 1 does there; the epilogue, the shortcut segment and the GroupNorm chunks (64 rows of
+// one tile: a disjoint cover of the image) map m back to the pixel.
 template <int BM, int BN, int WM, int WN, bool PRO, bool KSPLIT, bool SUB = false, int NT = 256, int MAXP = kMaxP,
-          int TABF = kTab, bool S2 = false>
+          int TABF = kTab, bool S2 = false, bool T2D = false>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) conv_k32_kernel(ConvArgs a, PatchGeom g) {
   constexpr int NWN = BN / WN;
   static_assert((BM / WM) * NWN == NT / 64, "one wave per 64 threads");
@@ -116,8 +130,10 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
   const int m0 = mt * BM, n0 = nt * BN;
   const int HWo = Ho * Wo;
   const int b0 = m0 / HWo;
-  const int y0 = (m0 - b0 * HWo) / Wo;
-  const int x0 = (m0 - b0 * HWo) - y0 * Wo;  // row-segment tiles (64 pixels of a wider row); 0 otherwise
+  // row-segment tiles (64 pixels of a wider row): x0 > 0; 2-D tiles: tile (m0 - b0 HWo) / BM of the image
+  const int tl2 = (m0 - b0 * HWo) / BM, ntx2 = Wo / g.TW;
+  const int y0 = T2D ? (tl2 / ntx2) * g.TH : (m0 - b0 * HWo) / Wo;
+  const int x0 = T2D ? (tl2 - (tl2 / ntx2) * ntx2) * g.TW : (m0 - b0 * HWo) - y0 * Wo;
 
   K32_RSTAMP(5);
   K32_STAMP(0);
@@ -420,7 +436,8 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const float* xsrc[RJ];
 #pragma unroll
     for (int j = 0; j < RJ; ++j)
-      xsrc[j] = a.x2 + (size_t)min(m0 + srow + SROWS * j, M - 1) * a.x2_pitch + 8 * sq;
+      xsrc[j] = a.x2 + (T2D ? t2d_pixel(min(m0 + srow + SROWS * j, M - 1), HWo, Wo, g.TH, g.TW)
+                            : (size_t)min(m0 + srow + SROWS * j, M - 1)) * a.x2_pitch + 8 * sq;
     for (int c2 = 0; c2 < a.Cin2 / kC; ++c2) {
       f4 r[RJ][2];
 #pragma unroll
@@ -457,6 +474,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
   const int wrow0 = m0 + wm * WM;
   Epi epi(a, M, HWo, b0, (HWo % BM) == 0, n0 + wn * WN, lane);
   if (SUB) epi.sub(Wo, a.Hout, a.Wout, py, px);
+  if (T2D) epi.t2d(Wo, g.TH, g.TW);
   float cs[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) cs[j] = a.ws_rowscale[min(n0 + wn * WN + j * 16 + l16, N - 1)];
@@ -922,8 +940,19 @@ static bool conv_k32s_ok(const ConvArgs& a) {
   return staged_epilogue_ok(a) || (a.gn_part && a.Cout % 4 == 0);
 }
 
+static bool t2d_geom(const ConvArgs& a, PatchGeom& g);
+
 int conv_k32_variant_ok(const ConvArgs& a, int v) {
   if (v == 6) return conv_k32s_ok(a) ? 1 : 0;
+  if (v == 10) {
+    if (!(a.ws && a.ws_np == 2 && a.ws_rowscale)) return 0;
+    if (a.Cin1 < kC || a.Cin1 % kC != 0 || a.Cin2 % kC != 0 || a.ksplit > 1 || a.K != 9 * a.Cin1 + a.Cin2) return 0;
+    PatchGeom g;
+    if (!t2d_geom(a, g)) return 0;
+    if (a.pro_scale && 2 * a.Cin1 > kTab) return 0;
+    if (a.gin_part && a.gin_G > kStats) return 0;
+    return staged_epilogue_ok(a) ? 1 : 0;
+  }
   if (v == 9) {
     if (!(a.ws && a.ws_np == 2 && a.ws_rowscale && a.taps == 9 && a.stride == 2 && a.upsample == 0)) return 0;
     if (a.Cin1 < kC || a.Cin1 % kC != 0 || a.Cin2 != 0 || a.ksplit > 1 || a.K != 9 * a.Cin1) return 0;
@@ -1000,6 +1029,25 @@ static bool conv_k32_bigtab_enabled() {
   return !(e && e[0] == '0');
 }
 
+// The 2-D tiles of wide maps (variant 10) unless DM_CONV_K32T2=0 (then variant 7)
+static bool conv_k32_t2d_enabled() {
+  const char* e = std::getenv("DM_CONV_K32T2");
+  return !(e && e[0] == '0');
+}
+
+// variant 10's geometry: 4 output rows x 32 columns per 128-row tile, a 6 x 34 patch
+static bool t2d_geom(const ConvArgs& a, PatchGeom& g) {
+  if (a.stride != 1 || a.upsample != 0 || a.taps != 9 || a.Hin != a.Hout || a.Win != a.Wout) return false;
+  if (a.Wout < 64 || a.Wout % 32 != 0 || a.Hout % 4 != 0) return false;
+  g.TB = 1;
+  g.TH = 4;
+  g.TW = 32;
+  g.PH = 6;
+  g.PW = 34;
+  g.P = 204;
+  return true;
+}
+
 // The stride-2 tiles (variant 9) unless DM_CONV_K32S2=0 (then conv_patch3 MODE 4, kept as their test oracle)
 static bool conv_k32_s2_enabled() {
   const char* e = std::getenv("DM_CONV_K32S2");
@@ -1014,7 +1062,7 @@ static bool conv_k32_small_enabled() {
 }
 
 int conv_k32_pick(const ConvArgs& a) {
-  if (a.tile >= 10 && a.tile <= 18) return conv_k32_variant_ok(a, a.tile - 9) ? a.tile - 9 : 0;
+  if (a.tile >= 10 && a.tile <= 19) return conv_k32_variant_ok(a, a.tile - 9) ? a.tile - 9 : 0;
   if (a.tile != 0 || !conv_k32_enabled()) return 0;
   if (a.stride == 2) {  // at least one block per CU (the nominal batch keeps the choice batch-invariant)
     const long M = (long)(a.pick_B > 0 ? a.pick_B : a.B) * a.Hout * a.Wout;
@@ -1030,6 +1078,7 @@ int conv_k32_pick(const ConvArgs& a) {
     // maps whose whole-row 128-row tiles do not fit the patch image (64^2 .. 256^2): 128-pixel row segments /
     // two-row tiles of 8 waves, else 64-pixel rows / segments
     const int wt = a.upsample == 2 ? a.Win : a.Wout;
+    if (wt >= 64 && conv_k32_t2d_enabled() && conv_k32_variant_ok(a, 10)) return 10;
     if (wt >= 64 && conv_k32_wide_enabled() && conv_k32_variant_ok(a, 7)) return 7;
     if (wt >= 64) return conv_k32_variant_ok(a, 5) ? 5 : 0;
     // 128-row tiles whose GroupNorm tables do not fit kTab: the big-table instantiation (one block per CU)
@@ -1058,6 +1107,9 @@ std::string conv_k32_label(const ConvArgs& a, int v) {
            (a.upsample == 2 ? "true,256,208,8192>" : "false,256,208,8192>");
   if (v == 9)
     return std::string("conv_k32_kernel<64,128,32,32,") + (a.pro_scale ? "true," : "false,") + "false,false,512,392,2048,true>";
+  if (v == 10)
+    return std::string("conv_k32_kernel<128,128,64,64,") + (a.pro_scale ? "true," : "false,") +
+           "false,false,256,208,2048,false,true>";
   static const char* names[] = {"", "conv_k32_kernel<128,128,64,64,", "conv_k32_kernel<128,64,64,32,",
                                 "conv_k32_kernel<64,64,32,32,", "conv_k32_kernel<64,128,32,64,",
                                 "conv_k32_kernel<64,128,32,64,"};
@@ -1065,7 +1117,8 @@ std::string conv_k32_label(const ConvArgs& a, int v) {
          (a.upsample == 2 ? "true>" : "false>");
 }
 
-template <int BM, int BN, int WM, int WN, bool KSPLIT, int NT = 256, int MAXP = kMaxP, int TABF = kTab, bool S2 = false>
+template <int BM, int BN, int WM, int WN, bool KSPLIT, int NT = 256, int MAXP = kMaxP, int TABF = kTab, bool S2 = false,
+          bool T2D = false>
 static void launch_k32(const ConvArgs& a, const PatchGeom& g, hipStream_t st) {
   const bool sub = a.upsample == 2;
   const int M = sub ? a.B * a.Hin * a.Win : a.B * a.Hout * a.Wout;
@@ -1082,15 +1135,15 @@ static void launch_k32(const ConvArgs& a, const PatchGeom& g, hipStream_t st) {
     }
   }
   if (a.pro_scale)
-    hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, true, KSPLIT, false, NT, MAXP, TABF, S2>), dim3(blocks), dim3(NT),
-                       0, st, a, g);
+    hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, true, KSPLIT, false, NT, MAXP, TABF, S2, T2D>), dim3(blocks),
+                       dim3(NT), 0, st, a, g);
   else
-    hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, false, KSPLIT, false, NT, MAXP, TABF, S2>), dim3(blocks),
+    hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, false, KSPLIT, false, NT, MAXP, TABF, S2, T2D>), dim3(blocks),
                        dim3(NT), 0, st, a, g);
 }
 
 int conv2d_k32(const ConvArgs& a, int v, hipStream_t st) {
-  DM_REQUIRE(v >= 1 && v <= 9 && conv_k32_variant_ok(a, v), "conv: shape not supported by the K = 32 split kernel");
+  DM_REQUIRE(v >= 1 && v <= 10 && conv_k32_variant_ok(a, v), "conv: shape not supported by the K = 32 split kernel");
   PatchGeom g;
   if (v == 6) {
     conv_patch_geom(a, 64, g);
@@ -1105,6 +1158,12 @@ int conv2d_k32(const ConvArgs& a, int v, hipStream_t st) {
       if (pro) hipLaunchKernelGGL((conv_k32s_kernel<true, 8>), dim3(blocks), dim3(512), 0, st, a, g);
       else hipLaunchKernelGGL((conv_k32s_kernel<false, 8>), dim3(blocks), dim3(512), 0, st, a, g);
     }
+    DM_LAUNCH_CHECK();
+    return DM_OK;
+  }
+  if (v == 10) {
+    t2d_geom(a, g);
+    launch_k32<128, 128, 64, 64, false, 256, kMaxP, kTab, false, true>(a, g, st);
     DM_LAUNCH_CHECK();
     return DM_OK;
   }

@@ -1077,7 +1077,8 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
         // DM_ATTN_BLOCK=2: g = xn Wg^T + cb from linear_k32 as the fp16x2 plane, then attn_block_kernel
         // (113 + 67 us)
         const char* avs = std::getenv("DM_ATTN_BLOCK");
-        const int av = avs && avs[0] == '2' ? 2 : avs && avs[0] == '3' ? 3 : 4;
+        // DM_ATTN_BLOCK=5: variant 4's kernel on 64-query work-groups (two per CU)
+        const int av = avs && avs[0] >= '2' && avs[0] <= '5' ? avs[0] - '0' : 4;
         const bool v3 = av != 2;
         ab.variant = av;
         if (v3) {
@@ -1100,7 +1101,8 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
           // v2: T, S, P g; x read, y written, the g^T plane (fp16x2, 4 B per element) read
           const double fl = 2.0 * B * ((v3 ? 2.0 : 1.0) * hw * C * C + 2.0 * hw * hw * C);
           const double by = 4.0 * B * hw * C * (v3 ? 2.0 : 3.0);
-          add(av == 4 ? "attn_block4_kernel" : v3 ? "attn_block3_kernel" : "attn_block_kernel", fl, by,
+          add(av == 5 ? "attn_block4_kernel<4>" : av == 4 ? "attn_block4_kernel<8>" : v3 ? "attn_block3_kernel"
+                                                                                          : "attn_block_kernel", fl, by,
               [=](hipStream_t st) { return attn_block(ab, st); });
           x_cur = y;
           continue;

@@ -24,14 +24,15 @@ def _labels(h):
     return [op['label'] for op in dmhip.unet_profile_read(h)]
 
 
-@pytest.mark.parametrize('B,variant', [(2, '3'), (7, '3'), (3, '2'), (5, '4')])
+@pytest.mark.parametrize('B,variant', [(2, '3'), (7, '3'), (3, '2'), (5, '4'), (3, '5')])
 def test_folded_attention_vs_unfolded(cuda, golden, monkeypatch, B, variant):
     """The CIFAR-10 UNet's five 16 x 16 attention blocks run folded (variant 4, the default, and 3:
     attn_block4_kernel / attn_block3_kernel alone; variant 2: g GEMM + attn_block_kernel; no q / k / v planes in
     any): whole forwards within 1e-5 of the unfolded path (same weights, same inputs), and the folded kernels
     are the ones in the plan."""
     monkeypatch.setenv('DM_ATTN_BLOCK', variant)
-    kname = {'2': 'attn_block_kernel', '3': 'attn_block3_kernel', '4': 'attn_block4_kernel'}[variant]
+    kname = {'2': 'attn_block_kernel', '3': 'attn_block3_kernel', '4': 'attn_block4_kernel<8>',
+             '5': 'attn_block4_kernel<4>'}[variant]
     _, meta = golden('forward')
     g = torch.Generator().manual_seed(31)
     x = torch.randn((B, 3, 32, 32), generator=g).to(cuda)
@@ -82,19 +83,21 @@ def test_folded_attention_batch_invariance(cuda, golden, monkeypatch, variant):
 
 
 def test_folded_attention_8_waves_bit_identical(cuda, golden, monkeypatch):
-    """Variant 4 (8 waves of 16 queries) runs variant 3's MFMA sequence per output element with the same
-    staging layouts and scales: whole forwards equal bit for bit."""
+    """Variants 4 (8 waves of 16 queries) and 5 (4 waves of 16 queries, two work-groups per CU) run variant
+    3's MFMA sequence per output element with the same staging layouts and scales: whole forwards equal bit for
+    bit."""
     _, meta = golden('forward')
     g = torch.Generator().manual_seed(34)
     x = torch.randn((4, 3, 32, 32), generator=g).to(cuda)
     t = torch.randint(0, 1000, (4, ), generator=g).to(cuda)
     outs = {}
-    for v in ('3', '4'):
+    for v in ('3', '4', '5'):
         monkeypatch.setenv('DM_ATTN_BLOCK', v)
         model, _ = _model(meta, 'cifar10', cuda)
         outs[v] = model(x, t)
         del model
     assert torch.equal(outs['3'], outs['4'])
+    assert torch.equal(outs['3'], outs['5'])
 
 
 # ------------------------------------------------------------------ DiT accuracy evidence (VERDICT r3 item 3)
@@ -246,3 +249,79 @@ def test_downsample_k32_vs_patch3(cuda, golden, report, monkeypatch):
     report('downsample_k32_maxabs_vs_patch3', err)
     assert torch.isfinite(outs['k32']).all()
     assert err <= 1e-5, err
+
+
+# ------------------------------------------------------------------ 2-D tiles of wide maps (conv_k32.hip T2D)
+@pytest.mark.parametrize('B,Cin,Cout,H,W', [(1, 32, 64, 4, 256), (2, 64, 96, 8, 64), (1, 64, 32, 12, 128),
+                                            (3, 32, 128, 4, 96)])
+def test_t2d_tiles_exact(cuda, B, Cin, Cout, H, W):
+    """Wide maps (ADM 64^2 .. 256^2) on 2-D tiles (tile 19: 4 rows x 32 columns per 128-row tile, the GEMM rows
+    enumerating pixels tile by tile): bias, integer operands bit-exact vs fp64."""
+    from tests.test_gpu_ops import _ints, _nhwc, _pack, _run_conv
+    import torch.nn.functional as F
+    x = _ints((B, Cin, H, W), -2, 3, seed=110)
+    w = _ints((Cout, Cin, 3, 3), -2, 3, seed=111)
+    b = _ints((Cout, ), seed=112)
+    ref = F.conv2d(x.double(), w.double(), b.double(), padding=1).float()
+    y = _run_conv(cuda, _nhwc(x).to(cuda), _pack(w, cuda), Cout, H, W, 9, 1, 0, b.to(cuda), tile=19, split='fp16x2')
+    assert torch.equal(y.cpu(), _nhwc(ref))
+
+
+def test_t2d_tiles_shortcut_residual_rowvec(cuda):
+    """2-D tiles with the ResBlock epilogue pieces: the 1x1 shortcut segment (its rows mapped through the tile
+    order), per-image row vector, residual, output pitch."""
+    from tests.test_gpu_ops import _ints, _nhwc, _pack, _run_conv
+    import torch.nn.functional as F
+    B, C1, C2, Cout, H, W = 2, 64, 32, 64, 8, 128
+    h = _ints((B, C1, H, W), seed=113)
+    x = _ints((B, C2, H, W), seed=114)
+    w2 = _ints((Cout, C1, 3, 3), -2, 3, seed=115)
+    ws = _ints((Cout, C2, 1, 1), seed=116)
+    b = _ints((Cout, ), seed=117)
+    rv = _ints((B, Cout), seed=118)
+    res = _ints((B, Cout, H, W), seed=119)
+    K = 9 * C1 + C2
+    wp = torch.zeros((Cout, K), device=cuda)
+    _pack(w2, cuda, K, 0, wp)
+    _pack(ws, cuda, K, 9 * C1, wp)
+    ref = (F.conv2d(h.double(), w2.double(), b.double(), padding=1) + rv.double()[:, :, None, None]
+           + F.conv2d(x.double(), ws.double()) + res.double()).float()
+    y = _run_conv(cuda, _nhwc(h).to(cuda), wp, Cout, H, W, 9, bias=b.to(cuda), rowvec=rv.to(cuda),
+                  res=_nhwc(res).to(cuda), x2=_nhwc(x).to(cuda), Cin2=C2, y_pitch=72, tile=19, split='fp16x2')
+    assert torch.equal(y[..., :Cout].cpu(), _nhwc(ref))
+    assert torch.isnan(y[..., Cout:]).all()
+
+
+def test_adm256_t2d_vs_row_segments(cuda, golden, report, monkeypatch):  # noqa: C901
+    """The RePaint CelebA-HQ ADM-256 (reference fixture config, B = 1) with its 64^2 .. 256^2 convs on the 2-D
+    tiles (their GroupNorm partials from the epilogue, chunks = 64 pixels of a tile) against the 128-pixel row
+    segments (DM_CONV_K32T2=0): within 1e-5, and the 2-D kernel is in the plan."""
+    from models.adm.unet import UNetModel
+    g, meta = golden('adm')
+    name = 'adm256_celebahq'
+    x = torch.from_numpy(g[f'{name}_x']).to(cuda)
+    t = torch.from_numpy(g[f'{name}_t']).to(cuda)
+    y = torch.from_numpy(g[f'{name}_labels']).to(cuda) if f'{name}_labels' in g else None
+    outs = {}
+    for mode in ('t2d', 'rows'):
+        if mode == 'rows':
+            monkeypatch.setenv('DM_CONV_K32T2', '0')
+        model = UNetModel(**meta['archs'][name]).eval()
+        init_synthetic_(model)
+        model = model.to(cuda)
+        outs[mode] = model(x, t, y).cpu()
+        h = model.native_handle(torch.device(cuda))
+        dmhip.unet_profile_enable(h, 1)
+        model(x, t, y)
+        labels = _labels(h)
+        dmhip.unet_profile_enable(h, 0)
+        assert any(lb.startswith('conv_k32_kernel<128,128,64,64,') and lb.endswith(',2048,false,true>')
+                   for lb in labels) == (mode == 't2d'), labels
+        del model
+        torch.cuda.empty_cache()
+    err = (outs['t2d'] - outs['rows']).abs().max().item()
+    report('adm256_t2d_maxabs_vs_row_segments', err)
+    ref_err = (outs['t2d'] - torch.from_numpy(g[f'{name}_out'])).abs().max().item()
+    report('adm256_t2d_maxabs_vs_reference', ref_err)
+    assert err <= 1e-5, err
+    assert ref_err <= TOL, ref_err
