@@ -343,9 +343,11 @@ bool conv_can_emit_gn(const ConvArgs& a) {
   // the K32 stride-2 tiles: a block's 64 rows are one 64-pixel chunk (two 32-row waves per column slice)
   if (a.stride == 2 && conv_k32_pick(a) == 9)
     return (a.Hout * a.Wout) % 64 == 0 && a.gn_G > 0 && a.Cout % a.gn_G == 0 && 32 % (a.Cout / a.gn_G) == 0;
-  // the K32 2-D tiles of wide maps: each wave's 64 rows are one tile's 64 pixels (a disjoint cover of the image)
+  // the K32 2-D tiles of wide maps: each wave's 64 rows are one tile's 64 pixels (a disjoint cover of the image;
+  // of one parity's low-res pixels for the sub-pixel upsample)
   if (conv_k32_pick(a) == 10)
-    return a.gn_G > 0 && a.Cout % a.gn_G == 0 && 32 % (a.Cout / a.gn_G) == 0;
+    return a.gn_G > 0 && a.Cout % a.gn_G == 0 && 32 % (a.Cout / a.gn_G) == 0 &&
+           (a.upsample != 2 || (!std::getenv("DM_GN_NO_SUB") && (a.Cout / a.gn_G) % 4 == 0));
   const int pick = conv_pick(a);
   if (pick != 3 && pick != 4 && pick != 6 && pick != 7 && pick != 8) return false;  // waves own whole 64-row chunks
   if (conv_k32_pick(a) && a.Cout % a.gn_G == 0 && a.Cout / a.gn_G > 32) return false;  // K32: groups within 32 columns

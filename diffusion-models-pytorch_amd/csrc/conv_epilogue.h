@@ -103,11 +103,13 @@ struct StagedEpilogue {
     t2_tw = tw;
   }
   __device__ __forceinline__ size_t out_row(int m) const {
-    if (t2_wo) {
+    if (t2_wo) {  // (pixel of the tiled map: the output, or the sub-pixel conv's low-res map, then scattered)
       const int bb = m / HWo, rr = m - bb * HWo, tsz = t2_th * t2_tw;
       const int tl = rr / tsz, r = rr - tl * tsz, ntx = t2_wo / t2_tw;
-      const int ty = tl / ntx, tx = tl - ty * ntx, iy = r / t2_tw;
-      return (size_t)bb * HWo + (size_t)(ty * t2_th + iy) * t2_wo + tx * t2_tw + (r - iy * t2_tw);
+      const int ty = tl / ntx, tx = tl - ty * ntx, ry = r / t2_tw;
+      const int iy = ty * t2_th + ry, ix = tx * t2_tw + (r - ry * t2_tw);
+      if (sub_w) return ((size_t)bb * sub_ho + 2 * iy + sub_py) * sub_wo + 2 * ix + sub_px;
+      return (size_t)bb * HWo + (size_t)iy * t2_wo + ix;
     }
     if (!sub_w) return (size_t)m;
     const int bb = m / HWo, rr = m - bb * HWo;

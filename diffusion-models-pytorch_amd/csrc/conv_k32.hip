@@ -946,7 +946,8 @@ int conv_k32_variant_ok(const ConvArgs& a, int v) {
   if (v == 6) return conv_k32s_ok(a) ? 1 : 0;
   if (v == 10) {
     if (!(a.ws && a.ws_np == 2 && a.ws_rowscale)) return 0;
-    if (a.Cin1 < kC || a.Cin1 % kC != 0 || a.Cin2 % kC != 0 || a.ksplit > 1 || a.K != 9 * a.Cin1 + a.Cin2) return 0;
+    if (a.Cin1 < kC || a.Cin1 % kC != 0 || a.Cin2 % kC != 0 || a.ksplit > 1) return 0;
+    if (a.upsample == 2 ? (a.Cin2 != 0 || a.K != 4 * a.Cin1) : a.K != 9 * a.Cin1 + a.Cin2) return 0;
     PatchGeom g;
     if (!t2d_geom(a, g)) return 0;
     if (a.pro_scale && 2 * a.Cin1 > kTab) return 0;
@@ -1037,8 +1038,11 @@ static bool conv_k32_t2d_enabled() {
 
 // variant 10's geometry: 4 output rows x 32 columns per 128-row tile, a 6 x 34 patch
 static bool t2d_geom(const ConvArgs& a, PatchGeom& g) {
-  if (a.stride != 1 || a.upsample != 0 || a.taps != 9 || a.Hin != a.Hout || a.Win != a.Wout) return false;
-  if (a.Wout < 64 || a.Wout % 32 != 0 || a.Hout % 4 != 0) return false;
+  // tiles over the output map, or over the low-res map of the sub-pixel upsample (4 parities x 4 taps)
+  const bool sub = a.upsample == 2;
+  if (a.stride != 1 || a.taps != 9 || (a.upsample != 0 && !sub)) return false;
+  if (sub ? (a.Hout != 2 * a.Hin || a.Wout != 2 * a.Win) : (a.Hin != a.Hout || a.Win != a.Wout)) return false;
+  if (a.Win < 64 || a.Win % 32 != 0 || a.Hin % 4 != 0) return false;
   g.TB = 1;
   g.TH = 4;
   g.TW = 32;
@@ -1108,8 +1112,8 @@ std::string conv_k32_label(const ConvArgs& a, int v) {
   if (v == 9)
     return std::string("conv_k32_kernel<64,128,32,32,") + (a.pro_scale ? "true," : "false,") + "false,false,512,392,2048,true>";
   if (v == 10)
-    return std::string("conv_k32_kernel<128,128,64,64,") + (a.pro_scale ? "true," : "false,") +
-           "false,false,256,208,2048,false,true>";
+    return std::string("conv_k32_kernel<128,128,64,64,") + (a.pro_scale ? "true," : "false,") + "false," +
+           (a.upsample == 2 ? "true" : "false") + ",256,208,2048,false,true>";
   static const char* names[] = {"", "conv_k32_kernel<128,128,64,64,", "conv_k32_kernel<128,64,64,32,",
                                 "conv_k32_kernel<64,64,32,32,", "conv_k32_kernel<64,128,32,64,",
                                 "conv_k32_kernel<64,128,32,64,"};
@@ -1126,11 +1130,11 @@ static void launch_k32(const ConvArgs& a, const PatchGeom& g, hipStream_t st) {
   if constexpr (!KSPLIT) {
     if (sub) {
       if (a.pro_scale)
-        hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, true, false, true, NT, MAXP, TABF>), dim3(blocks), dim3(NT),
-                           0, st, a, g);
-      else
-        hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, false, false, true, NT, MAXP, TABF>), dim3(blocks),
+        hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, true, false, true, NT, MAXP, TABF, false, T2D>), dim3(blocks),
                            dim3(NT), 0, st, a, g);
+      else
+        hipLaunchKernelGGL((conv_k32_kernel<BM, BN, WM, WN, false, false, true, NT, MAXP, TABF, false, T2D>),
+                           dim3(blocks), dim3(NT), 0, st, a, g);
       return;
     }
   }

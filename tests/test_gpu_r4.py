@@ -267,6 +267,23 @@ def test_t2d_tiles_exact(cuda, B, Cin, Cout, H, W):
     assert torch.equal(y.cpu(), _nhwc(ref))
 
 
+@pytest.mark.parametrize('B,Cin,Cout,H,W', [(1, 32, 64, 4, 64), (2, 64, 32, 8, 128)])
+def test_t2d_tiles_subpixel_exact(cuda, B, Cin, Cout, H, W):
+    """The sub-pixel upsample (nearest-2x + 3x3, models/modules.py:60-63) of a wide low-res map on 2-D tiles
+    (tile 19: 4 x 32 low-res pixels per tile, 4 parity convs of 4 taps, rows scattered to 2 iy + py, 2 ix + px):
+    integer operands bit-exact vs fp64."""
+    from tests.test_gpu_ops import _ints, _nhwc, _pack_subpix, _run_conv
+    import torch.nn.functional as F
+    x = _ints((B, Cin, H, W), -2, 3, seed=120)
+    w = _ints((Cout, Cin, 3, 3), -1, 2, seed=121)
+    b = _ints((Cout, ), seed=122)
+    ref = F.conv2d(F.interpolate(x, scale_factor=2, mode='nearest').double(), w.double(), b.double(),
+                   padding=1).float()
+    y = _run_conv(cuda, _nhwc(x).to(cuda), _pack_subpix(w, cuda), Cout, 2 * H, 2 * W, 9, 1, 2, b.to(cuda), tile=19,
+                  split='fp16x2')
+    assert torch.equal(y.cpu(), _nhwc(ref))
+
+
 def test_t2d_tiles_shortcut_residual_rowvec(cuda):
     """2-D tiles with the ResBlock epilogue pieces: the 1x1 shortcut segment (its rows mapped through the tile
     order), per-image row vector, residual, output pitch."""
