@@ -308,10 +308,14 @@ __global__ void __launch_bounds__(256) presplit_a_kernel(GemmArgs g, void* out_)
   if (bad && g.range_flag) *g.range_flag = 1;
 }
 
-template <int PRO, int WM = 128, int WN = 32>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) linear_k32_kernel(GemmArgs g) {
-  constexpr int BM = kLBM, BN = 128, TM = WM / 16, TN = WN / 16, WD = 2, NWN = BN / WN;
-  static_assert((BM / WM) * NWN == 4, "4 waves");
+// NW = 8 (pre-split A only): 128 x 256 blocks of eight 128 x 32 wave tiles, one block per CU -- the staged A
+// tile feeds twice the MFMA work of the 4-wave block, so the A refills (global loads + LDS stores) per MAC halve.
+template <int PRO, int WM = 128, int WN = 32, int NW = 4>
+__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) linear_k32_kernel(GemmArgs g) {
+  constexpr int BM = kLBM, BN = 32 * NW * WM / BM * WN / 32, TM = WM / 16, TN = WN / 16, WD = 2, NWN = BN / WN;
+  static_assert((BM / WM) * NWN == NW, "one wave tile per wave");
+  static_assert(NW == 4 || PRO == 3, "8 waves: pre-split A only");
+  constexpr int NT = NW * 64, RS = NT / 16, NU = BM / RS;   // PRO 3 loader: row step, rows per thread
   constexpr int STAGE = BM * kLP;  // fp16 elements per buffer
   __shared__ __attribute__((aligned(16))) _Float16 abuf[2 * STAGE];
   // prologue tables of three K stages (staged two stages ahead): [stage % 3][image of the tile][scale, shift][ch]
@@ -352,26 +356,26 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   const int aimg = TABS ? am / rows_img - img0 : 0;  // 0 or 1
   const float2 lns = PRO == 2 ? g.ln_stats[am] : make_float2(0.f, 1.f);
   const float apow = ldexpf(1.f, g.split_ea);
-  f4 ra[2][8];  // A rows of two stages in flight (stage s in ra[s & 1])
+  f4 ra[2][PRO == 3 ? NU : 8];  // A rows of two stages in flight (stage s in ra[s & 1])
   f4 rt;  // threads 0 .. 63: one f4 of a stage's tables
   const int ti = t >> 4, tk = (t & 15) * 4;  // table loader: (image, scale | shift) pair ti, channels tk
-  auto load_a = [&](f4 (&dst)[8], int st) {
+  auto load_a = [&](f4 (&dst)[PRO == 3 ? NU : 8], int st) {
     // whole tiles (the usual case) address their rows linearly from one per-lane base; the last, partial
     // tile clamps each row
-    if (PRO == 3) {  // slot a3s of the stage's 256 B in 8 rows
+    if constexpr (PRO == 3) {  // slot a3s of the stage's 256 B in NU rows
       if (m0 + kLBM <= M) {
         const f4* b0 = asp + (size_t)(m0 + a3r) * a3pitch + 16 * st;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) dst[u] = b0[(size_t)(16 * u) * a3pitch];
+        for (int u = 0; u < NU; ++u) dst[u] = b0[(size_t)(RS * u) * a3pitch];
       } else {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) dst[u] = asp[(size_t)min(m0 + a3r + 16 * u, M - 1) * a3pitch + 16 * st];
+        for (int u = 0; u < NU; ++u) dst[u] = asp[(size_t)min(m0 + a3r + RS * u, M - 1) * a3pitch + 16 * st];
       }
-      return;
-    }
-    const float* p = asrc + 64 * st;
+    } else {
+      const float* p = asrc + 64 * st;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) dst[u] = *reinterpret_cast<const f4*>(p + 4 * u);
+      for (int u = 0; u < 8; ++u) dst[u] = *reinterpret_cast<const f4*>(p + 4 * u);
+    }
   };
   auto load_tab = [&](int st) {
     if (TABS && t < 64) {
@@ -388,13 +392,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   };
   bool bad = false;
   // prologue + split + LDS store of this thread's 32 channels (tables of the stage in tab[buf])
-  auto finish_a = [&](const f4 (&src)[8], int buf, int tb) {
-    if (PRO == 3) {
+  auto finish_a = [&](const f4 (&src)[PRO == 3 ? NU : 8], int buf, int tb) {
+    if constexpr (PRO == 3) {
       _Float16* d3 = abuf + buf * STAGE + a3r * kLP + a3s * 8;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) *reinterpret_cast<f4*>(d3 + 16 * u * kLP) = src[u];
+      for (int u = 0; u < NU; ++u) *reinterpret_cast<f4*>(d3 + RS * u * kLP) = src[u];
       return;
-    }
+    } else {
     _Float16* dst = abuf + buf * STAGE + lrow * kLP + lh * 64;
 #pragma unroll
     for (int u = 0; u < 8; u += 2) {  // k-group u / 2: channels 8 (u / 2) .. + 7 of the step
@@ -423,6 +427,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
       Split<2>::split(v0 * apow, v1 * apow, pc, bad);
       *reinterpret_cast<f16x8*>(dst + (u >> 1) * 8) = pc[0];       // piece 0 at slot 8 s + q
       *reinterpret_cast<f16x8*>(dst + 32 + (u >> 1) * 8) = pc[1];  // piece 1 at slot 8 s + 4 + q
+    }
     }
   };
 
@@ -491,7 +496,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   // GEMMs have 4 stages: one stage did not cover the load latency); after step 1 the tables go to LDS
   // and stage st + 1 is finished into the other buffer (its tables were stored a stage earlier).
   // DM_LIN_ABL (diagnostic builds only, wrong results): 1 no B refills, 2 no A refills, 3 no barrier
-  auto stage = [&](int st, f4 (&cur)[8], f4 (&nxt)[8]) {
+  auto stage = [&](int st, f4 (&cur)[PRO == 3 ? NU : 8], f4 (&nxt)[PRO == 3 ? NU : 8]) {
 #if DM_LIN_ABL != 2
     load_a(cur, min(st + 2, nst - 1));
 #endif
@@ -531,9 +536,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   const int nc = c_ok ? ncol : 0;
   const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
   const f4 bias4 = g.bias ? *reinterpret_cast<const f4*>(g.bias + nc) : zero4;
-  if (g.ap_q && g.ap_L % BM == 0) {  // attention planes from the whole block tile (the loop ended on a barrier)
+  if (NW == 4 && g.ap_q && g.ap_L % BM == 0) {  // attention planes from the whole block tile (the loop ended on a barrier)
     constexpr int TP = BN + 4;
-    static_assert(BM * TP * 4 <= 2 * STAGE * 2, "block tile fits the stage buffers");
+    static_assert(NW != 4 || BM * TP * 4 <= 2 * STAGE * 2, "block tile fits the stage buffers");
     float* tile = reinterpret_cast<float*>(abuf);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -658,11 +663,25 @@ int linear_presplit_a(const GemmArgs& g, _Float16* out, hipStream_t st) {
   return DM_OK;
 }
 
+// DM_LIN_BN256 (A/B): 1 = the 8-wave 128 x 256 blocks for pre-split-A GEMMs with N % 256 == 0, 2 = for all N;
+// read per call (plans capture their launches once)
+bool linear_k32_wide(const GemmArgs& g) {
+  const char* e = std::getenv("DM_LIN_BN256");
+  const int w = e ? std::atoi(e) : 0;
+  return g.as && !g.ap_q && (w >= 2 || (w == 1 && g.N % 256 == 0));
+}
+
 int linear_k32(const GemmArgs& g0, hipStream_t st) {
   DM_REQUIRE(linear_k32_ok(g0), "linear_k32: needs pre-split weights, K % 64 == 0, 16-byte aligned 4-column rows");
   static const int env_gm = std::getenv("DM_LIN_GM") ? std::atoi(std::getenv("DM_LIN_GM")) : 0;  // tile-order A/B
   GemmArgs g = g0;
   if (env_gm > 0 && g.lin_gm == 0) g.lin_gm = env_gm;
+  if (linear_k32_wide(g)) {
+    hipLaunchKernelGGL((linear_k32_kernel<3, 128, 32, 8>), dim3(ceil_div(g.M, kLBM) * ceil_div(g.N, 256)), dim3(512), 0,
+                       st, g);
+    DM_LAUNCH_CHECK();
+    return DM_OK;
+  }
   const int blocks = ceil_div(g.M, kLBM) * ceil_div(g.N, 128);
   if (g.as)
     hipLaunchKernelGGL(linear_k32_kernel<3>, dim3(blocks), dim3(256), 0, st, g);

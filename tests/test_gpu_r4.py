@@ -342,3 +342,35 @@ def test_adm256_t2d_vs_row_segments(cuda, golden, report, monkeypatch):  # noqa:
     report('adm256_t2d_maxabs_vs_reference', ref_err)
     assert err <= 1e-5, err
     assert ref_err <= TOL, ref_err
+
+
+# ------------------------------------------------------------------ 8-wave 128 x 256 linear_k32 blocks (DiT)
+@pytest.mark.parametrize('wide', ['1', '2'])
+def test_linear_k32_wide_blocks_bit_identical(cuda, golden, monkeypatch, wide):
+    """DiT-S/2 (oracle fixture config) with its pre-split-A token GEMMs on the 8-wave 128 x 256 blocks
+    (DM_LIN_BN256=1: N % 256 == 0 only; 2: all, ragged last tiles) equals the 4-wave 128 x 128 form bit for bit
+    (same MFMA sequence per output element), and the wide kernel is in the plan."""
+    from models.dit.model import DiT
+    g, meta = golden('dit')
+    name = 'dit_s2'
+    x = torch.from_numpy(g[f'{name}_x']).to(cuda)
+    t = torch.from_numpy(g[f'{name}_t']).to(cuda)
+    y = torch.from_numpy(g[f'{name}_labels']).to(cuda)
+    outs = {}
+    for mode in ('base', 'wide'):
+        if mode == 'wide':
+            monkeypatch.setenv('DM_LIN_BN256', wide)
+        m = DiT(**meta['archs'][name]).eval()
+        init_synthetic_(m)
+        m = m.to(cuda)
+        outs[mode] = m(x, t, y).cpu()
+        h = m.native_handle(torch.device(cuda))
+        dmhip.unet_profile_enable(h, 1, m._abi)
+        m(x, t, y)
+        labels = [op['label'] for op in dmhip.unet_profile_read(h, m._abi)]
+        dmhip.unet_profile_enable(h, 0, m._abi)
+        assert ('linear_k32_kernel<3,128,32,8>' in labels) == (mode == 'wide'), labels
+        del m
+    assert torch.equal(outs['base'], outs['wide'])
+    err = (outs['wide'] - torch.from_numpy(g[f'{name}_out_y'])).abs().max().item()
+    assert err <= TOL, err
