@@ -509,8 +509,11 @@ def main():
                         skip_unused_noise=wl['diffuser'].skip_unused_noise if wl['diffuser'] else None),
             roofline=roof,
             step_level=dict(model_tflops=round(total_flops / (total_gpu_ms * 1e-3) / 1e12, 2) if total_gpu_ms else None,
-                            # observed forwards are 1 in PROFILE_EVERY: their kernel time scaled to all forwards
-                            kernel_time_frac=round(kernel_s / elapsed, 4) if kernel_s else None),
+                            # observed forwards are 1 in PROFILE_EVERY: their event-summed launch time scaled to
+                            # all forwards, over the wall time. The events bracket every launch of an observed
+                            # forward, which makes that forward a few % slower than the unobserved ones: the ratio
+                            # can exceed 1 and is no kernel-busy fraction
+                            sampled_forward_time_over_wall=round(kernel_s / elapsed, 4) if kernel_s else None),
         )
         if args.workload != 'c3':
             line['config']['bench_workload'] = args.workload

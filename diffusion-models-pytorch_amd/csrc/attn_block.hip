@@ -901,9 +901,31 @@ __global__ void __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2
   const int qrow0 = qh * QB + wave * 16;   // this wave's 16 queries
   const float xs = ldexpf(1.f, a.ex);
   bool bad = false;
-  for (int i = t; i < kBC; i += NT) {
-    tab[0][i] = a.gsc[(size_t)b * kBC + i];
-    tab[1][i] = a.gsh[(size_t)b * kBC + i];
+  if (a.gin_part) {  // gn_finalize (gn.hip) for this image's channels, same expressions
+    const int cpg = kBC / a.gin_G;
+    const double n = (double)kBL * cpg;
+    for (int c = t; c < kBC; c += NT) {
+      const int g = c / cpg;
+      double s1 = 0, s2 = 0;
+      for (int k = 0; k < a.gin_nchunk; ++k) {
+        const double2 v = a.gin_part[((size_t)b * a.gin_nchunk + k) * a.gin_G + g];
+        s1 += v.x;
+        s2 += v.y;
+      }
+      const double m = s1 / n;
+      double var = s2 / n - m * m;
+      if (var < 0) var = 0;
+      const float mu = (float)m;
+      const float rs = (float)(1.0 / sqrt(var + (double)a.gin_eps));
+      const float sc = rs * (a.gin_gamma ? a.gin_gamma[c] : 1.0f);
+      tab[0][c] = sc;
+      tab[1][c] = -sc * mu + (a.gin_beta ? a.gin_beta[c] : 0.0f);
+    }
+  } else {
+    for (int i = t; i < kBC; i += NT) {
+      tab[0][i] = a.gsc[(size_t)b * kBC + i];
+      tab[1][i] = a.gsh[(size_t)b * kBC + i];
+    }
   }
 
   f4 rg[RD][NS];
@@ -1234,10 +1256,13 @@ int attn_perm_cols(const float* wg, float* wgp, int C, hipStream_t st) {
 int attn_block(const AttnBlockArgs& a, hipStream_t st) {
   auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   DM_REQUIRE(a.variant >= 2 && a.variant <= 5, "attention block: variant 2 .. 5");
-  DM_REQUIRE(a.B > 0 && a.x && a.y && a.gsc && a.gsh && a.at_img && a.at_rowscale && a.w &&
+  DM_REQUIRE(!a.gin_part || (a.variant >= 4 && a.gin_G > 0 && kBC % a.gin_G == 0 && a.gin_nchunk > 0),
+             "attention block: in-kernel GroupNorm finalize needs variant 4 / 5 and groups dividing 256 channels");
+  DM_REQUIRE(a.B > 0 && a.x && a.y && (a.gin_part || (a.gsc && a.gsh)) && a.at_img && a.at_rowscale && a.w &&
                  (a.variant == 2 ? a.g_plane != nullptr : (a.wg_img && a.wg_rowscale && a.cb)),
              "attention block: null argument");
-  DM_REQUIRE(a.x_pitch % 4 == 0 && a.y_pitch % 4 == 0 && al16(a.x) && al16(a.y) && al16(a.gsc) && al16(a.gsh) &&
+  DM_REQUIRE(a.x_pitch % 4 == 0 && a.y_pitch % 4 == 0 && al16(a.x) && al16(a.y) &&
+                 (a.gin_part || (al16(a.gsc) && al16(a.gsh))) &&
                  al16(a.at_img) && al16(a.at_rowscale) && al16(a.w) &&
                  (a.variant == 2 ? al16(a.g_plane) : (al16(a.wg_img) && al16(a.wg_rowscale) && al16(a.cb))),
              "attention block: 16-byte aligned rows");

@@ -345,6 +345,12 @@ struct AttnBlockArgs {
   int gn_G;
   int B, ex, eg;
   int* range_flag;
+  // variants 4 / 5: the GroupNorm affine of x from its chunk partials in the kernel (gn_finalize's expressions)
+  // instead of gsc / gsh, when gin_part is set
+  const double2* gin_part;
+  int gin_G, gin_nchunk;
+  const float *gin_gamma, *gin_beta;
+  float gin_eps;
 };
 bool attn_block_ok(int L, int C, int heads);
 // at = s Wk^T Wq, w = s Wk^T bq, wg = Wp Wv, cb = Wp bv + bp (float64 sums, fp32 results)

@@ -1085,10 +1085,17 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
           ab.g_plane = nullptr;
           ab.wg_img = static_cast<const _Float16*>(fw->wgp_img); ab.wg_rowscale = fw->wgp_rs; ab.cb = fw->cb;
         }
+        // variants 4 / 5 finalize the block's GroupNorm statistics themselves (DM_ATTN_GNFIN=1: gn_finalize)
+        const bool infin = av >= 4 && C % G == 0 && !(std::getenv("DM_ATTN_GNFIN") && std::getenv("DM_ATTN_GNFIN")[0] == '1');
+        if (infin) {
+          ab.gin_part = sta; ab.gin_G = G; ab.gin_nchunk = gn_num_chunks(hw);
+          ab.gin_gamma = P(p.gn.g); ab.gin_beta = P(p.gn.b); ab.gin_eps = 1e-5f;
+        }
         if (v3 || linear_k32_ok(gg)) {
-          add("gn_finalize", 0, 8.0 * B * C, [=](hipStream_t st) {
-            return gn_finalize(xin, G, sta, 1e-5f, self->P(p.gn.g), self->P(p.gn.b), gsc, gsh, st);
-          });
+          if (!infin)
+            add("gn_finalize", 0, 8.0 * B * C, [=](hipStream_t st) {
+              return gn_finalize(xin, G, sta, 1e-5f, self->P(p.gn.g), self->P(p.gn.b), gsc, gsh, st);
+            });
           if (!v3) add_gemm(gg);
           gn_ready.erase(y.p);
           const int cpg = C / G;

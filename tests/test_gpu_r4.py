@@ -100,6 +100,29 @@ def test_folded_attention_8_waves_bit_identical(cuda, golden, monkeypatch):
     assert torch.equal(outs['3'], outs['5'])
 
 
+def test_attention_in_kernel_gn_finalize_bit_identical(cuda, golden, monkeypatch):
+    """Variant 4 computes its GroupNorm affine from the chunk partials in the kernel (gn_finalize's expressions
+    and summation order): whole forwards equal the separate gn_finalize launch's (DM_ATTN_GNFIN=1) bit for bit,
+    with five gn_finalize launches fewer per forward."""
+    _, meta = golden('forward')
+    g = torch.Generator().manual_seed(35)
+    x = torch.randn((3, 3, 32, 32), generator=g).to(cuda)
+    t = torch.randint(0, 1000, (3, ), generator=g).to(cuda)
+    outs, nfin = {}, {}
+    for mode in ('kernel', 'launch'):
+        if mode == 'launch':
+            monkeypatch.setenv('DM_ATTN_GNFIN', '1')
+        model, _ = _model(meta, 'cifar10', cuda)
+        outs[mode] = model(x, t)
+        h = _profile_labels(model, cuda)
+        model(x, t)
+        nfin[mode] = _labels(h).count('gn_finalize')
+        dmhip.unet_profile_enable(h, 0)
+        del model
+    assert nfin['launch'] == nfin['kernel'] + 5, nfin
+    assert torch.equal(outs['kernel'], outs['launch'])
+
+
 # ------------------------------------------------------------------ DiT accuracy evidence (VERDICT r3 item 3)
 def _dit_xl2(cuda, golden):
     from models.dit.model import DiT
