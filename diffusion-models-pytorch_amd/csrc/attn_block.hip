@@ -882,7 +882,9 @@ __device__ __forceinline__ void kstep1(const _Float16* img, int l16, int q, cons
 // NWV waves of 16 queries per work-group: 8 (variant 4: 128 queries, one work-group per CU) or 4 (variant 5:
 // 64 queries, two independent work-groups per CU -- the two waves of a SIMD no longer meet at the same barriers
 // -- at twice the L2 -> LDS staging of the weight images per query).
-template <int NWV>
+// OPT (A/B builds of the same arithmetic, DM_ATTN_OPT): bit 1 reads the S A-operands one key step ahead. (A
+// wave-uniform skip of the O rescale when no running maximum moved spills 572 B per lane here, as in variant 3.)
+template <int NWV, int OPT = 0>
 __global__ void __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) attn_block4_kernel(AttnBlockArgs a) {
   constexpr int NT = NWV * 64, QB = 16 * NWV, NS = 2048 / NT;   // threads, queries, staging slots per thread
   // staging register sets: 2 (loads two k-steps / key chunks ahead) with 4 slots per thread, 1 (one ahead) with 8
@@ -1064,17 +1066,37 @@ __global__ void __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2
   for (int kc = 0; kc < 8; ++kc) {
     const _Float16* img = stg + (kc & 1) * kKImg;
     fq sacc[2] = {fq{0.f, 0.f, 0.f, 0.f}, fq{0.f, 0.f, 0.f, 0.f}};
+    if constexpr ((OPT & 2) != 0) {
+      f16x8 sv[2][2][2];   // [buffer][kt][piece]
+      auto rd_s = [&](int ks, f16x8 (&dst)[2][2]) {
 #pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
+        for (int kt = 0; kt < 2; ++kt) {
+          const _Float16* pr = img + (16 * kt + l16) * kKP + 32 * ks + 8 * q;
+          dst[kt][0] = *reinterpret_cast<const f16x8*>(pr);
+          dst[kt][1] = *reinterpret_cast<const f16x8*>(pr + kKPiece);
+        }
+      };
+      rd_s(0, sv[0]);
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        const _Float16* pr = img + (16 * kt + l16) * kKP + 32 * ks + 8 * q;
-        f16x8 av[2];
-        av[0] = *reinterpret_cast<const f16x8*>(pr);
-        av[1] = *reinterpret_cast<const f16x8*>(pr + kKPiece);
-        mma3(av, tp[ks], sacc[kt]);
+      for (int ks = 0; ks < 8; ++ks) {
+        if (ks + 1 < 8) rd_s(ks + 1, sv[(ks + 1) & 1]);
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) mma3(sv[ks & 1][kt], tp[ks], sacc[kt]);
+        if (kc + RD < 8 && ks % SD == 0) load_k(kc + RD, ks / SD, rg[(kc + RD) % RD][ks / SD]);
       }
-      if (kc + RD < 8 && ks % SD == 0) load_k(kc + RD, ks / SD, rg[(kc + RD) % RD][ks / SD]);
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          const _Float16* pr = img + (16 * kt + l16) * kKP + 32 * ks + 8 * q;
+          f16x8 av[2];
+          av[0] = *reinterpret_cast<const f16x8*>(pr);
+          av[1] = *reinterpret_cast<const f16x8*>(pr + kKPiece);
+          mma3(av, tp[ks], sacc[kt]);
+        }
+        if (kc + RD < 8 && ks % SD == 0) load_k(kc + RD, ks / SD, rg[(kc + RD) % RD][ks / SD]);
+      }
     }
     f16x8 pp[2];
     {
@@ -1271,8 +1293,12 @@ int attn_block(const AttnBlockArgs& a, hipStream_t st) {
              "attention block: GroupNorm statistics need groups of 4, 8, 16 or 32 channels");
   if (a.variant == 5)
     hipLaunchKernelGGL(attn_block4_kernel<4>, dim3(a.B * (kBL / 64)), dim3(256), 0, st, a);
-  else if (a.variant == 4)
-    hipLaunchKernelGGL(attn_block4_kernel<8>, dim3(a.B * (kBL / 128)), dim3(512), 0, st, a);
+  else if (a.variant == 4) {
+    const int opt = std::getenv("DM_ATTN_OPT") ? std::atoi(std::getenv("DM_ATTN_OPT")) : 0;  // read per plan build
+    const dim3 grid(a.B * (kBL / 128));
+    if (opt == 2) hipLaunchKernelGGL((attn_block4_kernel<8, 2>), grid, dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((attn_block4_kernel<8, 0>), grid, dim3(512), 0, st, a);
+  }
   else if (a.variant == 3)
     hipLaunchKernelGGL(attn_block3_kernel, dim3(a.B * (kBL / kBQ)), dim3(256), 0, st, a);
   else
