@@ -767,11 +767,16 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
     c.ksplit = ks;
     c.kpart = kpart_ws;
   };
+  static const bool plan_debug = std::getenv("DM_PLAN_DEBUG") != nullptr;  // diagnostics: each conv's shape
   auto add_conv = [&](ConvArgs c) {
     maybe_split(c);
     split_for(c);
     double fl, by;
     conv_cost(c, fl, by);
+    if (plan_debug)
+      fprintf(stderr, "[plan] %s B %d %dx%d -> %dx%d Cin %d + %d Cout %d stride %d up %d pro %d gin %d ksplit %d\n",
+              conv_label(c).c_str(), c.B, c.Hin, c.Win, c.Hout, c.Wout, c.Cin1, c.Cin2, c.Cout, c.stride, c.upsample,
+              c.pro_scale != nullptr, c.gin_part != nullptr, c.ksplit);
     add(conv_label(c), fl, by, [=](hipStream_t st) { return conv2d_igemm(c, st); });
   };
   auto add_gemm = [&](const GemmArgs& g) {
