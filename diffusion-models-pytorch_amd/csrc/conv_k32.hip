@@ -126,7 +126,10 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
     bid -= par * per_par;
   }
   const int py = par >> 1, px = par & 1;
-  const int mt = bid / nN, nt = bid - (bid / nN) * nN;
+  // tile order: N tiles fastest (the blocks of one M tile share its patch in L2), or with nslow all M tiles of
+  // an N tile first (concurrent blocks share that N tile's weights)
+  const int nM = ceil_div(M, BM);
+  const int mt = a.nslow ? bid % nM : bid / nN, nt = a.nslow ? bid / nM : bid - (bid / nN) * nN;
   const int m0 = mt * BM, n0 = nt * BN;
   const int HWo = Ho * Wo;
   const int b0 = m0 / HWo;
@@ -1167,7 +1170,10 @@ int conv2d_k32(const ConvArgs& a, int v, hipStream_t st) {
   }
   if (v == 10) {
     t2d_geom(a, g);
-    launch_k32<128, 128, 64, 64, false, 256, kMaxP, kTab, false, true>(a, g, st);
+    ConvArgs an = a;
+    // DM_K32_NSLOW=1 (A/B): the N-slow tile order for the 2-D tiles
+    an.nslow = std::getenv("DM_K32_NSLOW") && std::getenv("DM_K32_NSLOW")[0] == '1';
+    launch_k32<128, 128, 64, 64, false, 256, kMaxP, kTab, false, true>(an, g, st);
     DM_LAUNCH_CHECK();
     return DM_OK;
   }

@@ -35,7 +35,8 @@ struct ConvArgs {
   int rowvec_pitch;
   const float* res;     // residual at output resolution or null
   int res_pitch;
-  int tile;             // 0 auto; 1..3 force an im2col tile, 4..6 a halo-patch tile
+  int tile;
+  int nslow;     // K32 tile order: 1 = all M tiles of an N tile before the next N tile (conv_k32.hip)             // 0 auto; 1..3 force an im2col tile, 4..6 a halo-patch tile
   int pick_B;           // batch the tile heuristics assume (0: B). Plans pass a fixed one, so a layer's
                         // kernel (and its summation order) never changes with B: batch-invariant results
   // optional operand prologue on segment 1 (halo-patch kernel only):
