@@ -1,7 +1,13 @@
-"""Round-4 GPU tests: the folded single-head attention block (attn_block.hip) against the unfolded path
-(q / k / v / proj as the reference computes them, DM_ATTN_FOLD=0) and the reference fixtures.
+"""Round-4 GPU tests.
 
-Reference: models/modules.py:77-102 (SelfAttentionBlock), models/unet.py:121-152.
+* the folded single-head attention block (attn_block.hip, variants 2-5) against the unfolded path (q / k / v /
+  proj as the reference computes them, DM_ATTN_FOLD=0) and the reference fixtures (models/modules.py:77-102,
+  models/unet.py:121-152);
+* DiT-XL/2 per-step accuracy vs float64 and the 2^-20 chaos envelope (models/dit/model.py:234-252; parity
+  unpinned, timm absent);
+* the K32 convs added this round: small-map 8 waves, stride-2 tiles (models/modules.py:70-72), 2-D tiles of
+  wide maps incl. the sub-pixel upsample (models/adm/unet.py:162-275), each against the path it replaces;
+* the 8-wave 128 x 256 linear_k32 blocks (DiT token GEMMs) bit for bit against the 4-wave form.
 """
 import numpy as np
 import pytest
