@@ -894,6 +894,8 @@ __global__ void __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2
   __shared__ __attribute__((aligned(16))) float lds[LDSF];
   __shared__ __attribute__((aligned(16))) float tab[2][kBC];
   _Float16* stg = reinterpret_cast<_Float16*>(lds);
+  AB_RSTAMP(8);
+  AB_STAMP(0);
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int l16 = lane & 15, q = lane >> 4;
@@ -1020,6 +1022,7 @@ __global__ void __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2
     load_k(0, u, rg[0][u]);
     if (RD == 2) load_k(1, u, rg[RD - 1][u]);
   }
+  AB_STAMP(1);
   f16x8 tp[8][2];
   float tun;
   {
@@ -1055,6 +1058,7 @@ __global__ void __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2
     }
   }
 
+  AB_STAMP(2);
   // ------------------------------------------------------------------ 2. one pass over the keys (chunks of 32)
 #pragma unroll
   for (int u = 0; u < NS; ++u) store_k(0, u, rg[0][u]);
@@ -1147,6 +1151,7 @@ __global__ void __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2
     load_w(a.wg_img, 0, u, rg[0][u]);
     if (RD == 2) load_w(a.wg_img, 1, u, rg[RD - 1][u]);
   }
+  AB_STAMP(3);
   // O x 2^ex = acc / (2^14 l) (the staged keys carry xn x 2^ex), rows in storage order -> the projection's B
   f16x8 op[8][2];
   {
@@ -1165,6 +1170,7 @@ __global__ void __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2
     }
   }
 
+  AB_STAMP(4);
   // ------------------------------------------------------------------ 3. Y^T = Wg' O^T
 #pragma unroll
   for (int u = 0; u < NS; ++u) store_w(0, u, rg[0][u]);
@@ -1197,6 +1203,7 @@ __global__ void __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2
   for (int i = 0; i < NX; ++i) load_res(RD * NS + i, xr2[i]);
   if (bad && a.range_flag) *a.range_flag = 1;
 
+  AB_STAMP(5);
   // ------------------------------------------------------------------ 4. y = x + Y + cb, GroupNorm statistics
   const float yun = ldexpf(1.f, -a.ex);
 #pragma unroll
@@ -1234,6 +1241,8 @@ __global__ void __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2
     if (rsub == 0 && (c4 % (cpg / 4)) == 0)
       a.gn_part[((size_t)b * (kBL / 64) + (tok0 >> 6)) * a.gn_G + col / cpg] = make_double2(s, qq);
   }
+  AB_STAMP(6);
+  AB_RSTAMP(9);
 }
 
 __device__ __forceinline__ int pi32(int m) { return 4 * (m >> 3) + (m & 3) + 16 * ((m >> 2) & 1); }
