@@ -1,5 +1,8 @@
 """Phase timing of attn_block_kernel (the folded CIFAR attention block) from the diagnostic build
 (-DDM_K32_STAMPS): CIFAR-10 UNet forwards at B=256, then the last attention launch's per-work-group stamps.
+Caveat: variants 3-5 sit at the register limit, and the stamps' scheduling barriers make their diagnostic builds
+spill (556-968 B per lane, -Rpass-analysis=kernel-resource-usage): their phase shares (the "O finalize" above
+all) describe the spilled build, not the product kernel; variant 2 does not spill.
 
     make -C diffusion-models-pytorch_amd/csrc BUILD=build_stamps OUT=../../tools/lib/libdm_stamps.so EXTRA=-DDM_K32_STAMPS
     DM_HIP_LIB=tools/lib/libdm_stamps.so [DM_ATTN_BLOCK=2] python tools/ab_stamps.py
