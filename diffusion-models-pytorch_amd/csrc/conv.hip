@@ -278,7 +278,7 @@ int conv2d_igemm(const ConvArgs& a, hipStream_t st) {
   }
   const long M = (long)a.B * a.Hout * a.Wout;
   DM_REQUIRE(M > 0 && M < (1L << 31), "conv: M out of range");
-  DM_REQUIRE(a.tile >= 0 && a.tile <= 19, "conv: tile must be 0..19");
+  DM_REQUIRE(a.tile >= 0 && a.tile <= 20, "conv: tile must be 0..20");
   const int mode = conv_mode(a);
   const int pick = conv_pick(a);
   DM_REQUIRE(!a.gn_part || conv_can_emit_gn(a), "conv: GroupNorm statistics need a 128-row halo-patch tile, "
@@ -319,6 +319,7 @@ int conv_pick(const ConvArgs& a) {
   if (a.tile == 17 && conv_k32_variant_ok(a, 8)) return 3;  // forced K32 big-table 128 x 128 tiles
   if (a.tile == 18 && conv_k32_variant_ok(a, 9)) return 5;  // forced K32 stride-2 tiles
   if (a.tile == 19 && conv_k32_variant_ok(a, 10)) return 3;  // forced K32 2-D tiles of wide maps
+  if (a.tile == 20 && conv_k32_variant_ok(a, 11)) return 3;  // forced K32 64-row single-image tiles (8^2)
   if (conv_pw_ok(a)) {  // split 1x1: 128x128 tiles when they still give >= 2 blocks per CU, else 128x64
     const long M = (long)(a.pick_B > 0 ? a.pick_B : a.B) * a.Hout * a.Wout;
     return (a.Cout >= 128 && ((M + 127) / 128) * ((a.Cout + 127) / 128) >= 512) ? 3 : 4;

@@ -947,6 +947,16 @@ static bool t2d_geom(const ConvArgs& a, PatchGeom& g);
 
 int conv_k32_variant_ok(const ConvArgs& a, int v) {
   if (v == 6) return conv_k32s_ok(a) ? 1 : 0;
+  if (v == 11) {  // 64-row tiles of one <= 64-pixel image (8^2 maps), 4 waves of 32 x 64
+    if (!(a.ws && a.ws_np == 2 && a.ws_rowscale && a.taps == 9 && a.stride == 1 && a.upsample == 0)) return 0;
+    if (a.Cin1 < kC || a.Cin1 % kC != 0 || a.Cin2 % kC != 0 || a.ksplit > 1 || a.K != 9 * a.Cin1 + a.Cin2) return 0;
+    if (a.Hout * a.Wout != 64 || a.Wout % 8 != 0) return 0;
+    PatchGeom g;
+    if (!conv_patch_geom(a, 64, g) || g.P > kMaxP || g.TB != 1) return 0;
+    if (a.pro_scale && 2 * a.Cin1 > kTab) return 0;
+    if (a.gin_part && a.gin_G > kStats) return 0;
+    return staged_epilogue_ok(a) ? 1 : 0;
+  }
   if (v == 10) {
     if (!(a.ws && a.ws_np == 2 && a.ws_rowscale)) return 0;
     if (a.Cin1 < kC || a.Cin1 % kC != 0 || a.Cin2 % kC != 0 || a.ksplit > 1) return 0;
@@ -1069,7 +1079,7 @@ static bool conv_k32_small_enabled() {
 }
 
 int conv_k32_pick(const ConvArgs& a) {
-  if (a.tile >= 10 && a.tile <= 19) return conv_k32_variant_ok(a, a.tile - 9) ? a.tile - 9 : 0;
+  if (a.tile >= 10 && a.tile <= 20) return conv_k32_variant_ok(a, a.tile - 9) ? a.tile - 9 : 0;
   if (a.tile != 0 || !conv_k32_enabled()) return 0;
   if (a.stride == 2) {  // at least one block per CU (the nominal batch keeps the choice batch-invariant)
     const long M = (long)(a.pick_B > 0 ? a.pick_B : a.B) * a.Hout * a.Wout;
@@ -1094,6 +1104,8 @@ int conv_k32_pick(const ConvArgs& a) {
   }
   const int p = conv_pick(a);
   if (p != 3 && p != 4) return 0;
+  // DM_K32_8X=1 (A/B): 8^2 maps on 64-row single-image tiles (two blocks per CU where 128 x 128 tiles give one)
+  if (std::getenv("DM_K32_8X") && std::getenv("DM_K32_8X")[0] == '1' && conv_k32_variant_ok(a, 11)) return 11;
   // 128 x 128 tiles down to one block per CU (measured on 8^2 maps at B = 256: 256 blocks of 128 x 128 beat
   // 512 of 128 x 64 by 6 %); the nominal batch (pick_B) keeps the choice batch-invariant
   const long M = (long)(a.pick_B > 0 ? a.pick_B : a.B) * a.Hout * a.Wout;
@@ -1114,6 +1126,7 @@ std::string conv_k32_label(const ConvArgs& a, int v) {
            (a.upsample == 2 ? "true,256,208,8192>" : "false,256,208,8192>");
   if (v == 9)
     return std::string("conv_k32_kernel<64,128,32,32,") + (a.pro_scale ? "true," : "false,") + "false,false,512,392,2048,true>";
+  if (v == 11) return std::string("conv_k32_kernel<64,128,32,64,") + (a.pro_scale ? "true," : "false,") + "false,false>";
   if (v == 10)
     return std::string("conv_k32_kernel<128,128,64,64,") + (a.pro_scale ? "true," : "false,") + "false," +
            (a.upsample == 2 ? "true" : "false") + ",256,208,2048,false,true>";
@@ -1150,7 +1163,7 @@ static void launch_k32(const ConvArgs& a, const PatchGeom& g, hipStream_t st) {
 }
 
 int conv2d_k32(const ConvArgs& a, int v, hipStream_t st) {
-  DM_REQUIRE(v >= 1 && v <= 10 && conv_k32_variant_ok(a, v), "conv: shape not supported by the K = 32 split kernel");
+  DM_REQUIRE(v >= 1 && v <= 11 && conv_k32_variant_ok(a, v), "conv: shape not supported by the K = 32 split kernel");
   PatchGeom g;
   if (v == 6) {
     conv_patch_geom(a, 64, g);
@@ -1177,8 +1190,9 @@ int conv2d_k32(const ConvArgs& a, int v, hipStream_t st) {
     DM_LAUNCH_CHECK();
     return DM_OK;
   }
-  conv_patch_geom(a, (v >= 3 && v <= 6) || v == 9 ? 64 : BM_K32, g);
+  conv_patch_geom(a, (v >= 3 && v <= 6) || v == 9 || v == 11 ? 64 : BM_K32, g);
   switch (v) {
+    case 11: launch_k32<64, 128, 32, 64, false>(a, g, st); break;
     case 9: launch_k32<64, 128, 32, 32, false, 512, kMaxPW, kTab, true>(a, g, st); break;
     case 8: launch_k32<128, 128, 64, 64, false, 256, kMaxP, kTabBig>(a, g, st); break;
     case 7: launch_k32<128, 128, 64, 32, false, 512, kMaxPW>(a, g, st); break;
