@@ -624,7 +624,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 // Q stays in registers (its DHP / 16 slices, both pieces); K and V^T blocks are staged through LDS (double
 // buffered, one barrier per 64 keys, loads for the next block in flight during this one's MFMAs), with row
 // pitches of an odd number of 16-B slots times 4 dwords so the 32-row fragment reads are conflict free.
-// Head dims below DHP (72 in an 80-deep contraction) are zero-padded in registers / LDS, never in memory;
+// Head dims below DHP (72 in an 80-deep contraction) are zero-padded in registers / LDS, never in memory.
+//  * Head dims that are not a multiple of 32 (72, 80) take their last Dh % 32 rows of O^T on
+//    v_mfma_f32_16x16x32_f16 (a 16-row tail, 2 x 16 queries per 32-key chunk) instead of a third 32-row tile:
+//    DiT's 72 wide heads had wasted a quarter of their P V products on rows 72 .. 95. The 16x16x32 B operand
+//    wants 16 queries x 4 k-groups of 8 where the S^T accumulators give 32 queries x 2 k-groups per 16-key
+//    step: v_permlane32_swap + v_permlane16_swap of the two steps' pieces produce both 16-query halves
+//    exactly (no LDS round trip); the V^T rows are read at the same permuted key offsets.
 // O^T rows >= Dh read clamped V rows and are not stored. Each wave owns 32 queries; NW waves per block.
 // Not bit-identical to the unfused path (exp2 and the online rescale round differently): within a few ulp of
 // the unfused softmax (tests/test_gpu_r3.py test_flash_attention_vs_unfused).
@@ -636,7 +642,9 @@ __global__ void __launch_bounds__(NW * 64) attn_flash_kernel(AttnArgs a) {
   constexpr int KP = DHP == 80 ? 168 : DHP == 48 ? 104 : DHP == 32 ? 72 : 136;  // fp16 pitch of a K row:
                                              // 2 DHP + pad, 4 x an odd number of dwords (conflict-free reads)
   constexpr int VP = 136;                    // fp16 pitch of a V^T row (64 keys x 2 pieces + pad: 68 dwords)
-  constexpr int NDT = (DHP + 31) / 32;       // 32-row d tiles of O^T
+  constexpr bool TAIL = Dh % 32 != 0;        // last Dh % 32 rows of O^T on a 16x16x32 tail
+  static_assert(!TAIL || Dh % 32 <= 16, "16-row tail");
+  constexpr int NDT = TAIL ? Dh / 32 : (DHP + 31) / 32;   // 32-row d tiles of O^T
   constexpr int KBUF = KB * KP, VBUF = DHP * VP, BUF = KBUF + VBUF;
   constexpr int NT = NW * 64;
   __shared__ __attribute__((aligned(16))) _Float16 lds[2 * BUF];
@@ -723,6 +731,10 @@ __global__ void __launch_bounds__(NW * 64) attn_flash_kernel(AttnArgs a) {
   for (int i = 0; i < NDT; ++i)
 #pragma unroll
     for (int r = 0; r < 16; ++r) oacc[i][r] = 0.f;
+  // tail accumulators: [query half qh] lane (j = lane & 15, g = lane >> 4) holds O^T rows 32 NDT + 4 g .. + 3 of
+  // query 16 qh + j
+  f4 otail[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+  const int tq = lane & 15, tg = lane >> 4;
   float m_run = -INFINITY, l_run = 0.f;
 
   const int nkb = L / KB;
@@ -768,6 +780,14 @@ __global__ void __launch_bounds__(NW * 64) attn_flash_kernel(AttnArgs a) {
     for (int i = 0; i < NDT; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) oacc[i][r] *= corr;
+    if constexpr (TAIL) {
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh) {
+        const float c = __shfl(corr, 16 * qh + tq);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) otail[qh][r] *= c;
+      }
+    }
     const float mb = (float)a.ep - m_new;
     // P^T pieces: k-step ks = 16 keys = accumulator registers 8 (ks & 1) .. + 7 of tile ks >> 1
     f16x8 pb[4][2];
@@ -794,6 +814,36 @@ __global__ void __launch_bounds__(NW * 64) attn_flash_kernel(AttnArgs a) {
         Split<2>::mma(va, pb[ks], oacc[dt]);
       }
     }
+    if constexpr (TAIL) {
+      // rows 32 NDT .. + 15 (clamped to Dh - 1: not stored), 32-key chunk c = steps 2c, 2c + 1
+      const int drow = min(NDT * 32 + tq, Dh - 1);
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        f16x8 va[2], pq[2][2];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          va[p] = *reinterpret_cast<const f16x8*>(Vb + drow * VP + (2 * c + (tg >> 1)) * 32 + p * 16 + (tg & 1) * 8);
+          // lane (j, g) of half qh <- step 2c + (g >> 1), lane 16 qh + j + 32 (g & 1)
+          const u4 x = __builtin_bit_cast(u4, pb[2 * c][p]), y = __builtin_bit_cast(u4, pb[2 * c + 1][p]);
+          u4 h0, h1;
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            const auto s32 = __builtin_amdgcn_permlane32_swap(x[w], y[w], false, false);
+            const auto s16 = __builtin_amdgcn_permlane16_swap(s32[0], s32[1], false, false);
+            h0[w] = s16[0];
+            h1[w] = s16[1];
+          }
+          pq[0][p] = __builtin_bit_cast(f16x8, h0);
+          pq[1][p] = __builtin_bit_cast(f16x8, h1);
+        }
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh) {
+          otail[qh] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va[1], pq[qh][0], otail[qh], 0, 0, 0);
+          otail[qh] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va[0], pq[qh][1], otail[qh], 0, 0, 0);
+          otail[qh] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va[0], pq[qh][0], otail[qh], 0, 0, 0);
+        }
+      }
+    }
     if (kb + 1 < nkb) store_blk((kb + 1) & 1);
     __syncthreads();
   }
@@ -810,6 +860,17 @@ __global__ void __launch_bounds__(NW * 64) attn_flash_kernel(AttnArgs a) {
       const int d = dt * 32 + acc_row(r, lh);
       if (d < Dh) st[lr * OP + d] = oacc[dt][r] * scale;
     }
+  if constexpr (TAIL) {
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh) {
+      const float sq = __shfl(scale, 16 * qh + tq);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int d = NDT * 32 + 4 * tg + r;
+        if (d < Dh) st[(16 * qh + tq) * OP + d] = otail[qh][r] * sq;
+      }
+    }
+  }
   __builtin_amdgcn_s_waitcnt(0xc07f);
   __builtin_amdgcn_wave_barrier();
   const int h = bh % a.heads, b = bh / a.heads;

@@ -327,7 +327,7 @@ def test_flash_attention_vs_unfused(cuda, golden, report, monkeypatch, case):
     """attn_flash_kernel (online softmax, S never in HBM) against the unfused S GEMM -> softmax_rows -> PV
     GEMM path it replaces, which stays as the test oracle: ADM's 8^2 blocks (adm_tiny: L = 64, heads of 32,
     zero-padded to a 64-deep contraction), DiT-S/2 at 16^2 latents (L = 64, heads of 64), DiT-XL/2 (L = 256,
-    16 heads of 72: an 80-deep contraction, 96-row output tiles), the guided-diffusion 256^2 UNet (L = 1024 at
+    16 heads of 72: an 80-deep contraction, O^T rows 64 .. 71 on the 16x16x32 tail), the guided-diffusion 256^2 UNet (L = 1024 at
     32^2 and L = 64 at 8^2, heads of 64), CFG-CIFAR AdaGN (8^2 blocks, heads of 64). Forwards within 1e-5 of
     each other (the attention core alone differs by exp2 vs expf and the online rescaling, a few 1e-7
     relative)."""
