@@ -430,11 +430,17 @@ def main():
         wl = build_workload(args.workload, args, dev, rank)
     B, shape = wl['images'], wl['shape']
     gathered = torch.empty((world * B, *shape[1:]), device=dev) if world > 1 else None
+    comm = None
+    if world > 1 and backend == 'nccl' and os.environ.get('DM_GATHER') != 'torch':
+        from dmhip.comm import Comm   # the C-ABI RCCL all-gather (dm_allgather_f32), bootstrapped over the group
+        comm = Comm.from_process_group()
 
     def fold():
         x = wl['fold']()
         if world > 1:   # the reference's accelerator.gather of the fold (sample_uncond.py:190): one all-gather
-            if backend == 'nccl':
+            if comm is not None:
+                comm.allgather(x, gathered)
+            elif backend == 'nccl':
                 dist.all_gather_into_tensor(gathered, x)
             else:
                 parts = [torch.empty(tuple(x.shape)) for _ in range(world)]
@@ -531,6 +537,8 @@ def main():
             with open(args.profile_json, 'w') as f:
                 json.dump(dict(families=fam, ops=prof), f, indent=1)
         print(json.dumps(line), flush=True)
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
 

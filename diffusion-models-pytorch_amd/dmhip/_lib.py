@@ -278,6 +278,13 @@ def _declare(L: ctypes.CDLL):
     L.dm_dit_plan_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int)]
     L.dm_lincomb.argtypes = [ctypes.c_int, vp, vp, vp, ctypes.c_int64, ctypes.c_int64, vp, vp, ctypes.c_float,
                              ctypes.c_float, vp]
+    L.dm_comm_unique_id.argtypes = [vp]
+    L.dm_comm_init.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
+    L.dm_comm_info.argtypes = [vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                               ctypes.POINTER(ctypes.c_int)]
+    L.dm_allgather_f32.argtypes = [vp, vp, vp, ctypes.c_int64, vp]
+    L.dm_comm_destroy.argtypes = [vp]
+    L.dm_comm_destroy.restype = None
 
 
 def load() -> ctypes.CDLL:

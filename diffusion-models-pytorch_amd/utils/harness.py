@@ -4,7 +4,8 @@ scripts/sample_cfg.py:157-182), independent of the launcher.
 One process per GPU. Each rank draws its own init noise (seeded seed + rank,
 as accelerate's set_seed(device_specific=True)), samples a fold of `bspp`
 images fully independently, and the fold is gathered once over the process
-group (RCCL `all_gather_into_tensor` on ROCm, gloo on CPU) in rank order;
+group in rank order (on GPUs: the C-ABI RCCL all-gather `dm_allgather_f32`, dmhip/comm.py; DM_GATHER=torch
+selects torch.distributed's `all_gather_into_tensor` instead; gloo on CPU);
 only the first `bs` images of each fold are kept, exactly as
 `accelerator.gather(samples)[:bs]`.
 """
@@ -37,6 +38,7 @@ class DistEnv:
         if self.world > 1 and not dist.is_initialized():
             kw = dict(device_id=self.device) if self.backend == 'nccl' else {}
             dist.init_process_group(self.backend, **kw)
+        self._comm = None
 
     @property
     def is_main(self):
@@ -52,8 +54,13 @@ class DistEnv:
             return x
         x = x.contiguous()
         out = torch.empty((self.world * x.shape[0], *x.shape[1:]), dtype=x.dtype, device=x.device)
-        if x.device.type == 'cuda' and self.backend == 'nccl':
-            dist.all_gather_into_tensor(out, x)   # one RCCL all-gather over xGMI
+        if x.device.type == 'cuda' and self.backend == 'nccl' and os.environ.get('DM_GATHER') != 'torch':
+            if self._comm is None:   # RCCL communicator of the C ABI, bootstrapped once over the process group
+                from dmhip.comm import Comm
+                self._comm = Comm.from_process_group()
+            self._comm.allgather(x, out)   # one RCCL all-gather over xGMI (dm_allgather_f32)
+        elif x.device.type == 'cuda' and self.backend == 'nccl':
+            dist.all_gather_into_tensor(out, x)
         else:
             host = out.cpu() if out.device.type != 'cpu' else out
             dist.all_gather(list(host.chunk(self.world)), x.cpu())
@@ -62,6 +69,9 @@ class DistEnv:
         return out
 
     def close(self):
+        if self._comm is not None:
+            self._comm.close()
+            self._comm = None
         if self.world > 1 and dist.is_initialized():
             dist.destroy_process_group()
 

@@ -346,6 +346,22 @@ int dm_softmax_rows(float* x, int64_t rows, int L, int ld, void* stream);
 int dm_timestep_embedding(const int64_t* t, int B, int dim, int kind, const float* freqs, float* out,
                           void* stream);
 
+/* ---------------------------------------------------------------- data-parallel gather (comm.hip)
+ * Replaces accelerate's gather of each rank's finished fold (reference scripts/sample_uncond.py:190,
+ * scripts/sample_cfg.py:177: `accelerator.gather(samples)[:bs]`): an RCCL all-gather in rank order over the
+ * ranks' own HIP devices (xGMI between the GPUs of a node). Bootstrap: rank 0 calls dm_comm_unique_id, the
+ * caller hands the DM_COMM_UID_BYTES bytes to every rank, each rank calls dm_comm_init with the HIP device it
+ * samples on current. RCCL is loaded on first use (dlopen "librccl.so.1"): DM_ERR_UNSUPPORTED without it.
+ * dm_allgather_f32: recv holds nranks x count floats, rank r's send lands at recv + r x count; enqueued on
+ * `stream` (asynchronous, like every launch here); send may be recv + rank x count (in place). */
+#define DM_COMM_UID_BYTES 128
+typedef struct dm_comm dm_comm;
+int dm_comm_unique_id(void* uid);
+int dm_comm_init(const void* uid, int nranks, int rank, dm_comm** comm);
+int dm_comm_info(const dm_comm* comm, int* nranks, int* rank, int* device);
+int dm_allgather_f32(dm_comm* comm, const float* send, float* recv, int64_t count, void* stream);
+void dm_comm_destroy(dm_comm* comm);
+
 #ifdef __cplusplus
 }
 #endif
