@@ -430,10 +430,17 @@ def main():
         wl = build_workload(args.workload, args, dev, rank)
     B, shape = wl['images'], wl['shape']
     gathered = torch.empty((world * B, *shape[1:]), device=dev) if world > 1 else None
-    comm = None
+    comm, gather_path = None, None
+    if world > 1:
+        gather_path = 'torch.distributed' if backend == 'nccl' else f'{backend} (host)'
     if world > 1 and backend == 'nccl' and os.environ.get('DM_GATHER') != 'torch':
         from dmhip.comm import Comm   # the C-ABI RCCL all-gather (dm_allgather_f32), bootstrapped over the group
-        comm = Comm.from_process_group()
+        try:
+            comm = Comm.from_process_group()
+            gather_path = 'dm_allgather_f32 (RCCL, C ABI)'
+        except Exception as e:   # reported in the JSON line; the fold's gather then runs on torch.distributed
+            print(f'bench.py: rank {rank}: dm_comm_init failed ({e}); gathering with torch.distributed', file=sys.stderr)
+            gather_path = f'torch.distributed (dm_comm_init failed: {str(e)[:120]})'
 
     def fold():
         x = wl['fold']()
@@ -512,7 +519,8 @@ def main():
                         denoise_steps=wl['denoise_steps'], weights_gb=round(wbytes_t / 1e9, 3),
                         workspace_gb=round(wsbytes_t / 1e9, 3), conv_math=math,
                         # the reference draws randn_like every step even at eta=0 (ddim.py:76): so does the bench
-                        skip_unused_noise=wl['diffuser'].skip_unused_noise if wl['diffuser'] else None),
+                        skip_unused_noise=wl['diffuser'].skip_unused_noise if wl['diffuser'] else None,
+                        gather=gather_path),
             roofline=roof,
             step_level=dict(model_tflops=round(total_flops / (total_gpu_ms * 1e-3) / 1e12, 2) if total_gpu_ms else None,
                             # observed forwards are 1 in PROFILE_EVERY: their event-summed launch time scaled to
