@@ -59,27 +59,32 @@ constexpr int kLGM = 4;    // M tiles per group of the tile order
 // loaded by both row waves) or 64 x 64.
 // One 32 x WN slab (acc * rowscale * 2^-ea, no bias yet) of the qkv projection -> the attention operand
 // planes: q * alpha * 2^ea and k * b_scale * 2^eb as [B][heads][2][L][Dh], v * 2^ev transposed as
-// [B][heads][2][Dh][L] (plane 0 = fp16(x), plane 1 = fp16(x - plane 0)), 16-B stores. The slab's columns
-// lie in one of q / k / v and in one head (3C, C and Dh are multiples of 32).
+// [B][heads][2][Dh][L] (plane 0 = fp16(x), plane 1 = fp16(x - plane 0)), 16-B stores. The slab's columns lie
+// in one of q / k / v (3C and C are multiples of 32; with the legacy per-head [q; k; v] order Dh is), but with
+// a head dim that 32 does not divide (DiT's 72, or 80, at L = 64) they span two heads: every 8-column group is
+// located on its own (Dh % 8 == 0, linear_k32_ok).
 template <int WN>
 __device__ __forceinline__ void plane_slab(const GemmArgs& g, const float* st, int EP, int row0, int col0, int lane,
                                            f4 bias4, bool& bad) {
   if (col0 >= g.N) return;
   const int Dh = g.ap_Dh, C = g.ap_heads * Dh;
-  int part, h, d0;
-  if (g.ap_vonly) {
-    part = 2;
-    h = col0 / Dh;
-    d0 = col0 - h * Dh;
-  } else if (g.ap_legacy) {
-    h = col0 / (3 * Dh);
-    part = (col0 - h * 3 * Dh) / Dh;
-    d0 = col0 - h * 3 * Dh - part * Dh;
-  } else {
-    part = col0 / C;
-    h = (col0 - part * C) / Dh;
-    d0 = col0 - part * C - h * Dh;
-  }
+  auto locate = [&](int col, int& part, int& h, int& d) {
+    if (g.ap_vonly) {
+      part = 2;
+      h = col / Dh;
+      d = col - h * Dh;
+    } else if (g.ap_legacy) {
+      h = col / (3 * Dh);
+      part = (col - h * 3 * Dh) / Dh;
+      d = col - h * 3 * Dh - part * Dh;
+    } else {
+      part = col / C;
+      h = (col - part * C) / Dh;
+      d = col - part * C - h * Dh;
+    }
+  };
+  int part, h0, d0;
+  locate(col0, part, h0, d0);
   const float scale = part == 0 ? g.ap_alpha : part == 1 ? g.ap_bscale : 1.f;
   const bool use_scale = part == 0 ? g.ap_alpha != 1.0f : part == 1 && g.ap_bscale != 0.0f && g.ap_bscale != 1.0f;
   const float pw = ldexpf(1.f, part == 0 ? g.ap_ea : part == 1 ? g.ap_eb : g.ap_ev);
@@ -102,13 +107,15 @@ __device__ __forceinline__ void plane_slab(const GemmArgs& g, const float* st, i
       const int row = it / G8, c8 = it - row * G8;
       const int m = row0 + row;
       if (m >= g.M) continue;
+      int pt, h, d;
+      locate(col0 + 8 * c8, pt, h, d);
       float x[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) x[e] = st[row * EP + 8 * c8 + e] + (bias ? bias[8 * c8 + e] : 0.f);
       f16x8 hi, lo;
       split8(x, hi, lo);
       const int b = m / g.ap_L, tok = m - b * g.ap_L;
-      _Float16* p = dst + ((size_t)b * g.ap_heads + h) * 2 * plane + (size_t)tok * Dh + d0 + 8 * c8;
+      _Float16* p = dst + ((size_t)b * g.ap_heads + h) * 2 * plane + (size_t)tok * Dh + d;
       *reinterpret_cast<f16x8*>(p) = hi;
       *reinterpret_cast<f16x8*>(p + plane) = lo;
     }
@@ -117,6 +124,8 @@ __device__ __forceinline__ void plane_slab(const GemmArgs& g, const float* st, i
       const int col = it % WN, r8 = it / WN;
       const int m = row0 + 8 * r8;  // tokens m .. m + 7 lie in one image (L % 8 == 0)
       if (m >= g.M) continue;
+      int pt, h, d;
+      locate(col0 + col, pt, h, d);
       float x[8];
       const float bc = bias ? bias[col] : 0.f;
 #pragma unroll
@@ -124,7 +133,7 @@ __device__ __forceinline__ void plane_slab(const GemmArgs& g, const float* st, i
       f16x8 hi, lo;
       split8(x, hi, lo);
       const int b = m / g.ap_L, tok = m - b * g.ap_L;
-      _Float16* p = g.ap_v + ((size_t)b * g.ap_heads + h) * 2 * plane + (size_t)(d0 + col) * g.ap_L + tok;
+      _Float16* p = g.ap_v + ((size_t)b * g.ap_heads + h) * 2 * plane + (size_t)d * g.ap_L + tok;
       *reinterpret_cast<f16x8*>(p) = hi;
       *reinterpret_cast<f16x8*>(p + plane) = lo;
     }
@@ -641,6 +650,9 @@ bool linear_k32_ok(const GemmArgs& g) {
   if (g.as && (g.pro_scale || g.ln_stats || (reinterpret_cast<uintptr_t>(g.as) & 15) != 0)) return false;
   if (g.c_split && (g.N % 64 != 0 || g.ap_q || (reinterpret_cast<uintptr_t>(g.c_split) & 15) != 0)) return false;
   if (g.ap_vonly && (!g.ap_q || g.ap_frag || g.ap_legacy)) return false;
+  // attention planes: 8-column groups of one head (plane_slab / plane_block), q / k / v never inside one slab
+  if (g.ap_q && (g.ap_Dh % 8 != 0 || (g.ap_heads * g.ap_Dh) % 32 != 0 || (g.ap_legacy && g.ap_Dh % 32 != 0)))
+    return false;
   if (g.ap_frag && (!g.ap_q || g.ap_legacy || (g.ap_heads * g.ap_Dh) % 128 != 0 || g.ap_L % 128 != 0 ||
                     g.ap_Dh % 32 != 0))
     return false;
