@@ -1066,6 +1066,105 @@ __global__ void __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2
   zero_acc();   // O^T accumulators
   float m_run = -INFINITY, l_run = 0.f;
   const float sl2 = tun * 1.4426950408889634f;
+  if constexpr ((OPT & 4) != 0) {
+    // Software-pipelined key pass (DM_ATTN_OPT=4): iteration kc computes S of chunk kc, then P V of chunk kc - 1
+    // with chunk kc's online softmax placed between its MFMAs, so the softmax's VALU / exp2 / cross-lane chain
+    // issues while the matrix pipe runs P V -- in the plain loop both waves of a SIMD leave the barrier together
+    // and both run their softmax with the pipe idle. Key chunks rotate over three LDS images (kc % 3: S reads
+    // kc, P V reads kc - 1, chunk kc + 1 is staged into the third), inside the epilogue region. Every
+    // accumulator sees the same operations in the same order as the plain loop (rescale by chunk j's correction
+    // just before P V of chunk j), so the results are bit-identical.
+    static_assert(3 * kKImg <= 2 * LDSF, "three key-chunk images fit the staging region");
+    auto s_chunk = [&](int kc, fq (&sacc)[2]) {
+      const _Float16* img = stg + (kc % 3) * kKImg;
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          const _Float16* pr = img + (16 * kt + l16) * kKP + 32 * ks + 8 * q;
+          f16x8 av[2];
+          av[0] = *reinterpret_cast<const f16x8*>(pr);
+          av[1] = *reinterpret_cast<const f16x8*>(pr + kKPiece);
+          mma3(av, tp[ks], sacc[kt]);
+        }
+        if (kc + RD < 8 && ks % SD == 0) load_k(kc + RD, ks / SD, rg[(kc + RD) % RD][ks / SD]);
+      }
+    };
+    auto softmax = [&](const fq (&sacc)[2], f16x8 (&pp)[2], float& corr) {
+      float mx = fmaxf(fmaxf(fmaxf(sacc[0][0], sacc[0][1]), fmaxf(sacc[0][2], sacc[0][3])),
+                       fmaxf(fmaxf(sacc[1][0], sacc[1][1]), fmaxf(sacc[1][2], sacc[1][3])));
+      mx = fmaxf(mx, __shfl_xor(mx, 16));
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      const float m_new = fmaxf(m_run, mx * sl2);
+      corr = __builtin_amdgcn_exp2f(m_run - m_new);
+      m_run = m_new;
+      float ls = 0.f, v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[0][e], sl2, -m_new));
+        v[4 + e] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[1][e], sl2, -m_new));
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        ls += v[e];
+        v[e] *= 16384.f;
+      }
+      l_run = l_run * corr + ls;
+      split8(v, pp[0], pp[1]);
+    };
+    // P V of chunk kc (its P pieces pp), with `mid(ot)` after each output tile's MFMAs
+    auto pv_chunk = [&](int kc, const f16x8 (&pp)[2], auto&& mid) {
+      const _Float16* pt = stg + (kc % 3) * kKImg + (4 * q + (l16 >> 2)) * kKP + 4 * (l16 & 3);
+#pragma unroll
+      for (int ot = 0; ot < 16; ++ot) {
+        f16x8 av[2];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const f16x4_t lo4 = lds_tr16(pt + p * kKPiece + 16 * ot);
+          const f16x4_t hi4 = lds_tr16(pt + p * kKPiece + 16 * kKP + 16 * ot);
+          av[p] = f16x8{lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+        }
+        mma3(av, pp, acc[ot]);
+        mid(ot);
+      }
+    };
+    f16x8 pprev[2];
+    float cprev = 1.f;
+#pragma unroll
+    for (int kc = 0; kc < 8; ++kc) {
+      fq sacc[2] = {fq{0.f, 0.f, 0.f, 0.f}, fq{0.f, 0.f, 0.f, 0.f}};
+      s_chunk(kc, sacc);
+      f16x8 pc[2];
+      float cc;
+      if (kc == 0) {
+        softmax(sacc, pc, cc);
+#pragma unroll
+        for (int u = 0; u < NS; ++u) store_k(1, u, rg[1 % RD][u]);
+      } else {
+        if (kc - 1 > 0) {
+#pragma unroll
+          for (int ot = 0; ot < 16; ++ot) acc[ot] *= cprev;
+        }
+        pv_chunk(kc - 1, pprev, [&](int ot) {
+          if (ot == 1) softmax(sacc, pc, cc);
+          if (ot >= 8 && ot % SD == 0 && kc + 1 < 8)
+            store_k((kc + 1) % 3, (ot - 8) / SD, rg[(kc + 1) % RD][(ot - 8) / SD]);
+        });
+      }
+      pprev[0] = pc[0];
+      pprev[1] = pc[1];
+      cprev = cc;
+      __syncthreads();
+    }
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      load_w(a.wg_img, 0, u, rg[0][u]);
+      if (RD == 2) load_w(a.wg_img, 1, u, rg[RD - 1][u]);
+    }
+#pragma unroll
+    for (int ot = 0; ot < 16; ++ot) acc[ot] *= cprev;
+    pv_chunk(7, pprev, [](int) {});
+  } else {
 #pragma unroll
   for (int kc = 0; kc < 8; ++kc) {
     const _Float16* img = stg + (kc & 1) * kKImg;
@@ -1150,6 +1249,7 @@ __global__ void __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2
   for (int u = 0; u < NS; ++u) {
     load_w(a.wg_img, 0, u, rg[0][u]);
     if (RD == 2) load_w(a.wg_img, 1, u, rg[RD - 1][u]);
+  }
   }
   AB_STAMP(3);
   // O x 2^ex = acc / (2^14 l) (the staged keys carry xn x 2^ex), rows in storage order -> the projection's B
@@ -1306,6 +1406,7 @@ int attn_block(const AttnBlockArgs& a, hipStream_t st) {
     const int opt = std::getenv("DM_ATTN_OPT") ? std::atoi(std::getenv("DM_ATTN_OPT")) : 0;  // read per plan build
     const dim3 grid(a.B * (kBL / 128));
     if (opt == 2) hipLaunchKernelGGL((attn_block4_kernel<8, 2>), grid, dim3(512), 0, st, a);
+    else if (opt == 4) hipLaunchKernelGGL((attn_block4_kernel<8, 4>), grid, dim3(512), 0, st, a);
     else hipLaunchKernelGGL((attn_block4_kernel<8, 0>), grid, dim3(512), 0, st, a);
   }
   else if (a.variant == 3)

@@ -106,6 +106,27 @@ def test_folded_attention_8_waves_bit_identical(cuda, golden, monkeypatch):
     assert torch.equal(outs['3'], outs['5'])
 
 
+@pytest.mark.parametrize('opt', ['2', '4'])
+def test_folded_attention_opt_variants_bit_identical(cuda, golden, monkeypatch, opt):
+    """Variant 4's scheduling options run the same operations per accumulator in the same order: DM_ATTN_OPT=2
+    (S operands read one key step ahead) and DM_ATTN_OPT=4 (the key pass software-pipelined over three key-chunk
+    images, each chunk's softmax between the previous chunk's P V MFMAs) give whole forwards equal to the plain
+    loop's bit for bit (B = 4 and the batch-invariant B = 7)."""
+    _, meta = golden('forward')
+    g = torch.Generator().manual_seed(36)
+    x = torch.randn((7, 3, 32, 32), generator=g).to(cuda)
+    t = torch.randint(0, 1000, (7, ), generator=g).to(cuda)
+    outs = {}
+    for mode in ('plain', opt):
+        if mode != 'plain':
+            monkeypatch.setenv('DM_ATTN_OPT', opt)
+        model, _ = _model(meta, 'cifar10', cuda)
+        outs[mode] = (model(x[:4], t[:4]), model(x, t))
+        del model
+    assert torch.equal(outs['plain'][0], outs[opt][0])
+    assert torch.equal(outs['plain'][1], outs[opt][1])
+
+
 def test_attention_in_kernel_gn_finalize_bit_identical(cuda, golden, monkeypatch):
     """Variant 4 computes its GroupNorm affine from the chunk partials in the kernel (gn_finalize's expressions
     and summation order): whole forwards equal the separate gn_finalize launch's (DM_ATTN_GNFIN=1) bit for bit,
