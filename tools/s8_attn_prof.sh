@@ -11,6 +11,6 @@ import json
 for tag in ('base', 'opt4'):
     for i in (1, 2):
         f = json.load(open(f'gpurun_out/s8_{tag}_{i}.json'))['families']
-        a = f.get('attn_block4_kernel')
+        a = f.get('attn_block4_kernel<8>')
         print(tag, i, 'attn_block4 us/launch', round(a['ms'] / a['launches'] * 1e3, 2))
 PY
