@@ -271,6 +271,7 @@ bool linear_k32_ok(const GemmArgs& g);
 int linear_k32(const GemmArgs& g, hipStream_t st);
 // whether linear_k32 runs g on the 8-wave 128 x 256 blocks (DM_LIN_BN256)
 bool linear_k32_wide(const GemmArgs& g);
+bool linear_k32_bn64(const GemmArgs& g);
 // the pre-split A image of g (prologue, alpha, 2^split_ea, fp16x2 split; |value| > 65504 sets range_flag)
 int linear_presplit_a(const GemmArgs& g, _Float16* out, hipStream_t st);
 int conv_splitk_reduce(const ConvArgs& a, hipStream_t st);

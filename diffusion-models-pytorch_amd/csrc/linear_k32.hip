@@ -683,6 +683,19 @@ bool linear_k32_wide(const GemmArgs& g) {
   return g.as && !g.ap_q && (w >= 2 || (w == 1 && g.N % 256 == 0));
 }
 
+// DM_LIN_BN64 (A/B): 128 x 64 blocks of four 64 x 32 wave tiles for pre-split-A GEMMs whose 128 x 128 tiles
+// leave the last round of 512 resident blocks at most half full (DiT-XL/2's N = 1152 proj / fc2 at 2B = 64:
+// 1152 tiles = 2.25 rounds; 2304 half-width tiles = 4.5); 2 = for every pre-split-A GEMM with N % 64 == 0.
+// Same K-step sequence per output element, so bit-identical to the 128 x 128 blocks. Read per call.
+bool linear_k32_bn64(const GemmArgs& g) {
+  const char* e = std::getenv("DM_LIN_BN64");
+  const int w = e ? std::atoi(e) : 0;
+  if (!w || !g.as || g.ap_q || g.c_split || g.N % 64 != 0) return false;
+  if (w >= 2) return true;
+  const long tiles = (long)ceil_div(g.M, kLBM) * ceil_div(g.N, 128), rem = tiles % 512;
+  return rem != 0 && rem <= 256;
+}
+
 int linear_k32(const GemmArgs& g0, hipStream_t st) {
   DM_REQUIRE(linear_k32_ok(g0), "linear_k32: needs pre-split weights, K % 64 == 0, 16-byte aligned 4-column rows");
   static const int env_gm = std::getenv("DM_LIN_GM") ? std::atoi(std::getenv("DM_LIN_GM")) : 0;  // tile-order A/B
@@ -690,6 +703,12 @@ int linear_k32(const GemmArgs& g0, hipStream_t st) {
   if (env_gm > 0 && g.lin_gm == 0) g.lin_gm = env_gm;
   if (linear_k32_wide(g)) {
     hipLaunchKernelGGL((linear_k32_kernel<3, 128, 32, 8>), dim3(ceil_div(g.M, kLBM) * ceil_div(g.N, 256)), dim3(512), 0,
+                       st, g);
+    DM_LAUNCH_CHECK();
+    return DM_OK;
+  }
+  if (linear_k32_bn64(g)) {
+    hipLaunchKernelGGL((linear_k32_kernel<3, 64, 32, 4>), dim3(ceil_div(g.M, kLBM) * ceil_div(g.N, 64)), dim3(256), 0,
                        st, g);
     DM_LAUNCH_CHECK();
     return DM_OK;

@@ -426,6 +426,36 @@ def test_linear_k32_wide_blocks_bit_identical(cuda, golden, monkeypatch, wide):
     assert err <= TOL, err
 
 
+def test_linear_k32_half_width_blocks_bit_identical(cuda, golden, monkeypatch):
+    """DiT-S/2 with its pre-split-A token GEMMs on 128 x 64 blocks of 64 x 32 wave tiles (DM_LIN_BN64=2; =1 picks
+    them where the 128 x 128 tiles leave the last round of resident blocks at most half full) equals the 128 x 128
+    form bit for bit (same K-step sequence per output element), and the half-width kernel is in the plan."""
+    from models.dit.model import DiT
+    g, meta = golden('dit')
+    name = 'dit_s2'
+    x = torch.from_numpy(g[f'{name}_x']).to(cuda)
+    t = torch.from_numpy(g[f'{name}_t']).to(cuda)
+    y = torch.from_numpy(g[f'{name}_labels']).to(cuda)
+    outs = {}
+    for mode in ('base', 'bn64'):
+        if mode == 'bn64':
+            monkeypatch.setenv('DM_LIN_BN64', '2')
+        m = DiT(**meta['archs'][name]).eval()
+        init_synthetic_(m)
+        m = m.to(cuda)
+        outs[mode] = m(x, t, y).cpu()
+        h = m.native_handle(torch.device(cuda))
+        dmhip.unet_profile_enable(h, 1, m._abi)
+        m(x, t, y)
+        labels = [op['label'] for op in dmhip.unet_profile_read(h, m._abi)]
+        dmhip.unet_profile_enable(h, 0, m._abi)
+        assert ('linear_k32_kernel<3,64,32,4>' in labels) == (mode == 'bn64'), labels
+        del m
+    assert torch.equal(outs['base'], outs['bn64'])
+    err = (outs['bn64'] - torch.from_numpy(g[f'{name}_out_y'])).abs().max().item()
+    assert err <= TOL, err
+
+
 def test_k32_8x8_single_image_tiles_bit_identical(cuda, golden, monkeypatch):
     """DM_K32_8X=1: the 8^2 convs on 64-row single-image tiles (4 waves of 32 x 64, two blocks per CU) give the
     same bits as the 128 x 128 two-image tiles (same K order per output element), GroupNorm partials included."""
