@@ -82,6 +82,8 @@ def test_bench_gpus2_launches_two_ranks():
     line = lines[0]
     assert line['n_gpus'] == 2 and line['config']['global_batch'] == 8 and line['config']['parallelism'] == 'dp2'
     assert line['value'] > 0 and line['steps'] == 2
+    # the fold's gather path is named in the line (on GPUs: the C-ABI RCCL all-gather, dm_allgather_f32)
+    assert line['config']['gather'] == 'gloo (host)', line['config']
 
 
 def test_bench_rejects_gpus_world_mismatch():
