@@ -351,7 +351,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
         double s1 = 0, s2 = 0;
 #pragma unroll 4
         for (int k = 0; k < a.gin_nchunk; ++k) {
-          const double2 v = gin_chunk(a, b, k, gg, G);
+          const double2 v = a.gin_part[((size_t)b * a.gin_nchunk + k) * G + gg];
           s1 += v.x;
           s2 += v.y;
         }
@@ -709,7 +709,7 @@ __global__ void __launch_bounds__(NW * 64) conv_k32s_kernel(ConvArgs a, PatchGeo
         const int b = b0 + i / G, gg = i - (i / G) * G;
         double s1 = 0, s2 = 0;
         for (int k = 0; k < a.gin_nchunk; ++k) {
-          const double2 v = gin_chunk(a, b, k, gg, G);
+          const double2 v = a.gin_part[((size_t)b * a.gin_nchunk + k) * G + gg];
           s1 += v.x;
           s2 += v.y;
         }

@@ -454,7 +454,7 @@ conv_patch3_kernel(ConvArgs a, PatchGeom g) {
         const int b = tab_img0 + i / G, gg = i - (i / G) * G;
         double s1 = 0, s2 = 0;
         for (int k = 0; k < a.gin_nchunk; ++k) {
-          const double2 v = gin_chunk(a, b, k, gg, G);
+          const double2 v = a.gin_part[((size_t)b * a.gin_nchunk + k) * G + gg];
           s1 += v.x;
           s2 += v.y;
         }

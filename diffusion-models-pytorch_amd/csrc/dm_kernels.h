@@ -54,12 +54,6 @@ struct ConvArgs {
   float gin_eps;
   const float *gin_gamma, *gin_beta, *gin_ms, *gin_mb;
   int gin_mp;
-  // with gin_ps: x1 is an up-path concat [h | skip] and the partials are its slices' own (h: gin_part, gin_Gh
-  // groups of gin_cph channels over the first gin_Ch; skip: gin_ps, gin_Gs groups of gin_cps): each concat
-  // group's chunk partial is summed from them in the kernel exactly as gn_concat_stats sums it (gn.hip), and
-  // that launch is skipped (gin_chunk)
-  const double2* gin_ps;
-  int gin_Ch, gin_cph, gin_Gh, gin_cps, gin_Gs;
   // split-K over input-channel chunks (halo-patch kernel, MODE 0/1): ksplit > 1 writes raw partial
   // sums to kpart [ksplit][M][Cout] and a reduction pass sums them in split order and applies the
   // epilogue. The split count is fixed per layer shape (not per batch), so results stay batch-invariant.
@@ -90,26 +84,6 @@ struct ConvArgs {
   float ap_alpha, ap_bscale;
   int ap_ea, ap_eb, ap_ev;
 };
-
-// Chunk k's {sum, sumsq} of GroupNorm group gg (of G over Cin1) for image b, for the in-kernel finalize: the
-// partial as stored, or, for a concat input (gin_ps), gn_concat_stats's sum of the slices' groups in its order.
-__device__ __forceinline__ double2 gin_chunk(const ConvArgs& a, int b, int k, int gg, int G) {
-  const size_t bk = (size_t)b * a.gin_nchunk + k;
-  if (!a.gin_ps) return a.gin_part[bk * G + gg];
-  const int cpg = a.Cin1 / G, c_lo = gg * cpg, c_hi = c_lo + cpg;
-  double s1 = 0.0, s2 = 0.0;
-  for (int c = c_lo; c < min(c_hi, a.gin_Ch); c += a.gin_cph) {
-    const double2 v = a.gin_part[bk * a.gin_Gh + c / a.gin_cph];
-    s1 += v.x;
-    s2 += v.y;
-  }
-  for (int c = max(c_lo, a.gin_Ch); c < c_hi; c += a.gin_cps) {
-    const double2 v = a.gin_ps[bk * a.gin_Gs + (c - a.gin_Ch) / a.gin_cps];
-    s1 += v.x;
-    s2 += v.y;
-  }
-  return make_double2(s1, s2);
-}
 
 // Patch-pixel capacity of the halo-patch kernels' LDS images (fp32 / split-bf16; 128- / 64-row tiles)
 constexpr int kPatchMax128 = 288;

@@ -734,26 +734,7 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
   }
   if (alloc_failed) { set_error("workspace allocation failed"); return DM_ERR_HIP; }
 
-  // an up-path concat's GroupNorm statistics still to be combined from its slices' partials (gn_stats_concat,
-  // DM_GN_CONCAT_INKERNEL=1): taken over by the consumer conv's in-kernel finalize (gn_prologue:
-  // ConvArgs::gin_ps, no launch), or the gn_concat_stats launch is added before the next op of the plan
-  struct ConcatGn {
-    const double2* ph = nullptr;
-    const double2* ps = nullptr;
-    int Ch = 0, Gh = 0, Cs = 0, Gs = 0, HW = 0;
-  };
-  ConcatGn concat_pending;
-  auto flush_concat = [&]() {
-    if (!concat_pending.ph) return;
-    const ConcatGn cg = concat_pending;
-    concat_pending = ConcatGn{};
-    double2* out = part;
-    pl.add("gn_concat_stats", 0, 32.0 * B * gn_num_chunks(cg.HW) * G, [=](hipStream_t st) {
-      return gn_concat_stats(cg.ph, cg.Ch, cg.Gh, cg.ps, cg.Cs, cg.Gs, B, cg.HW, G, out, st);
-    });
-  };
   auto add = [&](std::string label, double flops, double bytes, std::function<int(hipStream_t)> fn) {
-    flush_concat();
     pl.add(std::move(label), flops, bytes, std::move(fn));
   };
   auto conv_cost = [](const ConvArgs& c, double& fl, double& by) {
@@ -917,14 +898,12 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
     auto ih = gn_ready.find(v.p), is = gn_ready.find(sk.p);
     if (!std::getenv("DM_GN_NO_CONCAT") && ih != gn_ready.end() && ih->second.C == Ch && is != gn_ready.end() &&
         is->second.C == sk.C && gn_concat_ok(Ch, ih->second.G, sk.C, is->second.G, G)) {
-      concat_pending.ph = ih->second.p;
-      concat_pending.ps = is->second.p;
-      concat_pending.Ch = Ch; concat_pending.Gh = ih->second.G;
-      concat_pending.Cs = sk.C; concat_pending.Gs = is->second.G;
-      concat_pending.HW = v.H * v.W;
-      // the separate gn_concat_stats launch by default: combining in the consumer's in-kernel finalize
-      // (DM_GN_CONCAT_INKERNEL=1) re-reads the slices' partials in every block's prologue, C3 A/B -0.7 %
-      if (!std::getenv("DM_GN_CONCAT_INKERNEL")) flush_concat();
+      const double2* ph = ih->second.p;
+      const double2* ps = is->second.p;
+      const int Cs = sk.C, HW = v.H * v.W, Gh = ih->second.G, Gs = is->second.G;
+      add("gn_concat_stats", 0, 32.0 * B * gn_num_chunks(HW) * G, [=](hipStream_t st) {
+        return gn_concat_stats(ph, Ch, Gh, ps, Cs, Gs, B, HW, G, part, st);
+      });
       return part;
     }
     return gn_stats(v);
@@ -944,15 +923,7 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
     // in-kernel finalize: every block re-reduces its images' chunk partials, so only for small maps
     // (CIFAR: <= 16 chunks per image); the 256^2 maps of ADM have 1024 and take the finalize launch
     if (conv_lds_tables(c) && imgs * G <= 512 && v.C == c.Cin1 && gn_num_chunks(v.H * v.W) <= 64) {
-      c.gin_part = stp; c.gin_ps = nullptr;
-      if (concat_pending.ph && stp == part && concat_pending.Ch + concat_pending.Cs == v.C &&
-          concat_pending.HW == v.H * v.W) {  // the concat's slices' partials, combined in the kernel
-        c.gin_part = concat_pending.ph; c.gin_ps = concat_pending.ps;
-        c.gin_Ch = concat_pending.Ch; c.gin_Gh = concat_pending.Gh; c.gin_cph = concat_pending.Ch / concat_pending.Gh;
-        c.gin_Gs = concat_pending.Gs; c.gin_cps = concat_pending.Cs / concat_pending.Gs;
-        concat_pending = ConcatGn{};
-      }
-      c.gin_G = G; c.gin_nchunk = gn_num_chunks(v.H * v.W);
+      c.gin_part = stp; c.gin_G = G; c.gin_nchunk = gn_num_chunks(v.H * v.W);
       c.gin_n = (double)v.H * v.W * (v.C / G); c.gin_eps = 1e-5f;
       c.gin_gamma = P(gamma); c.gin_beta = P(beta); c.gin_ms = ms; c.gin_mb = mb; c.gin_mp = mp;
       return;

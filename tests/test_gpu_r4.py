@@ -127,39 +127,6 @@ def test_folded_attention_opt_variants_bit_identical(cuda, golden, monkeypatch, 
     assert torch.equal(outs['plain'][1], outs[opt][1])
 
 
-@pytest.mark.parametrize('arch', ['cifar10', 'adagn'])
-def test_concat_gn_stats_in_kernel_bit_identical(cuda, golden, monkeypatch, arch):
-    """The up-path concats' GroupNorm statistics combined from their slices' partials inside the consumer conv's
-    in-kernel finalize (DM_GN_CONCAT_INKERNEL=1: ConvArgs::gin_ps, gn_concat_stats's summation order) equal the
-    separate gn_concat_stats launch's (the default) bit for bit, with no gn_concat_stats launch left."""
-    _, meta = golden('forward')
-    g = torch.Generator().manual_seed(37)
-    x = torch.randn((3, 3, 32, 32), generator=g).to(cuda)
-    t = torch.randint(0, 1000, (3, ), generator=g).to(cuda)
-    outs, ncat = {}, {}
-    for mode in ('launch', 'kernel'):
-        if mode == 'kernel':
-            monkeypatch.setenv('DM_GN_CONCAT_INKERNEL', '1')
-        if arch == 'cifar10':
-            model, _ = _model(meta, 'cifar10', cuda)
-            run = lambda: model(x, t)  # noqa: E731
-        else:
-            from models.unet_categorial_adagn import UNetCategorialAdaGN
-            model = UNetCategorialAdaGN(**golden('adagn')[1]['archs']['cfg_cifar10']).eval()
-            init_synthetic_(model)
-            model = model.to(cuda)
-            y = torch.tensor([1, 3, 5], device=cuda)
-            run = lambda: model(x, t, y)  # noqa: E731
-        outs[mode] = run()
-        h = _profile_labels(model, cuda)
-        run()
-        ncat[mode] = _labels(h).count('gn_concat_stats')
-        dmhip.unet_profile_enable(h, 0)
-        del model
-    assert ncat['kernel'] == 0 and ncat['launch'] > 0, ncat
-    assert torch.equal(outs['kernel'], outs['launch'])
-
-
 def test_attention_in_kernel_gn_finalize_bit_identical(cuda, golden, monkeypatch):
     """Variant 4 computes its GroupNorm affine from the chunk partials in the kernel (gn_finalize's expressions
     and summation order): whole forwards equal the separate gn_finalize launch's (DM_ATTN_GNFIN=1) bit for bit,
