@@ -1104,8 +1104,10 @@ int conv_k32_pick(const ConvArgs& a) {
   }
   const int p = conv_pick(a);
   if (p != 3 && p != 4) return 0;
-  // DM_K32_8X=1 (A/B): 8^2 maps on 64-row single-image tiles (two blocks per CU where 128 x 128 tiles give one)
-  if (std::getenv("DM_K32_8X") && std::getenv("DM_K32_8X")[0] == '1' && conv_k32_variant_ok(a, 11)) return 11;
+  // 8^2 maps on 64-row single-image tiles (two blocks per CU where 128 x 128 tiles give one; bit-identical):
+  // C3 A/B +0.3 % / +0.25 % over two sessions' alternations; DM_K32_8X=0 keeps the 128 x 128 two-image tiles
+  const char* e8 = std::getenv("DM_K32_8X");
+  if (!(e8 && e8[0] == '0') && conv_k32_variant_ok(a, 11)) return 11;
   // 128 x 128 tiles down to one block per CU (measured on 8^2 maps at B = 256: 256 blocks of 128 x 128 beat
   // 512 of 128 x 64 by 6 %); the nominal batch (pick_B) keeps the choice batch-invariant
   const long M = (long)(a.pick_B > 0 ? a.pick_B : a.B) * a.Hout * a.Wout;

@@ -457,16 +457,19 @@ def test_linear_k32_half_width_blocks_bit_identical(cuda, golden, monkeypatch):
 
 
 def test_k32_8x8_single_image_tiles_bit_identical(cuda, golden, monkeypatch):
-    """DM_K32_8X=1: the 8^2 convs on 64-row single-image tiles (4 waves of 32 x 64, two blocks per CU) give the
-    same bits as the 128 x 128 two-image tiles (same K order per output element), GroupNorm partials included."""
+    """The 8^2 convs on 64-row single-image tiles (4 waves of 32 x 64, two blocks per CU; the default) give the
+    same bits as the 128 x 128 two-image tiles (DM_K32_8X=0; same K order per output element), GroupNorm partials
+    included."""
     _, meta = golden('forward')
     g = torch.Generator().manual_seed(37)
     x = torch.randn((4, 3, 32, 32), generator=g).to(cuda)
     t = torch.randint(0, 1000, (4, ), generator=g).to(cuda)
     outs = {}
     for mode in ('base', '8x'):
-        if mode == '8x':
-            monkeypatch.setenv('DM_K32_8X', '1')
+        if mode == 'base':
+            monkeypatch.setenv('DM_K32_8X', '0')
+        else:
+            monkeypatch.delenv('DM_K32_8X', raising=False)
         model, _ = _model(meta, 'cifar10', cuda)
         outs[mode] = model(x, t)
         del model
