@@ -1,4 +1,7 @@
 // C-ABI wrappers over the kernel launchers (include/dm_hip.h).
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <string>
 #include "dm_common.h"
 #include "dm_kernels.h"
@@ -9,7 +12,43 @@ thread_local std::string g_last_error;
 }
 void set_error(const std::string& msg) { g_last_error = msg; }
 const char* last_error() { return g_last_error.c_str(); }
+
+namespace {
+Toggles g_toggles;
+bool env_is(const char* name, char c) {
+  const char* e = std::getenv(name);
+  return e && e[0] == c;
+}
+bool g_launch_log_on = false;
+std::string g_launch_log;
+}  // namespace
+const Toggles& toggles() { return g_toggles; }
+void refresh_toggles() {
+  Toggles t;
+  t.wino = !env_is("DM_CONV_WINO", '0');
+  t.k32s_w4 = env_is("DM_K32S_W4", '1');
+  g_toggles = t;
+}
+void note_launch(const char* name) {
+  if (!g_launch_log_on) return;
+  g_launch_log += name;
+  g_launch_log += '\n';
+}
 }  // namespace dm
+
+/* Test hook: enable (1, clearing it) / disable (0) the launch log; read copies it NUL-terminated into buf. */
+extern "C" int dm_debug_launch_log(int enable) {
+  dm::g_launch_log_on = enable != 0;
+  if (enable) dm::g_launch_log.clear();
+  return DM_OK;
+}
+extern "C" int dm_debug_launch_log_read(char* buf, int len) {
+  if (!buf || len <= 0) { dm::set_error("launch log: null buffer"); return DM_ERR_ARG; }
+  const size_t n = std::min(dm::g_launch_log.size(), (size_t)len - 1);
+  memcpy(buf, dm::g_launch_log.data(), n);
+  buf[n] = 0;
+  return (int)n;
+}
 
 using dm::View;
 
@@ -96,6 +135,7 @@ extern "C" int dm_pack_conv_weight(const float* w, int Cout, int Cin, int taps, 
 }
 
 extern "C" int dm_conv2d_nhwc(const dm_conv_desc* d, void* stream) {
+  dm::refresh_toggles();
   if (!d || !d->x || !d->w || !d->y) { dm::set_error("null tensor"); return DM_ERR_ARG; }
   dm::ConvArgs a{};
   a.x1 = d->x; a.x1_pitch = d->x_pitch; a.Cin1 = d->Cin; a.Hin = d->Hin; a.Win = d->Win;
@@ -122,7 +162,24 @@ extern "C" int dm_conv2d_nhwc(const dm_conv_desc* d, void* stream) {
       a.ws_rowscale = dm::split_conv_rowscale(a.ws, a.upsample == 2 ? 4 : 1, a.Cout, a.K);
     a.range_flag = d->range_flag;
   }
+  if (d->w_wino) {
+    if (!a.ws || a.ws_np != DM_SPLIT_FP16X2) {
+      dm::set_error("conv: w_wino needs w_split of kind DM_SPLIT_FP16X2");
+      return DM_ERR_ARG;
+    }
+    a.wino_ws = d->w_wino;
+    a.wino_rowscale = dm::wino_rowscale(d->w_wino, a.Cout, a.Cin1);
+  }
   return dm::conv2d_igemm(a, (hipStream_t)stream);
+}
+
+extern "C" int64_t dm_conv_weight_wino_bytes(int Cout, int Cin) {
+  if (Cout <= 0 || Cin <= 0 || Cin % 32 != 0) return -1;
+  return (int64_t)dm::wino_weights_bytes(Cout, Cin);
+}
+
+extern "C" int dm_pack_conv_weight_wino(const float* w, int Cout, int Cin, void* out, void* stream) {
+  return dm::wino_weights(w, Cout, Cin, out, (hipStream_t)stream);
 }
 
 extern "C" int64_t dm_conv_weight_split_bytes(int nmat, int Cout, int K, int kind) {
@@ -143,6 +200,7 @@ extern "C" int dm_pack_conv_weight_subpixel(const float* w, int Cout, int Cin, f
 }
 
 extern "C" int dm_gemm(const dm_gemm_desc* d, void* stream) {
+  dm::refresh_toggles();
   if (!d || !d->A || !d->B || !d->C) { dm::set_error("null tensor"); return DM_ERR_ARG; }
   dm::GemmArgs g{};
   g.M = d->M; g.N = d->N; g.K = d->K; g.Z1 = d->Z1; g.Z2 = d->Z2;

@@ -278,14 +278,21 @@ int conv2d_igemm(const ConvArgs& a, hipStream_t st) {
   }
   const long M = (long)a.B * a.Hout * a.Wout;
   DM_REQUIRE(M > 0 && M < (1L << 31), "conv: M out of range");
-  DM_REQUIRE(a.tile >= 0 && a.tile <= 20, "conv: tile must be 0..20");
+  DM_REQUIRE(a.tile >= 0 && a.tile <= 21, "conv: tile must be 0..21");
+  if (a.tile == 21 || (a.tile == 0 && a.wino_ws)) {  // the Winograd F(2,3) kernel (conv_wino.hip)
+    if (conv_wino_ok(a)) {
+      DM_REQUIRE(!a.gn_part || conv_can_emit_gn(a), "conv: GroupNorm statistics need groups of 4..32 channels");
+      return conv2d_wino(a, st);
+    }
+    DM_REQUIRE(a.tile == 0, "conv: tile 21 needs Winograd weights and a shape conv_wino_kernel takes");
+  }
   const int mode = conv_mode(a);
   const int pick = conv_pick(a);
   DM_REQUIRE(!a.gn_part || conv_can_emit_gn(a), "conv: GroupNorm statistics need a 128-row halo-patch tile, "
                                                  "whole 64-pixel chunks and groups within 32 channels");
   DM_REQUIRE(!a.pro_scale || (pick >= 3 && a.pro_shift && aligned16(a.pro_scale) && aligned16(a.pro_shift)),
              "conv: the GroupNorm prologue needs a halo-patch shape (3x3 stride 1 / upsample, whole-row tiles)");
-  if (const int k32 = conv_k32_pick(a)) return conv2d_k32(a, k32, st);
+  if (const int k32 = a.k32_resolved ? a.k32_resolved - 1 : conv_k32_pick(a)) return conv2d_k32(a, k32, st);
   if (pick >= 3 && a.taps == 1) return conv2d_patch3(a, pick + 1, PatchGeom{}, st);  // MODE 3 (split 1x1)
   if (pick >= 3) {
     PatchGeom g;
@@ -338,6 +345,8 @@ int conv_pick(const ConvArgs& a) {
 }
 
 bool conv_can_emit_gn(const ConvArgs& a) {
+  if ((a.tile == 0 || a.tile == 21) && conv_wino_ok(a))  // StagedEpilogue over 64-pixel chunks of one image
+    return a.gn_G > 0 && a.Cout % a.gn_G == 0 && (a.Cout / a.gn_G) % 4 == 0 && a.Cout / a.gn_G <= 32;
   if (a.ksplit > 1)  // the split-K reduction emits them (conv_splitk_reduce_gn_kernel): one chunk per image
     return !a.upsample && a.Hout * a.Wout <= kGnPixPerChunk && a.gn_G > 0 && a.Cout % a.gn_G == 0 &&
            a.Cout <= 1024;
@@ -372,7 +381,8 @@ std::string conv_label(const ConvArgs& a) {
                                 "conv_patch_kernel<128,64,64,32",  "conv_patch_kernel<64,64,32,32",
                                 "conv_patch_kernel<256,256,128,128", "conv_patch_kernel<512,128,128,128",
                                 "conv_patch_kernel<128,128,64,64"};
-  if (const int k32 = conv_k32_pick(a)) return conv_k32_label(a, k32);
+  if ((a.tile == 0 || a.tile == 21) && conv_wino_ok(a)) return conv_wino_label(a);
+  if (const int k32 = a.k32_resolved ? a.k32_resolved - 1 : conv_k32_pick(a)) return conv_k32_label(a, k32);
   const int p = conv_pick(a);
   std::string s = names[p];
   if (p < 3) s += "," + std::to_string(conv_mode(a)) + ">";  // <BM,BN,WM,WN,MODE>

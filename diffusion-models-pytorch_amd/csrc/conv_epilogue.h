@@ -118,6 +118,11 @@ struct StagedEpilogue {
   }
   // the slab's rows are output rows row0 .. row0 + 31 (this wave's slab written and visible)
   __device__ __forceinline__ void rows(const float* st, int row0) {
+    rows_f([&](int row) { return *reinterpret_cast<const f4*>(st + row * EP + 4 * c4); }, row0);
+  }
+  // the same with the lane's 4 values of slab row `row` (columns 4 c4 ..) from val(row) instead of a staged slab
+  template <class F>
+  __device__ __forceinline__ void rows_f(F val, int row0) {
     f4 rs4[32 / RPI];
     if (a.res) {
 #pragma unroll
@@ -130,7 +135,7 @@ struct StagedEpilogue {
     for (int it = 0; it < 32 / RPI; ++it) {
       const int row = it * RPI + rsub;
       const int m = row0 + row;
-      f4 v = *reinterpret_cast<const f4*>(st + row * EP + 4 * c4);
+      f4 v = val(row);
       if (a.bias) v = v + bias4;
       if (a.rowvec)
         v = v + (one_image ? rv4
@@ -142,6 +147,45 @@ struct StagedEpilogue {
         for (int e = 0; e < 4; ++e) {
           gs[e] += (double)v[e];
           gq[e] += (double)v[e] * v[e];
+        }
+      }
+    }
+  }
+  // output rows in pairs (row0 + 2 i, row0 + 2 i + 1 for i < 16: a 32-row slab): val2(i, v0, v1) gives the lane's 4
+  // values of both (the Winograd output transform, conv_wino.hip), then as rows()
+  template <class F>
+  __device__ __forceinline__ void pairs_f(F val2, int row0) {
+    constexpr int IT = 16 / RPI;
+    f4 rs4[IT][2];
+    if (a.res) {
+#pragma unroll
+      for (int it = 0; it < IT; ++it)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int m = min(row0 + 2 * (it * RPI + rsub) + s, M - 1);
+          rs4[it][s] = *reinterpret_cast<const f4*>(a.res + out_row(m) * a.res_pitch + nc);
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int i = it * RPI + rsub;
+      f4 v[2];
+      val2(i, v[0], v[1]);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int m = row0 + 2 * i + s;
+        if (a.bias) v[s] = v[s] + bias4;
+        if (a.rowvec)
+          v[s] = v[s] + (one_image ? rv4
+                                   : *reinterpret_cast<const f4*>(a.rowvec + (size_t)(min(m, M - 1) / HWo) * a.rowvec_pitch + nc));
+        if (a.res) v[s] = v[s] + rs4[it][s];
+        if (m < M && c_ok) *reinterpret_cast<f4*>(a.y + out_row(m) * a.y_pitch + ncol) = v[s];
+        if (a.gn_part && m < M) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            gs[e] += (double)v[s][e];
+            gq[e] += (double)v[s][e] * v[s][e];
+          }
         }
       }
     }

@@ -946,7 +946,7 @@ static bool conv_k32s_ok(const ConvArgs& a) {
 static bool t2d_geom(const ConvArgs& a, PatchGeom& g);
 
 int conv_k32_variant_ok(const ConvArgs& a, int v) {
-  if (v == 6) return conv_k32s_ok(a) ? 1 : 0;
+  if (v == 6 || v == 12) return conv_k32s_ok(a) ? 1 : 0;
   if (v == 11) {  // 64-row tiles of one <= 64-pixel image (8^2 maps), 4 waves of 32 x 64
     if (!(a.ws && a.ws_np == 2 && a.ws_rowscale && a.taps == 9 && a.stride == 1 && a.upsample == 0)) return 0;
     if (a.Cin1 < kC || a.Cin1 % kC != 0 || a.Cin2 % kC != 0 || a.ksplit > 1 || a.K != 9 * a.Cin1 + a.Cin2) return 0;
@@ -1088,7 +1088,7 @@ int conv_k32_pick(const ConvArgs& a) {
   // split-K convs of maps of <= 16 pixels: 64 x 128 tiles (4x4 maps at B = 256, K split 2: 32.5 us vs
   // 34.2 us for 64 x 64 and for conv_patch3's 64 x 64 split tiles)
   if (a.ksplit > 1) {
-    if (conv_k32_small_enabled() && conv_k32_variant_ok(a, 6)) return 6;
+    if (conv_k32_small_enabled() && conv_k32_variant_ok(a, 6)) return toggles().k32s_w4 ? 12 : 6;
     return conv_k32_variant_ok(a, 4) ? 4 : conv_k32_variant_ok(a, 3) ? 3 : 0;
   }
   if (!conv_k32_ok(a)) {
@@ -1116,10 +1116,8 @@ int conv_k32_pick(const ConvArgs& a) {
 
 // rocprofv3's name of the instantiation conv2d_k32 launches (spaces removed)
 std::string conv_k32_label(const ConvArgs& a, int v) {
-  if (v == 6) {
-    const bool w4 = std::getenv("DM_K32S_W4") && std::getenv("DM_K32S_W4")[0] == '1';
-    return std::string("conv_k32s_kernel<") + (a.pro_scale || a.gin_part ? "true," : "false,") + (w4 ? "4>" : "8>");
-  }
+  if (v == 6 || v == 12)
+    return std::string("conv_k32s_kernel<") + (a.pro_scale || a.gin_part ? "true," : "false,") + (v == 12 ? "4>" : "8>");
   if (v == 7)
     return std::string("conv_k32_kernel<128,128,64,32,") + (a.pro_scale ? "true," : "false,") + "false," +
            (a.upsample == 2 ? "true,512>" : "false,512>");
@@ -1165,20 +1163,20 @@ static void launch_k32(const ConvArgs& a, const PatchGeom& g, hipStream_t st) {
 }
 
 int conv2d_k32(const ConvArgs& a, int v, hipStream_t st) {
-  DM_REQUIRE(v >= 1 && v <= 11 && conv_k32_variant_ok(a, v), "conv: shape not supported by the K = 32 split kernel");
+  DM_REQUIRE(v >= 1 && v <= 12 && conv_k32_variant_ok(a, v), "conv: shape not supported by the K = 32 split kernel");
   PatchGeom g;
-  if (v == 6) {
+  if (v == 6 || v == 12) {  // the small-map kernel: 8 waves (6), or its 4-wave form (12, one wave per SIMD)
     conv_patch_geom(a, 64, g);
     const int blocks = ceil_div(a.B * a.Hout * a.Wout, 64) * (a.Cout / 64);
-    // DM_K32S_W4=1: the 4-wave form (one wave per SIMD)
-    static const bool w4 = std::getenv("DM_K32S_W4") && std::getenv("DM_K32S_W4")[0] == '1';
     const bool pro = a.pro_scale || a.gin_part;
-    if (w4) {
+    if (v == 12) {
       if (pro) hipLaunchKernelGGL((conv_k32s_kernel<true, 4>), dim3(blocks), dim3(256), 0, st, a, g);
       else hipLaunchKernelGGL((conv_k32s_kernel<false, 4>), dim3(blocks), dim3(256), 0, st, a, g);
+      note_launch(pro ? "conv_k32s_kernel<true,4>" : "conv_k32s_kernel<false,4>");
     } else {
       if (pro) hipLaunchKernelGGL((conv_k32s_kernel<true, 8>), dim3(blocks), dim3(512), 0, st, a, g);
       else hipLaunchKernelGGL((conv_k32s_kernel<false, 8>), dim3(blocks), dim3(512), 0, st, a, g);
+      note_launch(pro ? "conv_k32s_kernel<true,8>" : "conv_k32s_kernel<false,8>");
     }
     DM_LAUNCH_CHECK();
     return DM_OK;

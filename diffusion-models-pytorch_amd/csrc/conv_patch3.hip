@@ -820,7 +820,7 @@ int split_conv_weights(const float* w, int nmat, int rows, int K, int cin1, int 
                        hipStream_t st) {
   DM_REQUIRE(w && out && nmat > 0 && rows > 0, "split weights: empty");
   DM_REQUIRE(np == 2 || np == 3, "split weights: kind must be 2 (fp16x2) or 3 (bf16x3)");
-  DM_REQUIRE(K % kSK == 0 && cin1 % 32 == 0 && ntap * cin1 <= K && (ntap == 9 || ntap == 4 || ntap == 1),
+  DM_REQUIRE(K % kSK == 0 && cin1 % 32 == 0 && ntap * cin1 <= K && (ntap == 9 || ntap == 4 || ntap == 3 || ntap == 1),
              "split weights: K must be ntap * cin1 (+ a second segment), cin1 a multiple of 32");
   DM_REQUIRE((reinterpret_cast<uintptr_t>(w) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0,
              "split weights: 16-byte alignment");

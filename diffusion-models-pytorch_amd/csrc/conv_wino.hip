@@ -1,0 +1,500 @@
+// 3x3 stride-1 convolution (models/unet.py:16,26: the ResBlock convs) as a Winograd F(2,3) along x and a direct
+// 3-tap sum along y, on the fp16x2 split matrix cores of conv_k32.hip.
+//
+// Per output row y and output pixel pair (2j, 2j + 1), tap row dy and input channel c, the 1-D filter
+// g = w[dy][0..2] over d = x[y + dy - 1][2j - 1 .. 2j + 2] (zero padding outside the map) is
+//   V = B^T d = (d0 - d2, d1 + d2, d2 - d1, d1 - d3),  U = G g = (g0, (g0 + g1 + g2) / 2, (g0 - g1 + g2) / 2, g2),
+//   y0 = m0 + m1 + m2,  y1 = m1 - m2 - m3,  m_nu = sum over (c, dy) of V_nu U_nu,
+// i.e. four GEMMs (nu = 0..3) with K = 3 Cin: 12 K = 32 steps per pair and 32-channel chunk where the direct
+// conv takes 9 per pixel (18 per pair) -- 2/3 of the MFMA products. U is formed once at plan build in float64
+// (wino_pack_kernel) and split like every other weight (split_conv_weights, nmat = 4, ntap = 3: one power-of-two
+// row scale per output channel over all four matrices); V is formed in fp32 from the GroupNorm + SiLU'd patch
+// (one rounding) and split in the loader; the output transform is fp32 in the epilogue.
+//
+// Block: 512 threads, a 128-pixel tile (TH = 128 / W whole rows of a W = 32 or 16 wide map: 64 pairs) x 128
+// output channels. Wave w = (nu = w >> 1, ch = w & 1) computes GEMM nu for the 64 pairs x 64 channels of column
+// half ch: 4 x 4 tiles of v_mfma_f32_16x16x32_f16, three per product (a1 w0 + a0 w1 + a0 w0), 48 MFMAs per
+// K step as conv_k32's 64 x 64 wave tiles -- so the operand traffic per MFMA is conv_k32's, and the 8 waves
+// (two per SIMD) keep the same occupancy in one block per CU.
+// LDS: per 32-channel chunk the transformed patch, [nu][(TH + 2) x NP pair rows][piece][4 k-groups][8] fp16 with
+// conv_k32's 160-B row pitch (A fragment i of tap row dy for wave nu = 16 consecutive rows
+// nu NR + 16 i + dy NP: conflict-free ds_read_b128), double buffered, one barrier per chunk. The loader: lane j
+// of a (patch row, 8-channel quarter) unit loads pixels 2j, 2j + 1, applies GroupNorm + SiLU, and takes its
+// neighbours' 2j - 1 and 2j + 2 from lanes j -/+ 1 by DPP row shifts (each pixel normalised once).
+// Epilogue: the 8 waves' m_nu tiles (row scale undone) into LDS, then each wave takes 32 output pixels x 64
+// channels through StagedEpilogue (output transform, bias, temb row vector, residual, 16-B stores, GroupNorm
+// partials of the consumer per 64-pixel chunk, the two 32-pixel halves combined in LDS).
+#include <cstdlib>
+#include <string>
+
+#include "dm_common.h"
+#include "dm_kernels.h"
+#include "mfma_tile.h"
+#include "split16.h"
+#include "conv_epilogue.h"
+
+namespace dm {
+
+namespace {
+
+#ifndef DM_WINO_ABL
+#define DM_WINO_ABL 0
+#endif
+
+constexpr int kWC = 32;                        // input channels per chunk (K of one MFMA step)
+constexpr int kWRowH = 80;                     // LDS row pitch in fp16 (160 B), as conv_k32
+constexpr int kWNR = 96;                       // pair rows per nu plane at most: (TH + 2) NP = 6 x 16 / 10 x 8
+constexpr int kWBuf = 4 * kWNR * kWRowH;       // fp16 per patch buffer (61440 B)
+constexpr int kWTab = 4096;                    // GroupNorm table floats: one image, Cin <= 2048 (scales, shifts)
+constexpr int kWEP = 68;                       // epilogue plane pitch (floats)
+constexpr int kWSmem = 2 * kWBuf * 2 + kWTab * 4;  // 139264 B
+static_assert(4 * 2 * 64 * kWEP * 4 <= kWSmem, "the epilogue's m planes fit the main loop's LDS");
+constexpr int kWMaxG = 32;                     // in-kernel GroupNorm finalize: groups of the input
+
+#ifdef DM_K32_STAMPS
+// Diagnostic build only (-DDM_K32_STAMPS, tools/wino_stamps.py): per block, wave 0's s_memtime at the start, after
+// the prologue, after the main loop and at the end, and s_memrealtime at the start and the end, into this buffer only.
+__device__ unsigned long long g_wino_stamps[65536][8];
+#define W_STAMP(k)                                                                                           \
+  do {                                                                                                       \
+    if (threadIdx.x == 0 && blockIdx.x < 65536) g_wino_stamps[blockIdx.x][k] = __builtin_amdgcn_s_memtime();     \
+  } while (0)
+#define W_RSTAMP(k)                                                                                          \
+  do {                                                                                                       \
+    if (threadIdx.x == 0 && blockIdx.x < 65536) g_wino_stamps[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define W_STAMP(k) do {} while (0)
+#define W_RSTAMP(k) do {} while (0)
+#endif
+
+// x - hi[k] (hi[k] an fp16 piece of x: exact) in one v_fma_mix_f32 (the f16 operand converted in the instruction) instead
+// of a conversion and a subtraction
+__device__ __forceinline__ float sub_f16(float x, f16x4 hi, int k) {
+  typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+  const u2v hp = __builtin_bit_cast(u2v, hi);
+  float r;
+  if (k & 1)
+    asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(hp[k >> 1]), "v"(x));
+  else
+    asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[0,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(hp[k >> 1]), "v"(x));
+  return r;
+}
+
+// DPP row shift by one lane (row_shr:1 = from lane - 1, row_shl:1 = from lane + 1), 0 where the source lane is
+// outside the 16-lane row (bound_ctrl)
+__device__ __forceinline__ float dpp_f(float v, int ctrl_shr) {
+  return __builtin_bit_cast(float, ctrl_shr ? __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x111, 0xF, 0xF, true)
+                                            : __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x101, 0xF, 0xF, true));
+}
+
+// PROM: input prologue -- 0 none, 1 GroupNorm affine, 2 GroupNorm affine + SiLU
+template <int W, int PROM>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) conv_wino_kernel(ConvArgs a) {
+  constexpr bool PRO = PROM != 0;
+  constexpr int NP = W / 2, TH = 128 / W, PR = TH + 2, NR = PR * NP;
+  static_assert(NR <= kWNR, "patch plane");
+  constexpr int UPW = PR * 4 / 8;  // loader units (patch row, 8-channel quarter) per wave: 3 (W 32) / 5 (W 16)
+  static_assert(UPW * 8 == PR * 4 && UPW * NP <= 64, "loader units tile the waves");
+  constexpr int TM = 4, TN = 4, NTAP = 3;
+#ifndef DM_WINO_WD
+#define DM_WINO_WD 3
+#endif
+  constexpr int WD = DM_WINO_WD;  // B ring depth: a refill issued behind the next chunk's pixel loads (in-order vmcnt)
+                                 // is consumed WD tap rows later
+  __shared__ __attribute__((aligned(16))) char smem[kWSmem];
+  __shared__ float gstat[2 * kWMaxG];
+  __shared__ double gxr[8 * 16 * 2];
+  __shared__ __attribute__((aligned(16))) float gzero[8];  // the padding rows' table: 0 scale, 0 shift
+  _Float16* patch = reinterpret_cast<_Float16*>(smem);
+  float* gtab = reinterpret_cast<float*>(smem + 2 * kWBuf * 2);
+
+  const int HW = a.Hout * W;
+  const int M = a.B * HW, N = a.Cout;
+  const int nN = N / 128;
+  const int bid = xcd_remap_p(blockIdx.x, gridDim.x);
+  const int mt = bid / nN, nt = bid - mt * nN;
+  const int m0 = mt * 128, n0 = nt * 128;
+  const int b0 = m0 / HW;
+  const int y0 = (m0 - b0 * HW) / W;
+
+  W_RSTAMP(5);
+  W_STAMP(0);
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int nu = wave >> 1, ch = wave & 1;
+  const int l16 = lane & 15, q = lane >> 4;
+
+  // ---- loader: unit u = (patch row pr, quarter sq), lane lj of the unit = pair lj (pixels 2 lj, 2 lj + 1)
+  const int lu = lane / NP, lj = lane - (lane / NP) * NP;
+  const bool lact = lu < UPW;
+  const int u = min(wave * UPW + lu, PR * 4 - 1);
+  const int pr = u >> 2, sq = u & 3;
+  const int iy = y0 - 1 + pr;
+  const bool rok = lact && iy >= 0 && iy < a.Hin;
+  const float* p0 = rok ? a.x1 + ((size_t)(b0 * a.Hin + iy) * W + 2 * lj) * a.x1_pitch + 8 * sq : kZeroPage + 8 * sq;
+  const float* p1 = rok ? p0 + a.x1_pitch : p0;
+  // chunk c + 1's pixels: loaded during chunk c - 1's tap row 2 (after its last use of the registers), finished at
+  // chunk c's tap rows 0 / 1 -- two tap rows of MFMAs and a barrier to cover a load from the Infinity Cache / HBM
+  f4 rw[4];
+  auto load_raw = [&](int c) {
+    const int co = c * kWC;
+    rw[0] = *reinterpret_cast<const f4*>(p0 + co);
+    rw[1] = *reinterpret_cast<const f4*>(p0 + co + 4);
+    rw[2] = *reinterpret_cast<const f4*>(p1 + co);
+    rw[3] = *reinterpret_cast<const f4*>(p1 + co + 4);
+  };
+  if (t < 8) gzero[t] = 0.f;  // (visible after the prologue's barrier)
+  // channels 4 h .. 4 h + 3 of the lane's 8: GroupNorm (+ SiLU) of its two pixels, the neighbours by DPP,
+  // V = B^T d, split, stored into buffer buf. PROM 2: the tables hold -log2(e) (scale, shift), so z' = -log2(e) z
+  // comes out of one fma and silu(z) = -ln 2 * z' / (1 + 2^z'): the loader keeps z' / (1 + 2^z') and the epilogue
+  // scales by -ln 2 (exact algebra; one rounding each). Padding rows read the zero table: exactly 0. Range: a V
+  // beyond fp16's range splits into an infinite piece, which every product carries into the accumulators -- the
+  // epilogue's finiteness check raises the range flag.
+  auto finish = [&](int c, int buf, int h) {
+    f4 e0 = rw[h], e1 = rw[2 + h];
+    if (PROM) {
+      const float* ts = rok ? gtab + 2 * (c * kWC + 8 * sq + 4 * h) : gzero;  // [4 scales][4 shifts]
+      const f4 sc = *reinterpret_cast<const f4*>(ts), sh = *reinterpret_cast<const f4*>(ts + 4);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float z0 = __builtin_fmaf(e0[k], sc[k], sh[k]);
+        const float z1 = __builtin_fmaf(e1[k], sc[k], sh[k]);
+        e0[k] = PROM == 2 ? z0 * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(z0)) : z0;
+        e1[k] = PROM == 2 ? z1 * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(z1)) : z1;
+      }
+    }
+    f4 vv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float d0 = dpp_f(e1[k], 1);  // x[2j - 1]: lane j - 1's second pixel (0 at the row's first pair)
+      float d3 = dpp_f(e0[k], 0);  // x[2j + 2]: lane j + 1's first pixel (0 at the row's last pair)
+      if (NP < 16) {               // two units per DPP row: their boundary is a map edge too
+        d0 = lj == 0 ? 0.f : d0;
+        d3 = lj == NP - 1 ? 0.f : d3;
+      }
+      vv[0][k] = d0 - e1[k];
+      vv[1][k] = e0[k] + e1[k];
+      vv[2][k] = e1[k] - e0[k];
+      vv[3][k] = e0[k] - d3;
+    }
+    if (lact) {
+      _Float16* dst = patch + buf * kWBuf + (pr * NP + lj) * kWRowH + sq * 8 + 4 * h;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        f16x4 hi, lo;  // x = hi + lo, lo = fp16(x - hi) (the difference exact)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) hi[k] = (_Float16)vv[v][k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) lo[k] = (_Float16)sub_f16(vv[v][k], hi, k);
+        *reinterpret_cast<f16x4*>(dst + v * NR * kWRowH) = hi;
+        *reinterpret_cast<f16x4*>(dst + v * NR * kWRowH + 32) = lo;
+      }
+    }
+  };
+
+  // ---- B: the fp16x2 fragment images of U_nu (split_conv_weights, nmat 4, ntap 3), 16-column halves
+  const int Kp = NTAP * a.Cin1;
+  const int ngrp = ceil_div(N, 32);
+  const size_t sl = (size_t)ngrp * 1024;  // fp16 per 16-deep slice
+  // column n0 + ch 64 + 16 j + l16 (n0 % 128 == 0): 32-column group (n0 + ch 64) / 32 + j / 2, column 16 (j & 1) + l16
+  // of it -- one base pointer, compile-time offsets per j
+  const _Float16* wbase = reinterpret_cast<const _Float16*>(a.wino_ws) + (size_t)nu * (Kp / 16) * sl +
+                          (size_t)((n0 + ch * 64) >> 5) * 1024 + ((q & 1) * 32 + l16) * 8;
+  const size_t qoff = (size_t)(q >> 1) * NTAP * sl;
+  auto slice_off = [&](int kt) { return (size_t)(kt + (kt / NTAP) * NTAP) * sl + qoff; };
+  f16x8 bq[WD][TN][2];
+  auto load_b = [&](f16x8 (&dst)[TN][2], size_t off) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+        dst[j][p] = *reinterpret_cast<const f16x8*>(wbase + off + (j >> 1) * 1024 + (j & 1) * 128 + p * 512);
+  };
+
+  f4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  // tap row dy: A fragment i = pair rows nu NR + 16 i + l16 + dy NP of buffer pbuf, the lane's k-group q
+  const int abase = (nu * NR + l16) * kWRowH + q * 8;
+  // a0: tile 0's fragment of this tap row on entry (read ahead); within a chunk, the next tap row's on exit
+  f16x8 a0[2];
+  auto read_a0 = [&](int dy, int pbuf) {
+    const _Float16* As = patch + pbuf * kWBuf + abase + dy * NP * kWRowH;
+    a0[0] = *reinterpret_cast<const f16x8*>(As);
+    a0[1] = *reinterpret_cast<const f16x8*>(As + 32);
+  };
+  auto compute = [&](int dy, int pbuf, const f16x8 (&bv)[TN][2]) {
+    const _Float16* As = patch + pbuf * kWBuf + abase + dy * NP * kWRowH;
+    f16x8 av[TM][2];
+#ifdef DM_WINO_NO_READAHEAD
+    if (dy > 0) read_a0(dy, pbuf);
+#endif
+    av[0][0] = a0[0];
+    av[0][1] = a0[1];
+#pragma unroll
+    for (int i = 1; i < TM; ++i)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) av[i][p] = *reinterpret_cast<const f16x8*>(As + i * 16 * kWRowH + p * 32);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[i][1], bv[j][0], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[i][0], bv[j][1], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[i][0], bv[j][0], acc[i][j], 0, 0, 0);
+      }
+#ifndef DM_WINO_NO_READAHEAD
+      if (i == TM - 2 && dy + 1 < NTAP) read_a0(dy + 1, pbuf);
+#endif
+    }
+  };
+
+  // ---- prologue: B ring and the first chunk's pixels in flight while the GroupNorm tables are built
+  const int nch = a.Cin1 / kWC;
+  const int kt_end = nch * NTAP;
+#pragma unroll
+  for (int d = 0; d < WD; ++d) load_b(bq[d], slice_off(min(d, kt_end - 1)));
+  load_raw(0);
+  if (PRO) {
+    const int C = a.Cin1;
+    if (a.gin_part) {  // gn_finalize (gn.hip) for the tile's image, its expressions (conv_k32's in-kernel finalize)
+      const int G = a.gin_G, cpg = C / G;
+      for (int i = t; i < G; i += 512) {
+        double s1 = 0, s2 = 0;
+#pragma unroll 4
+        for (int k = 0; k < a.gin_nchunk; ++k) {  // (unrolled: the partials' loads in flight together)
+          const double2 v = a.gin_part[((size_t)b0 * a.gin_nchunk + k) * G + i];
+          s1 += v.x;
+          s2 += v.y;
+        }
+        const double mu = s1 / a.gin_n;
+        double var = s2 / a.gin_n - mu * mu;
+        if (var < 0) var = 0;
+        gstat[2 * i] = (float)mu;
+        gstat[2 * i + 1] = (float)(1.0 / sqrt(var + (double)a.gin_eps));
+      }
+      __syncthreads();
+      for (int c = t; c < C; c += 512) {
+        const int si = 2 * (c / cpg);
+        const float mu = gstat[si], rs = gstat[si + 1];
+        float sc = rs * (a.gin_gamma ? a.gin_gamma[c] : 1.0f);
+        float sh = -sc * mu + (a.gin_beta ? a.gin_beta[c] : 0.0f);
+        if (a.gin_ms) {
+          const size_t mo = (size_t)b0 * a.gin_mp + c;
+          const float f = 1.0f + a.gin_ms[mo];
+          sc = sc * f;
+          sh = sh * f + a.gin_mb[mo];
+        }
+        const int ti = 2 * c - (c & 3);  // [c / 4][4 scales][4 shifts], times -log2(e) under SiLU
+        gtab[ti] = PROM == 2 ? sc * -1.4426950408889634f : sc;
+        gtab[ti + 4] = PROM == 2 ? sh * -1.4426950408889634f : sh;
+      }
+    } else {
+      for (int c = t; c < C; c += 512) {
+        const int ti = 2 * c - (c & 3);
+        const float sc = a.pro_scale[(size_t)b0 * C + c], sh = a.pro_shift[(size_t)b0 * C + c];
+        gtab[ti] = PROM == 2 ? sc * -1.4426950408889634f : sc;
+        gtab[ti + 4] = PROM == 2 ? sh * -1.4426950408889634f : sh;
+      }
+    }
+    __syncthreads();
+  }
+  finish(0, 0, 0);
+  finish(0, 0, 1);
+  load_raw(min(1, nch - 1));
+  __syncthreads();
+  W_STAMP(1);
+
+#ifndef DM_WINO_NOPRIO
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+#endif  // the second-dispatched half first (MI355X_MICROARCH.md 2-waves item 4)
+  // ---- main loop: chunk c's three tap rows from buffer c & 1; the next chunk's pixels loaded at tap row 0 and
+  // finished into the other buffer after tap row 2; one barrier per chunk
+  // ping-pong of the two waves of each SIMD (waves w and w + 4): the early group finishes chunk c + 1 before
+  // chunk c's MFMAs, the late group after them, so each wave's loader VALU runs beside its partner's MFMAs
+  // (MI355X_MICROARCH.md, two waves per SIMD); each loads chunk c + 2's pixels right after its finish, a chunk ahead
+  const bool late = wave >= 4;
+  for (int c0 = 0; c0 < nch; c0 += 2) {
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      const int c = c0 + cc;
+      if (c >= nch) continue;  // (not break: keeps the two-chunk body unrolled, bq[slot] statically indexed)
+      const int cn = min(c + 1, nch - 1);  // after the last chunk: refilled into the unused buffer
+#if DM_WINO_ABL != 1 && DM_WINO_ABL != 3
+      if (!late) {
+        finish(cn, (c + 1) & 1, 0);
+        finish(cn, (c + 1) & 1, 1);
+        load_raw(min(c + 2, nch - 1));
+      }
+#endif
+#pragma unroll
+      for (int dy = 0; dy < NTAP; ++dy) {
+        const int kt = c * NTAP + dy;
+        const int slot = (cc * NTAP + dy) % WD;
+        if (dy == 0) {
+          read_a0(0, c & 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        compute(dy, c & 1, bq[slot]);
+#if DM_WINO_ABL != 2 && DM_WINO_ABL != 3  // ablation builds (timing only, wrong results): 1 no finish, 2 no B refills, 3 neither
+        load_b(bq[slot], slice_off(min(kt + WD, kt_end - 1)));
+#endif
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#if DM_WINO_ABL != 1 && DM_WINO_ABL != 3
+      if (late) {
+        finish(cn, (c + 1) & 1, 0);
+        finish(cn, (c + 1) & 1, 1);
+        load_raw(min(c + 2, nch - 1));
+      }
+#endif
+      __syncthreads();
+    }
+  }
+  W_STAMP(2);
+
+  // ---- epilogue: m_nu tiles (row scale undone) to LDS planes [nu][ch][64 pairs][kWEP]
+  float* E = reinterpret_cast<float*>(smem);
+  {
+    float* dst = E + (nu * 2 + ch) * 64 * kWEP;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const float cs = a.wino_rowscale[n0 + ch * 64 + j * 16 + l16] * (PROM == 2 ? -0.6931471805599453f : 1.0f);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dst[(i * 16 + 4 * q + r) * kWEP + j * 16 + l16] = acc[i][j][r] * cs;
+    }
+    float sum = 0.f;  // inf / NaN in any accumulator (an operand past fp16's range) makes the sum non-finite
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sum += acc[i][j][r];
+    if (!__builtin_isfinite(sum) && a.range_flag) *a.range_flag = 1;
+  }
+  __syncthreads();
+  // wave (chunk k, half hf, column half cj): output pixels 64 k + 32 hf .. + 31 of the tile = pairs 32 k + 16 hf ..,
+  // pixel 2 p + s of pair p: y0 = (m0 + m1) + m2, y1 = (m1 - m2) - m3
+  const int kq = wave >> 2, hf = (wave >> 1) & 1, cj = wave & 1;
+  typedef StagedEpilogue<64> Epi;
+  Epi epi(a, M, HW, b0, true, n0 + cj * 64, lane);
+  const int px0 = 64 * kq + 32 * hf;
+  const float* Ec = E + cj * 64 * kWEP + 4 * epi.c4;
+  epi.pairs_f(
+      [&](int i, f4& y0, f4& y1) {
+        const int pp = (px0 >> 1) + i;
+        const f4 mv0 = *reinterpret_cast<const f4*>(Ec + (0 * 2 * 64 + pp) * kWEP);
+        const f4 mv1 = *reinterpret_cast<const f4*>(Ec + (1 * 2 * 64 + pp) * kWEP);
+        const f4 mv2 = *reinterpret_cast<const f4*>(Ec + (2 * 2 * 64 + pp) * kWEP);
+        const f4 mv3 = *reinterpret_cast<const f4*>(Ec + (3 * 2 * 64 + pp) * kWEP);
+        y0 = (mv0 + mv1) + mv2;
+        y1 = (mv1 - mv2) - mv3;
+      },
+      m0 + px0);
+  if (a.gn_part) {  // the 64-pixel chunk's two halves: the hf = 1 wave's quad sums to LDS, added by the hf = 0 wave
+    double s, qq;
+    epi.quad_sums(s, qq);
+    double* xr = gxr + (kq * 2 + cj) * 16 * 2;
+    if (hf == 1 && lane < Epi::LPR) {
+      xr[2 * lane] = s;
+      xr[2 * lane + 1] = qq;
+    }
+    __syncthreads();
+    if (hf == 0) {
+      s += xr[2 * (lane % Epi::LPR)];
+      qq += xr[2 * (lane % Epi::LPR) + 1];
+      epi.store_quads(s, qq, m0 + 64 * kq);
+    }
+  }
+  W_STAMP(3);
+  W_RSTAMP(6);
+}
+
+// U = G g per (nu, output channel, chunk, tap row, channel of the chunk) from the packed 3x3 weights [Cout][K]
+// (K = 9 Cin1 chunk-major, conv_k32's order): [4][Cout][3 Cin1] in the same chunk-major order with 3 taps,
+// float64 sums rounded once to fp32
+__global__ void wino_pack_kernel(const float* w, int Cout, int K, int Cin1, float* out) {
+  const int Kp = 3 * Cin1;
+  const long total = 4L * Cout * Kp;
+  const long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= total) return;
+  const int k = id % Kp;
+  const long r = id / Kp;
+  const int co = r % Cout, nu = r / Cout;
+  const int c = k / (3 * kWC), rem = k - c * 3 * kWC, dy = rem / kWC, ci = rem - dy * kWC;
+  const float* src = w + (size_t)co * K + (size_t)(c * 9 + dy * 3) * kWC + ci;
+  const double g0 = src[0], g1 = src[kWC], g2 = src[2 * kWC];
+  double u;
+  switch (nu) {
+    case 0: u = g0; break;
+    case 1: u = (g0 + g1 + g2) * 0.5; break;
+    case 2: u = (g0 - g1 + g2) * 0.5; break;
+    default: u = g2; break;
+  }
+  out[id] = (float)u;
+}
+
+}  // namespace
+
+#ifdef DM_K32_STAMPS
+extern "C" int dm_debug_wino_stamps(void* host, int nblocks) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wino_stamps), (size_t)nblocks * 8 * sizeof(unsigned long long)) ==
+                 hipSuccess ? 0 : -2;
+}
+#endif
+
+bool conv_wino_shape_ok(const ConvArgs& a) {
+  if (!(a.taps == 9 && a.stride == 1 && a.upsample == 0 && a.ksplit <= 1)) return false;
+  if (a.Hin != a.Hout || a.Win != a.Wout || (a.Wout != 32 && a.Wout != 16) || (a.Hout * a.Wout) % 128 != 0) return false;
+  if (a.Cin1 < kWC || a.Cin1 % kWC != 0 || 2 * a.Cin1 > kWTab || a.Cin2 != 0 || a.K != 9 * a.Cin1) return false;
+  if (a.Cout % 128 != 0) return false;
+  if (a.gin_part && (a.gin_G <= 0 || a.gin_G > kWMaxG || a.Cin1 % a.gin_G != 0)) return false;
+  return staged_epilogue_ok(a);
+}
+
+bool conv_wino_ok(const ConvArgs& a) { return a.wino_ws && a.wino_rowscale && conv_wino_shape_ok(a); }
+
+size_t wino_weights_bytes(int Cout, int Cin1) { return split_conv_weights_bytes(4, Cout, 3 * Cin1, 2); }
+
+const float* wino_rowscale(const void* ws, int Cout, int Cin1) { return split_conv_rowscale(ws, 4, Cout, 3 * Cin1); }
+
+int wino_weights(const float* w, int Cout, int Cin1, void* out, hipStream_t st) {
+  DM_REQUIRE(w && out && Cout > 0 && Cin1 > 0 && Cin1 % kWC == 0, "winograd weights: Cin must be a multiple of 32");
+  const long n = 4L * Cout * 3 * Cin1;
+  float* tmp = nullptr;  // plan-build time only: synchronous
+  DM_CHECK_HIP(hipMalloc(reinterpret_cast<void**>(&tmp), n * sizeof(float)));
+  hipLaunchKernelGGL(wino_pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, w, Cout, 9 * Cin1, Cin1, tmp);
+  int rc = hipGetLastError() == hipSuccess ? DM_OK : DM_ERR_HIP;
+  if (rc == DM_OK) rc = split_conv_weights(tmp, 4, Cout, 3 * Cin1, Cin1, 3, 2, out, st);
+  if (hipStreamSynchronize(st) != hipSuccess && rc == DM_OK) rc = DM_ERR_HIP;
+  (void)hipFree(tmp);
+  if (rc == DM_ERR_HIP) set_error("winograd weights: kernel launch failed");
+  return rc;
+}
+
+std::string conv_wino_label(const ConvArgs& a) {
+  const int prom = (a.pro_scale || a.gin_part) ? (a.pro_nosilu ? 1 : 2) : 0;
+  return std::string("conv_wino_kernel<") + std::to_string(a.Wout) + "," + std::to_string(prom) + ">";
+}
+
+int conv2d_wino(const ConvArgs& a, hipStream_t st) {
+  DM_REQUIRE(conv_wino_ok(a), "conv: shape not supported by the Winograd F(2,3) kernel");
+  const int blocks = (a.B * a.Hout * a.Wout / 128) * (a.Cout / 128);
+  const int prom = (a.pro_scale || a.gin_part) ? (a.pro_nosilu ? 1 : 2) : 0;
+#define DM_WINO_LAUNCH(W_, P_)                                                                \
+  if (a.Wout == W_ && prom == P_) {                                                           \
+    hipLaunchKernelGGL((conv_wino_kernel<W_, P_>), dim3(blocks), dim3(512), 0, st, a);         \
+    note_launch("conv_wino_kernel<" #W_ "," #P_ ">");                                         \
+  }
+  DM_WINO_LAUNCH(32, 0) DM_WINO_LAUNCH(32, 1) DM_WINO_LAUNCH(32, 2)
+  DM_WINO_LAUNCH(16, 0) DM_WINO_LAUNCH(16, 1) DM_WINO_LAUNCH(16, 2)
+#undef DM_WINO_LAUNCH
+  DM_LAUNCH_CHECK();
+  return DM_OK;
+}
+
+}  // namespace dm

@@ -191,6 +191,7 @@ static int dit_create(const dm_dit_arch* arch, const float* const* params, const
 }
 
 int DiTModel::build_plan(Plan& pl, int B) {
+  refresh_toggles();
   pl.B = B;
   pl.math = math;
   const dm_dit_arch& a = arch;

@@ -9,6 +9,19 @@ namespace dm {
 
 constexpr int kGnPixPerChunk = 64;
 
+// Plan toggles: the environment, read ONCE per plan build (refresh_toggles(): the UNet / DiT plan builders and the
+// direct-launch ABI entry points call it), so every decision of one plan -- and the label each op is profiled
+// under -- comes from one snapshot. Each keeps the path it replaces as a test oracle / A/B arm.
+struct Toggles {
+  bool wino = true;      // DM_CONV_WINO=0: the 3x3 convs of 32^2 / 16^2 maps on conv_k32 instead of conv_wino
+  bool k32s_w4 = false;  // DM_K32S_W4=1: the small-map conv's 4-wave form (conv_k32 variant 12)
+};
+const Toggles& toggles();
+void refresh_toggles();
+// Launch log for tests (dm_debug_launch_log): the kernel instantiations the conv launchers issued, recorded in the
+// branch that launches them
+void note_launch(const char* name);
+
 // Nominal batch of the plans' tile heuristics (ConvArgs::pick_B, GemmArgs::pick_M / pick_Z): every layer
 // runs the kernel it would at B = kPickBatch, whatever B is, so each image's result is bit-identical at
 // any batch size (the reference parity pinned at B = 1..2 holds at the benchmark's B).
@@ -83,6 +96,13 @@ struct ConvArgs {
   int ap_L, ap_heads, ap_Dh, ap_legacy;
   float ap_alpha, ap_bscale;
   int ap_ea, ap_eb, ap_ev;
+  // optional Winograd F(2,3) weights (conv_wino.hip, wino_weights): U = G g of the 3x3 taps, fp16x2 fragment
+  // images of 4 matrices [Cout][3 Cin1] with their inverse row scales; set, the conv runs conv_wino_kernel
+  const void* wino_ws;
+  const float* wino_rowscale;
+  // the K32 variant the plan resolved at build time (conv_k32_pick + 1; 0: pick at launch), so the launch and the
+  // op's profile label come from one decision
+  int k32_resolved;
 };
 
 // Patch-pixel capacity of the halo-patch kernels' LDS images (fp32 / split-bf16; 128- / 64-row tiles)
@@ -266,6 +286,16 @@ int conv_k32_pick(const ConvArgs& a);
 bool conv_k32_enabled();  // DM_CONV_K32 != 0
 int conv2d_k32(const ConvArgs& a, int v, hipStream_t st);
 std::string conv_k32_label(const ConvArgs& a, int v);
+// Winograd F(2,3)-along-x 3x3 convs (conv_wino.hip): the shapes the kernel takes (32- / 16-wide maps, 128-pixel
+// tiles, Cout % 128 == 0, no second K segment), whether a conv has its weights and shape, the weights (U = G g,
+// float64, then the fp16x2 split of split_conv_weights with nmat 4, ntap 3), their size / row scales, launcher
+bool conv_wino_shape_ok(const ConvArgs& a);
+bool conv_wino_ok(const ConvArgs& a);
+size_t wino_weights_bytes(int Cout, int Cin1);
+const float* wino_rowscale(const void* ws, int Cout, int Cin1);
+int wino_weights(const float* w, int Cout, int Cin1, void* out, hipStream_t st);
+std::string conv_wino_label(const ConvArgs& a);
+int conv2d_wino(const ConvArgs& a, hipStream_t st);
 // static-weight GEMM on pre-split weights with K = 32 MFMA steps (linear_k32.hip)
 bool linear_k32_ok(const GemmArgs& g);
 int linear_k32(const GemmArgs& g, hipStream_t st);

@@ -185,6 +185,7 @@ struct UNetModel {
   bool range_deferred = false;
   long range_fallbacks = 0;   // forwards / loops re-run in bf16x3 (dm_unet_range_stats)
   std::map<std::pair<const float*, int>, void*> split_w;
+  std::map<const float*, void*> wino_w;  // Winograd F(2,3) weights of the convs conv_wino_kernel takes
   size_t split_bytes = 0;
   void split_for(ConvArgs& c);
   // folded single-head attention blocks (attn_block.hip): per block's qkv weights, the fp32 products At, w,
@@ -216,6 +217,7 @@ UNetModel::~UNetModel() {
   for (void* q : fold_mem) (void)hipFree(q);
   if (last_packed) (void)hipFree(last_packed);
   for (auto& kv : split_w) (void)hipFree(kv.second);
+  for (auto& kv : wino_w) (void)hipFree(kv.second);
   if (range_flag) (void)hipFree(range_flag);
   if (range_flag_host) (void)hipHostFree(range_flag_host);
   if (arena) (void)hipFree(arena);
@@ -255,6 +257,29 @@ void UNetModel::split_for(ConvArgs& c) {
     c.ws_rowscale = split_conv_rowscale(p, nmat, c.Cout, c.K);
     c.range_flag = range_flag;
   }
+  // the Winograd F(2,3) kernel for the 3x3 convs it takes (DM_CONV_WINO=0: conv_k32, its test oracle)
+  c.wino_ws = nullptr;
+  c.wino_rowscale = nullptr;
+  if (conv_math != 2 || !toggles().wino || !conv_wino_shape_ok(c)) return;
+  auto iw = wino_w.find(c.w);
+  void* wp = nullptr;
+  if (iw != wino_w.end()) {
+    wp = iw->second;
+  } else {
+    const size_t nb = wino_weights_bytes(c.Cout, c.Cin1);
+    if (hipMalloc(&wp, nb) != hipSuccess) {
+      (void)hipGetLastError();
+      return;
+    }
+    if (wino_weights(c.w, c.Cout, c.Cin1, wp, nullptr) != DM_OK) {
+      (void)hipFree(wp);
+      return;
+    }
+    wino_w[c.w] = wp;
+    split_bytes += nb;
+  }
+  c.wino_ws = wp;
+  c.wino_rowscale = wino_rowscale(wp, c.Cout, c.Cin1);
 }
 
 // The folded weights of a single-head attention block (attn_fold, float64 products of the block's own
@@ -655,6 +680,7 @@ static int unet_create(const dm_unet_arch* arch, const float* const* params, con
 // plan (per batch size / resolution)
 // ---------------------------------------------------------------------------
 int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
+  refresh_toggles();
   pl.B = B;
   pl.math = conv_math;
   pl.H = H;
@@ -771,6 +797,7 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
   auto add_conv = [&](ConvArgs c) {
     maybe_split(c);
     split_for(c);
+    c.k32_resolved = 1 + conv_k32_pick(c);  // one decision for the launch and the label
     double fl, by;
     conv_cost(c, fl, by);
     if (plan_debug)

@@ -94,7 +94,7 @@ class ConvDesc(ctypes.Structure):
         ('tile', ctypes.c_int),
         ('pro_scale', vp), ('pro_shift', vp),
         ('w_split', vp), ('w_split_kind', ctypes.c_int), ('range_flag', vp), ('pro_nosilu', ctypes.c_int),
-        ('ksplit', ctypes.c_int), ('kpart', vp),
+        ('ksplit', ctypes.c_int), ('kpart', vp), ('w_wino', vp),
     ]
 
 
@@ -240,6 +240,11 @@ def _declare(L: ctypes.CDLL):
                                       vp]
     L.dm_conv2d_nhwc.argtypes = [ctypes.POINTER(ConvDesc), vp]
     L.dm_pack_conv_weight_subpixel.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp]
+    L.dm_debug_launch_log.argtypes = [ctypes.c_int]
+    L.dm_debug_launch_log_read.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    L.dm_conv_weight_wino_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
+    L.dm_conv_weight_wino_bytes.restype = ctypes.c_int64
+    L.dm_pack_conv_weight_wino.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp]
     L.dm_conv_weight_split_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
     L.dm_conv_weight_split_bytes.restype = ctypes.c_int64
     L.dm_pack_conv_weight_split.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -410,6 +415,19 @@ def pack_conv_weight_split(wp: torch.Tensor, nmat: int, Cin: int, taps: int, kin
     return out
 
 
+def pack_conv_weight_wino(wp: torch.Tensor, Cin: int) -> torch.Tensor:
+    """Packed fp32 3x3 conv weights [Cout, 9 Cin] -> the Winograd F(2,3) weight images (a uint8 device tensor)
+    for ConvDesc.w_wino (used with ConvDesc.w_split of kind SPLIT_FP16X2)."""
+    Cout, K = wp.shape
+    nbytes = load().dm_conv_weight_wino_bytes(Cout, Cin)
+    if nbytes <= 0 or K != 9 * Cin:
+        raise ValueError('Winograd packing needs [Cout, 9 Cin] weights with Cin a multiple of 32')
+    out = torch.empty(nbytes, dtype=torch.uint8, device=wp.device)
+    check(load().dm_pack_conv_weight_wino(wp.data_ptr(), Cout, Cin, out.data_ptr(), stream_handle(wp.device)),
+          'dm_pack_conv_weight_wino')
+    return out
+
+
 def dit_math(handle, kind: Optional[str] = None) -> str:
     """Set (kind given) and return the GEMM arithmetic of a native DiT handle: 'fp16x2' (default) or
     'fp32' (dm_dit_set_math / dm_dit_get_math)."""
@@ -476,6 +494,21 @@ def unet_profile_read(handle, abi: str = 'dm_unet'):
         out.append(dict(label=buf.value.decode(), flops=fl.value, bytes=by.value, ms_total=ms.value,
                         launches=nl.value))
     return out
+
+
+def launch_log(enable: bool) -> None:
+    """Start (clearing it) or stop the library's launch log: the kernel instantiations its conv launchers issue
+    (dm_debug_launch_log; a hipGraph plan launches at capture, i.e. on the forward that builds the plan)."""
+    check(load().dm_debug_launch_log(1 if enable else 0), 'dm_debug_launch_log')
+
+
+def launch_log_read() -> list:
+    """The kernel instantiations logged since launch_log(True), in launch order."""
+    buf = ctypes.create_string_buffer(1 << 20)
+    n = load().dm_debug_launch_log_read(buf, len(buf))
+    if n < 0:
+        raise RuntimeError('dm_debug_launch_log_read failed')
+    return [ln for ln in buf.value.decode().split('\n') if ln]
 
 
 def range_stats(handle, abi: str = 'dm_unet'):

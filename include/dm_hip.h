@@ -289,6 +289,17 @@ int64_t dm_conv_weight_split_bytes(int nmat, int Cout, int K, int kind);
 int dm_pack_conv_weight_split(const float* w, int nmat, int Cout, int K, int Cin, int taps, int kind, void* out,
                               void* stream);
 
+/* Winograd F(2,3)-along-x weights of a packed 3x3 conv (dm_pack_conv_weight, K = 9 Cin, Cin % 32 == 0):
+ * U = G g per tap row (float64, one rounding), split to fp16x2 fragment images of 4 matrices [Cout][3 Cin]
+ * with per-output-channel power-of-two scales: dm_conv_weight_wino_bytes(Cout, Cin) bytes at `out`. */
+int64_t dm_conv_weight_wino_bytes(int Cout, int Cin);
+/* Test hook: the conv launchers record the kernel instantiation they issue while the log is on.
+ * dm_debug_launch_log(1) clears and starts it, (0) stops it; _read copies it (newline-separated, NUL-terminated)
+ * into buf and returns its length. */
+int dm_debug_launch_log(int enable);
+int dm_debug_launch_log_read(char* buf, int len);
+int dm_pack_conv_weight_wino(const float* w, int Cout, int Cin, void* out, void* stream);
+
 typedef struct dm_conv_desc {
   const float* x;  int x_pitch, Cin, Hin, Win;
   int taps, stride;
@@ -317,6 +328,10 @@ typedef struct dm_conv_desc {
    * ranges go to kpart ([ksplit][B * Hout * Wout][Cout] floats), then one reduction applies the epilogue */
   int ksplit;
   float* kpart;
+  /* optional Winograd F(2,3) weights of a 3x3 stride-1 conv from dm_pack_conv_weight_wino (needs w_split of kind
+   * DM_SPLIT_FP16X2 too): 32- / 16-pixel-wide maps with Cout % 128 == 0 then run the Winograd kernel (tile 0 or
+   * 21; 21 fails on any other shape) */
+  const void* w_wino;
 } dm_conv_desc;
 /* 1x1 convs (taps 1, K = Cin, Cin % 32 == 0) with DM_SPLIT_FP16X2 weights run on the split kernel
  * with the same prologue / epilogue options: the static-weight GEMMs of the attention blocks. */

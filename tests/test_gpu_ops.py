@@ -127,7 +127,7 @@ def _pack(w, cuda, K=None, col0=0, out=None):
 
 def _run_conv(cuda, x_nhwc, w_packed, Cout, Hout, Wout, taps, stride=1, upsample=0, bias=None, rowvec=None,
               res=None, x2=None, Cin2=0, y_pitch=None, x_pitch=None, tile=0, pro=None, split=False,
-              range_flag=None, pro_nosilu=0, ksplit=0):
+              range_flag=None, pro_nosilu=0, ksplit=0, wino=False):
     B, Hin, Win, Cin = x_nhwc.shape[0], x_nhwc.shape[1], x_nhwc.shape[2], x_nhwc.shape[3]
     x_pitch = x_pitch or Cin
     y_pitch = y_pitch or Cout
@@ -154,10 +154,15 @@ def _run_conv(cuda, x_nhwc, w_packed, Cout, Hout, Wout, taps, stride=1, upsample
         d.w_split, d.w_split_kind = ws.data_ptr(), kind
         if range_flag is not None:
             d.range_flag = range_flag.data_ptr()
+    if wino:  # Winograd F(2,3) weights (conv_wino.hip; with fp16x2 split weights)
+        ww = dmhip.pack_conv_weight_wino(w_packed[:, :9 * Cin].contiguous(), Cin)
+        d.w_wino = ww.data_ptr()
     if ksplit > 1:  # split-K partial sums [ksplit][B * Hout * Wout][Cout]
         kpart = torch.empty((ksplit, B * Hout * Wout, Cout), device=cuda)
         d.ksplit, d.kpart = ksplit, kpart.data_ptr()
     dmhip.conv2d_nhwc(d, cuda)
+    if wino:
+        torch.cuda.synchronize(cuda)  # ww is freed on return
     return y
 
 

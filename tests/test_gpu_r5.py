@@ -1,0 +1,148 @@
+"""Round-5 GPU tests.
+
+* the Winograd F(2,3)-along-x 3x3 conv (conv_wino.hip; models/unet.py:13-27, the ResBlock convs): integer operands
+  bit for bit against float64 (transforms, padding, tap rows, epilogue), random operands at fp32-class accuracy,
+  the range flag; whole CIFAR / CFG-CIFAR / ADM forwards against the direct conv (DM_CONV_WINO=0) and the
+  reference fixtures, with the launch log showing which kernels ran;
+* the plan-resolved small-map variants: the 4- and 8-wave forms (conv_k32s_kernel) are both launched (launch log)
+  and give the same bits.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+import dmhip
+from tests.test_gpu_conv_split import _rand_case
+from tests.test_gpu_ops import _ints, _nhwc, _pack, _run_conv
+from tests.test_gpu_parity import TOL, _model
+
+pytestmark = pytest.mark.gpu
+
+WINO = 21  # ConvDesc.tile: force the Winograd kernel
+
+
+@pytest.mark.parametrize('B,Cin,Cout,H', [(1, 128, 128, 32), (2, 32, 128, 32), (3, 64, 256, 16), (2, 256, 128, 16),
+                                          (1, 96, 384, 32), (5, 160, 128, 16)])
+def test_wino_conv3x3_exact(cuda, B, Cin, Cout, H):
+    """Integer operands: V = B^T d, U = G g (half-integers), their fp16 pieces and the fp32 sums are exact, so the
+    Winograd conv equals the float64 conv bit for bit (zero padding at every map edge, all tap rows)."""
+    x = _ints((B, Cin, H, H), -2, 3, seed=50)
+    w = _ints((Cout, Cin, 3, 3), -2, 3, seed=51)
+    b = _ints((Cout, ), seed=52)
+    ref = F.conv2d(x.double(), w.double(), b.double(), padding=1).float()
+    dmhip.launch_log(True)
+    y = _run_conv(cuda, _nhwc(x).to(cuda), _pack(w, cuda), Cout, H, H, 9, 1, 0, b.to(cuda), tile=WINO,
+                  split='fp16x2', wino=True)
+    log = dmhip.launch_log_read()
+    dmhip.launch_log(False)
+    assert log == [f'conv_wino_kernel<{H},0>'], log
+    assert torch.equal(y.cpu(), _nhwc(ref))
+
+
+@pytest.mark.parametrize('H', [32, 16])
+def test_wino_rowvec_residual_pitch(cuda, H):
+    """temb row vector, residual, pitched input and output (untouched beyond Cout), integer-exact."""
+    B, Cin, Cout = 3, 64, 128
+    x = _ints((B, Cin, H, H), seed=60)
+    w = _ints((Cout, Cin, 3, 3), -2, 3, seed=61)
+    b = _ints((Cout, ), seed=62)
+    rv = _ints((B, Cout), seed=63)
+    res = _ints((B, Cout, H, H), seed=64)
+    ref = (F.conv2d(x.double(), w.double(), b.double(), padding=1) + rv.double()[:, :, None, None]
+           + res.double()).float()
+    xp = torch.full((B, H, H, 96), float('nan'), device=cuda)
+    xp[..., :Cin] = _nhwc(x).to(cuda)
+    y = _run_conv(cuda, xp[..., :Cin], _pack(w, cuda), Cout, H, H, 9, bias=b.to(cuda), rowvec=rv.to(cuda),
+                  res=_nhwc(res).to(cuda), y_pitch=160, x_pitch=96, tile=WINO, split='fp16x2', wino=True)
+    assert torch.equal(y[..., :Cout].cpu(), _nhwc(ref))
+    assert torch.isnan(y[..., Cout:]).all()
+
+
+@pytest.mark.parametrize('B,Cin,Cout,H', [(4, 128, 128, 32), (8, 256, 256, 16), (2, 384, 128, 32), (4, 512, 256, 16)])
+def test_wino_fp32_accuracy(cuda, report, B, Cin, Cout, H):
+    """Fused GroupNorm + SiLU conv on random data: the Winograd kernel's error vs float64 stays at the fp32 level
+    (within 3x the fp32 MFMA kernel's; the direct fp16x2 kernel's is within 2x)."""
+    xd, wp, b, pro, ref = _rand_case(cuda, B, Cin, Cout, H, 0, seed=91)
+    errs, rms = {}, {}
+    for name, split, tile, wino in (('fp32', False, 0, False), ('k32', 'fp16x2', 10, False),
+                                    ('wino', 'fp16x2', WINO, True)):
+        y = _run_conv(cuda, xd, wp, Cout, H, H, 9, 1, 0, b.to(cuda), pro=pro, split=split, tile=tile, wino=wino)
+        d = y.cpu().double() - _nhwc(ref)
+        errs[name] = d.abs().max().item()
+        rms[name] = d.pow(2).mean().sqrt().item()
+    scale = ref.abs().max().item()
+    for k in errs:
+        report(f'wino_accuracy_{B}_{Cin}_{Cout}_{H}_{k}_max_rel', errs[k] / scale)
+        report(f'wino_accuracy_{B}_{Cin}_{Cout}_{H}_{k}_rms_rel', rms[k] / scale)
+    assert errs['wino'] < 3.0 * errs['fp32'] + 1e-7 * scale, errs
+    assert rms['wino'] < 3.0 * rms['fp32'], rms
+    assert errs['wino'] < 6e-6 * scale, (errs, scale)
+
+
+def test_wino_range_flag(cuda):
+    """A transformed activation beyond 65504 (no fp16 image) raises the range flag; in range it stays clear."""
+    B, C, H = 2, 64, 16
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn((B, C, H, H), generator=g)
+    w = torch.randn((128, C, 3, 3), generator=g) * 0.05
+    for big, expect in ((1.0, 0), (1e5, 1)):
+        flag = torch.zeros(1, dtype=torch.int32, device=cuda)
+        _run_conv(cuda, _nhwc(x * big).to(cuda), _pack(w, cuda), 128, H, H, 9, tile=WINO, split='fp16x2',
+                  wino=True, range_flag=flag)
+        assert int(flag.item()) == expect
+
+
+def _forward_logged(meta, name, cuda, x, t, y=None):
+    dmhip.launch_log(True)
+    model, _ = _model(meta, name, cuda)
+    out = model(x, t) if y is None else model(x, t, y)
+    log = dmhip.launch_log_read()
+    dmhip.launch_log(False)
+    return model, out, log
+
+
+@pytest.mark.parametrize('B', [2, 5])
+def test_wino_cifar_forward(cuda, golden, monkeypatch, report, B):
+    """The CIFAR-10 UNet with its 32^2 / 16^2 ResBlock convs (no shortcut segment) on the Winograd kernel: within
+    1e-5 of the direct-conv forward (DM_CONV_WINO=0) and within TOL of the reference fixture; the launch log holds
+    the Winograd launches and the direct forward none."""
+    g, meta = golden('forward')
+    xg = torch.Generator().manual_seed(41)
+    x = torch.randn((B, 3, 32, 32), generator=xg).to(cuda)
+    t = torch.randint(0, 1000, (B, ), generator=xg).to(cuda)
+    _, out_w, log_w = _forward_logged(meta, 'cifar10', cuda, x, t)
+    monkeypatch.setenv('DM_CONV_WINO', '0')
+    _, out_d, log_d = _forward_logged(meta, 'cifar10', cuda, x, t)
+    n32 = log_w.count('conv_wino_kernel<32,2>')
+    n16 = log_w.count('conv_wino_kernel<16,2>')
+    assert n32 >= 4 and n16 >= 4, log_w
+    assert not any(s.startswith('conv_wino') for s in log_d), log_d
+    err = (out_w - out_d).abs().max().item()
+    report(f'wino_cifar_forward_B{B}_vs_direct', err)
+    assert err <= 1e-5, err
+    monkeypatch.delenv('DM_CONV_WINO')
+    model, _ = _model(meta, 'cifar10', cuda)
+    xr = torch.from_numpy(g['cifar10_x']).to(cuda)
+    tr = torch.from_numpy(g['cifar10_t']).to(cuda)
+    err_ref = (model(xr, tr).cpu() - torch.from_numpy(g['cifar10_y'])).abs().max().item()
+    report('wino_cifar_vs_reference', err_ref)
+    assert err_ref <= TOL, err_ref
+
+
+def test_small_map_variants_both_launched_bit_identical(cuda, golden, monkeypatch):
+    """The 4x4-level convs: DM_K32S_W4=1 resolves the 4-wave conv_k32s_kernel at plan build (variant 12) and the
+    default the 8-wave one (variant 6) -- the launch log proves each ran -- with the same bits."""
+    _, meta = golden('forward')
+    xg = torch.Generator().manual_seed(33)
+    x = torch.randn((5, 3, 32, 32), generator=xg).to(cuda)
+    t = torch.randint(0, 1000, (5, ), generator=xg).to(cuda)
+    outs, logs = {}, {}
+    for w4 in ('0', '1'):
+        monkeypatch.setenv('DM_K32S_W4', w4)
+        _, outs[w4], logs[w4] = _forward_logged(meta, 'cifar10', cuda, x, t)
+    k8 = [s for s in logs['0'] if s.startswith('conv_k32s_kernel<')]
+    k4 = [s for s in logs['1'] if s.startswith('conv_k32s_kernel<')]
+    assert k8 and all(s.endswith(',8>') for s in k8), logs['0']
+    assert k4 and all(s.endswith(',4>') for s in k4), logs['1']
+    assert len(k4) == len(k8)
+    assert torch.equal(outs['0'], outs['1'])

@@ -76,6 +76,9 @@ def run(name, iters, split, tile=0, ksplit=0):
         kind = dmhip.SPLIT_FP16X2 if split == 'fp16x2' else dmhip.SPLIT_BF16X3
         ws = dmhip.pack_conv_weight_split(wp, 4 if up == 2 else 1, Cin, 4 if up == 2 else taps, kind)
         d.w_split, d.w_split_kind = ws.data_ptr(), kind
+    if tile == 21:  # the Winograd F(2,3) kernel (conv_wino.hip)
+        ww = dmhip.pack_conv_weight_wino(wp, Cin)
+        d.w_wino = ww.data_ptr()
     if ksplit > 1:
         kpart = torch.empty((ksplit, B * Ho * Ho, Cout), device=dev)
         d.ksplit, d.kpart = ksplit, kpart.data_ptr()

@@ -1,0 +1,49 @@
+"""Phase timing of conv_wino_kernel from a diagnostic build (-DDM_K32_STAMPS): per block, wave 0's s_memtime at the
+start, after the prologue, after the main loop and at the end, plus s_memrealtime start / end.
+
+    make -C diffusion-models-pytorch_amd/csrc OUT=../../tools/bin/libdm_stamps.so BUILD=build_stamps \
+        EXTRA=-DDM_K32_STAMPS
+    DM_HIP_LIB=tools/bin/libdm_stamps.so python tools/wino_stamps.py --shape res32_128
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import conv_bench  # noqa: E402
+
+import dmhip  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--shape', default='res32_128')
+    args = ap.parse_args()
+    dmhip.load()
+    conv_bench.run(args.shape, 5, 'fp16x2', 21)
+    B, Cin, Cout, H, pro, up = conv_bench.SHAPES[args.shape]
+    nblk = (B * H * H // 128) * (Cout // 128)
+    buf = np.zeros((nblk, 8), dtype=np.uint64)
+    L = dmhip.load()
+    L.dm_debug_wino_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    assert L.dm_debug_wino_stamps(buf.ctypes.data, nblk) == 0
+    s = buf.astype(np.int64)
+    phases = (('prologue', s[:, 1] - s[:, 0]), ('main loop', s[:, 2] - s[:, 1]), ('epilogue', s[:, 3] - s[:, 2]))
+    tot = s[:, 3] - s[:, 0]
+    rt0, rt1 = s[:, 5], s[:, 6]
+    wall_us = (rt1.max() - rt0.min()) / 100.0
+    clk = tot / np.maximum(rt1 - rt0, 1) * 100e6 / 1e9
+    print(f'{args.shape} wino: {nblk} blocks, Cin {Cin} ({Cin // 32} chunks), kernel wall (stamps) {wall_us:.1f} us')
+    for name, v in phases + (('block total', tot), ):
+        print(f'  {name:12s} cycles mean {v.mean():10.0f}  p10 {np.percentile(v, 10):10.0f}  '
+              f'p90 {np.percentile(v, 90):10.0f}  share {v.mean() / tot.mean():.3f}')
+    print(f'  main loop cycles per chunk {(s[:, 2] - s[:, 1]).mean() / (Cin // 32):.0f} '
+          f'(MFMA floor 4608 per SIMD: 2 waves x 144 x 16)')
+    print(f'  block wall us mean {((rt1 - rt0) / 100.0).mean():.2f}, clock GHz mean {clk.mean():.3f}')
+
+
+if __name__ == '__main__':
+    main()
