@@ -364,8 +364,33 @@ def launch_ranks(n):
         env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')   # RCCL over dmabuf IPC on this pool
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
                                       stdout=subprocess.PIPE if r == 0 else None, text=True))
-    out0 = procs[0].communicate()[0]
-    codes = [procs[0].returncode] + [p.wait() for p in procs[1:]]
+    # poll every rank: the first non-zero exit ends the others (a dead rank would leave rank 0 blocked in a
+    # collective forever -- ADVICE r4); rank 0's stdout is drained by a thread meanwhile
+    import threading
+    import time
+    out_buf = []
+    reader = threading.Thread(target=lambda: out_buf.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    codes = [None] * n
+    while any(c is None for c in codes):
+        for r, p in enumerate(procs):
+            if codes[r] is None:
+                codes[r] = p.poll()
+        if any(c not in (None, 0) for c in codes):
+            for r, p in enumerate(procs):
+                if codes[r] is None:
+                    p.terminate()
+            for r, p in enumerate(procs):
+                if codes[r] is None:
+                    try:
+                        codes[r] = p.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        codes[r] = p.wait()
+            break
+        time.sleep(0.2)
+    reader.join(timeout=30)
+    out0 = out_buf[0] if out_buf else ''
     if out0:
         sys.stdout.write(out0)
         sys.stdout.flush()
@@ -435,12 +460,30 @@ def main():
         gather_path = 'torch.distributed' if backend == 'nccl' else f'{backend} (host)'
     if world > 1 and backend == 'nccl' and os.environ.get('DM_GATHER') != 'torch':
         from dmhip.comm import Comm   # the C-ABI RCCL all-gather (dm_allgather_f32), bootstrapped over the group
-        try:
-            comm = Comm.from_process_group()
-            gather_path = 'dm_allgather_f32 (RCCL, C ABI)'
-        except Exception as e:   # reported in the JSON line; the fold's gather then runs on torch.distributed
-            print(f'bench.py: rank {rank}: dm_comm_init failed ({e}); gathering with torch.distributed', file=sys.stderr)
-            gather_path = f'torch.distributed (dm_comm_init failed: {str(e)[:120]})'
+        # every rank gets the communicator or every rank gathers with torch.distributed
+        comm = Comm.try_from_process_group()
+        if comm is None:
+            print(f'bench.py: rank {rank}: dm_comm could not be set up on every rank; gathering with torch.distributed',
+                  file=sys.stderr)
+            gather_path = 'torch.distributed (dm_comm unavailable on some rank)'
+        else:
+            # before the timed region: the C-ABI gather of a rank-tagged fold against all_gather_into_tensor, agreed
+            # over the ranks; on any difference every rank drops to torch.distributed
+            n_el = 1
+            for d_ in shape[1:]:
+                n_el *= int(d_)
+            probe = torch.arange(B * n_el, dtype=torch.float32, device=dev).view(B, *shape[1:]) + rank
+            got, ref = torch.empty_like(gathered), torch.empty_like(gathered)
+            comm.allgather(probe, got)
+            dist.all_gather_into_tensor(ref, probe)
+            same = torch.tensor([1 if torch.equal(got, ref) else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(same, op=dist.ReduceOp.MIN)
+            if int(same.item()):
+                gather_path = 'dm_allgather_f32 (RCCL, C ABI; equal to all_gather_into_tensor at start)'
+            else:
+                comm.close()
+                comm = None
+                gather_path = 'torch.distributed (dm_allgather_f32 differed from all_gather_into_tensor)'
 
     def fold():
         x = wl['fold']()

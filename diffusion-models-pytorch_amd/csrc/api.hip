@@ -168,18 +168,19 @@ extern "C" int dm_conv2d_nhwc(const dm_conv_desc* d, void* stream) {
       return DM_ERR_ARG;
     }
     a.wino_ws = d->w_wino;
-    a.wino_rowscale = dm::wino_rowscale(d->w_wino, a.Cout, a.Cin1);
+    a.wino_rowscale = dm::wino_rowscale(d->w_wino, a.Cout, a.Cin1, a.Cin2);
+    a.wino_fold = d->w_wino_fold;
   }
   return dm::conv2d_igemm(a, (hipStream_t)stream);
 }
 
-extern "C" int64_t dm_conv_weight_wino_bytes(int Cout, int Cin) {
-  if (Cout <= 0 || Cin <= 0 || Cin % 32 != 0) return -1;
-  return (int64_t)dm::wino_weights_bytes(Cout, Cin);
+extern "C" int64_t dm_conv_weight_wino_bytes(int Cout, int Cin, int Cin2) {
+  if (Cout <= 0 || Cin <= 0 || Cin % 32 != 0 || Cin2 < 0 || Cin2 % 64 != 0) return -1;
+  return (int64_t)dm::wino_weights_bytes(Cout, Cin, Cin2);
 }
 
-extern "C" int dm_pack_conv_weight_wino(const float* w, int Cout, int Cin, void* out, void* stream) {
-  return dm::wino_weights(w, Cout, Cin, out, (hipStream_t)stream);
+extern "C" int dm_pack_conv_weight_wino(const float* w, int Cout, int Cin, int Cin2, int fold, void* out, void* stream) {
+  return dm::wino_weights(w, Cout, Cin, Cin2, fold, out, (hipStream_t)stream);
 }
 
 extern "C" int64_t dm_conv_weight_split_bytes(int nmat, int Cout, int K, int kind) {

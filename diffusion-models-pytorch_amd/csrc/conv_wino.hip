@@ -11,8 +11,9 @@
 // row scale per output channel over all four matrices); V is formed in fp32 from the GroupNorm + SiLU'd patch
 // (one rounding) and split in the loader; the output transform is fp32 in the epilogue.
 //
-// Block: 512 threads, a 128-pixel tile (TH = 128 / W whole rows of a W = 32 or 16 wide map: 64 pairs) x 128
-// output channels. Wave w = (nu = w >> 1, ch = w & 1) computes GEMM nu for the 64 pairs x 64 channels of column
+// Block: 512 threads, persistent over the 128-pixel tiles (TH = 128 / W whole rows of a W = 32 or 16 wide map: 64
+// pairs) x 128 output channels of one image (its GroupNorm tables built once; the next tile's first pixels loaded
+// during the epilogue). Wave w = (nu = w >> 1, ch = w & 1) computes GEMM nu for the 64 pairs x 64 channels of column
 // half ch: 4 x 4 tiles of v_mfma_f32_16x16x32_f16, three per product (a1 w0 + a0 w1 + a0 w0), 48 MFMAs per
 // K step as conv_k32's 64 x 64 wave tiles -- so the operand traffic per MFMA is conv_k32's, and the 8 waves
 // (two per SIMD) keep the same occupancy in one block per CU.
@@ -47,14 +48,14 @@ constexpr int kWNR = 96;                       // pair rows per nu plane at most
 constexpr int kWBuf = 4 * kWNR * kWRowH;       // fp16 per patch buffer (61440 B)
 constexpr int kWTab = 4096;                    // GroupNorm table floats: one image, Cin <= 2048 (scales, shifts)
 constexpr int kWEP = 68;                       // epilogue plane pitch (floats)
-constexpr int kWSmem = 2 * kWBuf * 2 + kWTab * 4;  // 139264 B
-static_assert(4 * 2 * 64 * kWEP * 4 <= kWSmem, "the epilogue's m planes fit the main loop's LDS");
+constexpr int kWSmem = 4 * 2 * 64 * kWEP * 4;     // the epilogue's m planes (139264 B), over the two patch buffers
+static_assert(2 * kWBuf * 2 <= kWSmem, "patch buffers");
 constexpr int kWMaxG = 32;                     // in-kernel GroupNorm finalize: groups of the input
 
 #ifdef DM_K32_STAMPS
 // Diagnostic build only (-DDM_K32_STAMPS, tools/wino_stamps.py): per block, wave 0's s_memtime at the start, after
 // the prologue, after the main loop and at the end, and s_memrealtime at the start and the end, into this buffer only.
-__device__ unsigned long long g_wino_stamps[65536][8];
+__device__ unsigned long long g_wino_stamps[65536][16];
 #define W_STAMP(k)                                                                                           \
   do {                                                                                                       \
     if (threadIdx.x == 0 && blockIdx.x < 65536) g_wino_stamps[blockIdx.x][k] = __builtin_amdgcn_s_memtime();     \
@@ -67,6 +68,37 @@ __device__ unsigned long long g_wino_stamps[65536][8];
 #define W_STAMP(k) do {} while (0)
 #define W_RSTAMP(k) do {} while (0)
 #endif
+
+// lo[k] = fp16(x[k] - hi[k]) (hi[k] = fp16(x[k]): the difference exact) by v_fma_mixlo_f16 / v_fma_mixhi_f16: the
+// fp16 operand converted and the result rounded to fp16 in the instruction, two lanes of lo per register
+__device__ __forceinline__ void split_lo4(f4 x, f16x4 hi, f16x4& lo) {
+  typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+  const u2v hp = __builtin_bit_cast(u2v, hi);
+  u2v lp = {0u, 0u};
+#pragma unroll
+  for (int w = 0; w < 2; ++w) {
+    asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "+v"(lp[w]) : "v"(hp[w]), "v"(x[2 * w]));
+    asm("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(lp[w]) : "v"(hp[w]), "v"(x[2 * w + 1]));
+  }
+  lo = __builtin_bit_cast(f16x4, lp);
+}
+
+// v0[k] = row_shr(e1)[k] - e1[k], v3[k] = e0[k] - row_shl(e0)[k], DPP folded into the subtractions (bound_ctrl: the
+// shifted operand is 0 outside the 16-lane row). The leading s_nop 1 covers the VALU-write -> DPP-read hazard of the
+// inputs (the compiler does not see DPP inside inline asm).
+__device__ __forceinline__ void dpp_sub4(f4 e0, f4 e1, f4& v0, f4& v3) {
+  asm("s_nop 1\n"
+      "v_sub_f32_dpp %0, %8, %8 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+      "v_sub_f32_dpp %1, %9, %9 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+      "v_sub_f32_dpp %2, %10, %10 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+      "v_sub_f32_dpp %3, %11, %11 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+      "v_subrev_f32_dpp %4, %12, %12 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+      "v_subrev_f32_dpp %5, %13, %13 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+      "v_subrev_f32_dpp %6, %14, %14 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+      "v_subrev_f32_dpp %7, %15, %15 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+      : "=&v"(v0[0]), "=&v"(v0[1]), "=&v"(v0[2]), "=&v"(v0[3]), "=&v"(v3[0]), "=&v"(v3[1]), "=&v"(v3[2]), "=&v"(v3[3])
+      : "v"(e1[0]), "v"(e1[1]), "v"(e1[2]), "v"(e1[3]), "v"(e0[0]), "v"(e0[1]), "v"(e0[2]), "v"(e0[3]));
+}
 
 // x - hi[k] (hi[k] an fp16 piece of x: exact) in one v_fma_mix_f32 (the f16 operand converted in the instruction) instead
 // of a conversion and a subtraction
@@ -88,8 +120,8 @@ __device__ __forceinline__ float dpp_f(float v, int ctrl_shr) {
                                             : __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x101, 0xF, 0xF, true));
 }
 
-// PROM: input prologue -- 0 none, 1 GroupNorm affine, 2 GroupNorm affine + SiLU
-template <int W, int PROM>
+// PROM: input prologue -- 0 none, 1 GroupNorm affine, 2 GroupNorm affine + SiLU; SC: a shortcut segment (Cin2 > 0)
+template <int W, int PROM, bool SC>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) conv_wino_kernel(ConvArgs a) {
   constexpr bool PRO = PROM != 0;
   constexpr int NP = W / 2, TH = 128 / W, PR = TH + 2, NR = PR * NP;
@@ -98,43 +130,63 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   static_assert(UPW * 8 == PR * 4 && UPW * NP <= 64, "loader units tile the waves");
   constexpr int TM = 4, TN = 4, NTAP = 3;
 #ifndef DM_WINO_WD
-#define DM_WINO_WD 3
+#define DM_WINO_WD 2
 #endif
   constexpr int WD = DM_WINO_WD;  // B ring depth: a refill issued behind the next chunk's pixel loads (in-order vmcnt)
                                  // is consumed WD tap rows later
   __shared__ __attribute__((aligned(16))) char smem[kWSmem];
+  __shared__ __attribute__((aligned(16))) float gtab[kWTab];  // the image's GroupNorm tables (all its tiles)
   __shared__ float gstat[2 * kWMaxG];
   __shared__ double gxr[8 * 16 * 2];
   __shared__ __attribute__((aligned(16))) float gzero[8];  // the padding rows' table: 0 scale, 0 shift
   _Float16* patch = reinterpret_cast<_Float16*>(smem);
-  float* gtab = reinterpret_cast<float*>(smem + 2 * kWBuf * 2);
 
   const int HW = a.Hout * W;
   const int M = a.B * HW, N = a.Cout;
   const int nN = N / 128;
-  const int bid = xcd_remap_p(blockIdx.x, gridDim.x);
-  const int mt = bid / nN, nt = bid - mt * nN;
-  const int m0 = mt * 128, n0 = nt * 128;
-  const int b0 = m0 / HW;
-  const int y0 = (m0 - b0 * HW) / W;
-
+  // persistent blocks over the tiles of ONE image (its GroupNorm tables built once): grid = B x parts, block
+  // (image b0, part) takes tiles part * tpb .. + tpb - 1 of the image's (HW / 128) x nN, row tiles outer
+  const int parts = gridDim.x / a.B;
+  const int b0 = blockIdx.x / parts, part = blockIdx.x - b0 * parts;
+  const int tpb = (HW / 128) * nN / parts;
+  const int t_first = part * tpb, t_end = t_first + tpb;
   W_RSTAMP(5);
   W_STAMP(0);
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int nu = wave >> 1, ch = wave & 1;
   const int l16 = lane & 15, q = lane >> 4;
-
-  // ---- loader: unit u = (patch row pr, quarter sq), lane lj of the unit = pair lj (pixels 2 lj, 2 lj + 1)
-  const int lu = lane / NP, lj = lane - (lane / NP) * NP;
+  const int lu = lane / NP, lj = lane - (lane / NP) * NP;  // loader: unit lu of the wave, pair lj of the unit
   const bool lact = lu < UPW;
-  const int u = min(wave * UPW + lu, PR * 4 - 1);
+  const int u = min(wave * UPW + lu, PR * 4 - 1);  // unit u = (patch row pr, 8-channel quarter sq)
   const int pr = u >> 2, sq = u & 3;
-  const int iy = y0 - 1 + pr;
-  const bool rok = lact && iy >= 0 && iy < a.Hin;
-  const float* p0 = rok ? a.x1 + ((size_t)(b0 * a.Hin + iy) * W + 2 * lj) * a.x1_pitch + 8 * sq : kZeroPage + 8 * sq;
-  const float* p1 = rok ? p0 + a.x1_pitch : p0;
-  // chunk c + 1's pixels: loaded during chunk c - 1's tap row 2 (after its last use of the registers), finished at
-  // chunk c's tap rows 0 / 1 -- two tap rows of MFMAs and a barrier to cover a load from the Infinity Cache / HBM
+  const int Kp = NTAP * a.Cin1 + (SC ? a.Cin2 / 2 : 0);  // K of each U matrix (their stride in the image)
+  const int ngrp = ceil_div(N, 32);
+  const size_t sl = (size_t)ngrp * 1024;  // fp16 per 16-deep slice of the U images
+  const size_t qoff = (size_t)(q >> 1) * NTAP * sl;
+  const int nch = a.Cin1 / kWC;
+  const int kt_end = nch * NTAP;
+
+  // ---- per-tile state: the tile's rows and columns, the loader's pixel pointers, the B base
+  int m0 = 0, n0 = 0;
+  bool rok = false;
+  const float *p0 = nullptr, *p1 = nullptr;
+  const _Float16* wbase = nullptr;
+  auto set_tile = [&](int tile) {
+    const int mt = tile / nN, nt = tile - mt * nN;
+    m0 = b0 * HW + mt * 128;
+    n0 = nt * 128;
+    const int iy = mt * TH - 1 + pr;
+    rok = lact && iy >= 0 && iy < a.Hin;
+    p0 = rok ? a.x1 + ((size_t)(b0 * a.Hin + iy) * W + 2 * lj) * a.x1_pitch + 8 * sq : kZeroPage + 8 * sq;
+    p1 = rok ? p0 + a.x1_pitch : p0;
+    // column n0 + ch 64 + 16 j + l16 (n0 % 128 == 0): 32-column group (n0 + ch 64) / 32 + j / 2, column
+    // 16 (j & 1) + l16 of it -- one base pointer, compile-time offsets per j
+    wbase = reinterpret_cast<const _Float16*>(a.wino_ws) + (size_t)nu * (Kp / 16) * sl +
+            (size_t)((n0 + ch * 64) >> 5) * 1024 + ((q & 1) * 32 + l16) * 8;
+  };
+
+  // chunk c + 1's pixels: loaded a chunk ahead (right after the previous finish), finished before / after chunk c's
+  // MFMAs (the ping-pong below)
   f4 rw[4];
   auto load_raw = [&](int c) {
     const int co = c * kWC;
@@ -154,38 +206,49 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     f4 e0 = rw[h], e1 = rw[2 + h];
     if (PROM) {
       const float* ts = rok ? gtab + 2 * (c * kWC + 8 * sq + 4 * h) : gzero;  // [4 scales][4 shifts]
+#if DM_WINO_ABL == 6
+      const f4 sc = {1.f, 1.f, 1.f, 1.f}, sh = {0.f, 0.f, 0.f, 0.f};
+#else
       const f4 sc = *reinterpret_cast<const f4*>(ts), sh = *reinterpret_cast<const f4*>(ts + 4);
+#endif
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const float z0 = __builtin_fmaf(e0[k], sc[k], sh[k]);
         const float z1 = __builtin_fmaf(e1[k], sc[k], sh[k]);
+#if DM_WINO_ABL == 5
+        e0[k] = z0;
+        e1[k] = z1;
+#else
         e0[k] = PROM == 2 ? z0 * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(z0)) : z0;
         e1[k] = PROM == 2 ? z1 * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(z1)) : z1;
+#endif
       }
     }
     f4 vv[4];
+    // V0 = x[2j - 1] - x[2j + 1] (lane j - 1's second pixel: DPP row_shr), V3 = x[2j] - x[2j + 2] (lane j + 1's first
+    // pixel: row_shl), the shifted operand zero outside the 16-lane row (bound_ctrl) -- the map's padding columns
+    dpp_sub4(e0, e1, vv[0], vv[3]);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      float d0 = dpp_f(e1[k], 1);  // x[2j - 1]: lane j - 1's second pixel (0 at the row's first pair)
-      float d3 = dpp_f(e0[k], 0);  // x[2j + 2]: lane j + 1's first pixel (0 at the row's last pair)
-      if (NP < 16) {               // two units per DPP row: their boundary is a map edge too
-        d0 = lj == 0 ? 0.f : d0;
-        d3 = lj == NP - 1 ? 0.f : d3;
+      if (NP < 16) {  // two units per DPP row: their boundary is a map edge too
+        vv[0][k] = lj == 0 ? -e1[k] : vv[0][k];
+        vv[3][k] = lj == NP - 1 ? e0[k] : vv[3][k];
       }
-      vv[0][k] = d0 - e1[k];
       vv[1][k] = e0[k] + e1[k];
       vv[2][k] = e1[k] - e0[k];
-      vv[3][k] = e0[k] - d3;
     }
+#if DM_WINO_ABL == 4
+    if (lact && a.Cout < 0) {
+#else
     if (lact) {
+#endif
       _Float16* dst = patch + buf * kWBuf + (pr * NP + lj) * kWRowH + sq * 8 + 4 * h;
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
-        f16x4 hi, lo;  // x = hi + lo, lo = fp16(x - hi) (the difference exact)
+        f16x4 hi, lo;  // x = hi + lo, lo = fp16(x - hi) (the difference exact, one rounding to fp16)
 #pragma unroll
         for (int k = 0; k < 4; ++k) hi[k] = (_Float16)vv[v][k];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) lo[k] = (_Float16)sub_f16(vv[v][k], hi, k);
+        split_lo4(vv[v], hi, lo);
         *reinterpret_cast<f16x4*>(dst + v * NR * kWRowH) = hi;
         *reinterpret_cast<f16x4*>(dst + v * NR * kWRowH + 32) = lo;
       }
@@ -193,15 +256,14 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   };
 
   // ---- B: the fp16x2 fragment images of U_nu (split_conv_weights, nmat 4, ntap 3), 16-column halves
-  const int Kp = NTAP * a.Cin1;
-  const int ngrp = ceil_div(N, 32);
-  const size_t sl = (size_t)ngrp * 1024;  // fp16 per 16-deep slice
-  // column n0 + ch 64 + 16 j + l16 (n0 % 128 == 0): 32-column group (n0 + ch 64) / 32 + j / 2, column 16 (j & 1) + l16
-  // of it -- one base pointer, compile-time offsets per j
-  const _Float16* wbase = reinterpret_cast<const _Float16*>(a.wino_ws) + (size_t)nu * (Kp / 16) * sl +
-                          (size_t)((n0 + ch * 64) >> 5) * 1024 + ((q & 1) * 32 + l16) * 8;
-  const size_t qoff = (size_t)(q >> 1) * NTAP * sl;
   auto slice_off = [&](int kt) { return (size_t)(kt + (kt / NTAP) * NTAP) * sl + qoff; };
+  // all K steps of a tile: the 3 nch tap rows, then the ns shortcut steps (16-slices 3 Cin1 / 16 + 2 s (+ 1 for
+  // k-groups 2, 3)); past the end: the last step again (refills nothing uses)
+  const int ns = SC ? a.Cin2 / (2 * kWC) : 0, nst = kt_end + ns, nst_g = nch + ns;  // K steps, stages
+  auto step_off = [&](int kt) {
+    kt = min(kt, nst - 1);
+    return kt < kt_end ? slice_off(kt) : (size_t)(kt_end / 3 * 3 * kWC / 16 + 2 * (kt - kt_end) + (q >> 1)) * sl;
+  };
   f16x8 bq[WD][TN][2];
   auto load_b = [&](f16x8 (&dst)[TN][2], size_t off) {
 #pragma unroll
@@ -212,10 +274,6 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   };
 
   f4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
   // tap row dy: A fragment i = pair rows nu NR + 16 i + l16 + dy NP of buffer pbuf, the lane's k-group q
   const int abase = (nu * NR + l16) * kWRowH + q * 8;
   // a0: tile 0's fragment of this tap row on entry (read ahead); within a chunk, the next tap row's on exit
@@ -228,9 +286,6 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   auto compute = [&](int dy, int pbuf, const f16x8 (&bv)[TN][2]) {
     const _Float16* As = patch + pbuf * kWBuf + abase + dy * NP * kWRowH;
     f16x8 av[TM][2];
-#ifdef DM_WINO_NO_READAHEAD
-    if (dy > 0) read_a0(dy, pbuf);
-#endif
     av[0][0] = a0[0];
     av[0][1] = a0[1];
 #pragma unroll
@@ -240,24 +295,59 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[i][1], bv[j][0], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[i][0], bv[j][1], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[i][0], bv[j][0], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < TN; ++j) {  // (B, A): the transposed tile, lane (l16, q) = couts 4 q .. 4 q + 3 of pair l16
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bv[j][0], av[i][1], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bv[j][1], av[i][0], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bv[j][0], av[i][0], acc[i][j], 0, 0, 0);
       }
-#ifndef DM_WINO_NO_READAHEAD
       if (i == TM - 2 && dy + 1 < NTAP) read_a0(dy + 1, pbuf);
-#endif
     }
   };
 
-  // ---- prologue: B ring and the first chunk's pixels in flight while the GroupNorm tables are built
-  const int nch = a.Cin1 / kWC;
-  const int kt_end = nch * NTAP;
+  // ---- shortcut steps (the ResBlock's 1x1 of x2, a second K segment; wino_pack_kernel): step s stages, per pair p
+  // and 4-channel slot ks of the 32, nu 0 x2[2p][H1], nu 3 x2[2p + 1][H1], nu 1 / 2 x2[2p][H2] +/- x2[2p + 1][H2]
+  // (H1 = channels 32 s + .., H2 = Cin2 / 2 + 32 s + ..) as pair rows [nu][64] of a patch buffer
+  const int sp = t >> 3, sks = t & 7;
+  auto load_sc = [&](int st) {
+    const float* xs = a.x2 + (size_t)(m0 + 2 * sp) * a.x2_pitch + st * kWC + 4 * sks;
+    rw[0] = *reinterpret_cast<const f4*>(xs);
+    rw[1] = *reinterpret_cast<const f4*>(xs + a.x2_pitch);
+    rw[2] = *reinterpret_cast<const f4*>(xs + a.Cin2 / 2);
+    rw[3] = *reinterpret_cast<const f4*>(xs + a.x2_pitch + a.Cin2 / 2);
+  };
+  auto finish_sc = [&](int buf, int h) {  // h 0: planes 0, 3 (H1); h 1: planes 1, 2 (H2)
+    _Float16* dst = patch + buf * kWBuf + sp * kWRowH + 4 * sks;
 #pragma unroll
-  for (int d = 0; d < WD; ++d) load_b(bq[d], slice_off(min(d, kt_end - 1)));
-  load_raw(0);
-  if (PRO) {
+    for (int v2 = 0; v2 < 2; ++v2) {
+      const int v = h ? 1 + v2 : 3 * v2;
+      const f4 x = h ? (v2 ? rw[2] - rw[3] : rw[2] + rw[3]) : rw[v2];
+      f16x4 hi, lo;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) hi[k] = (_Float16)x[k];
+      split_lo4(x, hi, lo);
+      *reinterpret_cast<f16x4*>(dst + v * 64 * kWRowH) = hi;
+      *reinterpret_cast<f16x4*>(dst + v * 64 * kWRowH + 32) = lo;
+    }
+  };
+  // stage g of a tile: chunk g < nch, else shortcut step g - nch
+  auto load_stage = [&](int g) {
+    if (!SC || g < nch) load_raw(g);
+    else load_sc(g - nch);
+  };
+  auto finish_stage = [&](int g, int buf) {
+    if (!SC || g < nch) {
+      finish(g, buf, 0);
+      finish(g, buf, 1);
+    } else {
+      finish_sc(buf, 0);
+      finish_sc(buf, 1);
+    }
+  };
+
+  // GroupNorm tables of image b0 into LDS (scale, shift per channel, [c / 4][4 scales][4 shifts], times -log2(e)
+  // under SiLU); the caller's barrier publishes them
+  auto build_table = [&]() {
+    if (!PRO) return;
     const int C = a.Cin1;
     if (a.gin_part) {  // gn_finalize (gn.hip) for the tile's image, its expressions (conv_k32's in-kernel finalize)
       const int G = a.gin_G, cpg = C / G;
@@ -287,7 +377,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
           sc = sc * f;
           sh = sh * f + a.gin_mb[mo];
         }
-        const int ti = 2 * c - (c & 3);  // [c / 4][4 scales][4 shifts], times -log2(e) under SiLU
+        const int ti = 2 * c - (c & 3);
         gtab[ti] = PROM == 2 ? sc * -1.4426950408889634f : sc;
         gtab[ti + 4] = PROM == 2 ? sh * -1.4426950408889634f : sh;
       }
@@ -299,141 +389,268 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
         gtab[ti + 4] = PROM == 2 ? sh * -1.4426950408889634f : sh;
       }
     }
-    __syncthreads();
-  }
+  };
+
+  // ---- first tile's prologue: B ring and the first chunk's pixels in flight while the GroupNorm tables are built
+  int tile = t_first;
+  set_tile(tile);
+#pragma unroll
+  for (int d = 0; d < WD; ++d) load_b(bq[d], step_off(d));
+  load_raw(0);
+  build_table();
+  __syncthreads();
   finish(0, 0, 0);
   finish(0, 0, 1);
-  load_raw(min(1, nch - 1));
+  load_stage(min(1, nst_g - 1));
   __syncthreads();
   W_STAMP(1);
-
-#ifndef DM_WINO_NOPRIO
-  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
-#endif  // the second-dispatched half first (MI355X_MICROARCH.md 2-waves item 4)
-  // ---- main loop: chunk c's three tap rows from buffer c & 1; the next chunk's pixels loaded at tap row 0 and
-  // finished into the other buffer after tap row 2; one barrier per chunk
-  // ping-pong of the two waves of each SIMD (waves w and w + 4): the early group finishes chunk c + 1 before
-  // chunk c's MFMAs, the late group after them, so each wave's loader VALU runs beside its partner's MFMAs
+#ifdef DM_K32_STAMPS
+  unsigned long long loop_cycles = 0, t_loop = 0, ew_cycles = 0, out_cycles = 0, np_cycles = 0, t_s = 0;
+  int ntile_done = 0;
+#define W_ACC(var)                                       \
+  do {                                                   \
+    const unsigned long long now = __builtin_amdgcn_s_memtime(); \
+    var += now - t_s;                                    \
+    t_s = now;                                           \
+  } while (0)
+#else
+#define W_ACC(var) do {} while (0)
+#endif
+  // ping-pong of the two waves of each SIMD (waves w and w + 4): the early group finishes chunk c + 1 before chunk
+  // c's MFMAs, the late group after them, so each wave's loader VALU runs beside its partner's MFMAs
   // (MI355X_MICROARCH.md, two waves per SIMD); each loads chunk c + 2's pixels right after its finish, a chunk ahead
   const bool late = wave >= 4;
-  for (int c0 = 0; c0 < nch; c0 += 2) {
-#pragma unroll
-    for (int cc = 0; cc < 2; ++cc) {
-      const int c = c0 + cc;
-      if (c >= nch) continue;  // (not break: keeps the two-chunk body unrolled, bq[slot] statically indexed)
-      const int cn = min(c + 1, nch - 1);  // after the last chunk: refilled into the unused buffer
-#if DM_WINO_ABL != 1 && DM_WINO_ABL != 3
-      if (!late) {
-        finish(cn, (c + 1) & 1, 0);
-        finish(cn, (c + 1) & 1, 1);
-        load_raw(min(c + 2, nch - 1));
-      }
+  for (;;) {
+#ifdef DM_K32_STAMPS
+    t_loop = __builtin_amdgcn_s_memtime();
 #endif
-#pragma unroll
-      for (int dy = 0; dy < NTAP; ++dy) {
-        const int kt = c * NTAP + dy;
-        const int slot = (cc * NTAP + dy) % WD;
-        if (dy == 0) {
-          read_a0(0, c & 1);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        compute(dy, c & 1, bq[slot]);
-#if DM_WINO_ABL != 2 && DM_WINO_ABL != 3  // ablation builds (timing only, wrong results): 1 no finish, 2 no B refills, 3 neither
-        load_b(bq[slot], slice_off(min(kt + WD, kt_end - 1)));
-#endif
-        __builtin_amdgcn_sched_barrier(0);
-      }
-#if DM_WINO_ABL != 1 && DM_WINO_ABL != 3
-      if (late) {
-        finish(cn, (c + 1) & 1, 0);
-        finish(cn, (c + 1) & 1, 1);
-        load_raw(min(c + 2, nch - 1));
-      }
-#endif
-      __syncthreads();
-    }
-  }
-  W_STAMP(2);
-
-  // ---- epilogue: m_nu tiles (row scale undone) to LDS planes [nu][ch][64 pairs][kWEP]
-  float* E = reinterpret_cast<float*>(smem);
-  {
-    float* dst = E + (nu * 2 + ch) * 64 * kWEP;
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const float cs = a.wino_rowscale[n0 + ch * 64 + j * 16 + l16] * (PROM == 2 ? -0.6931471805599453f : 1.0f);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) dst[(i * 16 + 4 * q + r) * kWEP + j * 16 + l16] = acc[i][j][r] * cs;
-    }
-    float sum = 0.f;  // inf / NaN in any accumulator (an operand past fp16's range) makes the sum non-finite
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
+      for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    // ---- main loop: chunk c's three tap rows from buffer c & 1, chunk c + 1 finished into the other; one barrier
+    // per chunk
+    for (int c0 = 0; c0 < nch; c0 += 2) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) sum += acc[i][j][r];
-    if (!__builtin_isfinite(sum) && a.range_flag) *a.range_flag = 1;
-  }
-  __syncthreads();
-  // wave (chunk k, half hf, column half cj): output pixels 64 k + 32 hf .. + 31 of the tile = pairs 32 k + 16 hf ..,
-  // pixel 2 p + s of pair p: y0 = (m0 + m1) + m2, y1 = (m1 - m2) - m3
-  const int kq = wave >> 2, hf = (wave >> 1) & 1, cj = wave & 1;
-  typedef StagedEpilogue<64> Epi;
-  Epi epi(a, M, HW, b0, true, n0 + cj * 64, lane);
-  const int px0 = 64 * kq + 32 * hf;
-  const float* Ec = E + cj * 64 * kWEP + 4 * epi.c4;
-  epi.pairs_f(
-      [&](int i, f4& y0, f4& y1) {
-        const int pp = (px0 >> 1) + i;
-        const f4 mv0 = *reinterpret_cast<const f4*>(Ec + (0 * 2 * 64 + pp) * kWEP);
-        const f4 mv1 = *reinterpret_cast<const f4*>(Ec + (1 * 2 * 64 + pp) * kWEP);
-        const f4 mv2 = *reinterpret_cast<const f4*>(Ec + (2 * 2 * 64 + pp) * kWEP);
-        const f4 mv3 = *reinterpret_cast<const f4*>(Ec + (3 * 2 * 64 + pp) * kWEP);
-        y0 = (mv0 + mv1) + mv2;
-        y1 = (mv1 - mv2) - mv3;
-      },
-      m0 + px0);
-  if (a.gn_part) {  // the 64-pixel chunk's two halves: the hf = 1 wave's quad sums to LDS, added by the hf = 0 wave
-    double s, qq;
-    epi.quad_sums(s, qq);
-    double* xr = gxr + (kq * 2 + cj) * 16 * 2;
-    if (hf == 1 && lane < Epi::LPR) {
-      xr[2 * lane] = s;
-      xr[2 * lane + 1] = qq;
+      for (int cc = 0; cc < 2; ++cc) {
+        const int c = c0 + cc;
+        if (c >= nch) continue;  // (not break: keeps the two-chunk body unrolled, bq[slot] statically indexed)
+        const int gn = min(c + 1, nch - 1);  // after the last chunk: refilled into the unused buffer
+#if DM_WINO_ABL != 1 && DM_WINO_ABL != 3
+        if (!late) {
+          finish(gn, (c + 1) & 1, 0);
+          finish(gn, (c + 1) & 1, 1);
+          load_raw(min(c + 2, nch - 1));
+        }
+#endif
+#pragma unroll
+        for (int dy = 0; dy < NTAP; ++dy) {
+          const int kt = c * NTAP + dy;
+          const int slot = (cc * NTAP + dy) % WD;
+          if (dy == 0) {
+            read_a0(0, c & 1);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          compute(dy, c & 1, bq[slot]);
+#if DM_WINO_ABL != 2 && DM_WINO_ABL != 3  // ablation builds (timing only, wrong results): 1 no finish, 2 no B refills
+          load_b(bq[slot], step_off(kt + WD));
+#endif
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#if DM_WINO_ABL != 1 && DM_WINO_ABL != 3
+        if (late) {
+          finish(gn, (c + 1) & 1, 0);
+          finish(gn, (c + 1) & 1, 1);
+          load_raw(min(c + 2, nch - 1));
+        }
+#endif
+        __syncthreads();
+      }
+    }
+    // ---- the shortcut steps: stage g = nch + s from buffer g & 1, one K step each; the ring slot of step kt is
+    // kt & 1 (WD 2): after an odd number of tap rows the two slots trade places
+    if (SC && ns > 0) {
+      // its first step staged here (the main loop ends with every wave past its last read of buffer nch & 1)
+      load_sc(0);
+      finish_sc(nch & 1, 0);
+      finish_sc(nch & 1, 1);
+      load_sc(min(1, ns - 1));
+      __syncthreads();
+      if (kt_end & 1) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int p = 0; p < 2; ++p) {
+            const f16x8 tmp = bq[0][j][p];
+            bq[0][j][p] = bq[1][j][p];
+            bq[1][j][p] = tmp;
+          }
+      }
+      for (int s0 = 0; s0 < ns; s0 += 2) {
+#pragma unroll
+        for (int cc = 0; cc < 2; ++cc) {
+          const int st = s0 + cc;
+          if (st >= ns) continue;
+          const int g = nch + st, buf = g & 1;
+          if (!late) {
+            finish_sc(buf ^ 1, 0);  // stage min(g + 1, last): a shortcut step (its pixels loaded a stage ahead)
+            finish_sc(buf ^ 1, 1);
+            load_sc(min(st + 2, ns - 1));
+          }
+          const _Float16* As = patch + buf * kWBuf + (nu * 64 + l16) * kWRowH + q * 8;
+          a0[0] = *reinterpret_cast<const f16x8*>(As);
+          a0[1] = *reinterpret_cast<const f16x8*>(As + 32);
+          __builtin_amdgcn_sched_barrier(0);
+          f16x8 av[TM][2];
+          av[0][0] = a0[0];
+          av[0][1] = a0[1];
+#pragma unroll
+          for (int i = 1; i < TM; ++i)
+#pragma unroll
+            for (int p = 0; p < 2; ++p) av[i][p] = *reinterpret_cast<const f16x8*>(As + i * 16 * kWRowH + p * 32);
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bq[cc][j][0], av[i][1], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bq[cc][j][1], av[i][0], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bq[cc][j][0], av[i][0], acc[i][j], 0, 0, 0);
+            }
+          load_b(bq[cc], step_off(kt_end + st + WD));
+          __builtin_amdgcn_sched_barrier(0);
+          if (late) {
+            finish_sc(buf ^ 1, 0);
+            finish_sc(buf ^ 1, 1);
+            load_sc(min(st + 2, ns - 1));
+          }
+          __syncthreads();
+        }
+      }
+    }
+#ifdef DM_K32_STAMPS
+    t_s = __builtin_amdgcn_s_memtime();
+    loop_cycles += t_s - t_loop;
+    ++ntile_done;
+#endif
+
+    // the output lane's row scales (couts n0 + (wave & 1) 64 + 4 (lane % 16) ..): loaded under the E stores
+    const f4 cs4 = *reinterpret_cast<const f4*>(a.wino_rowscale + n0 + (wave & 1) * 64 + 4 * (lane & 15)) *
+                   (PROM == 2 ? -0.6931471805599453f : 1.0f);
+    // ---- epilogue: the m_nu tiles to LDS planes [nu][ch][64 pairs][kWEP] (16-B stores: the accumulators are the
+    // transposed tile); the row scale (times -ln 2 under SiLU) is applied after the output transform
+    float* E = reinterpret_cast<float*>(smem);
+    {
+      float* dst = E + (nu * 2 + ch) * 64 * kWEP + l16 * kWEP + 4 * q;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) *reinterpret_cast<f4*>(dst + i * 16 * kWEP + j * 16) = acc[i][j];
+    }
+    // the next tile's first pixels and B ring in flight during this tile's epilogue
+    const int cm0 = m0, cn0 = n0, cb0 = b0;
+    const int next = tile + 1;
+    const bool has_next = next < t_end;
+    if (has_next) {
+      set_tile(next);
+      load_raw(0);
+#pragma unroll
+      for (int d = 0; d < WD; ++d) load_b(bq[d], step_off(d));
     }
     __syncthreads();
-    if (hf == 0) {
-      s += xr[2 * (lane % Epi::LPR)];
-      qq += xr[2 * (lane % Epi::LPR) + 1];
-      epi.store_quads(s, qq, m0 + 64 * kq);
+    W_ACC(ew_cycles);
+    // wave (chunk k, half hf, column half cj): output pixels 64 k + 32 hf .. + 31 of the tile = pairs 32 k + 16 hf ..,
+    // pixel 2 p + s of pair p: y0 = (m0 + m1) + m2, y1 = (m1 - m2) - m3
+    {
+      const int kq = wave >> 2, hf = (wave >> 1) & 1, cj = wave & 1;
+      typedef StagedEpilogue<64> Epi;
+      Epi epi(a, M, HW, cb0, true, cn0 + cj * 64, lane);
+      const int px0 = 64 * kq + 32 * hf;
+      const float* Ec = E + cj * 64 * kWEP + 4 * epi.c4;
+      f4 fin = {0.f, 0.f, 0.f, 0.f};  // inf / NaN in any m (an operand past fp16's range) makes fin non-finite
+      epi.pairs_f(
+          [&](int i, f4& y0, f4& y1) {
+            const int pp = (px0 >> 1) + i;
+            const f4 mv0 = *reinterpret_cast<const f4*>(Ec + (0 * 2 * 64 + pp) * kWEP);
+            const f4 mv1 = *reinterpret_cast<const f4*>(Ec + (1 * 2 * 64 + pp) * kWEP);
+            const f4 mv2 = *reinterpret_cast<const f4*>(Ec + (2 * 2 * 64 + pp) * kWEP);
+            const f4 mv3 = *reinterpret_cast<const f4*>(Ec + (3 * 2 * 64 + pp) * kWEP);
+            y0 = ((mv0 + mv1) + mv2) * cs4;
+            y1 = ((mv1 - mv2) - mv3) * cs4;
+            fin += y0 + y1;
+          },
+          cm0 + px0);
+      if (!__builtin_isfinite(fin[0] + fin[1] + fin[2] + fin[3]) && a.range_flag) *a.range_flag = 1;
+      if (a.gn_part) {  // the 64-pixel chunk's two halves: the hf = 1 wave's quad sums via LDS to the hf = 0 wave
+        double s, qq;
+        epi.quad_sums(s, qq);
+        double* xr = gxr + (kq * 2 + cj) * 16 * 2;
+        if (hf == 1 && lane < Epi::LPR) {
+          xr[2 * lane] = s;
+          xr[2 * lane + 1] = qq;
+        }
+        __syncthreads();
+        if (hf == 0) {
+          s += xr[2 * (lane % Epi::LPR)];
+          qq += xr[2 * (lane % Epi::LPR) + 1];
+          epi.store_quads(s, qq, cm0 + 64 * kq);
+        }
+      }
     }
+    W_ACC(out_cycles);
+    if (!has_next) break;
+    // ---- the next tile's prologue: its first chunk (the E planes are dead after this barrier; same image: same
+    // GroupNorm tables, which sit outside the E planes)
+    tile = next;
+    __syncthreads();
+    finish(0, 0, 0);
+    finish(0, 0, 1);
+    load_stage(min(1, nst_g - 1));
+    __syncthreads();
+    W_ACC(np_cycles);
   }
+#ifdef DM_K32_STAMPS
+  if (threadIdx.x == 0 && blockIdx.x < 65536) {
+    g_wino_stamps[blockIdx.x][2] = loop_cycles;
+    g_wino_stamps[blockIdx.x][4] = ntile_done;
+    g_wino_stamps[blockIdx.x][8] = ew_cycles;
+    g_wino_stamps[blockIdx.x][9] = out_cycles;
+    g_wino_stamps[blockIdx.x][10] = np_cycles;
+  }
+#endif
   W_STAMP(3);
   W_RSTAMP(6);
 }
 
 // U = G g per (nu, output channel, chunk, tap row, channel of the chunk) from the packed 3x3 weights [Cout][K]
-// (K = 9 Cin1 chunk-major, conv_k32's order): [4][Cout][3 Cin1] in the same chunk-major order with 3 taps,
-// float64 sums rounded once to fp32
-__global__ void wino_pack_kernel(const float* w, int Cout, int K, int Cin1, float* out) {
-  const int Kp = 3 * Cin1;
+// (K = 9 Cin1 chunk-major, conv_k32's order, + Cin2 of the ResBlock shortcut): [4][Cout][3 Cin1 + Cin2 / 2] in the
+// same chunk-major order with 3 taps, float64 sums rounded once to fp32. The shortcut (y += Ws x2 per pixel) in the
+// pair domain: with its channels in halves H1, H2, nu 0 takes Ws_H1 x2[2j] (y0 only), nu 3 -Ws_H1 x2[2j + 1] (y1 only),
+// nu 1 / 2 Ws_H2 / 2 against x2[2j] +/- x2[2j + 1] (y0 = m1 + m2, y1 = m1 - m2): Cin2 / 2 more K per GEMM, balanced;
+// times -log2(e) when the main segment's SiLU constant is folded into the epilogue (fold).
+__global__ void wino_pack_kernel(const float* w, int Cout, int K, int Cin1, int Cin2, int fold, float* out) {
+  const int Kp = 3 * Cin1 + Cin2 / 2;
   const long total = 4L * Cout * Kp;
   const long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (id >= total) return;
   const int k = id % Kp;
   const long r = id / Kp;
   const int co = r % Cout, nu = r / Cout;
-  const int c = k / (3 * kWC), rem = k - c * 3 * kWC, dy = rem / kWC, ci = rem - dy * kWC;
-  const float* src = w + (size_t)co * K + (size_t)(c * 9 + dy * 3) * kWC + ci;
-  const double g0 = src[0], g1 = src[kWC], g2 = src[2 * kWC];
   double u;
-  switch (nu) {
-    case 0: u = g0; break;
-    case 1: u = (g0 + g1 + g2) * 0.5; break;
-    case 2: u = (g0 - g1 + g2) * 0.5; break;
-    default: u = g2; break;
+  if (k < 3 * Cin1) {
+    const int c = k / (3 * kWC), rem = k - c * 3 * kWC, dy = rem / kWC, ci = rem - dy * kWC;
+    const float* src = w + (size_t)co * K + (size_t)(c * 9 + dy * 3) * kWC + ci;
+    const double g0 = src[0], g1 = src[kWC], g2 = src[2 * kWC];
+    switch (nu) {
+      case 0: u = g0; break;
+      case 1: u = (g0 + g1 + g2) * 0.5; break;
+      case 2: u = (g0 - g1 + g2) * 0.5; break;
+      default: u = g2; break;
+    }
+  } else {
+    const int i = k - 3 * Cin1, hh = Cin2 / 2;
+    const float* src = w + (size_t)co * K + 9 * Cin1;
+    u = nu == 0 ? (double)src[i] : nu == 3 ? -(double)src[i] : 0.5 * (double)src[hh + i];
+    if (fold) u *= -1.4426950408889634074;  // 1 / (-ln 2)
   }
   out[id] = (float)u;
 }
@@ -442,7 +659,7 @@ __global__ void wino_pack_kernel(const float* w, int Cout, int K, int Cin1, floa
 
 #ifdef DM_K32_STAMPS
 extern "C" int dm_debug_wino_stamps(void* host, int nblocks) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wino_stamps), (size_t)nblocks * 8 * sizeof(unsigned long long)) ==
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wino_stamps), (size_t)nblocks * 16 * sizeof(unsigned long long)) ==
                  hipSuccess ? 0 : -2;
 }
 #endif
@@ -450,26 +667,38 @@ extern "C" int dm_debug_wino_stamps(void* host, int nblocks) {
 bool conv_wino_shape_ok(const ConvArgs& a) {
   if (!(a.taps == 9 && a.stride == 1 && a.upsample == 0 && a.ksplit <= 1)) return false;
   if (a.Hin != a.Hout || a.Win != a.Wout || (a.Wout != 32 && a.Wout != 16) || (a.Hout * a.Wout) % 128 != 0) return false;
-  if (a.Cin1 < kWC || a.Cin1 % kWC != 0 || 2 * a.Cin1 > kWTab || a.Cin2 != 0 || a.K != 9 * a.Cin1) return false;
+  if (a.Cin1 < kWC || a.Cin1 % kWC != 0 || 2 * a.Cin1 > kWTab || a.Cin2 % (2 * kWC) != 0 || a.K != 9 * a.Cin1 + a.Cin2)
+    return false;
+  if (a.Cin2 && (!a.x2 || a.x2_pitch % 4 != 0 || (reinterpret_cast<uintptr_t>(a.x2) & 15) != 0)) return false;
   if (a.Cout % 128 != 0) return false;
   if (a.gin_part && (a.gin_G <= 0 || a.gin_G > kWMaxG || a.Cin1 % a.gin_G != 0)) return false;
   return staged_epilogue_ok(a);
 }
 
-bool conv_wino_ok(const ConvArgs& a) { return a.wino_ws && a.wino_rowscale && conv_wino_shape_ok(a); }
+// the shortcut weights carry the SiLU fold of the epilogue iff the main segment's prologue has the SiLU
+static bool wino_fold_of(const ConvArgs& a) { return (a.pro_scale || a.gin_part) && !a.pro_nosilu; }
 
-size_t wino_weights_bytes(int Cout, int Cin1) { return split_conv_weights_bytes(4, Cout, 3 * Cin1, 2); }
+bool conv_wino_ok(const ConvArgs& a) {
+  return a.wino_ws && a.wino_rowscale && conv_wino_shape_ok(a) && (a.Cin2 == 0 || a.wino_fold == (int)wino_fold_of(a));
+}
 
-const float* wino_rowscale(const void* ws, int Cout, int Cin1) { return split_conv_rowscale(ws, 4, Cout, 3 * Cin1); }
+size_t wino_weights_bytes(int Cout, int Cin1, int Cin2) { return split_conv_weights_bytes(4, Cout, 3 * Cin1 + Cin2 / 2, 2); }
 
-int wino_weights(const float* w, int Cout, int Cin1, void* out, hipStream_t st) {
-  DM_REQUIRE(w && out && Cout > 0 && Cin1 > 0 && Cin1 % kWC == 0, "winograd weights: Cin must be a multiple of 32");
-  const long n = 4L * Cout * 3 * Cin1;
+const float* wino_rowscale(const void* ws, int Cout, int Cin1, int Cin2) {
+  return split_conv_rowscale(ws, 4, Cout, 3 * Cin1 + Cin2 / 2);
+}
+
+int wino_weights(const float* w, int Cout, int Cin1, int Cin2, int fold, void* out, hipStream_t st) {
+  DM_REQUIRE(w && out && Cout > 0 && Cin1 > 0 && Cin1 % kWC == 0 && Cin2 >= 0 && Cin2 % (2 * kWC) == 0,
+             "winograd weights: Cin must be a multiple of 32, the shortcut's a multiple of 64");
+  const int Kp = 3 * Cin1 + Cin2 / 2;
+  const long n = 4L * Cout * Kp;
   float* tmp = nullptr;  // plan-build time only: synchronous
   DM_CHECK_HIP(hipMalloc(reinterpret_cast<void**>(&tmp), n * sizeof(float)));
-  hipLaunchKernelGGL(wino_pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, w, Cout, 9 * Cin1, Cin1, tmp);
+  hipLaunchKernelGGL(wino_pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, w, Cout, 9 * Cin1 + Cin2,
+                     Cin1, Cin2, fold, tmp);
   int rc = hipGetLastError() == hipSuccess ? DM_OK : DM_ERR_HIP;
-  if (rc == DM_OK) rc = split_conv_weights(tmp, 4, Cout, 3 * Cin1, Cin1, 3, 2, out, st);
+  if (rc == DM_OK) rc = split_conv_weights(tmp, 4, Cout, Kp, Cin1, 3, 2, out, st);
   if (hipStreamSynchronize(st) != hipSuccess && rc == DM_OK) rc = DM_ERR_HIP;
   (void)hipFree(tmp);
   if (rc == DM_ERR_HIP) set_error("winograd weights: kernel launch failed");
@@ -478,17 +707,34 @@ int wino_weights(const float* w, int Cout, int Cin1, void* out, hipStream_t st) 
 
 std::string conv_wino_label(const ConvArgs& a) {
   const int prom = (a.pro_scale || a.gin_part) ? (a.pro_nosilu ? 1 : 2) : 0;
-  return std::string("conv_wino_kernel<") + std::to_string(a.Wout) + "," + std::to_string(prom) + ">";
+  return std::string("conv_wino_kernel<") + std::to_string(a.Wout) + "," + std::to_string(prom) + (a.Cin2 ? ",true>" : ",false>");
 }
 
 int conv2d_wino(const ConvArgs& a, hipStream_t st) {
   DM_REQUIRE(conv_wino_ok(a), "conv: shape not supported by the Winograd F(2,3) kernel");
-  const int blocks = (a.B * a.Hout * a.Wout / 128) * (a.Cout / 128);
+  // persistent blocks over one image's tiles: parts per image = the smallest divisor of its tile count that gives
+  // at least one block per CU (B = 256 at CIFAR size: one block per image)
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || ncu <= 0)
+      ncu = 256;
+  }
+  const int tpi = (a.Hout * a.Wout / 128) * (a.Cout / 128);
+  int parts = tpi;
+  for (int p = 1; p <= tpi; ++p)
+    if (tpi % p == 0 && (long)a.B * p >= ncu) {
+      parts = p;
+      break;
+    }
+  const int blocks = a.B * parts;
   const int prom = (a.pro_scale || a.gin_part) ? (a.pro_nosilu ? 1 : 2) : 0;
-#define DM_WINO_LAUNCH(W_, P_)                                                                \
-  if (a.Wout == W_ && prom == P_) {                                                           \
-    hipLaunchKernelGGL((conv_wino_kernel<W_, P_>), dim3(blocks), dim3(512), 0, st, a);         \
-    note_launch("conv_wino_kernel<" #W_ "," #P_ ">");                                         \
+#define DM_WINO_LAUNCH(W_, P_)                                                                              \
+  if (a.Wout == W_ && prom == P_) {                                                                         \
+    if (a.Cin2) hipLaunchKernelGGL((conv_wino_kernel<W_, P_, true>), dim3(blocks), dim3(512), 0, st, a);       \
+    else hipLaunchKernelGGL((conv_wino_kernel<W_, P_, false>), dim3(blocks), dim3(512), 0, st, a);             \
+    note_launch(a.Cin2 ? "conv_wino_kernel<" #W_ "," #P_ ",true>" : "conv_wino_kernel<" #W_ "," #P_ ",false>"); \
   }
   DM_WINO_LAUNCH(32, 0) DM_WINO_LAUNCH(32, 1) DM_WINO_LAUNCH(32, 2)
   DM_WINO_LAUNCH(16, 0) DM_WINO_LAUNCH(16, 1) DM_WINO_LAUNCH(16, 2)

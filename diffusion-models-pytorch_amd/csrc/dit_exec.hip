@@ -517,29 +517,35 @@ extern "C" int dm_dit_forward(dm_dit* h, const float* x, const int64_t* t, const
   const size_t nx = (size_t)B * m->arch.in_channels * S * S, no = (size_t)B * m->OC * S * S;
   // at most two passes: the caller's arithmetic, then (an fp16x2 operand beyond the fp16 range) fp32
   if (const int rco = m->plans.pool->order(st)) return rco;
-  for (int math = m->run_math();;) {
-    dm::DiTModel::Plan* plp = nullptr;
-    const int rc0 = m->get_plan(B, math, &plp);
-    if (rc0) return rc0;
-    auto& pl = *plp;
-    DM_CHECK_HIP(hipMemcpyAsync(pl.x, x, nx * sizeof(float), hipMemcpyDeviceToDevice, st));
-    DM_CHECK_HIP(hipMemcpyAsync(pl.t, t, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
-    if (y)
-      DM_CHECK_HIP(hipMemcpyAsync(pl.y, y, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
-    else
-      DM_CHECK_HIP(hipMemsetAsync(pl.y, 0xff, (size_t)B * sizeof(int64_t), st));  // -1: the null class
-    const int rc = pl.run(st);
-    if (rc) return rc;
-    DM_CHECK_HIP(hipMemcpyAsync(out, pl.out, no * sizeof(float), hipMemcpyDeviceToDevice, st));
-    if (math != 2 || !m->range_check || m->range_deferred) break;
-    DM_CHECK_HIP(hipMemcpyAsync(m->range_flag_host, m->range_flag, sizeof(int), hipMemcpyDeviceToHost, st));
-    DM_CHECK_HIP(hipStreamSynchronize(st));
-    if (!*m->range_flag_host) break;
-    DM_CHECK_HIP(hipMemsetAsync(m->range_flag, 0, sizeof(int), st));
-    m->range_fallbacks++;
-    math = 0;
-  }
-  return m->plans.pool->mark(st);
+  // every exit after order() records the completion event, so a later forward on another stream waits for
+  // whatever this one enqueued over the shared slab, even when it failed part way
+  const int rc_body = [&]() -> int {
+    for (int math = m->run_math();;) {
+      dm::DiTModel::Plan* plp = nullptr;
+      const int rc0 = m->get_plan(B, math, &plp);
+      if (rc0) return rc0;
+      auto& pl = *plp;
+      DM_CHECK_HIP(hipMemcpyAsync(pl.x, x, nx * sizeof(float), hipMemcpyDeviceToDevice, st));
+      DM_CHECK_HIP(hipMemcpyAsync(pl.t, t, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+      if (y)
+        DM_CHECK_HIP(hipMemcpyAsync(pl.y, y, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+      else
+        DM_CHECK_HIP(hipMemsetAsync(pl.y, 0xff, (size_t)B * sizeof(int64_t), st));  // -1: the null class
+      const int rc = pl.run(st);
+      if (rc) return rc;
+      DM_CHECK_HIP(hipMemcpyAsync(out, pl.out, no * sizeof(float), hipMemcpyDeviceToDevice, st));
+      if (math != 2 || !m->range_check || m->range_deferred) break;
+      DM_CHECK_HIP(hipMemcpyAsync(m->range_flag_host, m->range_flag, sizeof(int), hipMemcpyDeviceToHost, st));
+      DM_CHECK_HIP(hipStreamSynchronize(st));
+      if (!*m->range_flag_host) break;
+      DM_CHECK_HIP(hipMemsetAsync(m->range_flag, 0, sizeof(int), st));
+      m->range_fallbacks++;
+      math = 0;
+    }
+    return DM_OK;
+  }();
+  const int rc_mark = m->plans.pool->mark(st);
+  return rc_body ? rc_body : rc_mark;
 }
 
 extern "C" int dm_dit_set_range_deferred(dm_dit* h, int deferred) {

@@ -100,6 +100,7 @@ struct ConvArgs {
   // images of 4 matrices [Cout][3 Cin1] with their inverse row scales; set, the conv runs conv_wino_kernel
   const void* wino_ws;
   const float* wino_rowscale;
+  int wino_fold;  // the shortcut segment's weights were packed with the SiLU fold (wino_weights fold = 1)
   // the K32 variant the plan resolved at build time (conv_k32_pick + 1; 0: pick at launch), so the launch and the
   // op's profile label come from one decision
   int k32_resolved;
@@ -287,13 +288,14 @@ bool conv_k32_enabled();  // DM_CONV_K32 != 0
 int conv2d_k32(const ConvArgs& a, int v, hipStream_t st);
 std::string conv_k32_label(const ConvArgs& a, int v);
 // Winograd F(2,3)-along-x 3x3 convs (conv_wino.hip): the shapes the kernel takes (32- / 16-wide maps, 128-pixel
-// tiles, Cout % 128 == 0, no second K segment), whether a conv has its weights and shape, the weights (U = G g,
-// float64, then the fp16x2 split of split_conv_weights with nmat 4, ntap 3), their size / row scales, launcher
+// tiles, Cout % 128 == 0, a ResBlock shortcut segment of Cin2 % 64 == 0), whether a conv has its weights and shape, the
+// weights (U = G g, float64, then the fp16x2 split of split_conv_weights with nmat 4, ntap 3; fold: the shortcut's
+// weights times -log2(e), for convs whose prologue has the SiLU), their size / row scales, launcher
 bool conv_wino_shape_ok(const ConvArgs& a);
 bool conv_wino_ok(const ConvArgs& a);
-size_t wino_weights_bytes(int Cout, int Cin1);
-const float* wino_rowscale(const void* ws, int Cout, int Cin1);
-int wino_weights(const float* w, int Cout, int Cin1, void* out, hipStream_t st);
+size_t wino_weights_bytes(int Cout, int Cin1, int Cin2);
+const float* wino_rowscale(const void* ws, int Cout, int Cin1, int Cin2);
+int wino_weights(const float* w, int Cout, int Cin1, int Cin2, int fold, void* out, hipStream_t st);
 std::string conv_wino_label(const ConvArgs& a);
 int conv2d_wino(const ConvArgs& a, hipStream_t st);
 // static-weight GEMM on pre-split weights with K = 32 MFMA steps (linear_k32.hip)

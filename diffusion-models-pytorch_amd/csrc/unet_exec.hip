@@ -185,7 +185,7 @@ struct UNetModel {
   bool range_deferred = false;
   long range_fallbacks = 0;   // forwards / loops re-run in bf16x3 (dm_unet_range_stats)
   std::map<std::pair<const float*, int>, void*> split_w;
-  std::map<const float*, void*> wino_w;  // Winograd F(2,3) weights of the convs conv_wino_kernel takes
+  std::map<std::pair<const float*, int>, void*> wino_w;  // Winograd F(2,3) weights (per shortcut fold) of its convs
   size_t split_bytes = 0;
   void split_for(ConvArgs& c);
   // folded single-head attention blocks (attn_block.hip): per block's qkv weights, the fp32 products At, w,
@@ -261,25 +261,27 @@ void UNetModel::split_for(ConvArgs& c) {
   c.wino_ws = nullptr;
   c.wino_rowscale = nullptr;
   if (conv_math != 2 || !toggles().wino || !conv_wino_shape_ok(c)) return;
-  auto iw = wino_w.find(c.w);
+  const int fold = c.Cin2 && (c.pro_scale || c.gin_part) && !c.pro_nosilu ? 1 : 0;
+  auto iw = wino_w.find(std::make_pair(c.w, fold));
   void* wp = nullptr;
   if (iw != wino_w.end()) {
     wp = iw->second;
   } else {
-    const size_t nb = wino_weights_bytes(c.Cout, c.Cin1);
+    const size_t nb = wino_weights_bytes(c.Cout, c.Cin1, c.Cin2);
     if (hipMalloc(&wp, nb) != hipSuccess) {
       (void)hipGetLastError();
       return;
     }
-    if (wino_weights(c.w, c.Cout, c.Cin1, wp, nullptr) != DM_OK) {
+    if (wino_weights(c.w, c.Cout, c.Cin1, c.Cin2, fold, wp, nullptr) != DM_OK) {
       (void)hipFree(wp);
       return;
     }
-    wino_w[c.w] = wp;
+    wino_w[std::make_pair(c.w, fold)] = wp;
     split_bytes += nb;
   }
   c.wino_ws = wp;
-  c.wino_rowscale = wino_rowscale(wp, c.Cout, c.Cin1);
+  c.wino_rowscale = wino_rowscale(wp, c.Cout, c.Cin1, c.Cin2);
+  c.wino_fold = fold;
 }
 
 // The folded weights of a single-head attention block (attn_fold, float64 products of the block's own
@@ -1421,29 +1423,35 @@ extern "C" int dm_unet_forward(dm_unet* h, const float* x, const int64_t* t, con
   // at most two passes: the caller's arithmetic, then (fp16x2 met an activation beyond the fp16 range) the
   // same forward in bf16x3; the model's next forward is fp16x2 again
   if (const int rco = m->plans.pool->order(st)) return rco;
-  for (int math = m->run_math();;) {
-    dm::UNetModel::Plan* plp = nullptr;
-    const int rc0 = m->get_plan(B, H, W, math, &plp);
-    if (rc0) return rc0;
-    auto& pl = *plp;
-    DM_CHECK_HIP(hipMemcpyAsync(pl.x, x, nx * sizeof(float), hipMemcpyDeviceToDevice, st));
-    DM_CHECK_HIP(hipMemcpyAsync(pl.t, t, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
-    if (y)
-      DM_CHECK_HIP(hipMemcpyAsync(pl.y, y, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
-    else
-      DM_CHECK_HIP(hipMemsetAsync(pl.y, 0xff, (size_t)B * sizeof(int64_t), st));  // -1: no label
-    const int rc = pl.run(st);
-    if (rc) return rc;
-    DM_CHECK_HIP(hipMemcpyAsync(out, pl.out, no * sizeof(float), hipMemcpyDeviceToDevice, st));
-    if (math != 2 || !m->range_check || m->range_deferred) break;
-    DM_CHECK_HIP(hipMemcpyAsync(m->range_flag_host, m->range_flag, sizeof(int), hipMemcpyDeviceToHost, st));
-    DM_CHECK_HIP(hipStreamSynchronize(st));
-    if (!*m->range_flag_host) break;
-    DM_CHECK_HIP(hipMemsetAsync(m->range_flag, 0, sizeof(int), st));
-    m->range_fallbacks++;
-    math = 3;
-  }
-  return m->plans.pool->mark(st);
+  // every exit after order() records the completion event, so a later forward on another stream waits for
+  // whatever this one enqueued over the shared slab, even when it failed part way
+  const int rc_body = [&]() -> int {
+    for (int math = m->run_math();;) {
+      dm::UNetModel::Plan* plp = nullptr;
+      const int rc0 = m->get_plan(B, H, W, math, &plp);
+      if (rc0) return rc0;
+      auto& pl = *plp;
+      DM_CHECK_HIP(hipMemcpyAsync(pl.x, x, nx * sizeof(float), hipMemcpyDeviceToDevice, st));
+      DM_CHECK_HIP(hipMemcpyAsync(pl.t, t, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+      if (y)
+        DM_CHECK_HIP(hipMemcpyAsync(pl.y, y, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+      else
+        DM_CHECK_HIP(hipMemsetAsync(pl.y, 0xff, (size_t)B * sizeof(int64_t), st));  // -1: no label
+      const int rc = pl.run(st);
+      if (rc) return rc;
+      DM_CHECK_HIP(hipMemcpyAsync(out, pl.out, no * sizeof(float), hipMemcpyDeviceToDevice, st));
+      if (math != 2 || !m->range_check || m->range_deferred) break;
+      DM_CHECK_HIP(hipMemcpyAsync(m->range_flag_host, m->range_flag, sizeof(int), hipMemcpyDeviceToHost, st));
+      DM_CHECK_HIP(hipStreamSynchronize(st));
+      if (!*m->range_flag_host) break;
+      DM_CHECK_HIP(hipMemsetAsync(m->range_flag, 0, sizeof(int), st));
+      m->range_fallbacks++;
+      math = 3;
+    }
+    return DM_OK;
+  }();
+  const int rc_mark = m->plans.pool->mark(st);
+  return rc_body ? rc_body : rc_mark;
 }
 
 extern "C" int dm_unet_set_range_deferred(dm_unet* h, int deferred) {

@@ -94,7 +94,7 @@ class ConvDesc(ctypes.Structure):
         ('tile', ctypes.c_int),
         ('pro_scale', vp), ('pro_shift', vp),
         ('w_split', vp), ('w_split_kind', ctypes.c_int), ('range_flag', vp), ('pro_nosilu', ctypes.c_int),
-        ('ksplit', ctypes.c_int), ('kpart', vp), ('w_wino', vp),
+        ('ksplit', ctypes.c_int), ('kpart', vp), ('w_wino', vp), ('w_wino_fold', ctypes.c_int),
     ]
 
 
@@ -242,9 +242,9 @@ def _declare(L: ctypes.CDLL):
     L.dm_pack_conv_weight_subpixel.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp]
     L.dm_debug_launch_log.argtypes = [ctypes.c_int]
     L.dm_debug_launch_log_read.argtypes = [ctypes.c_char_p, ctypes.c_int]
-    L.dm_conv_weight_wino_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
+    L.dm_conv_weight_wino_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
     L.dm_conv_weight_wino_bytes.restype = ctypes.c_int64
-    L.dm_pack_conv_weight_wino.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp]
+    L.dm_pack_conv_weight_wino.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp]
     L.dm_conv_weight_split_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
     L.dm_conv_weight_split_bytes.restype = ctypes.c_int64
     L.dm_pack_conv_weight_split.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -415,16 +415,17 @@ def pack_conv_weight_split(wp: torch.Tensor, nmat: int, Cin: int, taps: int, kin
     return out
 
 
-def pack_conv_weight_wino(wp: torch.Tensor, Cin: int) -> torch.Tensor:
-    """Packed fp32 3x3 conv weights [Cout, 9 Cin] -> the Winograd F(2,3) weight images (a uint8 device tensor)
-    for ConvDesc.w_wino (used with ConvDesc.w_split of kind SPLIT_FP16X2)."""
+def pack_conv_weight_wino(wp: torch.Tensor, Cin: int, Cin2: int = 0, fold: bool = False) -> torch.Tensor:
+    """Packed fp32 3x3 conv weights [Cout, 9 Cin + Cin2] (Cin2: the 1x1 shortcut segment) -> the Winograd F(2,3)
+    weight images (a uint8 device tensor) for ConvDesc.w_wino (with ConvDesc.w_split of kind SPLIT_FP16X2);
+    fold = True for a conv whose prologue has the SiLU (set ConvDesc.w_wino_fold alike)."""
     Cout, K = wp.shape
-    nbytes = load().dm_conv_weight_wino_bytes(Cout, Cin)
-    if nbytes <= 0 or K != 9 * Cin:
-        raise ValueError('Winograd packing needs [Cout, 9 Cin] weights with Cin a multiple of 32')
+    nbytes = load().dm_conv_weight_wino_bytes(Cout, Cin, Cin2)
+    if nbytes <= 0 or K != 9 * Cin + Cin2:
+        raise ValueError('Winograd packing needs [Cout, 9 Cin + Cin2] weights, Cin % 32 == 0, Cin2 % 64 == 0')
     out = torch.empty(nbytes, dtype=torch.uint8, device=wp.device)
-    check(load().dm_pack_conv_weight_wino(wp.data_ptr(), Cout, Cin, out.data_ptr(), stream_handle(wp.device)),
-          'dm_pack_conv_weight_wino')
+    check(load().dm_pack_conv_weight_wino(wp.data_ptr(), Cout, Cin, Cin2, int(bool(fold)), out.data_ptr(),
+                                          stream_handle(wp.device)), 'dm_pack_conv_weight_wino')
     return out
 
 

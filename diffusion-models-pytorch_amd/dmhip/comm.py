@@ -40,12 +40,45 @@ class Comm:
 
     @classmethod
     def from_process_group(cls, group=None) -> 'Comm':
-        """Bootstrap over an initialised torch.distributed group (gloo or RCCL): rank 0's id is broadcast."""
+        """Bootstrap over an initialised torch.distributed group (gloo or RCCL): rank 0's id is broadcast.
+        Raises on every rank together if any rank could not set up its communicator (try_from_process_group)."""
+        comm = cls.try_from_process_group(group)
+        if comm is None:
+            raise RuntimeError('dm_comm: the C-ABI communicator could not be set up on every rank')
+        return comm
+
+    @classmethod
+    def try_from_process_group(cls, group=None) -> Optional['Comm']:
+        """The communicator on every rank, or None on every rank (the ranks agree). Rank 0 always
+        broadcasts -- the unique id, or None when RCCL cannot be loaded -- and the ranks then all-reduce whether
+        their dm_comm_init succeeded, so a failure on any rank sends all of them to the torch.distributed path
+        together instead of leaving collectives paired wrongly."""
         import torch.distributed as dist
         rank, world = dist.get_rank(group), dist.get_world_size(group)
-        obj = [unique_id() if rank == 0 else None]
+        uid = None
+        if rank == 0:
+            try:
+                uid = unique_id()
+            except (RuntimeError, ValueError, OSError):
+                uid = None
+        obj = [uid]
         dist.broadcast_object_list(obj, src=0, group=group)
-        return cls(obj[0], world, rank)
+        if obj[0] is None:
+            return None
+        comm = None
+        try:
+            comm = cls(obj[0], world, rank)
+        except (RuntimeError, ValueError, OSError):
+            comm = None
+        backend = dist.get_backend(group)
+        dev = torch.device('cuda', torch.cuda.current_device()) if backend == 'nccl' else torch.device('cpu')
+        ok = torch.tensor([1 if comm is not None else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+        if int(ok.item()) == 0:
+            if comm is not None:
+                comm.close()
+            return None
+        return comm
 
     def info(self):
         n, r, d = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()

@@ -38,7 +38,8 @@ class DistEnv:
         if self.world > 1 and not dist.is_initialized():
             kw = dict(device_id=self.device) if self.backend == 'nccl' else {}
             dist.init_process_group(self.backend, **kw)
-        self._comm = None
+        self._comm = None  # the C-ABI communicator (None: not set up yet; False: the torch path on every rank)
+        self._checked = False
 
     @property
     def is_main(self):
@@ -54,13 +55,20 @@ class DistEnv:
             return x
         x = x.contiguous()
         out = torch.empty((self.world * x.shape[0], *x.shape[1:]), dtype=x.dtype, device=x.device)
-        if x.device.type == 'cuda' and self.backend == 'nccl' and os.environ.get('DM_GATHER') != 'torch':
+        if (x.device.type == 'cuda' and self.backend == 'nccl' and x.dtype == torch.float32
+                and os.environ.get('DM_GATHER') != 'torch' and self._comm is not False):
             if self._comm is None:   # RCCL communicator of the C ABI, bootstrapped once over the process group
                 from dmhip.comm import Comm
-                self._comm = Comm.from_process_group()
-            self._comm.allgather(x, out)   # one RCCL all-gather over xGMI (dm_allgather_f32)
-        elif x.device.type == 'cuda' and self.backend == 'nccl':
+                self._comm = Comm.try_from_process_group() or False  # False: every rank takes the torch path
+            if self._comm is not False:
+                self._comm.allgather(x, out)   # one RCCL all-gather over xGMI (dm_allgather_f32)
+                if not self._checked:
+                    self._check_gather(x, out)
+                if self._comm is not False:
+                    return out
             dist.all_gather_into_tensor(out, x)
+        elif x.device.type == 'cuda' and self.backend == 'nccl':
+            dist.all_gather_into_tensor(out, x)   # other dtypes (dm_allgather_f32 is float32 only)
         else:
             host = out.cpu() if out.device.type != 'cpu' else out
             dist.all_gather(list(host.chunk(self.world)), x.cpu())
@@ -68,10 +76,26 @@ class DistEnv:
                 out.copy_(host)
         return out
 
-    def close(self):
-        if self._comm is not None:
+    def _check_gather(self, x: torch.Tensor, out: torch.Tensor) -> None:
+        """First gather at world > 1: the C-ABI all-gather against all_gather_into_tensor of the same
+        fold; if any rank sees a difference, every rank drops to the torch path (agreed by an all-reduce)."""
+        ref = torch.empty_like(out)
+        dist.all_gather_into_tensor(ref, x)
+        same = torch.tensor([1 if torch.equal(ref, out) else 0], dtype=torch.int32, device=out.device)
+        dist.all_reduce(same, op=dist.ReduceOp.MIN)
+        self._checked = True
+        if int(same.item()) == 0:
+            import sys
+            print('dm_comm: dm_allgather_f32 differs from all_gather_into_tensor; using torch.distributed',
+                  file=sys.stderr)
             self._comm.close()
-            self._comm = None
+            self._comm = False
+            out.copy_(ref)
+
+    def close(self):
+        if self._comm:
+            self._comm.close()
+        self._comm = None
         if self.world > 1 and dist.is_initialized():
             dist.destroy_process_group()
 

@@ -289,16 +289,13 @@ int64_t dm_conv_weight_split_bytes(int nmat, int Cout, int K, int kind);
 int dm_pack_conv_weight_split(const float* w, int nmat, int Cout, int K, int Cin, int taps, int kind, void* out,
                               void* stream);
 
-/* Winograd F(2,3)-along-x weights of a packed 3x3 conv (dm_pack_conv_weight, K = 9 Cin, Cin % 32 == 0):
- * U = G g per tap row (float64, one rounding), split to fp16x2 fragment images of 4 matrices [Cout][3 Cin]
- * with per-output-channel power-of-two scales: dm_conv_weight_wino_bytes(Cout, Cin) bytes at `out`. */
-int64_t dm_conv_weight_wino_bytes(int Cout, int Cin);
-/* Test hook: the conv launchers record the kernel instantiation they issue while the log is on.
- * dm_debug_launch_log(1) clears and starts it, (0) stops it; _read copies it (newline-separated, NUL-terminated)
- * into buf and returns its length. */
-int dm_debug_launch_log(int enable);
-int dm_debug_launch_log_read(char* buf, int len);
-int dm_pack_conv_weight_wino(const float* w, int Cout, int Cin, void* out, void* stream);
+/* Winograd F(2,3)-along-x weights of a packed 3x3 conv (dm_pack_conv_weight, K = 9 Cin + Cin2, Cin % 32 == 0; Cin2: a
+ * second 1x1 segment (the ResBlock shortcut), Cin2 % 64 == 0): U = G g per tap row (float64, one rounding), split to
+ * fp16x2 fragment images of 4 matrices [Cout][3 Cin + Cin2 / 2] with per-output-channel power-of-two scales:
+ * dm_conv_weight_wino_bytes(Cout, Cin, Cin2) bytes at `out`. fold = 1 for a conv whose input prologue has the SiLU
+ * (dm_conv_desc pro_scale set, pro_nosilu 0) and a shortcut (its weights carry the kernel's SiLU constant). */
+int64_t dm_conv_weight_wino_bytes(int Cout, int Cin, int Cin2);
+int dm_pack_conv_weight_wino(const float* w, int Cout, int Cin, int Cin2, int fold, void* out, void* stream);
 
 typedef struct dm_conv_desc {
   const float* x;  int x_pitch, Cin, Hin, Win;
@@ -332,6 +329,7 @@ typedef struct dm_conv_desc {
    * DM_SPLIT_FP16X2 too): 32- / 16-pixel-wide maps with Cout % 128 == 0 then run the Winograd kernel (tile 0 or
    * 21; 21 fails on any other shape) */
   const void* w_wino;
+  int w_wino_fold;   /* the fold dm_pack_conv_weight_wino packed w_wino with */
 } dm_conv_desc;
 /* 1x1 convs (taps 1, K = Cin, Cin % 32 == 0) with DM_SPLIT_FP16X2 weights run on the split kernel
  * with the same prologue / epilogue options: the static-weight GEMMs of the attention blocks. */

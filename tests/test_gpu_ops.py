@@ -155,8 +155,9 @@ def _run_conv(cuda, x_nhwc, w_packed, Cout, Hout, Wout, taps, stride=1, upsample
         if range_flag is not None:
             d.range_flag = range_flag.data_ptr()
     if wino:  # Winograd F(2,3) weights (conv_wino.hip; with fp16x2 split weights)
-        ww = dmhip.pack_conv_weight_wino(w_packed[:, :9 * Cin].contiguous(), Cin)
-        d.w_wino = ww.data_ptr()
+        fold = pro is not None and not pro_nosilu
+        ww = dmhip.pack_conv_weight_wino(w_packed, Cin, Cin2, fold)
+        d.w_wino, d.w_wino_fold = ww.data_ptr(), int(fold)
     if ksplit > 1:  # split-K partial sums [ksplit][B * Hout * Wout][Cout]
         kpart = torch.empty((ksplit, B * Hout * Wout, Cout), device=cuda)
         d.ksplit, d.kpart = ksplit, kpart.data_ptr()

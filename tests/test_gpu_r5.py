@@ -35,7 +35,7 @@ def test_wino_conv3x3_exact(cuda, B, Cin, Cout, H):
                   split='fp16x2', wino=True)
     log = dmhip.launch_log_read()
     dmhip.launch_log(False)
-    assert log == [f'conv_wino_kernel<{H},0>'], log
+    assert log == [f'conv_wino_kernel<{H},0,false>'], log
     assert torch.equal(y.cpu(), _nhwc(ref))
 
 
@@ -56,6 +56,66 @@ def test_wino_rowvec_residual_pitch(cuda, H):
                   res=_nhwc(res).to(cuda), y_pitch=160, x_pitch=96, tile=WINO, split='fp16x2', wino=True)
     assert torch.equal(y[..., :Cout].cpu(), _nhwc(ref))
     assert torch.isnan(y[..., Cout:]).all()
+
+
+@pytest.mark.parametrize('C1,C2,H,Cout,pro', [(64, 64, 32, 128, False), (128, 384, 32, 128, False), (96, 128, 16, 256, False),
+                                              (32, 192, 16, 128, False), (64, 128, 32, 128, True)])
+def test_wino_shortcut_segment_exact(cuda, C1, C2, H, Cout, pro):
+    """ResBlock conv2: 3x3 over h plus the 1x1 shortcut of x as a second K segment (nu 0 / 3: the pair's pixels,
+    nu 1 / 2: their sum and difference against half the weights), temb row vector, residual -- integer-exact (with the
+    GroupNorm affine prologue of integer tables and no SiLU: exact too)."""
+    B = 2
+    h = _ints((B, C1, H, H), seed=70)
+    x = _ints((B, C2, H, H), seed=71)
+    w2 = _ints((Cout, C1, 3, 3), -2, 3, seed=72)
+    ws = _ints((Cout, C2, 1, 1), seed=73)
+    b = _ints((Cout, ), seed=74)
+    rv = _ints((B, Cout), seed=75)
+    res = _ints((B, Cout, H, H), seed=76)
+    K = 9 * C1 + C2
+    wp = torch.zeros((Cout, K), device=cuda)
+    _pack(w2, cuda, K, 0, wp)
+    _pack(ws, cuda, K, 9 * C1, wp)
+    hin = h
+    prot = None
+    if pro:  # integer GroupNorm-affine tables (scale 2, shift -1), no SiLU: exact
+        sc = torch.full((B, C1), 2.0)
+        sh = torch.full((B, C1), -1.0)
+        hin = h * 2 - 1
+        prot = (sc.to(cuda), sh.to(cuda))
+    ref = (F.conv2d(hin.double(), w2.double(), b.double(), padding=1) + rv.double()[:, :, None, None]
+           + F.conv2d(x.double(), ws.double()) + res.double()).float()
+    dmhip.launch_log(True)
+    y = _run_conv(cuda, _nhwc(h).to(cuda), wp, Cout, H, H, 9, bias=b.to(cuda), rowvec=rv.to(cuda),
+                  res=_nhwc(res).to(cuda), x2=_nhwc(x).to(cuda), Cin2=C2, tile=WINO, split='fp16x2', wino=True,
+                  pro=prot, pro_nosilu=1 if pro else 0)
+    log = dmhip.launch_log_read()
+    dmhip.launch_log(False)
+    assert log == [f'conv_wino_kernel<{H},{1 if pro else 0},true>'], log
+    assert torch.equal(y.cpu(), _nhwc(ref))
+
+
+@pytest.mark.parametrize('B,C1,C2,Cout,H', [(4, 128, 384, 128, 32), (8, 256, 128, 256, 16)])
+def test_wino_shortcut_fp32_accuracy(cuda, report, B, C1, C2, Cout, H):
+    """GroupNorm + SiLU conv2 with the shortcut segment (the SiLU fold in its weights) on random data: within 3x the
+    fp32 MFMA kernel's error vs float64."""
+    xd, wp3, b, pro, ref3 = _rand_case(cuda, B, C1, Cout, H, 0, seed=93)
+    g = torch.Generator().manual_seed(94)
+    x2 = torch.randn((B, C2, H, H), generator=g)
+    ws = torch.randn((Cout, C2, 1, 1), generator=g) * (1.0 / C2 ** 0.5)
+    K = 9 * C1 + C2
+    wp = torch.zeros((Cout, K), device=cuda)
+    wp[:, :9 * C1] = wp3
+    _pack(ws, cuda, K, 9 * C1, wp)
+    ref = ref3 + F.conv2d(x2.double(), ws.double())
+    errs = {}
+    for name, split, tile, wino in (('fp32', False, 0, False), ('wino', 'fp16x2', WINO, True)):
+        y = _run_conv(cuda, xd, wp, Cout, H, H, 9, 1, 0, b.to(cuda), pro=pro, split=split, tile=tile, wino=wino,
+                      x2=_nhwc(x2).to(cuda), Cin2=C2)
+        errs[name] = (y.cpu().double() - _nhwc(ref)).abs().max().item()
+    scale = ref.abs().max().item()
+    report(f'wino_shortcut_accuracy_{B}_{C1}_{C2}_{H}_max_rel', errs['wino'] / scale)
+    assert errs['wino'] < 3.0 * errs['fp32'] + 1e-7 * scale, errs
 
 
 @pytest.mark.parametrize('B,Cin,Cout,H', [(4, 128, 128, 32), (8, 256, 256, 16), (2, 384, 128, 32), (4, 512, 256, 16)])
@@ -113,9 +173,9 @@ def test_wino_cifar_forward(cuda, golden, monkeypatch, report, B):
     _, out_w, log_w = _forward_logged(meta, 'cifar10', cuda, x, t)
     monkeypatch.setenv('DM_CONV_WINO', '0')
     _, out_d, log_d = _forward_logged(meta, 'cifar10', cuda, x, t)
-    n32 = log_w.count('conv_wino_kernel<32,2>')
-    n16 = log_w.count('conv_wino_kernel<16,2>')
-    assert n32 >= 4 and n16 >= 4, log_w
+    n32 = sum(log_w.count(f'conv_wino_kernel<32,2,{sc}>') for sc in ('false', 'true'))
+    n16 = sum(log_w.count(f'conv_wino_kernel<16,2,{sc}>') for sc in ('false', 'true'))
+    assert n32 == 10 and n16 == 10, log_w  # every 3x3 ResBlock conv of the 32^2 / 16^2 levels, shortcuts included
     assert not any(s.startswith('conv_wino') for s in log_d), log_d
     err = (out_w - out_d).abs().max().item()
     report(f'wino_cifar_forward_B{B}_vs_direct', err)

@@ -78,7 +78,7 @@ def run(name, iters, split, tile=0, ksplit=0):
         d.w_split, d.w_split_kind = ws.data_ptr(), kind
     if tile == 21:  # the Winograd F(2,3) kernel (conv_wino.hip)
         ww = dmhip.pack_conv_weight_wino(wp, Cin)
-        d.w_wino = ww.data_ptr()
+        d.w_wino = ww.data_ptr()  # (no shortcut segment here: the fold does not apply)
     if ksplit > 1:
         kpart = torch.empty((ksplit, B * Ho * Ho, Cout), device=dev)
         d.ksplit, d.kpart = ksplit, kpart.data_ptr()

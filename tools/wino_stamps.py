@@ -25,22 +25,30 @@ def main():
     dmhip.load()
     conv_bench.run(args.shape, 5, 'fp16x2', 21)
     B, Cin, Cout, H, pro, up = conv_bench.SHAPES[args.shape]
-    nblk = (B * H * H // 128) * (Cout // 128)
-    buf = np.zeros((nblk, 8), dtype=np.uint64)
+    tpi = (H * H // 128) * (Cout // 128)
+    parts = next((p for p in range(1, tpi + 1) if tpi % p == 0 and B * p >= 256), tpi)
+    nblk = B * parts
+    buf = np.zeros((nblk, 16), dtype=np.uint64)
     L = dmhip.load()
     L.dm_debug_wino_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
     assert L.dm_debug_wino_stamps(buf.ctypes.data, nblk) == 0
     s = buf.astype(np.int64)
-    phases = (('prologue', s[:, 1] - s[:, 0]), ('main loop', s[:, 2] - s[:, 1]), ('epilogue', s[:, 3] - s[:, 2]))
+    ntile = np.maximum(s[:, 4], 1)
+    pro = s[:, 1] - s[:, 0]
+    loop = s[:, 2]
     tot = s[:, 3] - s[:, 0]
+    rest = tot - pro - loop
     rt0, rt1 = s[:, 5], s[:, 6]
     wall_us = (rt1.max() - rt0.min()) / 100.0
     clk = tot / np.maximum(rt1 - rt0, 1) * 100e6 / 1e9
-    print(f'{args.shape} wino: {nblk} blocks, Cin {Cin} ({Cin // 32} chunks), kernel wall (stamps) {wall_us:.1f} us')
-    for name, v in phases + (('block total', tot), ):
-        print(f'  {name:12s} cycles mean {v.mean():10.0f}  p10 {np.percentile(v, 10):10.0f}  '
-              f'p90 {np.percentile(v, 90):10.0f}  share {v.mean() / tot.mean():.3f}')
-    print(f'  main loop cycles per chunk {(s[:, 2] - s[:, 1]).mean() / (Cin // 32):.0f} '
+    print(f'{args.shape} wino: {nblk} persistent blocks x {ntile.mean():.1f} tiles, Cin {Cin} ({Cin // 32} chunks), '
+          f'kernel wall (stamps) {wall_us:.1f} us')
+    for name, v in (('first prologue', pro), ('main loops', loop), ('epilogues + next prologues', rest),
+                    ('  E writes + barrier', s[:, 8]), ('  outputs + GroupNorm', s[:, 9]), ('  next prologues', s[:, 10]),
+                    ('block total', tot)):
+        print(f'  {name:28s} cycles mean {v.mean():10.0f}  per tile {(v / ntile).mean():9.0f}  '
+              f'share {v.mean() / tot.mean():.3f}')
+    print(f'  main loop cycles per chunk {(loop / ntile).mean() / (Cin // 32):.0f} '
           f'(MFMA floor 4608 per SIMD: 2 waves x 144 x 16)')
     print(f'  block wall us mean {((rt1 - rt0) / 100.0).mean():.2f}, clock GHz mean {clk.mean():.3f}')
 
