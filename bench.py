@@ -69,28 +69,29 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(label, workload='c3'):
+def pmc_traffic(label, workload='c3', build=None, launches_per_step=None, root=ROOT):
     """HBM bytes per launch of `label` from the newest committed PMC summary of this workload
     (profiles/rNN_vM_pmc.json, FETCH_SIZE x2 + WRITE_SIZE passes of this bench, tools/gpu_profile.sh;
-    summaries without a "workload" field are of the default c3 run)."""
+    summaries without a "workload" field are of the default c3 run) -- only from a summary of the SAME library
+    build (its "build" = dm_build_info() of this run) in which `label` ran as many launches per denoising step
+    as in this run; none such: (None, None), and the roofline's traffic is null."""
     import glob
     import re
 
     def order(path):
         m = re.search(r'r(\d+)_v(\d+)(?:_c\d)?_pmc\.json$', path)
         return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
-    files = sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*_v*_pmc.json')), key=order)
+    files = sorted(glob.glob(os.path.join(root, 'profiles', 'r*_v*_pmc.json')), key=order)
     for path in reversed(files):
         with open(path) as f:
             summary = json.load(f)
-        if summary.get('workload', 'c3') != workload:
+        if summary.get('workload', 'c3') != workload or build is None or summary.get('build') != build:
             continue
-        kernels = summary.get('kernels', {})
-        k = kernels.get(label)
-        if k is None and label.endswith('>'):  # family label with fewer template arguments than the trace's
-            k = next((v for n, v in kernels.items() if n.startswith(label[:-1] + ',')), None)
-        if k and k.get('hbm_bytes_per_launch'):
-            return float(k['hbm_bytes_per_launch']), os.path.relpath(path, ROOT)
+        k = summary.get('kernels', {}).get(label)
+        if not k or not k.get('hbm_bytes_per_launch') or launches_per_step is None or \
+                k.get('launches_per_step') is None or abs(k['launches_per_step'] - launches_per_step) > 1e-6:
+            continue
+        return float(k['hbm_bytes_per_launch']), os.path.relpath(path, root)
     return None, None
 
 
@@ -189,8 +190,12 @@ def cpu_baseline_cfg(name, model_sd, arch, batch, n_steps, guidance_scale, timed
                        f'{os.cpu_count()} logical CPUs on the host); {dt:.2f} s per step, extrapolated x{n_steps}')
 
 
-def roofline(prof, workload='c3'):
-    """Roofline of the dominant kernel family (most GPU time in the timed region)."""
+WINO_PRODUCTS = 2.0 / 3.0   # conv_wino_kernel: F(2,3) issues 12 K-rows per output pair where the direct conv issues 18
+
+
+def roofline(prof, workload='c3', build=None, launches_per_step=None):
+    """Roofline of the dominant kernel family (most GPU time in the timed region). launches_per_step: label ->
+    launches per denoising step in this run (pmc_traffic's match key)."""
     fam = {}
     for op in prof:
         f = fam.setdefault(op['label'], dict(flops=0.0, bytes=0.0, ms=0.0, launches=0))
@@ -208,25 +213,36 @@ def roofline(prof, workload='c3'):
         np_ = int(dom_name.rstrip('>').split(',')[-1]) if split else 0
         if dom_name.startswith('gemm_kernel') and dom_name.endswith(',true>'):   # <..., B_KN, SPLIT>: fp16x2
             split, np_ = True, 2
-        if dom_name.startswith('conv_k32_kernel') or dom_name.startswith('linear_k32_kernel'):  # fp16x2 only
-            split, np_ = True, 2
+        if dom_name.startswith(('conv_k32_kernel', 'conv_k32s_kernel', 'linear_k32_kernel', 'conv_wino_kernel')):
+            split, np_ = True, 2   # fp16x2 only
+        wino = dom_name.startswith('conv_wino_kernel')
         prods = SPLIT_PRODUCTS.get(np_, 0)
-        peak = round(BF16_PEAK_TFLOPS / prods, 1) if split else FP32_PEAK_TFLOPS
+        # FLOPs are the direct convolution's (2 M N K) for every conv kernel; the Winograd kernel issues WINO_PRODUCTS
+        # of its products, so its peak in those FLOPs is the issue peak / WINO_PRODUCTS
+        peak = round(BF16_PEAK_TFLOPS / prods / (WINO_PRODUCTS if wino else 1.0), 1) if split else FP32_PEAK_TFLOPS
         roof = dict(bound='mfma', achieved=round(achieved, 2), peak=peak, unit='TFLOP/s',
                     frac=round(achieved / peak, 4), traffic=None)
         if split:
             kind = {2: 'fp16x2', 3: 'bf16x3'}[np_]
+            issued = achieved * prods * (WINO_PRODUCTS if wino else 1.0)
             roof['peak_basis'] = (f'fp32-equivalent: dense 16-bit MFMA {BF16_PEAK_TFLOPS:.0f} TF / {prods} '
-                                  f'piece products per fp32 product ({kind}); issued 16-bit MFMA rate '
-                                  f'{achieved * prods:.1f} TF; vs the fp32 MFMA peak '
-                                  f'{achieved / FP32_PEAK_TFLOPS:.3f}')
+                                  f'piece products per fp32 product ({kind})' +
+                                  (' / (2/3): achieved and peak in direct-convolution FLOPs (2 M N 9 Cin), of which '
+                                   'the Winograd F(2,3) kernel issues 2/3 as products (12 K-rows per output pixel pair '
+                                   'where the direct conv takes 18; its ResBlock-shortcut variants issue their 1x1 '
+                                   'segment at the direct count, so this peak is an upper bound for those)'
+                                   if wino else '') +
+                                  f'; issued 16-bit MFMA rate {issued:.1f} TF of {BF16_PEAK_TFLOPS:.0f}; vs the fp32 '
+                                  f'MFMA peak {achieved / FP32_PEAK_TFLOPS:.3f}')
     else:
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
         roof = dict(bound='hbm', achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit='GB/s',
                     frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None)
-    traffic, traffic_src = pmc_traffic(dom_name, workload)
+    lps = (launches_per_step or {}).get(dom_name)
+    traffic, traffic_src = pmc_traffic(dom_name, workload, build, lps)
     roof.update(traffic=traffic, traffic_source=traffic_src, algorithmic_bytes_per_launch=bytes_per_launch,
-                kernel=dom_name, avg_launch_ms=round(avg_ms, 4), launches=dom['launches'],
+                kernel=dom_name, avg_launch_ms=round(avg_ms, 4), launches=dom['launches'], launches_per_step=lps,
+                build=build,
                 algorithmic_per_launch=flops_per_launch if flops_per_launch > 0 else bytes_per_launch)
     total_gpu_ms = sum(f['ms'] for f in fam.values())
     total_flops = sum(f['flops'] for f in fam.values())
@@ -521,9 +537,12 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = tt.item()
     prof, kernel_s, wbytes_t, wsbytes_t = [], 0.0, 0, 0
+    lps = {}   # launches per denoising step of each kernel label: its ops per forward x forwards per step
     for h, abi, fwd_per_fold in wl['handles']:
         p = dmhip.unet_profile_read(h, abi=abi)
         prof += p
+        for op in p:
+            lps[op['label']] = lps.get(op['label'], 0.0) + fwd_per_fold / max(1, wl['denoise_steps'])
         observed = max((op['launches'] for op in p), default=0)   # forwards of this handle that ran with events
         if observed:
             kernel_s += sum(op['ms_total'] for op in p) * 1e-3 * fwd_per_fold * args.steps / observed
@@ -536,7 +555,7 @@ def main():
 
     roof, total_gpu_ms, total_flops, fam = None, 0.0, 0.0, {}
     if not args.no_profile and prof:
-        roof, total_gpu_ms, total_flops, fam = roofline(prof, args.workload)
+        roof, total_gpu_ms, total_flops, fam = roofline(prof, args.workload, None if stub else dmhip.build_info(), lps)
 
     if rank == 0:
         images = world * B * args.steps

@@ -23,10 +23,29 @@ bool g_launch_log_on = false;
 std::string g_launch_log;
 }  // namespace
 const Toggles& toggles() { return g_toggles; }
+// every environment switch of the library, read here and nowhere else (DESIGN.md §6 toggle table)
 void refresh_toggles() {
   Toggles t;
+  if (const char* m = std::getenv("DM_CONV_MATH")) {
+    const std::string v(m);
+    t.conv_math = v == "fp32" ? 0 : v == "bf16x3" ? 3 : 2;
+  }
+  t.range_check = !env_is("DM_RANGE_CHECK", '0');
+  t.graph = std::getenv("DM_NO_GRAPH") == nullptr;
   t.wino = !env_is("DM_CONV_WINO", '0');
   t.k32s_w4 = env_is("DM_K32S_W4", '1');
+  t.k32_small = !env_is("DM_CONV_K32S", '0');
+  t.k32_s2 = !env_is("DM_CONV_K32S2", '0');
+  t.k32_t2d = !env_is("DM_CONV_K32T2", '0');
+  t.k32_8x = !env_is("DM_K32_8X", '0');
+  t.gn_fusion = !env_is("DM_GN_FUSION", '0');
+  if (const char* e = std::getenv("DM_ATTN")) {
+    const std::string v(e);
+    t.attn = v == "3" ? 3 : v == "0" || v == "presplit" ? 0 : v == "noproj" ? kAttnNoProj : v == "fused" ? kAttnFused
+           : v == "unfused" ? kAttnUnfused : 4;
+  }
+  t.attn_gn_launch = env_is("DM_ATTN_GNFIN", '1');
+  t.dit_presplit = !env_is("DM_DIT_PRESPLIT", '0');
   g_toggles = t;
 }
 void note_launch(const char* name) {

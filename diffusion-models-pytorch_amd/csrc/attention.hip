@@ -410,10 +410,7 @@ __device__ __forceinline__ void attn_proj(const ConvArgs& c, f16v (&oacc)[2][2],
 // 125.6 to 110.3 us but measured 1.6 % slower end to end -- every other kernel of the forward then ran at
 // a lower clock -- so the [token][d] / [d][token] planes stay.) 64 query rows per block (75 KB of LDS for
 // the S / P rows: two blocks per CU). Same MFMA sequence as the unfused GEMMs.
-// FRAG: k and v^T are fragment images (frag_off; the qkv projection's ap_frag epilogue): every k / v operand
-// fragment is one contiguous 1-KiB wave instruction instead of 32 rows x 32 B (32 cache lines touched per
-// instruction, each line four times over the 16-deep slices).
-template <int DH, bool FRAG>
+template <int DH>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) attn_presplit_kernel(AttnArgs a) {
   static_assert(DH == 64 || DH == 256, "head dims 64 / 256");
   constexpr int QT = 64, NS = DH / 16, RD = 6;
@@ -445,8 +442,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 #pragma unroll
       for (int q = 0; q < 2; ++q)
         rb[slot][i][q] =
-            FRAG ? *reinterpret_cast<const f16x8*>(K + frag_off(wave * 64 + i * 32, 16 * s, kAL) + q * 512 + lane * 8)
-                 : *reinterpret_cast<const f16x8*>(K + q * plane + (size_t)(wave * 64 + i * 32 + lr) * DH + 16 * s + 8 * lh);
+            *reinterpret_cast<const f16x8*>(K + q * plane + (size_t)(wave * 64 + i * 32 + lr) * DH + 16 * s + 8 * lh);
   };
 #pragma unroll
   for (int s = 0; s < RD; ++s) load_k(min(s, NS - 1), s);
@@ -557,8 +553,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 #pragma unroll
       for (int q = 0; q < 2; ++q)
         rv[slot][j][q] =
-            FRAG ? *reinterpret_cast<const f16x8*>(V + frag_off(ocol0 + j * 32, 16 * s, DH) + q * 512 + lane * 8)
-                 : *reinterpret_cast<const f16x8*>(V + q * plane + (size_t)(ocol0 + j * 32 + lr) * kAL + 16 * s + 8 * lh);
+            *reinterpret_cast<const f16x8*>(V + q * plane + (size_t)(ocol0 + j * 32 + lr) * kAL + 16 * s + 8 * lh);
   };
   f16v oacc[TM][TN];
 #pragma unroll
@@ -957,14 +952,10 @@ int attn_fused(const AttnArgs& args, hipStream_t st) {
   if (a.pq) {
     DM_REQUIRE(a.pk && a.pv, "fused attention: all three operand planes");
     const dim3 grid(a.B * a.heads * (kAL / 64));
-    if (a.Dh == 256 && a.frag)
-      hipLaunchKernelGGL((attn_presplit_kernel<256, true>), grid, dim3(256), 0, st, a);
-    else if (a.Dh == 256)
-      hipLaunchKernelGGL((attn_presplit_kernel<256, false>), grid, dim3(256), 0, st, a);
-    else if (a.frag)
-      hipLaunchKernelGGL((attn_presplit_kernel<64, true>), grid, dim3(256), 0, st, a);
+    if (a.Dh == 256)
+      hipLaunchKernelGGL((attn_presplit_kernel<256>), grid, dim3(256), 0, st, a);
     else
-      hipLaunchKernelGGL((attn_presplit_kernel<64, false>), grid, dim3(256), 0, st, a);
+      hipLaunchKernelGGL((attn_presplit_kernel<64>), grid, dim3(256), 0, st, a);
     DM_LAUNCH_CHECK();
     return DM_OK;
   }

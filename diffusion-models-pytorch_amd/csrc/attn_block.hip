@@ -8,13 +8,10 @@
 //   y_i = x_i + sum_j P_ij g_j,   g_j = Wg xn_j + cb,   Wg = Wp Wv, cb = Wp bv + bp   (sum_j P_ij = 1)
 //
 // The folded matrices are products of the block's own weights, formed once in float64 (attn_fold_kernel)
-// and rounded to fp32; g is a plain static-weight GEMM (linear_k32 with the GroupNorm prologue, writing
-// g^T as the fp16x2 v-plane [B][2][C][L]); this kernel does T, S, softmax, P g and the residual for 128
-// query tokens of one image. Per image that is 4 GEMMs of 256^3 (T, S, g, Pg) instead of the reference's
-// 6 (q, k, v, S, Pv, proj): 134 instead of 201 MFLOP, no q / k / v planes in HBM.
+// and rounded to fp32. (Round 4's first form computed g with a separate static-weight GEMM into an fp16x2 plane;
+// variant 3 below moved the projection after the key pass -- the values are xn itself -- and variant 4, the
+// default, runs variant 3's arithmetic on 8 waves; the g-plane form was removed in round 5.)
 //
-// Work-group = (image, 128 query tokens), 4 waves of 32 queries, one wave per SIMD (up to 512 VGPR+AGPR:
-// the wave keeps T's split pieces (128 registers) next to S (128), then P's pieces next to O (128 each)).
 // Every contraction is C^T = A B^T-style with the 256-row operand (At rows c', the keys' xn rows, g^T rows
 // d) staged per 32-deep k-step through LDS in the fragment-image layout of split_conv_weights (shared by
 // the four waves, double buffered, loads two k-steps ahead in registers), and the wave's 32 query columns
@@ -159,326 +156,6 @@ __global__ void attn_fold_kernel(const float* __restrict__ wqkv, const float* __
 }
 
 namespace {
-
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) attn_block_kernel(AttnBlockArgs a) {
-  // LDS: two staged k-step images (64 KB) during the contractions; the epilogue's O rows (130 KB) after
-  __shared__ __attribute__((aligned(16))) float lds[kBQ * kOP];
-  __shared__ __attribute__((aligned(16))) float tab[2][kBC];   // GroupNorm scale / shift of the image
-  static_assert(2 * kStepH * 2 <= kBQ * kOP * 4, "two k-step images fit the epilogue region");
-  _Float16* stg = reinterpret_cast<_Float16*>(lds);
-  AB_RSTAMP(8);
-  AB_STAMP(0);
-#ifdef DM_K32_STAMPS
-  if (threadIdx.x == 0 && blockIdx.x < 4096) g_ab_stamps[blockIdx.x][7] = __smid();
-#endif
-
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int l16 = lane & 15, q = lane >> 4;
-  const int bid = xcd_remap_p(blockIdx.x, gridDim.x);
-  const int b = bid >> 1, qh = bid & 1;
-  const float* xb = a.x + (size_t)b * kBL * a.x_pitch;
-  const int qrow0 = qh * kBQ + wave * 32;          // this wave's first query token
-  const float xs = ldexpf(1.f, a.ex);
-  bool bad = false;
-
-  for (int i = t; i < kBC; i += 256) {
-    tab[0][i] = a.gsc[(size_t)b * kBC + i];
-    tab[1][i] = a.gsh[(size_t)b * kBC + i];
-  }
-
-  // ------------------------------------------------------------------ staging (8 x 16 B per thread per k-step)
-  // A k-step image is 8 slots of one 16-B load + LDS store per thread; during k-step kk the slots of k-step
-  // kk + 2 are loaded (after tiles 0 .. 7) and those of k-step kk + 1 stored (after tiles 8 .. 15).
-  f4 rg[2][8];
-  // At image rows (a verbatim copy of the k-step's two 16-slices of split_conv_weights' image)
-  auto load_at = [&](int kk, int s, f4& r) {
-    r = reinterpret_cast<const f4*>(a.at_img + (size_t)kk * kStepH)[t + 256 * s];
-  };
-  auto store_at = [&](int buf, int s, const f4& r) { reinterpret_cast<f4*>(stg + buf * kStepH)[t + 256 * s] = r; };
-  // the keys' x rows, channels 32 ks + 4 u .. + 3 (u = g + 4 hi): lane group g, lanes 8 hi .. + 7 hold 8
-  // consecutive keys; slot s of this wave covers keys 64 wave + 8 s ..
-  const int kg = lane >> 4, khi = (lane >> 3) & 1, kkey = lane & 7;
-  const int ku = kg + 4 * khi;
-  auto load_keys = [&](int ks, int s, f4& r) {
-    r = *reinterpret_cast<const f4*>(xb + (size_t)(64 * wave + 8 * s + kkey) * a.x_pitch + 32 * ks + 4 * ku);
-  };
-  auto store_keys = [&](int ks, int buf, int s, const f4& r) {
-    const int c = 32 * ks + 4 * ku;
-    const f4 sc = *reinterpret_cast<const f4*>(&tab[0][c]), sh = *reinterpret_cast<const f4*>(&tab[1][c]);
-    f4 v = r;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = (v[e] * sc[e] + sh[e]) * xs;
-    bad |= fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))) > 65504.f;
-    f16x4 hi, lo;
-    split4(v, hi, lo);
-    _Float16* dst = stg + buf * kStepH + img_off(64 * wave + 8 * s + kkey, kg, 0) + 4 * khi;
-    *reinterpret_cast<f16x4*>(dst) = hi;
-    *reinterpret_cast<f16x4*>(dst + 512) = lo;
-  };
-  // g^T rows d (the v-plane [2][C][L] of this image), keys 32 ks + 8 u' .. + 7 (u' = 2 hi + g1, piece g0)
-  const _Float16* gb = a.g_plane + (size_t)b * 2 * kBC * kBL;
-  const int gu = 2 * khi + (kg & 1), gp = kg >> 1;
-  auto load_g = [&](int ks, int s, f4& r) {
-    r = *reinterpret_cast<const f4*>(gb + ((size_t)gp * kBC + 64 * wave + 8 * s + kkey) * kBL + 32 * ks + 8 * gu);
-  };
-  auto store_g = [&](int buf, int s, const f4& r) {
-    // keys 8 u' .. + 3 -> lane group 2 (u' & 1), e0 = 4 (u' >> 1); keys 8 u' + 4 .. + 7 -> lane group + 1
-    _Float16* img = stg + buf * kStepH;
-    const int q0 = 2 * (gu & 1), e0 = 4 * (gu >> 1), d = 64 * wave + 8 * s + kkey;
-    *reinterpret_cast<float2*>(img + img_off(d, q0, gp) + e0) = make_float2(r[0], r[1]);
-    *reinterpret_cast<float2*>(img + img_off(d, q0 + 1, gp) + e0) = make_float2(r[2], r[3]);
-  };
-
-  fq acc[16][2];
-  auto zero_acc = [&]() {
-#pragma unroll
-    for (int i = 0; i < 16; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = fq{0.f, 0.f, 0.f, 0.f};
-  };
-
-  // ------------------------------------------------------------------ 1. T^T = At xn^T (+ w)
-  // B operand: the wave's queries (lane l16 of tile qt), channels 32 kk + 8 q .. + 7, GroupNorm'd and split
-  f4 rx[2][2][2];   // [set][qt][half]
-  auto load_xq = [&](int kk, f4 (&r)[2][2]) {
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      const float* p = xb + (size_t)(qrow0 + 16 * qt + l16) * a.x_pitch + 32 * kk + 8 * q;
-      r[qt][0] = *reinterpret_cast<const f4*>(p);
-      r[qt][1] = *reinterpret_cast<const f4*>(p + 4);
-    }
-  };
-  auto xq_frag = [&](int kk, const f4 (&r)[2][2], f16x8 (&bf)[2][2]) {
-    const int c = 32 * kk + 8 * q;
-    const f4 s0 = *reinterpret_cast<const f4*>(&tab[0][c]), s1 = *reinterpret_cast<const f4*>(&tab[0][c + 4]);
-    const f4 h0 = *reinterpret_cast<const f4*>(&tab[1][c]), h1 = *reinterpret_cast<const f4*>(&tab[1][c + 4]);
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      float v[8];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] = (r[qt][0][e] * s0[e] + h0[e]) * xs;
-        v[4 + e] = (r[qt][1][e] * s1[e] + h1[e]) * xs;
-      }
-      float m = 0.f;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(v[e]));
-      bad |= m > 65504.f;
-      split8(v, bf[qt][0], bf[qt][1]);
-    }
-  };
-
-  zero_acc();
-#pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    load_at(0, u, rg[0][u]);
-    load_at(1, u, rg[1][u]);
-  }
-  load_xq(0, rx[0]);
-  load_xq(1, rx[1]);
-#pragma unroll
-  for (int u = 0; u < 8; ++u) store_at(0, u, rg[0][u]);
-  __syncthreads();   // tab and the first image
-#pragma unroll
-  for (int kk = 0; kk < 8; ++kk) {
-    f16x8 bf[2][2];
-    xq_frag(kk, rx[kk & 1], bf);
-    if (kk + 2 < 8 && DM_AB_ABL != 1) load_xq(kk + 2, rx[kk & 1]);
-    kstep(stg + (kk & 1) * kStepH, l16, q, bf, acc, [&](int tt) {
-      if (tt < 8) {
-        if (kk + 2 < 8 && DM_AB_ABL != 1) load_at(kk + 2, tt, rg[kk & 1][tt]);
-      } else if (kk + 1 < 8) {
-        store_at((kk + 1) & 1, tt - 8, rg[(kk + 1) & 1][tt - 8]);
-      }
-    });
-    __syncthreads();
-  }
-  AB_STAMP(1);
-  // keys' rows for the S contraction: first two k-steps in flight during the T epilogue
-#pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    load_keys(0, u, rg[0][u]);
-    load_keys(1, u, rg[1][u]);
-  }
-
-  // T = acc * rowscale * 2^-ex + w; per query the exponent eT with max |T| 2^eT in [2^13, 2^14)
-  f16x8 tp[8][2][2];   // [k-step][qt][piece]: T's split pieces as the S contraction's B operand
-  float tun[2];        // 2^-(ex + eT) per query tile
-  {
-    const float xun = ldexpf(1.f, -a.ex);
-    float mx[2] = {0.f, 0.f};
-#pragma unroll
-    for (int ct = 0; ct < 16; ++ct) {
-      const f4 rs = *reinterpret_cast<const f4*>(a.at_rowscale + 16 * ct + 4 * q);
-      const f4 wv = *reinterpret_cast<const f4*>(a.w + 16 * ct + 4 * q);
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float v = acc[ct][qt][r] * (rs[r] * xun) + wv[r];
-          acc[ct][qt][r] = v;
-          mx[qt] = fmaxf(mx[qt], fabsf(v));
-        }
-    }
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      float m = fmaxf(mx[qt], __shfl_xor(mx[qt], 16));
-      m = fmaxf(m, __shfl_xor(m, 32));
-      int E = 0;
-      (void)frexpf(m, &E);
-      const int eT = m > 0.f ? 14 - E : 0;
-      const float sc = ldexpf(1.f, eT);
-      tun[qt] = ldexpf(1.f, -(a.ex + eT));
-#pragma unroll
-      for (int ks = 0; ks < 8; ++ks) {
-        float v[8];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          v[e] = acc[2 * ks][qt][e] * sc;
-          v[4 + e] = acc[2 * ks + 1][qt][e] * sc;
-        }
-        split8(v, tp[ks][qt][0], tp[ks][qt][1]);
-      }
-    }
-  }
-
-  AB_STAMP(2);
-  // ------------------------------------------------------------------ 2. S^T = xn_keys T^T
-#pragma unroll
-  for (int u = 0; u < 8; ++u) store_keys(0, 0, u, rg[0][u]);
-  __syncthreads();
-  zero_acc();
-#pragma unroll
-  for (int ks = 0; ks < 8; ++ks) {
-    kstep(stg + (ks & 1) * kStepH, l16, q, tp[ks], acc, [&](int tt) {
-      if (tt < 8) {
-        if (ks + 2 < 8 && DM_AB_ABL != 1) load_keys(ks + 2, tt, rg[ks & 1][tt]);
-      } else if (ks + 1 < 8) {
-        store_keys(ks + 1, (ks + 1) & 1, tt - 8, rg[(ks + 1) & 1][tt - 8]);
-      }
-    });
-    __syncthreads();
-  }
-  AB_STAMP(3);
-#pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    load_g(0, u, rg[0][u]);
-    load_g(1, u, rg[1][u]);
-  }
-
-  // ------------------------------------------------------------------ 3. softmax over the keys (per query lane)
-  // S = acc 2^-(ex + eT); p = exp2(S log2 e - max) on the hardware exp2 (scale folded into one FMA), P = p / sum
-  f16x8 pp[8][2][2];   // [k-step][qt][piece]: P x 2^14 as the Pg contraction's B operand
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const float sl2 = tun[qt] * 1.4426950408889634f;
-    float m = -INFINITY;
-#pragma unroll
-    for (int kt = 0; kt < 16; ++kt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) m = fmaxf(m, acc[kt][qt][r]);
-    m = fmaxf(m, __shfl_xor(m, 16));
-    m = fmaxf(m, __shfl_xor(m, 32));
-    const float mb = -m * sl2;
-    float sum = 0.f;
-#pragma unroll
-    for (int kt = 0; kt < 16; ++kt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(acc[kt][qt][r], sl2, mb));
-        acc[kt][qt][r] = e;
-        sum += e;
-      }
-    sum += __shfl_xor(sum, 16);
-    sum += __shfl_xor(sum, 32);
-    const float inv = 16384.f / sum;
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-      float v[8];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] = acc[2 * ks][qt][e] * inv;
-        v[4 + e] = acc[2 * ks + 1][qt][e] * inv;
-      }
-      split8(v, pp[ks][qt][0], pp[ks][qt][1]);
-    }
-  }
-
-  AB_STAMP(4);
-  // ------------------------------------------------------------------ 4. O^T = g^T P^T
-#pragma unroll
-  for (int u = 0; u < 8; ++u) store_g(0, u, rg[0][u]);
-  __syncthreads();
-  zero_acc();
-  // epilogue slice of this wave: 64-row chunk ch, 128-column half chalf; lane = 4 channels of rows 2 i + rsub.
-  // The residual rows are loaded during the last two k-steps (slots free there) and right after the loop.
-  const int ch = wave >> 1, chalf = wave & 1;
-  const int c4 = lane & 31, rsub = lane >> 5;
-  const int col = 128 * chalf + 4 * c4;
-  const int tok0 = qh * kBQ + 64 * ch;
-  auto load_res = [&](int i, f4& r) {
-    r = DM_AB_ABL == 2 ? f4{0.f, 0.f, 0.f, 0.f}
-                       : *reinterpret_cast<const f4*>(xb + (size_t)(tok0 + 2 * i + rsub) * a.x_pitch + col);
-  };
-#pragma unroll
-  for (int ks = 0; ks < 8; ++ks) {
-    kstep(stg + (ks & 1) * kStepH, l16, q, pp[ks], acc, [&](int tt) {
-      if (tt < 8) {
-        if (ks + 2 < 8) {
-          if (DM_AB_ABL != 1) load_g(ks + 2, tt, rg[ks & 1][tt]);
-        } else {
-          load_res(8 * (ks - 6) + tt, rg[ks & 1][tt]);   // residual rows 0 .. 15
-        }
-      } else if (ks + 1 < 8) {
-        store_g((ks + 1) & 1, tt - 8, rg[(ks + 1) & 1][tt - 8]);
-      }
-    });
-    __syncthreads();
-  }
-  f4 xr2[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) load_res(16 + i, xr2[i]);
-  if (bad && a.range_flag) *a.range_flag = 1;
-  AB_STAMP(5);
-
-  // ------------------------------------------------------------------ 5. y = x + O, GroupNorm statistics
-  // O rows to LDS ([128 queries][C] fp32): lane (l16, q) holds d = 16 dt + 4 q .. + 3 of query 16 qt + l16
-  const float oun = ldexpf(1.f, -(a.eg + 14));
-#pragma unroll
-  for (int dt = 0; dt < 16; ++dt)
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt)
-      *reinterpret_cast<fq*>(lds + (wave * 32 + 16 * qt + l16) * kOP + 16 * dt + 4 * q) = acc[dt][qt] * oun;
-  __syncthreads();
-  double gs[4] = {0.0, 0.0, 0.0, 0.0}, gq[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int i = 0; i < 32; ++i) {
-    const int tok = tok0 + 2 * i + rsub;
-    const f4 o = *reinterpret_cast<const f4*>(lds + (64 * ch + 2 * i + rsub) * kOP + col);
-    const f4 xr = i < 8 ? rg[0][i & 7] : i < 16 ? rg[1][i & 7] : xr2[i & 15];
-    const f4 yv = xr + o;
-    *reinterpret_cast<f4*>(a.y + ((size_t)b * kBL + tok) * a.y_pitch + col) = yv;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      gs[e] += (double)yv[e];
-      gq[e] += (double)yv[e] * yv[e];
-    }
-  }
-  if (a.gn_part) {
-    double s = gs[0] + gs[1] + gs[2] + gs[3], qq = gq[0] + gq[1] + gq[2] + gq[3];
-    s += __shfl_xor(s, 32);
-    qq += __shfl_xor(qq, 32);
-    const int cpg = kBC / a.gn_G;   // 4 .. 32 channels: cpg / 4 lanes
-    for (int o = 1; o < cpg / 4; o <<= 1) {
-      s += __shfl_xor(s, o);
-      qq += __shfl_xor(qq, o);
-    }
-    if (rsub == 0 && (c4 % (cpg / 4)) == 0)
-      a.gn_part[((size_t)b * (kBL / 64) + (tok0 >> 6)) * a.gn_G + col / cpg] = make_double2(s, qq);
-  }
-  AB_STAMP(6);
-  AB_RSTAMP(9);
-}
 
 // ======================================================================================================
 // Variant 3 (default): no g GEMM. The values are xn itself and the folded projection comes after:
@@ -879,12 +556,11 @@ __device__ __forceinline__ void kstep1(const _Float16* img, int l16, int q, cons
   }
 }
 
-// NWV waves of 16 queries per work-group: 8 (variant 4: 128 queries, one work-group per CU) or 4 (variant 5:
-// 64 queries, two independent work-groups per CU -- the two waves of a SIMD no longer meet at the same barriers
-// -- at twice the L2 -> LDS staging of the weight images per query).
-// OPT (A/B builds of the same arithmetic, DM_ATTN_OPT): bit 1 reads the S A-operands one key step ahead. (A
-// wave-uniform skip of the O rescale when no running maximum moved spills 572 B per lane here, as in variant 3.)
-template <int NWV, int OPT = 0>
+// NWV = 8 waves of 16 queries per work-group (variant 4: 128 queries, one work-group per CU; the 4-wave form on
+// 64-query work-groups and the software-pipelined / read-ahead key passes measured neutral or negative and were
+// removed in round 5). (A wave-uniform skip of the O rescale when no running maximum moved spills 572 B per lane
+// here, as in variant 3.)
+template <int NWV>
 __global__ void __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) attn_block4_kernel(AttnBlockArgs a) {
   constexpr int NT = NWV * 64, QB = 16 * NWV, NS = 2048 / NT;   // threads, queries, staging slots per thread
   // staging register sets: 2 (loads two k-steps / key chunks ahead) with 4 slots per thread, 1 (one ahead) with 8
@@ -1066,140 +742,21 @@ __global__ void __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2
   zero_acc();   // O^T accumulators
   float m_run = -INFINITY, l_run = 0.f;
   const float sl2 = tun * 1.4426950408889634f;
-  if constexpr ((OPT & 4) != 0) {
-    // Software-pipelined key pass (DM_ATTN_OPT=4): iteration kc computes S of chunk kc, then P V of chunk kc - 1
-    // with chunk kc's online softmax placed between its MFMAs, so the softmax's VALU / exp2 / cross-lane chain
-    // issues while the matrix pipe runs P V -- in the plain loop both waves of a SIMD leave the barrier together
-    // and both run their softmax with the pipe idle. Key chunks rotate over three LDS images (kc % 3: S reads
-    // kc, P V reads kc - 1, chunk kc + 1 is staged into the third), inside the epilogue region. Every
-    // accumulator sees the same operations in the same order as the plain loop (rescale by chunk j's correction
-    // just before P V of chunk j), so the results are bit-identical.
-    static_assert(3 * kKImg <= 2 * LDSF, "three key-chunk images fit the staging region");
-    auto s_chunk = [&](int kc, fq (&sacc)[2]) {
-      const _Float16* img = stg + (kc % 3) * kKImg;
-#pragma unroll
-      for (int ks = 0; ks < 8; ++ks) {
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt) {
-          const _Float16* pr = img + (16 * kt + l16) * kKP + 32 * ks + 8 * q;
-          f16x8 av[2];
-          av[0] = *reinterpret_cast<const f16x8*>(pr);
-          av[1] = *reinterpret_cast<const f16x8*>(pr + kKPiece);
-          mma3(av, tp[ks], sacc[kt]);
-        }
-        if (kc + RD < 8 && ks % SD == 0) load_k(kc + RD, ks / SD, rg[(kc + RD) % RD][ks / SD]);
-      }
-    };
-    auto softmax = [&](const fq (&sacc)[2], f16x8 (&pp)[2], float& corr) {
-      float mx = fmaxf(fmaxf(fmaxf(sacc[0][0], sacc[0][1]), fmaxf(sacc[0][2], sacc[0][3])),
-                       fmaxf(fmaxf(sacc[1][0], sacc[1][1]), fmaxf(sacc[1][2], sacc[1][3])));
-      mx = fmaxf(mx, __shfl_xor(mx, 16));
-      mx = fmaxf(mx, __shfl_xor(mx, 32));
-      const float m_new = fmaxf(m_run, mx * sl2);
-      corr = __builtin_amdgcn_exp2f(m_run - m_new);
-      m_run = m_new;
-      float ls = 0.f, v[8];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[0][e], sl2, -m_new));
-        v[4 + e] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[1][e], sl2, -m_new));
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        ls += v[e];
-        v[e] *= 16384.f;
-      }
-      l_run = l_run * corr + ls;
-      split8(v, pp[0], pp[1]);
-    };
-    // P V of chunk kc (its P pieces pp), with `mid(ot)` after each output tile's MFMAs
-    auto pv_chunk = [&](int kc, const f16x8 (&pp)[2], auto&& mid) {
-      const _Float16* pt = stg + (kc % 3) * kKImg + (4 * q + (l16 >> 2)) * kKP + 4 * (l16 & 3);
-#pragma unroll
-      for (int ot = 0; ot < 16; ++ot) {
-        f16x8 av[2];
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-          const f16x4_t lo4 = lds_tr16(pt + p * kKPiece + 16 * ot);
-          const f16x4_t hi4 = lds_tr16(pt + p * kKPiece + 16 * kKP + 16 * ot);
-          av[p] = f16x8{lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
-        }
-        mma3(av, pp, acc[ot]);
-        mid(ot);
-      }
-    };
-    f16x8 pprev[2];
-    float cprev = 1.f;
-#pragma unroll
-    for (int kc = 0; kc < 8; ++kc) {
-      fq sacc[2] = {fq{0.f, 0.f, 0.f, 0.f}, fq{0.f, 0.f, 0.f, 0.f}};
-      s_chunk(kc, sacc);
-      f16x8 pc[2];
-      float cc;
-      if (kc == 0) {
-        softmax(sacc, pc, cc);
-#pragma unroll
-        for (int u = 0; u < NS; ++u) store_k(1, u, rg[1 % RD][u]);
-      } else {
-        if (kc - 1 > 0) {
-#pragma unroll
-          for (int ot = 0; ot < 16; ++ot) acc[ot] *= cprev;
-        }
-        pv_chunk(kc - 1, pprev, [&](int ot) {
-          if (ot == 1) softmax(sacc, pc, cc);
-          if (ot >= 8 && ot % SD == 0 && kc + 1 < 8)
-            store_k((kc + 1) % 3, (ot - 8) / SD, rg[(kc + 1) % RD][(ot - 8) / SD]);
-        });
-      }
-      pprev[0] = pc[0];
-      pprev[1] = pc[1];
-      cprev = cc;
-      __syncthreads();
-    }
-#pragma unroll
-    for (int u = 0; u < NS; ++u) {
-      load_w(a.wg_img, 0, u, rg[0][u]);
-      if (RD == 2) load_w(a.wg_img, 1, u, rg[RD - 1][u]);
-    }
-#pragma unroll
-    for (int ot = 0; ot < 16; ++ot) acc[ot] *= cprev;
-    pv_chunk(7, pprev, [](int) {});
-  } else {
 #pragma unroll
   for (int kc = 0; kc < 8; ++kc) {
     const _Float16* img = stg + (kc & 1) * kKImg;
     fq sacc[2] = {fq{0.f, 0.f, 0.f, 0.f}, fq{0.f, 0.f, 0.f, 0.f}};
-    if constexpr ((OPT & 2) != 0) {
-      f16x8 sv[2][2][2];   // [buffer][kt][piece]
-      auto rd_s = [&](int ks, f16x8 (&dst)[2][2]) {
 #pragma unroll
-        for (int kt = 0; kt < 2; ++kt) {
-          const _Float16* pr = img + (16 * kt + l16) * kKP + 32 * ks + 8 * q;
-          dst[kt][0] = *reinterpret_cast<const f16x8*>(pr);
-          dst[kt][1] = *reinterpret_cast<const f16x8*>(pr + kKPiece);
-        }
-      };
-      rd_s(0, sv[0]);
+    for (int ks = 0; ks < 8; ++ks) {
 #pragma unroll
-      for (int ks = 0; ks < 8; ++ks) {
-        if (ks + 1 < 8) rd_s(ks + 1, sv[(ks + 1) & 1]);
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt) mma3(sv[ks & 1][kt], tp[ks], sacc[kt]);
-        if (kc + RD < 8 && ks % SD == 0) load_k(kc + RD, ks / SD, rg[(kc + RD) % RD][ks / SD]);
+      for (int kt = 0; kt < 2; ++kt) {
+        const _Float16* pr = img + (16 * kt + l16) * kKP + 32 * ks + 8 * q;
+        f16x8 av[2];
+        av[0] = *reinterpret_cast<const f16x8*>(pr);
+        av[1] = *reinterpret_cast<const f16x8*>(pr + kKPiece);
+        mma3(av, tp[ks], sacc[kt]);
       }
-    } else {
-#pragma unroll
-      for (int ks = 0; ks < 8; ++ks) {
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt) {
-          const _Float16* pr = img + (16 * kt + l16) * kKP + 32 * ks + 8 * q;
-          f16x8 av[2];
-          av[0] = *reinterpret_cast<const f16x8*>(pr);
-          av[1] = *reinterpret_cast<const f16x8*>(pr + kKPiece);
-          mma3(av, tp[ks], sacc[kt]);
-        }
-        if (kc + RD < 8 && ks % SD == 0) load_k(kc + RD, ks / SD, rg[(kc + RD) % RD][ks / SD]);
-      }
+      if (kc + RD < 8 && ks % SD == 0) load_k(kc + RD, ks / SD, rg[(kc + RD) % RD][ks / SD]);
     }
     f16x8 pp[2];
     {
@@ -1250,7 +807,7 @@ __global__ void __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2
     load_w(a.wg_img, 0, u, rg[0][u]);
     if (RD == 2) load_w(a.wg_img, 1, u, rg[RD - 1][u]);
   }
-  }
+  
   AB_STAMP(3);
   // O x 2^ex = acc / (2^14 l) (the staged keys carry xn x 2^ex), rows in storage order -> the projection's B
   f16x8 op[8][2];
@@ -1386,33 +943,24 @@ int attn_perm_cols(const float* wg, float* wgp, int C, hipStream_t st) {
 
 int attn_block(const AttnBlockArgs& a, hipStream_t st) {
   auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-  DM_REQUIRE(a.variant >= 2 && a.variant <= 5, "attention block: variant 2 .. 5");
+  DM_REQUIRE(a.variant == 3 || a.variant == 4, "attention block: variant 3 or 4");
   DM_REQUIRE(!a.gin_part || (a.variant >= 4 && a.gin_G > 0 && kBC % a.gin_G == 0 && a.gin_nchunk > 0),
-             "attention block: in-kernel GroupNorm finalize needs variant 4 / 5 and groups dividing 256 channels");
+             "attention block: in-kernel GroupNorm finalize needs variant 4 and groups dividing 256 channels");
   DM_REQUIRE(a.B > 0 && a.x && a.y && (a.gin_part || (a.gsc && a.gsh)) && a.at_img && a.at_rowscale && a.w &&
-                 (a.variant == 2 ? a.g_plane != nullptr : (a.wg_img && a.wg_rowscale && a.cb)),
+                 a.wg_img && a.wg_rowscale && a.cb,
              "attention block: null argument");
   DM_REQUIRE(a.x_pitch % 4 == 0 && a.y_pitch % 4 == 0 && al16(a.x) && al16(a.y) &&
                  (a.gin_part || (al16(a.gsc) && al16(a.gsh))) &&
                  al16(a.at_img) && al16(a.at_rowscale) && al16(a.w) &&
-                 (a.variant == 2 ? al16(a.g_plane) : (al16(a.wg_img) && al16(a.wg_rowscale) && al16(a.cb))),
+                 al16(a.wg_img) && al16(a.wg_rowscale) && al16(a.cb),
              "attention block: 16-byte aligned rows");
   DM_REQUIRE(!a.gn_part || (a.gn_G > 0 && kBC % a.gn_G == 0 && kBC / a.gn_G >= 4 && kBC / a.gn_G <= 32 &&
                             ((kBC / a.gn_G) & (kBC / a.gn_G - 1)) == 0),
              "attention block: GroupNorm statistics need groups of 4, 8, 16 or 32 channels");
-  if (a.variant == 5)
-    hipLaunchKernelGGL(attn_block4_kernel<4>, dim3(a.B * (kBL / 64)), dim3(256), 0, st, a);
-  else if (a.variant == 4) {
-    const int opt = std::getenv("DM_ATTN_OPT") ? std::atoi(std::getenv("DM_ATTN_OPT")) : 0;  // read per plan build
-    const dim3 grid(a.B * (kBL / 128));
-    if (opt == 2) hipLaunchKernelGGL((attn_block4_kernel<8, 2>), grid, dim3(512), 0, st, a);
-    else if (opt == 4) hipLaunchKernelGGL((attn_block4_kernel<8, 4>), grid, dim3(512), 0, st, a);
-    else hipLaunchKernelGGL((attn_block4_kernel<8, 0>), grid, dim3(512), 0, st, a);
-  }
-  else if (a.variant == 3)
-    hipLaunchKernelGGL(attn_block3_kernel, dim3(a.B * (kBL / kBQ)), dim3(256), 0, st, a);
+  if (a.variant == 4)
+    hipLaunchKernelGGL(attn_block4_kernel<8>, dim3(a.B * (kBL / 128)), dim3(512), 0, st, a);
   else
-    hipLaunchKernelGGL(attn_block_kernel, dim3(a.B * (kBL / kBQ)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(attn_block3_kernel, dim3(a.B * (kBL / kBQ)), dim3(256), 0, st, a);
   DM_LAUNCH_CHECK();
   return DM_OK;
 }

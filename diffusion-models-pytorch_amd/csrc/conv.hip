@@ -357,14 +357,14 @@ bool conv_can_emit_gn(const ConvArgs& a) {
   // of one parity's low-res pixels for the sub-pixel upsample)
   if (conv_k32_pick(a) == 10)
     return a.gn_G > 0 && a.Cout % a.gn_G == 0 && 32 % (a.Cout / a.gn_G) == 0 &&
-           (a.upsample != 2 || (!std::getenv("DM_GN_NO_SUB") && (a.Cout / a.gn_G) % 4 == 0));
+           (a.upsample != 2 || (toggles().gn_fusion && (a.Cout / a.gn_G) % 4 == 0));
   const int pick = conv_pick(a);
   if (pick != 3 && pick != 4 && pick != 6 && pick != 7 && pick != 8) return false;  // waves own whole 64-row chunks
   if (conv_k32_pick(a) && a.Cout % a.gn_G == 0 && a.Cout / a.gn_G > 32) return false;  // K32: groups within 32 columns
   // the K32 sub-pixel upsample (128-row tiles, 64-row waves of one parity): chunks of 64 low-res pixels
   if (a.upsample == 2) {
     const int v = conv_k32_pick(a);
-    return (v == 1 || v == 2) && !std::getenv("DM_GN_NO_SUB") && (a.Hin * a.Win) % 64 == 0 && a.gn_G > 0 &&
+    return (v == 1 || v == 2) && toggles().gn_fusion && (a.Hin * a.Win) % 64 == 0 && a.gn_G > 0 &&
            a.Cout % a.gn_G == 0 && 32 % (a.Cout / a.gn_G) == 0 && (a.Cout / a.gn_G) % 4 == 0;
   }
   if (a.upsample || (a.ksplit > 1)) return false;

@@ -126,10 +126,8 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
     bid -= par * per_par;
   }
   const int py = par >> 1, px = par & 1;
-  // tile order: N tiles fastest (the blocks of one M tile share its patch in L2), or with nslow all M tiles of
-  // an N tile first (concurrent blocks share that N tile's weights)
-  const int nM = ceil_div(M, BM);
-  const int mt = a.nslow ? bid % nM : bid / nN, nt = a.nslow ? bid / nM : bid - (bid / nN) * nN;
+  // tile order: N tiles fastest (the blocks of one M tile share its patch in L2; the N-slow order measured -0.6 %)
+  const int mt = bid / nN, nt = bid - (bid / nN) * nN;
   const int m0 = mt * BM, n0 = nt * BN;
   const int HWo = Ho * Wo;
   const int b0 = m0 / HWo;
@@ -1020,35 +1018,9 @@ int conv_k32_variant_ok(const ConvArgs& a, int v) {
 bool conv_k32_ok(const ConvArgs& a) { return conv_k32_variant_ok(a, 1) != 0; }
 
 // Which conv_k32 variant runs this conv, 0 = none. Forced by tile 10 / 11 (128-row tiles) and 12 / 13
-// (split-K 64-row tiles); otherwise it replaces conv_patch3's fp16x2 tiles for 3x3 stride-1 convs
-// unless DM_CONV_K32=0.
-bool conv_k32_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("DM_CONV_K32");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
-// The 512-thread wide-map tiles (variant 7) unless DM_CONV_K32W=0 (then variant 5, the 64-pixel segments)
-static bool conv_k32_wide_enabled() {
-  const char* e = std::getenv("DM_CONV_K32W");
-  return !(e && e[0] == '0');
-}
-
-// The big-table 128 x 128 tiles (variant 8) for convs whose GroupNorm tables exceed kTab (ADM's 8^2 / 16^2 levels:
-// 1024-2048 input channels) unless DM_CONV_K32B=0 (then conv_patch3)
-static bool conv_k32_bigtab_enabled() {
-  const char* e = std::getenv("DM_CONV_K32B");
-  return !(e && e[0] == '0');
-}
-
-// The 2-D tiles of wide maps (variant 10) unless DM_CONV_K32T2=0 (then variant 7)
-static bool conv_k32_t2d_enabled() {
-  const char* e = std::getenv("DM_CONV_K32T2");
-  return !(e && e[0] == '0');
-}
-
+// (split-K 64-row tiles); otherwise it replaces conv_patch3's fp16x2 tiles for 3x3 stride-1 convs. The plan
+// toggles (Toggles: DM_CONV_K32S, DM_CONV_K32S2, DM_CONV_K32T2, DM_K32_8X, DM_K32S_W4) keep the paths each form
+// replaced as its test oracle.
 // variant 10's geometry: 4 output rows x 32 columns per 128-row tile, a 6 x 34 patch
 static bool t2d_geom(const ConvArgs& a, PatchGeom& g) {
   // tiles over the output map, or over the low-res map of the sub-pixel upsample (4 parities x 4 taps)
@@ -1065,49 +1037,35 @@ static bool t2d_geom(const ConvArgs& a, PatchGeom& g) {
   return true;
 }
 
-// The stride-2 tiles (variant 9) unless DM_CONV_K32S2=0 (then conv_patch3 MODE 4, kept as their test oracle)
-static bool conv_k32_s2_enabled() {
-  const char* e = std::getenv("DM_CONV_K32S2");
-  return !(e && e[0] == '0');
-}
-
-// The small-map kernel (variant 6) unless DM_CONV_K32S=0 (the two-launch split-K path, kept as its test oracle;
-// read per call: plans capture their launches once, so this costs nothing per forward)
-static bool conv_k32_small_enabled() {
-  const char* e = std::getenv("DM_CONV_K32S");
-  return !(e && e[0] == '0');
-}
-
 int conv_k32_pick(const ConvArgs& a) {
   if (a.tile >= 10 && a.tile <= 20) return conv_k32_variant_ok(a, a.tile - 9) ? a.tile - 9 : 0;
-  if (a.tile != 0 || !conv_k32_enabled()) return 0;
+  if (a.tile != 0) return 0;
   if (a.stride == 2) {  // at least one block per CU (the nominal batch keeps the choice batch-invariant)
     const long M = (long)(a.pick_B > 0 ? a.pick_B : a.B) * a.Hout * a.Wout;
-    return conv_k32_s2_enabled() && conv_k32_variant_ok(a, 9) && (M / 64) * ((a.Cout + 127) / 128) >= 256 ? 9 : 0;
+    return toggles().k32_s2 && conv_k32_variant_ok(a, 9) && (M / 64) * ((a.Cout + 127) / 128) >= 256 ? 9 : 0;
   }
   // split-K convs of maps of <= 16 pixels: 64 x 128 tiles (4x4 maps at B = 256, K split 2: 32.5 us vs
   // 34.2 us for 64 x 64 and for conv_patch3's 64 x 64 split tiles)
   if (a.ksplit > 1) {
-    if (conv_k32_small_enabled() && conv_k32_variant_ok(a, 6)) return toggles().k32s_w4 ? 12 : 6;
+    if (toggles().k32_small && conv_k32_variant_ok(a, 6)) return toggles().k32s_w4 ? 12 : 6;
     return conv_k32_variant_ok(a, 4) ? 4 : conv_k32_variant_ok(a, 3) ? 3 : 0;
   }
   if (!conv_k32_ok(a)) {
     // maps whose whole-row 128-row tiles do not fit the patch image (64^2 .. 256^2): 128-pixel row segments /
     // two-row tiles of 8 waves, else 64-pixel rows / segments
     const int wt = a.upsample == 2 ? a.Win : a.Wout;
-    if (wt >= 64 && conv_k32_t2d_enabled() && conv_k32_variant_ok(a, 10)) return 10;
-    if (wt >= 64 && conv_k32_wide_enabled() && conv_k32_variant_ok(a, 7)) return 7;
+    if (wt >= 64 && toggles().k32_t2d && conv_k32_variant_ok(a, 10)) return 10;
+    if (wt >= 64 && conv_k32_variant_ok(a, 7)) return 7;
     if (wt >= 64) return conv_k32_variant_ok(a, 5) ? 5 : 0;
     // 128-row tiles whose GroupNorm tables do not fit kTab: the big-table instantiation (one block per CU)
     const int p = conv_pick(a);
-    return ((p == 3 || p == 4) && conv_k32_bigtab_enabled() && conv_k32_variant_ok(a, 8)) ? 8 : 0;
+    return ((p == 3 || p == 4) && conv_k32_variant_ok(a, 8)) ? 8 : 0;
   }
   const int p = conv_pick(a);
   if (p != 3 && p != 4) return 0;
   // 8^2 maps on 64-row single-image tiles (two blocks per CU where 128 x 128 tiles give one; bit-identical):
   // C3 A/B +0.3 % / +0.25 % over two sessions' alternations; DM_K32_8X=0 keeps the 128 x 128 two-image tiles
-  const char* e8 = std::getenv("DM_K32_8X");
-  if (!(e8 && e8[0] == '0') && conv_k32_variant_ok(a, 11)) return 11;
+  if (toggles().k32_8x && conv_k32_variant_ok(a, 11)) return 11;
   // 128 x 128 tiles down to one block per CU (measured on 8^2 maps at B = 256: 256 blocks of 128 x 128 beat
   // 512 of 128 x 64 by 6 %); the nominal batch (pick_B) keeps the choice batch-invariant
   const long M = (long)(a.pick_B > 0 ? a.pick_B : a.B) * a.Hout * a.Wout;
@@ -1183,10 +1141,7 @@ int conv2d_k32(const ConvArgs& a, int v, hipStream_t st) {
   }
   if (v == 10) {
     t2d_geom(a, g);
-    ConvArgs an = a;
-    // DM_K32_NSLOW=1 (A/B): the N-slow tile order for the 2-D tiles
-    an.nslow = std::getenv("DM_K32_NSLOW") && std::getenv("DM_K32_NSLOW")[0] == '1';
-    launch_k32<128, 128, 64, 64, false, 256, kMaxP, kTab, false, true>(an, g, st);
+    launch_k32<128, 128, 64, 64, false, 256, kMaxP, kTab, false, true>(a, g, st);
     DM_LAUNCH_CHECK();
     return DM_OK;
   }

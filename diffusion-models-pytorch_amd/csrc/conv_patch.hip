@@ -460,11 +460,6 @@ int conv_patch_pick(const ConvArgs& a, PatchGeom& g) {
     return conv_patch_geom(a, 64, g) && g.P <= kPatchS2Max ? 6 : 0;
   }
   // big-tile fp16x2 split kernels (one wave per SIMD): forced by tile 7 / 8 only (for now)
-  // 16 x 16 maps, Cout a multiple of 256, plain stride-1 MODE 0 with the GroupNorm prologue: one image per
-  // 256 x 256 block, one wave per SIMD with 128 x 128 wave tiles (+4 % over 128 x 128 blocks, measured)
-  if (a.tile == 0 && std::getenv("DM_CONV_BIG16") && a.ws && a.ws_np == 2 && !a.upsample && a.Hout == 16 &&
-      a.Wout == 16 && a.Cout % 256 == 0 && a.ksplit <= 1 && conv_patch_geom(a, 256, g) && g.P <= kPatch3Max256)
-    return 7;
   if (a.tile == 7 || a.tile == 8) {
     if (!(a.ws && a.ws_np == 2)) return 0;
     if (a.tile == 7) return conv_patch_geom(a, 256, g) && g.P <= kPatch3Max256 ? 7 : 0;

@@ -27,6 +27,7 @@
 // partials of the consumer per 64-pixel chunk, the two 32-pixel halves combined in LDS).
 #include <cstdlib>
 #include <string>
+#include <type_traits>
 
 #include "dm_common.h"
 #include "dm_kernels.h"
@@ -41,6 +42,10 @@ namespace {
 #ifndef DM_WINO_ABL
 #define DM_WINO_ABL 0
 #endif
+
+// the loader / tap-row / chunk lambdas are called from both roles' loop copies: always inlined (an outlined call would
+// put the accumulators and the B ring in scratch)
+#define DM_WINO_INL __attribute__((always_inline))
 
 constexpr int kWC = 32;                        // input channels per chunk (K of one MFMA step)
 constexpr int kWRowH = 80;                     // LDS row pitch in fp16 (160 B), as conv_k32
@@ -74,12 +79,12 @@ __device__ unsigned long long g_wino_stamps[65536][16];
 __device__ __forceinline__ void split_lo4(f4 x, f16x4 hi, f16x4& lo) {
   typedef unsigned int u2v __attribute__((ext_vector_type(2)));
   const u2v hp = __builtin_bit_cast(u2v, hi);
-  u2v lp = {0u, 0u};
+  u2v lp;
 #pragma unroll
-  for (int w = 0; w < 2; ++w) {
-    asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "+v"(lp[w]) : "v"(hp[w]), "v"(x[2 * w]));
-    asm("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(lp[w]) : "v"(hp[w]), "v"(x[2 * w + 1]));
-  }
+  for (int w = 0; w < 2; ++w)  // one asm per register: its two halves written by the pair (no zero-initialisation)
+    asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]\n"
+        "v_fma_mixhi_f16 %0, %1, -1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+        : "=&v"(lp[w]) : "v"(hp[w]), "v"(x[2 * w]), "v"(x[2 * w + 1]));
   lo = __builtin_bit_cast(f16x4, lp);
 }
 
@@ -126,8 +131,10 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   constexpr bool PRO = PROM != 0;
   constexpr int NP = W / 2, TH = 128 / W, PR = TH + 2, NR = PR * NP;
   static_assert(NR <= kWNR, "patch plane");
-  constexpr int UPW = PR * 4 / 8;  // loader units (patch row, 8-channel quarter) per wave: 3 (W 32) / 5 (W 16)
-  static_assert(UPW * 8 == PR * 4 && UPW * NP <= 64, "loader units tile the waves");
+  // loader units (patch row, 4-channel eighth of the chunk) of NP lanes, 64 / NP per wave instruction: NSET = 12
+  // (W 32) / 10 (W 16) full sets over the 8 waves -- set s = w and, for the first NSET - 8 waves of one role, 8 + w'
+  constexpr int NSET = PR * 8 * NP / 64;
+  static_assert(NSET * 64 == PR * 8 * NP && NSET > 8 && NSET <= 16, "loader sets");
   constexpr int TM = 4, TN = 4, NTAP = 3;
 #ifndef DM_WINO_WD
 #define DM_WINO_WD 2
@@ -155,10 +162,24 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int nu = wave >> 1, ch = wave & 1;
   const int l16 = lane & 15, q = lane >> 4;
-  const int lu = lane / NP, lj = lane - (lane / NP) * NP;  // loader: unit lu of the wave, pair lj of the unit
-  const bool lact = lu < UPW;
-  const int u = min(wave * UPW + lu, PR * 4 - 1);  // unit u = (patch row pr, 8-channel quarter sq)
-  const int pr = u >> 2, sq = u & 3;
+  const int lj = lane & (NP - 1);  // loader: pair lj of the lane's unit
+#ifndef DM_WINO_XSET
+#define DM_WINO_XSET 0
+#endif
+  // Set s covers 16-lane rows 4 s .. 4 s + 3, unit u = row (W 32) or 2 row + (lane & 15) / 8 (W 16): patch row u / 8
+  // -- s / 2 or s, the same for the wave's lanes -- and channels 4 (u & 7) .. + 3, the same in both of its sets (s and
+  // s + 8). The NSET - 8 extra sets go to waves 0.. of the early role (XSET 0) or of the late role (XSET 1).
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const int xw = DM_WINO_XSET ? wave_u - 4 : wave_u;
+  const bool has2 = xw >= 0 && xw < NSET - 8;
+  const int loff = NP == 16 ? 16 * (wave_u & 1) + 4 * (lane >> 4) : 4 * (lane >> 3);
+  int lpr[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int s_ = k ? 8 + max(xw, 0) : wave_u;
+    lpr[k] = min(NP == 16 ? s_ >> 1 : s_, PR - 1);
+  }
+  const int ldst = lj * kWRowH + loff;  // the lane's offset in a patch row group
   const int Kp = NTAP * a.Cin1 + (SC ? a.Cin2 / 2 : 0);  // K of each U matrix (their stride in the image)
   const int ngrp = ceil_div(N, 32);
   const size_t sl = (size_t)ngrp * 1024;  // fp16 per 16-deep slice of the U images
@@ -168,17 +189,20 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
 
   // ---- per-tile state: the tile's rows and columns, the loader's pixel pointers, the B base
   int m0 = 0, n0 = 0;
-  bool rok = false;
-  const float *p0 = nullptr, *p1 = nullptr;
+  bool rok[2] = {false, false};
+  // the set's pixel 2 lj (pixel 2 lj + 1 one pitch on; padding rows: the zero page, which covers a pitch and a row)
+  const float* pp[2] = {nullptr, nullptr};
   const _Float16* wbase = nullptr;
-  auto set_tile = [&](int tile) {
+  auto set_tile = [&](int tile) DM_WINO_INL {
     const int mt = tile / nN, nt = tile - mt * nN;
     m0 = b0 * HW + mt * 128;
     n0 = nt * 128;
-    const int iy = mt * TH - 1 + pr;
-    rok = lact && iy >= 0 && iy < a.Hin;
-    p0 = rok ? a.x1 + ((size_t)(b0 * a.Hin + iy) * W + 2 * lj) * a.x1_pitch + 8 * sq : kZeroPage + 8 * sq;
-    p1 = rok ? p0 + a.x1_pitch : p0;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int iy = mt * TH - 1 + lpr[k];
+      rok[k] = iy >= 0 && iy < a.Hin;
+      pp[k] = rok[k] ? a.x1 + ((size_t)(b0 * a.Hin + iy) * W + 2 * lj) * a.x1_pitch + loff : kZeroPage + loff;
+    }
     // column n0 + ch 64 + 16 j + l16 (n0 % 128 == 0): 32-column group (n0 + ch 64) / 32 + j / 2, column
     // 16 (j & 1) + l16 of it -- one base pointer, compile-time offsets per j
     wbase = reinterpret_cast<const _Float16*>(a.wino_ws) + (size_t)nu * (Kp / 16) * sl +
@@ -187,25 +211,27 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
 
   // chunk c + 1's pixels: loaded a chunk ahead (right after the previous finish), finished before / after chunk c's
   // MFMAs (the ping-pong below)
-  f4 rw[4];
-  auto load_raw = [&](int c) {
+  f4 rw[4];  // set k: pixels 2 lj, 2 lj + 1 in rw[2 k], rw[2 k + 1]
+  auto load_raw = [&](int c) DM_WINO_INL {
     const int co = c * kWC;
-    rw[0] = *reinterpret_cast<const f4*>(p0 + co);
-    rw[1] = *reinterpret_cast<const f4*>(p0 + co + 4);
-    rw[2] = *reinterpret_cast<const f4*>(p1 + co);
-    rw[3] = *reinterpret_cast<const f4*>(p1 + co + 4);
+    rw[0] = *reinterpret_cast<const f4*>(pp[0] + co);
+    rw[1] = *reinterpret_cast<const f4*>(pp[0] + a.x1_pitch + co);
+    if (has2) {
+      rw[2] = *reinterpret_cast<const f4*>(pp[1] + co);
+      rw[3] = *reinterpret_cast<const f4*>(pp[1] + a.x1_pitch + co);
+    }
   };
   if (t < 8) gzero[t] = 0.f;  // (visible after the prologue's barrier)
-  // channels 4 h .. 4 h + 3 of the lane's 8: GroupNorm (+ SiLU) of its two pixels, the neighbours by DPP,
+  // set k's 4 channels: GroupNorm (+ SiLU) of the lane's two pixels, the neighbours by DPP,
   // V = B^T d, split, stored into buffer buf. PROM 2: the tables hold -log2(e) (scale, shift), so z' = -log2(e) z
   // comes out of one fma and silu(z) = -ln 2 * z' / (1 + 2^z'): the loader keeps z' / (1 + 2^z') and the epilogue
   // scales by -ln 2 (exact algebra; one rounding each). Padding rows read the zero table: exactly 0. Range: a V
   // beyond fp16's range splits into an infinite piece, which every product carries into the accumulators -- the
   // epilogue's finiteness check raises the range flag.
-  auto finish = [&](int c, int buf, int h) {
-    f4 e0 = rw[h], e1 = rw[2 + h];
+  auto finish_set = [&](int c, int buf, int k) DM_WINO_INL {
+    f4 e0 = rw[2 * k], e1 = rw[2 * k + 1];
     if (PROM) {
-      const float* ts = rok ? gtab + 2 * (c * kWC + 8 * sq + 4 * h) : gzero;  // [4 scales][4 shifts]
+      const float* ts = rok[k] ? gtab + 2 * (c * kWC + loff) : gzero;  // [4 scales][4 shifts]
 #if DM_WINO_ABL == 6
       const f4 sc = {1.f, 1.f, 1.f, 1.f}, sh = {0.f, 0.f, 0.f, 0.f};
 #else
@@ -238,11 +264,11 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
       vv[2][k] = e1[k] - e0[k];
     }
 #if DM_WINO_ABL == 4
-    if (lact && a.Cout < 0) {
+    if (a.Cout < 0) {
 #else
-    if (lact) {
+    {
 #endif
-      _Float16* dst = patch + buf * kWBuf + (pr * NP + lj) * kWRowH + sq * 8 + 4 * h;
+      _Float16* dst = patch + buf * kWBuf + lpr[k] * NP * kWRowH + ldst;
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         f16x4 hi, lo;  // x = hi + lo, lo = fp16(x - hi) (the difference exact, one rounding to fp16)
@@ -255,12 +281,17 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     }
   };
 
+  auto finish = [&](int c, int buf) DM_WINO_INL {
+    finish_set(c, buf, 0);
+    if (has2) finish_set(c, buf, 1);
+  };
+
   // ---- B: the fp16x2 fragment images of U_nu (split_conv_weights, nmat 4, ntap 3), 16-column halves
-  auto slice_off = [&](int kt) { return (size_t)(kt + (kt / NTAP) * NTAP) * sl + qoff; };
+  auto slice_off = [&](int kt) DM_WINO_INL { return (size_t)(kt + (kt / NTAP) * NTAP) * sl + qoff; };
   // all K steps of a tile: the 3 nch tap rows, then the ns shortcut steps (16-slices 3 Cin1 / 16 + 2 s (+ 1 for
   // k-groups 2, 3)); past the end: the last step again (refills nothing uses)
   const int ns = SC ? a.Cin2 / (2 * kWC) : 0, nst = kt_end + ns, nst_g = nch + ns;  // K steps, stages
-  auto step_off = [&](int kt) {
+  auto step_off = [&](int kt) DM_WINO_INL {
     kt = min(kt, nst - 1);
     return kt < kt_end ? slice_off(kt) : (size_t)(kt_end / 3 * 3 * kWC / 16 + 2 * (kt - kt_end) + (q >> 1)) * sl;
   };
@@ -278,7 +309,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   const int abase = (nu * NR + l16) * kWRowH + q * 8;
   // a0: tile 0's fragment of this tap row on entry (read ahead); within a chunk, the next tap row's on exit
   f16x8 a0[2];
-  auto read_a0 = [&](int dy, int pbuf) {
+  auto read_a0 = [&](int dy, int pbuf) DM_WINO_INL {
     const _Float16* As = patch + pbuf * kWBuf + abase + dy * NP * kWRowH;
     a0[0] = *reinterpret_cast<const f16x8*>(As);
     a0[1] = *reinterpret_cast<const f16x8*>(As + 32);
@@ -308,14 +339,14 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   // and 4-channel slot ks of the 32, nu 0 x2[2p][H1], nu 3 x2[2p + 1][H1], nu 1 / 2 x2[2p][H2] +/- x2[2p + 1][H2]
   // (H1 = channels 32 s + .., H2 = Cin2 / 2 + 32 s + ..) as pair rows [nu][64] of a patch buffer
   const int sp = t >> 3, sks = t & 7;
-  auto load_sc = [&](int st) {
+  auto load_sc = [&](int st) DM_WINO_INL {
     const float* xs = a.x2 + (size_t)(m0 + 2 * sp) * a.x2_pitch + st * kWC + 4 * sks;
     rw[0] = *reinterpret_cast<const f4*>(xs);
     rw[1] = *reinterpret_cast<const f4*>(xs + a.x2_pitch);
     rw[2] = *reinterpret_cast<const f4*>(xs + a.Cin2 / 2);
     rw[3] = *reinterpret_cast<const f4*>(xs + a.x2_pitch + a.Cin2 / 2);
   };
-  auto finish_sc = [&](int buf, int h) {  // h 0: planes 0, 3 (H1); h 1: planes 1, 2 (H2)
+  auto finish_sc = [&](int buf, int h) DM_WINO_INL {  // h 0: planes 0, 3 (H1); h 1: planes 1, 2 (H2)
     _Float16* dst = patch + buf * kWBuf + sp * kWRowH + 4 * sks;
 #pragma unroll
     for (int v2 = 0; v2 < 2; ++v2) {
@@ -330,14 +361,13 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     }
   };
   // stage g of a tile: chunk g < nch, else shortcut step g - nch
-  auto load_stage = [&](int g) {
+  auto load_stage = [&](int g) DM_WINO_INL {
     if (!SC || g < nch) load_raw(g);
     else load_sc(g - nch);
   };
-  auto finish_stage = [&](int g, int buf) {
+  auto finish_stage = [&](int g, int buf) DM_WINO_INL {
     if (!SC || g < nch) {
-      finish(g, buf, 0);
-      finish(g, buf, 1);
+      finish(g, buf);
     } else {
       finish_sc(buf, 0);
       finish_sc(buf, 1);
@@ -346,7 +376,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
 
   // GroupNorm tables of image b0 into LDS (scale, shift per channel, [c / 4][4 scales][4 shifts], times -log2(e)
   // under SiLU); the caller's barrier publishes them
-  auto build_table = [&]() {
+  auto build_table = [&]() DM_WINO_INL {
     if (!PRO) return;
     const int C = a.Cin1;
     if (a.gin_part) {  // gn_finalize (gn.hip) for the tile's image, its expressions (conv_k32's in-kernel finalize)
@@ -391,17 +421,19 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     }
   };
 
-  // ---- first tile's prologue: B ring and the first chunk's pixels in flight while the GroupNorm tables are built
+  // ---- first tile's prologue: B ring and the first chunk's pixels in flight while the GroupNorm tables are built.
+  // The ring's last slot is requested after the second stage's pixels, as in the loop (pixels, then B refills): the
+  // loop head's memory-counter waits, merged over the prologue and the loop's own back edge, then stay partial.
   int tile = t_first;
   set_tile(tile);
 #pragma unroll
-  for (int d = 0; d < WD; ++d) load_b(bq[d], step_off(d));
+  for (int d = 0; d < WD - 1; ++d) load_b(bq[d], step_off(d));
   load_raw(0);
   build_table();
   __syncthreads();
-  finish(0, 0, 0);
-  finish(0, 0, 1);
+  finish(0, 0);
   load_stage(min(1, nst_g - 1));
+  load_b(bq[WD - 1], step_off(WD - 1));
   __syncthreads();
   W_STAMP(1);
 #ifdef DM_K32_STAMPS
@@ -413,13 +445,132 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     var += now - t_s;                                    \
     t_s = now;                                           \
   } while (0)
+  // per-role phases of the main loop (waves 0 and 4, the two roles of SIMD 0): first phase, second phase, barrier
+  unsigned long long ph_t[4] = {0, 0, 0, 0}, ph_sum[3] = {0, 0, 0};
+#define W_PH(k)                                                     \
+  do {                                                              \
+    ph_t[k] = __builtin_amdgcn_s_memtime();                         \
+    if (k > 0) ph_sum[k - 1] += ph_t[k] - ph_t[k - 1];              \
+  } while (0)
 #else
 #define W_ACC(var) do {} while (0)
+#define W_PH(k) do {} while (0)
 #endif
   // ping-pong of the two waves of each SIMD (waves w and w + 4): the early group finishes chunk c + 1 before chunk
   // c's MFMAs, the late group after them, so each wave's loader VALU runs beside its partner's MFMAs
-  // (MI355X_MICROARCH.md, two waves per SIMD); each loads chunk c + 2's pixels right after its finish, a chunk ahead
+  // (MI355X_MICROARCH.md, two waves per SIMD); each loads chunk c + 2's pixels right after its finish, a chunk ahead.
+  // The two roles are separate copies of the loop (role_loop below): in one loop body with a branch per role the
+  // compiler's memory-counter waits merge both load orders and wait for everything -- the early wave for the pixels
+  // it has just requested before its first MFMA, the late wave for the B refills it has just issued before its finish.
   const bool late = wave >= 4;
+#ifndef DM_WINO_PRIO
+#define DM_WINO_PRIO 2
+#endif
+#if DM_WINO_PRIO == 1
+  if (late) __builtin_amdgcn_s_setprio(1);
+#endif
+  // ---- main loop: chunk c's three tap rows from buffer c & 1, chunk c + 1 finished into the other; one barrier
+  // per chunk. Two chunks per iteration (CC: the B ring slots are compile-time), an odd last chunk after the loop --
+  // not a skipped half inside it, whose path into the loop head would merge a second load order there as well
+  auto chunk = [&](int c, auto cc_c, auto late_c) DM_WINO_INL {
+    constexpr int CC = decltype(cc_c)::value;
+    constexpr bool LATE = decltype(late_c)::value;
+    const int gn = min(c + 1, nch - 1);  // after the last chunk: refilled into the unused buffer
+    W_PH(0);
+#if DM_WINO_ABL != 1 && DM_WINO_ABL != 3
+    if (!LATE) {
+      finish(gn, (c + 1) & 1);
+      load_raw(min(c + 2, nch - 1));
+      W_PH(1);
+    }
+#endif
+#if DM_WINO_PRIO == 2
+    if (LATE) __builtin_amdgcn_s_setprio(1);
+#endif
+#pragma unroll
+    for (int dy = 0; dy < NTAP; ++dy) {
+      const int kt = c * NTAP + dy;
+      const int slot = (CC * NTAP + dy) % WD;
+      if (dy == 0) {
+        read_a0(0, c & 1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      compute(dy, c & 1, bq[slot]);
+#if DM_WINO_ABL != 2 && DM_WINO_ABL != 3  // ablation builds (timing only, wrong results): 1 no finish, 2 no B refills
+      load_b(bq[slot], step_off(kt + WD));
+#endif
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#if DM_WINO_ABL != 1 && DM_WINO_ABL != 3
+    if (LATE) {
+#if DM_WINO_PRIO == 2
+      __builtin_amdgcn_s_setprio(0);
+#endif
+      W_PH(1);
+      finish(gn, (c + 1) & 1);
+      load_raw(min(c + 2, nch - 1));
+    }
+#endif
+    W_PH(2);
+    __syncthreads();
+    W_PH(3);
+  };
+  typedef std::integral_constant<int, 0> Cc0;
+  typedef std::integral_constant<int, 1> Cc1;
+  auto role_loop = [&](auto late_c) DM_WINO_INL {
+    int c0 = 0;
+    for (; c0 + 1 < nch; c0 += 2) {
+      chunk(c0, Cc0{}, late_c);
+      chunk(c0 + 1, Cc1{}, late_c);
+    }
+    if (c0 < nch) chunk(c0, Cc0{}, late_c);
+  };
+  // ---- the shortcut steps: stage g = nch + s from buffer g & 1, one K step each (ring slot CC, after the swap below)
+  auto sc_step = [&](int st, auto cc_c, auto late_c) DM_WINO_INL {
+    constexpr int CC = decltype(cc_c)::value;
+    constexpr bool LATE = decltype(late_c)::value;
+    const int g = nch + st, buf = g & 1;
+    if (!LATE) {
+      finish_sc(buf ^ 1, 0);  // stage min(g + 1, last): a shortcut step (its pixels loaded a stage ahead)
+      finish_sc(buf ^ 1, 1);
+      load_sc(min(st + 2, ns - 1));
+    }
+    const _Float16* As = patch + buf * kWBuf + (nu * 64 + l16) * kWRowH + q * 8;
+    a0[0] = *reinterpret_cast<const f16x8*>(As);
+    a0[1] = *reinterpret_cast<const f16x8*>(As + 32);
+    __builtin_amdgcn_sched_barrier(0);
+    f16x8 av[TM][2];
+    av[0][0] = a0[0];
+    av[0][1] = a0[1];
+#pragma unroll
+    for (int i = 1; i < TM; ++i)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) av[i][p] = *reinterpret_cast<const f16x8*>(As + i * 16 * kWRowH + p * 32);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bq[CC][j][0], av[i][1], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bq[CC][j][1], av[i][0], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bq[CC][j][0], av[i][0], acc[i][j], 0, 0, 0);
+      }
+    load_b(bq[CC], step_off(kt_end + st + WD));
+    __builtin_amdgcn_sched_barrier(0);
+    if (LATE) {
+      finish_sc(buf ^ 1, 0);
+      finish_sc(buf ^ 1, 1);
+      load_sc(min(st + 2, ns - 1));
+    }
+    __syncthreads();
+  };
+  auto sc_loop = [&](auto late_c) DM_WINO_INL {
+    int s0 = 0;
+    for (; s0 + 1 < ns; s0 += 2) {
+      sc_step(s0, Cc0{}, late_c);
+      sc_step(s0 + 1, Cc1{}, late_c);
+    }
+    if (s0 < ns) sc_step(s0, Cc0{}, late_c);
+  };
   for (;;) {
 #ifdef DM_K32_STAMPS
     t_loop = __builtin_amdgcn_s_memtime();
@@ -428,47 +579,10 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-    // ---- main loop: chunk c's three tap rows from buffer c & 1, chunk c + 1 finished into the other; one barrier
-    // per chunk
-    for (int c0 = 0; c0 < nch; c0 += 2) {
-#pragma unroll
-      for (int cc = 0; cc < 2; ++cc) {
-        const int c = c0 + cc;
-        if (c >= nch) continue;  // (not break: keeps the two-chunk body unrolled, bq[slot] statically indexed)
-        const int gn = min(c + 1, nch - 1);  // after the last chunk: refilled into the unused buffer
-#if DM_WINO_ABL != 1 && DM_WINO_ABL != 3
-        if (!late) {
-          finish(gn, (c + 1) & 1, 0);
-          finish(gn, (c + 1) & 1, 1);
-          load_raw(min(c + 2, nch - 1));
-        }
-#endif
-#pragma unroll
-        for (int dy = 0; dy < NTAP; ++dy) {
-          const int kt = c * NTAP + dy;
-          const int slot = (cc * NTAP + dy) % WD;
-          if (dy == 0) {
-            read_a0(0, c & 1);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-          compute(dy, c & 1, bq[slot]);
-#if DM_WINO_ABL != 2 && DM_WINO_ABL != 3  // ablation builds (timing only, wrong results): 1 no finish, 2 no B refills
-          load_b(bq[slot], step_off(kt + WD));
-#endif
-          __builtin_amdgcn_sched_barrier(0);
-        }
-#if DM_WINO_ABL != 1 && DM_WINO_ABL != 3
-        if (late) {
-          finish(gn, (c + 1) & 1, 0);
-          finish(gn, (c + 1) & 1, 1);
-          load_raw(min(c + 2, nch - 1));
-        }
-#endif
-        __syncthreads();
-      }
-    }
-    // ---- the shortcut steps: stage g = nch + s from buffer g & 1, one K step each; the ring slot of step kt is
-    // kt & 1 (WD 2): after an odd number of tap rows the two slots trade places
+    if (late) role_loop(std::true_type{});
+    else role_loop(std::false_type{});
+    // ---- the shortcut steps; the ring slot of step kt is kt & 1 (WD 2): after an odd number of tap rows the two
+    // slots trade places
     if (SC && ns > 0) {
       // its first step staged here (the main loop ends with every wave past its last read of buffer nch & 1)
       load_sc(0);
@@ -486,46 +600,8 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
             bq[1][j][p] = tmp;
           }
       }
-      for (int s0 = 0; s0 < ns; s0 += 2) {
-#pragma unroll
-        for (int cc = 0; cc < 2; ++cc) {
-          const int st = s0 + cc;
-          if (st >= ns) continue;
-          const int g = nch + st, buf = g & 1;
-          if (!late) {
-            finish_sc(buf ^ 1, 0);  // stage min(g + 1, last): a shortcut step (its pixels loaded a stage ahead)
-            finish_sc(buf ^ 1, 1);
-            load_sc(min(st + 2, ns - 1));
-          }
-          const _Float16* As = patch + buf * kWBuf + (nu * 64 + l16) * kWRowH + q * 8;
-          a0[0] = *reinterpret_cast<const f16x8*>(As);
-          a0[1] = *reinterpret_cast<const f16x8*>(As + 32);
-          __builtin_amdgcn_sched_barrier(0);
-          f16x8 av[TM][2];
-          av[0][0] = a0[0];
-          av[0][1] = a0[1];
-#pragma unroll
-          for (int i = 1; i < TM; ++i)
-#pragma unroll
-            for (int p = 0; p < 2; ++p) av[i][p] = *reinterpret_cast<const f16x8*>(As + i * 16 * kWRowH + p * 32);
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bq[cc][j][0], av[i][1], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bq[cc][j][1], av[i][0], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bq[cc][j][0], av[i][0], acc[i][j], 0, 0, 0);
-            }
-          load_b(bq[cc], step_off(kt_end + st + WD));
-          __builtin_amdgcn_sched_barrier(0);
-          if (late) {
-            finish_sc(buf ^ 1, 0);
-            finish_sc(buf ^ 1, 1);
-            load_sc(min(st + 2, ns - 1));
-          }
-          __syncthreads();
-        }
-      }
+      if (late) sc_loop(std::true_type{});
+      else sc_loop(std::false_type{});
     }
 #ifdef DM_K32_STAMPS
     t_s = __builtin_amdgcn_s_memtime();
@@ -554,7 +630,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
       set_tile(next);
       load_raw(0);
 #pragma unroll
-      for (int d = 0; d < WD; ++d) load_b(bq[d], step_off(d));
+      for (int d = 0; d < WD - 1; ++d) load_b(bq[d], step_off(d));
     }
     __syncthreads();
     W_ACC(ew_cycles);
@@ -602,9 +678,9 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     // GroupNorm tables, which sit outside the E planes)
     tile = next;
     __syncthreads();
-    finish(0, 0, 0);
-    finish(0, 0, 1);
+    finish(0, 0);
     load_stage(min(1, nst_g - 1));
+    load_b(bq[WD - 1], step_off(WD - 1));
     __syncthreads();
     W_ACC(np_cycles);
   }
@@ -615,6 +691,12 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     g_wino_stamps[blockIdx.x][8] = ew_cycles;
     g_wino_stamps[blockIdx.x][9] = out_cycles;
     g_wino_stamps[blockIdx.x][10] = np_cycles;
+  }
+  if ((threadIdx.x == 0 || threadIdx.x == 256) && blockIdx.x < 65536) {
+    const int o = threadIdx.x ? 14 : 11;
+    g_wino_stamps[blockIdx.x][o] = ph_sum[0];
+    g_wino_stamps[blockIdx.x][o + 1] = ph_sum[1];
+    g_wino_stamps[blockIdx.x][threadIdx.x ? 7 : 13] = ph_sum[2];
   }
 #endif
   W_STAMP(3);
@@ -669,6 +751,7 @@ bool conv_wino_shape_ok(const ConvArgs& a) {
   if (a.Hin != a.Hout || a.Win != a.Wout || (a.Wout != 32 && a.Wout != 16) || (a.Hout * a.Wout) % 128 != 0) return false;
   if (a.Cin1 < kWC || a.Cin1 % kWC != 0 || 2 * a.Cin1 > kWTab || a.Cin2 % (2 * kWC) != 0 || a.K != 9 * a.Cin1 + a.Cin2)
     return false;
+  if (a.x1_pitch + a.Cin1 > kZeroPageFloats) return false;  // the loader's padding rows read the zero page
   if (a.Cin2 && (!a.x2 || a.x2_pitch % 4 != 0 || (reinterpret_cast<uintptr_t>(a.x2) & 15) != 0)) return false;
   if (a.Cout % 128 != 0) return false;
   if (a.gin_part && (a.gin_G <= 0 || a.gin_G > kWMaxG || a.Cin1 % a.gin_G != 0)) return false;

@@ -67,15 +67,15 @@ struct DiTModel {
   long range_fallbacks = 0;
   int math = base_math;
   int run_math() const { return base_math == 2 && fallback ? 0 : base_math; }
-  bool range_check = !(std::getenv("DM_RANGE_CHECK") && std::string(std::getenv("DM_RANGE_CHECK")) == "0");
+  bool range_check = toggles().range_check;
   int* range_flag = nullptr;
   int* range_flag_host = nullptr;
   bool range_deferred = false;  // dm_dit_set_range_deferred / dm_dit_range_poll, as for the UNet
   std::map<const float*, int> w_exp;
   // fp16x2 fragment images of the token-GEMM weights (split_conv_weights, taps 1), built once: those GEMMs
-  // run linear_k32 (K = 32 MFMA steps, no per-load split of the weights); DM_DIT_LINEAR_K32=0 keeps gemm.hip
+  // run linear_k32 (K = 32 MFMA steps, no per-load split of the weights)
   std::map<const float*, void*> split_w;
-  bool linear_k32_on = !(std::getenv("DM_DIT_LINEAR_K32") && std::string(std::getenv("DM_DIT_LINEAR_K32")) == "0");
+  bool linear_k32_on = true;
 
   struct Plan : PlanBase {
     int B = 0;
@@ -112,6 +112,7 @@ static int dit_create(const dm_dit_arch* arch, const float* const* params, const
   const dm_dit_arch a = *arch;
   DM_REQUIRE(n_params == dit_count(a), "expected " + std::to_string(dit_count(a)) + " parameter tensors, got " +
                                            std::to_string(n_params));
+  refresh_toggles();  // the model's arithmetic and range check (member initialisers) from this snapshot
   auto m = std::make_unique<DiTModel>();
   m->arch = a;
   const int D = a.hidden_size, p = a.patch_size, C = a.in_channels, Hm = a.mlp_hidden;
@@ -192,6 +193,7 @@ static int dit_create(const dm_dit_arch* arch, const float* const* params, const
 
 int DiTModel::build_plan(Plan& pl, int B) {
   refresh_toggles();
+  pl.graph_enabled = toggles().graph;
   pl.B = B;
   pl.math = math;
   const dm_dit_arch& a = arch;
@@ -236,7 +238,7 @@ int DiTModel::build_plan(Plan& pl, int B) {
   // token GEMMs on linear_k32: LayerNorm-modulate (or nothing) + fp16x2 split of A once per GEMM
   // (linear_presplit_a) instead of once per 128-column tile inside it (27 x for qkv, 36 x for fc1);
   // one buffer shared by all of them (stream-ordered). DM_DIT_PRESPLIT=0: split inside the GEMM.
-  const bool presplit_on = !(std::getenv("DM_DIT_PRESPLIT") && std::getenv("DM_DIT_PRESPLIT")[0] == '0');
+  const bool presplit_on = toggles().dit_presplit;
   _Float16* as_buf = nullptr;
   size_t as_bytes = 0;
   // LayerNorm statistics for the next GEMM with the LN + modulate prologue: computed by that GEMM's
@@ -352,7 +354,7 @@ int DiTModel::build_plan(Plan& pl, int B) {
   // 128 columns streaming its K x 128 slice (the fp32 gemm_kernel took 558 us, 1.6 TB/s)
   {
     GemmArgs g = linear(se, D, B, ada_w, ada_b, ada_total, D, mods, ada_total);
-    if (!std::getenv("DM_DIT_ADA_FP32")) split(g, 6, ada_w, (size_t)ada_total * D, 6);
+    split(g, 6, ada_w, (size_t)ada_total * D, 6);
     add_gemm(g);
   }
 
@@ -376,7 +378,7 @@ int DiTModel::build_plan(Plan& pl, int B) {
     split(gq, 6, bp.qkv_w, (size_t)3 * D * D, 0);
     // flash attention (attention.hip attn_flash_kernel): the qkv GEMM's epilogue writes q * d^-1/2, k, v as
     // the fp16x2 operand planes (over the qkv buffer: same bytes), S never leaves the CU
-    const bool flash = math == 2 && gq.ws && attn_flash_ok(T, Dh) && !std::getenv("DM_DIT_ATTN_UNFUSED");
+    const bool flash = math == 2 && gq.ws && attn_flash_ok(T, Dh) && toggles().attn != kAttnUnfused;
     _Float16* planes = reinterpret_cast<_Float16*>(qkv);
     const size_t plane_n = (size_t)M * D * 2;   // fp16 elements of one operand's two planes
     if (flash) {

@@ -12,9 +12,25 @@ constexpr int kGnPixPerChunk = 64;
 // Plan toggles: the environment, read ONCE per plan build (refresh_toggles(): the UNet / DiT plan builders and the
 // direct-launch ABI entry points call it), so every decision of one plan -- and the label each op is profiled
 // under -- comes from one snapshot. Each keeps the path it replaces as a test oracle / A/B arm.
+constexpr int kAttnNoProj = 1, kAttnFused = 2, kAttnUnfused = 5;  // Toggles::attn oracle modes (DM_ATTN=noproj|fused|unfused)
 struct Toggles {
-  bool wino = true;      // DM_CONV_WINO=0: the 3x3 convs of 32^2 / 16^2 maps on conv_k32 instead of conv_wino
-  bool k32s_w4 = false;  // DM_K32S_W4=1: the small-map conv's 4-wave form (conv_k32 variant 12)
+  int conv_math = 2;          // DM_CONV_MATH=fp32|bf16x3: the conv / GEMM arithmetic (0 / 3; 2: fp16x2)
+  bool range_check = true;    // DM_RANGE_CHECK=0: no per-forward range flag check (and no fp32 re-run)
+  bool graph = true;          // DM_NO_GRAPH: launch the plan op by op instead of as a hipGraph
+  bool wino = true;           // DM_CONV_WINO=0: the 3x3 convs of 32^2 / 16^2 maps on conv_k32 instead of conv_wino
+  bool k32s_w4 = false;       // DM_K32S_W4=1: the small-map conv's 4-wave form (conv_k32 variant 12)
+  bool k32_small = true;      // DM_CONV_K32S=0: split-K convs of <= 16-pixel maps as two launches (conv_k32 3 / 4)
+  bool k32_s2 = true;         // DM_CONV_K32S2=0: stride-2 convs on conv_patch3 MODE 4 instead of conv_k32 variant 9
+  bool k32_t2d = true;        // DM_CONV_K32T2=0: wide maps on 128-pixel row segments (variant 7), not 2-D tiles
+  bool k32_8x = true;         // DM_K32_8X=0: 8^2 maps on 128 x 128 two-image tiles instead of 64-row tiles
+  bool gn_fusion = true;      // DM_GN_FUSION=0: GroupNorm statistics by separate passes (no producer epilogues,
+                              // no concat units, no first-conv statistics)
+  int attn = 4;               // DM_ATTN: the attention path -- 4 (default) the folded single-head block on 8
+                              // waves + flash / pre-split fused kernels elsewhere; 3 the folded block's 4-wave
+                              // form; the unfolded oracles (no folding, no flash kernel): 0 "presplit" (q / k /
+                              // v planes from the qkv epilogue, proj fused), kAttnNoProj, kAttnFused, kAttnUnfused
+  bool attn_gn_launch = false;  // DM_ATTN_GNFIN=1: the folded block's GroupNorm finalize as its own launch
+  bool dit_presplit = true;   // DM_DIT_PRESPLIT=0: DiT token GEMMs split their activations per tile
 };
 const Toggles& toggles();
 void refresh_toggles();
@@ -48,8 +64,7 @@ struct ConvArgs {
   int rowvec_pitch;
   const float* res;     // residual at output resolution or null
   int res_pitch;
-  int tile;
-  int nslow;     // K32 tile order: 1 = all M tiles of an N tile before the next N tile (conv_k32.hip)             // 0 auto; 1..3 force an im2col tile, 4..6 a halo-patch tile
+  int tile;      // 0 auto; 1..3 force an im2col tile, 4..6 a halo-patch tile
   int pick_B;           // batch the tile heuristics assume (0: B). Plans pass a fixed one, so a layer's
                         // kernel (and its summation order) never changes with B: batch-invariant results
   // optional operand prologue on segment 1 (halo-patch kernel only):
@@ -189,14 +204,10 @@ struct GemmArgs {
   // linear_k32 only: the attention operand planes instead of C (as ConvArgs::ap_*, the qkv projection
   // feeding attn_presplit_kernel)
   _Float16 *ap_q, *ap_k, *ap_v;
-  int lin_gm;     // linear_k32 tile order: M tiles per group (0: kLGM = 4)
   int ap_vonly;   // every column is a v column (the folded attention's g^T plane; ap_q = ap_k = ap_v)
   int ap_L, ap_heads, ap_Dh, ap_legacy;
   float ap_alpha, ap_bscale;
   int ap_ea, ap_eb, ap_ev;
-  // k ([L][Dh]) and v^T ([Dh][L]) as MFMA fragment images (frag_off, mfma_tile.h) instead of row planes:
-  // attn_presplit_kernel then loads every k / v operand fragment as one contiguous 1-KiB wave instruction
-  int ap_frag;
   int* range_flag;
 };
 
@@ -284,7 +295,6 @@ int conv2d_patch3(const ConvArgs& a, int which, const PatchGeom& g, hipStream_t 
 bool conv_k32_ok(const ConvArgs& a);
 int conv_k32_variant_ok(const ConvArgs& a, int v);
 int conv_k32_pick(const ConvArgs& a);
-bool conv_k32_enabled();  // DM_CONV_K32 != 0
 int conv2d_k32(const ConvArgs& a, int v, hipStream_t st);
 std::string conv_k32_label(const ConvArgs& a, int v);
 // Winograd F(2,3)-along-x 3x3 convs (conv_wino.hip): the shapes the kernel takes (32- / 16-wide maps, 128-pixel
@@ -301,9 +311,6 @@ int conv2d_wino(const ConvArgs& a, hipStream_t st);
 // static-weight GEMM on pre-split weights with K = 32 MFMA steps (linear_k32.hip)
 bool linear_k32_ok(const GemmArgs& g);
 int linear_k32(const GemmArgs& g, hipStream_t st);
-// whether linear_k32 runs g on the 8-wave 128 x 256 blocks (DM_LIN_BN256)
-bool linear_k32_wide(const GemmArgs& g);
-bool linear_k32_bn64(const GemmArgs& g);
 // the pre-split A image of g (prologue, alpha, 2^split_ea, fp16x2 split; |value| > 65504 sets range_flag)
 int linear_presplit_a(const GemmArgs& g, _Float16* out, hipStream_t st);
 int conv_splitk_reduce(const ConvArgs& a, hipStream_t st);
@@ -314,13 +321,9 @@ const float* split_conv_rowscale(const void* ws, int nmat, int rows, int K);
 int split_conv_weights(const float* w, int nmat, int rows, int K, int cin1, int ntap, int np, void* out,
                        hipStream_t st);
 std::string conv_label(const ConvArgs& a);
-// DM_CONV_MATH: fp16x2 (default) -> 2, bf16x3 -> 3, fp32 -> 0 (ConvArgs::ws_np of the model's convs)
-inline int conv_math_from_env() {
-  const char* e = std::getenv("DM_CONV_MATH");
-  if (!e) return 2;
-  const std::string s(e);
-  return s == "fp32" ? 0 : s == "bf16x3" ? 3 : 2;
-}
+// DM_CONV_MATH: fp16x2 (default) -> 2, bf16x3 -> 3, fp32 -> 0 (ConvArgs::ws_np of the model's convs), from the
+// plan's toggle snapshot
+inline int conv_math_from_env() { return toggles().conv_math; }
 int gemm_batched(const GemmArgs& g, hipStream_t st);
 // exponent e with max|x| * 2^e in [2^13, 2^14) (0 for all-zero x): fp16x2 operand scale of a weight
 // matrix, computed once at plan build (synchronous)
@@ -355,12 +358,11 @@ struct AttnArgs {
   // columns h Dh ..): the output projection reads it without a split pass
   _Float16* o_split;
   int o_split_ea, o_ld;
-  int frag;  // attn_presplit_kernel: pk / pv are fragment images (GemmArgs::ap_frag)
 };
 bool attn_fused_ok(int L, int Dh);
 int attn_fused(const AttnArgs& a, hipStream_t st);
 // Folded single-head attention block (attn_block.hip): T = xn At^T + w, S = T xn^T, P = softmax(S),
-// y = x + P g (g^T from a linear_k32 GEMM with the folded Wg = Wp Wv as the v-plane), GroupNorm statistics of y.
+// y = x + Wg' (P xn) + cb (Wg = Wp Wv), GroupNorm statistics of y.
 struct AttnBlockArgs {
   const float* x;               // [B][256][x_pitch] block input (NHWC rows)
   int x_pitch;
@@ -368,18 +370,17 @@ struct AttnBlockArgs {
   const _Float16* at_img;       // split_conv_weights image of At [256][256] (fp16x2)
   const float* at_rowscale;     // its row-scale undo (split_conv_rowscale)
   const float* w;               // [256] T bias
-  const _Float16* g_plane;      // variant 2: [B][2][256][256] g^T pieces x 2^eg (GemmArgs::ap_v with ap_vonly)
-  const _Float16* wg_img;       // variant 3: split_conv_weights image of Wg' (Wg, columns permuted: attn_perm_cols)
+  const _Float16* wg_img;       // split_conv_weights image of Wg' (Wg, columns permuted: attn_perm_cols)
   const float* wg_rowscale;
-  const float* cb;              // variant 3: [256] output bias Wp bv + bp
-  int variant;                  // 2: g from the linear_k32 plane; 3 (default): values = xn, Wg' after
+  const float* cb;              // [256] output bias Wp bv + bp
+  int variant;                  // 4 (default): 8 waves of 16 queries; 3: 4 waves of 32 (bit-identical)
   float* y;                     // [B][256][y_pitch]
   int y_pitch;
   double2* gn_part;             // optional GroupNorm(gn_G) chunk partials of y
   int gn_G;
   int B, ex, eg;
   int* range_flag;
-  // variants 4 / 5: the GroupNorm affine of x from its chunk partials in the kernel (gn_finalize's expressions)
+  // variant 4: the GroupNorm affine of x from its chunk partials in the kernel (gn_finalize's expressions)
   // instead of gsc / gsh, when gin_part is set
   const double2* gin_part;
   int gin_G, gin_nchunk;

@@ -400,8 +400,6 @@ int gemm_pick(const GemmArgs& g) {
 
 std::string gemm_label(const GemmArgs& g) {
   if (g.ws) {
-    if (linear_k32_wide(g)) return "linear_k32_kernel<3,128,32,8>";
-    if (linear_k32_bn64(g)) return "linear_k32_kernel<3,64,32,4>";
     return std::string("linear_k32_kernel<") + (g.as ? "3>" : g.pro_scale ? "1>" : g.ln_stats ? "2>" : "0>");
   }
   std::string s = gemm_pick(g) == 0 ? "gemm_kernel<128,128,64,64" : "gemm_kernel<64,64,32,32";

@@ -179,50 +179,6 @@ __device__ __forceinline__ void plane_block(const GemmArgs& g, const float* tile
   };
   const int b = m0 / g.ap_L, tok0 = m0 - b * g.ap_L;
   const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
-  if (g.ap_frag) {  // k / v^T as fragment images (frag_off): the tile is one part of whole heads (linear_k32_ok)
-    int part, h, d;
-    col_map(n0, part, h, d);
-    if (part == 1) {  // k: item (token r, 8-column group c8), 32 consecutive tokens per 32 lanes: 512-B runs
-#pragma unroll 2
-      for (int it = 0; it < 8; ++it) {
-        const int r = (t & 31) + 32 * (it & 3), c8 = (t >> 5) + 8 * (it >> 2);
-        const int col = n0 + 8 * c8;
-        if (col >= g.N || m0 + r >= g.M) continue;
-        col_map(col, part, h, d);
-        const f4 b0 = g.bias ? *reinterpret_cast<const f4*>(g.bias + col) : zero4;
-        const f4 b1 = g.bias ? *reinterpret_cast<const f4*>(g.bias + col + 4) : zero4;
-        const f4 v0 = *reinterpret_cast<const f4*>(tile + r * TP + 8 * c8) + b0;
-        const f4 v1 = *reinterpret_cast<const f4*>(tile + r * TP + 8 * c8 + 4) + b1;
-        const float x[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-        f16x8 hi, lo;
-        split8(1, x, hi, lo);
-        _Float16* p = g.ap_k + ((size_t)b * g.ap_heads + h) * 2 * plane + frag_off(tok0 + r, d, g.ap_L);
-        *reinterpret_cast<f16x8*>(p) = hi;
-        *reinterpret_cast<f16x8*>(p + 512) = lo;
-      }
-      return;
-    }
-    if (part == 2) {  // v^T: item (column c, 8-token group r8), 32 consecutive columns (= d) per 32 lanes
-#pragma unroll 2
-      for (int it = 0; it < 8; ++it) {
-        const int c = (t & 31) + 32 * (it & 3), r8 = (t >> 5) + 8 * (it >> 2);
-        const int col = n0 + c;
-        if (col >= g.N || m0 + 8 * r8 >= g.M) continue;
-        col_map(col, part, h, d);
-        const float bc = g.bias ? g.bias[col] : 0.f;
-        float x[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) x[e] = tile[(8 * r8 + e) * TP + c] + bc;
-        f16x8 hi, lo;
-        split8(2, x, hi, lo);
-        _Float16* p = g.ap_v + ((size_t)b * g.ap_heads + h) * 2 * plane + frag_off(d, tok0 + 8 * r8, Dh);
-        *reinterpret_cast<f16x8*>(p) = hi;
-        *reinterpret_cast<f16x8*>(p + 512) = lo;
-      }
-      return;
-    }
-    // q: the row planes below
-  }
   {  // q / k: item (row, 8-column group), 16 groups per row; a thread keeps its column group
     const int c8 = t & 15, col = n0 + 8 * c8;
     int part, h, d;
@@ -317,10 +273,11 @@ __global__ void __launch_bounds__(256) presplit_a_kernel(GemmArgs g, void* out_)
   if (bad && g.range_flag) *g.range_flag = 1;
 }
 
-// NW = 8 (pre-split A only): 128 x 256 blocks of eight 128 x 32 wave tiles, one block per CU -- the staged A
-// tile feeds twice the MFMA work of the 4-wave block, so the A refills (global loads + LDS stores) per MAC halve.
-template <int PRO, int WM = 128, int WN = 32, int NW = 4>
-__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) linear_k32_kernel(GemmArgs g) {
+// 128 x 128 blocks of four 128 x 32 wave tiles (the 8-wave 128 x 256 and the 128 x 64 forms measured -2 % and -7 %
+// on DiT-XL/2 and were removed in round 5)
+template <int PRO>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) linear_k32_kernel(GemmArgs g) {
+  constexpr int WM = 128, WN = 32, NW = 4;
   constexpr int BM = kLBM, BN = 32 * NW * WM / BM * WN / 32, TM = WM / 16, TN = WN / 16, WD = 2, NWN = BN / WN;
   static_assert((BM / WM) * NWN == NW, "one wave tile per wave");
   static_assert(NW == 4 || PRO == 3, "8 waves: pre-split A only");
@@ -339,9 +296,8 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2,
   // for each of 128 M tiles otherwise); the group's A tiles stay in the XCD's L2 during the sweep.
   const int nN = ceil_div(N, BN), nM = ceil_div(M, BM);
   const int bid = xcd_remap_p(blockIdx.x, gridDim.x);
-  const int LGM = g.lin_gm > 0 ? g.lin_gm : kLGM;
-  const int tgrp = bid / (LGM * nN), gm0 = tgrp * LGM, gsz = min(LGM, nM - gm0);
-  const int r = bid - tgrp * (LGM * nN);
+  const int tgrp = bid / (kLGM * nN), gm0 = tgrp * kLGM, gsz = min(kLGM, nM - gm0);
+  const int r = bid - tgrp * (kLGM * nN);
   const int nt = r / gsz, mt = gm0 + (r - nt * gsz);
   const int m0 = mt * BM, n0 = nt * BN;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -649,12 +605,9 @@ bool linear_k32_ok(const GemmArgs& g) {
   if (g.pro_scale && g.ln_stats) return false;
   if (g.as && (g.pro_scale || g.ln_stats || (reinterpret_cast<uintptr_t>(g.as) & 15) != 0)) return false;
   if (g.c_split && (g.N % 64 != 0 || g.ap_q || (reinterpret_cast<uintptr_t>(g.c_split) & 15) != 0)) return false;
-  if (g.ap_vonly && (!g.ap_q || g.ap_frag || g.ap_legacy)) return false;
+  if (g.ap_vonly && (!g.ap_q || g.ap_legacy)) return false;
   // attention planes: 8-column groups of one head (plane_slab / plane_block), q / k / v never inside one slab
   if (g.ap_q && (g.ap_Dh % 8 != 0 || (g.ap_heads * g.ap_Dh) % 32 != 0 || (g.ap_legacy && g.ap_Dh % 32 != 0)))
-    return false;
-  if (g.ap_frag && (!g.ap_q || g.ap_legacy || (g.ap_heads * g.ap_Dh) % 128 != 0 || g.ap_L % 128 != 0 ||
-                    g.ap_Dh % 32 != 0))
     return false;
   return true;
 }
@@ -675,44 +628,8 @@ int linear_presplit_a(const GemmArgs& g, _Float16* out, hipStream_t st) {
   return DM_OK;
 }
 
-// DM_LIN_BN256 (A/B): 1 = the 8-wave 128 x 256 blocks for pre-split-A GEMMs with N % 256 == 0, 2 = for all N;
-// read per call (plans capture their launches once)
-bool linear_k32_wide(const GemmArgs& g) {
-  const char* e = std::getenv("DM_LIN_BN256");
-  const int w = e ? std::atoi(e) : 0;
-  return g.as && !g.ap_q && (w >= 2 || (w == 1 && g.N % 256 == 0));
-}
-
-// DM_LIN_BN64 (A/B): 128 x 64 blocks of four 64 x 32 wave tiles for pre-split-A GEMMs whose 128 x 128 tiles
-// leave the last round of 512 resident blocks at most half full (DiT-XL/2's N = 1152 proj / fc2 at 2B = 64:
-// 1152 tiles = 2.25 rounds; 2304 half-width tiles = 4.5); 2 = for every pre-split-A GEMM with N % 64 == 0.
-// Same K-step sequence per output element, so bit-identical to the 128 x 128 blocks. Read per call.
-bool linear_k32_bn64(const GemmArgs& g) {
-  const char* e = std::getenv("DM_LIN_BN64");
-  const int w = e ? std::atoi(e) : 0;
-  if (!w || !g.as || g.ap_q || g.c_split || g.N % 64 != 0) return false;
-  if (w >= 2) return true;
-  const long tiles = (long)ceil_div(g.M, kLBM) * ceil_div(g.N, 128), rem = tiles % 512;
-  return rem != 0 && rem <= 256;
-}
-
-int linear_k32(const GemmArgs& g0, hipStream_t st) {
-  DM_REQUIRE(linear_k32_ok(g0), "linear_k32: needs pre-split weights, K % 64 == 0, 16-byte aligned 4-column rows");
-  static const int env_gm = std::getenv("DM_LIN_GM") ? std::atoi(std::getenv("DM_LIN_GM")) : 0;  // tile-order A/B
-  GemmArgs g = g0;
-  if (env_gm > 0 && g.lin_gm == 0) g.lin_gm = env_gm;
-  if (linear_k32_wide(g)) {
-    hipLaunchKernelGGL((linear_k32_kernel<3, 128, 32, 8>), dim3(ceil_div(g.M, kLBM) * ceil_div(g.N, 256)), dim3(512), 0,
-                       st, g);
-    DM_LAUNCH_CHECK();
-    return DM_OK;
-  }
-  if (linear_k32_bn64(g)) {
-    hipLaunchKernelGGL((linear_k32_kernel<3, 64, 32, 4>), dim3(ceil_div(g.M, kLBM) * ceil_div(g.N, 64)), dim3(256), 0,
-                       st, g);
-    DM_LAUNCH_CHECK();
-    return DM_OK;
-  }
+int linear_k32(const GemmArgs& g, hipStream_t st) {
+  DM_REQUIRE(linear_k32_ok(g), "linear_k32: needs pre-split weights, K % 64 == 0, 16-byte aligned 4-column rows");
   const int blocks = ceil_div(g.M, kLBM) * ceil_div(g.N, 128);
   if (g.as)
     hipLaunchKernelGGL(linear_k32_kernel<3>, dim3(blocks), dim3(256), 0, st, g);

@@ -108,11 +108,5 @@ __device__ __forceinline__ void mfma_slice(const float* __restrict__ As, const f
 // Row (within the wave's 32x32 tile) of accumulator register r for lane half lh.
 __device__ __forceinline__ int acc_row(int r, int lh) { return (r & 3) + 8 * (r >> 2) + 4 * lh; }
 
-// Fragment image of an R x Kd operand (row r, contraction index k) of v_mfma_f32_32x32x16_f16 with two fp16
-// pieces: [k / 16][r / 32][piece][lane group (k / 8) % 2][r % 32][8], piece 1 at +512. Lane (lr, lh) of a
-// 32 x 16 fragment reads 16 B at lane * 8: one wave instruction = 1 KiB contiguous per piece.
-__device__ __forceinline__ size_t frag_off(int r, int k, int R) {
-  return ((size_t)(k >> 4) * (R >> 5) + (r >> 5)) * 1024 + ((k >> 3) & 1) * 256 + (r & 31) * 8 + (k & 7);
-}
 
 }  // namespace dm

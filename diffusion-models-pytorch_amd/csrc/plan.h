@@ -113,7 +113,7 @@ struct PlanBase {
   int profile_every = 1;  // record events on every N-th run only (the others run unobserved)
   long runs = 0;
   // hipGraph of the op list (captured on a private stream, launched on the caller's)
-  bool graph_enabled = std::getenv("DM_NO_GRAPH") == nullptr;
+  bool graph_enabled = true;  // Toggles::graph of the plan's build (DM_NO_GRAPH)
   hipGraphExec_t gexec = nullptr;
   hipStream_t cap_stream = nullptr;
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;

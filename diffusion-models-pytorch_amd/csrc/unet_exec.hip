@@ -177,7 +177,7 @@ struct UNetModel {
   bool fallback = false;
   int conv_math = base_math;
   int run_math() const { return base_math == 2 && fallback ? 3 : base_math; }
-  bool range_check = !(std::getenv("DM_RANGE_CHECK") && std::string(std::getenv("DM_RANGE_CHECK")) == "0");
+  bool range_check = toggles().range_check;
   int* range_flag = nullptr;       // device
   int* range_flag_host = nullptr;  // pinned
   // Deferred mode (dm_unet_set_range_deferred): forwards neither read the flag nor sync; the caller
@@ -189,11 +189,12 @@ struct UNetModel {
   size_t split_bytes = 0;
   void split_for(ConvArgs& c);
   // folded single-head attention blocks (attn_block.hip): per block's qkv weights, the fp32 products At, w,
-  // Wg, cb and the fp16x2 fragment images of At and Wg, made at the first fp16x2 plan build
+  // Wg, cb and the fp16x2 fragment images of At and Wg' (Wg with permuted columns), made at the first fp16x2
+  // plan build
   struct FoldW {
     float *at = nullptr, *w = nullptr, *wg = nullptr, *cb = nullptr, *wgp = nullptr;
-    void *at_img = nullptr, *wg_img = nullptr, *wgp_img = nullptr;
-    const float *at_rs = nullptr, *wg_rs = nullptr, *wgp_rs = nullptr;
+    void *at_img = nullptr, *wgp_img = nullptr;
+    const float *at_rs = nullptr, *wgp_rs = nullptr;
   };
   std::map<size_t, FoldW> folds;
   std::vector<void*> fold_mem;
@@ -295,7 +296,7 @@ const UNetModel::FoldW* UNetModel::fold_for(const AttnP& p) {
   void* mem = nullptr;
   const size_t nimg = split_conv_weights_bytes(1, C, C, 2);
   const size_t nf = (3 * CC + 2 * (size_t)C) * sizeof(float);
-  if (hipMalloc(&mem, nf + 3 * nimg + 64) != hipSuccess) {
+  if (hipMalloc(&mem, nf + 2 * nimg + 64) != hipSuccess) {
     (void)hipGetLastError();
     folds[p.wqkv] = FoldW{};  // plan builds stay deterministic: every later build sees the same failure
     return nullptr;
@@ -308,21 +309,18 @@ const UNetModel::FoldW* UNetModel::fold_for(const AttnP& p) {
   f.cb = f.w + C;
   f.wgp = f.cb + C;
   f.at_img = base + ((nf + 15) & ~size_t(15));
-  f.wg_img = static_cast<char*>(f.at_img) + nimg;
-  f.wgp_img = static_cast<char*>(f.wg_img) + nimg;
+  f.wgp_img = static_cast<char*>(f.at_img) + nimg;
   const double s = (double)p.sa * (p.sb != 0.f ? (double)p.sb : 1.0);
   if (attn_fold(P(p.wqkv), P(p.bqkv), P(p.wproj), P(p.bproj), C, s, f.at, f.w, f.wg, f.cb, nullptr) != DM_OK ||
       split_conv_weights(f.at, 1, C, C, C, 1, 2, f.at_img, nullptr) != DM_OK ||
-      split_conv_weights(f.wg, 1, C, C, C, 1, 2, f.wg_img, nullptr) != DM_OK ||
       attn_perm_cols(f.wg, f.wgp, C, nullptr) != DM_OK ||
       split_conv_weights(f.wgp, 1, C, C, C, 1, 2, f.wgp_img, nullptr) != DM_OK || hipDeviceSynchronize() != hipSuccess) {
     folds[p.wqkv] = FoldW{};
     return nullptr;
   }
   f.at_rs = split_conv_rowscale(f.at_img, 1, C, C);
-  f.wg_rs = split_conv_rowscale(f.wg_img, 1, C, C);
   f.wgp_rs = split_conv_rowscale(f.wgp_img, 1, C, C);
-  split_bytes += nf + 3 * nimg;
+  split_bytes += nf + 2 * nimg;
   return &(folds[p.wqkv] = f);
 }
 
@@ -441,6 +439,7 @@ static int unet_create(const dm_unet_arch* arch, const float* const* params, con
   const int expect = count_params(a);
   DM_REQUIRE(n_params == expect, "expected " + std::to_string(expect) + " parameter tensors, got " +
                                      std::to_string(n_params));
+  refresh_toggles();  // the model's arithmetic and range check (member initialisers) from this snapshot
   auto m = std::make_unique<UNetModel>();
   m->arch = a;
   ParamReader rd{params, numels, n_params};
@@ -683,6 +682,7 @@ static int unet_create(const dm_unet_arch* arch, const float* const* params, con
 // ---------------------------------------------------------------------------
 int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
   refresh_toggles();
+  pl.graph_enabled = toggles().graph;
   pl.B = B;
   pl.math = conv_math;
   pl.H = H;
@@ -785,7 +785,7 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
     if (c.upsample == 2 || c.taps != 9 || c.stride != 1 || c.Hout * c.Wout > 16 || conv_pick(c) < 3) return;
     // K32 split tiles (conv_k32.hip): 2 splits (4x4 maps, B = 256: 32.5 us vs 37.8 us with 4, the
     // reduction included); conv_patch3's 16-channel chunks: 4
-    const int ks = std::min(conv_k32_enabled() ? 2 : 4, c.Cin1 / 32);
+    const int ks = std::min(2, c.Cin1 / 32);
     if (ks < 2) return;
     const size_t need = (size_t)ks * c.B * c.Hout * c.Wout * c.Cout;
     if (need > kpart_floats) {
@@ -795,17 +795,12 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
     c.ksplit = ks;
     c.kpart = kpart_ws;
   };
-  static const bool plan_debug = std::getenv("DM_PLAN_DEBUG") != nullptr;  // diagnostics: each conv's shape
   auto add_conv = [&](ConvArgs c) {
     maybe_split(c);
     split_for(c);
     c.k32_resolved = 1 + conv_k32_pick(c);  // one decision for the launch and the label
     double fl, by;
     conv_cost(c, fl, by);
-    if (plan_debug)
-      fprintf(stderr, "[plan] %s B %d %dx%d -> %dx%d Cin %d + %d Cout %d stride %d up %d pro %d gin %d ksplit %d\n",
-              conv_label(c).c_str(), c.B, c.Hin, c.Win, c.Hout, c.Wout, c.Cin1, c.Cin2, c.Cout, c.stride, c.upsample,
-              c.pro_scale != nullptr, c.gin_part != nullptr, c.ksplit);
     add(conv_label(c), fl, by, [=](hipStream_t st) { return conv2d_igemm(c, st); });
   };
   auto add_gemm = [&](const GemmArgs& g) {
@@ -886,7 +881,7 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
   for (const View& cx : concat_x)
     if (cx.p) concat_base.insert(cx.p);
   auto emit_groups = [&](const View& v) -> int {
-    if (std::getenv("DM_GN_NO_UNITS") || !concat_base.count(v.p) || v.pitch == v.C || v.pitch % G != 0) return G;
+    if (!toggles().gn_fusion || !concat_base.count(v.p) || v.pitch == v.C || v.pitch % G != 0) return G;
     const int cpg = v.pitch / G;
     return (v.C % cpg != 0 && cpg % 4 == 0 && v.C % 4 == 0) ? v.C / 4 : G;
   };
@@ -925,7 +920,7 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
   auto gn_stats_concat = [&](const View& v, const View& sk) -> const double2* {
     const int Ch = v.C - sk.C;
     auto ih = gn_ready.find(v.p), is = gn_ready.find(sk.p);
-    if (!std::getenv("DM_GN_NO_CONCAT") && ih != gn_ready.end() && ih->second.C == Ch && is != gn_ready.end() &&
+    if (toggles().gn_fusion && ih != gn_ready.end() && ih->second.C == Ch && is != gn_ready.end() &&
         is->second.C == sk.C && gn_concat_ok(Ch, ih->second.G, sk.C, is->second.G, G)) {
       const double2* ph = ih->second.p;
       const double2* ps = is->second.p;
@@ -972,7 +967,7 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
     // the first ResBlock's GroupNorm statistics (and the last up-path concat's skip slice: skip 0 is never
     // rewritten) from the conv's epilogue
     double2* gp = nullptr;
-    if (conv3x3_small_in_can_emit(H, W, C0, G) && !std::getenv("DM_GN_NO_FIRST")) {
+    if (conv3x3_small_in_can_emit(H, W, C0, G) && toggles().gn_fusion) {
       gp = gn_buf_for(y, G);
       gn_ready[y.p] = {gp, C0, G};
     }
@@ -1082,72 +1077,45 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
       // GroupNorm folded into the QKV projection's A load (modules.py:91-94): one pass over x
       const double2* sta = gn_stats(xin);
       // One head of 256 channels on a 16 x 16 map (the CIFAR UNet's stage-1 blocks): the folded block
-      // (attn_block.hip): g = GroupNorm(x) Wg^T + cb as the fp16x2 g^T plane (linear_k32, GroupNorm prologue),
-      // then T, S, softmax, P g and the residual in one kernel. DM_ATTN_FOLD=0: the unfolded path below.
+      // (attn_block.hip): T, S, softmax, P xn, the folded projection Wg' and the residual in one kernel, no q / k /
+      // v planes. Variant 4 (default): 8 waves of 16 queries (attn_block4_kernel); DM_ATTN=3: the 4-wave form
+      // (attn_block3_kernel, bit-identical); DM_ATTN=0 / unfused / ...: the unfolded path below.
+      const int av = toggles().attn;
       const FoldW* fw = nullptr;
-      if (conv_math == 2 && arch.variant != 2 && attn_block_ok(hw, C, heads) && y.p != xin.p &&
-          !(std::getenv("DM_ATTN_FOLD") && std::getenv("DM_ATTN_FOLD")[0] == '0'))
+      if (conv_math == 2 && arch.variant != 2 && (av == 3 || av == 4) && attn_block_ok(hw, C, heads) && y.p != xin.p)
         fw = fold_for(p);
       if (fw) {
-        GemmArgs gg{};
-        gg.M = B * hw; gg.N = C; gg.K = C; gg.Z1 = 1; gg.Z2 = 1;
-        gg.A = xin.p; gg.lda = xin.pitch; gg.ldc = C; gg.alpha = 1.f;
-        gg.pro_scale = gsc; gg.pro_shift = gsh; gg.pro_rows = hw;
-        gg.split = 2; gg.split_ea = 0; gg.range_flag = range_flag;
-        _Float16* gplane = reinterpret_cast<_Float16*>(qkv);
-        gg.C = qkv;   // unused by the plane epilogue (alignment check only)
-        gg.ap_q = gg.ap_k = gg.ap_v = gplane; gg.ap_vonly = 1;
-        gg.ap_L = hw; gg.ap_heads = 1; gg.ap_Dh = C; gg.ap_ev = 6;
-        gg.Bm = fw->wg; gg.ldb = C; gg.bias = fw->cb;
-        gg.ws = fw->wg_img; gg.ws_rowscale = fw->wg_rs;
         AttnBlockArgs ab{};
         ab.x = xin.p; ab.x_pitch = xin.pitch; ab.gsc = gsc; ab.gsh = gsh;
         ab.at_img = static_cast<const _Float16*>(fw->at_img); ab.at_rowscale = fw->at_rs; ab.w = fw->w;
-        ab.g_plane = gplane; ab.y = y.p; ab.y_pitch = y.pitch; ab.B = B; ab.ex = 6; ab.eg = 6;
+        ab.y = y.p; ab.y_pitch = y.pitch; ab.B = B; ab.ex = 6; ab.eg = 6;
         ab.range_flag = range_flag;
-        // variant 4 (default): values = xn and the folded projection Wg' inside the kernel, no g GEMM, on 8
-        // waves of 16 queries (attn_block4_kernel: 129 us per block; C3 A/B +0.9 % over variant 3, its 4-wave
-        // form at 156 us, bit-identical); DM_ATTN_BLOCK=3: that 4-wave kernel (C3 A/B +2.3 % over variant 2);
-        // DM_ATTN_BLOCK=2: g = xn Wg^T + cb from linear_k32 as the fp16x2 plane, then attn_block_kernel
-        // (113 + 67 us)
-        const char* avs = std::getenv("DM_ATTN_BLOCK");
-        // DM_ATTN_BLOCK=5: variant 4's kernel on 64-query work-groups (two per CU)
-        const int av = avs && avs[0] >= '2' && avs[0] <= '5' ? avs[0] - '0' : 4;
-        const bool v3 = av != 2;
         ab.variant = av;
-        if (v3) {
-          ab.g_plane = nullptr;
-          ab.wg_img = static_cast<const _Float16*>(fw->wgp_img); ab.wg_rowscale = fw->wgp_rs; ab.cb = fw->cb;
-        }
-        // variants 4 / 5 finalize the block's GroupNorm statistics themselves (DM_ATTN_GNFIN=1: gn_finalize)
-        const bool infin = av >= 4 && C % G == 0 && !(std::getenv("DM_ATTN_GNFIN") && std::getenv("DM_ATTN_GNFIN")[0] == '1');
+        ab.wg_img = static_cast<const _Float16*>(fw->wgp_img); ab.wg_rowscale = fw->wgp_rs; ab.cb = fw->cb;
+        // variant 4 finalizes the block's GroupNorm statistics itself (DM_ATTN_GNFIN=1: gn_finalize)
+        const bool infin = av == 4 && C % G == 0 && !toggles().attn_gn_launch;
         if (infin) {
           ab.gin_part = sta; ab.gin_G = G; ab.gin_nchunk = gn_num_chunks(hw);
           ab.gin_gamma = P(p.gn.g); ab.gin_beta = P(p.gn.b); ab.gin_eps = 1e-5f;
+        } else {
+          add("gn_finalize", 0, 8.0 * B * C, [=](hipStream_t st) {
+            return gn_finalize(xin, G, sta, 1e-5f, self->P(p.gn.g), self->P(p.gn.b), gsc, gsh, st);
+          });
         }
-        if (v3 || linear_k32_ok(gg)) {
-          if (!infin)
-            add("gn_finalize", 0, 8.0 * B * C, [=](hipStream_t st) {
-              return gn_finalize(xin, G, sta, 1e-5f, self->P(p.gn.g), self->P(p.gn.b), gsc, gsh, st);
-            });
-          if (!v3) add_gemm(gg);
-          gn_ready.erase(y.p);
-          const int cpg = C / G;
-          if (C % G == 0 && cpg >= 4 && cpg <= 32 && (cpg & (cpg - 1)) == 0) {
-            ab.gn_part = gn_buf_for(y, G);
-            ab.gn_G = G;
-            gn_ready[y.p] = {ab.gn_part, y.C, G};
-          }
-          // v3: T (2 L C^2), S (2 L^2 C), P xn (2 L^2 C), Wg' O (2 L C^2) per image; x read, y written.
-          // v2: T, S, P g; x read, y written, the g^T plane (fp16x2, 4 B per element) read
-          const double fl = 2.0 * B * ((v3 ? 2.0 : 1.0) * hw * C * C + 2.0 * hw * hw * C);
-          const double by = 4.0 * B * hw * C * (v3 ? 2.0 : 3.0);
-          add(av == 5 ? "attn_block4_kernel<4>" : av == 4 ? "attn_block4_kernel<8>" : v3 ? "attn_block3_kernel"
-                                                                                          : "attn_block_kernel", fl, by,
-              [=](hipStream_t st) { return attn_block(ab, st); });
-          x_cur = y;
-          continue;
+        gn_ready.erase(y.p);
+        const int cpg = C / G;
+        if (C % G == 0 && cpg >= 4 && cpg <= 32 && (cpg & (cpg - 1)) == 0) {
+          ab.gn_part = gn_buf_for(y, G);
+          ab.gn_G = G;
+          gn_ready[y.p] = {ab.gn_part, y.C, G};
         }
+        // T (2 L C^2), S (2 L^2 C), P xn (2 L^2 C), Wg' O (2 L C^2) per image; x read, y written
+        const double fl = 2.0 * B * (2.0 * hw * C * C + 2.0 * hw * hw * C);
+        const double by = 4.0 * B * hw * C * 2.0;
+        add(av == 4 ? "attn_block4_kernel<8>" : "attn_block3_kernel", fl, by,
+            [=](hipStream_t st) { return attn_block(ab, st); });
+        x_cur = y;
+        continue;
       }
       GemmArgs gq{};
       gq.M = B * hw; gq.N = 3 * C; gq.K = C; gq.Z1 = 1; gq.Z2 = 1; gq.pick_M = (long)kPickBatch * hw;
@@ -1163,10 +1131,13 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
       // Fused attention (attention.hip) on 16 x 16 maps; with the qkv conv on the split kernel, its epilogue
       // writes q / k / v as the fp16x2 operand planes the fused kernel reads (over the qkv buffer: same bytes)
       // other shapes (ADM's 32^2 and 8^2 blocks): flash attention on the pre-split planes (attn_flash)
+      // (DM_ATTN oracle modes, Toggles::attn: no flash kernel outside the defaults 3 / 4; "fused": no pre-split
+      // planes; "unfused": S GEMM, softmax_rows, PV GEMM; "noproj": proj as its own launch)
       const bool l256 = attn_fused_ok(hw, Dh);
-      const bool flash = !l256 && attn_flash_ok(hw, Dh) && !std::getenv("DM_ATTN_NO_FLASH");
-      bool fuse_attn = conv_math == 2 && (l256 || flash) && !std::getenv("DM_ATTN_UNFUSED");
-      const bool presplit = fuse_attn && conv_pw_ok(cq) && !std::getenv("DM_ATTN_NO_PRESPLIT");
+      const bool attn_default = av == 3 || av == 4;
+      const bool flash = !l256 && attn_flash_ok(hw, Dh) && attn_default;
+      bool fuse_attn = conv_math == 2 && (l256 || flash) && av != kAttnUnfused;
+      const bool presplit = fuse_attn && conv_pw_ok(cq) && av != kAttnFused;
       if (flash && !presplit) fuse_attn = false;   // the flash kernel reads the planes only
       _Float16* planes = reinterpret_cast<_Float16*>(qkv);
       const size_t plane_n = (size_t)B * hw * C * 2;  // fp16 elements of one operand's two planes
@@ -1191,42 +1162,24 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
         gl.ap_alpha = cq.ap_alpha; gl.ap_bscale = cq.ap_bscale;
         gl.ap_ea = cq.ap_ea; gl.ap_eb = cq.ap_eb; gl.ap_ev = cq.ap_ev;
       }
-      const bool qkv_linear = conv_math == 2 && cq.ws && cq.ws_np == 2 && linear_k32_ok(gl) &&
-                              !std::getenv("DM_QKV_NO_LINEAR");
-      // k / v^T as fragment images for attn_presplit_kernel (DM_ATTN_FRAG=1; the L = 256 kernels only). Measured
-      // (tools/attn_stamps.py, same box): the attention block 118.5k -> 89.9k cycles (S 40.9k -> 25.5k, PV 26.4k
-      // -> 14.2k), the qkv epilogue +1.8k; but the forward A/B is -0.6 % (the kernel runs at a lower clock under
-      // the power cap: 2.05 -> 1.90 GHz), so the row planes stay the default.
-      bool frag = false;
-      if (qkv_linear && presplit && l256 && std::getenv("DM_ATTN_FRAG") && std::getenv("DM_ATTN_FRAG")[0] == '1') {
-        GemmArgs gf = gl;
-        gf.ap_frag = 1;
-        gf.as = reinterpret_cast<const _Float16*>(uintptr_t(256));  // as the pre-split GEMM runs it
-        gf.pro_scale = gf.pro_shift = nullptr;
-        frag = linear_k32_ok(gf);
-        gl.ap_frag = frag ? 1 : 0;
-      }
+      const bool qkv_linear = conv_math == 2 && cq.ws && cq.ws_np == 2 && linear_k32_ok(gl);
       if (qkv_linear) {
         add("gn_finalize", 0, 8.0 * B * C, [=](hipStream_t st) {
           return gn_finalize(xin, G, sta, 1e-5f, self->P(p.gn.g), self->P(p.gn.b), gsc, gsh, st);
         });
-        if (!std::getenv("DM_QKV_NO_PRESPLIT")) {
-          // GroupNorm + split of the input once (linear_presplit_a) instead of once per 128-column tile inside
-          // the GEMM: one buffer shared by the attention blocks (the plan's launches are stream-ordered)
-          const size_t need = (size_t)gl.M * gl.K * 4;
-          if (need > qkv_as_bytes) {
-            qkv_as = reinterpret_cast<_Float16*>(alloc(need));
-            qkv_as_bytes = need;
-          }
-          _Float16* asb = qkv_as;
-          add("linear_presplit_a", 0, 8.0 * gl.M * gl.K, [=](hipStream_t st) { return linear_presplit_a(gl, asb, st); });
-          GemmArgs g2 = gl;
-          g2.as = asb;
-          g2.pro_scale = g2.pro_shift = nullptr;
-          add_gemm(g2);
-        } else {
-          add_gemm(gl);
+        // GroupNorm + split of the input once (linear_presplit_a) instead of once per 128-column tile inside
+        // the GEMM: one buffer shared by the attention blocks (the plan's launches are stream-ordered)
+        const size_t need = (size_t)gl.M * gl.K * 4;
+        if (need > qkv_as_bytes) {
+          qkv_as = reinterpret_cast<_Float16*>(alloc(need));
+          qkv_as_bytes = need;
         }
+        _Float16* asb = qkv_as;
+        add("linear_presplit_a", 0, 8.0 * gl.M * gl.K, [=](hipStream_t st) { return linear_presplit_a(gl, asb, st); });
+        GemmArgs g2 = gl;
+        g2.as = asb;
+        g2.pro_scale = g2.pro_shift = nullptr;
+        add_gemm(g2);
       } else if (conv_pw_ok(cq)) {
         gn_prologue(cq, xin, sta, p.gn.g, p.gn.b, nullptr, nullptr, 0);
         add_conv(cq);
@@ -1255,7 +1208,7 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
       if (proj_conv) emit_conv(cp, y);
       // one head of 256 channels (the CIFAR UNet's 16 x 16 attention): proj runs inside the fused kernel on
       // its O rows (O never goes to HBM), same MFMA sequence and epilogue as the MODE 3 launch
-      const bool fuse_proj = presplit && proj_conv && heads == 1 && Dh == 256 && !std::getenv("DM_ATTN_NO_PROJ");
+      const bool fuse_proj = presplit && proj_conv && heads == 1 && Dh == 256 && av != kAttnNoProj;
       if (fuse_attn) {
         // S, softmax and PV in one kernel (attention.hip), bit-identical to the three launches below
         AttnArgs at{};
@@ -1265,7 +1218,6 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
         }
         if (presplit) {
           at.pq = planes; at.pk = planes + plane_n; at.pv = planes + 2 * plane_n;
-          at.frag = frag ? 1 : 0;
         }
         at.qkv = qkv; at.ld = 3 * C; at.L = hw; at.Dh = Dh; at.heads = heads; at.B = B;
         at.q0 = 0; at.k0 = k0; at.v0 = v0; at.hs = hs;

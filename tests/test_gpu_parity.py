@@ -381,23 +381,11 @@ def test_fused_attention_bit_identical(cuda, golden, arch, monkeypatch):
     from models.unet_categorial_adagn import UNetCategorialAdaGN
     outs = {}
     kernel = {'unfused': None, 'fused': 'attn_fused_kernel', 'presplit': 'attn_presplit_kernel',
-              'noproj': 'attn_presplit_kernel', 'frag': 'attn_presplit_kernel'}
-    for mode in ('unfused', 'fused', 'noproj', 'frag', 'presplit'):
-        for var in ('DM_ATTN_UNFUSED', 'DM_ATTN_NO_PRESPLIT', 'DM_ATTN_NO_PROJ', 'DM_ATTN_FRAG'):
-            monkeypatch.delenv(var, raising=False)
-        # the other shapes' flash kernel (AdaGN's 8^2 blocks) is not bit-identical by design: it has its
-        # own test against the unfused path (test_gpu_r3.py test_flash_attention_vs_unfused)
-        monkeypatch.setenv('DM_ATTN_NO_FLASH', '1')
-        # the unfolded kernels (q / k / v planes); the folded block has its own tests (test_gpu_r4.py)
-        monkeypatch.setenv('DM_ATTN_FOLD', '0')
-        if mode == 'unfused':
-            monkeypatch.setenv('DM_ATTN_UNFUSED', '1')
-        elif mode == 'fused':
-            monkeypatch.setenv('DM_ATTN_NO_PRESPLIT', '1')
-        elif mode == 'noproj':
-            monkeypatch.setenv('DM_ATTN_NO_PROJ', '1')
-        elif mode == 'frag':   # k / v^T as fragment images instead of row planes
-            monkeypatch.setenv('DM_ATTN_FRAG', '1')
+              'noproj': 'attn_presplit_kernel'}
+    for mode in ('unfused', 'fused', 'noproj', 'presplit'):
+        # DM_ATTN's unfolded oracle modes: no folded block (it has its own tests, test_gpu_r4.py) and no flash
+        # kernel (AdaGN's 8^2 blocks: not bit-identical by design, test_gpu_r3.py test_flash_attention_vs_unfused)
+        monkeypatch.setenv('DM_ATTN', mode)
         if arch == 'cifar10':
             m, _ = _model(golden('forward')[1], 'cifar10', cuda)
         else:
@@ -412,10 +400,9 @@ def test_fused_attention_bit_identical(cuda, golden, arch, monkeypatch):
         for name in ('attn_fused_kernel', 'attn_presplit_kernel'):
             assert any(lb.startswith(name) for lb in labels) == (kernel[mode] == name), (mode, labels)
         fused_proj = any(lb.endswith(',proj>') for lb in labels)
-        assert fused_proj == (mode in ('presplit', 'frag') and arch == 'cifar10'), (mode, labels)
+        assert fused_proj == (mode == 'presplit' and arch == 'cifar10'), (mode, labels)
     assert torch.equal(outs['fused'], outs['unfused'])
     assert torch.equal(outs['noproj'], outs['unfused'])
-    assert torch.equal(outs['frag'], outs['unfused'])
     assert torch.equal(outs['presplit'], outs['unfused'])
 
 

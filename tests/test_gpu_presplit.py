@@ -3,11 +3,11 @@ rewrite switched off by its environment toggle (read at plan build):
 
 * linear_k32 with the A operand pre-split once per GEMM (`linear_presplit_a`, `row_stats_split`, fc1's
   epilogue writing fc2's pre-split A) against the split inside the GEMM: the same fp32 expressions, so
-  the outputs are bit-identical (DiT: DM_DIT_PRESPLIT=0; the UNet attention qkv: DM_QKV_NO_PRESPLIT);
-* GroupNorm partials emitted by producers instead of a `gn_partial` pass over the tensor: a concat's
-  combined from its slices' partials (`gn_concat_stats`; DM_GN_NO_CONCAT), the 4-channel units the h slice
-  of a 384 = 256 + 128 concat emits (DM_GN_NO_UNITS), the first conv's epilogue (DM_GN_NO_FIRST): the same
-  sums in another fp64 order, so equal to within a few fp32 ulps of the output.
+  the outputs are bit-identical (DiT: DM_DIT_PRESPLIT=0);
+* GroupNorm partials emitted by producers instead of a `gn_partial` pass over the tensor (DM_GN_FUSION=0 turns
+  all of them off): a concat's combined from its slices' partials (`gn_concat_stats`), the 4-channel units the
+  h slice of a 384 = 256 + 128 concat emits, the first conv's epilogue, the sub-pixel upsample's epilogue: the
+  same sums in another fp64 order, so equal to within a few fp32 ulps of the output.
 """
 import os
 
@@ -78,18 +78,9 @@ def unet_case(cuda):
     return ref.state_dict(), x, t
 
 
-def test_unet_qkv_presplit_bit_identical(cuda, unet_case):
+def test_unet_emitted_gn_stats(cuda, unet_case):
     sd, x, t = unet_case
-    on = _with_env('DM_QKV_NO_PRESPLIT', None, lambda: _unet_out(cuda, sd, x, t))
-    off = _with_env('DM_QKV_NO_PRESPLIT', '1', lambda: _unet_out(cuda, sd, x, t))
-    assert torch.isfinite(on).all()
-    assert torch.equal(on, off), (on - off).abs().max().item()
-
-
-@pytest.mark.parametrize('toggle', ['DM_GN_NO_CONCAT', 'DM_GN_NO_UNITS', 'DM_GN_NO_FIRST'])
-def test_unet_emitted_gn_stats(cuda, unet_case, toggle):
-    sd, x, t = unet_case
-    on = _with_env(toggle, None, lambda: _unet_out(cuda, sd, x, t))
-    off = _with_env(toggle, '1', lambda: _unet_out(cuda, sd, x, t))
+    on = _with_env('DM_GN_FUSION', None, lambda: _unet_out(cuda, sd, x, t))
+    off = _with_env('DM_GN_FUSION', '0', lambda: _unet_out(cuda, sd, x, t))
     scale = off.abs().max().item()
     assert (on - off).abs().max().item() <= 1e-6 * scale

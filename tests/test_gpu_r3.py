@@ -346,8 +346,7 @@ def test_flash_attention_vs_unfused(cuda, golden, report, monkeypatch, case):
     outs = {}
     for mode in ('flash', 'unfused'):
         if mode == 'unfused':
-            monkeypatch.setenv('DM_ATTN_NO_FLASH', '1')
-            monkeypatch.setenv('DM_DIT_ATTN_UNFUSED', '1')
+            monkeypatch.setenv('DM_ATTN', 'unfused')
         gen = torch.Generator().manual_seed(21)
         if case == 'adagn':
             m = UNetCategorialAdaGN(**golden('adagn')[1]['archs']['cfg_cifar10']).eval()

@@ -1,13 +1,12 @@
 """Round-4 GPU tests.
 
-* the folded single-head attention block (attn_block.hip, variants 2-5) against the unfolded path (q / k / v /
-  proj as the reference computes them, DM_ATTN_FOLD=0) and the reference fixtures (models/modules.py:77-102,
+* the folded single-head attention block (attn_block.hip, variants 3 and 4) against the unfolded path (q / k / v /
+  proj as the reference computes them, DM_ATTN=0) and the reference fixtures (models/modules.py:77-102,
   models/unet.py:121-152);
 * DiT-XL/2 per-step accuracy vs float64 and the 2^-20 chaos envelope (models/dit/model.py:234-252; parity
   unpinned, timm absent);
 * the K32 convs added this round: small-map 8 waves, stride-2 tiles (models/modules.py:70-72), 2-D tiles of
-  wide maps incl. the sub-pixel upsample (models/adm/unet.py:162-275), each against the path it replaces;
-* the 8-wave 128 x 256 linear_k32 blocks (DiT token GEMMs) bit for bit against the 4-wave form.
+  wide maps incl. the sub-pixel upsample (models/adm/unet.py:162-275), each against the path it replaces.
 """
 import numpy as np
 import pytest
@@ -30,15 +29,13 @@ def _labels(h):
     return [op['label'] for op in dmhip.unet_profile_read(h)]
 
 
-@pytest.mark.parametrize('B,variant', [(2, '3'), (7, '3'), (3, '2'), (5, '4'), (3, '5')])
+@pytest.mark.parametrize('B,variant', [(2, '3'), (7, '3'), (5, '4'), (3, '4')])
 def test_folded_attention_vs_unfolded(cuda, golden, monkeypatch, B, variant):
     """The CIFAR-10 UNet's five 16 x 16 attention blocks run folded (variant 4, the default, and 3:
-    attn_block4_kernel / attn_block3_kernel alone; variant 2: g GEMM + attn_block_kernel; no q / k / v planes in
-    any): whole forwards within 1e-5 of the unfolded path (same weights, same inputs), and the folded kernels
-    are the ones in the plan."""
-    monkeypatch.setenv('DM_ATTN_BLOCK', variant)
-    kname = {'2': 'attn_block_kernel', '3': 'attn_block3_kernel', '4': 'attn_block4_kernel<8>',
-             '5': 'attn_block4_kernel<4>'}[variant]
+    attn_block4_kernel / attn_block3_kernel alone, no q / k / v planes): whole forwards within 1e-5 of the
+    unfolded path (same weights, same inputs), and the folded kernels are the ones in the plan."""
+    monkeypatch.setenv('DM_ATTN', variant)
+    kname = {'3': 'attn_block3_kernel', '4': 'attn_block4_kernel<8>'}[variant]
     _, meta = golden('forward')
     g = torch.Generator().manual_seed(31)
     x = torch.randn((B, 3, 32, 32), generator=g).to(cuda)
@@ -51,9 +48,9 @@ def test_folded_attention_vs_unfolded(cuda, golden, monkeypatch, B, variant):
     labels = _labels(h)
     dmhip.unet_profile_enable(h, 0)
     assert labels.count(kname) == 5, labels
-    assert any(lb.startswith('linear_k32_kernel') for lb in labels) == (variant == '2')
+    assert not any(lb.startswith('linear_k32_kernel') for lb in labels)
     assert not any(lb.startswith('attn_presplit_kernel') for lb in labels)
-    monkeypatch.setenv('DM_ATTN_FOLD', '0')
+    monkeypatch.setenv('DM_ATTN', '0')
     unfolded, _ = _model(meta, 'cifar10', cuda)
     out_u = unfolded(x, t)
     err = (out_f - out_u).abs().max().item()
@@ -72,11 +69,11 @@ def test_folded_attention_vs_reference(cuda, golden, report):
     assert err <= TOL, err
 
 
-@pytest.mark.parametrize('variant', ['2', '3', '4'])
+@pytest.mark.parametrize('variant', ['3', '4'])
 def test_folded_attention_batch_invariance(cuda, golden, monkeypatch, variant):
     """B = 256 (the benchmark batch) rows equal the B = 3 forward's rows bit for bit: every work-group is one
     (image, query half) and reads only its image."""
-    monkeypatch.setenv('DM_ATTN_BLOCK', variant)
+    monkeypatch.setenv('DM_ATTN', variant)
     _, meta = golden('forward')
     model, _ = _model(meta, 'cifar10', cuda)
     g = torch.Generator().manual_seed(32)
@@ -89,42 +86,19 @@ def test_folded_attention_batch_invariance(cuda, golden, monkeypatch, variant):
 
 
 def test_folded_attention_8_waves_bit_identical(cuda, golden, monkeypatch):
-    """Variants 4 (8 waves of 16 queries) and 5 (4 waves of 16 queries, two work-groups per CU) run variant
-    3's MFMA sequence per output element with the same staging layouts and scales: whole forwards equal bit for
-    bit."""
+    """Variant 4 (8 waves of 16 queries) runs variant 3's MFMA sequence per output element with the same staging
+    layouts and scales: whole forwards equal bit for bit."""
     _, meta = golden('forward')
     g = torch.Generator().manual_seed(34)
     x = torch.randn((4, 3, 32, 32), generator=g).to(cuda)
     t = torch.randint(0, 1000, (4, ), generator=g).to(cuda)
     outs = {}
-    for v in ('3', '4', '5'):
-        monkeypatch.setenv('DM_ATTN_BLOCK', v)
+    for v in ('3', '4'):
+        monkeypatch.setenv('DM_ATTN', v)
         model, _ = _model(meta, 'cifar10', cuda)
         outs[v] = model(x, t)
         del model
     assert torch.equal(outs['3'], outs['4'])
-    assert torch.equal(outs['3'], outs['5'])
-
-
-@pytest.mark.parametrize('opt', ['2', '4'])
-def test_folded_attention_opt_variants_bit_identical(cuda, golden, monkeypatch, opt):
-    """Variant 4's scheduling options run the same operations per accumulator in the same order: DM_ATTN_OPT=2
-    (S operands read one key step ahead) and DM_ATTN_OPT=4 (the key pass software-pipelined over three key-chunk
-    images, each chunk's softmax between the previous chunk's P V MFMAs) give whole forwards equal to the plain
-    loop's bit for bit (B = 4 and the batch-invariant B = 7)."""
-    _, meta = golden('forward')
-    g = torch.Generator().manual_seed(36)
-    x = torch.randn((7, 3, 32, 32), generator=g).to(cuda)
-    t = torch.randint(0, 1000, (7, ), generator=g).to(cuda)
-    outs = {}
-    for mode in ('plain', opt):
-        if mode != 'plain':
-            monkeypatch.setenv('DM_ATTN_OPT', opt)
-        model, _ = _model(meta, 'cifar10', cuda)
-        outs[mode] = (model(x[:4], t[:4]), model(x, t))
-        del model
-    assert torch.equal(outs['plain'][0], outs[opt][0])
-    assert torch.equal(outs['plain'][1], outs[opt][1])
 
 
 def test_attention_in_kernel_gn_finalize_bit_identical(cuda, golden, monkeypatch):
@@ -392,68 +366,6 @@ def test_adm256_t2d_vs_row_segments(cuda, golden, report, monkeypatch):  # noqa:
     report('adm256_t2d_maxabs_vs_reference', ref_err)
     assert err <= 1e-5, err
     assert ref_err <= TOL, ref_err
-
-
-# ------------------------------------------------------------------ 8-wave 128 x 256 linear_k32 blocks (DiT)
-@pytest.mark.parametrize('wide', ['1', '2'])
-def test_linear_k32_wide_blocks_bit_identical(cuda, golden, monkeypatch, wide):
-    """DiT-S/2 (oracle fixture config) with its pre-split-A token GEMMs on the 8-wave 128 x 256 blocks
-    (DM_LIN_BN256=1: N % 256 == 0 only; 2: all, ragged last tiles) equals the 4-wave 128 x 128 form bit for bit
-    (same MFMA sequence per output element), and the wide kernel is in the plan."""
-    from models.dit.model import DiT
-    g, meta = golden('dit')
-    name = 'dit_s2'
-    x = torch.from_numpy(g[f'{name}_x']).to(cuda)
-    t = torch.from_numpy(g[f'{name}_t']).to(cuda)
-    y = torch.from_numpy(g[f'{name}_labels']).to(cuda)
-    outs = {}
-    for mode in ('base', 'wide'):
-        if mode == 'wide':
-            monkeypatch.setenv('DM_LIN_BN256', wide)
-        m = DiT(**meta['archs'][name]).eval()
-        init_synthetic_(m)
-        m = m.to(cuda)
-        outs[mode] = m(x, t, y).cpu()
-        h = m.native_handle(torch.device(cuda))
-        dmhip.unet_profile_enable(h, 1, m._abi)
-        m(x, t, y)
-        labels = [op['label'] for op in dmhip.unet_profile_read(h, m._abi)]
-        dmhip.unet_profile_enable(h, 0, m._abi)
-        assert ('linear_k32_kernel<3,128,32,8>' in labels) == (mode == 'wide'), labels
-        del m
-    assert torch.equal(outs['base'], outs['wide'])
-    err = (outs['wide'] - torch.from_numpy(g[f'{name}_out_y'])).abs().max().item()
-    assert err <= TOL, err
-
-
-def test_linear_k32_half_width_blocks_bit_identical(cuda, golden, monkeypatch):
-    """DiT-S/2 with its pre-split-A token GEMMs on 128 x 64 blocks of 64 x 32 wave tiles (DM_LIN_BN64=2; =1 picks
-    them where the 128 x 128 tiles leave the last round of resident blocks at most half full) equals the 128 x 128
-    form bit for bit (same K-step sequence per output element), and the half-width kernel is in the plan."""
-    from models.dit.model import DiT
-    g, meta = golden('dit')
-    name = 'dit_s2'
-    x = torch.from_numpy(g[f'{name}_x']).to(cuda)
-    t = torch.from_numpy(g[f'{name}_t']).to(cuda)
-    y = torch.from_numpy(g[f'{name}_labels']).to(cuda)
-    outs = {}
-    for mode in ('base', 'bn64'):
-        if mode == 'bn64':
-            monkeypatch.setenv('DM_LIN_BN64', '2')
-        m = DiT(**meta['archs'][name]).eval()
-        init_synthetic_(m)
-        m = m.to(cuda)
-        outs[mode] = m(x, t, y).cpu()
-        h = m.native_handle(torch.device(cuda))
-        dmhip.unet_profile_enable(h, 1, m._abi)
-        m(x, t, y)
-        labels = [op['label'] for op in dmhip.unet_profile_read(h, m._abi)]
-        dmhip.unet_profile_enable(h, 0, m._abi)
-        assert ('linear_k32_kernel<3,64,32,4>' in labels) == (mode == 'bn64'), labels
-        del m
-    assert torch.equal(outs['base'], outs['bn64'])
-    err = (outs['bn64'] - torch.from_numpy(g[f'{name}_out_y'])).abs().max().item()
-    assert err <= TOL, err
 
 
 def test_k32_8x8_single_image_tiles_bit_identical(cuda, golden, monkeypatch):

@@ -19,14 +19,16 @@ run pmc_fetch_$TAG 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/p
     python3 $BENCH --steps 1 --warmup 0 --respace-steps 2
 run pmc_write_$TAG 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write_$TAG -o write -- \
     python3 $BENCH --steps 1 --warmup 0 --respace-steps 2
-python3 tools/rocpd_report.py --tag $TAG --workload $WL \
+BUILD=$(python3 -c "import sys; sys.path.insert(0, 'diffusion-models-pytorch_amd'); import dmhip; print(dmhip.build_info())")
+python3 tools/rocpd_report.py --tag $TAG --workload $WL --build "$BUILD" \
     --trace "$(find gpurun_out/prof_$TAG -name 'trace_results.db' | head -n 1)" \
     --fetch "$(find gpurun_out/pmc_fetch_$TAG -name 'fetch_results.db' | head -n 1)" \
     --write "$(find gpurun_out/pmc_write_$TAG -name 'write_results.db' | head -n 1)" \
     --command "rocprofv3 --pmc FETCH_SIZE|WRITE_SIZE --kernel-trace -- python3 $BENCH --steps 1 --warmup 0 --respace-steps 2" \
     > gpurun_out/report_$TAG.log 2>&1 || { echo "report failed"; cat gpurun_out/report_$TAG.log; }
 else
-python3 tools/rocpd_report.py --tag $TAG --workload $WL \
+BUILD=$(python3 -c "import sys; sys.path.insert(0, 'diffusion-models-pytorch_amd'); import dmhip; print(dmhip.build_info())")
+python3 tools/rocpd_report.py --tag $TAG --workload $WL --build "$BUILD" \
     --trace "$(find gpurun_out/prof_$TAG -name 'trace_results.db' | head -n 1)" > gpurun_out/report_$TAG.log 2>&1
 fi
 cat gpurun_out/report_$TAG.log

@@ -44,6 +44,14 @@ def kernel_stats(db):
     return rows
 
 
+def calls_by_name(db):
+    c = sqlite3.connect(db)
+    agg = defaultdict(int)
+    for (name, ) in c.execute('select name from kernels'):
+        agg[short(name)] += 1
+    return agg
+
+
 def pmc(db, counter):
     c = sqlite3.connect(db)
     agg = defaultdict(list)
@@ -60,6 +68,7 @@ def main():
     ap.add_argument('--tag', default='r01')
     ap.add_argument('--command', default='')
     ap.add_argument('--workload', default='c3')
+    ap.add_argument('--build', default=None, help='dm_build_info() of the library the passes ran')
     args = ap.parse_args()
     out_dir = os.path.join(ROOT, 'profiles')
     os.makedirs(out_dir, exist_ok=True)
@@ -77,14 +86,20 @@ def main():
         fetch = pmc(args.fetch, 'FETCH_SIZE')
         write = pmc(args.write, 'WRITE_SIZE')
         res = {}
+        # launches per denoising step of each kernel in the FETCH pass: its dispatches over the sampler update's
+        # (one per step); bench.py's roofline takes this summary's traffic only for the same build and the same count
+        calls = calls_by_name(args.fetch)
+        steps = calls.get('sampler_step_kernel', 0)
         for name in set(fetch) | set(write):
             rb = 2 * 1024 * fetch.get(name, 0.0)
             wb = 1024 * write.get(name, 0.0)
-            res[short(name)] = dict(read_bytes_per_launch=rb, write_bytes_per_launch=wb, hbm_bytes_per_launch=rb + wb,
-                                    fetch_size_kib=fetch.get(name), write_size_kib=write.get(name))
+            k = short(name)
+            res[k] = dict(read_bytes_per_launch=rb, write_bytes_per_launch=wb, hbm_bytes_per_launch=rb + wb,
+                          fetch_size_kib=fetch.get(name), write_size_kib=write.get(name), calls=calls.get(k, 0),
+                          launches_per_step=(calls.get(k, 0) / steps) if steps else None)
         meta = dict(note='read = 2 x FETCH_SIZE (gfx950 half-count of 16B/lane coalesced reads); '
                          'write = WRITE_SIZE (exact for 16B stores, uncalibrated for 4B stores)',
-                    command=args.command, workload=args.workload, kernels=res)
+                    command=args.command, workload=args.workload, build=args.build, sampler_steps=steps, kernels=res)
         path = os.path.join(out_dir, f'{args.tag}_pmc.json')
         with open(path, 'w') as f:
             json.dump(meta, f, indent=1, sort_keys=True)

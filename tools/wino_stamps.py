@@ -50,6 +50,11 @@ def main():
               f'share {v.mean() / tot.mean():.3f}')
     print(f'  main loop cycles per chunk {(loop / ntile).mean() / (Cin // 32):.0f} '
           f'(MFMA floor 4608 per SIMD: 2 waves x 144 x 16)')
+    nck = ntile * (Cin // 32)
+    for role, (a, b, c) in (('early (wave 0): finish | MFMAs | barrier', (11, 12, 13)),
+                            ('late  (wave 4): MFMAs | finish | barrier', (14, 15, 7))):
+        print(f'  {role}: per chunk {(s[:, a] / nck).mean():6.0f} | {(s[:, b] / nck).mean():6.0f} | '
+              f'{(s[:, c] / nck).mean():6.0f}')
     print(f'  block wall us mean {((rt1 - rt0) / 100.0).mean():.2f}, clock GHz mean {clk.mean():.3f}')
 
 
