@@ -164,7 +164,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   const int l16 = lane & 15, q = lane >> 4;
   const int lj = lane & (NP - 1);  // loader: pair lj of the lane's unit
 #ifndef DM_WINO_XSET
-#define DM_WINO_XSET 0
+#define DM_WINO_XSET 1
 #endif
   // Set s covers 16-lane rows 4 s .. 4 s + 3, unit u = row (W 32) or 2 row + (lane & 15) / 8 (W 16): patch row u / 8
   // -- s / 2 or s, the same for the wave's lanes -- and channels 4 (u & 7) .. + 3, the same in both of its sets (s and
@@ -475,12 +475,13 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   auto chunk = [&](int c, auto cc_c, auto late_c) DM_WINO_INL {
     constexpr int CC = decltype(cc_c)::value;
     constexpr bool LATE = decltype(late_c)::value;
-    const int gn = min(c + 1, nch - 1);  // after the last chunk: refilled into the unused buffer
+    // the next chunk's finish and the one after's pixel loads: skipped (a uniform branch) past the tile's last chunk
+    const bool more = c + 1 < nch, more2 = c + 2 < nch;
     W_PH(0);
 #if DM_WINO_ABL != 1 && DM_WINO_ABL != 3
     if (!LATE) {
-      finish(gn, (c + 1) & 1);
-      load_raw(min(c + 2, nch - 1));
+      if (more) finish(c + 1, (c + 1) & 1);
+      if (more2) load_raw(c + 2);
       W_PH(1);
     }
 #endif
@@ -507,8 +508,8 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
       __builtin_amdgcn_s_setprio(0);
 #endif
       W_PH(1);
-      finish(gn, (c + 1) & 1);
-      load_raw(min(c + 2, nch - 1));
+      if (more) finish(c + 1, (c + 1) & 1);
+      if (more2) load_raw(c + 2);
     }
 #endif
     W_PH(2);
@@ -530,10 +531,13 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     constexpr int CC = decltype(cc_c)::value;
     constexpr bool LATE = decltype(late_c)::value;
     const int g = nch + st, buf = g & 1;
+    const bool more = st + 1 < ns, more2 = st + 2 < ns;
     if (!LATE) {
-      finish_sc(buf ^ 1, 0);  // stage min(g + 1, last): a shortcut step (its pixels loaded a stage ahead)
-      finish_sc(buf ^ 1, 1);
-      load_sc(min(st + 2, ns - 1));
+      if (more) {
+        finish_sc(buf ^ 1, 0);  // stage g + 1: a shortcut step (its pixels loaded a stage ahead)
+        finish_sc(buf ^ 1, 1);
+      }
+      if (more2) load_sc(st + 2);
     }
     const _Float16* As = patch + buf * kWBuf + (nu * 64 + l16) * kWRowH + q * 8;
     a0[0] = *reinterpret_cast<const f16x8*>(As);
@@ -557,9 +561,11 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     load_b(bq[CC], step_off(kt_end + st + WD));
     __builtin_amdgcn_sched_barrier(0);
     if (LATE) {
-      finish_sc(buf ^ 1, 0);
-      finish_sc(buf ^ 1, 1);
-      load_sc(min(st + 2, ns - 1));
+      if (more) {
+        finish_sc(buf ^ 1, 0);
+        finish_sc(buf ^ 1, 1);
+      }
+      if (more2) load_sc(st + 2);
     }
     __syncthreads();
   };
