@@ -5,7 +5,7 @@ spill (556-968 B per lane, -Rpass-analysis=kernel-resource-usage): their phase s
 all) describe the spilled build, not the product kernel; variant 2 does not spill.
 
     make -C diffusion-models-pytorch_amd/csrc BUILD=build_stamps OUT=../../tools/lib/libdm_stamps.so EXTRA=-DDM_K32_STAMPS
-    DM_HIP_LIB=tools/lib/libdm_stamps.so [DM_ATTN_BLOCK=2] python tools/ab_stamps.py
+    DM_HIP_LIB=tools/lib/libdm_stamps.so [DM_ATTN=3] python tools/ab_stamps.py
 """
 import ctypes
 import os
@@ -40,14 +40,10 @@ def main():
     L.dm_debug_ab_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
     assert L.dm_debug_ab_stamps(buf.ctypes.data, nblk) == 0
     s = buf.astype(np.int64)
-    if os.environ.get("DM_ATTN_BLOCK", "4") == "2":
-        names = ['T (At xn^T)', 'T finalize + split', 'S (xn T^T)', 'softmax', 'P g', 'epilogue']
-    else:
-        names = ['T (At xn^T)', 'T finalize + split', 'keys: S + softmax + P xn', 'O finalize', 'Y = Wg O',
-                 'epilogue']
+    names = ['T (At xn^T)', 'T finalize + split', 'keys: S + softmax + P xn', 'O finalize', 'Y = Wg O', 'epilogue']
     tot = s[:, 6] - s[:, 0]
     wall = s[:, 9] - s[:, 8]
-    print(f'attn_block kernel (variant {os.environ.get("DM_ATTN_BLOCK", "4")}): {nblk} work-groups, wall (stamps) {(s[:, 9].max() - s[:, 8].min()) / 100.0:.1f} us, '
+    print(f'attn_block kernel (variant {os.environ.get("DM_ATTN", "4")}): {nblk} work-groups, wall (stamps) {(s[:, 9].max() - s[:, 8].min()) / 100.0:.1f} us, '
           f'work-group cycles mean {tot.mean():.0f}, clock {np.mean(tot / np.maximum(wall, 1)) / 100:.3f} GHz')
     for i, n in enumerate(names):
         v = s[:, i + 1] - s[:, i]

@@ -35,11 +35,9 @@ def build(which):
 
 def run(which, mode, iters):
     if mode == 'unfused':
-        os.environ['DM_ATTN_NO_FLASH'] = '1'
-        os.environ['DM_DIT_ATTN_UNFUSED'] = '1'
+        os.environ['DM_ATTN'] = 'unfused'
     else:
-        os.environ.pop('DM_ATTN_NO_FLASH', None)
-        os.environ.pop('DM_DIT_ATTN_UNFUSED', None)
+        os.environ.pop('DM_ATTN', None)
     dev = torch.device('cuda', 0)
     m, B, shape = build(which)
     m = m.to(dev)

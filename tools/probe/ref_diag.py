@@ -21,9 +21,9 @@ def main():
     t = torch.from_numpy(z['cifar10_t']).to(cuda)
     ref = torch.from_numpy(z['cifar10_y'])
     print('x absmax', float(x.abs().max()), 't', t.tolist(), flush=True)
-    for env in ([], [('DM_CONV_K32S2', '0')], [('DM_ATTN_BLOCK', '2')], [('DM_ATTN_FOLD', '0')],
-                [('DM_ATTN_BLOCK', '4')], [('DM_CONV_K32S2', '0'), ('DM_ATTN_FOLD', '0')]):
-        for k in ('DM_CONV_K32S2', 'DM_ATTN_BLOCK', 'DM_ATTN_FOLD'):
+    for env in ([], [('DM_CONV_K32S2', '0')], [('DM_ATTN', '3')], [('DM_ATTN', '0')],
+                [('DM_ATTN', '4')], [('DM_CONV_K32S2', '0'), ('DM_ATTN', '0')]):
+        for k in ('DM_CONV_K32S2', 'DM_ATTN'):
             os.environ.pop(k, None)
         for k, v in env:
             os.environ[k] = v

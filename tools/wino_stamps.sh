@@ -3,7 +3,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
-T=${T:-r5_st}
+T=${T:-wino_st}
 for lib in $LIBS; do
   for sh in ${SHAPES:-res32_128 res16_256}; do
     echo "== $lib"
