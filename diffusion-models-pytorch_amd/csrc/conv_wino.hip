@@ -129,10 +129,14 @@ __device__ __forceinline__ float dpp_f(float v, int ctrl_shr) {
 template <int W, int PROM, bool SC>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) conv_wino_kernel(ConvArgs a) {
   constexpr bool PRO = PROM != 0;
-  constexpr int NP = W / 2, TH = 128 / W, PR = TH + 2, NR = PR * NP;
+  // a 128-pixel tile: 128 / W whole rows of one image (W 32, 16) or two whole 8 x 8 images (W 8); per image RIMG
+  // output rows and PRI = RIMG + 2 patch rows (the halo)
+  constexpr int IMGS = W == 8 ? 2 : 1, RIMG = 128 / W / IMGS, PRI = RIMG + 2;
+  constexpr int NP = W / 2, PR = IMGS * PRI, NR = PR * NP;
   static_assert(NR <= kWNR, "patch plane");
   // loader units (patch row, 4-channel eighth of the chunk) of NP lanes, 64 / NP per wave instruction: NSET = 12
-  // (W 32) / 10 (W 16) full sets over the 8 waves -- set s = w and, for the first NSET - 8 waves of one role, 8 + w'
+  // (W 32) / 10 (W 16, W 8) full sets over the 8 waves -- set s = w and, for the first NSET - 8 waves of one role,
+  // 8 + w'
   constexpr int NSET = PR * 8 * NP / 64;
   static_assert(NSET * 64 == PR * 8 * NP && NSET > 8 && NSET <= 16, "loader sets");
   constexpr int TM = 4, TN = 4, NTAP = 3;
@@ -143,7 +147,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
                                  // is consumed WD tap rows later
   __shared__ __attribute__((aligned(16))) char smem[kWSmem];
   __shared__ __attribute__((aligned(16))) float gtab[kWTab];  // the image's GroupNorm tables (all its tiles)
-  __shared__ float gstat[2 * kWMaxG];
+  __shared__ float gstat[IMGS * 2 * kWMaxG];
   __shared__ double gxr[8 * 16 * 2];
   __shared__ __attribute__((aligned(16))) float gzero[8];  // the padding rows' table: 0 scale, 0 shift
   _Float16* patch = reinterpret_cast<_Float16*>(smem);
@@ -151,11 +155,13 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   const int HW = a.Hout * W;
   const int M = a.B * HW, N = a.Cout;
   const int nN = N / 128;
-  // persistent blocks over the tiles of ONE image (its GroupNorm tables built once): grid = B x parts, block
-  // (image b0, part) takes tiles part * tpb .. + tpb - 1 of the image's (HW / 128) x nN, row tiles outer
-  const int parts = gridDim.x / a.B;
-  const int b0 = blockIdx.x / parts, part = blockIdx.x - b0 * parts;
-  const int tpb = (HW / 128) * nN / parts;
+  // persistent blocks over the tiles of ONE image (two for 8 x 8 maps; their GroupNorm tables built once): grid =
+  // ceil(B / IMGS) x parts, block (images b0 .., part) takes tiles part * tpb .. + tpb - 1 of the group's
+  // (IMGS HW / 128) x nN, row tiles outer
+  const int parts = gridDim.x / ceil_div(a.B, IMGS);
+  const int g0 = blockIdx.x / parts, part = blockIdx.x - g0 * parts;
+  const int b0 = g0 * IMGS;
+  const int tpb = (IMGS * HW / 128) * nN / parts;
   const int t_first = part * tpb, t_end = t_first + tpb;
   W_RSTAMP(5);
   W_STAMP(0);
@@ -166,18 +172,22 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
 #ifndef DM_WINO_XSET
 #define DM_WINO_XSET 1
 #endif
-  // Set s covers 16-lane rows 4 s .. 4 s + 3, unit u = row (W 32) or 2 row + (lane & 15) / 8 (W 16): patch row u / 8
-  // -- s / 2 or s, the same for the wave's lanes -- and channels 4 (u & 7) .. + 3, the same in both of its sets (s and
-  // s + 8). The NSET - 8 extra sets go to waves 0.. of the early role (XSET 0) or of the late role (XSET 1).
+  // Set s covers 16-lane rows 4 s .. 4 s + 3, unit u = row (W 32), 2 row + (lane & 15) / 8 (W 16) or 4 row +
+  // (lane & 15) / 4 (W 8): patch row u / 8 -- s / 2, s (the same for the wave's lanes) or 2 s + lane / 32 -- and
+  // channels 4 (u & 7) .. + 3, the same in both of a wave's sets (s and s + 8). The NSET - 8 extra sets go to waves
+  // 0.. of the early role (XSET 0) or of the late role (XSET 1).
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   const int xw = DM_WINO_XSET ? wave_u - 4 : wave_u;
   const bool has2 = xw >= 0 && xw < NSET - 8;
-  const int loff = NP == 16 ? 16 * (wave_u & 1) + 4 * (lane >> 4) : 4 * (lane >> 3);
-  int lpr[2];
+  const int loff = NP == 16 ? 16 * (wave_u & 1) + 4 * (lane >> 4)
+                 : NP == 8  ? 4 * (lane >> 3)
+                            : 16 * ((lane >> 4) & 1) + 4 * ((lane >> 2) & 3);
+  int lpr[2], ltab[2];  // per set: patch row, the offset of its image's GroupNorm table
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const int s_ = k ? 8 + max(xw, 0) : wave_u;
-    lpr[k] = min(NP == 16 ? s_ >> 1 : s_, PR - 1);
+    lpr[k] = min(NP == 16 ? s_ >> 1 : NP == 8 ? s_ : 2 * s_ + (lane >> 5), PR - 1);
+    ltab[k] = IMGS == 1 ? 0 : (lpr[k] / PRI) * 2 * a.Cin1;
   }
   const int ldst = lj * kWRowH + loff;  // the lane's offset in a patch row group
   const int Kp = NTAP * a.Cin1 + (SC ? a.Cin2 / 2 : 0);  // K of each U matrix (their stride in the image)
@@ -199,9 +209,10 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     n0 = nt * 128;
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-      const int iy = mt * TH - 1 + lpr[k];
-      rok[k] = iy >= 0 && iy < a.Hin;
-      pp[k] = rok[k] ? a.x1 + ((size_t)(b0 * a.Hin + iy) * W + 2 * lj) * a.x1_pitch + loff : kZeroPage + loff;
+      const int ti = IMGS == 1 ? 0 : lpr[k] / PRI, bi = b0 + ti;
+      const int iy = mt * RIMG - 1 + lpr[k] - ti * PRI;
+      rok[k] = iy >= 0 && iy < a.Hin && bi < a.B;  // (a group's second image past B: padding throughout)
+      pp[k] = rok[k] ? a.x1 + ((size_t)(bi * a.Hin + iy) * W + 2 * lj) * a.x1_pitch + loff : kZeroPage + loff;
     }
     // column n0 + ch 64 + 16 j + l16 (n0 % 128 == 0): 32-column group (n0 + ch 64) / 32 + j / 2, column
     // 16 (j & 1) + l16 of it -- one base pointer, compile-time offsets per j
@@ -231,7 +242,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   auto finish_set = [&](int c, int buf, int k) DM_WINO_INL {
     f4 e0 = rw[2 * k], e1 = rw[2 * k + 1];
     if (PROM) {
-      const float* ts = rok[k] ? gtab + 2 * (c * kWC + loff) : gzero;  // [4 scales][4 shifts]
+      const float* ts = rok[k] ? gtab + ltab[k] + 2 * (c * kWC + loff) : gzero;  // [4 scales][4 shifts]
 #if DM_WINO_ABL == 6
       const f4 sc = {1.f, 1.f, 1.f, 1.f}, sh = {0.f, 0.f, 0.f, 0.f};
 #else
@@ -314,6 +325,8 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     a0[0] = *reinterpret_cast<const f16x8*>(As);
     a0[1] = *reinterpret_cast<const f16x8*>(As + 32);
   };
+  // pair rows 16 i .. of the tile: image i / 2 of a W 8 tile sits 2 halo rows (2 NP pair rows) further down the patch
+  auto arow = [](int i) { return IMGS == 2 && i >= 2 ? 2 * NP : 0; };
   auto compute = [&](int dy, int pbuf, const f16x8 (&bv)[TN][2]) {
     const _Float16* As = patch + pbuf * kWBuf + abase + dy * NP * kWRowH;
     f16x8 av[TM][2];
@@ -322,7 +335,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
 #pragma unroll
     for (int i = 1; i < TM; ++i)
 #pragma unroll
-      for (int p = 0; p < 2; ++p) av[i][p] = *reinterpret_cast<const f16x8*>(As + i * 16 * kWRowH + p * 32);
+      for (int p = 0; p < 2; ++p) av[i][p] = *reinterpret_cast<const f16x8*>(As + (i * 16 + arow(i)) * kWRowH + p * 32);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -340,7 +353,8 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   // (H1 = channels 32 s + .., H2 = Cin2 / 2 + 32 s + ..) as pair rows [nu][64] of a patch buffer
   const int sp = t >> 3, sks = t & 7;
   auto load_sc = [&](int st) DM_WINO_INL {
-    const float* xs = a.x2 + (size_t)(m0 + 2 * sp) * a.x2_pitch + st * kWC + 4 * sks;
+    // (rows past M -- a W 8 group's missing second image -- read the last pair: their outputs are not stored)
+    const float* xs = a.x2 + (size_t)min(m0 + 2 * sp, M - 2) * a.x2_pitch + st * kWC + 4 * sks;
     rw[0] = *reinterpret_cast<const f4*>(xs);
     rw[1] = *reinterpret_cast<const f4*>(xs + a.x2_pitch);
     rw[2] = *reinterpret_cast<const f4*>(xs + a.Cin2 / 2);
@@ -379,44 +393,50 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   auto build_table = [&]() DM_WINO_INL {
     if (!PRO) return;
     const int C = a.Cin1;
-    if (a.gin_part) {  // gn_finalize (gn.hip) for the tile's image, its expressions (conv_k32's in-kernel finalize)
-      const int G = a.gin_G, cpg = C / G;
-      for (int i = t; i < G; i += 512) {
-        double s1 = 0, s2 = 0;
+#pragma unroll
+    for (int im = 0; im < IMGS; ++im) {
+      const int bi = min(b0 + im, a.B - 1);  // (a group's second image past B: any table, its rows are padding)
+      float* tab = gtab + im * 2 * C;
+      if (a.gin_part) {  // gn_finalize (gn.hip) for the image, its expressions (conv_k32's in-kernel finalize)
+        const int G = a.gin_G, cpg = C / G;
+        float* st = gstat + im * 2 * kWMaxG;
+        for (int i = t; i < G; i += 512) {
+          double s1 = 0, s2 = 0;
 #pragma unroll 4
-        for (int k = 0; k < a.gin_nchunk; ++k) {  // (unrolled: the partials' loads in flight together)
-          const double2 v = a.gin_part[((size_t)b0 * a.gin_nchunk + k) * G + i];
-          s1 += v.x;
-          s2 += v.y;
+          for (int k = 0; k < a.gin_nchunk; ++k) {  // (unrolled: the partials' loads in flight together)
+            const double2 v = a.gin_part[((size_t)bi * a.gin_nchunk + k) * G + i];
+            s1 += v.x;
+            s2 += v.y;
+          }
+          const double mu = s1 / a.gin_n;
+          double var = s2 / a.gin_n - mu * mu;
+          if (var < 0) var = 0;
+          st[2 * i] = (float)mu;
+          st[2 * i + 1] = (float)(1.0 / sqrt(var + (double)a.gin_eps));
         }
-        const double mu = s1 / a.gin_n;
-        double var = s2 / a.gin_n - mu * mu;
-        if (var < 0) var = 0;
-        gstat[2 * i] = (float)mu;
-        gstat[2 * i + 1] = (float)(1.0 / sqrt(var + (double)a.gin_eps));
-      }
-      __syncthreads();
-      for (int c = t; c < C; c += 512) {
-        const int si = 2 * (c / cpg);
-        const float mu = gstat[si], rs = gstat[si + 1];
-        float sc = rs * (a.gin_gamma ? a.gin_gamma[c] : 1.0f);
-        float sh = -sc * mu + (a.gin_beta ? a.gin_beta[c] : 0.0f);
-        if (a.gin_ms) {
-          const size_t mo = (size_t)b0 * a.gin_mp + c;
-          const float f = 1.0f + a.gin_ms[mo];
-          sc = sc * f;
-          sh = sh * f + a.gin_mb[mo];
+        __syncthreads();
+        for (int c = t; c < C; c += 512) {
+          const int si = 2 * (c / cpg);
+          const float mu = st[si], rs = st[si + 1];
+          float sc = rs * (a.gin_gamma ? a.gin_gamma[c] : 1.0f);
+          float sh = -sc * mu + (a.gin_beta ? a.gin_beta[c] : 0.0f);
+          if (a.gin_ms) {
+            const size_t mo = (size_t)bi * a.gin_mp + c;
+            const float f = 1.0f + a.gin_ms[mo];
+            sc = sc * f;
+            sh = sh * f + a.gin_mb[mo];
+          }
+          const int ti = 2 * c - (c & 3);
+          tab[ti] = PROM == 2 ? sc * -1.4426950408889634f : sc;
+          tab[ti + 4] = PROM == 2 ? sh * -1.4426950408889634f : sh;
         }
-        const int ti = 2 * c - (c & 3);
-        gtab[ti] = PROM == 2 ? sc * -1.4426950408889634f : sc;
-        gtab[ti + 4] = PROM == 2 ? sh * -1.4426950408889634f : sh;
-      }
-    } else {
-      for (int c = t; c < C; c += 512) {
-        const int ti = 2 * c - (c & 3);
-        const float sc = a.pro_scale[(size_t)b0 * C + c], sh = a.pro_shift[(size_t)b0 * C + c];
-        gtab[ti] = PROM == 2 ? sc * -1.4426950408889634f : sc;
-        gtab[ti + 4] = PROM == 2 ? sh * -1.4426950408889634f : sh;
+      } else {
+        for (int c = t; c < C; c += 512) {
+          const int ti = 2 * c - (c & 3);
+          const float sc = a.pro_scale[(size_t)bi * C + c], sh = a.pro_shift[(size_t)bi * C + c];
+          tab[ti] = PROM == 2 ? sc * -1.4426950408889634f : sc;
+          tab[ti + 4] = PROM == 2 ? sh * -1.4426950408889634f : sh;
+        }
       }
     }
   };
@@ -645,7 +665,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     {
       const int kq = wave >> 2, hf = (wave >> 1) & 1, cj = wave & 1;
       typedef StagedEpilogue<64> Epi;
-      Epi epi(a, M, HW, cb0, true, cn0 + cj * 64, lane);
+      Epi epi(a, M, HW, cb0, IMGS == 1, cn0 + cj * 64, lane);
       const int px0 = 64 * kq + 32 * hf;
       const float* Ec = E + cj * 64 * kWEP + 4 * epi.c4;
       f4 fin = {0.f, 0.f, 0.f, 0.f};  // inf / NaN in any m (an operand past fp16's range) makes fin non-finite
@@ -754,8 +774,12 @@ extern "C" int dm_debug_wino_stamps(void* host, int nblocks) {
 
 bool conv_wino_shape_ok(const ConvArgs& a) {
   if (!(a.taps == 9 && a.stride == 1 && a.upsample == 0 && a.ksplit <= 1)) return false;
-  if (a.Hin != a.Hout || a.Win != a.Wout || (a.Wout != 32 && a.Wout != 16) || (a.Hout * a.Wout) % 128 != 0) return false;
-  if (a.Cin1 < kWC || a.Cin1 % kWC != 0 || 2 * a.Cin1 > kWTab || a.Cin2 % (2 * kWC) != 0 || a.K != 9 * a.Cin1 + a.Cin2)
+  if (a.Hin != a.Hout || a.Win != a.Wout) return false;
+  // 32- or 16-wide maps in whole-row 128-pixel tiles; 8 x 8 maps two images per tile
+  const int imgs = a.Wout == 8 ? 2 : 1;
+  if (a.Wout == 8 ? a.Hout != 8 : ((a.Wout != 32 && a.Wout != 16) || (a.Hout * a.Wout) % 128 != 0)) return false;
+  if (a.Cin1 < kWC || a.Cin1 % kWC != 0 || 2 * imgs * a.Cin1 > kWTab || a.Cin2 % (2 * kWC) != 0 ||
+      a.K != 9 * a.Cin1 + a.Cin2)
     return false;
   if (a.x1_pitch + a.Cin1 > kZeroPageFloats) return false;  // the loader's padding rows read the zero page
   if (a.Cin2 && (!a.x2 || a.x2_pitch % 4 != 0 || (reinterpret_cast<uintptr_t>(a.x2) & 15) != 0)) return false;
@@ -810,14 +834,15 @@ int conv2d_wino(const ConvArgs& a, hipStream_t st) {
                                                  hipSuccess || ncu <= 0)
       ncu = 256;
   }
-  const int tpi = (a.Hout * a.Wout / 128) * (a.Cout / 128);
+  const int imgs = a.Wout == 8 ? 2 : 1, groups = ceil_div(a.B, imgs);  // image groups (two 8 x 8 images per tile)
+  const int tpi = (imgs * a.Hout * a.Wout / 128) * (a.Cout / 128);
   int parts = tpi;
   for (int p = 1; p <= tpi; ++p)
-    if (tpi % p == 0 && (long)a.B * p >= ncu) {
+    if (tpi % p == 0 && (long)groups * p >= ncu) {
       parts = p;
       break;
     }
-  const int blocks = a.B * parts;
+  const int blocks = groups * parts;
   const int prom = (a.pro_scale || a.gin_part) ? (a.pro_nosilu ? 1 : 2) : 0;
 #define DM_WINO_LAUNCH(W_, P_)                                                                              \
   if (a.Wout == W_ && prom == P_) {                                                                         \
@@ -827,6 +852,7 @@ int conv2d_wino(const ConvArgs& a, hipStream_t st) {
   }
   DM_WINO_LAUNCH(32, 0) DM_WINO_LAUNCH(32, 1) DM_WINO_LAUNCH(32, 2)
   DM_WINO_LAUNCH(16, 0) DM_WINO_LAUNCH(16, 1) DM_WINO_LAUNCH(16, 2)
+  DM_WINO_LAUNCH(8, 0) DM_WINO_LAUNCH(8, 1) DM_WINO_LAUNCH(8, 2)
 #undef DM_WINO_LAUNCH
   DM_LAUNCH_CHECK();
   return DM_OK;

@@ -22,7 +22,8 @@ WINO = 21  # ConvDesc.tile: force the Winograd kernel
 
 
 @pytest.mark.parametrize('B,Cin,Cout,H', [(1, 128, 128, 32), (2, 32, 128, 32), (3, 64, 256, 16), (2, 256, 128, 16),
-                                          (1, 96, 384, 32), (5, 160, 128, 16)])
+                                          (1, 96, 384, 32), (5, 160, 128, 16), (1, 128, 128, 8), (3, 64, 256, 8),
+                                          (4, 512, 256, 8)])
 def test_wino_conv3x3_exact(cuda, B, Cin, Cout, H):
     """Integer operands: V = B^T d, U = G g (half-integers), their fp16 pieces and the fp32 sums are exact, so the
     Winograd conv equals the float64 conv bit for bit (zero padding at every map edge, all tap rows)."""
@@ -39,7 +40,7 @@ def test_wino_conv3x3_exact(cuda, B, Cin, Cout, H):
     assert torch.equal(y.cpu(), _nhwc(ref))
 
 
-@pytest.mark.parametrize('H', [32, 16])
+@pytest.mark.parametrize('H', [32, 16, 8])
 def test_wino_rowvec_residual_pitch(cuda, H):
     """temb row vector, residual, pitched input and output (untouched beyond Cout), integer-exact."""
     B, Cin, Cout = 3, 64, 128
@@ -59,7 +60,8 @@ def test_wino_rowvec_residual_pitch(cuda, H):
 
 
 @pytest.mark.parametrize('C1,C2,H,Cout,pro', [(64, 64, 32, 128, False), (128, 384, 32, 128, False), (96, 128, 16, 256, False),
-                                              (32, 192, 16, 128, False), (64, 128, 32, 128, True)])
+                                              (32, 192, 16, 128, False), (64, 128, 32, 128, True), (256, 256, 8, 256, False),
+                                              (128, 128, 8, 256, True)])
 def test_wino_shortcut_segment_exact(cuda, C1, C2, H, Cout, pro):
     """ResBlock conv2: 3x3 over h plus the 1x1 shortcut of x as a second K segment (nu 0 / 3: the pair's pixels,
     nu 1 / 2: their sum and difference against half the weights), temb row vector, residual -- integer-exact (with the
@@ -118,7 +120,8 @@ def test_wino_shortcut_fp32_accuracy(cuda, report, B, C1, C2, Cout, H):
     assert errs['wino'] < 3.0 * errs['fp32'] + 1e-7 * scale, errs
 
 
-@pytest.mark.parametrize('B,Cin,Cout,H', [(4, 128, 128, 32), (8, 256, 256, 16), (2, 384, 128, 32), (4, 512, 256, 16)])
+@pytest.mark.parametrize('B,Cin,Cout,H', [(4, 128, 128, 32), (8, 256, 256, 16), (2, 384, 128, 32), (4, 512, 256, 16),
+                                          (8, 256, 256, 8), (5, 512, 256, 8)])
 def test_wino_fp32_accuracy(cuda, report, B, Cin, Cout, H):
     """Fused GroupNorm + SiLU conv on random data: the Winograd kernel's error vs float64 stays at the fp32 level
     (within 3x the fp32 MFMA kernel's; the direct fp16x2 kernel's is within 2x)."""
@@ -163,7 +166,7 @@ def _forward_logged(meta, name, cuda, x, t, y=None):
 
 @pytest.mark.parametrize('B', [2, 5])
 def test_wino_cifar_forward(cuda, golden, monkeypatch, report, B):
-    """The CIFAR-10 UNet with its 32^2 / 16^2 ResBlock convs (no shortcut segment) on the Winograd kernel: within
+    """The CIFAR-10 UNet with its 32^2 / 16^2 / 8^2 ResBlock convs (no shortcut segment) on the Winograd kernel: within
     1e-5 of the direct-conv forward (DM_CONV_WINO=0) and within TOL of the reference fixture; the launch log holds
     the Winograd launches and the direct forward none."""
     g, meta = golden('forward')
@@ -175,7 +178,9 @@ def test_wino_cifar_forward(cuda, golden, monkeypatch, report, B):
     _, out_d, log_d = _forward_logged(meta, 'cifar10', cuda, x, t)
     n32 = sum(log_w.count(f'conv_wino_kernel<32,2,{sc}>') for sc in ('false', 'true'))
     n16 = sum(log_w.count(f'conv_wino_kernel<16,2,{sc}>') for sc in ('false', 'true'))
-    assert n32 == 10 and n16 == 10, log_w  # every 3x3 ResBlock conv of the 32^2 / 16^2 levels, shortcuts included
+    n8 = sum(log_w.count(f'conv_wino_kernel<8,2,{sc}>') for sc in ('false', 'true'))
+    # every 3x3 ResBlock conv of the 32^2 / 16^2 / 8^2 levels, shortcuts included
+    assert n32 == 10 and n16 == 10 and n8 == 10, log_w
     assert not any(s.startswith('conv_wino') for s in log_d), log_d
     err = (out_w - out_d).abs().max().item()
     report(f'wino_cifar_forward_B{B}_vs_direct', err)
