@@ -191,6 +191,12 @@ def test_bench_traffic_needs_same_build_and_launch_count(tmp_path):
     assert bench.pmc_traffic('kern<1>', 'c3', None, 8.0, root=str(tmp_path)) == (None, None)
 
 
+def test_dmhip_exports_build_info():
+    """bench.py keys the roofline's traffic on dmhip.build_info() (no library call needed to resolve it)."""
+    import dmhip
+    assert callable(dmhip.build_info)
+
+
 def test_bench_wino_roofline_priced_in_direct_flops():
     """The Winograd kernel's FLOPs are the direct conv's: its peak is the fp16x2 issue peak / (2/3)."""
     import bench
