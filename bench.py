@@ -69,11 +69,11 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(label, workload='c3', build=None, launches_per_step=None, root=ROOT):
+def pmc_traffic(label, workload='c3', build=None, launches_per_forward=None, root=ROOT):
     """HBM bytes per launch of `label` from the newest committed PMC summary of this workload
     (profiles/rNN_vM_pmc.json, FETCH_SIZE x2 + WRITE_SIZE passes of this bench, tools/gpu_profile.sh;
     summaries without a "workload" field are of the default c3 run) -- only from a summary of the SAME library
-    build (its "build" = dm_build_info() of this run) in which `label` ran as many launches per denoising step
+    build (its "build" = dm_build_info() of this run) in which `label` ran as many launches per network forward
     as in this run; none such: (None, None), and the roofline's traffic is null."""
     import glob
     import re
@@ -88,8 +88,8 @@ def pmc_traffic(label, workload='c3', build=None, launches_per_step=None, root=R
         if summary.get('workload', 'c3') != workload or build is None or summary.get('build') != build:
             continue
         k = summary.get('kernels', {}).get(label)
-        if not k or not k.get('hbm_bytes_per_launch') or launches_per_step is None or \
-                k.get('launches_per_step') is None or abs(k['launches_per_step'] - launches_per_step) > 1e-6:
+        if not k or not k.get('hbm_bytes_per_launch') or launches_per_forward is None or \
+                k.get('launches_per_forward') is None or abs(k['launches_per_forward'] - launches_per_forward) > 1e-6:
             continue
         return float(k['hbm_bytes_per_launch']), os.path.relpath(path, root)
     return None, None
@@ -193,9 +193,9 @@ def cpu_baseline_cfg(name, model_sd, arch, batch, n_steps, guidance_scale, timed
 WINO_PRODUCTS = 2.0 / 3.0   # conv_wino_kernel: F(2,3) issues 12 K-rows per output pair where the direct conv issues 18
 
 
-def roofline(prof, workload='c3', build=None, launches_per_step=None):
-    """Roofline of the dominant kernel family (most GPU time in the timed region). launches_per_step: label ->
-    launches per denoising step in this run (pmc_traffic's match key)."""
+def roofline(prof, workload='c3', build=None, launches_per_forward=None):
+    """Roofline of the dominant kernel family (most GPU time in the timed region). launches_per_forward: label ->
+    launches per network forward in this run (pmc_traffic's match key)."""
     fam = {}
     for op in prof:
         f = fam.setdefault(op['label'], dict(flops=0.0, bytes=0.0, ms=0.0, launches=0))
@@ -238,10 +238,11 @@ def roofline(prof, workload='c3', build=None, launches_per_step=None):
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
         roof = dict(bound='hbm', achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit='GB/s',
                     frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None)
-    lps = (launches_per_step or {}).get(dom_name)
-    traffic, traffic_src = pmc_traffic(dom_name, workload, build, lps)
+    lpf = (launches_per_forward or {}).get(dom_name)
+    traffic, traffic_src = pmc_traffic(dom_name, workload, build, lpf)
     roof.update(traffic=traffic, traffic_source=traffic_src, algorithmic_bytes_per_launch=bytes_per_launch,
-                kernel=dom_name, avg_launch_ms=round(avg_ms, 4), launches=dom['launches'], launches_per_step=lps,
+                traffic_over_algorithmic=round(traffic / bytes_per_launch, 3) if traffic and bytes_per_launch else None,
+                kernel=dom_name, avg_launch_ms=round(avg_ms, 4), launches=dom['launches'], launches_per_forward=lpf,
                 build=build,
                 algorithmic_per_launch=flops_per_launch if flops_per_launch > 0 else bytes_per_launch)
     total_gpu_ms = sum(f['ms'] for f in fam.values())
@@ -537,12 +538,13 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = tt.item()
     prof, kernel_s, wbytes_t, wsbytes_t = [], 0.0, 0, 0
-    lps = {}   # launches per denoising step of each kernel label: its ops per forward x forwards per step
+    # launches per network forward of each kernel label: each handle's ops with the label, weighted by its forwards
+    lpf, nfwd = {}, sum(f for _, _, f in wl['handles'])
     for h, abi, fwd_per_fold in wl['handles']:
         p = dmhip.unet_profile_read(h, abi=abi)
         prof += p
         for op in p:
-            lps[op['label']] = lps.get(op['label'], 0.0) + fwd_per_fold / max(1, wl['denoise_steps'])
+            lpf[op['label']] = lpf.get(op['label'], 0.0) + fwd_per_fold / max(1, nfwd)
         observed = max((op['launches'] for op in p), default=0)   # forwards of this handle that ran with events
         if observed:
             kernel_s += sum(op['ms_total'] for op in p) * 1e-3 * fwd_per_fold * args.steps / observed
@@ -555,7 +557,7 @@ def main():
 
     roof, total_gpu_ms, total_flops, fam = None, 0.0, 0.0, {}
     if not args.no_profile and prof:
-        roof, total_gpu_ms, total_flops, fam = roofline(prof, args.workload, None if stub else dmhip.build_info(), lps)
+        roof, total_gpu_ms, total_flops, fam = roofline(prof, args.workload, None if stub else dmhip.build_info(), lpf)
 
     if rank == 0:
         images = world * B * args.steps

@@ -174,12 +174,12 @@ def test_load_weights_formats(tmp_path):
 
 def test_bench_traffic_needs_same_build_and_launch_count(tmp_path):
     """bench.py's roofline traffic comes only from a PMC summary of the same library build whose kernel ran as many
-    launches per denoising step as the measured run; otherwise traffic is null."""
+    launches per network forward as the measured run; otherwise traffic is null."""
     import json
     import bench
     prof = tmp_path / 'profiles'
     prof.mkdir()
-    k = dict(hbm_bytes_per_launch=123.0, launches_per_step=8.0)
+    k = dict(hbm_bytes_per_launch=123.0, launches_per_forward=8.0)
     (prof / 'r05_v1_pmc.json').write_text(json.dumps(dict(workload='c3', build='aaaa', kernels={'kern<1>': k})))
     (prof / 'r05_v2_pmc.json').write_text(json.dumps(dict(workload='c3', build='bbbb',
                                                           kernels={'kern<1>': dict(k, hbm_bytes_per_launch=7.0)})))
@@ -203,4 +203,4 @@ def test_bench_wino_roofline_priced_in_direct_flops():
     prof = [dict(label='conv_wino_kernel<32,2,false>', flops=1e12, bytes=1e9, ms_total=2.0, launches=1)]
     roof = bench.roofline(prof, 'c3', None, {'conv_wino_kernel<32,2,false>': 4.0})[0]
     assert roof['peak'] == round(2500.0 / 3 / (2 / 3), 1) and abs(roof['achieved'] - 500.0) < 1e-6
-    assert roof['traffic'] is None and roof['launches_per_step'] == 4.0 and 'direct-convolution' in roof['peak_basis']
+    assert roof['traffic'] is None and roof['launches_per_forward'] == 4.0 and 'direct-convolution' in roof['peak_basis']

@@ -86,20 +86,21 @@ def main():
         fetch = pmc(args.fetch, 'FETCH_SIZE')
         write = pmc(args.write, 'WRITE_SIZE')
         res = {}
-        # launches per denoising step of each kernel in the FETCH pass: its dispatches over the sampler update's
-        # (one per step); bench.py's roofline takes this summary's traffic only for the same build and the same count
+        # launches per forward of each kernel in the FETCH pass: its dispatches over the timestep embedding's (one per
+        # network forward, the plan-building forward included); bench.py's roofline takes this summary's traffic only
+        # for the same build and the same count
         calls = calls_by_name(args.fetch)
-        steps = calls.get('sampler_step_kernel', 0)
+        fwds = calls.get('timestep_embed_kernel', 0)
         for name in set(fetch) | set(write):
             rb = 2 * 1024 * fetch.get(name, 0.0)
             wb = 1024 * write.get(name, 0.0)
             k = short(name)
             res[k] = dict(read_bytes_per_launch=rb, write_bytes_per_launch=wb, hbm_bytes_per_launch=rb + wb,
                           fetch_size_kib=fetch.get(name), write_size_kib=write.get(name), calls=calls.get(k, 0),
-                          launches_per_step=(calls.get(k, 0) / steps) if steps else None)
+                          launches_per_forward=(calls.get(k, 0) / fwds) if fwds else None)
         meta = dict(note='read = 2 x FETCH_SIZE (gfx950 half-count of 16B/lane coalesced reads); '
                          'write = WRITE_SIZE (exact for 16B stores, uncalibrated for 4B stores)',
-                    command=args.command, workload=args.workload, build=args.build, sampler_steps=steps, kernels=res)
+                    command=args.command, workload=args.workload, build=args.build, forwards=fwds, kernels=res)
         path = os.path.join(out_dir, f'{args.tag}_pmc.json')
         with open(path, 'w') as f:
             json.dump(meta, f, indent=1, sort_keys=True)
