@@ -42,21 +42,23 @@ typedef float fq __attribute__((ext_vector_type(4)));
 
 #ifdef DM_K32_STAMPS
 // Diagnostic build only (tools/ab_stamps.py): per work-group, wave 0's s_memtime at the phase boundaries and
-// s_memrealtime at start / end. Written to this buffer only.
+// s_memrealtime at start / end, kept in scalar registers and written to this buffer at the end (no scheduling
+// barriers and no stores at the boundaries, so the stamped build keeps the product kernel's registers: round 4's
+// per-boundary stores spilled it).
 __device__ unsigned long long g_ab_stamps[4096][10];
-#define AB_STAMP(k)                                                                                      \
-  do {                                                                                                   \
-    __builtin_amdgcn_sched_barrier(0);                                                                   \
-    if (threadIdx.x == 0 && blockIdx.x < 4096) g_ab_stamps[blockIdx.x][k] = __builtin_amdgcn_s_memtime();  \
-    __builtin_amdgcn_sched_barrier(0);                                                                   \
-  } while (0)
-#define AB_RSTAMP(k)                                                                                     \
-  do {                                                                                                   \
-    if (threadIdx.x == 0 && blockIdx.x < 4096) g_ab_stamps[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); \
+#define AB_DECL unsigned long long ab_t[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}
+#define AB_STAMP(k) (ab_t[k] = __builtin_amdgcn_s_memtime())
+#define AB_RSTAMP(k) (ab_t[k] = __builtin_amdgcn_s_memrealtime())
+#define AB_FLUSH                                                                         \
+  do {                                                                                   \
+    if (threadIdx.x == 0 && blockIdx.x < 4096)                                           \
+      for (int k_ = 0; k_ < 10; ++k_) g_ab_stamps[blockIdx.x][k_] = ab_t[k_];             \
   } while (0)
 #else
+#define AB_DECL do {} while (0)
 #define AB_STAMP(k) do {} while (0)
 #define AB_RSTAMP(k) do {} while (0)
+#define AB_FLUSH do {} while (0)
 #endif
 // DM_AB_ABL (diagnostic builds only, wrong results): 1 no staging refills after the first two k-steps of a
 // phase, 2 no residual loads in the epilogue
@@ -192,6 +194,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
   __shared__ __attribute__((aligned(16))) float tab[2][kBC];
   static_assert(2 * kKImg * 2 <= kBQ * kOP * 4, "two key-chunk images fit the epilogue region");
   _Float16* stg = reinterpret_cast<_Float16*>(lds);
+  AB_DECL;
   AB_RSTAMP(8);
   AB_STAMP(0);
 
@@ -526,6 +529,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
   }
   AB_STAMP(6);
   AB_RSTAMP(9);
+  AB_FLUSH;
 }
 
 // ---- variant 4: attn_block3_kernel's algorithm with 8 waves of 16 queries (512 threads, 128 queries per
@@ -570,6 +574,7 @@ __global__ void __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2
   __shared__ __attribute__((aligned(16))) float lds[LDSF];
   __shared__ __attribute__((aligned(16))) float tab[2][kBC];
   _Float16* stg = reinterpret_cast<_Float16*>(lds);
+  AB_DECL;
   AB_RSTAMP(8);
   AB_STAMP(0);
 
@@ -900,6 +905,7 @@ __global__ void __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2
   }
   AB_STAMP(6);
   AB_RSTAMP(9);
+  AB_FLUSH;
 }
 
 __device__ __forceinline__ int pi32(int m) { return 4 * (m >> 3) + (m & 3) + 16 * ((m >> 2) & 1); }
