@@ -46,6 +46,7 @@ void refresh_toggles() {
   }
   t.attn_gn_launch = env_is("DM_ATTN_GNFIN", '1');
   t.dit_presplit = !env_is("DM_DIT_PRESPLIT", '0');
+  t.lin_sk = !env_is("DM_LIN_SK", '0');
   g_toggles = t;
 }
 void note_launch(const char* name) {

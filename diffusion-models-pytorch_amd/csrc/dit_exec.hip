@@ -76,6 +76,12 @@ struct DiTModel {
   // run linear_k32 (K = 32 MFMA steps, no per-load split of the weights)
   std::map<const float*, void*> split_w;
   bool linear_k32_on = true;
+  // linear_k32's split-K tail (GemmArgs::sk_*): one 64-KB slab per resident block and one arrival counter per
+  // tile, zeroed once (each tile's reducing block resets its counter); forwards of this model's plans are
+  // stream-ordered (ScratchPool::order), so one set serves them all
+  float* sk_ws = nullptr;
+  unsigned* sk_cnt = nullptr;
+  int sk_cap = 0;
 
   struct Plan : PlanBase {
     int B = 0;
@@ -94,6 +100,8 @@ struct DiTModel {
     plans.clear();
     for (auto& kv : split_w) (void)hipFree(kv.second);
     if (range_flag) (void)hipFree(range_flag);
+    if (sk_ws) (void)hipFree(sk_ws);
+    if (sk_cnt) (void)hipFree(sk_cnt);
     if (range_flag_host) (void)hipHostFree(range_flag_host);
     if (arena) (void)hipFree(arena);
   }
@@ -207,6 +215,14 @@ int DiTModel::build_plan(Plan& pl, int B) {
     DM_CHECK_HIP(hipMemset(range_flag, 0, sizeof(int)));
     DM_CHECK_HIP(hipHostMalloc(&range_flag_host, sizeof(int)));
   }
+  if (!sk_ws && toggles().lin_sk && linear_k32_slots() > 0) {
+    const int slots = linear_k32_slots();
+    DM_CHECK_HIP(hipMalloc(&sk_ws, (size_t)slots * 65536));
+    DM_CHECK_HIP(hipMalloc(&sk_cnt, (size_t)slots * sizeof(unsigned)));
+    DM_CHECK_HIP(hipMemset(sk_cnt, 0, (size_t)slots * sizeof(unsigned)));
+    sk_cap = slots;
+  }
+  const bool sk_on = toggles().lin_sk && sk_ws;
   pl.x = pl.alloc((size_t)B * C * S * S * 4);
   pl.t = (int64_t*)pl.alloc((size_t)B * 8);
   pl.y = (int64_t*)pl.alloc((size_t)B * 8);
@@ -311,6 +327,11 @@ int DiTModel::build_plan(Plan& pl, int B) {
       }
       g.ws = it->second;
       g.ws_rowscale = split_conv_rowscale(it->second, 1, g.N, g.K);
+      if (sk_on) {
+        g.sk_ws = sk_ws;
+        g.sk_cnt = sk_cnt;
+        g.sk_cap = sk_cap;
+      }
       // with the pre-split A image (add_token_gemm) the GEMM takes no prologue: check that form
       GemmArgs probe = g;
       if (presplit_on && g.pick_M >= 4096 && !probe.c_split) {

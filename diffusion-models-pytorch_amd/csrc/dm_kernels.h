@@ -31,6 +31,7 @@ struct Toggles {
                               // v planes from the qkv epilogue, proj fused), kAttnNoProj, kAttnFused, kAttnUnfused
   bool attn_gn_launch = false;  // DM_ATTN_GNFIN=1: the folded block's GroupNorm finalize as its own launch
   bool dit_presplit = true;   // DM_DIT_PRESPLIT=0: DiT token GEMMs split their activations per tile
+  bool lin_sk = true;         // DM_LIN_SK=0: no split-K of linear_k32's last, partial round of tiles
 };
 const Toggles& toggles();
 void refresh_toggles();
@@ -209,6 +210,14 @@ struct GemmArgs {
   float ap_alpha, ap_bscale;
   int ap_ea, ap_eb, ap_ev;
   int* range_flag;
+  // linear_k32 only: split-K of the tiles of the last, partial round (the tile count modulo the resident
+  // blocks, when at most half a round): sk_cap slabs of 128 x 128 fp32 and one arrival counter per tile
+  // (zero before the first use; the reducing block resets it), owned by the caller. sk_S / sk_tdp are set by
+  // linear_k32 itself (slices per tail tile, first tail tile).
+  float* sk_ws;
+  unsigned* sk_cnt;
+  int sk_cap;
+  int sk_S, sk_tdp;
 };
 
 struct StepArgs {
@@ -311,6 +320,8 @@ int conv2d_wino(const ConvArgs& a, hipStream_t st);
 // static-weight GEMM on pre-split weights with K = 32 MFMA steps (linear_k32.hip)
 bool linear_k32_ok(const GemmArgs& g);
 int linear_k32(const GemmArgs& g, hipStream_t st);
+// resident linear_k32 blocks of the device (blocks per CU x CUs): the split-K tail's slab capacity
+int linear_k32_slots();
 // the pre-split A image of g (prologue, alpha, 2^split_ea, fp16x2 split; |value| > 65504 sets range_flag)
 int linear_presplit_a(const GemmArgs& g, _Float16* out, hipStream_t st);
 int conv_splitk_reduce(const ConvArgs& a, hipStream_t st);

@@ -295,7 +295,25 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   // memory side once per group instead of once per M tile (DiT-XL/2 qkv: 16 MB of split weights re-read
   // for each of 128 M tiles otherwise); the group's A tiles stay in the XCD's L2 during the sweep.
   const int nN = ceil_div(N, BN), nM = ceil_div(M, BM);
-  const int bid = xcd_remap_p(blockIdx.x, gridDim.x);
+  // Split-K tail (g.sk_S > 1): blocks sk_tdp .. sk_tdp + tail * S - 1 take the tiles of the last, partial
+  // round, S blocks per tile, each a contiguous 1 / S of the K stages; S consecutive logical blocks of one
+  // XCD share a tile (the reducer reads same-XCD slabs). The tiles before sk_tdp run whole, as without.
+  // (a function of the block index, evaluated again after the K loop rather than kept live across it: the
+  // loop holds all 256 VGPRs)
+  auto sk_place = [&](int bx, int& bid_, int& slice_) {
+    if (g.sk_S > 1 && bx >= g.sk_tdp) {
+      const int v = xcd_remap_p(bx - g.sk_tdp, (int)gridDim.x - g.sk_tdp);
+      bid_ = g.sk_tdp + v / g.sk_S;
+      slice_ = v - (v / g.sk_S) * g.sk_S;
+    } else {
+      bid_ = xcd_remap_p(bx, g.sk_S > 1 ? g.sk_tdp : (int)gridDim.x);
+      slice_ = 0;
+    }
+  };
+  int bid, slice;
+  sk_place((int)blockIdx.x, bid, slice);
+  const int sk_S = g.sk_S > 1 && (int)blockIdx.x >= g.sk_tdp ? g.sk_S : 1;
+  const int sbeg = slice * (K / 64) / sk_S;  // first K stage (64 channels) of this block
   const int tgrp = bid / (kLGM * nN), gm0 = tgrp * kLGM, gsz = min(kLGM, nM - gm0);
   const int r = bid - tgrp * (kLGM * nN);
   const int nt = r / gsz, mt = gm0 + (r - nt * gsz);
@@ -313,11 +331,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   // DiT GEMMs' time (DM_LIN_ABL=2; fc1 / fc2 at 2B = 64: 663 -> 512 us). The in-GEMM prologues (PRO 0-2,
   // fp32 A) keep the row-half mapping: the same remap spills them past 256 VGPRs.
   const int a3s = t & 15, a3r = t >> 4;
-  const f4* asp = PRO == 3 ? reinterpret_cast<const f4*>(g.as) + a3s : nullptr;
+  const f4* asp = PRO == 3 ? reinterpret_cast<const f4*>(g.as) + a3s + 16 * sbeg : nullptr;
   const size_t a3pitch = (size_t)K / 4;  // f4 per pre-split row
   const int lrow = t >> 1, lh = t & 1;  // PRO 0-2 loader: row, 32-channel half of the stage (= K32 step)
   const int am = min(m0 + lrow, M - 1);  // rows >= M: clamped, never stored
-  const float* asrc = g.A + (size_t)am * g.lda + 32 * lh;
+  const float* asrc = g.A + (size_t)am * g.lda + 32 * lh + 64 * sbeg;
   const int aimg = TABS ? am / rows_img - img0 : 0;  // 0 or 1
   const float2 lns = PRO == 2 ? g.ln_stats[am] : make_float2(0.f, 1.f);
   const float apow = ldexpf(1.f, g.split_ea);
@@ -345,7 +363,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   auto load_tab = [&](int st) {
     if (TABS && t < 64) {
       const int im = min(img0 + (ti >> 1), (M - 1) / rows_img);
-      const int kk = 64 * st + tk;
+      const int kk = 64 * (sbeg + st) + tk;
       if (PRO == 1)
         rt = *reinterpret_cast<const f4*>(((ti & 1) ? g.pro_shift : g.pro_scale) + (size_t)im * K + kk);
       else
@@ -405,7 +423,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   for (int j = 0; j < TN; ++j) {
     const int col = n0 + wn * WN + j * 16 + l16;
     const int grp = min(col >> 5, ngrp - 1);
-    wbase[j] = reinterpret_cast<const _Float16*>(g.ws) + (size_t)(q >> 1) * sl + (size_t)grp * 1024 +
+    wbase[j] = reinterpret_cast<const _Float16*>(g.ws) + (size_t)((q >> 1) + 4 * sbeg) * sl + (size_t)grp * 1024 +
                ((q & 1) * 32 + (col & 31)) * 8;
   }
   f16x8 bq[WD][TN][2];
@@ -443,7 +461,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
       }
   };
 
-  const int nst = K / 64, nkk = K / 32;
+  const int nst = (slice + 1) * (K / 64) / sk_S - sbeg, nkk = 2 * nst;  // this block's K stages and steps
 #pragma unroll
   for (int d = 0; d < WD; ++d) load_b(bq[d], min(d, nkk - 1));
   load_a(ra[0], 0);
@@ -487,6 +505,65 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     if (st + 1 < nst) stage(st + 1, ra[1], ra[0]);
   }
   LIN_STAMP(2);
+  if (g.sk_S > 1 && (int)blockIdx.x >= g.sk_tdp) {
+    const int sk_S = g.sk_S;
+    int bx = (int)blockIdx.x, bid, slice;
+    asm volatile("" : "+s"(bx));  // recomputed here, not carried through the loop
+    sk_place(bx, bid, slice);
+    // Split-K hand-off (cdna_hip_programming.md §5 'In-launch split-K reduction', its write-through form):
+    // every slice stores its accumulators as a 64-KB slab in register order with sc1 (write-through) 16-B
+    // buffer stores, 1 KB per wave instruction, drains them (every wave), and one lane draws a ticket -- no
+    // release fence, whose L2 write-back of every dirty line of the XCD cost more than the tail saved; the
+    // block drawing S - 1 resets the counter, acquires, and sums the S slabs in slice order (its own from
+    // memory too: the same sum whichever block arrives last, so the result is deterministic), then runs the
+    // epilogue. Nobody waits: no residency assumption.
+    const int tt = bid - g.sk_tdp;
+    constexpr int SLAB = NW * TM * TN * 64;  // f4 per slab
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(g.sk_ws, 0, g.sk_cap * 65536, 0x00020000);
+    const int sbyte = (((tt * sk_S + slice) * SLAB) + wave * (TM * TN * 64) + lane) * 16;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs, sbyte + (i * TN + j) * 1024,
+                                               0, 16 /* sc1 */);
+      }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* last = reinterpret_cast<int*>(&tab[0][0][0][0]);  // (the tables are dead after the K loop)
+    if (t == 0) {
+      const unsigned tk = __hip_atomic_fetch_add(g.sk_cnt + tt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int is_last = tk == (unsigned)(sk_S - 1);
+      if (is_last) {
+        __hip_atomic_store(g.sk_cnt + tt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      *last = is_last;
+    }
+    __syncthreads();
+    if (!*last) {
+      if (bad && g.range_flag) *g.range_flag = 1;
+      return;
+    }
+    const f4* s0 = reinterpret_cast<const f4*>(g.sk_ws) + (size_t)tt * sk_S * SLAB + wave * (TM * TN * 64) + lane;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = s0[(i * TN + j) * 64];
+    for (int s = 1; s < sk_S; ++s) {
+      f4 v[TM][TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) v[i][j] = s0[(size_t)s * SLAB + (i * TN + j) * 64];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] += v[i][j];
+    }
+  }
   // ---- epilogue: per 32-row slab of the wave's 64 rows, acc * rowscale * 2^-ea to LDS ([32][68] fp32),
   // then 4 consecutive columns per lane: bias, residual / gated residual, activation, 16-B store
   constexpr int EP = WN + 4, LPR = WN / 4, RPI = 64 / LPR;
@@ -628,9 +705,57 @@ int linear_presplit_a(const GemmArgs& g, _Float16* out, hipStream_t st) {
   return DM_OK;
 }
 
-int linear_k32(const GemmArgs& g, hipStream_t st) {
-  DM_REQUIRE(linear_k32_ok(g), "linear_k32: needs pre-split weights, K % 64 == 0, 16-byte aligned 4-column rows");
-  const int blocks = ceil_div(g.M, kLBM) * ceil_div(g.N, 128);
+namespace {
+struct LinSlots {
+  int per_cu = 0, cus = 0;
+};
+const LinSlots& lin_slots() {
+  static const LinSlots s = [] {
+    LinSlots r;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&r.per_cu, linear_k32_kernel<3>, 256, 0) != hipSuccess ||
+        hipDeviceGetAttribute(&r.cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+      (void)hipGetLastError();
+      r = LinSlots{};
+    }
+    return r;
+  }();
+  return s;
+}
+}  // namespace
+
+int linear_k32_slots() { return lin_slots().per_cu * lin_slots().cus; }
+
+int linear_k32(const GemmArgs& g_in, hipStream_t st) {
+  DM_REQUIRE(linear_k32_ok(g_in), "linear_k32: needs pre-split weights, K % 64 == 0, 16-byte aligned 4-column rows");
+  GemmArgs g = g_in;
+  const int tiles = ceil_div(g.M, kLBM) * ceil_div(g.N, 128);
+  int blocks = tiles;
+  g.sk_S = 1;
+  g.sk_tdp = 0;
+  // Split-K of the last, partial round: with T tiles on P resident blocks (2 per CU) the last round holds
+  // T % P tiles and leaves the rest of the chip idle (DiT-XL/2's N = 1152 GEMMs at 2B = 64: 1152 tiles = 2.25
+  // rounds of 512). When that tail is at most half a round, its tiles are split S ways over K (S a power of
+  // two, S <= the K stages) with tail * S <= the CU count: one block per CU, 1 / S of the K loop each. (Filling
+  // both slots of every CU measured slower: on DiT-XL/2 C5 S = 2 +1.5 %, S = 4 -0.6 % against no split; the
+  // tail's unsplit tiles already run one per CU, at a CU's whole issue rate.) Those tiles' sums are re-associated (slice partials summed in slice
+  // order): not bit-identical to the whole-K tile, so a row's result depends on whether its tile is in the
+  // tail (DM_LIN_SK=0: every tile whole).
+  const int nst = g.K / 64, P = linear_k32_slots(), cus = lin_slots().cus;
+  if (g.sk_ws && g.sk_cnt && nst >= 2 && P > 0) {
+    const int tail = tiles % P;
+    if (tail > 0 && 2 * tail <= P) {
+      int S = 1;
+      while (2 * S <= 8 && 2 * S <= nst && tail * 2 * S <= cus && tail * 2 * S <= g.sk_cap) S *= 2;
+      if (S > 1) {
+        g.sk_S = S;
+        g.sk_tdp = tiles - tail;
+        blocks = g.sk_tdp + tail * S;
+        note_launch("linear_k32_sk");
+      }
+    }
+  }
   if (g.as)
     hipLaunchKernelGGL(linear_k32_kernel<3>, dim3(blocks), dim3(256), 0, st, g);
   else if (g.pro_scale)

@@ -211,3 +211,44 @@ def test_small_map_variants_both_launched_bit_identical(cuda, golden, monkeypatc
     assert k4 and all(s.endswith(',4>') for s in k4), logs['1']
     assert len(k4) == len(k8)
     assert torch.equal(outs['0'], outs['1'])
+
+
+def test_linear_split_k_tail(cuda, monkeypatch, report):
+    """linear_k32's split-K tail (DiT-S/2 at B = 16: the N = 384 proj / fc2 GEMMs have 96 tiles, a tail of less
+    than half a round on 512 resident blocks, split 2 ways over K, one block per CU): the launch log shows it with the default and
+    not with DM_LIN_SK=0; two forwards are bit-identical (the slabs are summed in slice order whichever block
+    arrives last); the re-associated sums stay within 1e-5 (relative to the output's max) of the whole-K tiles."""
+    from models.dit.model import DiT_models
+    from utils.synthetic import init_synthetic_
+    ref = DiT_models['DiT-S/2'](input_size=32, num_classes=1000, learn_sigma=True).eval()
+    init_synthetic_(ref)
+    sd = ref.state_dict()
+    g = torch.Generator().manual_seed(17)
+    B = 16
+    x = torch.randn((B, 4, 32, 32), generator=g).to(cuda)
+    t = torch.randint(0, 1000, (B, ), generator=g).to(cuda)
+    y = torch.randint(0, 1000, (B, ), generator=g).to(cuda)
+
+    def run(sk):
+        monkeypatch.setenv('DM_LIN_SK', sk)
+        dmhip.launch_log(True)
+        m = DiT_models['DiT-S/2'](input_size=32, num_classes=1000, learn_sigma=True).eval()
+        m.load_state_dict(sd)
+        m = m.to(cuda)
+        with torch.no_grad():
+            a = m(x, t, y).cpu()
+            b = m(x, t, y).cpu()
+        log = dmhip.launch_log_read()
+        dmhip.launch_log(False)
+        return a, b, log
+
+    on_a, on_b, log_on = run('1')
+    off_a, off_b, log_off = run('0')
+    assert 'linear_k32_sk' in log_on, log_on
+    assert 'linear_k32_sk' not in log_off, log_off
+    assert torch.isfinite(on_a).all()
+    assert torch.equal(on_a, on_b)
+    assert torch.equal(off_a, off_b)
+    rel = ((on_a - off_a).abs().max() / off_a.abs().max()).item()
+    report('linear_split_k_tail_dit_s2_rel_vs_whole_k', rel)
+    assert rel <= 1e-5, rel
