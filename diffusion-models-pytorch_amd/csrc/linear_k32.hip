@@ -769,3 +769,56 @@ int linear_k32(const GemmArgs& g_in, hipStream_t st) {
 }
 
 }  // namespace dm
+
+/* Test hook (tests/test_gpu_r5.py): one linear_k32 launch on weights W [N][K] split here, A fp32 rows (presplit 0:
+ * in-GEMM split, with the GroupNorm affine of pro_scale / pro_shift [M / pro_rows][K] when given; 1: through
+ * linear_presplit_a, PRO 3), C = A W^T (+ bias, + res), 2^ea on A; sk 1 with the split-K tail's workspace (the
+ * kernel decides whether the shape has a tail to split), 0 without. Synchronous; allocates and frees its buffers. */
+extern "C" int dm_debug_linear_k32(const float* A, int lda, const float* W, const float* bias, const float* res,
+                                   int ld_res, const float* pro_scale, const float* pro_shift, int pro_rows, float* C,
+                                   int ldc, int M, int N, int K, int ea, int presplit, int sk, void* stream) {
+  using namespace dm;
+  refresh_toggles();
+  hipStream_t st = (hipStream_t)stream;
+  void* ws = nullptr;
+  _Float16* as = nullptr;
+  float* skw = nullptr;
+  unsigned* skc = nullptr;
+  int rc = DM_OK;
+  auto fail = [&](const char* m) {
+    set_error(m);
+    return DM_ERR_HIP;
+  };
+  do {
+    if (hipMalloc(&ws, split_conv_weights_bytes(1, N, K, 2)) != hipSuccess) { rc = fail("alloc"); break; }
+    if ((rc = split_conv_weights(W, 1, N, K, K, 1, 2, ws, st)) != DM_OK) break;
+    GemmArgs g{};
+    g.M = M; g.N = N; g.K = K; g.Z1 = 1; g.Z2 = 1;
+    g.A = A; g.lda = lda; g.C = C; g.ldc = ldc; g.alpha = 1.f;
+    g.bias = bias; g.res = res; g.ld_res = ld_res;
+    g.pro_scale = pro_scale; g.pro_shift = pro_shift; g.pro_rows = pro_rows;
+    g.split = 2; g.split_ea = ea;
+    g.ws = ws; g.ws_rowscale = split_conv_rowscale(ws, 1, N, K);
+    if (presplit) {
+      if (hipMalloc(&as, (size_t)M * K * 4) != hipSuccess) { rc = fail("alloc"); break; }
+      if ((rc = linear_presplit_a(g, as, st)) != DM_OK) break;
+      g.as = as;
+      g.pro_scale = g.pro_shift = nullptr;
+    }
+    if (sk) {
+      const int slots = linear_k32_slots();
+      if (slots <= 0) { rc = fail("no occupancy"); break; }
+      if (hipMalloc(&skw, (size_t)slots * 65536) != hipSuccess || hipMalloc(&skc, (size_t)slots * 4) != hipSuccess ||
+          hipMemsetAsync(skc, 0, (size_t)slots * 4, st) != hipSuccess) { rc = fail("alloc"); break; }
+      g.sk_ws = skw; g.sk_cnt = skc; g.sk_cap = slots;
+    }
+    if ((rc = linear_k32(g, st)) != DM_OK) break;
+    if (hipStreamSynchronize(st) != hipSuccess) rc = fail("sync");
+  } while (false);
+  (void)hipStreamSynchronize(st);
+  if (ws) (void)hipFree(ws);
+  if (as) (void)hipFree(as);
+  if (skw) (void)hipFree(skw);
+  if (skc) (void)hipFree(skc);
+  return rc;
+}

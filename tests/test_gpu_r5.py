@@ -252,3 +252,71 @@ def test_linear_split_k_tail(cuda, monkeypatch, report):
     rel = ((on_a - off_a).abs().max() / off_a.abs().max()).item()
     report('linear_split_k_tail_dit_s2_rel_vs_whole_k', rel)
     assert rel <= 1e-5, rel
+
+
+def _linear_k32(A, W, bias=None, res=None, sc=None, sh=None, rows=0, ea=0, presplit=0, sk=1):
+    """dm_debug_linear_k32: one linear_k32 launch (weights split in the hook), with or without the split-K tail's
+    workspace."""
+    import ctypes
+    from dmhip import _lib
+    L = _lib.load()
+    f = L.dm_debug_linear_k32
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                  ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    M, K = A.shape
+    N = W.shape[0]
+    C = torch.full((M, N), float('nan'), device=A.device)
+    p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    _lib.check(f(p(A), K, p(W), p(bias), p(res), N, p(sc), p(sh), rows, p(C), N, M, N, K, ea, presplit, sk,
+                 torch.cuda.current_stream().cuda_stream), 'dm_debug_linear_k32')
+    return C
+
+
+# (M, N, K): tile counts 64 (tail 64: 4 slices; partial M and N tiles, 9 K stages split 3/2/2/2), 1152 (the DiT-XL/2
+# proj shape: tail 128, 2 slices), 96 (K = 128: 2 stages, 2 slices), 600 (tail 88: 2 slices of 9)
+SK_SHAPES = [(1000, 996, 576), (16384, 1152, 1152), (4096, 384, 128), (7680, 1280, 1152)]
+
+
+@pytest.mark.parametrize('M,N,K', SK_SHAPES)
+@pytest.mark.parametrize('form', ['fp32', 'presplit', 'groupnorm'])
+def test_linear_k32_split_k_tail_vs_fp64(cuda, report, M, N, K, form):
+    """linear_k32 with the split-K tail (write-through slabs, arrival ticket, slice-order reduce) against the whole-K
+    tiles and a float64 reference, across the A forms (in-GEMM split, pre-split A, GroupNorm prologue), with bias and
+    residual epilogues and partial tiles: the split launch agrees with the whole-K one to fp32 re-association
+    (<= 2e-6 of the output's max) and both meet the fp16x2 bound against float64; two split launches are
+    bit-identical (the reducer sums in slice order whichever block arrives last)."""
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn((M, K), generator=g).to(cuda)
+    W = (torch.randn((N, K), generator=g) / K ** 0.5).to(cuda)
+    bias = torch.randn((N, ), generator=g).to(cuda)
+    res = torch.randn((M, N), generator=g).to(cuda)
+    kw = dict(bias=bias, res=res, ea=4)
+    Ar = A.double()
+    if form == 'presplit':
+        kw['presplit'] = 1
+    if form == 'groupnorm':
+        rows = 128 if M % 128 == 0 else M
+        imgs = (M + rows - 1) // rows
+        sc = (torch.rand((imgs, K), generator=g) + 0.5).to(cuda)
+        sh = (torch.rand((imgs, K), generator=g) - 0.5).to(cuda)
+        kw.update(sc=sc, sh=sh, rows=rows)
+        idx = torch.arange(M, device=cuda) // rows
+        Ar = (A * sc[idx] + sh[idx]).double()  # (the kernel's fp32 mul + add, then the split)
+    ref = Ar @ W.double().t() + bias.double() + res.double()
+    dmhip.launch_log(True)
+    whole = _linear_k32(A, W, sk=0, **kw)
+    assert 'linear_k32_sk' not in dmhip.launch_log_read()
+    split1 = _linear_k32(A, W, sk=1, **kw)
+    assert dmhip.launch_log_read().count('linear_k32_sk') == 1  # this shape has a tail to split
+    dmhip.launch_log(False)
+    split2 = _linear_k32(A, W, sk=1, **kw)
+    assert torch.isfinite(split1).all()
+    assert torch.equal(split1, split2)
+    scale = ref.abs().max().item()
+    rel_sk = (split1.double() - whole.double()).abs().max().item() / scale
+    rel_ref = max((split1.double() - ref).abs().max().item(), (whole.double() - ref).abs().max().item()) / scale
+    report(f'linear_k32_sk_{form}_{M}x{N}x{K}_rel_vs_whole_k', rel_sk)
+    report(f'linear_k32_sk_{form}_{M}x{N}x{K}_rel_vs_fp64', rel_ref)
+    assert rel_sk <= 2e-6, rel_sk
+    assert rel_ref <= 2e-6, rel_ref
