@@ -41,7 +41,10 @@ void note_launch(const char* name);
 
 // Nominal batch of the plans' tile heuristics (ConvArgs::pick_B, GemmArgs::pick_M / pick_Z): every layer
 // runs the kernel it would at B = kPickBatch, whatever B is, so each image's result is bit-identical at
-// any batch size (the reference parity pinned at B = 1..2 holds at the benchmark's B).
+// any batch size (the reference parity pinned at B = 1..2 holds at the benchmark's B). One exception, by
+// design: linear_k32's split-K tail (GemmArgs::sk_*, DiT plans) re-associates the sums of the tiles in a
+// launch's last partial round, so a DiT row agrees across batch sizes to fp32 re-association (DM_LIN_SK=0:
+// bit for bit; tests/test_gpu_r3.py test_dit_xl2_cfg_batch64).
 constexpr int kPickBatch = 256;
 
 struct ConvArgs {

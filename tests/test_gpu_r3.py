@@ -185,11 +185,16 @@ def _xl2(cuda, golden):
     return m.to(cuda), meta
 
 
-def test_dit_xl2_cfg_batch64(cuda, golden, report):
+@pytest.mark.parametrize('sk', ['1', '0'])
+def test_dit_xl2_cfg_batch64(cuda, golden, report, monkeypatch, sk):
     """BASELINE config C5's forward: DiT-XL/2, 32 images per GPU as one CFG batch of 2B = 64 rows (rows
     32..63 the null class, y = -1 inside the samplers' null-label scope). Row 0 / row 32 are the pinned
-    dit_xl2 input with its label / the null class: within 1e-4 of oracle/dit.py; rows 0, 31, 32 and 63 equal
-    B = 1 forwards bit for bit, so the B = 1 oracle parity extends to the benchmark batch."""
+    dit_xl2 input with its label / the null class: within 1e-4 of oracle/dit.py; rows 0, 31, 32 and 63 against
+    B = 1 / B = 2 forwards, so the B = 1 oracle parity extends to the benchmark batch: bit for bit with every tile
+    over the whole K (DM_LIN_SK=0); with linear_k32's split-K tail (the default) a tile's sum is re-associated
+    when it falls in a launch's last partial round -- which tiles do depends on the batch -- so within 2e-6 of
+    the output's max (fp32 re-association; measured ~5e-7)."""
+    monkeypatch.setenv('DM_LIN_SK', sk)
     g, _ = golden('dit')
     model, meta = _xl2(cuda, golden)
     gen = torch.Generator().manual_seed(64)
@@ -209,11 +214,19 @@ def test_dit_xl2_cfg_batch64(cuda, golden, report):
         report('dit_xl2_2B64_row0_cond_maxabs_vs_oracle', e_c)
         report('dit_xl2_2B64_row32_null_maxabs_vs_oracle', e_u)
         assert e_c <= TOL and e_u <= TOL, (e_c, e_u)
+        scale = big.abs().max().item()
+        worst = 0.0
         for r in (0, 31, 32, 63):
             one = model(x2[r:r + 1].contiguous(), t2[r:r + 1].contiguous(), y2[r:r + 1].contiguous())
-            assert torch.equal(big[r:r + 1], one), r
+            if sk == '0':
+                assert torch.equal(big[r:r + 1], one), r
+            worst = max(worst, (big[r:r + 1] - one).abs().max().item() / scale)
         two = model(x2[[0, 63]].contiguous(), t2[[0, 63]].contiguous(), y2[[0, 63]].contiguous())
-        assert torch.equal(two, big[[0, 63]])
+        if sk == '0':
+            assert torch.equal(two, big[[0, 63]])
+        worst = max(worst, (two - big[[0, 63]]).abs().max().item() / scale)
+        report(f'dit_xl2_2B64_rows_vs_B1_rel_sk{sk}', worst)
+        assert worst <= 2e-6, worst
     assert torch.isfinite(big).all()
     del model, big
     torch.cuda.empty_cache()
