@@ -742,7 +742,8 @@ int linear_k32(const GemmArgs& g_in, hipStream_t st) {
   // tail's unsplit tiles already run one per CU, at a CU's whole issue rate.) Those tiles' sums are re-associated (slice partials summed in slice
   // order): not bit-identical to the whole-K tile, so a row's result depends on whether its tile is in the
   // tail (DM_LIN_SK=0: every tile whole).
-  const int nst = g.K / 64, P = linear_k32_slots(), cus = lin_slots().cus;
+  const int nst = g.K / 64;
+  const int P = g.sk_ws ? linear_k32_slots() : 0, cus = g.sk_ws ? lin_slots().cus : 0;  // (queried at plan build)
   if (g.sk_ws && g.sk_cnt && nst >= 2 && P > 0) {
     const int tail = tiles % P;
     if (tail > 0 && 2 * tail <= P) {

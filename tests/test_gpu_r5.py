@@ -320,3 +320,26 @@ def test_linear_k32_split_k_tail_vs_fp64(cuda, report, M, N, K, form):
     report(f'linear_k32_sk_{form}_{M}x{N}x{K}_rel_vs_fp64', rel_ref)
     assert rel_sk <= 2e-6, rel_sk
     assert rel_ref <= 2e-6, rel_ref
+
+
+def test_linear_split_k_tail_plan_cache(cuda):
+    """The split-K tail's arrival counters are shared by a DiT model's cached plans (one workspace per model, the
+    reducing block resets its tile's counter): alternating batch sizes (plans built, captured and replayed in turn)
+    gives the same bits for the same batch every time."""
+    from models.dit.model import DiT_models
+    from utils.synthetic import init_synthetic_
+    m = DiT_models['DiT-S/2'](input_size=32, num_classes=1000, learn_sigma=True).eval()
+    init_synthetic_(m)
+    m = m.to(cuda)
+    g = torch.Generator().manual_seed(23)
+    xs = {B: (torch.randn((B, 4, 32, 32), generator=g).to(cuda), torch.randint(0, 1000, (B, ), generator=g).to(cuda),
+              torch.randint(0, 1000, (B, ), generator=g).to(cuda)) for B in (16, 3, 24)}
+    first = {}
+    with torch.no_grad():
+        for B in (16, 3, 24, 16, 24, 3, 16):
+            out = m(*xs[B]).cpu()
+            assert torch.isfinite(out).all()
+            if B in first:
+                assert torch.equal(out, first[B]), B
+            else:
+                first[B] = out
