@@ -121,8 +121,8 @@ __global__ void softmax_rows_kernel(float* __restrict__ x, long rows, int L, int
 }
 
 // first conv: NCHW input with few channels -> NHWC (pitched) output.
-// One block per R output rows of one image (R = 64 / W for W < 64, so a block is one 64-pixel GroupNorm
-// chunk; else one row). The R + 2 input rows and the weights sit in LDS (coalesced loads). Thread t owns the
+// One block per R output rows of one image (R = 2 * 64 / W for W < 64, so a block is two 64-pixel GroupNorm
+// chunks -- small_in_rows; else one row). The R + 2 input rows and the weights sit in LDS (coalesced loads). Thread t owns the
 // output channel pair 2 cp, 2 cp + 1 (cp = t % (Cout / 2); its 2 x 9 Cin weights in registers) and a run of
 // pixels of the block: per pixel 9 Cin packed multiply + packed add pairs (v_pk_mul_f32 / v_pk_add_f32, both
 // channels from one broadcast input value) over a 3-column window whose column slots rotate (no register
@@ -636,7 +636,17 @@ int softmax_rows(float* x, long rows, int L, int ld, hipStream_t st) {
 }
 
 // rows per block of the first conv: a whole 64-pixel chunk when W < 64 divides it, else one row
-static int small_in_rows(int H, int W) { return (W < kGnPixPerChunk && kGnPixPerChunk % W == 0 && H % (kGnPixPerChunk / W) == 0) ? kGnPixPerChunk / W : 1; }
+// Rows per block: two 64-pixel GroupNorm chunks of a narrow map (the CIFAR first conv: 4 rows of 32, 1024 blocks
+// at B = 256) -- the per-block staging of the 3456 weights and the rows amortised over twice the pixels: C3 A/B
+// +0.24 % over one chunk per block (3 alternations; four chunks +0.17 %)
+constexpr int kSiChunksPerBlock = 2;
+static int small_in_rows(int H, int W) {
+  if (!(W < kGnPixPerChunk && kGnPixPerChunk % W == 0 && H % (kGnPixPerChunk / W) == 0)) return 1;
+  int R = kGnPixPerChunk / W;
+  for (int m = 1; m < kSiChunksPerBlock && H % (2 * R) == 0 && (2 * R * W) / kGnPixPerChunk <= kSiMaxChunks; m *= 2)
+    R *= 2;
+  return R;
+}
 
 bool conv3x3_small_in_can_emit(int H, int W, int Cout, int G) {
   const int R = small_in_rows(H, W);
