@@ -9,12 +9,13 @@
 // weights by their row scale, both undone exactly in the epilogue. |scaled activation| > 65504 raises
 // range_flag (the caller re-runs in fp32 / bf16x3).
 //
-// Block 128 x 128, four waves of 64 x 64 (4 x 4 tiles of 16 x 16). K is staged 64 channels at a time
+// Block 128 x 128, four waves of 128 x 32 (8 x 2 tiles of 16 x 16). K is staged 64 channels at a time
 // (two K = 32 steps per barrier), double-buffered in LDS as rows of [step][piece][4 k-groups][8] fp16 with
 // a 288-B pitch (18 x 16-B slots: the 16-row fragment reads are conflict free, searched offline); the
 // prologue (GroupNorm affine, or LayerNorm + adaLN modulate with per-row statistics) is applied on the
 // way into LDS with its per-(image, channel) tables staged per K stage. B fragments from L2 into a 2-deep
-// register ring. Epilogue staged through LDS so every lane stores 16 B.
+// register ring. Epilogue staged through LDS so every lane stores 16 B. A launch whose last round of tiles is
+// at most half full splits those tiles over K (the split-K tail: GemmArgs::sk_*, linear_k32 below).
 #include "dm_common.h"
 #include "dm_kernels.h"
 #include "mfma_tile.h"
@@ -54,9 +55,9 @@ constexpr int kLGM = 4;    // M tiles per group of the tile order
 // PRO: 0 none, 1 GroupNorm affine (pro_scale / pro_shift [img][K]), 2 LayerNorm + modulate, 3 pre-split A
 // (GemmArgs::as: no conversion on the way into LDS -- the split of A costs VALU work once per N tile
 // otherwise, which with K = 256 (the UNet's qkv) left the MFMAs idle most of the K loop).
-// Wave tiles WM x WN: 128 x 32 (each wave all 128 rows from LDS, its own 32 weight columns: every B
+// Wave tiles WM x WN = 128 x 32 (each wave all 128 rows from LDS, its own 32 weight columns: every B
 // fragment fetched once per block, half the L2 traffic of 64 x 64 wave tiles, where each weight fragment is
-// loaded by both row waves) or 64 x 64.
+// loaded by both row waves).
 // One 32 x WN slab (acc * rowscale * 2^-ea, no bias yet) of the qkv projection -> the attention operand
 // planes: q * alpha * 2^ea and k * b_scale * 2^eb as [B][heads][2][L][Dh], v * 2^ev transposed as
 // [B][heads][2][Dh][L] (plane 0 = fp16(x), plane 1 = fp16(x - plane 0)), 16-B stores. The slab's columns lie
