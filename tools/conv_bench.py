@@ -31,6 +31,9 @@ SHAPES = {
     'res4_256': (256, 256, 256, 4, True, 0),
     'res4_512': (256, 512, 256, 4, True, 0),      # up-path conv1 at 4x4 with concat input
     'up16_256': (256, 256, 256, 16, False, 2),     # sub-pixel upsample 16 -> 32
+    'up8_256': (256, 256, 256, 8, False, 2),       # sub-pixel upsample 8 -> 16
+    'up4_256': (256, 256, 256, 4, False, 2),       # sub-pixel upsample 4 -> 8 (conv_patch3 MODE 2)
+    'down8_256': (256, 256, 256, 8, True, -2),     # stride-2 downsample 8 -> 4 (conv_patch3 MODE 4)
     'qkv16': (256, 256, 768, 16, True, -1),        # attention qkv: 1x1 conv (GroupNorm prologue, no SiLU)
     'proj16': (256, 256, 256, 16, False, -1),      # attention proj: 1x1 conv
 }
@@ -41,6 +44,9 @@ def run(name, iters, split, tile=0, ksplit=0):
     dev = torch.device('cuda', 0)
     g = torch.Generator(device='cpu').manual_seed(0)
     x = torch.randn((B, H, H, Cin), generator=g).to(dev)
+    stride = 1
+    if up == -2:  # stride-2 downsample
+        up, stride = 0, 2
     taps = 1 if up < 0 else 9
     w = (torch.randn((Cout, Cin, 3, 3) if taps == 9 else (Cout, Cin, 1, 1), generator=g) * 0.02).to(dev)
     if up < 0:  # 1x1 (only the split path runs it with the prologue)
@@ -57,14 +63,14 @@ def run(name, iters, split, tile=0, ksplit=0):
     else:
         wp = torch.zeros((Cout, 9 * Cin), device=dev)
         dmhip.pack_conv_weight(w, wp, 9 * Cin, 0)
-        Ho = H
+        Ho = H // stride
     b = torch.zeros(Cout, device=dev)
     y = torch.empty((B, Ho, Ho, Cout), device=dev)
     sc = torch.rand((B, Cin), device=dev) + 0.5
     sh = torch.rand((B, Cin), device=dev) - 0.5
     d = dmhip.ConvDesc()
     d.x, d.x_pitch, d.Cin, d.Hin, d.Win = x.data_ptr(), Cin, Cin, H, H
-    d.taps, d.stride, d.upsample = taps, 1, up
+    d.taps, d.stride, d.upsample = taps, stride, up
     d.pro_nosilu = int(taps == 1)
     d.w, d.K = wp.data_ptr(), wp.shape[1]
     d.y, d.y_pitch, d.Cout, d.B, d.Hout, d.Wout = y.data_ptr(), Cout, Cout, B, Ho, Ho
