@@ -472,9 +472,10 @@ def main():
         wl = build_workload(args.workload, args, dev, rank)
     B, shape = wl['images'], wl['shape']
     gathered = torch.empty((world * B, *shape[1:]), device=dev) if world > 1 else None
-    comm, gather_path = None, None
+    comm, gather_path, gather_check = None, None, None
     if world > 1:
         gather_path = 'torch.distributed' if backend == 'nccl' else f'{backend} (host)'
+        gather_check = f'not run ({backend} host gather)' if backend != 'nccl' else 'not run (DM_GATHER=torch)'
     if world > 1 and backend == 'nccl' and os.environ.get('DM_GATHER') != 'torch':
         from dmhip.comm import Comm   # the C-ABI RCCL all-gather (dm_allgather_f32), bootstrapped over the group
         # every rank gets the communicator or every rank gathers with torch.distributed
@@ -483,6 +484,7 @@ def main():
             print(f'bench.py: rank {rank}: dm_comm could not be set up on every rank; gathering with torch.distributed',
                   file=sys.stderr)
             gather_path = 'torch.distributed (dm_comm unavailable on some rank)'
+            gather_check = 'not run (dm_comm unavailable on some rank)'
         else:
             # before the timed region: the C-ABI gather of a rank-tagged fold against all_gather_into_tensor, agreed
             # over the ranks; on any difference every rank drops to torch.distributed
@@ -495,6 +497,7 @@ def main():
             dist.all_gather_into_tensor(ref, probe)
             same = torch.tensor([1 if torch.equal(got, ref) else 0], dtype=torch.int32, device=dev)
             dist.all_reduce(same, op=dist.ReduceOp.MIN)
+            gather_check = 'equal on every rank' if int(same.item()) else 'differed on some rank'
             if int(same.item()):
                 gather_path = 'dm_allgather_f32 (RCCL, C ABI; equal to all_gather_into_tensor at start)'
             else:
@@ -533,10 +536,29 @@ def main():
     sync()
     barrier()
     elapsed = time.perf_counter() - t0
+    ranks = None
     if world > 1:
+        # what each rank saw, for a record that verifies itself: its device, its own fold time,
+        # the RCCL communicator's own view (ncclCommCount / ncclCommUserRank / device through dm_comm_info)
+        mine = dict(rank=rank, device=str(dev), fold_ms=round(elapsed / args.steps * 1e3, 3))
+        if not stub:
+            props = torch.cuda.get_device_properties(gpu)
+            mine.update(gpu_name=props.name, pci_bus_id=getattr(props, 'pci_bus_id', None),
+                        pci_device_id=getattr(props, 'pci_device_id', None))
+        if comm is not None:
+            n_, r_, d_ = comm.info()
+            mine.update(comm_nranks=n_, comm_rank=r_, comm_device=d_)
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
         tt = torch.tensor([elapsed], device=dev if backend == 'nccl' else 'cpu', dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = tt.item()
+        comm_n = sorted({r.get('comm_nranks') for r in per_rank}, key=str)
+        ranks = dict(process_group_size=dist.get_world_size(), backend=backend,
+                     comm_nranks=comm_n[0] if len(comm_n) == 1 else comm_n,
+                     distinct_devices=len({(r.get('pci_bus_id'), r.get('pci_device_id'), r['device'])
+                                           for r in per_rank}),
+                     gather_check=gather_check, per_rank=per_rank)
     prof, kernel_s, wbytes_t, wsbytes_t = [], 0.0, 0, 0
     # launches per network forward of each kernel label: each handle's ops with the label, weighted by its forwards
     lpf, nfwd = {}, sum(f for _, _, f in wl['handles'])
@@ -586,6 +608,7 @@ def main():
                         skip_unused_noise=wl['diffuser'].skip_unused_noise if wl['diffuser'] else None,
                         gather=gather_path),
             roofline=roof,
+            ranks=ranks,
             step_level=dict(model_tflops=round(total_flops / (total_gpu_ms * 1e-3) / 1e12, 2) if total_gpu_ms else None,
                             # observed forwards are 1 in PROFILE_EVERY: their event-summed launch time scaled to
                             # all forwards, over the wall time. The events bracket every launch of an observed

@@ -18,8 +18,10 @@
 // K step as conv_k32's 64 x 64 wave tiles -- so the operand traffic per MFMA is conv_k32's, and the 8 waves
 // (two per SIMD) keep the same occupancy in one block per CU.
 // LDS: per 32-channel chunk the transformed patch, [nu][(TH + 2) x NP pair rows][piece][4 k-groups][8] fp16 with
-// conv_k32's 160-B row pitch (A fragment i of tap row dy for wave nu = 16 consecutive rows
-// nu NR + 16 i + dy NP: conflict-free ds_read_b128), double buffered, one barrier per chunk. The loader: lane j
+// conv_k32's 160-B row pitch and the k-group bit swizzled by row (wswz below: A fragment i of tap row dy for wave
+// nu = 16 consecutive rows nu NR + 16 i + dy NP, conflict-free ds_read_b128; the loader's stores at most 2-way),
+// double buffered, one barrier per chunk. B: raw buffer loads from the U images, the wave-uniform part of each
+// address in the scalar offset. The loader: lane j
 // of a (patch row, 8-channel quarter) unit loads pixels 2j, 2j + 1, applies GroupNorm + SiLU, and takes its
 // neighbours' 2j - 1 and 2j + 2 from lanes j -/+ 1 by DPP row shifts (each pixel normalised once).
 // Epilogue: the 8 waves' m_nu tiles (row scale undone) into LDS, then each wave takes 32 output pixels x 64
@@ -51,6 +53,14 @@ constexpr int kWC = 32;                        // input channels per chunk (K of
 constexpr int kWRowH = 80;                     // LDS row pitch in fp16 (160 B), as conv_k32
 constexpr int kWNR = 96;                       // pair rows per nu plane at most: (TH + 2) NP = 6 x 16 / 10 x 8
 constexpr int kWBuf = 4 * kWNR * kWRowH;       // fp16 per patch buffer (61440 B)
+
+// Patch row layout: 16-B slots s = 4 piece + k-group, the k-group's low bit XORed with bit 2 of the pair row (slot s
+// of row r at 16 (s ^ wswz(r)) bytes). Chosen by an offline search over the pitch and the linear XOR maps of r mod 16
+// against the two access patterns (MI355X_MICROARCH.md LDS table): the A-fragment ds_read_b128 (16 rows from any
+// base) stay conflict-free and the loader's ds_write_b64 (16 lanes: 16 rows of one 8-B half at W 32, 8 rows x both
+// halves at W 16, 4 rows x 2 k-groups x 2 halves at W 8) go from 4-way / 2-way / 1 to 2-way (the minimum for one half)
+// / 1 / 1. The piece bit is untouched, so a fragment's two pieces stay 64 B apart (one address, two offsets).
+__device__ __forceinline__ int wswz(int r) { return (r >> 2) & 1; }
 constexpr int kWTab = 4096;                    // GroupNorm table floats: one image, Cin <= 2048 (scales, shifts)
 constexpr int kWEP = 68;                       // epilogue plane pitch (floats)
 constexpr int kWSmem = 4 * 2 * 64 * kWEP * 4;     // the epilogue's m planes (139264 B), over the two patch buffers
@@ -189,11 +199,20 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     lpr[k] = min(NP == 16 ? s_ >> 1 : NP == 8 ? s_ : 2 * s_ + (lane >> 5), PR - 1);
     ltab[k] = IMGS == 1 ? 0 : (lpr[k] / PRI) * 2 * a.Cin1;
   }
-  const int ldst = lj * kWRowH + loff;  // the lane's offset in a patch row group
+  // the lane's offset in a patch row group (pair row lpr NP + lj: its swizzle bit depends on the lane only -- lpr NP
+  // is a multiple of 8, or at W 8 of 4 with lpr's parity the lane's half-wave)
+  const int ldst = lj * kWRowH + 8 * ((loff >> 3) ^ wswz(NP == 4 ? 4 * (lane >> 5) + lj : lj)) + (loff & 4);
   const int Kp = NTAP * a.Cin1 + (SC ? a.Cin2 / 2 : 0);  // K of each U matrix (their stride in the image)
   const int ngrp = ceil_div(N, 32);
   const size_t sl = (size_t)ngrp * 1024;  // fp16 per 16-deep slice of the U images
-  const size_t qoff = (size_t)(q >> 1) * NTAP * sl;
+  // B (the U images) by raw buffer loads: the lane's part of the address in voffset (column l16 + 16 (q & 1) of the
+  // 32-column group, the 16-slice of k-groups 2, 3 for q >= 2: 3 slices on in the tap-row steps, 1 in the shortcut
+  // steps), the wave-uniform rest in soffset -- no 64-bit VALU address arithmetic per refill
+  const __amdgpu_buffer_rsrc_t wrs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.wino_ws), 0, 0x7FFFFFFF, 0x00020000);
+  const int vb_lane = ((q & 1) * 32 + l16) * 16;
+  const int vb_main = vb_lane + (q >> 1) * NTAP * (int)sl * 2, vb_sc = vb_lane + (q >> 1) * (int)sl * 2;
+  const int nu_u = wave_u >> 1, ch_u = wave_u & 1;
   const int nch = a.Cin1 / kWC;
   const int kt_end = nch * NTAP;
 
@@ -202,7 +221,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   bool rok[2] = {false, false};
   // the set's pixel 2 lj (pixel 2 lj + 1 one pitch on; padding rows: the zero page, which covers a pitch and a row)
   const float* pp[2] = {nullptr, nullptr};
-  const _Float16* wbase = nullptr;
+  int wcol = 0;  // bytes: the wave's nu plane and 32-column group of the tile (uniform)
   auto set_tile = [&](int tile) DM_WINO_INL {
     const int mt = tile / nN, nt = tile - mt * nN;
     m0 = b0 * HW + mt * 128;
@@ -216,8 +235,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     }
     // column n0 + ch 64 + 16 j + l16 (n0 % 128 == 0): 32-column group (n0 + ch 64) / 32 + j / 2, column
     // 16 (j & 1) + l16 of it -- one base pointer, compile-time offsets per j
-    wbase = reinterpret_cast<const _Float16*>(a.wino_ws) + (size_t)nu * (Kp / 16) * sl +
-            (size_t)((n0 + ch * 64) >> 5) * 1024 + ((q & 1) * 32 + l16) * 8;
+    wcol = __builtin_amdgcn_readfirstlane((nu_u * (Kp / 16) * (int)sl + ((n0 + ch_u * 64) >> 5) * 1024) * 2);
   };
 
   // chunk c + 1's pixels: loaded a chunk ahead (right after the previous finish), finished before / after chunk c's
@@ -298,37 +316,44 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   };
 
   // ---- B: the fp16x2 fragment images of U_nu (split_conv_weights, nmat 4, ntap 3), 16-column halves
-  auto slice_off = [&](int kt) DM_WINO_INL { return (size_t)(kt + (kt / NTAP) * NTAP) * sl + qoff; };
-  // all K steps of a tile: the 3 nch tap rows, then the ns shortcut steps (16-slices 3 Cin1 / 16 + 2 s (+ 1 for
-  // k-groups 2, 3)); past the end: the last step again (refills nothing uses)
+  // all K steps of a tile: the 3 nch tap rows (step kt = 3 c + dy: 16-slice 6 c + dy, + 3 for k-groups 2, 3), then
+  // the ns shortcut steps (16-slices 6 nch + 2 s, + 1 for k-groups 2, 3); past the end: the last step again
+  // (refills nothing uses)
   const int ns = SC ? a.Cin2 / (2 * kWC) : 0, nst = kt_end + ns, nst_g = nch + ns;  // K steps, stages
-  auto step_off = [&](int kt) DM_WINO_INL {
-    kt = min(kt, nst - 1);
-    return kt < kt_end ? slice_off(kt) : (size_t)(kt_end / 3 * 3 * kWC / 16 + 2 * (kt - kt_end) + (q >> 1)) * sl;
-  };
   f16x8 bq[WD][TN][2];
-  auto load_b = [&](f16x8 (&dst)[TN][2], size_t off) {
+  auto load_b = [&](f16x8 (&dst)[TN][2], int kt) DM_WINO_INL {
+    kt = __builtin_amdgcn_readfirstlane(min(kt, nst - 1));
+    // branch-free (a uniform select of two VGPRs became a branch around every refill): the shortcut case only in
+    // the SC kernels, its voffset by a bit blend under an all-ones / all-zeros scalar mask
+    const int msc = SC ? -(int)(kt >= kt_end) : 0;
+    const int so = wcol + (((kt + (kt / NTAP) * NTAP) & ~msc) | ((2 * nch * NTAP + 2 * (kt - kt_end)) & msc)) * (int)sl * 2;
+    const int vo = SC ? (vb_main & ~msc) | (vb_sc & msc) : vb_main;
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int p = 0; p < 2; ++p)
-        dst[j][p] = *reinterpret_cast<const f16x8*>(wbase + off + (j >> 1) * 1024 + (j & 1) * 128 + p * 512);
+        dst[j][p] = __builtin_bit_cast(
+            f16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, vo + ((j >> 1) * 1024 + (j & 1) * 128 + p * 512) * 2, so, 0));
   };
 
   f4 acc[TM][TN];
-  // tap row dy: A fragment i = pair rows nu NR + 16 i + l16 + dy NP of buffer pbuf, the lane's k-group q
-  const int abase = (nu * NR + l16) * kWRowH + q * 8;
+  // tap row dy: A fragment i = pair rows nu NR + 16 i + l16 + dy NP of buffer pbuf, the lane's k-group q (swizzled:
+  // every fragment's first row is a multiple of 8 except the W 8 tap rows at 4 dy, where the swizzle bit flips)
+  const int abase = (nu * NR + l16) * kWRowH + 8 * (q ^ wswz(l16));
+  const int abase_x = NP == 4 ? abase + 8 - 16 * ((q ^ wswz(l16)) & 1) : abase;  // (W 8, odd dy)
+  auto arow_base = [&](int dy) DM_WINO_INL { return ((dy * NP) & 4) ? abase_x : abase; };
   // a0: tile 0's fragment of this tap row on entry (read ahead); within a chunk, the next tap row's on exit
   f16x8 a0[2];
   auto read_a0 = [&](int dy, int pbuf) DM_WINO_INL {
-    const _Float16* As = patch + pbuf * kWBuf + abase + dy * NP * kWRowH;
+    const _Float16* As = patch + pbuf * kWBuf + arow_base(dy) + dy * NP * kWRowH;
     a0[0] = *reinterpret_cast<const f16x8*>(As);
     a0[1] = *reinterpret_cast<const f16x8*>(As + 32);
   };
   // pair rows 16 i .. of the tile: image i / 2 of a W 8 tile sits 2 halo rows (2 NP pair rows) further down the patch
   auto arow = [](int i) { return IMGS == 2 && i >= 2 ? 2 * NP : 0; };
   auto compute = [&](int dy, int pbuf, const f16x8 (&bv)[TN][2]) {
-    const _Float16* As = patch + pbuf * kWBuf + abase + dy * NP * kWRowH;
+    const _Float16* As = patch + pbuf * kWBuf + arow_base(dy) + dy * NP * kWRowH;
     f16x8 av[TM][2];
     av[0][0] = a0[0];
     av[0][1] = a0[1];
@@ -361,7 +386,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     rw[3] = *reinterpret_cast<const f4*>(xs + a.x2_pitch + a.Cin2 / 2);
   };
   auto finish_sc = [&](int buf, int h) DM_WINO_INL {  // h 0: planes 0, 3 (H1); h 1: planes 1, 2 (H2)
-    _Float16* dst = patch + buf * kWBuf + sp * kWRowH + 4 * sks;
+    _Float16* dst = patch + buf * kWBuf + sp * kWRowH + 8 * ((sks >> 1) ^ wswz(sp)) + 4 * (sks & 1);  // (swizzled)
 #pragma unroll
     for (int v2 = 0; v2 < 2; ++v2) {
       const int v = h ? 1 + v2 : 3 * v2;
@@ -447,13 +472,13 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   int tile = t_first;
   set_tile(tile);
 #pragma unroll
-  for (int d = 0; d < WD - 1; ++d) load_b(bq[d], step_off(d));
+  for (int d = 0; d < WD - 1; ++d) load_b(bq[d], d);
   load_raw(0);
   build_table();
   __syncthreads();
   finish(0, 0);
   load_stage(min(1, nst_g - 1));
-  load_b(bq[WD - 1], step_off(WD - 1));
+  load_b(bq[WD - 1], WD - 1);
   __syncthreads();
   W_STAMP(1);
 #ifdef DM_K32_STAMPS
@@ -518,7 +543,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
       }
       compute(dy, c & 1, bq[slot]);
 #if DM_WINO_ABL != 2 && DM_WINO_ABL != 3  // ablation builds (timing only, wrong results): 1 no finish, 2 no B refills
-      load_b(bq[slot], step_off(kt + WD));
+      load_b(bq[slot], kt + WD);
 #endif
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -559,7 +584,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
       }
       if (more2) load_sc(st + 2);
     }
-    const _Float16* As = patch + buf * kWBuf + (nu * 64 + l16) * kWRowH + q * 8;
+    const _Float16* As = patch + buf * kWBuf + nu * 64 * kWRowH + abase - nu * NR * kWRowH;
     a0[0] = *reinterpret_cast<const f16x8*>(As);
     a0[1] = *reinterpret_cast<const f16x8*>(As + 32);
     __builtin_amdgcn_sched_barrier(0);
@@ -578,7 +603,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bq[CC][j][1], av[i][0], acc[i][j], 0, 0, 0);
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bq[CC][j][0], av[i][0], acc[i][j], 0, 0, 0);
       }
-    load_b(bq[CC], step_off(kt_end + st + WD));
+    load_b(bq[CC], kt_end + st + WD);
     __builtin_amdgcn_sched_barrier(0);
     if (LATE) {
       if (more) {
@@ -656,7 +681,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
       set_tile(next);
       load_raw(0);
 #pragma unroll
-      for (int d = 0; d < WD - 1; ++d) load_b(bq[d], step_off(d));
+      for (int d = 0; d < WD - 1; ++d) load_b(bq[d], d);
     }
     __syncthreads();
     W_ACC(ew_cycles);
@@ -706,7 +731,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     __syncthreads();
     finish(0, 0);
     load_stage(min(1, nst_g - 1));
-    load_b(bq[WD - 1], step_off(WD - 1));
+    load_b(bq[WD - 1], WD - 1);
     __syncthreads();
     W_ACC(np_cycles);
   }

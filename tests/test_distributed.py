@@ -84,6 +84,21 @@ def test_bench_gpus2_launches_two_ranks():
     assert line['value'] > 0 and line['steps'] == 2
     # the fold's gather path is named in the line (on GPUs: the C-ABI RCCL all-gather, dm_allgather_f32)
     assert line['config']['gather'] == 'gloo (host)', line['config']
+    # the per-rank record: every rank's device and own fold time, the group's size, the
+    # gather check's outcome; on GPUs also the RCCL communicator's own rank count (dm_comm_info)
+    rk = line['ranks']
+    assert rk['process_group_size'] == 2 and rk['backend'] == 'gloo', rk
+    assert [r['rank'] for r in rk['per_rank']] == [0, 1], rk
+    assert all(r['device'] == 'cpu' and r['fold_ms'] > 0 for r in rk['per_rank']), rk
+    assert max(r['fold_ms'] for r in rk['per_rank']) <= line['ms_per_step'] + 0.01, (rk, line['ms_per_step'])
+    assert rk['gather_check'].startswith('not run (gloo'), rk
+    assert rk['comm_nranks'] is None, rk
+
+
+def test_bench_single_rank_has_no_rank_record():
+    rc, lines, err = _bench(['--workload', 'stub', '--steps', '1', '--warmup', '0'], {})
+    assert rc == 0, err
+    assert lines[0]['ranks'] is None and lines[0]['n_gpus'] == 1
 
 
 def test_bench_rejects_gpus_world_mismatch():
