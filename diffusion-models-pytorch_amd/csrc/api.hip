@@ -14,7 +14,8 @@ void set_error(const std::string& msg) { g_last_error = msg; }
 const char* last_error() { return g_last_error.c_str(); }
 
 namespace {
-Toggles g_toggles;
+thread_local Toggles t_toggles;                  // this thread's last refresh_toggles()
+thread_local const Toggles* t_scope = nullptr;   // the innermost ToggleScope
 bool env_is(const char* name, char c) {
   const char* e = std::getenv(name);
   return e && e[0] == c;
@@ -22,7 +23,12 @@ bool env_is(const char* name, char c) {
 bool g_launch_log_on = false;
 std::string g_launch_log;
 }  // namespace
-const Toggles& toggles() { return g_toggles; }
+const Toggles& toggles() { return t_scope ? *t_scope : t_toggles; }
+const Toggles* toggle_scope_swap(const Toggles* t) {
+  const Toggles* prev = t_scope;
+  t_scope = t;
+  return prev;
+}
 // every environment switch of the library, read here and nowhere else (DESIGN.md §6 toggle table)
 void refresh_toggles() {
   Toggles t;
@@ -47,7 +53,7 @@ void refresh_toggles() {
   t.attn_gn_launch = env_is("DM_ATTN_GNFIN", '1');
   t.dit_presplit = !env_is("DM_DIT_PRESPLIT", '0');
   t.lin_sk = !env_is("DM_LIN_SK", '0');
-  g_toggles = t;
+  t_toggles = t;
 }
 void note_launch(const char* name) {
   if (!g_launch_log_on) return;

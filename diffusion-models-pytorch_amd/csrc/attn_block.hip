@@ -60,11 +60,6 @@ __device__ unsigned long long g_ab_stamps[4096][10];
 #define AB_RSTAMP(k) do {} while (0)
 #define AB_FLUSH do {} while (0)
 #endif
-// DM_AB_ABL (diagnostic builds only, wrong results): 1 no staging refills after the first two k-steps of a
-// phase, 2 no residual loads in the epilogue
-#ifndef DM_AB_ABL
-#define DM_AB_ABL 0
-#endif
 
 // fragment-image offset (fp16 elements) of (row, lane group q, piece p) in a staged k-step, + e0
 __device__ __forceinline__ int img_off(int row, int q, int p) {

@@ -281,8 +281,13 @@ int conv2d_igemm(const ConvArgs& a, hipStream_t st) {
   DM_REQUIRE(a.tile >= 0 && a.tile <= 21, "conv: tile must be 0..21");
   if (a.tile == 21 || (a.tile == 0 && a.wino_ws)) {  // the Winograd F(2,3) kernel (conv_wino.hip)
     if (conv_wino_ok(a)) {
-      DM_REQUIRE(!a.gn_part || conv_can_emit_gn(a), "conv: GroupNorm statistics need groups of 4..32 channels");
-      return conv2d_wino(a, st);
+      if (!a.gn_part || conv_can_emit_gn(a)) return conv2d_wino(a, st);
+      DM_REQUIRE(a.tile == 0, "conv: GroupNorm statistics need groups of 4..32 channels");
+      // (automatic choice) statistics the Winograd epilogue cannot emit: the direct kernels without its weights
+      ConvArgs d = a;
+      d.wino_ws = nullptr;
+      d.wino_rowscale = nullptr;
+      return conv2d_igemm(d, st);
     }
     DM_REQUIRE(a.tile == 0, "conv: tile 21 needs Winograd weights and a shape conv_wino_kernel takes");
   }

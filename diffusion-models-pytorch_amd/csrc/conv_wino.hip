@@ -41,10 +41,6 @@ namespace dm {
 
 namespace {
 
-#ifndef DM_WINO_ABL
-#define DM_WINO_ABL 0
-#endif
-
 // the loader / tap-row / chunk lambdas are called from both roles' loop copies: always inlined (an outlined call would
 // put the accumulators and the B ring in scratch)
 #define DM_WINO_INL __attribute__((always_inline))
@@ -150,10 +146,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   constexpr int NSET = PR * 8 * NP / 64;
   static_assert(NSET * 64 == PR * 8 * NP && NSET > 8 && NSET <= 16, "loader sets");
   constexpr int TM = 4, TN = 4, NTAP = 3;
-#ifndef DM_WINO_WD
-#define DM_WINO_WD 2
-#endif
-  constexpr int WD = DM_WINO_WD;  // B ring depth: a refill issued behind the next chunk's pixel loads (in-order vmcnt)
+  constexpr int WD = 2;  // B ring depth: a refill issued behind the next chunk's pixel loads (in-order vmcnt)
                                  // is consumed WD tap rows later
   __shared__ __attribute__((aligned(16))) char smem[kWSmem];
   __shared__ __attribute__((aligned(16))) float gtab[kWTab];  // the image's GroupNorm tables (all its tiles)
@@ -179,15 +172,12 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   const int nu = wave >> 1, ch = wave & 1;
   const int l16 = lane & 15, q = lane >> 4;
   const int lj = lane & (NP - 1);  // loader: pair lj of the lane's unit
-#ifndef DM_WINO_XSET
-#define DM_WINO_XSET 1
-#endif
   // Set s covers 16-lane rows 4 s .. 4 s + 3, unit u = row (W 32), 2 row + (lane & 15) / 8 (W 16) or 4 row +
   // (lane & 15) / 4 (W 8): patch row u / 8 -- s / 2, s (the same for the wave's lanes) or 2 s + lane / 32 -- and
   // channels 4 (u & 7) .. + 3, the same in both of a wave's sets (s and s + 8). The NSET - 8 extra sets go to waves
-  // 0.. of the early role (XSET 0) or of the late role (XSET 1).
+  // 0.. of the late role.
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
-  const int xw = DM_WINO_XSET ? wave_u - 4 : wave_u;
+  const int xw = wave_u - 4;
   const bool has2 = xw >= 0 && xw < NSET - 8;
   const int loff = NP == 16 ? 16 * (wave_u & 1) + 4 * (lane >> 4)
                  : NP == 8  ? 4 * (lane >> 3)
@@ -261,22 +251,13 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     f4 e0 = rw[2 * k], e1 = rw[2 * k + 1];
     if (PROM) {
       const float* ts = rok[k] ? gtab + ltab[k] + 2 * (c * kWC + loff) : gzero;  // [4 scales][4 shifts]
-#if DM_WINO_ABL == 6
-      const f4 sc = {1.f, 1.f, 1.f, 1.f}, sh = {0.f, 0.f, 0.f, 0.f};
-#else
       const f4 sc = *reinterpret_cast<const f4*>(ts), sh = *reinterpret_cast<const f4*>(ts + 4);
-#endif
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const float z0 = __builtin_fmaf(e0[k], sc[k], sh[k]);
         const float z1 = __builtin_fmaf(e1[k], sc[k], sh[k]);
-#if DM_WINO_ABL == 5
-        e0[k] = z0;
-        e1[k] = z1;
-#else
         e0[k] = PROM == 2 ? z0 * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(z0)) : z0;
         e1[k] = PROM == 2 ? z1 * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(z1)) : z1;
-#endif
       }
     }
     f4 vv[4];
@@ -292,11 +273,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
       vv[1][k] = e0[k] + e1[k];
       vv[2][k] = e1[k] - e0[k];
     }
-#if DM_WINO_ABL == 4
-    if (a.Cout < 0) {
-#else
     {
-#endif
       _Float16* dst = patch + buf * kWBuf + lpr[k] * NP * kWRowH + ldst;
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
@@ -328,7 +305,6 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     const int msc = SC ? -(int)(kt >= kt_end) : 0;
     const int so = wcol + (((kt + (kt / NTAP) * NTAP) & ~msc) | ((2 * nch * NTAP + 2 * (kt - kt_end)) & msc)) * (int)sl * 2;
     const int vo = SC ? (vb_main & ~msc) | (vb_sc & msc) : vb_main;
-    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
@@ -508,12 +484,6 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   // compiler's memory-counter waits merge both load orders and wait for everything -- the early wave for the pixels
   // it has just requested before its first MFMA, the late wave for the B refills it has just issued before its finish.
   const bool late = wave >= 4;
-#ifndef DM_WINO_PRIO
-#define DM_WINO_PRIO 2
-#endif
-#if DM_WINO_PRIO == 1
-  if (late) __builtin_amdgcn_s_setprio(1);
-#endif
   // ---- main loop: chunk c's three tap rows from buffer c & 1, chunk c + 1 finished into the other; one barrier
   // per chunk. Two chunks per iteration (CC: the B ring slots are compile-time), an odd last chunk after the loop --
   // not a skipped half inside it, whose path into the loop head would merge a second load order there as well
@@ -523,16 +493,12 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     // the next chunk's finish and the one after's pixel loads: skipped (a uniform branch) past the tile's last chunk
     const bool more = c + 1 < nch, more2 = c + 2 < nch;
     W_PH(0);
-#if DM_WINO_ABL != 1 && DM_WINO_ABL != 3
     if (!LATE) {
       if (more) finish(c + 1, (c + 1) & 1);
       if (more2) load_raw(c + 2);
       W_PH(1);
     }
-#endif
-#if DM_WINO_PRIO == 2
-    if (LATE) __builtin_amdgcn_s_setprio(1);
-#endif
+    if (LATE) __builtin_amdgcn_s_setprio(1);  // the late role's MFMAs at priority 1 (its finish back at 0)
 #pragma unroll
     for (int dy = 0; dy < NTAP; ++dy) {
       const int kt = c * NTAP + dy;
@@ -542,21 +508,15 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
         __builtin_amdgcn_sched_barrier(0);
       }
       compute(dy, c & 1, bq[slot]);
-#if DM_WINO_ABL != 2 && DM_WINO_ABL != 3  // ablation builds (timing only, wrong results): 1 no finish, 2 no B refills
       load_b(bq[slot], kt + WD);
-#endif
       __builtin_amdgcn_sched_barrier(0);
     }
-#if DM_WINO_ABL != 1 && DM_WINO_ABL != 3
     if (LATE) {
-#if DM_WINO_PRIO == 2
       __builtin_amdgcn_s_setprio(0);
-#endif
       W_PH(1);
       if (more) finish(c + 1, (c + 1) & 1);
       if (more2) load_raw(c + 2);
     }
-#endif
     W_PH(2);
     __syncthreads();
     W_PH(3);

@@ -201,6 +201,8 @@ static int dit_create(const dm_dit_arch* arch, const float* const* params, const
 
 int DiTModel::build_plan(Plan& pl, int B) {
   refresh_toggles();
+  pl.toggles = toggles();
+  ToggleScope scope(pl.toggles);
   pl.graph_enabled = toggles().graph;
   pl.B = B;
   pl.math = math;

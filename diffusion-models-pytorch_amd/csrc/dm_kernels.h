@@ -33,8 +33,20 @@ struct Toggles {
   bool dit_presplit = true;   // DM_DIT_PRESPLIT=0: DiT token GEMMs split their activations per tile
   bool lin_sk = true;         // DM_LIN_SK=0: no split-K of linear_k32's last, partial round of tiles
 };
+// The calling thread's snapshot: the innermost ToggleScope's (a plan's, while it is built, captured or replayed op by
+// op), else the thread's last refresh_toggles(). Thread-local: plan builds in concurrent threads do not see each
+// other's writes, and a plan's launch-time checks read the decisions of its own build, not whatever
+// the environment or another call set since.
 const Toggles& toggles();
-void refresh_toggles();
+void refresh_toggles();  // this thread's snapshot from the environment
+const Toggles* toggle_scope_swap(const Toggles* t);
+struct ToggleScope {
+  const Toggles* prev;
+  explicit ToggleScope(const Toggles& t) : prev(toggle_scope_swap(&t)) {}
+  ~ToggleScope() { toggle_scope_swap(prev); }
+  ToggleScope(const ToggleScope&) = delete;
+  ToggleScope& operator=(const ToggleScope&) = delete;
+};
 // Launch log for tests (dm_debug_launch_log): the kernel instantiations the conv launchers issued, recorded in the
 // branch that launches them
 void note_launch(const char* name);

@@ -44,10 +44,6 @@ __device__ int g_lin_stamp_k;
 #define LIN_RSTAMP(k) do {} while (0)
 #endif
 
-#ifndef DM_LIN_ABL
-#define DM_LIN_ABL 0
-#endif
-
 constexpr int kLP = 144;   // LDS row pitch in fp16 (288 B) of one 64-channel stage
 constexpr int kLBM = 128;  // block rows
 constexpr int kLGM = 4;    // M tiles per group of the tile order
@@ -329,7 +325,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   // PRO 3 A loader: 16-B slot a3s = t & 15 (8 fp16 of one piece and k-group) of the stage's 256-B row span
   // in tile rows a3r + 16 u, u = 0 .. 7 -- every wave instruction reads 4 whole row spans (8 cache lines)
   // instead of 16 B of 64 different lines, as a row-half per thread did: those A refills cost 25 % of the
-  // DiT GEMMs' time (DM_LIN_ABL=2; fc1 / fc2 at 2B = 64: 663 -> 512 us). The in-GEMM prologues (PRO 0-2,
+  // DiT GEMMs' time (an ablation build without A refills; fc1 / fc2 at 2B = 64: 663 -> 512 us). The in-GEMM prologues (PRO 0-2,
   // fp32 A) keep the row-half mapping: the same remap spills them past 256 VGPRs.
   const int a3s = t & 15, a3r = t >> 4;
   const f4* asp = PRO == 3 ? reinterpret_cast<const f4*>(g.as) + a3s + 16 * sbeg : nullptr;
@@ -479,27 +475,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   // left) and the tables of stage st + 2 are loaded before step 0 -- two stages of MFMAs to land (K = 256
   // GEMMs have 4 stages: one stage did not cover the load latency); after step 1 the tables go to LDS
   // and stage st + 1 is finished into the other buffer (its tables were stored a stage earlier).
-  // DM_LIN_ABL (diagnostic builds only, wrong results): 1 no B refills, 2 no A refills, 3 no barrier
   auto stage = [&](int st, f4 (&cur)[PRO == 3 ? NU : 8], f4 (&nxt)[PRO == 3 ? NU : 8]) {
-#if DM_LIN_ABL != 2
     load_a(cur, min(st + 2, nst - 1));
-#endif
     load_tab(min(st + 2, nst - 1));
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int kk = 2 * st + s;
       compute(st & 1, s, bq[s]);
-#if DM_LIN_ABL != 1
       load_b(bq[s], min(kk + WD, nkk - 1));
-#endif
       __builtin_amdgcn_sched_barrier(0);
     }
     store_tab((st + 2) % 3);
     finish_a(nxt, (st + 1) & 1, (st + 1) % 3);
-#if DM_LIN_ABL != 3
     __syncthreads();
-#endif
   };
   for (int st = 0; st < nst; st += 2) {
     stage(st, ra[0], ra[1]);
@@ -728,6 +717,23 @@ const LinSlots& lin_slots() {
 
 int linear_k32_slots() { return lin_slots().per_cu * lin_slots().cus; }
 
+namespace {
+// The split-K tail's ways S for a GEMM of `tiles` 128 x 128 tiles and K / 64 stages with room for `cap` slices
+// (1: no split), on this device's slots (see linear_k32 below).
+int sk_ways(int tiles, int nst, int cap) {
+  const int P = linear_k32_slots(), cus = lin_slots().cus;
+  if (nst < 2 || P <= 0) return 1;
+  const int tail = tiles % P;
+  // (the tail's first block index a multiple of 8: sk_place's XCD-aware remap then keeps a tile's slices on one
+  // XCD under round-robin placement -- speed only; correctness rests on the write-through slab stores and the
+  // reducer's agent-scope acquire, which hold across XCDs too)
+  if (tail <= 0 || 2 * tail > P || (tiles - tail) % 8 != 0) return 1;
+  int S = 1;
+  while (2 * S <= 8 && 2 * S <= nst && tail * 2 * S <= cus && tail * 2 * S <= cap) S *= 2;
+  return S;
+}
+}  // namespace
+
 int linear_k32(const GemmArgs& g_in, hipStream_t st) {
   DM_REQUIRE(linear_k32_ok(g_in), "linear_k32: needs pre-split weights, K % 64 == 0, 16-byte aligned 4-column rows");
   GemmArgs g = g_in;
@@ -743,19 +749,13 @@ int linear_k32(const GemmArgs& g_in, hipStream_t st) {
   // tail's unsplit tiles already run one per CU, at a CU's whole issue rate.) Those tiles' sums are re-associated (slice partials summed in slice
   // order): not bit-identical to the whole-K tile, so a row's result depends on whether its tile is in the
   // tail (DM_LIN_SK=0: every tile whole).
-  const int nst = g.K / 64;
-  const int P = g.sk_ws ? linear_k32_slots() : 0, cus = g.sk_ws ? lin_slots().cus : 0;  // (queried at plan build)
-  if (g.sk_ws && g.sk_cnt && nst >= 2 && P > 0) {
-    const int tail = tiles % P;
-    if (tail > 0 && 2 * tail <= P) {
-      int S = 1;
-      while (2 * S <= 8 && 2 * S <= nst && tail * 2 * S <= cus && tail * 2 * S <= g.sk_cap) S *= 2;
-      if (S > 1) {
-        g.sk_S = S;
-        g.sk_tdp = tiles - tail;
-        blocks = g.sk_tdp + tail * S;
-        note_launch("linear_k32_sk");
-      }
+  if (g.sk_ws && g.sk_cnt) {  // (the slots are queried at plan build)
+    const int S = sk_ways(tiles, g.K / 64, g.sk_cap);
+    if (S > 1) {
+      g.sk_S = S;
+      g.sk_tdp = tiles - tiles % linear_k32_slots();
+      blocks = g.sk_tdp + (tiles - g.sk_tdp) * S;
+      note_launch("linear_k32_sk");
     }
   }
   if (g.as)
@@ -776,6 +776,18 @@ int linear_k32(const GemmArgs& g_in, hipStream_t st) {
  * in-GEMM split, with the GroupNorm affine of pro_scale / pro_shift [M / pro_rows][K] when given; 1: through
  * linear_presplit_a, PRO 3), C = A W^T (+ bias, + res), 2^ea on A; sk 1 with the split-K tail's workspace (the
  * kernel decides whether the shape has a tail to split), 0 without. Synchronous; allocates and frees its buffers. */
+/* Test hook: the split-K tail's ways (1: no split) linear_k32 chooses on this device for an M x N x K GEMM with the
+ * workspace dm_debug_linear_k32 gives it (one slice per resident block), and the device's resident blocks and CUs. */
+extern "C" int dm_debug_linear_k32_split(int M, int N, int K, int* S, int* slots, int* cus) {
+  using namespace dm;
+  if (M <= 0 || N <= 0 || K <= 0 || K % 64) { set_error("bad GEMM shape"); return DM_ERR_ARG; }
+  const int P = linear_k32_slots();
+  if (S) *S = P > 0 ? sk_ways(ceil_div(M, kLBM) * ceil_div(N, 128), K / 64, P) : 1;
+  if (slots) *slots = P;
+  if (cus) *cus = lin_slots().cus;
+  return DM_OK;
+}
+
 extern "C" int dm_debug_linear_k32(const float* A, int lda, const float* W, const float* bias, const float* res,
                                    int ld_res, const float* pro_scale, const float* pro_shift, int pro_rows, float* C,
                                    int ldc, int M, int N, int K, int ea, int presplit, int sk, void* stream) {

@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "dm_common.h"
+#include "dm_kernels.h"
 
 namespace dm {
 
@@ -114,6 +115,7 @@ struct PlanBase {
   long runs = 0;
   // hipGraph of the op list (captured on a private stream, launched on the caller's)
   bool graph_enabled = true;  // Toggles::graph of the plan's build (DM_NO_GRAPH)
+  Toggles toggles;            // the build's snapshot: in scope while the plan is captured or replayed op by op
   hipGraphExec_t gexec = nullptr;
   hipStream_t cap_stream = nullptr;
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
@@ -185,6 +187,7 @@ struct PlanBase {
   }
 
   int run(hipStream_t st) {
+    ToggleScope scope(toggles);  // launch-time checks decide as the build did
     const bool observe = profiling && (runs++ % profile_every) == 0;
     if (!observe && graph_enabled) {
       if (!gexec) {

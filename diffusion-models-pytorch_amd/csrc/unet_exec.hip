@@ -682,6 +682,8 @@ static int unet_create(const dm_unet_arch* arch, const float* const* params, con
 // ---------------------------------------------------------------------------
 int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
   refresh_toggles();
+  pl.toggles = toggles();
+  ToggleScope scope(pl.toggles);
   pl.graph_enabled = toggles().graph;
   pl.B = B;
   pl.math = conv_math;
@@ -892,6 +894,7 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
       sk.gn_part = reinterpret_cast<double2*>(16);  // placeholder: the shape check only
       sk.gn_G = Gv;
       maybe_split(sk);  // split-K is shape-determined; its reduction emits the statistics
+      split_for(sk);    // the kernel add_conv will launch (Winograd or direct: their statistics rules differ)
       if (!conv_can_emit_gn(sk)) continue;
       c.gn_part = gn_buf_for(v, Gv);
       c.gn_G = Gv;

@@ -15,6 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 lib_path = os.environ.get('DM_HIP_LIB') or os.path.join(_HERE, 'libdm_hip.so')
 _HEADER = os.path.join(os.path.dirname(os.path.dirname(_HERE)), 'include', 'dm_hip.h')
 
+ABI_VERSION = 2   # include/dm_hip.h DM_ABI_VERSION
 DM_OK = 0
 DM_ERR_ARG = -1
 DM_ERR_HIP = -2
@@ -302,8 +303,8 @@ def load() -> ctypes.CDLL:
                 f'`python -c "import __graft_entry__ as g; g.build()"` (no CPU fallback exists)')
         L = ctypes.CDLL(lib_path)
         _declare(L)
-        if L.dm_abi_version() != 1:
-            raise DMError(f'dm_hip ABI mismatch: library reports {L.dm_abi_version()}, binding expects 1')
+        if L.dm_abi_version() != ABI_VERSION:
+            raise DMError(f'dm_hip ABI mismatch: library reports {L.dm_abi_version()}, binding expects {ABI_VERSION}')
         _lib = L
     return _lib
 

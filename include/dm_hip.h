@@ -33,7 +33,9 @@
 extern "C" {
 #endif
 
-#define DM_ABI_VERSION 1
+/* ABI history: 1 (rounds 1-4); 2: dm_conv_desc gained w_wino / w_wino_fold at its end (a caller compiled against
+ * version 1 passes the shorter struct, so the library refuses a binding that expects another version) */
+#define DM_ABI_VERSION 2
 
 #define DM_OK 0
 #define DM_ERR_ARG (-1)

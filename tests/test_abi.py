@@ -14,7 +14,19 @@ def test_library_exports_every_header_symbol():
     assert len(names) >= 15
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing, missing
-    assert L.dm_abi_version() == 1
+    assert L.dm_abi_version() == 2  # (include/dm_hip.h DM_ABI_VERSION: dm_conv_desc grew in version 2)
+
+
+def test_abi_version_matches_header_and_conv_desc_layout():
+    """DM_ABI_VERSION in the header, the binding's expectation and the library agree, and the ctypes dm_conv_desc
+    ends with the fields version 2 added (a version-1 caller's shorter struct must be refused)."""
+    import re
+    from dmhip import _lib
+    hdr = open(_lib._HEADER).read()
+    v = int(re.search(r'#define DM_ABI_VERSION (\d+)', hdr).group(1))
+    assert v == _lib.ABI_VERSION == dmhip.load().dm_abi_version() == 2
+    fields = [f[0] for f in dmhip.ConvDesc._fields_]
+    assert fields[-2:] == ['w_wino', 'w_wino_fold'], fields
 
 
 def _arch(dim=128, mults=(1, 2, 2, 2), attn=(0, 1, 0, 0), nres=2, heads=1, cin=3, cout=3):
