@@ -48,6 +48,16 @@ __device__ __forceinline__ void conv_store_attn_planes(const ConvArgs& a, int m,
 }
 
 
+// T2D tiles (conv_k32.hip, conv_wino.hip on wide maps): GEMM row m -> pixel row of the NHWC tensor (image m / HWo,
+// tile (m % HWo) / (TH TW) in row-major tile order, row-major inside the tile)
+__device__ __forceinline__ size_t t2d_pixel(int m, int HWo, int Wo, int TH, int TW) {
+  const int bb = m / HWo, rr = m - bb * HWo, tsz = TH * TW;
+  const int tl = rr / tsz, r = rr - tl * tsz, ntx = Wo / TW;
+  const int ty = tl / ntx, tx = tl - ty * ntx;
+  const int iy = r / TW;
+  return ((size_t)bb * HWo + (size_t)(ty * TH + iy) * Wo) + tx * TW + (r - iy * TW);
+}
+
 // LDS-staged epilogue (conv_k32.hip, the fused attention's proj): a wave's tile of acc * rowscale is put
 // in LDS as 32-row slabs [32][WN + 4] fp32 by the kernel (in whatever MFMA layout it has), then each
 // lane takes 4 consecutive output columns of a row (WN / 4 lanes per row), adds bias, per-image row

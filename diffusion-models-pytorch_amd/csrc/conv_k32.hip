@@ -68,16 +68,6 @@ __device__ unsigned long long g_k32_stamps[65536][8];
 #define K32_RSTAMP(k) do {} while (0)
 #endif
 
-// T2D tiles: GEMM row m -> pixel row of the NHWC tensor (image m / HWo, tile (m % HWo) / (TH TW) in row-major
-// tile order, row-major inside the tile)
-__device__ __forceinline__ size_t t2d_pixel(int m, int HWo, int Wo, int TH, int TW) {
-  const int bb = m / HWo, rr = m - bb * HWo, tsz = TH * TW;
-  const int tl = rr / tsz, r = rr - tl * tsz, ntx = Wo / TW;
-  const int ty = tl / ntx, tx = tl - ty * ntx;
-  const int iy = r / TW;
-  return ((size_t)bb * HWo + (size_t)(ty * TH + iy) * Wo) + tx * TW + (r - iy * TW);
-}
-
 // KSPLIT: split-K over 32-channel chunks for maps of <= 16 pixels (64-row tiles of 4 images): raw partial
 // sums to kpart [ksplit][M][Cout], the epilogue in conv_splitk_reduce (conv_patch.hip), as conv_patch3.
 // SUB: the sub-pixel form of nearest-2x + 3x3 (models/modules.py:60-63; conv_patch3 MODE 2): per output

@@ -131,9 +131,13 @@ __device__ __forceinline__ float dpp_f(float v, int ctrl_shr) {
                                             : __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x101, 0xF, 0xF, true));
 }
 
-// PROM: input prologue -- 0 none, 1 GroupNorm affine, 2 GroupNorm affine + SiLU; SC: a shortcut segment (Cin2 > 0)
-template <int W, int PROM, bool SC>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) conv_wino_kernel(ConvArgs a) {
+// PROM: input prologue -- 0 none, 1 GroupNorm affine, 2 GroupNorm affine + SiLU; SC: a shortcut segment (Cin2 > 0);
+// WIDE: 2-D tiles of 4 rows x 32 columns of a map wider than 32 (ADM's 64^2 .. 256^2; W 32), the GEMM row index
+// enumerating pixels tile by tile as conv_k32's T2D tiles (t2d_pixel), with the halo columns (the pixels left and
+// right of the tile, GroupNorm + SiLU'd) from a small LDS edge buffer
+template <int W, int PROM, bool SC, bool WIDE>
+__device__ __forceinline__ void conv_wino_body(const ConvArgs& a) {
+  static_assert(!WIDE || W == 32, "wide maps: 32-column tiles");
   constexpr bool PRO = PROM != 0;
   // a 128-pixel tile: 128 / W whole rows of one image (W 32, 16) or two whole 8 x 8 images (W 8); per image RIMG
   // output rows and PRI = RIMG + 2 patch rows (the halo)
@@ -153,9 +157,13 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   __shared__ float gstat[IMGS * 2 * kWMaxG];
   __shared__ double gxr[8 * 16 * 2];
   __shared__ __attribute__((aligned(16))) float gzero[8];  // the padding rows' table: 0 scale, 0 shift
+  // WIDE: the halo columns of two chunks, [chunk & 1][patch row][left, right][32 channels] fp32, GroupNorm + SiLU'd
+  __shared__ __attribute__((aligned(16))) float wedge[WIDE ? 2 * 6 * 2 * kWC : 4];
   _Float16* patch = reinterpret_cast<_Float16*>(smem);
 
-  const int HW = a.Hout * W;
+  const int Wimg = WIDE ? a.Wout : W;  // the map's width (WIDE: a multiple of 32 tiles)
+  const int ntx = Wimg / W;            // tile columns (1 unless WIDE)
+  const int HW = a.Hout * Wimg;
   const int M = a.B * HW, N = a.Cout;
   const int nN = N / 128;
   // persistent blocks over the tiles of ONE image (two for 8 x 8 maps; their GroupNorm tables built once): grid =
@@ -192,6 +200,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   // the lane's offset in a patch row group (pair row lpr NP + lj: its swizzle bit depends on the lane only -- lpr NP
   // is a multiple of 8, or at W 8 of 4 with lpr's parity the lane's half-wave)
   const int ldst = lj * kWRowH + 8 * ((loff >> 3) ^ wswz(NP == 4 ? 4 * (lane >> 5) + lj : lj)) + (loff & 4);
+  const float emL = lj == 0 ? 1.f : 0.f, emR = lj == NP - 1 ? 1.f : 0.f;  // (WIDE: the tile's edge lanes)
   const int Kp = NTAP * a.Cin1 + (SC ? a.Cin2 / 2 : 0);  // K of each U matrix (their stride in the image)
   const int ngrp = ceil_div(N, 32);
   const size_t sl = (size_t)ngrp * 1024;  // fp16 per 16-deep slice of the U images
@@ -212,16 +221,20 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   // the set's pixel 2 lj (pixel 2 lj + 1 one pitch on; padding rows: the zero page, which covers a pitch and a row)
   const float* pp[2] = {nullptr, nullptr};
   int wcol = 0;  // bytes: the wave's nu plane and 32-column group of the tile (uniform)
+  int ty = 0, tx = 0;  // the tile's row / column among the image's tiles
   auto set_tile = [&](int tile) DM_WINO_INL {
     const int mt = tile / nN, nt = tile - mt * nN;
     m0 = b0 * HW + mt * 128;
     n0 = nt * 128;
+    ty = WIDE ? mt / ntx : mt;
+    tx = WIDE ? mt - ty * ntx : 0;
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int ti = IMGS == 1 ? 0 : lpr[k] / PRI, bi = b0 + ti;
-      const int iy = mt * RIMG - 1 + lpr[k] - ti * PRI;
+      const int iy = ty * RIMG - 1 + lpr[k] - ti * PRI;
       rok[k] = iy >= 0 && iy < a.Hin && bi < a.B;  // (a group's second image past B: padding throughout)
-      pp[k] = rok[k] ? a.x1 + ((size_t)(bi * a.Hin + iy) * W + 2 * lj) * a.x1_pitch + loff : kZeroPage + loff;
+      pp[k] = rok[k] ? a.x1 + ((size_t)(bi * a.Hin + iy) * Wimg + tx * W + 2 * lj) * a.x1_pitch + loff
+                     : kZeroPage + loff;
     }
     // column n0 + ch 64 + 16 j + l16 (n0 % 128 == 0): 32-column group (n0 + ch 64) / 32 + j / 2, column
     // 16 (j & 1) + l16 of it -- one base pointer, compile-time offsets per j
@@ -264,6 +277,14 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     // V0 = x[2j - 1] - x[2j + 1] (lane j - 1's second pixel: DPP row_shr), V3 = x[2j] - x[2j + 2] (lane j + 1's first
     // pixel: row_shl), the shifted operand zero outside the 16-lane row (bound_ctrl) -- the map's padding columns
     dpp_sub4(e0, e1, vv[0], vv[3]);
+    if (WIDE) {  // the tile's halo columns (zero at the map's edges): lane 0's x[-1], lane 15's x[32]
+      const f4 h = *reinterpret_cast<const f4*>(wedge + ((c & 1) * 6 + lpr[k]) * 2 * kWC + (lj == 15 ? kWC : 0) + loff);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        vv[0][k] = __builtin_fmaf(emL, h[k], vv[0][k]);   // (-x[1]) + x[-1]: one rounding, as the subtraction
+        vv[3][k] = __builtin_fmaf(-emR, h[k], vv[3][k]);  // x[30] - x[32]
+      }
+    }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       if (NP < 16) {  // two units per DPP row: their boundary is a map edge too
@@ -290,6 +311,41 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   auto finish = [&](int c, int buf) DM_WINO_INL {
     finish_set(c, buf, 0);
     if (has2) finish_set(c, buf, 1);
+  };
+
+  // ---- WIDE: the halo columns. Edge unit u = 64 ew + lane of the waves ew = 0, 1 (early role, one set each, so
+  // rw[2] / rw[3] are theirs to use): patch row u / 16, side u & 1, channel quad (u / 2) & 7 -- 6 x 2 x 8 = 96
+  // units per chunk. Chunk c's edges are finished a chunk before chunk c itself (its slot c & 1 published by the
+  // barrier between), the raw pixels loaded a chunk before that.
+  const int eu = wave_u * 64 + lane;
+  const bool ew = WIDE && wave_u < 2;  // an edge wave
+  const float* epx = kZeroPage;  // the edge unit's pixel (chunk 0), the zero page outside the map
+  int etab = -1;                 // its GroupNorm table offset (-1: padding)
+  auto set_edges = [&]() DM_WINO_INL {
+    if (!ew) return;
+    const int pr = eu >> 4, side = eu & 1, cq = (eu >> 1) & 7;
+    const int iy = ty * RIMG - 1 + pr, ix = side ? tx * W + W : tx * W - 1;
+    const bool ok = eu < 96 && iy >= 0 && iy < a.Hin && ix >= 0 && ix < Wimg;
+    epx = ok ? a.x1 + ((size_t)(b0 * a.Hin + iy) * Wimg + ix) * a.x1_pitch + 4 * cq : kZeroPage;
+    etab = ok ? 8 * cq : -1;
+  };
+  auto load_edge = [&](int c, f4& r) DM_WINO_INL {
+    if (ew) r = *reinterpret_cast<const f4*>(epx + (etab >= 0 ? c * kWC : 0));
+  };
+  auto finish_edge = [&](int c, const f4& r) DM_WINO_INL {  // chunk c's edges into slot c & 1
+    if (!ew || eu >= 96) return;
+    f4 v = r;  // (PROM 0: the raw pixels; the zero page outside the map)
+    if (PROM) {
+      const float* ts = etab >= 0 ? gtab + 2 * c * kWC + etab : gzero;
+      const f4 sc = *reinterpret_cast<const f4*>(ts), sh = *reinterpret_cast<const f4*>(ts + 4);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float z = __builtin_fmaf(r[k], sc[k], sh[k]);
+        v[k] = PROM == 2 ? z * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(z)) : z;  // (finish_set's)
+      }
+    }
+    const int pr = eu >> 4, side = eu & 1, cq = (eu >> 1) & 7;
+    *reinterpret_cast<f4*>(wedge + ((c & 1) * 6 + pr) * 2 * kWC + side * kWC + 4 * cq) = v;
   };
 
   // ---- B: the fp16x2 fragment images of U_nu (split_conv_weights, nmat 4, ntap 3), 16-column halves
@@ -355,7 +411,8 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   const int sp = t >> 3, sks = t & 7;
   auto load_sc = [&](int st) DM_WINO_INL {
     // (rows past M -- a W 8 group's missing second image -- read the last pair: their outputs are not stored)
-    const float* xs = a.x2 + (size_t)min(m0 + 2 * sp, M - 2) * a.x2_pitch + st * kWC + 4 * sks;
+    const int srow = min(m0 + 2 * sp, M - 2);  // (WIDE: the pair's first pixel of the tiled map; pairs stay in a row)
+    const float* xs = a.x2 + (WIDE ? t2d_pixel(srow, HW, Wimg, RIMG, W) : (size_t)srow) * a.x2_pitch + st * kWC + 4 * sks;
     rw[0] = *reinterpret_cast<const f4*>(xs);
     rw[1] = *reinterpret_cast<const f4*>(xs + a.x2_pitch);
     rw[2] = *reinterpret_cast<const f4*>(xs + a.Cin2 / 2);
@@ -447,11 +504,22 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   // loop head's memory-counter waits, merged over the prologue and the loop's own back edge, then stay partial.
   int tile = t_first;
   set_tile(tile);
+  if (WIDE) set_edges();
 #pragma unroll
   for (int d = 0; d < WD - 1; ++d) load_b(bq[d], d);
   load_raw(0);
+  if (WIDE) {
+    load_edge(0, rw[2]);
+    if (nch > 1) load_edge(1, rw[3]);
+  }
   build_table();
   __syncthreads();
+  if (WIDE) {  // chunks 0 and 1's halo columns (one barrier more, once per block)
+    finish_edge(0, rw[2]);
+    if (nch > 1) finish_edge(1, rw[3]);
+    __syncthreads();
+    if (nch > 2) load_edge(2, rw[2]);
+  }
   finish(0, 0);
   load_stage(min(1, nst_g - 1));
   load_b(bq[WD - 1], WD - 1);
@@ -496,6 +564,10 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     if (!LATE) {
       if (more) finish(c + 1, (c + 1) & 1);
       if (more2) load_raw(c + 2);
+      if (WIDE && more2) {  // (the edge waves) chunk c + 2's halo columns into slot c & 1, chunk c + 3's pixels
+        finish_edge(c + 2, rw[2]);
+        if (c + 3 < nch) load_edge(c + 3, rw[2]);
+      }
       W_PH(1);
     }
     if (LATE) __builtin_amdgcn_s_setprio(1);  // the late role's MFMAs at priority 1 (its finish back at 0)
@@ -640,6 +712,11 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     if (has_next) {
       set_tile(next);
       load_raw(0);
+      if (WIDE) {
+        set_edges();
+        load_edge(0, rw[2]);
+        if (nch > 1) load_edge(1, rw[3]);
+      }
 #pragma unroll
       for (int d = 0; d < WD - 1; ++d) load_b(bq[d], d);
     }
@@ -651,6 +728,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
       const int kq = wave >> 2, hf = (wave >> 1) & 1, cj = wave & 1;
       typedef StagedEpilogue<64> Epi;
       Epi epi(a, M, HW, cb0, IMGS == 1, cn0 + cj * 64, lane);
+      if (WIDE) epi.t2d(Wimg, RIMG, W);  // (tile rows -> pixels; GroupNorm chunks = tile halves)
       const int px0 = 64 * kq + 32 * hf;
       const float* Ec = E + cj * 64 * kWEP + 4 * epi.c4;
       f4 fin = {0.f, 0.f, 0.f, 0.f};  // inf / NaN in any m (an operand past fp16's range) makes fin non-finite
@@ -688,7 +766,12 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     // ---- the next tile's prologue: its first chunk (the E planes are dead after this barrier; same image: same
     // GroupNorm tables, which sit outside the E planes)
     tile = next;
+    if (WIDE) {  // the next tile's chunks 0 and 1 halo columns (the edge buffer lies outside the E planes)
+      finish_edge(0, rw[2]);
+      if (nch > 1) finish_edge(1, rw[3]);
+    }
     __syncthreads();
+    if (WIDE && nch > 2) load_edge(2, rw[2]);
     finish(0, 0);
     load_stage(min(1, nst_g - 1));
     load_b(bq[WD - 1], WD - 1);
@@ -712,6 +795,16 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
 #endif
   W_STAMP(3);
   W_RSTAMP(6);
+}
+
+template <int W, int PROM, bool SC>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) conv_wino_kernel(ConvArgs a) {
+  conv_wino_body<W, PROM, SC, false>(a);
+}
+// 2-D tiles of maps wider than 32 columns (4 x 32-pixel tiles, halo columns from neighbouring tiles)
+template <int PROM, bool SC>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) conv_wino_wide_kernel(ConvArgs a) {
+  conv_wino_body<32, PROM, SC, true>(a);
 }
 
 // U = G g per (nu, output channel, chunk, tap row, channel of the chunk) from the packed 3x3 weights [Cout][K]
@@ -760,9 +853,13 @@ extern "C" int dm_debug_wino_stamps(void* host, int nblocks) {
 bool conv_wino_shape_ok(const ConvArgs& a) {
   if (!(a.taps == 9 && a.stride == 1 && a.upsample == 0 && a.ksplit <= 1)) return false;
   if (a.Hin != a.Hout || a.Win != a.Wout) return false;
-  // 32- or 16-wide maps in whole-row 128-pixel tiles; 8 x 8 maps two images per tile
+  // 32- or 16-wide maps in whole-row 128-pixel tiles; 8 x 8 maps two images per tile; wider maps (a multiple of 32
+  // columns, of 4 rows) in 4 x 32 tiles
   const int imgs = a.Wout == 8 ? 2 : 1;
-  if (a.Wout == 8 ? a.Hout != 8 : ((a.Wout != 32 && a.Wout != 16) || (a.Hout * a.Wout) % 128 != 0)) return false;
+  const bool wide = a.Wout > 32;
+  if (wide ? (a.Wout % 32 != 0 || a.Hout % 4 != 0)
+           : a.Wout == 8 ? a.Hout != 8 : ((a.Wout != 32 && a.Wout != 16) || (a.Hout * a.Wout) % 128 != 0))
+    return false;
   if (a.Cin1 < kWC || a.Cin1 % kWC != 0 || 2 * imgs * a.Cin1 > kWTab || a.Cin2 % (2 * kWC) != 0 ||
       a.K != 9 * a.Cin1 + a.Cin2)
     return false;
@@ -805,6 +902,7 @@ int wino_weights(const float* w, int Cout, int Cin1, int Cin2, int fold, void* o
 
 std::string conv_wino_label(const ConvArgs& a) {
   const int prom = (a.pro_scale || a.gin_part) ? (a.pro_nosilu ? 1 : 2) : 0;
+  if (a.Wout > 32) return std::string("conv_wino_wide_kernel<") + std::to_string(prom) + (a.Cin2 ? ",true>" : ",false>");
   return std::string("conv_wino_kernel<") + std::to_string(a.Wout) + "," + std::to_string(prom) + (a.Cin2 ? ",true>" : ",false>");
 }
 
@@ -839,6 +937,14 @@ int conv2d_wino(const ConvArgs& a, hipStream_t st) {
   DM_WINO_LAUNCH(16, 0) DM_WINO_LAUNCH(16, 1) DM_WINO_LAUNCH(16, 2)
   DM_WINO_LAUNCH(8, 0) DM_WINO_LAUNCH(8, 1) DM_WINO_LAUNCH(8, 2)
 #undef DM_WINO_LAUNCH
+#define DM_WINO_WIDE(P_)                                                                                     \
+  if (a.Wout > 32 && prom == P_) {                                                                          \
+    if (a.Cin2) hipLaunchKernelGGL((conv_wino_wide_kernel<P_, true>), dim3(blocks), dim3(512), 0, st, a);       \
+    else hipLaunchKernelGGL((conv_wino_wide_kernel<P_, false>), dim3(blocks), dim3(512), 0, st, a);             \
+    note_launch(a.Cin2 ? "conv_wino_wide_kernel<" #P_ ",true>" : "conv_wino_wide_kernel<" #P_ ",false>");         \
+  }
+  DM_WINO_WIDE(0) DM_WINO_WIDE(1) DM_WINO_WIDE(2)
+#undef DM_WINO_WIDE
   DM_LAUNCH_CHECK();
   return DM_OK;
 }

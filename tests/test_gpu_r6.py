@@ -1,0 +1,168 @@
+"""Round-6 GPU tests: the Winograd F(2,3) conv on maps wider than 32 columns (conv_wino_wide_kernel: 4 x 32-pixel
+2-D tiles, the GEMM row index enumerating pixels tile by tile, the halo columns from the neighbouring tiles through
+an LDS edge buffer; ADM's 64^2 .. 256^2 ResBlock convs, models/adm/unet.py:162-275).
+
+* integer operands bit for bit against float64: zero padding only at the map's edges, the tile seams carry the real
+  neighbours (every tile column and row position, single-row-of-tiles maps, several tiles per image row);
+* the GroupNorm-affine prologue, temb row vector, residual, pitched tensors, the ResBlock shortcut segment;
+* random operands with GroupNorm + SiLU at fp32-class accuracy against float64;
+* whole ADM forwards against the direct conv (DM_CONV_WINO=0) and the reference fixture live in test_gpu_r5 / r4 /
+  adm (they now take the wide kernel for their 64^2+ convs; the launch log below proves it).
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+import dmhip
+from tests.test_gpu_ops import _ints, _nhwc, _pack, _run_conv
+
+pytestmark = pytest.mark.gpu
+
+WINO = 21  # ConvDesc.tile: force the Winograd kernel
+
+WIDE_SHAPES = [(1, 64, 128, 8, 64), (2, 32, 128, 12, 96), (1, 96, 256, 16, 128), (3, 64, 128, 4, 64),
+               (1, 160, 128, 8, 256)]
+
+
+def _conv_logged(cuda, *args, **kw):
+    dmhip.launch_log(True)
+    y = _run_conv(cuda, *args, **kw)
+    log = dmhip.launch_log_read()
+    dmhip.launch_log(False)
+    return y, log
+
+
+@pytest.mark.parametrize('B,Cin,Cout,H,W', WIDE_SHAPES)
+@pytest.mark.parametrize('pro', [False, True])
+def test_wino_wide_exact(cuda, B, Cin, Cout, H, W, pro):
+    """Integer operands (and integer GroupNorm-affine tables, no SiLU): V, U, their fp16 pieces and the fp32 sums are
+    exact, so the wide-map Winograd conv equals the float64 conv bit for bit -- the halo columns at every tile seam
+    included, zero padding at the map's edges only."""
+    x = _ints((B, Cin, H, W), -2, 3, seed=150)
+    w = _ints((Cout, Cin, 3, 3), -2, 3, seed=151)
+    b = _ints((Cout, ), seed=152)
+    xin, prot = x, None
+    if pro:
+        xin = x * 2 - 1
+        prot = (torch.full((B, Cin), 2.0, device=cuda), torch.full((B, Cin), -1.0, device=cuda))
+    ref = F.conv2d(xin.double(), w.double(), b.double(), padding=1).float()
+    y, log = _conv_logged(cuda, _nhwc(x).to(cuda), _pack(w, cuda), Cout, H, W, 9, 1, 0, b.to(cuda), tile=WINO,
+                          split='fp16x2', wino=True, pro=prot, pro_nosilu=1 if pro else 0)
+    assert log == [f'conv_wino_wide_kernel<{1 if pro else 0},false>'], log
+    assert torch.equal(y.cpu(), _nhwc(ref))
+
+
+@pytest.mark.parametrize('H,W', [(8, 64), (4, 96)])
+def test_wino_wide_rowvec_residual_pitch(cuda, H, W):
+    """temb row vector, residual, pitched input and output (untouched beyond Cout), integer-exact."""
+    B, Cin, Cout = 3, 64, 128
+    x = _ints((B, Cin, H, W), seed=160)
+    w = _ints((Cout, Cin, 3, 3), -2, 3, seed=161)
+    b = _ints((Cout, ), seed=162)
+    rv = _ints((B, Cout), seed=163)
+    res = _ints((B, Cout, H, W), seed=164)
+    ref = (F.conv2d(x.double(), w.double(), b.double(), padding=1) + rv.double()[:, :, None, None]
+           + res.double()).float()
+    xp = torch.full((B, H, W, 96), float('nan'), device=cuda)
+    xp[..., :Cin] = _nhwc(x).to(cuda)
+    y = _run_conv(cuda, xp[..., :Cin], _pack(w, cuda), Cout, H, W, 9, bias=b.to(cuda), rowvec=rv.to(cuda),
+                  res=_nhwc(res).to(cuda), y_pitch=160, x_pitch=96, tile=WINO, split='fp16x2', wino=True)
+    assert torch.equal(y[..., :Cout].cpu(), _nhwc(ref))
+    assert torch.isnan(y[..., Cout:]).all()
+
+
+@pytest.mark.parametrize('C1,C2,H,W,Cout,pro', [(64, 64, 8, 64, 128, False), (128, 256, 4, 128, 256, True),
+                                                (32, 128, 12, 96, 128, False)])
+def test_wino_wide_shortcut_exact(cuda, C1, C2, H, W, Cout, pro):
+    """ResBlock conv2 with the 1x1 shortcut of x as a second K segment on the 2-D tiles (the shortcut rows mapped
+    tile by tile), temb row vector, residual: integer-exact."""
+    B = 2
+    h = _ints((B, C1, H, W), seed=170)
+    x = _ints((B, C2, H, W), seed=171)
+    w2 = _ints((Cout, C1, 3, 3), -2, 3, seed=172)
+    ws = _ints((Cout, C2, 1, 1), seed=173)
+    b = _ints((Cout, ), seed=174)
+    rv = _ints((B, Cout), seed=175)
+    res = _ints((B, Cout, H, W), seed=176)
+    K = 9 * C1 + C2
+    wp = torch.zeros((Cout, K), device=cuda)
+    _pack(w2, cuda, K, 0, wp)
+    _pack(ws, cuda, K, 9 * C1, wp)
+    hin, prot = h, None
+    if pro:
+        hin = h * 2 - 1
+        prot = (torch.full((B, C1), 2.0, device=cuda), torch.full((B, C1), -1.0, device=cuda))
+    ref = (F.conv2d(hin.double(), w2.double(), b.double(), padding=1) + rv.double()[:, :, None, None]
+           + F.conv2d(x.double(), ws.double()) + res.double()).float()
+    y, log = _conv_logged(cuda, _nhwc(h).to(cuda), wp, Cout, H, W, 9, bias=b.to(cuda), rowvec=rv.to(cuda),
+                          res=_nhwc(res).to(cuda), x2=_nhwc(x).to(cuda), Cin2=C2, tile=WINO, split='fp16x2',
+                          wino=True, pro=prot, pro_nosilu=1 if pro else 0)
+    assert log == [f'conv_wino_wide_kernel<{1 if pro else 0},true>'], log
+    assert torch.equal(y.cpu(), _nhwc(ref))
+
+
+@pytest.mark.parametrize('B,Cin,Cout,H,W', [(2, 128, 128, 16, 64), (1, 256, 256, 8, 128), (1, 64, 128, 32, 256)])
+def test_wino_wide_fp32_accuracy(cuda, report, B, Cin, Cout, H, W):
+    """GroupNorm + SiLU prologue on random data: the wide-map Winograd conv's error vs float64 is at most that of the
+    direct fp16x2 2-D-tile conv it replaces (conv_k32 T2D, tile 19; max and rms) -- the fp32 MFMA kernels take no fused
+    prologue on wide maps; on the whole-row tiles the Winograd error is 0.28-0.47x the fp32 kernel's
+    (test_gpu_r5.test_wino_fp32_accuracy)."""
+    g = torch.Generator().manual_seed(180 + W)
+    x = torch.randn((B, Cin, H, W), generator=g) * 2 + 0.3
+    gamma, beta = torch.randn(Cin, generator=g), torch.randn(Cin, generator=g)
+    w = torch.randn((Cout, Cin, 3, 3), generator=g) * (1.0 / (9 * Cin) ** 0.5)
+    b = torch.randn(Cout, generator=g) * 0.01
+    a = F.silu(F.group_norm(x.double(), 32, gamma.double(), beta.double(), 1e-5))
+    ref = _nhwc(F.conv2d(a, w.double(), b.double(), padding=1))
+    xd = _nhwc(x).to(cuda)
+    pro = dmhip.groupnorm_affine(xd, B, H * W, Cin, 32, 1e-5, gamma.to(cuda), beta.to(cuda))
+    wp = _pack(w, cuda)
+    errs, rms = {}, {}
+    for name, split, tile, wino in (('k32', 'fp16x2', 19, False), ('wino', 'fp16x2', WINO, True)):
+        y = _run_conv(cuda, xd, wp, Cout, H, W, 9, 1, 0, b.to(cuda), pro=pro, split=split, tile=tile, wino=wino)
+        d = y.cpu().double() - ref
+        errs[name] = d.abs().max().item()
+        rms[name] = d.pow(2).mean().sqrt().item()
+    scale = ref.abs().max().item()
+    for k in errs:
+        report(f'wino_wide_accuracy_{B}_{Cin}_{Cout}_{H}x{W}_{k}_max_rel', errs[k] / scale)
+        report(f'wino_wide_accuracy_{B}_{Cin}_{Cout}_{H}x{W}_{k}_rms_rel', rms[k] / scale)
+    assert errs['wino'] <= errs['k32'], errs
+    assert rms['wino'] <= rms['k32'], rms
+    assert errs['wino'] < 4e-6 * scale, (errs, scale)
+
+
+def test_adm256_wide_wino_forward(cuda, golden, report, monkeypatch):
+    """The RePaint CelebA-HQ ADM-256 (reference fixture config, B = 1): its 64^2 .. 256^2 ResBlock convs on the wide-map
+    Winograd kernel (the launch log shows it, with GroupNorm partials from its epilogue over the tile halves) within
+    1e-5 of the direct 2-D-tile convs (DM_CONV_WINO=0) and within TOL of the reference."""
+    from models.adm.unet import UNetModel
+    from tests.test_gpu_parity import TOL
+    from utils.synthetic import init_synthetic_
+    g, meta = golden('adm')
+    name = 'adm256_celebahq'
+    x = torch.from_numpy(g[f'{name}_x']).to(cuda)
+    t = torch.from_numpy(g[f'{name}_t']).to(cuda)
+    y = torch.from_numpy(g[f'{name}_labels']).to(cuda) if f'{name}_labels' in g else None
+    outs, logs = {}, {}
+    for mode in ('wino', 'direct'):
+        if mode == 'direct':
+            monkeypatch.setenv('DM_CONV_WINO', '0')
+        model = UNetModel(**meta['archs'][name]).eval()
+        init_synthetic_(model)
+        model = model.to(cuda)
+        dmhip.launch_log(True)
+        outs[mode] = model(x, t, y).cpu()
+        logs[mode] = dmhip.launch_log_read()
+        dmhip.launch_log(False)
+        del model
+        torch.cuda.empty_cache()
+    monkeypatch.delenv('DM_CONV_WINO')
+    assert any(lb.startswith('conv_wino_wide_kernel<2,') for lb in logs['wino']), sorted(set(logs['wino']))
+    assert not any('conv_wino' in lb for lb in logs['direct'])
+    err = (outs['wino'] - outs['direct']).abs().max().item()
+    ref_err = (outs['wino'] - torch.from_numpy(g[f'{name}_out'])).abs().max().item()
+    report('adm256_wide_wino_maxabs_vs_direct', err)
+    report('adm256_wide_wino_maxabs_vs_reference', ref_err)
+    assert err <= 1e-5, err
+    assert ref_err <= TOL, ref_err
