@@ -213,9 +213,10 @@ def roofline(prof, workload='c3', build=None, launches_per_forward=None):
         np_ = int(dom_name.rstrip('>').split(',')[-1]) if split else 0
         if dom_name.startswith('gemm_kernel') and dom_name.endswith(',true>'):   # <..., B_KN, SPLIT>: fp16x2
             split, np_ = True, 2
-        if dom_name.startswith(('conv_k32_kernel', 'conv_k32s_kernel', 'linear_k32_kernel', 'conv_wino_kernel')):
+        if dom_name.startswith(('conv_k32_kernel', 'conv_k32s_kernel', 'linear_k32_kernel', 'conv_wino_kernel',
+                                 'conv_wino_wide_kernel')):
             split, np_ = True, 2   # fp16x2 only
-        wino = dom_name.startswith('conv_wino_kernel')
+        wino = dom_name.startswith(('conv_wino_kernel', 'conv_wino_wide_kernel'))
         prods = SPLIT_PRODUCTS.get(np_, 0)
         # FLOPs are the direct convolution's (2 M N K) for every conv kernel; the Winograd kernel issues WINO_PRODUCTS
         # of its products, so its peak in those FLOPs is the issue peak / WINO_PRODUCTS

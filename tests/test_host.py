@@ -204,3 +204,7 @@ def test_bench_wino_roofline_priced_in_direct_flops():
     roof = bench.roofline(prof, 'c3', None, {'conv_wino_kernel<32,2,false>': 4.0})[0]
     assert roof['peak'] == round(2500.0 / 3 / (2 / 3), 1) and abs(roof['achieved'] - 500.0) < 1e-6
     assert roof['traffic'] is None and roof['launches_per_forward'] == 4.0 and 'direct-convolution' in roof['peak_basis']
+    # the wide-map form (C4's dominant family) is priced the same way
+    prof = [dict(label='conv_wino_wide_kernel<2,false>', flops=1e12, bytes=1e9, ms_total=2.0, launches=1)]
+    roof = bench.roofline(prof, 'c4', None, None)[0]
+    assert roof['peak'] == round(2500.0 / 3 / (2 / 3), 1) and 'direct-convolution' in roof['peak_basis']
