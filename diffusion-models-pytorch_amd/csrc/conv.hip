@@ -350,11 +350,13 @@ int conv_pick(const ConvArgs& a) {
 }
 
 bool conv_can_emit_gn(const ConvArgs& a) {
-  if ((a.tile == 0 || a.tile == 21) && conv_wino_ok(a))  // StagedEpilogue over 64-pixel chunks of one image
-    return a.gn_G > 0 && a.Cout % a.gn_G == 0 && (a.Cout / a.gn_G) % 4 == 0 && a.Cout / a.gn_G <= 32;
-  if (a.ksplit > 1)  // the split-K reduction emits them (conv_splitk_reduce_gn_kernel): one chunk per image
+  // the split-K reduction emits them (conv_splitk_reduce_gn_kernel; after the 4 x 4 Winograd kernel, conv_k32s's own
+  // in-block reduction): one chunk per image
+  if (a.ksplit > 1)
     return !a.upsample && a.Hout * a.Wout <= kGnPixPerChunk && a.gn_G > 0 && a.Cout % a.gn_G == 0 &&
            a.Cout <= 1024;
+  if ((a.tile == 0 || a.tile == 21) && conv_wino_ok(a))  // StagedEpilogue over 64-pixel chunks of one image
+    return a.gn_G > 0 && a.Cout % a.gn_G == 0 && (a.Cout / a.gn_G) % 4 == 0 && a.Cout / a.gn_G <= 32;
   // the K32 stride-2 tiles: a block's 64 rows are one 64-pixel chunk (two 32-row waves per column slice)
   if (a.stride == 2 && conv_k32_pick(a) == 9)
     return (a.Hout * a.Wout) % 64 == 0 && a.gn_G > 0 && a.Cout % a.gn_G == 0 && 32 % (a.Cout / a.gn_G) == 0;

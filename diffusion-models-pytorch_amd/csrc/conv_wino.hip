@@ -139,13 +139,17 @@ template <int W, int PROM, bool SC, bool WIDE>
 __device__ __forceinline__ void conv_wino_body(const ConvArgs& a) {
   static_assert(!WIDE || W == 32, "wide maps: 32-column tiles");
   constexpr bool PRO = PROM != 0;
-  // a 128-pixel tile: 128 / W whole rows of one image (W 32, 16) or two whole 8 x 8 images (W 8); per image RIMG
-  // output rows and PRI = RIMG + 2 patch rows (the halo)
-  constexpr int IMGS = W == 8 ? 2 : 1, RIMG = 128 / W / IMGS, PRI = RIMG + 2;
+  // a 128-pixel tile: 128 / W whole rows of one image (W 32, 16), two whole 8 x 8 images (W 8) or eight whole 4 x 4
+  // images (W 4); per image RIMG output rows and PRI = RIMG + 2 patch rows (the halo)
+  constexpr int IMGS = W == 8 ? 2 : W == 4 ? 8 : 1, RIMG = 128 / W / IMGS, PRI = RIMG + 2;
   constexpr int NP = W / 2, PR = IMGS * PRI, NR = PR * NP;
   static_assert(NR <= kWNR, "patch plane");
+  // KS (the 4 x 4 maps: 64 tiles at B = 256 for 256 CUs): split-K over the input channels -- block (split, ..) takes
+  // chunks and shortcut steps split * n / ksplit .. of the tile and stores its raw m-transformed partial sums to
+  // kpart[split], conv_splitk_reduce adds them in split order with the epilogue (and the GroupNorm statistics)
+  constexpr bool KS = W == 4;
   // loader units (patch row, 4-channel eighth of the chunk) of NP lanes, 64 / NP per wave instruction: NSET = 12
-  // (W 32) / 10 (W 16, W 8) full sets over the 8 waves -- set s = w and, for the first NSET - 8 waves of one role,
+  // (W 32, W 4) / 10 (W 16, W 8) full sets over the 8 waves -- set s = w and, for the first NSET - 8 waves of one role,
   // 8 + w'
   constexpr int NSET = PR * 8 * NP / 64;
   static_assert(NSET * 64 == PR * 8 * NP && NSET > 8 && NSET <= 16, "loader sets");
@@ -166,11 +170,15 @@ __device__ __forceinline__ void conv_wino_body(const ConvArgs& a) {
   const int HW = a.Hout * Wimg;
   const int M = a.B * HW, N = a.Cout;
   const int nN = N / 128;
-  // persistent blocks over the tiles of ONE image (two for 8 x 8 maps; their GroupNorm tables built once): grid =
-  // ceil(B / IMGS) x parts, block (images b0 .., part) takes tiles part * tpb .. + tpb - 1 of the group's
-  // (IMGS HW / 128) x nN, row tiles outer
-  const int parts = gridDim.x / ceil_div(a.B, IMGS);
-  const int g0 = blockIdx.x / parts, part = blockIdx.x - g0 * parts;
+  // persistent blocks over the tiles of ONE image (two for 8 x 8 maps, eight for 4 x 4; their GroupNorm tables built
+  // once): grid = [ksplit x] ceil(B / IMGS) x parts, block (images b0 .., part) takes tiles part * tpb .. + tpb - 1 of
+  // the group's (IMGS HW / 128) x nN, row tiles outer
+  const int nks = KS ? a.ksplit : 1;
+  const int gsz = KS ? (int)gridDim.x / nks : (int)gridDim.x;  // blocks per split
+  const int split = KS ? (int)blockIdx.x / gsz : 0;
+  const int bidl = KS ? (int)blockIdx.x - split * gsz : (int)blockIdx.x;
+  const int parts = gsz / ceil_div(a.B, IMGS);
+  const int g0 = bidl / parts, part = bidl - g0 * parts;
   const int b0 = g0 * IMGS;
   const int tpb = (IMGS * HW / 128) * nN / parts;
   const int t_first = part * tpb, t_end = t_first + tpb;
@@ -187,19 +195,29 @@ __device__ __forceinline__ void conv_wino_body(const ConvArgs& a) {
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   const int xw = wave_u - 4;
   const bool has2 = xw >= 0 && xw < NSET - 8;
+  // (W 4: unit = 2 lanes, a 16-lane row one patch row's 8 channel quads, set s patch rows 4 s .. 4 s + 3)
   const int loff = NP == 16 ? 16 * (wave_u & 1) + 4 * (lane >> 4)
                  : NP == 8  ? 4 * (lane >> 3)
-                            : 16 * ((lane >> 4) & 1) + 4 * ((lane >> 2) & 3);
+                 : NP == 4  ? 16 * ((lane >> 4) & 1) + 4 * ((lane >> 2) & 3)
+                            : 4 * ((lane >> 1) & 7);
+  // the input channels of this block: all, or (KS) chunks cb .. cb + nch - 1 and shortcut steps sb .. sb + ns - 1
+  const int NCH = a.Cin1 / kWC, NSC = SC ? a.Cin2 / (2 * kWC) : 0;  // chunks, shortcut steps of the conv
+  const int cb = KS ? split * NCH / nks : 0, sb = KS ? split * NSC / nks : 0;
+  const int nch = KS ? (split + 1) * NCH / nks - cb : NCH;
+  const int tabc = KS ? nch * kWC : a.Cin1;  // GroupNorm table channels per image (from channel cb kWC)
   int lpr[2], ltab[2];  // per set: patch row, the offset of its image's GroupNorm table
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const int s_ = k ? 8 + max(xw, 0) : wave_u;
-    lpr[k] = min(NP == 16 ? s_ >> 1 : NP == 8 ? s_ : 2 * s_ + (lane >> 5), PR - 1);
-    ltab[k] = IMGS == 1 ? 0 : (lpr[k] / PRI) * 2 * a.Cin1;
+    lpr[k] = min(NP == 16 ? s_ >> 1 : NP == 8 ? s_ : NP == 4 ? 2 * s_ + (lane >> 5) : 4 * s_ + (lane >> 4), PR - 1);
+    ltab[k] = IMGS == 1 ? 0 : (lpr[k] / PRI) * 2 * tabc;
   }
   // the lane's offset in a patch row group (pair row lpr NP + lj: its swizzle bit depends on the lane only -- lpr NP
-  // is a multiple of 8, or at W 8 of 4 with lpr's parity the lane's half-wave)
-  const int ldst = lj * kWRowH + 8 * ((loff >> 3) ^ wswz(NP == 4 ? 4 * (lane >> 5) + lj : lj)) + (loff & 4);
+  // is a multiple of 8, at W 8 of 4 with lpr's parity the lane's half-wave, at W 4 of 2 with bit 1 of lpr the lane's
+  // half-wave)
+  const int ldst = lj * kWRowH +
+                   8 * ((loff >> 3) ^ wswz(NP == 4 ? 4 * (lane >> 5) + lj : NP == 2 ? 2 * (lane >> 4) + lj : lj)) +
+                   (loff & 4);
   const float emL = lj == 0 ? 1.f : 0.f, emR = lj == NP - 1 ? 1.f : 0.f;  // (WIDE: the tile's edge lanes)
   const int Kp = NTAP * a.Cin1 + (SC ? a.Cin2 / 2 : 0);  // K of each U matrix (their stride in the image)
   const int ngrp = ceil_div(N, 32);
@@ -212,7 +230,6 @@ __device__ __forceinline__ void conv_wino_body(const ConvArgs& a) {
   const int vb_lane = ((q & 1) * 32 + l16) * 16;
   const int vb_main = vb_lane + (q >> 1) * NTAP * (int)sl * 2, vb_sc = vb_lane + (q >> 1) * (int)sl * 2;
   const int nu_u = wave_u >> 1, ch_u = wave_u & 1;
-  const int nch = a.Cin1 / kWC;
   const int kt_end = nch * NTAP;
 
   // ---- per-tile state: the tile's rows and columns, the loader's pixel pointers, the B base
@@ -245,7 +262,7 @@ __device__ __forceinline__ void conv_wino_body(const ConvArgs& a) {
   // MFMAs (the ping-pong below)
   f4 rw[4];  // set k: pixels 2 lj, 2 lj + 1 in rw[2 k], rw[2 k + 1]
   auto load_raw = [&](int c) DM_WINO_INL {
-    const int co = c * kWC;
+    const int co = (cb + c) * kWC;
     rw[0] = *reinterpret_cast<const f4*>(pp[0] + co);
     rw[1] = *reinterpret_cast<const f4*>(pp[0] + a.x1_pitch + co);
     if (has2) {
@@ -352,14 +369,16 @@ __device__ __forceinline__ void conv_wino_body(const ConvArgs& a) {
   // all K steps of a tile: the 3 nch tap rows (step kt = 3 c + dy: 16-slice 6 c + dy, + 3 for k-groups 2, 3), then
   // the ns shortcut steps (16-slices 6 nch + 2 s, + 1 for k-groups 2, 3); past the end: the last step again
   // (refills nothing uses)
-  const int ns = SC ? a.Cin2 / (2 * kWC) : 0, nst = kt_end + ns, nst_g = nch + ns;  // K steps, stages
+  const int ns = KS ? (split + 1) * NSC / nks - sb : NSC, nst = kt_end + ns, nst_g = nch + ns;  // K steps, stages
   f16x8 bq[WD][TN][2];
   auto load_b = [&](f16x8 (&dst)[TN][2], int kt) DM_WINO_INL {
     kt = __builtin_amdgcn_readfirstlane(min(kt, nst - 1));
     // branch-free (a uniform select of two VGPRs became a branch around every refill): the shortcut case only in
-    // the SC kernels, its voffset by a bit blend under an all-ones / all-zeros scalar mask
+    // the SC kernels, its voffset by a bit blend under an all-ones / all-zeros scalar mask (KS: the block's steps
+    // are the conv's main steps cb NTAP .. and shortcut steps sb ..)
     const int msc = SC ? -(int)(kt >= kt_end) : 0;
-    const int so = wcol + (((kt + (kt / NTAP) * NTAP) & ~msc) | ((2 * nch * NTAP + 2 * (kt - kt_end)) & msc)) * (int)sl * 2;
+    const int kg = kt + cb * NTAP;
+    const int so = wcol + (((kg + (kg / NTAP) * NTAP) & ~msc) | ((2 * NCH * NTAP + 2 * (kt - kt_end + sb)) & msc)) * (int)sl * 2;
     const int vo = SC ? (vb_main & ~msc) | (vb_sc & msc) : vb_main;
 #pragma unroll
     for (int j = 0; j < TN; ++j)
@@ -372,9 +391,19 @@ __device__ __forceinline__ void conv_wino_body(const ConvArgs& a) {
   f4 acc[TM][TN];
   // tap row dy: A fragment i = pair rows nu NR + 16 i + l16 + dy NP of buffer pbuf, the lane's k-group q (swizzled:
   // every fragment's first row is a multiple of 8 except the W 8 tap rows at 4 dy, where the swizzle bit flips)
-  const int abase = (nu * NR + l16) * kWRowH + 8 * (q ^ wswz(l16));
+  // (W 4: pair 16 i + l16 of the tile is pair l16 & 7 of image 2 i + l16 / 8, whose pair rows start 12 further on per
+  // image: the lane's row 12 (l16 / 8) + (l16 & 7) of fragment i's 24, and its swizzle bit differs per tap row)
+  const int lrow = NP == 2 ? 12 * (l16 >> 3) + (l16 & 7) : l16;
+  auto aoff = [&](int r) { return (nu * NR + r) * kWRowH + 8 * (q ^ wswz(r)); };
+  const int abase = aoff(lrow);
   const int abase_x = NP == 4 ? abase + 8 - 16 * ((q ^ wswz(l16)) & 1) : abase;  // (W 8, odd dy)
-  auto arow_base = [&](int dy) DM_WINO_INL { return ((dy * NP) & 4) ? abase_x : abase; };
+  const int abase_2 = NP == 2 ? aoff(lrow + 2) - 2 * kWRowH : abase;            // (W 4, dy 1)
+  const int abase_4 = NP == 2 ? aoff(lrow + 4) - 4 * kWRowH : abase;            // (W 4, dy 2)
+  auto arow_base = [&](int dy) DM_WINO_INL {
+    if (NP == 2) return dy == 0 ? abase : dy == 1 ? abase_2 : abase_4;
+    return ((dy * NP) & 4) ? abase_x : abase;
+  };
+  const int abase_sc = l16 * kWRowH + 8 * (q ^ wswz(l16));  // the shortcut steps' [nu][64] pair rows
   // a0: tile 0's fragment of this tap row on entry (read ahead); within a chunk, the next tap row's on exit
   f16x8 a0[2];
   auto read_a0 = [&](int dy, int pbuf) DM_WINO_INL {
@@ -382,8 +411,9 @@ __device__ __forceinline__ void conv_wino_body(const ConvArgs& a) {
     a0[0] = *reinterpret_cast<const f16x8*>(As);
     a0[1] = *reinterpret_cast<const f16x8*>(As + 32);
   };
-  // pair rows 16 i .. of the tile: image i / 2 of a W 8 tile sits 2 halo rows (2 NP pair rows) further down the patch
-  auto arow = [](int i) { return IMGS == 2 && i >= 2 ? 2 * NP : 0; };
+  // pair rows 16 i .. of the tile: image i / 2 of a W 8 tile sits 2 halo rows (2 NP pair rows) further down the patch;
+  // images 2 i, 2 i + 1 of a W 4 tile 2 x 2 halo rows per earlier image pair (8 i pair rows)
+  auto arow = [](int i) { return IMGS == 8 ? 8 * i : IMGS == 2 && i >= 2 ? 2 * NP : 0; };
   auto compute = [&](int dy, int pbuf, const f16x8 (&bv)[TN][2]) {
     const _Float16* As = patch + pbuf * kWBuf + arow_base(dy) + dy * NP * kWRowH;
     f16x8 av[TM][2];
@@ -412,7 +442,8 @@ __device__ __forceinline__ void conv_wino_body(const ConvArgs& a) {
   auto load_sc = [&](int st) DM_WINO_INL {
     // (rows past M -- a W 8 group's missing second image -- read the last pair: their outputs are not stored)
     const int srow = min(m0 + 2 * sp, M - 2);  // (WIDE: the pair's first pixel of the tiled map; pairs stay in a row)
-    const float* xs = a.x2 + (WIDE ? t2d_pixel(srow, HW, Wimg, RIMG, W) : (size_t)srow) * a.x2_pitch + st * kWC + 4 * sks;
+    const float* xs =
+        a.x2 + (WIDE ? t2d_pixel(srow, HW, Wimg, RIMG, W) : (size_t)srow) * a.x2_pitch + (sb + st) * kWC + 4 * sks;
     rw[0] = *reinterpret_cast<const f4*>(xs);
     rw[1] = *reinterpret_cast<const f4*>(xs + a.x2_pitch);
     rw[2] = *reinterpret_cast<const f4*>(xs + a.Cin2 / 2);
@@ -450,13 +481,13 @@ __device__ __forceinline__ void conv_wino_body(const ConvArgs& a) {
   // under SiLU); the caller's barrier publishes them
   auto build_table = [&]() DM_WINO_INL {
     if (!PRO) return;
-    const int C = a.Cin1;
+    const int C = tabc, c0 = cb * kWC;  // (KS: the block's channels c0 .. c0 + C - 1)
 #pragma unroll
     for (int im = 0; im < IMGS; ++im) {
-      const int bi = min(b0 + im, a.B - 1);  // (a group's second image past B: any table, its rows are padding)
+      const int bi = min(b0 + im, a.B - 1);  // (a group's image past B: any table, its rows are padding)
       float* tab = gtab + im * 2 * C;
       if (a.gin_part) {  // gn_finalize (gn.hip) for the image, its expressions (conv_k32's in-kernel finalize)
-        const int G = a.gin_G, cpg = C / G;
+        const int G = a.gin_G, cpg = a.Cin1 / G;  // (the conv's groups: C is the block's share under KS)
         float* st = gstat + im * 2 * kWMaxG;
         for (int i = t; i < G; i += 512) {
           double s1 = 0, s2 = 0;
@@ -474,12 +505,13 @@ __device__ __forceinline__ void conv_wino_body(const ConvArgs& a) {
         }
         __syncthreads();
         for (int c = t; c < C; c += 512) {
-          const int si = 2 * (c / cpg);
+          const int cg = c0 + c;
+          const int si = 2 * (cg / cpg);
           const float mu = st[si], rs = st[si + 1];
-          float sc = rs * (a.gin_gamma ? a.gin_gamma[c] : 1.0f);
-          float sh = -sc * mu + (a.gin_beta ? a.gin_beta[c] : 0.0f);
+          float sc = rs * (a.gin_gamma ? a.gin_gamma[cg] : 1.0f);
+          float sh = -sc * mu + (a.gin_beta ? a.gin_beta[cg] : 0.0f);
           if (a.gin_ms) {
-            const size_t mo = (size_t)bi * a.gin_mp + c;
+            const size_t mo = (size_t)bi * a.gin_mp + cg;
             const float f = 1.0f + a.gin_ms[mo];
             sc = sc * f;
             sh = sh * f + a.gin_mb[mo];
@@ -491,7 +523,8 @@ __device__ __forceinline__ void conv_wino_body(const ConvArgs& a) {
       } else {
         for (int c = t; c < C; c += 512) {
           const int ti = 2 * c - (c & 3);
-          const float sc = a.pro_scale[(size_t)bi * C + c], sh = a.pro_shift[(size_t)bi * C + c];
+          const size_t po = (size_t)bi * a.Cin1 + c0 + c;
+          const float sc = a.pro_scale[po], sh = a.pro_shift[po];
           tab[ti] = PROM == 2 ? sc * -1.4426950408889634f : sc;
           tab[ti + 4] = PROM == 2 ? sh * -1.4426950408889634f : sh;
         }
@@ -616,7 +649,7 @@ __device__ __forceinline__ void conv_wino_body(const ConvArgs& a) {
       }
       if (more2) load_sc(st + 2);
     }
-    const _Float16* As = patch + buf * kWBuf + nu * 64 * kWRowH + abase - nu * NR * kWRowH;
+    const _Float16* As = patch + buf * kWBuf + nu * 64 * kWRowH + abase_sc;
     a0[0] = *reinterpret_cast<const f16x8*>(As);
     a0[1] = *reinterpret_cast<const f16x8*>(As + 32);
     __builtin_amdgcn_sched_barrier(0);
@@ -724,7 +757,30 @@ __device__ __forceinline__ void conv_wino_body(const ConvArgs& a) {
     W_ACC(ew_cycles);
     // wave (chunk k, half hf, column half cj): output pixels 64 k + 32 hf .. + 31 of the tile = pairs 32 k + 16 hf ..,
     // pixel 2 p + s of pair p: y0 = (m0 + m1) + m2, y1 = (m1 - m2) - m3
-    {
+    if (KS) {  // raw partial sums (the row scale undone) to kpart[split]; the reduction adds the epilogue
+      const int kq = wave >> 2, hf = (wave >> 1) & 1, cj = wave & 1;
+      const int c4 = lane & 15, rsub = lane >> 4;  // 4 columns of a pair row, 4 pair rows per wave instruction
+      const int px0 = 64 * kq + 32 * hf, ncol = cn0 + cj * 64 + 4 * c4;
+      const float* Ec = E + cj * 64 * kWEP + 4 * c4;
+      float* kp = a.kpart + (size_t)split * M * N + ncol;
+      f4 fin = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int i = 4 * it + rsub, pp = (px0 >> 1) + i;
+        const f4 mv0 = *reinterpret_cast<const f4*>(Ec + (0 * 2 * 64 + pp) * kWEP);
+        const f4 mv1 = *reinterpret_cast<const f4*>(Ec + (1 * 2 * 64 + pp) * kWEP);
+        const f4 mv2 = *reinterpret_cast<const f4*>(Ec + (2 * 2 * 64 + pp) * kWEP);
+        const f4 mv3 = *reinterpret_cast<const f4*>(Ec + (3 * 2 * 64 + pp) * kWEP);
+        const f4 y0 = ((mv0 + mv1) + mv2) * cs4, y1 = ((mv1 - mv2) - mv3) * cs4;
+        fin += y0 + y1;
+        const int m = cm0 + px0 + 2 * i;  // (m even, M even: both pixels or neither)
+        if (m < M) {
+          *reinterpret_cast<f4*>(kp + (size_t)m * N) = y0;
+          *reinterpret_cast<f4*>(kp + (size_t)(m + 1) * N) = y1;
+        }
+      }
+      if (!__builtin_isfinite(fin[0] + fin[1] + fin[2] + fin[3]) && a.range_flag) *a.range_flag = 1;
+    } else {
       const int kq = wave >> 2, hf = (wave >> 1) & 1, cj = wave & 1;
       typedef StagedEpilogue<64> Epi;
       Epi epi(a, M, HW, cb0, IMGS == 1, cn0 + cj * 64, lane);
@@ -851,22 +907,36 @@ extern "C" int dm_debug_wino_stamps(void* host, int nblocks) {
 #endif
 
 bool conv_wino_shape_ok(const ConvArgs& a) {
-  if (!(a.taps == 9 && a.stride == 1 && a.upsample == 0 && a.ksplit <= 1)) return false;
+  if (!(a.taps == 9 && a.stride == 1 && a.upsample == 0)) return false;
   if (a.Hin != a.Hout || a.Win != a.Wout) return false;
-  // 32- or 16-wide maps in whole-row 128-pixel tiles; 8 x 8 maps two images per tile; wider maps (a multiple of 32
-  // columns, of 4 rows) in 4 x 32 tiles
-  const int imgs = a.Wout == 8 ? 2 : 1;
+  // 32- or 16-wide maps in whole-row 128-pixel tiles; 8 x 8 maps two images per tile, 4 x 4 maps eight (split-K: 2 ..
+  // Cin1 / 32 splits, their partial sums in kpart); wider maps (a multiple of 32 columns, of 4 rows) in 4 x 32 tiles
+  const bool w4 = a.Wout == 4;
+  if (w4 ? !(a.Hout == 4 && a.ksplit >= 2 && a.ksplit <= a.Cin1 / kWC && a.kpart &&
+             (reinterpret_cast<uintptr_t>(a.kpart) & 15) == 0)
+         : a.ksplit > 1)
+    return false;
+  const int imgs = a.Wout == 8 ? 2 : w4 ? 8 : 1;
   const bool wide = a.Wout > 32;
   if (wide ? (a.Wout % 32 != 0 || a.Hout % 4 != 0)
-           : a.Wout == 8 ? a.Hout != 8 : ((a.Wout != 32 && a.Wout != 16) || (a.Hout * a.Wout) % 128 != 0))
+           : a.Wout == 8 ? a.Hout != 8
+           : w4          ? false
+                         : ((a.Wout != 32 && a.Wout != 16) || (a.Hout * a.Wout) % 128 != 0))
     return false;
-  if (a.Cin1 < kWC || a.Cin1 % kWC != 0 || 2 * imgs * a.Cin1 > kWTab || a.Cin2 % (2 * kWC) != 0 ||
+  const int tabc = w4 ? ceil_div(a.Cin1 / kWC, a.ksplit) * kWC : a.Cin1;  // GroupNorm table channels of a block
+  if (a.Cin1 < kWC || a.Cin1 % kWC != 0 || 2 * imgs * tabc > kWTab || a.Cin2 % (2 * kWC) != 0 ||
       a.K != 9 * a.Cin1 + a.Cin2)
     return false;
   if (a.x1_pitch + a.Cin1 > kZeroPageFloats) return false;  // the loader's padding rows read the zero page
   if (a.Cin2 && (!a.x2 || a.x2_pitch % 4 != 0 || (reinterpret_cast<uintptr_t>(a.x2) & 15) != 0)) return false;
   if (a.Cout % 128 != 0) return false;
   if (a.gin_part && (a.gin_G <= 0 || a.gin_G > kWMaxG || a.Cin1 % a.gin_G != 0)) return false;
+  if (w4) {  // the epilogue runs in conv_splitk_reduce (its GroupNorm statistics: one chunk per image)
+    ConvArgs e = a;
+    e.gn_part = nullptr;
+    return staged_epilogue_ok(e) && a.Cout % 4 == 0 &&
+           (!a.gn_part || (a.gn_G > 0 && a.Cout % a.gn_G == 0 && a.Cout <= 1024));
+  }
   return staged_epilogue_ok(a);
 }
 
@@ -917,15 +987,17 @@ int conv2d_wino(const ConvArgs& a, hipStream_t st) {
                                                  hipSuccess || ncu <= 0)
       ncu = 256;
   }
-  const int imgs = a.Wout == 8 ? 2 : 1, groups = ceil_div(a.B, imgs);  // image groups (two 8 x 8 images per tile)
+  // image groups (two 8 x 8 / eight 4 x 4 images per tile; the 4 x 4 maps split-K)
+  const int imgs = a.Wout == 8 ? 2 : a.Wout == 4 ? 8 : 1, groups = ceil_div(a.B, imgs);
+  const int ks = a.Wout == 4 ? a.ksplit : 1;
   const int tpi = (imgs * a.Hout * a.Wout / 128) * (a.Cout / 128);
   int parts = tpi;
   for (int p = 1; p <= tpi; ++p)
-    if (tpi % p == 0 && (long)groups * p >= ncu) {
+    if (tpi % p == 0 && (long)groups * p * ks >= ncu) {
       parts = p;
       break;
     }
-  const int blocks = groups * parts;
+  const int blocks = ks * groups * parts;
   const int prom = (a.pro_scale || a.gin_part) ? (a.pro_nosilu ? 1 : 2) : 0;
 #define DM_WINO_LAUNCH(W_, P_)                                                                              \
   if (a.Wout == W_ && prom == P_) {                                                                         \
@@ -936,6 +1008,7 @@ int conv2d_wino(const ConvArgs& a, hipStream_t st) {
   DM_WINO_LAUNCH(32, 0) DM_WINO_LAUNCH(32, 1) DM_WINO_LAUNCH(32, 2)
   DM_WINO_LAUNCH(16, 0) DM_WINO_LAUNCH(16, 1) DM_WINO_LAUNCH(16, 2)
   DM_WINO_LAUNCH(8, 0) DM_WINO_LAUNCH(8, 1) DM_WINO_LAUNCH(8, 2)
+  DM_WINO_LAUNCH(4, 0) DM_WINO_LAUNCH(4, 1) DM_WINO_LAUNCH(4, 2)
 #undef DM_WINO_LAUNCH
 #define DM_WINO_WIDE(P_)                                                                                     \
   if (a.Wout > 32 && prom == P_) {                                                                          \
@@ -946,6 +1019,7 @@ int conv2d_wino(const ConvArgs& a, hipStream_t st) {
   DM_WINO_WIDE(0) DM_WINO_WIDE(1) DM_WINO_WIDE(2)
 #undef DM_WINO_WIDE
   DM_LAUNCH_CHECK();
+  if (ks > 1) return conv_splitk_reduce(a, st);
   return DM_OK;
 }
 

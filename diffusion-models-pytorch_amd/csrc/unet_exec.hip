@@ -224,6 +224,14 @@ UNetModel::~UNetModel() {
   if (arena) (void)hipFree(arena);
 }
 
+// The split count of the Winograd kernel on a 4 x 4 map, 0 where the plan keeps the direct kernel: 4 splits when a
+// split has >= 12 K steps of 32 channels (maybe_split below; split_for attaches the Winograd weights to those only)
+static int wino_small_ks(const ConvArgs& c) {
+  if (c.Hout != 4 || c.Wout != 4) return 0;
+  const int ks = std::min(4, c.Cin1 / 32);
+  return ks >= 2 && (3 * (c.Cin1 / 32) + c.Cin2 / 64) / ks >= 12 ? ks : 0;
+}
+
 // Attach the split copy of a halo-patch conv's packed weights (none: the conv stays on the fp32
 // kernels).
 void UNetModel::split_for(ConvArgs& c) {
@@ -262,6 +270,7 @@ void UNetModel::split_for(ConvArgs& c) {
   c.wino_ws = nullptr;
   c.wino_rowscale = nullptr;
   if (conv_math != 2 || !toggles().wino || !conv_wino_shape_ok(c)) return;
+  if (c.Wout == 4 && c.ksplit != wino_small_ks(c)) return;  // (4 x 4: the plan's split decision)
   const int fold = c.Cin2 && (c.pro_scale || c.gin_part) && !c.pro_nosilu ? 1 : 0;
   auto iw = wino_w.find(std::make_pair(c.w, fold));
   void* wp = nullptr;
@@ -784,11 +793,24 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
   float* kpart_ws = nullptr;
   size_t kpart_floats = 0;
   auto maybe_split = [&](ConvArgs& c) {
-    if (c.upsample == 2 || c.taps != 9 || c.stride != 1 || c.Hout * c.Wout > 16 || conv_pick(c) < 3) return;
-    // K32 split tiles (conv_k32.hip): 2 splits (4x4 maps, B = 256: 32.5 us vs 37.8 us with 4, the
-    // reduction included); conv_patch3's 16-channel chunks: 4
-    const int ks = std::min(2, c.Cin1 / 32);
-    if (ks < 2) return;
+    if (c.upsample == 2 || c.taps != 9 || c.stride != 1 || c.Hout * c.Wout > 16) return;
+    // the Winograd kernel on 4 x 4 maps (conv_wino.hip, fp16x2): 4 splits (64 tiles x 4 = 256 blocks at B = 256),
+    // reduced by conv_splitk_reduce, where a split has >= 12 K steps of 32 channels (B = 256: 512 -> 256 33.2 us vs
+    // conv_k32s 39.8 us; at 256 -> 256, 6 steps, 26.6 vs 22.8 us: the per-block prologue / epilogue and the
+    // reduction pass dominate); else the K32 small-map kernel (conv_k32.hip): 2 splits inside the block (4x4
+    // maps, B = 256: 32.5 us vs 37.8 us with 4, the reduction included); conv_patch3's 16-channel chunks: 4
+    int ks = 0;
+    if (conv_math == 2 && toggles().wino && wino_small_ks(c)) {
+      ConvArgs w = c;
+      w.ksplit = wino_small_ks(c);
+      w.kpart = reinterpret_cast<float*>(16);  // placeholder: the shape check only
+      if (conv_wino_shape_ok(w)) ks = w.ksplit;
+    }
+    if (!ks) {
+      if (conv_pick(c) < 3) return;
+      ks = std::min(2, c.Cin1 / 32);
+      if (ks < 2) return;
+    }
     const size_t need = (size_t)ks * c.B * c.Hout * c.Wout * c.Cout;
     if (need > kpart_floats) {
       kpart_ws = alloc(need * 4);

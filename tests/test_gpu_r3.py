@@ -396,14 +396,16 @@ def test_flash_attention_vs_unfused(cuda, golden, report, monkeypatch, case):
 @pytest.mark.parametrize('arch', ['cifar10', 'adagn'])
 def test_small_map_conv_vs_splitk(cuda, golden, report, monkeypatch, arch):
     """The 4 x 4 level's convs on conv_k32s_kernel (one launch, K split inside the block, GroupNorm statistics
-    per image from its epilogue) against the two-launch split-K path with its reduction (DM_CONV_K32S=0):
-    whole forwards within 1e-5 (the ResBlock shortcut's chunks are split over the two K groups, so the
-    partial sums group differently), and the kernel is the one the plan runs."""
+    per image from its epilogue; DM_CONV_WINO=0) against the two-launch split-K path with its reduction
+    (DM_CONV_K32S=0) and against the default since round 6, which puts the up path's 512-channel conv1s on the split-K
+    Winograd kernel (conv_wino_kernel<4, ..> + conv_splitk_reduce, GroupNorm statistics from the reduction; its in-kernel
+    GroupNorm finalize over a split's channels): whole forwards within 1e-5 (the partial sums
+    group differently), and each kernel is the one the plan runs."""
     from models.unet_categorial_adagn import UNetCategorialAdaGN
     outs = {}
-    for mode in ('small', 'splitk'):
-        if mode == 'splitk':
-            monkeypatch.setenv('DM_CONV_K32S', '0')
+    for mode in ('small', 'splitk', 'wino'):
+        monkeypatch.setenv('DM_CONV_WINO', '1' if mode == 'wino' else '0')
+        monkeypatch.setenv('DM_CONV_K32S', '0' if mode == 'splitk' else '1')
         if arch == 'cifar10':
             m, _ = _model(golden('forward')[1], 'cifar10', cuda)
         else:
@@ -418,12 +420,17 @@ def test_small_map_conv_vs_splitk(cuda, golden, report, monkeypatch, arch):
         dmhip.unet_profile_enable(h, 1)
         dmhip.unet_profile_enable(h, 0)
         labels = [op['label'] for op in dmhip.unet_profile_read(h)]
-        assert any(lb.startswith('conv_k32s_kernel') for lb in labels) == (mode == 'small'), labels
+        assert dmhip.range_stats(h)[0] == 0  # (a range fallback would re-run the forward in bf16x3)
+        k32s = any(lb.startswith('conv_k32s_kernel') for lb in labels)
+        wino4 = any(lb.startswith('conv_wino_kernel<4,') for lb in labels)
+        # (the Winograd mode keeps conv_k32s for the convs with < 12 K steps per split: unet_exec.hip maybe_split)
+        assert (k32s, wino4) == {'small': (True, False), 'splitk': (False, False), 'wino': (k32s, True)}[mode], labels
         del m
-    err = (outs['small'] - outs['splitk']).abs().max().item()
-    report(f'small_map_conv_{arch}_maxabs_vs_splitk', err)
-    assert torch.isfinite(outs['small']).all()
-    assert err <= 1e-5, err
+    for other in ('splitk', 'wino'):
+        err = (outs['small'] - outs[other]).abs().max().item()
+        report(f'small_map_conv_{arch}_maxabs_vs_{other}', err)
+        assert torch.isfinite(outs[other]).all()
+        assert err <= 1e-5, (other, err)
 
 
 # ------------------------------------------------------------------ first conv row split

@@ -176,14 +176,20 @@ def test_wino_cifar_forward(cuda, golden, monkeypatch, report, B):
     xg = torch.Generator().manual_seed(41)
     x = torch.randn((B, 3, 32, 32), generator=xg).to(cuda)
     t = torch.randint(0, 1000, (B, ), generator=xg).to(cuda)
-    _, out_w, log_w = _forward_logged(meta, 'cifar10', cuda, x, t)
+    model_w, out_w, log_w = _forward_logged(meta, 'cifar10', cuda, x, t)
+    # no range fallback (a non-finite Winograd output raises the flag and the forward re-runs in bf16x3, which would
+    # hide it from the comparison below)
+    assert dmhip.range_stats(model_w.native_handle(cuda))[0] == 0
     monkeypatch.setenv('DM_CONV_WINO', '0')
     _, out_d, log_d = _forward_logged(meta, 'cifar10', cuda, x, t)
     n32 = sum(log_w.count(f'conv_wino_kernel<32,2,{sc}>') for sc in ('false', 'true'))
     n16 = sum(log_w.count(f'conv_wino_kernel<16,2,{sc}>') for sc in ('false', 'true'))
     n8 = sum(log_w.count(f'conv_wino_kernel<8,2,{sc}>') for sc in ('false', 'true'))
-    # every 3x3 ResBlock conv of the 32^2 / 16^2 / 8^2 levels, shortcuts included
-    assert n32 == 10 and n16 == 10 and n8 == 10, log_w
+    n4 = sum(log_w.count(f'conv_wino_kernel<4,2,{sc}>') for sc in ('false', 'true'))
+    # every 3x3 ResBlock conv of the 32^2 / 16^2 / 8^2 levels, shortcuts included; at 4^2 the up path's three
+    # 512-channel conv1s (split-K, round 6: >= 12 K steps per split), the other eleven on conv_k32s
+    assert n32 == 10 and n16 == 10 and n8 == 10 and n4 == 3, log_w
+    assert sum(s.startswith('conv_k32s_kernel') for s in log_w) == 11, log_w
     assert not any(s.startswith('conv_wino') for s in log_d), log_d
     err = (out_w - out_d).abs().max().item()
     report(f'wino_cifar_forward_B{B}_vs_direct', err)
@@ -198,9 +204,11 @@ def test_wino_cifar_forward(cuda, golden, monkeypatch, report, B):
 
 
 def test_small_map_variants_both_launched_bit_identical(cuda, golden, monkeypatch):
-    """The 4x4-level convs: DM_K32S_W4=1 resolves the 4-wave conv_k32s_kernel at plan build (variant 12) and the
-    default the 8-wave one (variant 6) -- the launch log proves each ran -- with the same bits."""
+    """The 4x4-level convs on the direct kernels (DM_CONV_WINO=0; the default takes the split-K Winograd kernel since
+    round 6): DM_K32S_W4=1 resolves the 4-wave conv_k32s_kernel at plan build (variant 12) and the default the 8-wave
+    one (variant 6) -- the launch log proves each ran -- with the same bits."""
     _, meta = golden('forward')
+    monkeypatch.setenv('DM_CONV_WINO', '0')
     xg = torch.Generator().manual_seed(33)
     x = torch.randn((5, 3, 32, 32), generator=xg).to(cuda)
     t = torch.randint(0, 1000, (5, ), generator=xg).to(cuda)

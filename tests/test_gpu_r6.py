@@ -166,3 +166,101 @@ def test_adm256_wide_wino_forward(cuda, golden, report, monkeypatch):
     report('adm256_wide_wino_maxabs_vs_reference', ref_err)
     assert err <= 1e-5, err
     assert ref_err <= TOL, ref_err
+
+
+# ---- 4 x 4 maps (the CIFAR UNet's 4^2 level, models/unet.py:121-152): eight images per 128-pixel tile, split-K over
+# the input channels (conv_wino_kernel<4, ..>: raw partial sums per split, conv_splitk_reduce adds them in split order
+# with the epilogue); the plan takes it with 4 splits in place of the direct conv_k32s_kernel
+SMALL_SHAPES = [(1, 64, 128, 2), (8, 256, 256, 4), (11, 128, 256, 4), (3, 512, 128, 3), (16, 96, 128, 3)]
+
+
+@pytest.mark.parametrize('B,Cin,Cout,ks', SMALL_SHAPES)
+@pytest.mark.parametrize('pro', [False, True])
+def test_wino_small_exact(cuda, B, Cin, Cout, ks, pro):
+    """Integer operands: every split's partial sums are exact, so the split-K Winograd conv on 4 x 4 maps equals the
+    float64 conv bit for bit (zero padding at every image edge -- eight images side by side in a tile's patch -- a
+    group's images past B, uneven splits)."""
+    x = _ints((B, Cin, 4, 4), -2, 3, seed=190)
+    w = _ints((Cout, Cin, 3, 3), -2, 3, seed=191)
+    b = _ints((Cout, ), seed=192)
+    xin, prot = x, None
+    if pro:
+        xin = x * 2 - 1
+        prot = (torch.full((B, Cin), 2.0, device=cuda), torch.full((B, Cin), -1.0, device=cuda))
+    ref = F.conv2d(xin.double(), w.double(), b.double(), padding=1).float()
+    y, log = _conv_logged(cuda, _nhwc(x).to(cuda), _pack(w, cuda), Cout, 4, 4, 9, 1, 0, b.to(cuda), tile=WINO,
+                          split='fp16x2', wino=True, pro=prot, pro_nosilu=1 if pro else 0, ksplit=ks)
+    assert log == [f'conv_wino_kernel<4,{1 if pro else 0},false>'], log
+    assert torch.equal(y.cpu(), _nhwc(ref))
+
+
+def test_wino_small_rowvec_residual_pitch(cuda):
+    """temb row vector, residual (added once, in the reduction), pitched input and output, integer-exact."""
+    B, Cin, Cout = 9, 64, 128
+    x = _ints((B, Cin, 4, 4), seed=200)
+    w = _ints((Cout, Cin, 3, 3), -2, 3, seed=201)
+    b = _ints((Cout, ), seed=202)
+    rv = _ints((B, Cout), seed=203)
+    res = _ints((B, Cout, 4, 4), seed=204)
+    ref = (F.conv2d(x.double(), w.double(), b.double(), padding=1) + rv.double()[:, :, None, None]
+           + res.double()).float()
+    xp = torch.full((B, 4, 4, 96), float('nan'), device=cuda)
+    xp[..., :Cin] = _nhwc(x).to(cuda)
+    y = _run_conv(cuda, xp[..., :Cin], _pack(w, cuda), Cout, 4, 4, 9, bias=b.to(cuda), rowvec=rv.to(cuda),
+                  res=_nhwc(res).to(cuda), y_pitch=160, x_pitch=96, tile=WINO, split='fp16x2', wino=True, ksplit=2)
+    assert torch.equal(y[..., :Cout].cpu(), _nhwc(ref))
+    assert torch.isnan(y[..., Cout:]).all()
+
+
+@pytest.mark.parametrize('C1,C2,Cout,ks,pro', [(256, 512, 256, 4, False), (64, 64, 128, 2, True),
+                                               (128, 192, 256, 4, False)])
+def test_wino_small_shortcut_exact(cuda, C1, C2, Cout, ks, pro):
+    """ResBlock conv2 with the 1x1 shortcut segment on 4 x 4 maps: each split takes its share of the shortcut steps
+    (none for some splits), integer-exact."""
+    B = 10
+    h = _ints((B, C1, 4, 4), seed=210)
+    x = _ints((B, C2, 4, 4), seed=211)
+    w2 = _ints((Cout, C1, 3, 3), -2, 3, seed=212)
+    ws = _ints((Cout, C2, 1, 1), seed=213)
+    b = _ints((Cout, ), seed=214)
+    rv = _ints((B, Cout), seed=215)
+    res = _ints((B, Cout, 4, 4), seed=216)
+    K = 9 * C1 + C2
+    wp = torch.zeros((Cout, K), device=cuda)
+    _pack(w2, cuda, K, 0, wp)
+    _pack(ws, cuda, K, 9 * C1, wp)
+    hin, prot = h, None
+    if pro:
+        hin = h * 2 - 1
+        prot = (torch.full((B, C1), 2.0, device=cuda), torch.full((B, C1), -1.0, device=cuda))
+    ref = (F.conv2d(hin.double(), w2.double(), b.double(), padding=1) + rv.double()[:, :, None, None]
+           + F.conv2d(x.double(), ws.double()) + res.double()).float()
+    y, log = _conv_logged(cuda, _nhwc(h).to(cuda), wp, Cout, 4, 4, 9, bias=b.to(cuda), rowvec=rv.to(cuda),
+                          res=_nhwc(res).to(cuda), x2=_nhwc(x).to(cuda), Cin2=C2, tile=WINO, split='fp16x2',
+                          wino=True, pro=prot, pro_nosilu=1 if pro else 0, ksplit=ks)
+    assert log == [f'conv_wino_kernel<4,{1 if pro else 0},true>'], log
+    assert torch.equal(y.cpu(), _nhwc(ref))
+
+
+@pytest.mark.parametrize('B,Cin,Cout', [(64, 256, 256), (24, 512, 256)])
+def test_wino_small_fp32_accuracy(cuda, report, B, Cin, Cout):
+    """GroupNorm + SiLU prologue on random data at 4 x 4: the split-K Winograd conv's error vs float64 is at most the
+    fp32 MFMA kernel's and its rms at most the direct fp16x2 small-map kernel's (conv_k32s, tile 15)."""
+    from tests.test_gpu_conv_split import _rand_case
+    xd, wp, b, pro, ref = _rand_case(cuda, B, Cin, Cout, 4, 0, seed=220)
+    errs, rms = {}, {}
+    for name, split, tile, wino, ks in (('fp32', False, 0, False, 0), ('k32s', 'fp16x2', 15, False, 2),
+                                        ('wino', 'fp16x2', WINO, True, 4)):
+        y = _run_conv(cuda, xd, wp, Cout, 4, 4, 9, 1, 0, b.to(cuda), pro=pro, split=split, tile=tile, wino=wino,
+                      ksplit=ks)
+        d = y.cpu().double() - _nhwc(ref)
+        errs[name] = d.abs().max().item()
+        rms[name] = d.pow(2).mean().sqrt().item()
+    scale = ref.abs().max().item()
+    for k in errs:
+        report(f'wino_small_accuracy_{B}_{Cin}_{Cout}_{k}_max_rel', errs[k] / scale)
+        report(f'wino_small_accuracy_{B}_{Cin}_{Cout}_{k}_rms_rel', rms[k] / scale)
+    assert errs['wino'] <= errs['fp32'], errs
+    assert rms['wino'] <= rms['fp32'], rms
+    assert rms['wino'] <= rms['k32s'], rms
+    assert errs['wino'] < 6e-6 * scale, (errs, scale)
