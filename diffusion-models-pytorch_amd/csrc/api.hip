@@ -51,8 +51,10 @@ void refresh_toggles() {
            : v == "unfused" ? kAttnUnfused : 4;
   }
   t.attn_gn_launch = env_is("DM_ATTN_GNFIN", '1');
+  t.attn_small = !env_is("DM_ATTN_SMALL", '0');
   t.dit_presplit = !env_is("DM_DIT_PRESPLIT", '0');
   t.lin_sk = !env_is("DM_LIN_SK", '0');
+  t.lin_rows = !env_is("DM_LIN_ROWS", '0');
   t_toggles = t;
 }
 void note_launch(const char* name) {

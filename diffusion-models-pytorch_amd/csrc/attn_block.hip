@@ -913,6 +913,208 @@ __global__ void attn_perm_cols_kernel(const float* __restrict__ wg, float* __res
   wgp[id] = wg[(size_t)d * C + (k & ~31) + pi32(pi32(k & 31))];
 }
 
+// dst[k][n] = src[n][k] (C x C): the small-map block's operands, read a row of k per step by 256 threads
+__global__ void attn_transpose_kernel(const float* __restrict__ src, float* __restrict__ dst, int C) {
+  const long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= (long)C * C) return;
+  const int k = (int)(id / C), n = (int)(id % C);
+  dst[id] = src[(size_t)n * C + k];
+}
+
+// ======================================================================================================
+// Small maps: the single-head block on a 4 x 4 map of 256 channels (the CIFAR UNet's middle block,
+// models/unet.py:97-99 -> models/modules.py:77-102), L = 16 tokens. The same folded form as variant 3/4,
+//   T = xn At^T + w,  S = T xn^T,  P = softmax(S),  y = x + Wg (P xn) + cb,
+// but at L = 16 the block is 2.1 M multiply-adds per image (the unfolded qkv / S / PV / proj launches took
+// 88 us per forward at B = 256, five launches with a q / k / v buffer between them): one work-group of 512
+// threads per image, fp32 throughout (no operand split), everything in LDS. The two C x C products run on
+// v_mfma_f32_16x16x4f32 (exact fp32 products, fp32 sums; wave w owns 32 channels x the 16 tokens; At^T and Wg^T
+// transposed at the fold so a K step reads 16 consecutive floats per row; on the vector ALUs they took 54 us per
+// launch), S / the softmax run on 16 lanes per query row, P xn on thread (n, h) = channel n x tokens 8 h .. + 7,
+// and the epilogue emits the consumer's GroupNorm partials (one 64-pixel chunk per image).
+constexpr int kSL = 16;          // tokens of the small map
+constexpr int kSTP = kBC + 4;    // fp32 pitch of the T rows
+
+__global__ void __launch_bounds__(512) attn_small_kernel(AttnBlockArgs a) {
+  __shared__ __attribute__((aligned(16))) float xnt[kBC][kSL];   // xn^T [channel][token]
+  __shared__ __attribute__((aligned(16))) float tt[kSL * kSTP];  // T [token][kSTP], then O^T [channel][token]
+  __shared__ __attribute__((aligned(16))) float pm[kSL][kSL];    // S partial sums, then P
+  __shared__ __attribute__((aligned(16))) float tab[2][kBC];
+  __shared__ double csum[2][kBC];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int n = t & (kBC - 1), h = t >> 8, r0 = 8 * h;
+  const float* xb = a.x + (size_t)b * kSL * a.x_pitch;
+  // x rows of this thread (kept for the residual), loaded while the GroupNorm affine is formed
+  float xv[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) xv[r] = xb[(size_t)(r0 + r) * a.x_pitch + n];
+  if (t < kBC) {
+    if (a.gin_part) {  // gn_finalize (gn.hip), the expressions of attn_block4_kernel's in-kernel finalize
+      const int cpg = kBC / a.gin_G, g = t / cpg;
+      const double cnt = (double)kSL * cpg;
+      double s1 = 0, s2 = 0;
+      for (int k = 0; k < a.gin_nchunk; ++k) {
+        const double2 v = a.gin_part[((size_t)b * a.gin_nchunk + k) * a.gin_G + g];
+        s1 += v.x;
+        s2 += v.y;
+      }
+      const double m = s1 / cnt;
+      double var = s2 / cnt - m * m;
+      if (var < 0) var = 0;
+      const float mu = (float)m;
+      const float rs = (float)(1.0 / sqrt(var + (double)a.gin_eps));
+      const float sc = rs * (a.gin_gamma ? a.gin_gamma[t] : 1.0f);
+      tab[0][t] = sc;
+      tab[1][t] = -sc * mu + (a.gin_beta ? a.gin_beta[t] : 0.0f);
+    } else {
+      tab[0][t] = a.gsc[(size_t)b * kBC + t];
+      tab[1][t] = a.gsh[(size_t)b * kBC + t];
+    }
+  }
+  __syncthreads();
+  {
+    const float sc = tab[0][n], sh = tab[1][n];
+    f4 v0, v1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      v0[r] = xv[r] * sc + sh;
+      v1[r] = xv[4 + r] * sc + sh;
+    }
+    *reinterpret_cast<f4*>(&xnt[n][r0]) = v0;
+    *reinterpret_cast<f4*>(&xnt[n][r0 + 4]) = v1;
+  }
+  __syncthreads();
+  // D[i][n] = sum_k tok[k][i] wt[k][n] on v_mfma_f32_16x16x4f32 (fp32 products and sums): wave w takes the column
+  // tiles nt = 2 w, 2 w + 1 (16 channels each) for all 16 tokens; lane l supplies A[l % 16][k0 + l / 16] (tok, LDS) and
+  // B[k0 + l / 16][16 nt + l % 16] (wt, global, 8 K steps ahead in registers) and holds D[4 (l / 16) + e][16 nt + l % 16]
+  const int lane = t & 63, wave = t >> 6, lc = lane & 15, lk = lane >> 4;
+  auto product = [&](const float* tok, const float* __restrict__ wt, f4 (&d)[2]) {
+    d[0] = f4{0.f, 0.f, 0.f, 0.f};
+    d[1] = d[0];
+    const float* wl = wt + (size_t)lk * kBC + 32 * wave + lc;
+    float bc[8][2], bn[8][2];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt) bc[u][jt] = wl[(size_t)(4 * u) * kBC + 16 * jt];
+    for (int k0 = 0; k0 < kBC; k0 += 32) {
+      if (k0 + 32 < kBC) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+#pragma unroll
+          for (int jt = 0; jt < 2; ++jt) bn[u][jt] = wl[(size_t)(k0 + 32 + 4 * u) * kBC + 16 * jt];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float av = tok[(k0 + 4 * u + lk) * kSL + lc];
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt) d[jt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bc[u][jt], d[jt], 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt) bc[u][jt] = bn[u][jt];
+    }
+  };
+  f4 dacc[2];
+  // T[i][n] = sum_k xn[i][k] At[n][k] + w[n]
+  product(&xnt[0][0], a.at_t, dacc);
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt) {
+    const int nn = 32 * wave + 16 * jt + lc;
+    const float wn_ = a.w[nn];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) tt[(4 * lk + e) * kSTP + nn] = dacc[jt][e] + wn_;
+  }
+  __syncthreads();
+  // S[i][j] = T_i . xn_j: thread (i, j) of the 256, k half h; the halves added in LDS
+  {
+    const int i = (t & 255) >> 4, j = t & 15, kb = 128 * h;
+    float s = 0.f;
+#pragma unroll 4
+    for (int k = kb; k < kb + 128; k += 4) {
+      const f4 tv = *reinterpret_cast<const f4*>(&tt[i * kSTP + k]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s = fmaf(tv[e], xnt[k + e][j], s);
+    }
+    if (h == 1) pm[i][j] = s;
+    __syncthreads();
+    if (h == 0) {
+      s += pm[i][j];
+      // softmax over the 16 lanes of row i
+      float m = s;
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) m = fmaxf(m, __shfl_xor(m, o));
+      const float e = expf(s - m);
+      float z = e;
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) z += __shfl_xor(z, o);
+      pm[i][j] = e / z;
+    }
+  }
+  __syncthreads();
+  // O^T[n][i] = sum_j P[i][j] xn[j][n] (over T's rows: T is dead)
+  {
+    float xc[kSL];
+#pragma unroll
+    for (int j = 0; j < kSL; j += 4) {
+      const f4 v = *reinterpret_cast<const f4*>(&xnt[n][j]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) xc[j + e] = v[e];
+    }
+    f4 o0, o1;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      float o = 0.f;
+#pragma unroll
+      for (int j = 0; j < kSL; ++j) o = fmaf(pm[r0 + r][j], xc[j], o);
+      if (r < 4) o0[r] = o; else o1[r - 4] = o;
+    }
+    *reinterpret_cast<f4*>(&tt[n * kSL + r0]) = o0;
+    *reinterpret_cast<f4*>(&tt[n * kSL + r0 + 4]) = o1;
+  }
+  __syncthreads();
+  // y[i][n] = x[i][n] + (sum_k O[i][k] Wg[n][k] + cb[n])
+  product(tt, a.wg_t, dacc);
+  float* yb = a.y + (size_t)b * kSL * a.y_pitch;
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt) {
+    const int nn = 32 * wave + 16 * jt + lc;
+    const float cbn = a.cb[nn];
+    double gs = 0.0, gq = 0.0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = 4 * lk + e;
+      const float v = xb[(size_t)row * a.x_pitch + nn] + (dacc[jt][e] + cbn);
+      yb[(size_t)row * a.y_pitch + nn] = v;
+      gs += (double)v;
+      gq += (double)v * v;
+    }
+    if (a.gn_part) {  // column sums over the 16 tokens, then the groups' cpg columns in order (below)
+      gs += __shfl_xor(gs, 16);
+      gq += __shfl_xor(gq, 16);
+      gs += __shfl_xor(gs, 32);
+      gq += __shfl_xor(gq, 32);
+      if (lk == 0) {
+        csum[0][nn] = gs;
+        csum[1][nn] = gq;
+      }
+    }
+  }
+  if (a.gn_part) {  // one 64-pixel chunk per image
+    __syncthreads();
+    const int cpg = kBC / a.gn_G;
+    if (t < a.gn_G) {
+      double s1 = 0.0, s2 = 0.0;
+      for (int c = t * cpg; c < (t + 1) * cpg; ++c) {
+        s1 += csum[0][c];
+        s2 += csum[1][c];
+      }
+      a.gn_part[(size_t)b * a.gn_G + t] = make_double2(s1, s2);
+    }
+  }
+}
+
 }  // namespace
 
 #ifdef DM_K32_STAMPS
@@ -938,6 +1140,29 @@ int attn_perm_cols(const float* wg, float* wgp, int C, hipStream_t st) {
   DM_REQUIRE(wg && wgp && C % 32 == 0, "attention fold: column permutation needs C % 32 == 0");
   const long n = (long)C * C;
   hipLaunchKernelGGL(attn_perm_cols_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, wg, wgp, C);
+  DM_LAUNCH_CHECK();
+  return DM_OK;
+}
+
+bool attn_small_ok(int L, int C, int heads) { return L == kSL && C == kBC && heads == 1; }
+
+int attn_transpose(const float* src, float* dst, int C, hipStream_t st) {
+  DM_REQUIRE(src && dst && C > 0, "attention fold: null argument");
+  const long n = (long)C * C;
+  hipLaunchKernelGGL(attn_transpose_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, src, dst, C);
+  DM_LAUNCH_CHECK();
+  return DM_OK;
+}
+
+int attn_small(const AttnBlockArgs& a, hipStream_t st) {
+  DM_REQUIRE(a.B > 0 && a.x && a.y && a.x != a.y && (a.gin_part || (a.gsc && a.gsh)) && a.at_t && a.w && a.wg_t && a.cb,
+             "small-map attention block: null or in-place argument");
+  DM_REQUIRE(!a.gin_part || (a.gin_G > 0 && kBC % a.gin_G == 0 && a.gin_nchunk > 0),
+             "small-map attention block: the in-kernel GroupNorm finalize needs groups dividing 256 channels");
+  DM_REQUIRE(!a.gn_part || (a.gn_G > 0 && kBC % a.gn_G == 0 && kBC / a.gn_G >= 4 && kBC / a.gn_G <= 64 &&
+                            ((kBC / a.gn_G) & (kBC / a.gn_G - 1)) == 0),
+             "small-map attention block: GroupNorm statistics need groups of 4 .. 64 channels (a power of two)");
+  hipLaunchKernelGGL(attn_small_kernel, dim3(a.B), dim3(512), 0, st, a);
   DM_LAUNCH_CHECK();
   return DM_OK;
 }

@@ -30,8 +30,11 @@ struct Toggles {
                               // form; the unfolded oracles (no folding, no flash kernel): 0 "presplit" (q / k /
                               // v planes from the qkv epilogue, proj fused), kAttnNoProj, kAttnFused, kAttnUnfused
   bool attn_gn_launch = false;  // DM_ATTN_GNFIN=1: the folded block's GroupNorm finalize as its own launch
+  bool attn_small = true;     // DM_ATTN_SMALL=0: the 4 x 4 single-head block unfolded (qkv / S / softmax / PV / proj
+                              // launches) instead of attn_small_kernel
   bool dit_presplit = true;   // DM_DIT_PRESPLIT=0: DiT token GEMMs split their activations per tile
   bool lin_sk = true;         // DM_LIN_SK=0: no split-K of linear_k32's last, partial round of tiles
+  bool lin_rows = true;       // DM_LIN_ROWS=0: the time MLP / temb projections on gemm_kernel instead of linear_rows
 };
 // The calling thread's snapshot: the innermost ToggleScope's (a plan's, while it is built, captured or replayed op by
 // op), else the thread's last refresh_toggles(). Thread-local: plan builds in concurrent threads do not see each
@@ -351,6 +354,9 @@ std::string conv_label(const ConvArgs& a);
 // plan's toggle snapshot
 inline int conv_math_from_env() { return toggles().conv_math; }
 int gemm_batched(const GemmArgs& g, hipStream_t st);
+// skinny fp32 linear (the time MLP / temb projections): C = act(A W^T + bias), W [n][k], no prologue / residual
+bool linear_rows_ok(const GemmArgs& g);
+int linear_rows(const GemmArgs& g, hipStream_t st);
 // exponent e with max|x| * 2^e in [2^13, 2^14) (0 for all-zero x): fp16x2 operand scale of a weight
 // matrix, computed once at plan build (synchronous)
 int split_weight_exponent(const float* x, size_t n);
@@ -412,8 +418,13 @@ struct AttnBlockArgs {
   int gin_G, gin_nchunk;
   const float *gin_gamma, *gin_beta;
   float gin_eps;
+  // attn_small (4 x 4 maps): At and Wg transposed, fp32 [k][n] (attn_transpose); w, cb, x, y, gin_*, gn_* as above
+  const float *at_t, *wg_t;
 };
 bool attn_block_ok(int L, int C, int heads);
+bool attn_small_ok(int L, int C, int heads);
+int attn_small(const AttnBlockArgs& a, hipStream_t st);
+int attn_transpose(const float* src, float* dst, int C, hipStream_t st);
 // at = s Wk^T Wq, w = s Wk^T bq, wg = Wp Wv, cb = Wp bv + bp (float64 sums, fp32 results)
 int attn_fold(const float* wqkv, const float* bqkv, const float* wproj, const float* bproj, int C, double scale,
               float* at, float* w, float* wg, float* cb, hipStream_t st);

@@ -367,7 +367,80 @@ int launch_gemm(const GemmArgs& g, hipStream_t st) {
   return DM_OK;
 }
 
+// Skinny fp32 linear, C[m][n] = act(sum_k A[m][k] W[n][k] + bias[n]) for M of a batch (the time MLP and the
+// ResBlocks' temb projections, models/unet.py:64-69 / :18-21: M = B rows, K <= 512). gemm_kernel's 64 x 64 tiles
+// give 32 blocks for M = 256, N = 512, each walking K alone (15-33 us per launch); here a block is 8 rows x 16 outputs:
+// the 8 A rows staged in LDS once (read back as broadcasts: straight from memory, the 16 lane groups' identical A
+// addresses each cost the CU's address unit a full pass, 4x the W traffic), 16 lanes per output splitting K (lane l
+// takes k = 4 l + 64 i .. + 3, a 256-B coalesced W segment per 16 lanes), each lane holding the 8 rows' partial sums,
+// then a 16-lane tree (xor 8, 4, 2, 1). Per row the sums depend on K only, not on M or the grid: batch-invariant as
+// the plans require.
+constexpr int kRowsR = 8, kRowsKMax = 512;
+template <int ACT>
+__global__ void __launch_bounds__(256) linear_rows_kernel(GemmArgs g) {
+  constexpr int R = kRowsR;
+  __shared__ __attribute__((aligned(16))) f4 as[R * kRowsKMax / 4];
+  const int t = threadIdx.x, l = t & 15;
+  const int n = blockIdx.x * 16 + (t >> 4), m0 = blockIdx.y * R;
+  const int nc = min(n, g.N - 1);
+  const int K4 = g.K / 4;
+  for (int i = t; i < R * K4; i += 256) {
+    const int r = i / K4, k = i - r * K4;
+    as[i] = reinterpret_cast<const f4*>(g.A + (size_t)min(m0 + r, g.M - 1) * g.lda)[k];
+  }
+  const f4* w = reinterpret_cast<const f4*>(g.Bm + (size_t)nc * g.ldb);
+  float acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = 0.f;
+  __syncthreads();
+#pragma unroll 2
+  for (int k = l; k < K4; k += 16) {
+    const f4 wv = w[k];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const f4 av = as[r * K4 + k];
+      acc[r] = fmaf(av.x, wv.x, acc[r]);
+      acc[r] = fmaf(av.y, wv.y, acc[r]);
+      acc[r] = fmaf(av.z, wv.z, acc[r]);
+      acc[r] = fmaf(av.w, wv.w, acc[r]);
+    }
+  }
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1)
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] += __shfl_xor(acc[r], o);
+  if (n >= g.N) return;
+  const float bn = g.bias ? g.bias[n] : 0.f;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (l != r || m0 + r >= g.M) continue;
+    float v = acc[r];
+    if (g.bias) v = v + bn;
+    if (ACT == 1) v = silu_f(v);
+    g.C[(size_t)(m0 + r) * g.ldc + n] = v;
+  }
+}
+
 }  // namespace
+
+bool linear_rows_ok(const GemmArgs& g) {
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  return g.M > 0 && g.N > 0 && g.K > 0 && g.K % 4 == 0 && g.K <= kRowsKMax && g.lda % 4 == 0 && g.ldb % 4 == 0 &&
+         al16(g.A) && al16(g.Bm) && g.Z1 == 1 && g.Z2 == 1 && !g.b_kn && g.split == 0 && !g.ws && !g.as &&
+         !g.pro_scale && !g.ln_stats && !g.res && !g.gate && !g.gn_part && g.alpha == 1.0f &&
+         (g.b_scale == 0.0f || g.b_scale == 1.0f) && (g.act == 0 || g.act == 1);
+}
+
+int linear_rows(const GemmArgs& g, hipStream_t st) {
+  DM_REQUIRE(linear_rows_ok(g) && g.C, "linear_rows: fp32 [n][k] weights, 16-byte aligned rows, no prologue / residual");
+  dim3 grid((unsigned)ceil_div(g.N, 16), (unsigned)ceil_div(g.M, kRowsR));
+  if (g.act == 1)
+    hipLaunchKernelGGL(linear_rows_kernel<1>, grid, dim3(256), 0, st, g);
+  else
+    hipLaunchKernelGGL(linear_rows_kernel<0>, grid, dim3(256), 0, st, g);
+  DM_LAUNCH_CHECK();
+  return DM_OK;
+}
 
 int gemm_batched(const GemmArgs& g, hipStream_t st) {
   DM_REQUIRE(g.M > 0 && g.N > 0 && g.K > 0, "gemm: empty problem");

@@ -193,6 +193,7 @@ struct UNetModel {
   // plan build
   struct FoldW {
     float *at = nullptr, *w = nullptr, *wg = nullptr, *cb = nullptr, *wgp = nullptr;
+    float *at_t = nullptr, *wg_t = nullptr;  // At, Wg transposed (attn_small)
     void *at_img = nullptr, *wgp_img = nullptr;
     const float *at_rs = nullptr, *wgp_rs = nullptr;
   };
@@ -304,7 +305,7 @@ const UNetModel::FoldW* UNetModel::fold_for(const AttnP& p) {
   FoldW f;
   void* mem = nullptr;
   const size_t nimg = split_conv_weights_bytes(1, C, C, 2);
-  const size_t nf = (3 * CC + 2 * (size_t)C) * sizeof(float);
+  const size_t nf = (5 * CC + 2 * (size_t)C) * sizeof(float);
   if (hipMalloc(&mem, nf + 2 * nimg + 64) != hipSuccess) {
     (void)hipGetLastError();
     folds[p.wqkv] = FoldW{};  // plan builds stay deterministic: every later build sees the same failure
@@ -317,13 +318,17 @@ const UNetModel::FoldW* UNetModel::fold_for(const AttnP& p) {
   f.w = f.wg + CC;
   f.cb = f.w + C;
   f.wgp = f.cb + C;
+  f.at_t = f.wgp + CC;
+  f.wg_t = f.at_t + CC;
   f.at_img = base + ((nf + 15) & ~size_t(15));
   f.wgp_img = static_cast<char*>(f.at_img) + nimg;
   const double s = (double)p.sa * (p.sb != 0.f ? (double)p.sb : 1.0);
   if (attn_fold(P(p.wqkv), P(p.bqkv), P(p.wproj), P(p.bproj), C, s, f.at, f.w, f.wg, f.cb, nullptr) != DM_OK ||
       split_conv_weights(f.at, 1, C, C, C, 1, 2, f.at_img, nullptr) != DM_OK ||
       attn_perm_cols(f.wg, f.wgp, C, nullptr) != DM_OK ||
-      split_conv_weights(f.wgp, 1, C, C, C, 1, 2, f.wgp_img, nullptr) != DM_OK || hipDeviceSynchronize() != hipSuccess) {
+      split_conv_weights(f.wgp, 1, C, C, C, 1, 2, f.wgp_img, nullptr) != DM_OK ||
+      attn_transpose(f.at, f.at_t, C, nullptr) != DM_OK || attn_transpose(f.wg, f.wg_t, C, nullptr) != DM_OK ||
+      hipDeviceSynchronize() != hipSuccess) {
     folds[p.wqkv] = FoldW{};
     return nullptr;
   }
@@ -845,12 +850,22 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
     return timestep_embed(P_->t, B, D, self->arch.variant == 2 ? 1 : 0,
                           self->te_freqs_set ? self->P(self->te_freqs) : nullptr, e0, st);
   });
+  // the time MLP and the temb projections: M = B rows, skinny. linear_rows where gemm_kernel's 64 x 64 tiles would
+  // not fill one round of the CUs (the 512-wide time MLP: 9.7 vs 15 / 24 us at B = 256); the 4992-wide temb projection
+  // stays on gemm_kernel (33 us vs 59 us on linear_rows). DM_LIN_ROWS=0: gemm_kernel for all three.
+  auto add_rows = [&](const GemmArgs& g) {
+    const long tiles64 = (long)ceil_div(kPickBatch, 64) * ceil_div(g.N, 64);
+    if (!toggles().lin_rows || !linear_rows_ok(g) || tiles64 >= 256) return add_gemm(g);
+    double fl, by;
+    gemm_cost(g, fl, by);
+    add("linear_rows_kernel", fl, by, [=](hipStream_t st) { return linear_rows(g, st); });
+  };
   {
     GemmArgs g{};
     g.M = B; g.N = TD; g.K = D; g.Z1 = 1; g.Z2 = 1; g.pick_M = kPickBatch;
     g.A = e0; g.lda = D; g.Bm = P(te_w1); g.ldb = D; g.C = e1; g.ldc = TD; g.alpha = 1.f;
     g.bias = P(te_b1); g.act = 1;
-    add_gemm(g);
+    add_rows(g);
     GemmArgs g2 = g;
     g2.K = TD; g2.A = e1; g2.lda = TD; g2.Bm = P(te_w2); g2.ldb = TD; g2.C = se; g2.bias = P(te_b2);
     g2.act = 1;  // only SiLU(temb) is ever consumed (ResBlock.proj / AdaGN.proj = SiLU -> Linear)
@@ -858,18 +873,18 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
       // temb + class_embed(y) before the SiLU (unet_categorial_adagn.py:172-174, adm/unet.py:669-671)
       g2.act = 0;
       g2.C = e2;
-      add_gemm(g2);
+      add_rows(g2);
       const float* table = P(class_embed);
       add("class_embed_silu", 0, 8.0 * B * TD, [=](hipStream_t st) {
         return embed_add_silu(e2, P_->y, table, B, TD, se, st);
       });
     } else {
-      add_gemm(g2);
+      add_rows(g2);
     }
     GemmArgs g3 = g;
     g3.N = proj_total; g3.K = TD; g3.A = se; g3.lda = TD; g3.Bm = P(proj_w); g3.ldb = TD; g3.C = projs;
     g3.ldc = proj_total; g3.bias = P(proj_b); g3.act = 0;
-    add_gemm(g3);
+    add_rows(g3);
   }
 
   // output view of node i (and of first_conv, i = -1)
@@ -1141,6 +1156,28 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
             [=](hipStream_t st) { return attn_block(ab, st); });
         x_cur = y;
         continue;
+      }
+      // The 4 x 4 middle block (16 tokens): the same folded form on the fp32 vector ALUs, one work-group per
+      // image, GroupNorm finalize and the consumer's statistics in the kernel (attn_small; DM_ATTN_SMALL=0 or an
+      // oracle DM_ATTN mode: the unfolded launches below)
+      if (conv_math == 2 && arch.variant != 2 && (av == 3 || av == 4) && toggles().attn_small && attn_small_ok(hw, C, heads) &&
+          y.p != xin.p && C % G == 0 && (C / G) >= 4 && ((C / G) & (C / G - 1)) == 0) {
+        if (const FoldW* fs = fold_for(p)) {
+          AttnBlockArgs ab{};
+          ab.x = xin.p; ab.x_pitch = xin.pitch; ab.y = y.p; ab.y_pitch = y.pitch; ab.B = B;
+          ab.at_t = fs->at_t; ab.w = fs->w; ab.wg_t = fs->wg_t; ab.cb = fs->cb;
+          ab.gin_part = sta; ab.gin_G = G; ab.gin_nchunk = gn_num_chunks(hw);
+          ab.gin_gamma = P(p.gn.g); ab.gin_beta = P(p.gn.b); ab.gin_eps = 1e-5f;
+          ab.gn_part = gn_buf_for(y, G);
+          ab.gn_G = G;
+          gn_ready.erase(y.p);
+          gn_ready[y.p] = {ab.gn_part, y.C, G};
+          const double fl = 2.0 * B * (2.0 * hw * C * C + 2.0 * hw * hw * C);
+          const double by = 4.0 * B * hw * C * 2.0;
+          add("attn_small_kernel", fl, by, [=](hipStream_t st) { return attn_small(ab, st); });
+          x_cur = y;
+          continue;
+        }
       }
       GemmArgs gq{};
       gq.M = B * hw; gq.N = 3 * C; gq.K = C; gq.Z1 = 1; gq.Z2 = 1; gq.pick_M = (long)kPickBatch * hw;

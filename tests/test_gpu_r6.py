@@ -264,3 +264,77 @@ def test_wino_small_fp32_accuracy(cuda, report, B, Cin, Cout):
     assert rms['wino'] <= rms['fp32'], rms
     assert rms['wino'] <= rms['k32s'], rms
     assert errs['wino'] < 6e-6 * scale, (errs, scale)
+
+
+# ------------------------------------------------------------------ the 4 x 4 middle attention block (attn_small)
+def _cifar_forward_labels(cuda, golden, x, t):
+    from tests.test_gpu_parity import _model
+    _, meta = golden('forward')
+    model, _ = _model(meta, 'cifar10', cuda)
+    out = model(x, t)
+    h = model.native_handle(torch.device(cuda))
+    dmhip.unet_profile_enable(h, 1)
+    model(x, t)
+    labels = [op['label'] for op in dmhip.unet_profile_read(h)]
+    dmhip.unet_profile_enable(h, 0)
+    return out, labels
+
+
+@pytest.mark.parametrize('B', [3, 8])
+def test_small_attention_vs_unfolded(cuda, golden, monkeypatch, B):
+    """The CIFAR-10 UNet's middle attention block (one head of 256 channels on the 4 x 4 map, models/unet.py:97-99,
+    models/modules.py:77-102) runs as one attn_small_kernel launch -- folded T / S / softmax / P xn / Wg, fp32 -- in
+    place of the unfolded qkv conv, S GEMM, softmax_rows, PV GEMM and projection launches (DM_ATTN_SMALL=0): whole
+    forwards within 1e-5 of each other, and the consumer's GroupNorm statistics come from the kernel (no gn_partial
+    pass after it)."""
+    g = torch.Generator().manual_seed(61)
+    x = torch.randn((B, 3, 32, 32), generator=g).to(cuda)
+    t = torch.randint(0, 1000, (B, ), generator=g).to(cuda)
+    out_s, lab_s = _cifar_forward_labels(cuda, golden, x, t)
+    monkeypatch.setenv('DM_ATTN_SMALL', '0')
+    out_u, lab_u = _cifar_forward_labels(cuda, golden, x, t)
+    assert lab_s.count('attn_small_kernel') == 1, lab_s
+    assert 'attn_small_kernel' not in lab_u and 'softmax_rows' in lab_u, lab_u
+    assert 'softmax_rows' not in lab_s, lab_s
+    assert lab_s.count('gn_partial') < lab_u.count('gn_partial'), (lab_s, lab_u)
+    assert len(lab_s) <= len(lab_u) - 5, (len(lab_s), len(lab_u))
+    err = (out_s - out_u).abs().max().item()
+    assert err <= 1e-5, err
+    assert torch.isfinite(out_s).all()
+
+
+def test_small_attention_vs_reference(cuda, golden, report):
+    """Reference fixture (tests/golden/forward.npz, the reference UNet at B = 2): the forward with the small-map block
+    within 1e-4 (north_star tolerance); the label proves the kernel ran."""
+    from tests.test_gpu_parity import TOL
+    arrays, _ = golden('forward')
+    y, labels = _cifar_forward_labels(cuda, golden, torch.from_numpy(arrays['cifar10_x']).to(cuda),
+                                      torch.from_numpy(arrays['cifar10_t']).to(cuda))
+    assert labels.count('attn_small_kernel') == 1, labels
+    err = (y.cpu() - torch.from_numpy(arrays['cifar10_y'])).abs().max().item()
+    report('forward_cifar10_small_attention_maxabs_vs_reference', err)
+    assert err <= TOL, err
+
+
+# ------------------------------------------------------------------ the time MLP / temb projections (linear_rows)
+@pytest.mark.parametrize('B', [2, 256])
+def test_linear_rows_vs_gemm(cuda, golden, monkeypatch, B):
+    """The time MLP and the ResBlocks' temb projections (models/unet.py:64-69, :18-21) run on linear_rows_kernel
+    (16 lanes per output over K, fp32 FMAs) where gemm_kernel's tiles would not fill the CUs: the two 512-wide time
+    MLP launches per forward (the 4992-wide temb projection stays on gemm_kernel), whole forwards within 1e-5 of the
+    gemm_kernel path (DM_LIN_ROWS=0, fp32 MFMA), and rows of the B = 256 forward equal the B = 3 forward's bit for
+    bit (per-row sums depend on K only)."""
+    g = torch.Generator().manual_seed(62)
+    x = torch.randn((B, 3, 32, 32), generator=g).to(cuda)
+    t = torch.randint(0, 1000, (B, ), generator=g).to(cuda)
+    out_r, lab_r = _cifar_forward_labels(cuda, golden, x, t)
+    assert lab_r.count('linear_rows_kernel') == 2, lab_r
+    if B == 256:
+        idx = [0, 77, 255]
+        small, _ = _cifar_forward_labels(cuda, golden, x[idx].contiguous(), t[idx].contiguous())
+        assert torch.equal(out_r[idx], small)
+    monkeypatch.setenv('DM_LIN_ROWS', '0')
+    out_g, lab_g = _cifar_forward_labels(cuda, golden, x, t)
+    assert 'linear_rows_kernel' not in lab_g, lab_g
+    err = (out_r - out_g).abs().max().item()
+    assert err <= 1e-5, err
