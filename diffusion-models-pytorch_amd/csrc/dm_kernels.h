@@ -441,8 +441,17 @@ int conv3x3_small_in(const float* x, int B, int Cin, int H, int W, const float* 
 bool conv3x3_small_in_can_emit(int H, int W, int Cout, int G);
 // last conv weights torch [Cout][Cin][3][3] -> [9][Cin][CO], CO = Cout rounded up to even (<= 8; zero-padded)
 int small_out_pack(const float* w, int Cout, int Cin, float* wp, hipStream_t st);
+// the prologue GroupNorm finalized in the kernel from the chunk partials (gn_finalize's expressions), instead of
+// pro_scale / pro_shift tables: part [B][nchunk][G] {sum, sumsq}, n = HW * C / G elements per group
+struct GnFin {
+  const double2* part = nullptr;
+  int G = 0, nchunk = 0;
+  double n = 0;
+  float eps = 1e-5f;
+  const float *gamma = nullptr, *beta = nullptr;
+};
 int conv3x3_small_out(const View& x, const float* wp, const float* bias, int Cout, float* y, hipStream_t st,
-                      const float* pro_scale = nullptr, const float* pro_shift = nullptr);
+                      const float* pro_scale = nullptr, const float* pro_shift = nullptr, const GnFin& fin = GnFin{});
 int sampler_step(const StepArgs& s, hipStream_t st);
 // out = c1 a + c2 b (mode 0), c1 a - c2 b (1), (c1 a - b) / c2 (2); per-row coefficients when c*_rows given
 int lincomb(int mode, const float* a, const float* b, float* out, long n, long row_elems, const float* c1_rows,

@@ -282,15 +282,16 @@ constexpr int kSoTW = 32, kSoTH = 8, kSoPP = (kSoTH + 2) * (kSoTW + 2);
 // before (a packed FMA rounds each lane as v_fma_f32 does). The patch registers are double
 // buffered: chunk c + 2's loads are issued right after chunk c's patch is stored, so each load has two
 // chunks' taps to land (one chunk's 432 FMAs per thread did not cover the load latency).
-constexpr int kSo2C = 16, kSo2LD = 20, kSo2PJ = (kSoPP * (kSo2C / 4) + 255) / 256;
+constexpr int kSo2C = 16, kSo2LD = 20, kSo2PJ = (kSoPP * (kSo2C / 4) + 255) / 256, kSoMaxC = 512;
 template <int CO>
 __global__ void __launch_bounds__(256) conv3x3_small_out2_kernel(const float* __restrict__ x, int B, int H, int W,
                                                                  int Cin, int pitch, const float* __restrict__ wp,
                                                                  const float* __restrict__ bias,
                                                                  float* __restrict__ y,
                                                                  const float* __restrict__ pro_scale,
-                                                                 const float* __restrict__ pro_shift) {
+                                                                 const float* __restrict__ pro_shift, GnFin fin) {
   __shared__ __attribute__((aligned(16))) float patch[kSoPP * kSo2LD];
+  __shared__ __attribute__((aligned(16))) float tab[2][kSoMaxC];  // fin: the image's GroupNorm affine
   const int tiles_x = ceil_div(W, kSoTW), tiles_y = ceil_div(H, kSoTH);
   const int b = blockIdx.x / (tiles_x * tiles_y);
   const int trem = blockIdx.x - b * tiles_x * tiles_y;
@@ -308,6 +309,7 @@ __global__ void __launch_bounds__(256) conv3x3_small_out2_kernel(const float* __
     ok[j] = t + 256 * j < kSoPP * 4 && iy >= 0 && iy < H && ix >= 0 && ix < W;
     src[j] = x + (((size_t)b * H + min(max(iy, 0), H - 1)) * W + min(max(ix, 0), W - 1)) * pitch + 4 * c4;
   }
+  const bool gn = pro_scale || fin.part;
   f4 rva[kSo2PJ], rvb[kSo2PJ];
   auto load = [&](f4 (&rv)[kSo2PJ], int c0) {
 #pragma unroll
@@ -322,9 +324,11 @@ __global__ void __launch_bounds__(256) conv3x3_small_out2_kernel(const float* __
       f4 v = {0.f, 0.f, 0.f, 0.f};
       if (ok[j]) {
         v = rv[j];
-        if (pro_scale) {  // GroupNorm + SiLU of last_conv (models/unet.py:115-119), padding stays 0
-          const f4 sc = *reinterpret_cast<const f4*>(pro_scale + (size_t)b * Cin + c0 + 4 * c4);
-          const f4 sh = *reinterpret_cast<const f4*>(pro_shift + (size_t)b * Cin + c0 + 4 * c4);
+        if (gn) {  // GroupNorm + SiLU of last_conv (models/unet.py:115-119), padding stays 0
+          const f4 sc = fin.part ? *reinterpret_cast<const f4*>(&tab[0][c0 + 4 * c4])
+                                 : *reinterpret_cast<const f4*>(pro_scale + (size_t)b * Cin + c0 + 4 * c4);
+          const f4 sh = fin.part ? *reinterpret_cast<const f4*>(&tab[1][c0 + 4 * c4])
+                                 : *reinterpret_cast<const f4*>(pro_shift + (size_t)b * Cin + c0 + 4 * c4);
           v.x = silu_fast(v.x * sc.x + sh.x); v.y = silu_fast(v.y * sc.y + sh.y);
           v.z = silu_fast(v.z * sc.z + sh.z); v.w = silu_fast(v.w * sc.w + sh.w);
         }
@@ -360,6 +364,27 @@ __global__ void __launch_bounds__(256) conv3x3_small_out2_kernel(const float* __
   };
   load(rva, 0);
   if (kSo2C < Cin) load(rvb, kSo2C);
+  if (fin.part) {  // gn_finalize (gn.hip) for this image, same expressions; read after the first chunk's barrier
+    const int cpg = Cin / fin.G;
+    for (int c = t; c < Cin; c += 256) {
+      const int g = c / cpg;
+      double a = 0, q = 0;
+      for (int k = 0; k < fin.nchunk; ++k) {
+        const double2 v = fin.part[((size_t)b * fin.nchunk + k) * fin.G + g];
+        a += v.x;
+        q += v.y;
+      }
+      const double m = a / fin.n;
+      double var = q / fin.n - m * m;
+      if (var < 0) var = 0;
+      const float mu = (float)m;
+      const float rs = (float)(1.0 / sqrt(var + (double)fin.eps));
+      const float sc = rs * (fin.gamma ? fin.gamma[c] : 1.0f);
+      tab[0][c] = sc;
+      tab[1][c] = -sc * mu + (fin.beta ? fin.beta[c] : 0.0f);
+    }
+    __syncthreads();
+  }
   for (int c0 = 0; c0 < Cin; c0 += 2 * kSo2C) {
     chunk(rva, c0);
     if (c0 + kSo2C < Cin) chunk(rvb, c0 + kSo2C);
@@ -692,15 +717,17 @@ int small_out_pack(const float* w, int Cout, int Cin, float* wp, hipStream_t st)
 }
 
 int conv3x3_small_out(const View& x, const float* wp, const float* bias, int Cout, float* y, hipStream_t st,
-                      const float* pro_scale, const float* pro_shift) {
+                      const float* pro_scale, const float* pro_shift, const GnFin& fin) {
   DM_REQUIRE(Cout >= 1 && Cout <= 8, "last conv: Cout out of range");
+  DM_REQUIRE(!fin.part || (!pro_scale && fin.G > 0 && x.C % fin.G == 0 && x.C <= kSoMaxC && fin.nchunk > 0),
+             "last conv: in-kernel GroupNorm finalize needs groups dividing <= 512 channels");
   DM_REQUIRE(x.C % 32 == 0 && x.pitch % 4 == 0, "last conv: Cin must be a multiple of 32");
   // wp: small_out_pack's [9][Cin][Cout rounded up to even]
   DM_REQUIRE((reinterpret_cast<uintptr_t>(x.p) & 15) == 0, "last conv: input must be 16-byte aligned");
   const long tiles = (long)x.B * ceil_div(x.H, kSoTH) * ceil_div(x.W, kSoTW);
 #define DM_SO2(CO)                                                                                            \
   hipLaunchKernelGGL(conv3x3_small_out2_kernel<CO>, dim3((unsigned)tiles), dim3(256), 0, st, x.p, x.B, x.H, x.W, \
-                     x.C, x.pitch, wp, bias, y, pro_scale, pro_shift)
+                     x.C, x.pitch, wp, bias, y, pro_scale, pro_shift, fin)
   if (Cout == 1)
     DM_SO2(1);
   else if (Cout == 2)

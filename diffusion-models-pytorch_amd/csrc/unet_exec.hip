@@ -1378,11 +1378,19 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
     const float* lb = P(last_b);
     const int oc = arch.out_channels;
     const double2* stl = gn_stats(xin);
-    add("gn_finalize", 0, 8.0 * B * C, [=](hipStream_t st) {
-      return gn_finalize(xin, G, stl, 1e-5f, self->P(lg.g), self->P(lg.b), gsc, gsh, st);
-    });
+    // the GroupNorm affine finalized in the last conv's blocks (one image each) from the partials, the serial chunk
+    // sums of gn_finalize_kernel (maps of <= 64 chunks: 64^2 and below); DM_GN_FUSION=0, wider maps or more than 512
+    // channels: the gn_finalize launch
+    GnFin fin;
+    if (toggles().gn_fusion && C <= 512 && C % G == 0 && nchunk <= 64) {
+      fin.part = stl; fin.G = G; fin.nchunk = nchunk; fin.n = (double)H * W * (C / G); fin.eps = 1e-5f;
+      fin.gamma = P(lg.g); fin.beta = P(lg.b);
+    } else {
+      add("gn_finalize", 0, 8.0 * B * C, [=](hipStream_t st) {
+        return gn_finalize(xin, G, stl, 1e-5f, self->P(lg.g), self->P(lg.b), gsc, gsh, st);
+      });
+    }
     (void)va;
-    (void)nchunk;
     if (!last_packed) {  // packed [9][C][CO] copy of the last conv weight (model-owned, built once)
       DM_CHECK_HIP(hipMalloc(&last_packed, (size_t)9 * C * 8 * sizeof(float)));
       DM_REQUIRE(small_out_pack(lw, oc, C, last_packed, nullptr) == DM_OK, "last conv: weight packing failed");
@@ -1390,7 +1398,10 @@ int UNetModel::build_plan(Plan& pl, int B, int H, int W) {
     }
     lw = last_packed;
     add("conv3x3_small_out", 2.0 * B * H * W * oc * 9 * C, 4.0 * B * H * W * (C + oc),
-        [=](hipStream_t st) { return conv3x3_small_out(xin, lw, lb, oc, P_->out, st, gsc, gsh); });
+        [=](hipStream_t st) {
+          return fin.part ? conv3x3_small_out(xin, lw, lb, oc, P_->out, st, nullptr, nullptr, fin)
+                          : conv3x3_small_out(xin, lw, lb, oc, P_->out, st, gsc, gsh);
+        });
   }
   return DM_OK;
 }
@@ -1447,10 +1458,13 @@ extern "C" int dm_unet_forward(dm_unet* h, const float* x, const int64_t* t, con
       auto& pl = *plp;
       DM_CHECK_HIP(hipMemcpyAsync(pl.x, x, nx * sizeof(float), hipMemcpyDeviceToDevice, st));
       DM_CHECK_HIP(hipMemcpyAsync(pl.t, t, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
-      if (y)
-        DM_CHECK_HIP(hipMemcpyAsync(pl.y, y, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
-      else
-        DM_CHECK_HIP(hipMemsetAsync(pl.y, 0xff, (size_t)B * sizeof(int64_t), st));  // -1: no label
+      // the labels are read only by the class embedding (class_embed_silu); without one the staging is skipped
+      if (m->has_class) {
+        if (y)
+          DM_CHECK_HIP(hipMemcpyAsync(pl.y, y, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+        else
+          DM_CHECK_HIP(hipMemsetAsync(pl.y, 0xff, (size_t)B * sizeof(int64_t), st));  // -1: no label
+      }
       const int rc = pl.run(st);
       if (rc) return rc;
       DM_CHECK_HIP(hipMemcpyAsync(out, pl.out, no * sizeof(float), hipMemcpyDeviceToDevice, st));
