@@ -25,9 +25,11 @@ def main():
     dmhip.load()
     conv_bench.run(args.shape, 5, 'fp16x2', 21)
     B, Cin, Cout, H, pro, up = conv_bench.SHAPES[args.shape]
-    tpi = (H * H // 128) * (Cout // 128)
-    parts = next((p for p in range(1, tpi + 1) if tpi % p == 0 and B * p >= 256), tpi)
-    nblk = B * parts
+    imgs = 2 if H == 8 else 8 if H == 4 else 1  # images per 128-pixel tile (8 x 8 / 4 x 4 maps)
+    groups = -(-B // imgs)
+    tpi = (imgs * H * H // 128) * (Cout // 128)  # tiles per image group
+    parts = next((p for p in range(1, tpi + 1) if tpi % p == 0 and groups * p >= 256), tpi)
+    nblk = groups * parts
     buf = np.zeros((nblk, 16), dtype=np.uint64)
     L = dmhip.load()
     L.dm_debug_wino_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
