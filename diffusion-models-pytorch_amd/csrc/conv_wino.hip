@@ -239,8 +239,11 @@ __device__ __forceinline__ void conv_wino_body(const ConvArgs& a) {
   const float* pp[2] = {nullptr, nullptr};
   int wcol = 0;  // bytes: the wave's nu plane and 32-column group of the tile (uniform)
   int ty = 0, tx = 0;  // the tile's row / column among the image's tiles
+  // wide maps: column halves outer (a block's tiles are one column half of its image when parts == nN, and with the
+  // blocks of an image adjacent the XCDs alternate halves: one half's U image per XCD L2); else row tiles outer
+  const int MT = IMGS * HW / 128;  // row tiles of the image group
   auto set_tile = [&](int tile) DM_WINO_INL {
-    const int mt = tile / nN, nt = tile - mt * nN;
+    const int mt = WIDE ? tile % MT : tile / nN, nt = WIDE ? tile / MT : tile - (tile / nN) * nN;
     m0 = b0 * HW + mt * 128;
     n0 = nt * 128;
     ty = WIDE ? mt / ntx : mt;
