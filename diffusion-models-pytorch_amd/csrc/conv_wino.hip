@@ -172,7 +172,7 @@ __device__ __forceinline__ void conv_wino_body(const ConvArgs& a) {
   const int nN = N / 128;
   // persistent blocks over the tiles of ONE image (two for 8 x 8 maps, eight for 4 x 4; their GroupNorm tables built
   // once): grid = [ksplit x] ceil(B / IMGS) x parts, block (images b0 .., part) takes tiles part * tpb .. + tpb - 1 of
-  // the group's (IMGS HW / 128) x nN, row tiles outer
+  // the group's nN x (IMGS HW / 128), column halves outer
   const int nks = KS ? a.ksplit : 1;
   const int gsz = KS ? (int)gridDim.x / nks : (int)gridDim.x;  // blocks per split
   const int split = KS ? (int)blockIdx.x / gsz : 0;
@@ -239,11 +239,12 @@ __device__ __forceinline__ void conv_wino_body(const ConvArgs& a) {
   const float* pp[2] = {nullptr, nullptr};
   int wcol = 0;  // bytes: the wave's nu plane and 32-column group of the tile (uniform)
   int ty = 0, tx = 0;  // the tile's row / column among the image's tiles
-  // wide maps: column halves outer (a block's tiles are one column half of its image when parts == nN, and with the
-  // blocks of an image adjacent the XCDs alternate halves: one half's U image per XCD L2); else row tiles outer
+  // column halves outer: a block's consecutive tiles share one 128-column half of U, so the blocks of an XCD, which
+  // run roughly in step, keep one half's U image in its L2 instead of both (wide maps: a block's tiles are one column
+  // half of its image when parts == nN, and the XCDs alternate halves)
   const int MT = IMGS * HW / 128;  // row tiles of the image group
   auto set_tile = [&](int tile) DM_WINO_INL {
-    const int mt = WIDE ? tile % MT : tile / nN, nt = WIDE ? tile / MT : tile - (tile / nN) * nN;
+    const int mt = tile % MT, nt = tile / MT;
     m0 = b0 * HW + mt * 128;
     n0 = nt * 128;
     ty = WIDE ? mt / ntx : mt;
